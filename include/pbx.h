@@ -1,0 +1,174 @@
+/*
+ * pbx.h — C-ABI of the MI355X-native /tile pipeline (drop-in for the
+ * omero-ms-pixel-buffer tile hot path).
+ *
+ * Plain C: no exceptions, no torch/HIP types, plain pointers and sizes.  Every
+ * entry point is thread-safe.  Each declaration cites the reference interface
+ * it replaces; paths are relative to
+ * /root/reference/src/main/java/com/glencoesoftware/omero/ms/pixelbuffer/.
+ *
+ * Mapping to the reference:
+ *   TileCtx (TileCtx.java:30-92)                  -> pbx_tile_req
+ *   TileRequestHandler.getTile (TileRequestHandler.java:80-139)
+ *                                                 -> pbx_get_tile / pbx_get_tiles
+ *   PixelBuffer.getTileDirect (:107-109)          -> kernel K1 (extract + big-endian)
+ *   writeImage("png"|"tif") (:176-199)            -> kernels K2..K7 (filter/deflate/frame)
+ *   PixelsService.getPixelBuffer (:201-211)       -> planes registered with pbx_plane_register
+ *   getPixels (Ice HQL, :220-241)                 -> the plane registry's image records
+ *   reply "filename" header (PixelBufferVerticle.java:116-126)  -> pbx_tile_filename
+ *   Content-Type (PixelBufferMicroserviceVerticle.java:373-379)  -> pbx_content_type
+ */
+#ifndef PBX_H
+#define PBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBX_ABI_VERSION 1
+
+/* Status codes are the HTTP status the reference's event-bus consumer ends with:
+ * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
+ * IllegalArgumentException -> 400 (:137-140); any other exception -> 500 (:141-146). */
+enum pbx_status {
+    PBX_OK = 0,
+    PBX_E_BADARG = 400,
+    PBX_E_NOTFOUND = 404,
+    PBX_E_INTERNAL = 500
+};
+
+/* OMERO pixel types (ome.xml.model.enums.PixelType; TileRequestHandler.java:100-101,164-165). */
+enum pbx_pixel_type {
+    PBX_INT8 = 0, PBX_UINT8, PBX_INT16, PBX_UINT16, PBX_INT32, PBX_UINT32, PBX_FLOAT, PBX_DOUBLE,
+    PBX_NPIXEL_TYPES
+};
+
+/* TileCtx.format (TileCtx.java:89): null -> raw bytes (:128), "png"/"tif" -> writeImage
+ * (:122-123), anything else -> null -> 404 (:125-126). */
+enum pbx_format { PBX_FMT_RAW = 0, PBX_FMT_PNG = 1, PBX_FMT_TIF = 2, PBX_FMT_UNKNOWN = 3 };
+
+/* Byte order of the samples of a registered plane as handed to pbx_plane_register. */
+enum pbx_byte_order { PBX_BIG_ENDIAN = 0, PBX_LITTLE_ENDIAN = 1 };
+
+/* Plane sources: host bytes (copied to HBM) or an on-device synthetic generator
+ * (Bio-Formats FakeReader-style G_FAKE, counter-hash G_NOISE). */
+enum pbx_source { PBX_SRC_HOST = 0, PBX_SRC_GEN_FAKE = 1, PBX_SRC_GEN_NOISE = 2 };
+
+/* PNG scanline filter used by the encoder.  NONE is what the reference's APNGWriter
+ * writes (filter byte 0 on every row); the others decode to identical pixels. */
+enum pbx_png_filter {
+    PBX_FILTER_NONE = 0, PBX_FILTER_SUB = 1, PBX_FILTER_UP = 2, PBX_FILTER_AVG = 3,
+    PBX_FILTER_PAETH = 4, PBX_FILTER_ADAPTIVE = 5
+};
+
+typedef struct pbx_config {
+    int32_t device;          /* HIP device ordinal; -1 = $PBX_DEVICE, else $LOCAL_RANK, else 0 */
+    int32_t png_filter;      /* enum pbx_png_filter; default NONE (reference) */
+    int32_t tiff_deflate;    /* 0 = uncompressed TIFF (reference default); 1 = Compression=8 */
+    int32_t segment_bytes;   /* deflate segment size (bytes of filtered stream); 0 = default */
+    uint64_t max_batch_bytes;/* device scratch budget per batch; 0 = default */
+} pbx_config;
+
+typedef struct pbx_ctx pbx_ctx;
+
+/* Lifecycle (PixelBufferMicroserviceVerticle.start/deploy :114-233, stop :298-308). */
+int pbx_config_default(pbx_config* cfg);
+int pbx_init(const pbx_config* cfg, pbx_ctx** out);
+void pbx_shutdown(pbx_ctx* ctx);
+/* Last error message of the calling thread (never NULL). */
+const char* pbx_last_error(void);
+int pbx_abi_version(void);
+int pbx_device_count(void);
+
+/* A plane (z,c,t,resolution) of an image.  Registering a resolution-0 plane creates or
+ * checks the image record (the `Pixels` row getPixels returns, TileRequestHandler.java:220-241):
+ * size_x/size_y/pixel_type are the image's. */
+typedef struct pbx_plane_desc {
+    int64_t image_id;
+    int32_t z, c, t;
+    int32_t resolution;      /* 0 = full resolution (PixelBuffer.setResolutionLevel, :89-91) */
+    int32_t pixel_type;      /* enum pbx_pixel_type */
+    int32_t size_x, size_y;
+    int32_t byte_order;      /* enum pbx_byte_order of host_data (ignored for generators) */
+    int32_t source;          /* enum pbx_source */
+    const void* host_data;   /* PBX_SRC_HOST: size_y rows of size_x samples, row-major */
+    uint64_t host_bytes;
+    uint64_t seed;           /* generators */
+    int32_t plane_no;        /* generators: FakeReader plane number / noise plane index */
+    int32_t reserved;
+} pbx_plane_desc;
+
+int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* desc, uint64_t* plane_id);
+int pbx_plane_release(pbx_ctx* ctx, uint64_t plane_id);
+/* Copy a registered plane back to the host, samples in big-endian order (test hook). */
+int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
+
+/* TileCtx (TileCtx.java:36-54, parsed at :67-90). */
+typedef struct pbx_tile_req {
+    int64_t image_id;
+    int32_t z, c, t;
+    int32_t resolution;      /* -1 = not given */
+    int32_t x, y, w, h;      /* w/h == 0 -> plane size (TileRequestHandler.java:92-97) */
+    int32_t format;          /* enum pbx_format */
+    int32_t reserved;
+} pbx_tile_req;
+
+/* One response: status plus the exact-length body (TileRequestHandler.java:188-193). */
+typedef struct pbx_result {
+    int32_t status;          /* enum pbx_status */
+    int32_t format;
+    int32_t w, h;            /* region after the w/h defaulting (used by the filename header) */
+    const uint8_t* data;     /* library-owned; valid until pbx_results_release */
+    uint64_t len;
+    void* owner;             /* internal */
+} pbx_result;
+
+/* Synchronous single tile: TileRequestHandler.getTile (TileRequestHandler.java:80-139). */
+int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out);
+/* Synchronous batch: n independent getTile calls executed as one set of GPU launches. */
+int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out);
+void pbx_results_release(pbx_ctx* ctx, pbx_result* results, uint64_t n);
+
+/* Device-resident batches: plan once, launch asynchronously on the context's stream,
+ * outputs stay in HBM until pbx_batch_fetch.  Used by callers that pipeline requests
+ * (and by bench.py, whose timed region is plan+launch+sync of one batch). */
+typedef struct pbx_batch pbx_batch;
+int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch** out);
+int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b);
+int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b);
+int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out);
+void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b);
+
+typedef struct pbx_batch_stats {
+    uint64_t tiles, ok_tiles, png_tiles, raw_tiles, tif_tiles;
+    uint64_t in_bytes;       /* w*h*bpp summed over OK tiles */
+    uint64_t stream_bytes;   /* bytes fed to deflate (PNG filtered streams, deflate-TIFF) */
+    uint64_t out_bytes;      /* total response bytes */
+    uint64_t deflate_out_bytes; /* compressed payload bytes (zlib streams) */
+    uint64_t segments;
+    double ms_extract, ms_filter, ms_deflate, ms_assemble, ms_total; /* HIP events, last launch */
+} pbx_batch_stats;
+int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* out);
+
+/* Reply metadata. */
+/* "image%d_z%d_c%d_t%d_x%d_y%d_w%d_h%d.%s" (PixelBufferVerticle.java:118-126), ext "bin" when
+ * format is raw.  format_str is the caller's original TileCtx.format (may be NULL). */
+int pbx_tile_filename(const pbx_tile_req* req, int32_t w, int32_t h, const char* format_str,
+                      char* out, uint64_t cap);
+/* PixelBufferMicroserviceVerticle.java:373-379. */
+const char* pbx_content_type(const char* format_str);
+/* TileCtx.format string -> enum pbx_format (null -> RAW). */
+int pbx_format_from_string(const char* format_str);
+int pbx_pixel_type_from_string(const char* name);
+int pbx_bytes_per_pixel(int32_t pixel_type);
+
+/* Synchronise the context's device (bench/test hook). */
+int pbx_device_synchronize(pbx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBX_H */

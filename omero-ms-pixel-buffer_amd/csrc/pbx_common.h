@@ -1,0 +1,304 @@
+// pbx_common.h — types and helpers shared by the HIP kernels, the host runtime and the
+// test-only CPU emulator of the deflate phases.  Plain C++ (no HIP headers): PBX_HD is
+// `__host__ __device__` under hipcc and empty under g++.
+//
+// Reference anchors (paths under /root/reference/src/main/java/com/glencoesoftware/omero/ms/pixelbuffer/):
+//   getTileDirect -> TileStream::be()            TileRequestHandler.java:107-109 (big-endian, :155)
+//   writeImage("png") -> PNG framing constants    TileRequestHandler.java:176-199 (APNGWriter upstream)
+//   writeImage("tif") -> TIFF header              TileRequestHandler.java:176-199 (TiffWriter upstream)
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PBX_HD __host__ __device__ __forceinline__
+#else
+#define PBX_HD inline
+#endif
+
+namespace pbx {
+
+// ----------------------------------------------------------------------------------- formats
+enum : int32_t { FMT_RAW = 0, FMT_PNG = 1, FMT_TIF = 2, FMT_UNKNOWN = 3 };
+enum : int32_t { PT_INT8 = 0, PT_UINT8, PT_INT16, PT_UINT16, PT_INT32, PT_UINT32, PT_FLOAT,
+                 PT_DOUBLE, PT_N };
+
+// Tile flags
+enum : uint32_t {
+    TF_SWAP = 1u,      // plane samples are little-endian -> swap to big-endian
+    TF_FLIP = 2u,      // PNG int8/int16: flip the sign bit of the MS byte (APNGWriter)
+    TF_PNGROWS = 4u,   // stream rows carry a leading PNG filter-type byte
+    TF_TIFF = 8u,      // container is TIFF (else PNG) for deflate tiles
+};
+
+// PNG container layout (APNGWriter: sig, IHDR, acTL, fcTL, IDAT, IEND).
+constexpr uint32_t PNG_SIG_BYTES = 8;
+constexpr uint32_t PNG_IHDR_BYTES = 12 + 13;
+constexpr uint32_t PNG_ACTL_BYTES = 12 + 8;
+constexpr uint32_t PNG_FCTL_BYTES = 12 + 26;
+constexpr uint32_t PNG_IDAT_DATA_OFF =
+    PNG_SIG_BYTES + PNG_IHDR_BYTES + PNG_ACTL_BYTES + PNG_FCTL_BYTES + 8;  // 99
+constexpr uint32_t ZLIB_HDR_BYTES = 2;
+constexpr uint32_t PNG_TAIL_BYTES = 4 /*adler*/ + 4 /*IDAT crc*/ + 12 /*IEND*/;
+// TIFF: header + 11-entry IFD, strip data at a 16-byte aligned offset.
+constexpr uint32_t TIFF_NTAGS = 11;
+constexpr uint32_t TIFF_DATA_OFFSET = 160;
+
+// Per-tile descriptor (device side).  64-byte aligned POD, filled by the host planner.
+struct alignas(16) TileDesc {
+    const uint8_t* plane;   // plane base in HBM
+    int64_t pitch;          // bytes per plane row
+    int32_t x, y, w, h;     // region (post-defaulting)
+    int32_t bpp, lbpp;      // bytes per sample and log2
+    uint32_t flags;         // TF_*
+    int32_t filter;         // PNG filter 0..4, 5 = per-row choice in rowfilt
+    int32_t pixel_type;
+    uint32_t rowlen;        // stream bytes per row: (png?1:0) + w*bpp
+    uint64_t stream_len;    // h * rowlen
+    uint64_t out_off;       // raw/tif: byte offset in the fixed arena; deflate: unused
+    uint32_t seg_first;     // deflate tiles: first segment index in the batch
+    uint32_t seg_count;
+    uint32_t seg_len;       // nominal segment length (the last may be shorter)
+    uint32_t rowfilt_off;   // offset of this tile's per-row filter bytes in the rowfilt buffer
+    uint32_t blk_first;     // first workgroup (extract) / first row (row filter) of this tile
+    uint32_t rows_per_blk;  // extract: rows handled by one workgroup
+};
+
+// Per-segment deflate result.
+struct SegOut {
+    uint32_t nbytes;        // compressed bytes in the slot
+    uint32_t crc;           // CRC-32 of those bytes (standard, zlib crc32 convention)
+    uint32_t crc_op;        // x^(8*nbytes) mod P, for crc32_combine
+    uint32_t adler_s1;      // sum of stream bytes mod 65521
+    uint32_t adler_s2;      // sum of (len - i) * byte_i mod 65521
+    uint32_t len;           // stream bytes in this segment
+    uint32_t btype;         // 0 stored, 1 fixed, 2 dynamic
+    uint32_t bits;          // bits of the block (diagnostics)
+};
+
+PBX_HD uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// ----------------------------------------------------------------------------- CRC-32 math
+// Standard reflected CRC-32 (poly 0xEDB88320) with zlib's crc32_combine formulation:
+// crc(A||B) = multmodp(x^(8|B|), crc(A)) ^ crc(B).
+constexpr uint32_t CRC_POLY = 0xEDB88320u;
+
+PBX_HD uint32_t crc_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    }
+    return p;
+}
+
+// x^(2^k) mod P for k = 0..31 is computed by repeated squaring; x^(8n) for a byte count n.
+PBX_HD uint32_t crc_x8n(uint64_t n) {
+    // p = x^0; sq = x^8 (k=3: x^(2^3))
+    uint32_t p = 1u << 31;
+    uint32_t sq = 1u << 30;  // x^1
+    // square x^1 three times -> x^8
+    sq = crc_multmodp(sq, sq);  // x^2
+    sq = crc_multmodp(sq, sq);  // x^4
+    sq = crc_multmodp(sq, sq);  // x^8
+    while (n) {
+        if (n & 1) p = crc_multmodp(sq, p);
+        n >>= 1;
+        if (n) sq = crc_multmodp(sq, sq);
+    }
+    return p;
+}
+
+PBX_HD uint32_t crc_combine_op(uint32_t crc1, uint32_t crc2, uint32_t op2) {
+    return crc_multmodp(op2, crc1) ^ crc2;
+}
+
+// Bytewise CRC with a caller-provided 256-entry table (LDS on the device).
+PBX_HD uint32_t crc_update(const uint32_t* table, uint32_t crc, uint8_t b) {
+    return table[(crc ^ b) & 0xFF] ^ (crc >> 8);
+}
+
+PBX_HD uint32_t crc_table_entry(uint32_t n) {
+    uint32_t c = n;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? CRC_POLY ^ (c >> 1) : c >> 1;
+    return c;
+}
+
+// --------------------------------------------------------------------------- Adler-32 math
+constexpr uint32_t ADLER_BASE = 65521u;
+
+// Combine raw partial sums (s1 = sum b, s2 = sum (n-i) b) of L (left) and R (right, lenR bytes).
+PBX_HD void adler_combine(uint32_t& s1L, uint32_t& s2L, uint32_t s1R, uint32_t s2R, uint64_t lenR) {
+    uint64_t s2 = (uint64_t)s2L + (uint64_t)(lenR % ADLER_BASE) * s1L + s2R;
+    s1L = (uint32_t)(((uint64_t)s1L + s1R) % ADLER_BASE);
+    s2L = (uint32_t)(s2 % ADLER_BASE);
+}
+
+// Final adler32 value for a stream of total length n with raw sums s1, s2.
+PBX_HD uint32_t adler_final(uint32_t s1, uint32_t s2, uint64_t n) {
+    uint32_t a = (uint32_t)((1 + (uint64_t)s1) % ADLER_BASE);
+    uint32_t b = (uint32_t)(((uint64_t)(n % ADLER_BASE) + s2) % ADLER_BASE);
+    return (b << 16) | a;
+}
+
+// ---------------------------------------------------------------------- deflate code maps
+// Length 3..258 -> symbol 257..285 and extra bits.
+PBX_HD uint32_t ilog2_u32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+PBX_HD void len_code(uint32_t len, uint32_t& sym, uint32_t& ebits, uint32_t& eval) {
+    uint32_t l = len - 3;
+    if (len == 258) { sym = 285; ebits = 0; eval = 0; return; }
+    if (l < 8) { sym = 257 + l; ebits = 0; eval = 0; return; }
+    uint32_t e = ilog2_u32(l) - 2;
+    sym = 261 + 4 * e + (l >> e) - 4;
+    ebits = e;
+    eval = l & ((1u << e) - 1);
+}
+
+// Distance 1..32768 -> symbol 0..29 and extra bits.
+PBX_HD void dist_code(uint32_t dist, uint32_t& sym, uint32_t& ebits, uint32_t& eval) {
+    uint32_t d = dist - 1;
+    if (d < 4) { sym = d; ebits = 0; eval = 0; return; }
+    uint32_t e = ilog2_u32(d) - 1;
+    sym = 2 * e + 2 + ((d >> e) & 1);
+    ebits = e;
+    eval = d & ((1u << e) - 1);
+}
+
+PBX_HD uint32_t len_sym_ebits(uint32_t sym) {
+    if (sym < 265 || sym == 285) return 0;
+    return (sym - 261) / 4;
+}
+PBX_HD uint32_t dist_sym_ebits(uint32_t sym) { return sym < 4 ? 0 : sym / 2 - 1; }
+
+PBX_HD uint32_t fixed_lit_len(uint32_t sym) {
+    return sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
+}
+
+PBX_HD uint32_t bitrev(uint32_t code, uint32_t len) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < len; i++) { r = (r << 1) | (code & 1); code >>= 1; }
+    return r;
+}
+
+// ----------------------------------------------------------------------- tile byte source
+// The byte stream a deflate segment reads: for PNG, h rows of (filter byte || filtered
+// big-endian row); for deflate-TIFF, the big-endian tile bytes.  Reads the plane in HBM
+// directly (getTileDirect fused with the filter: no intermediate tile buffer).
+struct TileStream {
+    const uint8_t* plane;
+    int64_t pitch;
+    int32_t x, y, bpp, lbpp;
+    uint32_t rowlen, flags;
+    int32_t filter;
+    const uint8_t* rowfilt;
+
+    PBX_HD void init(const TileDesc& d, const uint8_t* rowfilt_base) {
+        plane = d.plane; pitch = d.pitch; x = d.x; y = d.y; bpp = d.bpp; lbpp = d.lbpp;
+        rowlen = d.rowlen; flags = d.flags; filter = d.filter;
+        rowfilt = rowfilt_base ? rowfilt_base + d.rowfilt_off : nullptr;
+    }
+    // Big-endian byte i of tile row r, after the APNGWriter sign flip.
+    PBX_HD uint32_t be(int64_t r, uint32_t i) const {
+        uint32_t s = i >> lbpp, b = i & (uint32_t)(bpp - 1);
+        uint32_t sb = (flags & TF_SWAP) ? (uint32_t)(bpp - 1) - b : b;
+        uint32_t v = plane[(int64_t)(y + r) * pitch + ((int64_t)x + s) * bpp + sb];
+        if ((flags & TF_FLIP) && b == 0) v ^= 0x80u;
+        return v;
+    }
+    PBX_HD int row_filter(int64_t r) const {
+        return filter == 5 ? (int)rowfilt[r] : filter;
+    }
+    PBX_HD uint32_t filtered(int ft, int64_t r, uint32_t i) const {
+        uint32_t cur = be(r, i);
+        if (ft == 0) return cur;
+        uint32_t left = i >= (uint32_t)bpp ? be(r, i - bpp) : 0u;
+        uint32_t up = r > 0 ? be(r - 1, i) : 0u;
+        if (ft == 1) return (cur - left) & 0xFF;
+        if (ft == 2) return (cur - up) & 0xFF;
+        if (ft == 3) return (cur - ((left + up) >> 1)) & 0xFF;
+        uint32_t ul = (r > 0 && i >= (uint32_t)bpp) ? be(r - 1, i - bpp) : 0u;
+        int p = (int)left + (int)up - (int)ul;
+        int pa = p - (int)left, pb = p - (int)up, pc = p - (int)ul;
+        pa = pa < 0 ? -pa : pa; pb = pb < 0 ? -pb : pb; pc = pc < 0 ? -pc : pc;
+        uint32_t pr = (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
+        return (cur - pr) & 0xFF;
+    }
+    // Byte at (row r, column col) of the stream.
+    PBX_HD uint32_t at(int64_t r, uint32_t col) const {
+        if (flags & TF_PNGROWS) {
+            int ft = row_filter(r);
+            if (col == 0) return (uint32_t)ft;
+            return filtered(ft, r, col - 1);
+        }
+        return be(r, col);
+    }
+    // Up to 4 stream bytes starting at stream position p0, packed little-endian.
+    PBX_HD uint32_t fill_word(uint64_t p0, uint32_t nb) const {
+        uint32_t p = (uint32_t)p0;  // tiles are < 2^31 bytes (TileRequestHandler.java:102)
+        uint32_t r = p / rowlen, col = p - r * rowlen, v = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            v |= at(r, col) << (8 * b);
+            if (++col == rowlen) { col = 0; r++; }
+        }
+        return v;
+    }
+};
+
+// A stream already in memory (deflate-only callers and the CPU emulator).
+struct MemStream {
+    const uint8_t* p;
+    PBX_HD uint32_t fill_word(uint64_t p0, uint32_t nb) const {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < nb; b++) v |= (uint32_t)p[p0 + b] << (8 * b);
+        return v;
+    }
+};
+
+// ------------------------------------------------------------------- synthetic planes
+// G_FAKE: Bio-Formats FakeReader.openBytes (pixel = typeMin + x; rows y < 10 carry
+// {series=0, planeNo, z, c, t} in 10-pixel boxes).  G_NOISE: SURVEY.md §8(d) counter-hash
+// noise (12-bit-like 257..1486).  Returns the sample's bit pattern.
+enum : int32_t { GEN_FAKE = 1, GEN_NOISE = 2 };
+
+PBX_HD uint64_t splitmix64(uint64_t k) {
+    uint64_t z = k + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+PBX_HD uint64_t cast_sample(int32_t pt, int64_t v) {
+    switch (pt) {
+    case PT_INT8: case PT_UINT8: return (uint64_t)v & 0xFFull;
+    case PT_INT16: case PT_UINT16: return (uint64_t)v & 0xFFFFull;
+    case PT_INT32: case PT_UINT32: return (uint64_t)v & 0xFFFFFFFFull;
+    case PT_FLOAT: { float f = (float)v; return (uint64_t)__builtin_bit_cast(uint32_t, f); }
+    default: { double d = (double)v; return __builtin_bit_cast(uint64_t, d); }
+    }
+}
+
+PBX_HD uint64_t gen_sample(int32_t kind, uint64_t seed, int32_t plane_no, int32_t z, int32_t c,
+                           int32_t t, int32_t pt, int64_t x, int64_t y) {
+    if (kind == GEN_FAKE) {
+        int64_t v = (pt == PT_INT8 ? -128 : pt == PT_INT16 ? -32768 : pt == PT_INT32 ? -2147483648LL : 0) + x;
+        if (y < 10) {
+            int64_t box = x / 10;
+            if (box == 0) v = 0;
+            else if (box == 1) v = plane_no;
+            else if (box == 2) v = z;
+            else if (box == 3) v = c;
+            else if (box == 4) v = t;
+        }
+        return cast_sample(pt, v);
+    }
+    uint64_t k = (seed << 48) ^ ((uint64_t)(uint32_t)plane_no << 40) ^ ((uint64_t)y << 20) ^ (uint64_t)x;
+    uint64_t r = splitmix64(k);
+    int64_t v = 256 + (((x >> 5) + (y >> 5)) % 16) * 48 + (int64_t)(r & 0xFF) + (int64_t)((r >> 8) & 0xFF);
+    return cast_sample(pt, v);
+}
+
+}  // namespace pbx

@@ -1,0 +1,589 @@
+/*
+ * pbx_oracle.c — CPU restatement of the /tile hot path of omero-ms-pixel-buffer.
+ *
+ * TEST INFRASTRUCTURE ONLY (see pbx_oracle.h).  Never linked into libpbx.so.
+ *
+ * What it restates (all file:line citations are into /root/reference,
+ * src/main/java/com/glencoesoftware/omero/ms/pixelbuffer/):
+ *   - TileRequestHandler.getTile            TileRequestHandler.java:80-139
+ *       w/h == 0 -> full plane size          :92-97
+ *       bpp = bitSize/8, tileSize int math   :100-103
+ *       getTileDirect (big-endian samples)   :104-112, :155
+ *       format null -> raw; png|tif -> writeImage; else null (404)   :119-128
+ *       any exception -> null (404)          :133-138
+ *   - createMetadata (BigEndian, gray, 1 sample, Z=C=T=1)            :145-170
+ *   - writeImage by extension (ImageWriter -> APNGWriter / TiffWriter) :176-199
+ *   - filename header / content type   PixelBufferVerticle.java:118-126,
+ *                                      PixelBufferMicroserviceVerticle.java:373-379
+ * Upstream (third-party, absent from /root/reference) facts restated, per SURVEY.md §8(a):
+ *   1. raw tiles are big-endian;  2. APNGWriter flips the sign bit of int8/int16;
+ *   3. APNGWriter rejects 32/64-bit types (-> exception -> 404);
+ *   4. TiffWriter stores samples verbatim (uncompressed, "MM").
+ * PNG = APNGWriter layout: signature, IHDR, acTL(1 frame), fcTL, IDAT, IEND; every
+ * scanline filter byte 0 (None); zlib level 6 (java.util.zip.Deflater default -1 == 6).
+ * zlib here is the system zlib 1.2.11 (the same algorithm the JDK binds).
+ */
+#include "pbx_oracle.h"
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <zlib.h>
+
+int pbxo_bpp(int pt) {
+    switch (pt) {
+    case PBXO_INT8: case PBXO_UINT8: return 1;
+    case PBXO_INT16: case PBXO_UINT16: return 2;
+    case PBXO_INT32: case PBXO_UINT32: case PBXO_FLOAT: return 4;
+    case PBXO_DOUBLE: return 8;
+    default: return 0;
+    }
+}
+
+int pbxo_is_signed_int(int pt) {
+    return pt == PBXO_INT8 || pt == PBXO_INT16 || pt == PBXO_INT32;
+}
+
+/* ------------------------------------------------------------------ generators */
+
+static uint64_t splitmix64(uint64_t k) {
+    uint64_t z = k + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint64_t cast_to_type(int pt, int64_t v) {
+    union { float f; uint32_t u; } fu;
+    union { double d; uint64_t u; } du;
+    switch (pt) {
+    case PBXO_INT8: case PBXO_UINT8: return (uint64_t)v & 0xFFull;
+    case PBXO_INT16: case PBXO_UINT16: return (uint64_t)v & 0xFFFFull;
+    case PBXO_INT32: case PBXO_UINT32: return (uint64_t)v & 0xFFFFFFFFull;
+    case PBXO_FLOAT: fu.f = (float)v; return fu.u;
+    case PBXO_DOUBLE: du.d = (double)v; return du.u;
+    default: return 0;
+    }
+}
+
+/* G_FAKE follows Bio-Formats FakeReader.openBytes: pixel = typeMin + x, truncated to the
+ * type; rows y < 10 carry {series=0, planeNo, z, c, t} in 10-pixel boxes (x/10 = 0..4).
+ * G_NOISE: SURVEY.md §8(d) counter-hash noise, 12-bit-like values 257..1486. */
+uint64_t pbxo_gen_sample(int kind, uint64_t seed, int plane_no, int z, int c, int t,
+                         int pt, int64_t x, int64_t y) {
+    if (kind == PBXO_GEN_FAKE) {
+        int64_t mn = 0;
+        if (pt == PBXO_INT8) mn = -128;
+        else if (pt == PBXO_INT16) mn = -32768;
+        else if (pt == PBXO_INT32) mn = -2147483648LL;
+        int64_t v = mn + x;
+        if (y < 10) {
+            switch (x / 10) {
+            case 0: v = 0; break;
+            case 1: v = plane_no; break;
+            case 2: v = z; break;
+            case 3: v = c; break;
+            case 4: v = t; break;
+            default: break;
+            }
+        }
+        return cast_to_type(pt, v);
+    }
+    /* G_NOISE */
+    uint64_t k = (seed << 48) ^ ((uint64_t)plane_no << 40) ^ ((uint64_t)y << 20) ^ (uint64_t)x;
+    uint64_t r = splitmix64(k);
+    int64_t v = 256 + (int64_t)(((x >> 5) + (y >> 5)) % 16) * 48 + (int64_t)(r & 0xFF) +
+                (int64_t)((r >> 8) & 0xFF);
+    return cast_to_type(pt, v);
+}
+
+static void put_sample(uint8_t* p, uint64_t v, int bpp, int big_endian) {
+    for (int b = 0; b < bpp; b++) {
+        uint8_t byte = (uint8_t)(v >> (8 * b));
+        if (big_endian) p[bpp - 1 - b] = byte; else p[b] = byte;
+    }
+}
+
+void pbxo_gen_region(int kind, uint64_t seed, int plane_no, int z, int c, int t, int pt,
+                     int64_t x0, int64_t y0, int32_t w, int32_t h, int big_endian, uint8_t* out) {
+    int bpp = pbxo_bpp(pt);
+    for (int32_t yy = 0; yy < h; yy++)
+        for (int32_t xx = 0; xx < w; xx++) {
+            uint64_t v = pbxo_gen_sample(kind, seed, plane_no, z, c, t, pt, x0 + xx, y0 + yy);
+            put_sample(out + ((size_t)yy * w + xx) * bpp, v, bpp, big_endian);
+        }
+}
+
+/* ------------------------------------------------------------------ extraction */
+
+void pbxo_extract_be(const uint8_t* plane, int plane_be, int pt, int64_t pitch, int32_t x,
+                     int32_t y, int32_t w, int32_t h, uint8_t* out) {
+    int bpp = pbxo_bpp(pt);
+    for (int32_t r = 0; r < h; r++) {
+        const uint8_t* src = plane + (int64_t)(y + r) * pitch + (int64_t)x * bpp;
+        uint8_t* dst = out + (size_t)r * w * bpp;
+        if (plane_be || bpp == 1) {
+            memcpy(dst, src, (size_t)w * bpp);
+        } else {
+            for (int32_t i = 0; i < w; i++)
+                for (int b = 0; b < bpp; b++) dst[i * bpp + b] = src[i * bpp + bpp - 1 - b];
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ PNG */
+
+static void be32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+static void be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static uint32_t rd32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+static int paeth(int a, int b, int c) {
+    int p = a + b - c, pa = abs(p - a), pb = abs(p - b), pc = abs(p - c);
+    if (pa <= pb && pa <= pc) return a;
+    if (pb <= pc) return b;
+    return c;
+}
+
+static uint8_t filt_byte(int ft, int cur, int left, int up, int ul) {
+    switch (ft) {
+    case 0: return (uint8_t)cur;
+    case 1: return (uint8_t)(cur - left);
+    case 2: return (uint8_t)(cur - up);
+    case 3: return (uint8_t)(cur - ((left + up) >> 1));
+    default: return (uint8_t)(cur - paeth(left, up, ul));
+    }
+}
+
+/* APNGWriter sign flip for int8/int16: the most significant byte of
+ * each big-endian sample gets its top bit flipped (v + 2^(n-1) mod 2^n). */
+static void png_row_bytes(const uint8_t* row_be, int pt, int32_t w, uint8_t* dst) {
+    int bpp = pbxo_bpp(pt);
+    size_t n = (size_t)w * bpp;
+    memcpy(dst, row_be, n);
+    if (pt == PBXO_INT8 || pt == PBXO_INT16)
+        for (size_t i = 0; i < n; i += bpp) dst[i] ^= 0x80;
+}
+
+size_t pbxo_png_filter_stream(const uint8_t* tile_be, int pt, int32_t w, int32_t h, int filter,
+                              uint8_t* out) {
+    int bpp = pbxo_bpp(pt);
+    size_t rb = (size_t)w * bpp, rl = rb + 1;
+    uint8_t* prev = (uint8_t*)calloc(rb + 1, 1);
+    uint8_t* cur = (uint8_t*)calloc(rb + 1, 1);
+    for (int32_t r = 0; r < h; r++) {
+        png_row_bytes(tile_be + (size_t)r * rb, pt, w, cur);
+        int ft = filter;
+        if (filter == 5) { /* adaptive: minimum sum of |signed residual|, ties -> lowest */
+            uint64_t best = UINT64_MAX;
+            for (int f = 0; f < 5; f++) {
+                uint64_t s = 0;
+                for (size_t i = 0; i < rb; i++) {
+                    int left = i >= (size_t)bpp ? cur[i - bpp] : 0;
+                    int ul = i >= (size_t)bpp ? prev[i - bpp] : 0;
+                    int8_t v = (int8_t)filt_byte(f, cur[i], left, prev[i], ul);
+                    s += (uint64_t)(v < 0 ? -v : v);
+                }
+                if (s < best) { best = s; ft = f; }
+            }
+        }
+        uint8_t* o = out + (size_t)r * rl;
+        o[0] = (uint8_t)ft;
+        for (size_t i = 0; i < rb; i++) {
+            int left = i >= (size_t)bpp ? cur[i - bpp] : 0;
+            int ul = i >= (size_t)bpp ? prev[i - bpp] : 0;
+            o[1 + i] = filt_byte(ft, cur[i], left, prev[i], ul);
+        }
+        uint8_t* tmp = prev; prev = cur; cur = tmp;
+    }
+    free(prev);
+    free(cur);
+    return (size_t)h * rl;
+}
+
+static size_t put_chunk(uint8_t* out, const char* type, const uint8_t* data, uint32_t n) {
+    be32(out, n);
+    memcpy(out + 4, type, 4);
+    if (n) memcpy(out + 8, data, n);
+    uint32_t crc = (uint32_t)crc32(0L, out + 4, 4 + n);
+    be32(out + 8 + n, crc);
+    return 12 + (size_t)n;
+}
+
+size_t pbxo_png_max_size(int pt, int32_t w, int32_t h) {
+    size_t raw = (size_t)h * (1 + (size_t)w * pbxo_bpp(pt));
+    return 8 + 25 + 20 + 38 + 12 + compressBound((uLong)raw) + 12 + 64;
+}
+
+int pbxo_png_encode(const uint8_t* tile_be, int pt, int32_t w, int32_t h, int level,
+                    uint8_t* out, size_t cap, size_t* len) {
+    /* APNGWriter supports int8/uint8/int16/uint16 only ("Unsupported image type"). */
+    if (!(pt == PBXO_INT8 || pt == PBXO_UINT8 || pt == PBXO_INT16 || pt == PBXO_UINT16))
+        return PBXO_E_NOTFOUND;
+    if (w <= 0 || h <= 0) return PBXO_E_NOTFOUND;
+    if (cap < pbxo_png_max_size(pt, w, h)) return PBXO_E_INTERNAL;
+    int bpp = pbxo_bpp(pt);
+    size_t raw_len = (size_t)h * (1 + (size_t)w * bpp);
+    uint8_t* raw = (uint8_t*)malloc(raw_len);
+    pbxo_png_filter_stream(tile_be, pt, w, h, 0, raw);
+    uLongf zlen = compressBound((uLong)raw_len);
+    uint8_t* z = (uint8_t*)malloc(zlen);
+    int zr = compress2(z, &zlen, raw, (uLong)raw_len, level);
+    free(raw);
+    if (zr != Z_OK) { free(z); return PBXO_E_INTERNAL; }
+
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+    size_t o = 0;
+    memcpy(out, sig, 8); o += 8;
+    uint8_t ihdr[13];
+    be32(ihdr, (uint32_t)w); be32(ihdr + 4, (uint32_t)h);
+    ihdr[8] = (uint8_t)(8 * bpp); ihdr[9] = 0; ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;
+    o += put_chunk(out + o, "IHDR", ihdr, 13);
+    uint8_t actl[8];
+    be32(actl, 1); be32(actl + 4, 0);
+    o += put_chunk(out + o, "acTL", actl, 8);
+    uint8_t fctl[26];
+    memset(fctl, 0, sizeof fctl);
+    be32(fctl, 0); be32(fctl + 4, (uint32_t)w); be32(fctl + 8, (uint32_t)h);
+    o += put_chunk(out + o, "fcTL", fctl, 26);
+    o += put_chunk(out + o, "IDAT", z, (uint32_t)zlen);
+    o += put_chunk(out + o, "IEND", NULL, 0);
+    free(z);
+    *len = o;
+    return PBXO_OK;
+}
+
+/* ------------------------------------------------------------------ TIFF */
+
+#define TIFF_NTAGS 11
+#define TIFF_DATA_OFFSET 160 /* 8 + 2 + 11*12 + 4 = 146, rounded up to 16 */
+
+size_t pbxo_tiff_size(int pt, int32_t w, int32_t h) {
+    return TIFF_DATA_OFFSET + (size_t)w * h * pbxo_bpp(pt);
+}
+
+static size_t tiff_tag(uint8_t* p, uint16_t tag, uint16_t type, uint32_t count, uint32_t v) {
+    be16(p, tag); be16(p + 2, type); be32(p + 4, count);
+    if (type == 3) { be16(p + 8, v); be16(p + 10, 0); } else be32(p + 8, v);
+    return 12;
+}
+
+/* Classic big-endian TIFF (TiffWriter with PixelsBigEndian=true, TileRequestHandler.java:155),
+ * Compression=1, one strip.  Strip layout is Bio-Formats' choice upstream (unpinned); the
+ * decoded samples are what parity is defined on. */
+int pbxo_tiff_encode(const uint8_t* tile_be, int pt, int32_t w, int32_t h, uint8_t* out,
+                     size_t cap, size_t* len) {
+    int bpp = pbxo_bpp(pt);
+    if (bpp == 0 || w <= 0 || h <= 0) return PBXO_E_NOTFOUND;
+    size_t n = (size_t)w * h * bpp;
+    if (cap < TIFF_DATA_OFFSET + n) return PBXO_E_INTERNAL;
+    memset(out, 0, TIFF_DATA_OFFSET);
+    out[0] = 'M'; out[1] = 'M'; be16(out + 2, 42); be32(out + 4, 8);
+    uint8_t* p = out + 8;
+    be16(p, TIFF_NTAGS); p += 2;
+    int sf = (pt == PBXO_FLOAT || pt == PBXO_DOUBLE) ? 3 : (pbxo_is_signed_int(pt) ? 2 : 1);
+    p += tiff_tag(p, 256, 4, 1, (uint32_t)w);
+    p += tiff_tag(p, 257, 4, 1, (uint32_t)h);
+    p += tiff_tag(p, 258, 3, 1, (uint32_t)(8 * bpp));
+    p += tiff_tag(p, 259, 3, 1, 1);
+    p += tiff_tag(p, 262, 3, 1, 1);
+    p += tiff_tag(p, 273, 4, 1, TIFF_DATA_OFFSET);
+    p += tiff_tag(p, 277, 3, 1, 1);
+    p += tiff_tag(p, 278, 4, 1, (uint32_t)h);
+    p += tiff_tag(p, 279, 4, 1, (uint32_t)n);
+    p += tiff_tag(p, 284, 3, 1, 1);
+    p += tiff_tag(p, 339, 3, 1, (uint32_t)sf);
+    be32(p, 0);
+    memcpy(out + TIFF_DATA_OFFSET, tile_be, n);
+    *len = TIFF_DATA_OFFSET + n;
+    return PBXO_OK;
+}
+
+/* ------------------------------------------------------------------ getTile */
+
+int pbxo_get_tile(const uint8_t* plane, int plane_be, int pt, int32_t size_x, int32_t size_y,
+                  int32_t x, int32_t y, int32_t w, int32_t h, int format, uint8_t* out,
+                  size_t cap, size_t* len, int32_t* out_w, int32_t* out_h) {
+    if (w == 0) w = size_x; /* TileRequestHandler.java:92-94 */
+    if (h == 0) h = size_y; /* :95-97 */
+    if (out_w) *out_w = w;
+    if (out_h) *out_h = h;
+    int bpp = pbxo_bpp(pt);
+    if (bpp == 0) return PBXO_E_NOTFOUND;
+    /* int tileSize = width * height * bytesPerPixel (:102); Java int overflow -> negative
+     * array size or a short buffer -> exception -> null (:133-138). */
+    int64_t tile_size = (int64_t)w * h * bpp;
+    if (w < 0 || h < 0 || tile_size > 2147483647LL) return PBXO_E_NOTFOUND;
+    /* getTileDirect outside the plane throws (ext. PixelBuffer) -> 404 */
+    if (x < 0 || y < 0 || (int64_t)x + w > size_x || (int64_t)y + h > size_y)
+        return PBXO_E_NOTFOUND;
+    if (tile_size == 0) return PBXO_E_NOTFOUND;
+    uint8_t* tile = (uint8_t*)malloc((size_t)tile_size);
+    pbxo_extract_be(plane, plane_be, pt, (int64_t)size_x * bpp, x, y, w, h, tile);
+    int st = PBXO_OK;
+    if (format == PBXO_FMT_RAW) {
+        if (cap < (size_t)tile_size) st = PBXO_E_INTERNAL;
+        else { memcpy(out, tile, (size_t)tile_size); *len = (size_t)tile_size; }
+    } else if (format == PBXO_FMT_PNG) {
+        st = pbxo_png_encode(tile, pt, w, h, 6, out, cap, len);
+    } else if (format == PBXO_FMT_TIF) {
+        st = pbxo_tiff_encode(tile, pt, w, h, out, cap, len);
+    } else {
+        st = PBXO_E_NOTFOUND; /* "Unknown output format" -> null (:125-126) */
+    }
+    free(tile);
+    return st;
+}
+
+/* ------------------------------------------------------------------ decoders */
+
+int pbxo_zlib_compress(const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                       size_t* out_len) {
+    uLongf zl = (uLongf)cap;
+    int r = compress2(out, &zl, in, (uLong)n, level);
+    *out_len = zl;
+    return r == Z_OK ? 0 : -1;
+}
+
+int pbxo_zlib_inflate(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+    z_stream s;
+    memset(&s, 0, sizeof s);
+    if (inflateInit(&s) != Z_OK) return -1;
+    s.next_in = (Bytef*)in; s.avail_in = (uInt)n;
+    s.next_out = out; s.avail_out = (uInt)cap;
+    int r = inflate(&s, Z_FINISH);
+    *out_len = s.total_out;
+    int ok = (r == Z_STREAM_END) && s.avail_in == 0;
+    inflateEnd(&s);
+    return ok ? 0 : -1;
+}
+
+uint32_t pbxo_crc32(uint32_t crc, const uint8_t* p, size_t n) { return (uint32_t)crc32(crc, p, (uInt)n); }
+uint32_t pbxo_adler32(uint32_t a, const uint8_t* p, size_t n) { return (uint32_t)adler32(a, p, (uInt)n); }
+
+/* Collect IDAT payload after validating signature + chunk CRCs. */
+static int png_collect(const uint8_t* png, size_t len, uint8_t** idat, size_t* idat_len,
+                       int32_t* w, int32_t* h, int32_t* depth, int32_t* ctype) {
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+    if (len < 8 || memcmp(png, sig, 8) != 0) return -1;
+    size_t o = 8, cap = 0, n = 0;
+    uint8_t* buf = NULL;
+    int seen_ihdr = 0, seen_iend = 0;
+    while (o + 12 <= len) {
+        uint32_t cl = rd32(png + o);
+        if (o + 12 + (size_t)cl > len) { free(buf); return -2; }
+        const uint8_t* type = png + o + 4;
+        uint32_t crc = (uint32_t)crc32(0L, type, 4 + cl);
+        if (crc != rd32(png + o + 8 + cl)) { free(buf); return -3; }
+        if (!memcmp(type, "IHDR", 4)) {
+            if (cl != 13) { free(buf); return -4; }
+            *w = (int32_t)rd32(type + 4); *h = (int32_t)rd32(type + 8);
+            *depth = type[12]; *ctype = type[13];
+            if (type[14] || type[15] || type[16]) { free(buf); return -5; }
+            seen_ihdr = 1;
+        } else if (!memcmp(type, "IDAT", 4)) {
+            if (n + cl > cap) { cap = (n + cl) * 2 + 1024; buf = (uint8_t*)realloc(buf, cap); }
+            memcpy(buf + n, type + 4, cl); n += cl;
+        } else if (!memcmp(type, "IEND", 4)) {
+            seen_iend = 1;
+            o += 12 + cl;
+            break;
+        }
+        o += 12 + cl;
+    }
+    if (!seen_ihdr || !seen_iend || o != len) { free(buf); return -6; }
+    *idat = buf; *idat_len = n;
+    return 0;
+}
+
+int pbxo_png_inflate_idat(const uint8_t* png, size_t len, uint8_t* out, size_t cap, size_t* out_len) {
+    uint8_t* idat = NULL; size_t il = 0; int32_t w, h, d, ct;
+    int r = png_collect(png, len, &idat, &il, &w, &h, &d, &ct);
+    if (r) return r;
+    r = pbxo_zlib_inflate(idat, il, out, cap, out_len);
+    free(idat);
+    return r;
+}
+
+int pbxo_png_decode(const uint8_t* png, size_t len, uint8_t* out, size_t cap, int32_t* w,
+                    int32_t* h, int32_t* depth, int32_t* ctype) {
+    uint8_t* idat = NULL; size_t il = 0;
+    int r = png_collect(png, len, &idat, &il, w, h, depth, ctype);
+    if (r) return r;
+    if (*ctype != 0 || (*depth != 8 && *depth != 16)) { free(idat); return -7; }
+    int bpp = *depth / 8;
+    size_t rb = (size_t)(*w) * bpp, rl = rb + 1, need = rl * (size_t)(*h);
+    if (cap < rb * (size_t)(*h)) { free(idat); return -8; }
+    uint8_t* raw = (uint8_t*)malloc(need + 1);
+    size_t got = 0;
+    r = pbxo_zlib_inflate(idat, il, raw, need + 1, &got);
+    free(idat);
+    if (r || got != need) { free(raw); return -9; }
+    for (int32_t y = 0; y < *h; y++) {
+        const uint8_t* f = raw + (size_t)y * rl;
+        uint8_t* cur = out + (size_t)y * rb;
+        const uint8_t* prev = y ? out + (size_t)(y - 1) * rb : NULL;
+        int ft = f[0];
+        if (ft > 4) { free(raw); return -10; }
+        for (size_t i = 0; i < rb; i++) {
+            int a = i >= (size_t)bpp ? cur[i - bpp] : 0;
+            int b = prev ? prev[i] : 0;
+            int c = (prev && i >= (size_t)bpp) ? prev[i - bpp] : 0;
+            int x = f[1 + i], v;
+            switch (ft) {
+            case 0: v = x; break;
+            case 1: v = x + a; break;
+            case 2: v = x + b; break;
+            case 3: v = x + ((a + b) >> 1); break;
+            default: v = x + paeth(a, b, c); break;
+            }
+            cur[i] = (uint8_t)v;
+        }
+    }
+    free(raw);
+    return 0;
+}
+
+static uint32_t tget(const uint8_t* p, int be, int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; i++) v = be ? (v << 8) | p[i] : v | ((uint32_t)p[i] << (8 * i));
+    return v;
+}
+
+static uint32_t tiff_value(const uint8_t* tif, size_t len, const uint8_t* e, int be, uint32_t idx) {
+    uint16_t type = (uint16_t)tget(e + 2, be, 2);
+    uint32_t count = tget(e + 4, be, 4);
+    int sz = type == 3 ? 2 : 4;
+    const uint8_t* base = e + 8;
+    if ((uint64_t)count * sz > 4) {
+        uint32_t off = tget(e + 8, be, 4);
+        if ((size_t)off + (size_t)count * sz > len) return 0;
+        base = tif + off;
+    }
+    return tget(base + (size_t)idx * sz, be, sz);
+}
+
+int pbxo_tiff_decode(const uint8_t* tif, size_t len, uint8_t* out, size_t cap, int32_t* w,
+                     int32_t* h, int32_t* bits, int32_t* sf, int32_t* comp, int32_t* big_endian) {
+    if (len < 8) return -1;
+    int be;
+    if (tif[0] == 'M' && tif[1] == 'M') be = 1;
+    else if (tif[0] == 'I' && tif[1] == 'I') be = 0;
+    else return -1;
+    if (tget(tif + 2, be, 2) != 42) return -2;
+    uint32_t ifd = tget(tif + 4, be, 4);
+    if ((size_t)ifd + 2 > len) return -3;
+    uint32_t nt = tget(tif + ifd, be, 2);
+    if ((size_t)ifd + 2 + nt * 12 + 4 > len) return -3;
+    uint32_t rps = 0, nstrips = 0, spp = 1, planar = 1;
+    const uint8_t *offs = NULL, *cnts = NULL;
+    *w = *h = 0; *bits = 0; *sf = 1; *comp = 1; *big_endian = be;
+    for (uint32_t i = 0; i < nt; i++) {
+        const uint8_t* e = tif + ifd + 2 + 12 * i;
+        uint16_t tag = (uint16_t)tget(e, be, 2);
+        switch (tag) {
+        case 256: *w = (int32_t)tiff_value(tif, len, e, be, 0); break;
+        case 257: *h = (int32_t)tiff_value(tif, len, e, be, 0); break;
+        case 258: *bits = (int32_t)tiff_value(tif, len, e, be, 0); break;
+        case 259: *comp = (int32_t)tiff_value(tif, len, e, be, 0); break;
+        case 273: offs = e; nstrips = tget(e + 4, be, 4); break;
+        case 277: spp = tiff_value(tif, len, e, be, 0); break;
+        case 278: rps = tiff_value(tif, len, e, be, 0); break;
+        case 279: cnts = e; break;
+        case 284: planar = tiff_value(tif, len, e, be, 0); break;
+        case 339: *sf = (int32_t)tiff_value(tif, len, e, be, 0); break;
+        default: break;
+        }
+    }
+    if (!offs || !cnts || spp != 1 || planar != 1 || *bits % 8) return -4;
+    if (rps == 0) rps = (uint32_t)*h;
+    size_t rb = (size_t)(*w) * (*bits / 8), total = rb * (size_t)(*h), o = 0;
+    if (cap < total) return -5;
+    for (uint32_t s = 0; s < nstrips; s++) {
+        uint32_t off = tiff_value(tif, len, offs, be, s);
+        uint32_t cnt = tiff_value(tif, len, cnts, be, s);
+        if ((size_t)off + cnt > len) return -6;
+        size_t rows = rps;
+        if ((size_t)s * rps + rows > (size_t)*h) rows = (size_t)*h - (size_t)s * rps;
+        size_t want = rows * rb;
+        if (*comp == 1) {
+            if (cnt < want) return -7;
+            memcpy(out + o, tif + off, want);
+        } else if (*comp == 8 || *comp == 32946) {
+            size_t got = 0;
+            if (pbxo_zlib_inflate(tif + off, cnt, out + o, want, &got) || got != want) return -8;
+        } else {
+            return -9;
+        }
+        o += want;
+    }
+    return o == total ? 0 : -10;
+}
+
+/* ------------------------------------------------------------------ metadata */
+
+int pbxo_tile_filename(int64_t id, int32_t z, int32_t c, int32_t t, int32_t x, int32_t y, int32_t w,
+                       int32_t h, const char* format, char* out, size_t cap) {
+    return snprintf(out, cap, "image%lld_z%d_c%d_t%d_x%d_y%d_w%d_h%d.%s", (long long)id, z, c, t,
+                    x, y, w, h, format ? format : "bin");
+}
+
+const char* pbxo_content_type(const char* format) {
+    if (format && !strcmp(format, "png")) return "image/png";
+    if (format && !strcmp(format, "tif")) return "image/tiff";
+    return "application/octet-stream";
+}
+
+/* ------------------------------------------------------------------ CPU baseline */
+
+typedef struct {
+    const uint8_t* plane; int pt, format; int32_t pw, ph, w, h; int first, step, tiles;
+    uint64_t bytes;
+} bench_arg;
+
+static void* bench_worker(void* p) {
+    bench_arg* a = (bench_arg*)p;
+    int bpp = pbxo_bpp(a->pt);
+    size_t cap = pbxo_png_max_size(a->pt, a->w, a->h) + pbxo_tiff_size(a->pt, a->w, a->h);
+    uint8_t* out = (uint8_t*)malloc(cap);
+    int gx = a->pw / a->w, gy = a->ph / a->h;
+    (void)bpp;
+    for (int i = a->first; i < a->tiles; i += a->step) {
+        int tx = i % gx, ty = (i / gx) % gy;
+        size_t len = 0;
+        int32_t ow, oh;
+        pbxo_get_tile(a->plane, 0, a->pt, a->pw, a->ph, tx * a->w, ty * a->h, a->w, a->h,
+                      a->format, out, cap, &len, &ow, &oh);
+        a->bytes += len;
+    }
+    free(out);
+    return NULL;
+}
+
+double pbxo_bench(int kind, int pt, int format, int32_t pw, int32_t ph, int32_t w, int32_t h,
+                  int tiles, int threads, uint64_t* out_bytes) {
+    int bpp = pbxo_bpp(pt);
+    uint8_t* plane = (uint8_t*)malloc((size_t)pw * ph * bpp);
+    pbxo_gen_region(kind, 0, 0, 0, 0, 0, pt, 0, 0, pw, ph, 0, plane); /* little-endian plane */
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    bench_arg* args = (bench_arg*)calloc((size_t)threads, sizeof(bench_arg));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        bench_arg a = {plane, pt, format, pw, ph, w, h, i, threads, tiles, 0};
+        args[i] = a;
+        pthread_create(&th[i], NULL, bench_worker, &args[i]);
+    }
+    uint64_t total = 0;
+    for (int i = 0; i < threads; i++) { pthread_join(th[i], NULL); total += args[i].bytes; }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(th); free(args); free(plane);
+    if (out_bytes) *out_bytes = total;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
