@@ -1,0 +1,463 @@
+// kernels.hip — gfx950 (MI355X / CDNA4) kernels of the /tile pipeline.
+//
+//   k_gen_plane    synthetic planes in HBM (G_FAKE = Bio-Formats FakeReader, G_NOISE)
+//   k_extract      K1  raw + uncompressed TIFF: PixelBuffer.getTileDirect + big-endian
+//                      (TileRequestHandler.java:104-112,128; TiffWriter via :122-123)
+//   k_rowfilter    K2  per-scanline PNG filter choice (min sum |residual|), adaptive mode
+//   k_deflate      K3/K4 fused getTileDirect + PNG filter + LZ77 (LDS) + Huffman + packing,
+//                      one workgroup per 16 KiB segment (writeImage("png"), :176-199)
+//   k_tile_sizes   K7  container size per tile  -> k_scan_offsets: exclusive scan
+//   k_assemble     K5/K6 zlib framing (Adler-32 combine), PNG chunks (CRC-32 combine,
+//                      APNGWriter layout) or deflate-TIFF header, compacted output
+//
+// All integer/byte work, HBM- or LDS/ALU-bound: no MFMA.  Kernels are written for wave64
+// and use ballot/readlane for the serial parts of the parse.
+#include <hip/hip_runtime.h>
+
+#include "deflate_seg.h"
+#include "pbx_common.h"
+#include "pbx_config.h"
+#include "pbx_kernels.h"
+
+namespace pbx {
+
+using DC = DeflateMainCfg;
+
+struct DevOps {
+    __device__ static void amin(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+    __device__ static void add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+};
+
+// Bijective XCD-aware remap: consecutive logical ids land on the same XCD (shared L2),
+// since workgroups are dealt round-robin over the 8 XCDs.  Speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+    const uint32_t q = n / 8, r = n % 8, x = b % 8, i = b / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+// Largest i with key(i) <= v, for a non-decreasing key (uniform across the workgroup).
+template <class F>
+__device__ __forceinline__ uint32_t upper_index(uint32_t n, uint32_t v, F key) {
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (key(mid) <= v) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Exclusive prefix sum of arr[0..NT) in place; returns the total.  Wave64 shuffles + LDS.
+template <int NT>
+__device__ uint32_t block_scan_excl_add(uint32_t* arr, uint32_t* wtot, uint32_t tid) {
+    const uint32_t v = arr[tid], lane = tid & 63, w = tid >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= (uint32_t)off) inc += t;
+    }
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        const uint32_t x = wtot[i];
+        pre += (uint32_t)i < w ? x : 0u;
+        tot += x;
+    }
+    arr[tid] = pre + inc - v;
+    __syncthreads();
+    return tot;
+}
+
+// Wave-serial greedy parse of one sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).
+template <class C>
+__device__ void ph_parse_dev(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
+    const uint32_t w = tid >> 6, lane = tid & 63;
+    const uint32_t ss = w * C::SUB;
+    const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
+    uint32_t nm = 0, pos = ss;
+    while (pos < se) {
+        uint32_t L, D;
+        eval_pos<C>(S, sp, pos + lane, se, L, D);
+        const uint64_t mask = __ballot(L >= 3);
+        uint32_t o = 0;
+        while (o < 64) {
+            const uint64_t m = mask >> o;
+            if (!m) { o = 64; break; }
+            const uint32_t k = o + (uint32_t)__builtin_ctzll(m);
+            uint32_t Lk = __builtin_amdgcn_readlane(L, k);
+            const uint32_t Dk = __builtin_amdgcn_readlane(D, k);
+            if (k + 1 < 64) {
+                const uint32_t L1 = __builtin_amdgcn_readlane(L, k + 1);
+                if (L1 > Lk) { o = k + 1; continue; }  // lazy: a longer match starts next
+            }
+            const uint32_t p = pos + k;
+            const uint32_t rem = se - p;
+            const uint32_t maxlen = rem < 258 ? rem : 258;
+            if (Lk >= (uint32_t)C::CAP && Lk < maxlen) {
+                // one wave-wide compare of 4 bytes per lane extends the match past the cap
+                const uint32_t a = sp.wl + p, off = Lk + 4 * lane;
+                const uint32_t x = off < maxlen ? (lds_ld4(S, a - Dk + off) ^ lds_ld4(S, a + off)) : 0u;
+                const uint64_t mm = __ballot(off >= maxlen || x != 0);
+                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+                const uint32_t xf = __builtin_amdgcn_readlane(x, f);
+                const uint32_t of = Lk + 4 * f;
+                uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
+                Lk = l < maxlen ? l : maxlen;
+            }
+            if (nm < (uint32_t)C::MAXMW) {
+                if (lane == 0) {
+                    S.mpos[w * C::MAXMW + nm] = p | ((Lk - 3) << 16);
+                    S.mdist[w * C::MAXMW + nm] = Dk - 1;
+                }
+                nm++;
+            }
+            o = k + Lk;
+        }
+        pos += o;
+    }
+    if (lane == 0) S.w_nm[w] = nm;
+}
+
+template <class C>
+__global__ __launch_bounds__(C::NT) void k_deflate(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                   uint32_t nseg, const uint8_t* __restrict__ rowfilt,
+                                                   uint8_t* __restrict__ slots, uint32_t slot_stride,
+                                                   SegOut* __restrict__ segout) {
+    __shared__ DeflateSmem<C> S;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
+    if (seg >= nseg) return;
+    const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
+    const TileDesc d = dt[ti];
+    TileStream src;
+    src.init(d, rowfilt);
+    const uint32_t k = seg - d.seg_first;
+    const uint64_t s = (uint64_t)k * d.seg_len;
+    SegParams sp;
+    sp.sl = (uint32_t)((d.stream_len - s) < d.seg_len ? (d.stream_len - s) : d.seg_len);
+    sp.wl = (uint32_t)(s < (uint64_t)C::WIN ? s : (uint64_t)C::WIN);
+    sp.base = s - sp.wl;
+    sp.rowlen = d.rowlen;
+    sp.last = (k + 1 == d.seg_count) ? 1u : 0u;
+
+    ph_fill<C>(tid, S, src, sp);
+    __syncthreads();
+    ph_insert<C, DevOps>(tid, S, sp);
+    __syncthreads();
+    ph_parse_dev<C>(tid, S, sp);
+    __syncthreads();
+    ph_hist<C, DevOps>(tid, S, sp);
+    __syncthreads();
+    ph_rank<C>(tid, S);
+    __syncthreads();
+    ph_huff<C>(tid, S, sp);
+    __syncthreads();
+    ph_bits<C>(tid, S, sp);
+    __syncthreads();
+    const uint32_t total = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
+    if (tid == 0) S.misc[M_DATABITS] = total;
+    __syncthreads();
+    ph_write<C, DevOps>(tid, S, sp);
+    __syncthreads();
+    ph_store<C>(tid, S, sp, slots + (size_t)seg * slot_stride);
+    __syncthreads();
+#pragma unroll 1
+    for (int lv = 0; lv < C::LOGNT; lv++) {
+        ph_tree<C>(tid, S, lv);
+        __syncthreads();
+    }
+    ph_final<C>(tid, S, sp, &segout[seg]);
+}
+
+// ------------------------------------------------------------------- synthetic planes
+__global__ __launch_bounds__(256) void k_gen_plane(uint8_t* __restrict__ out, int64_t pitch,
+                                                   int32_t sx, int32_t sy, int32_t pt, int32_t bpp,
+                                                   int32_t kind, uint64_t seed, int32_t plane_no,
+                                                   int32_t z, int32_t c, int32_t t) {
+    const uint64_t total = (uint64_t)sx * (uint64_t)sy;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+        const uint64_t y = idx / (uint64_t)sx, x = idx - y * (uint64_t)sx;
+        const uint64_t v = gen_sample(kind, seed, plane_no, z, c, t, pt, (int64_t)x, (int64_t)y);
+        uint8_t* p = out + (int64_t)y * pitch + (int64_t)x * bpp;
+        switch (bpp) {
+        case 1: *p = (uint8_t)v; break;
+        case 2: *(uint16_t*)p = (uint16_t)v; break;
+        case 4: *(uint32_t*)p = (uint32_t)v; break;
+        default: *(uint64_t*)p = v; break;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ extraction
+__device__ __forceinline__ uint32_t bswap16x2(uint32_t v) {
+    return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu);
+}
+
+__device__ __forceinline__ uint4 swap16(uint4 q, int bpp) {
+    if (bpp == 2) {
+        q.x = bswap16x2(q.x); q.y = bswap16x2(q.y); q.z = bswap16x2(q.z); q.w = bswap16x2(q.w);
+    } else if (bpp == 4) {
+        q.x = __builtin_bswap32(q.x); q.y = __builtin_bswap32(q.y);
+        q.z = __builtin_bswap32(q.z); q.w = __builtin_bswap32(q.w);
+    } else if (bpp == 8) {
+        const uint32_t a = __builtin_bswap32(q.x), b = __builtin_bswap32(q.y);
+        const uint32_t c = __builtin_bswap32(q.z), d = __builtin_bswap32(q.w);
+        q.x = b; q.y = a; q.z = d; q.w = c;
+    }
+    return q;
+}
+
+__global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft, uint32_t nft,
+                                                 uint8_t* __restrict__ out) {
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t ti = upper_index(nft, b, [&](uint32_t i) { return ft[i].blk_first; });
+    const TileDesc d = ft[ti];
+    const uint32_t rb = (uint32_t)d.w * (uint32_t)d.bpp;
+    const uint32_t r0 = (b - d.blk_first) * d.rows_per_blk;
+    const uint32_t r1 = r0 + d.rows_per_blk < (uint32_t)d.h ? r0 + d.rows_per_blk : (uint32_t)d.h;
+    uint8_t* base = out + d.out_off;
+    if (d.flags & TF_TIFF) {
+        if (r0 == 0 && tid == 0)
+            write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 1, rb * d.h);
+        base += TIFF_DATA_OFFSET;
+    }
+    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
+    const bool fast = (((uintptr_t)src0 | (uintptr_t)base | (uintptr_t)d.pitch | rb) & 15u) == 0;
+    const bool swap = (d.flags & TF_SWAP) != 0;
+    if (fast) {
+        const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
+        for (uint32_t i = tid; i < nv; i += 256) {
+            const uint32_t r = r0 + i / n16, v = i % n16;
+            uint4 q = *(const uint4*)(src0 + (int64_t)r * d.pitch + 16 * v);
+            if (swap) q = swap16(q, d.bpp);
+            *(uint4*)(base + (size_t)r * rb + 16 * v) = q;
+        }
+    } else {
+        TileStream ts;
+        ts.init(d, nullptr);
+        const uint32_t nbytes = (r1 - r0) * rb;
+        for (uint32_t i = tid; i < nbytes; i += 256) {
+            const uint32_t r = r0 + i / rb, c = i % rb;
+            base[(size_t)r * rb + c] = (uint8_t)ts.be(r, c);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ PNG row filter
+__global__ __launch_bounds__(256) void k_rowfilter(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                   uint32_t nrows, uint8_t* __restrict__ rowfilt) {
+    const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (gw >= nrows) return;
+    const uint32_t ti = upper_index(ndt, gw, [&](uint32_t i) { return dt[i].blk_first; });
+    const TileDesc d = dt[ti];
+    TileStream ts;
+    ts.init(d, nullptr);
+    const int64_t r = gw - d.blk_first;
+    const uint32_t rb = (uint32_t)d.w * d.bpp, bpp = d.bpp;
+    uint32_t sum[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i = lane; i < rb; i += 64) {
+        const int cur = (int)ts.be(r, i);
+        const int left = i >= bpp ? (int)ts.be(r, i - bpp) : 0;
+        const int up = r > 0 ? (int)ts.be(r - 1, i) : 0;
+        const int ul = (r > 0 && i >= bpp) ? (int)ts.be(r - 1, i - bpp) : 0;
+        const int p = left + up - ul;
+        const int pa = abs(p - left), pb = abs(p - up), pc = abs(p - ul);
+        const int pr = (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
+        const int v[5] = {cur, cur - left, cur - up, cur - ((left + up) >> 1), cur - pr};
+#pragma unroll
+        for (int f = 0; f < 5; f++) sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)(v[f] & 0xFF));
+    }
+#pragma unroll
+    for (int f = 0; f < 5; f++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum[f] += __shfl_xor(sum[f], off, 64);
+    if (lane == 0) {
+        int best = 0;
+        for (int f = 1; f < 5; f++) if (sum[f] < sum[best]) best = f;
+        rowfilt[d.rowfilt_off + r] = (uint8_t)best;
+    }
+}
+
+// ------------------------------------------------------------------- sizes + scan
+__device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
+    return (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET + ZLIB_HDR_BYTES + payload + 4
+                               : PNG_IDAT_DATA_OFF + ZLIB_HDR_BYTES + payload + PNG_TAIL_BYTES;
+}
+
+__global__ __launch_bounds__(256) void k_tile_sizes(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                    const SegOut* __restrict__ so,
+                                                    uint64_t* __restrict__ sizes) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc& d = dt[i];
+    uint64_t tot = 0;
+    for (uint32_t k = 0; k < d.seg_count; k++) tot += so[d.seg_first + k].nbytes;
+    sizes[i] = container_bytes(d, tot);
+}
+
+__global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restrict__ sizes, uint32_t n,
+                                                       uint64_t* __restrict__ offs) {
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t b = tid * per, e = b + per < n ? b + per : n;
+    uint64_t s = 0;
+    for (uint32_t i = b; i < e; i++) s += sizes[i];
+    part[tid] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[tid] - s;
+    for (uint32_t i = b; i < e; i++) { offs[i] = run; run += sizes[i]; }
+    if (tid == 1023) offs[n] = part[1023];
+}
+
+// --------------------------------------------------------------------- assemble
+// Standard CRC-32 register update, bitwise (only for the few header bytes).
+__device__ uint32_t crc_bits(uint32_t c, const uint8_t* p, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        c ^= p[i];
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ CRC_POLY : c >> 1;
+    }
+    return c;
+}
+
+__device__ uint32_t put_chunk(uint8_t* o, const char* type, const uint8_t* data, uint32_t n) {
+    put_be32(o, n);
+    for (int i = 0; i < 4; i++) o[4 + i] = (uint8_t)type[i];
+    for (uint32_t i = 0; i < n; i++) o[8 + i] = data[i];
+    const uint32_t crc = crc_bits(0xFFFFFFFFu, o + 4, 4 + n) ^ 0xFFFFFFFFu;
+    put_be32(o + 8 + n, crc);
+    return 12 + n;
+}
+
+__global__ __launch_bounds__(256) void k_assemble(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                  const SegOut* __restrict__ so,
+                                                  const uint8_t* __restrict__ slots,
+                                                  uint32_t slot_stride,
+                                                  const uint64_t* __restrict__ offs,
+                                                  uint8_t* __restrict__ out) {
+    const uint32_t i = xcd_remap(blockIdx.x, gridDim.x), tid = threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc d = dt[i];
+    uint8_t* base = out + offs[i];
+    const bool tiff = (d.flags & TF_TIFF) != 0;
+    const uint32_t zoff = tiff ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+    uint64_t pos = zoff + ZLIB_HDR_BYTES;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        const uint32_t n = so[d.seg_first + k].nbytes;
+        const uint8_t* src = slots + (size_t)(d.seg_first + k) * slot_stride;
+        uint8_t* dst = base + pos;
+        for (uint32_t j = tid; j < n; j += 256) dst[j] = src[j];
+        pos += n;
+    }
+    if (tid != 0) return;
+    const uint64_t payload = pos - zoff - ZLIB_HDR_BYTES;
+    uint32_t s1 = 0, s2 = 0;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        const SegOut& g = so[d.seg_first + k];
+        adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.len);
+    }
+    const uint32_t adler = adler_final(s1, s2, d.stream_len);
+    base[zoff] = 0x78;      // CMF: deflate, 32 KiB window
+    base[zoff + 1] = 0x9C;  // FLG: default level (Deflater -1 == 6), check bits
+    put_be32(base + pos, adler);
+    if (tiff) {
+        write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8,
+                          (uint32_t)(ZLIB_HDR_BYTES + payload + 4));
+        return;
+    }
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+    for (int j = 0; j < 8; j++) base[j] = sig[j];
+    uint32_t o = 8;
+    uint8_t buf[26];
+    put_be32(buf, d.w); put_be32(buf + 4, d.h);
+    buf[8] = (uint8_t)(8 * d.bpp); buf[9] = 0; buf[10] = 0; buf[11] = 0; buf[12] = 0;
+    o += put_chunk(base + o, "IHDR", buf, 13);
+    put_be32(buf, 1); put_be32(buf + 4, 0);  // acTL: 1 frame, 0 plays
+    o += put_chunk(base + o, "acTL", buf, 8);
+    for (int j = 0; j < 26; j++) buf[j] = 0;  // fcTL: seq 0, w, h, offsets 0, delay 0/0, ops 0
+    put_be32(buf + 4, d.w); put_be32(buf + 8, d.h);
+    o += put_chunk(base + o, "fcTL", buf, 26);
+    // IDAT: length, type, zlib stream; CRC over type + data combined from segment CRCs
+    put_be32(base + o, (uint32_t)(ZLIB_HDR_BYTES + payload + 4));
+    base[o + 4] = 'I'; base[o + 5] = 'D'; base[o + 6] = 'A'; base[o + 7] = 'T';
+    uint32_t c = crc_bits(0xFFFFFFFFu, base + o + 4, 4 + ZLIB_HDR_BYTES) ^ 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        const SegOut& g = so[d.seg_first + k];
+        c = crc_combine_op(c, g.crc, g.crc_op);
+    }
+    c = crc_bits(c ^ 0xFFFFFFFFu, base + pos, 4) ^ 0xFFFFFFFFu;
+    put_be32(base + pos + 4, c);
+    put_chunk(base + pos + 8, "IEND", nullptr, 0);
+}
+
+// ------------------------------------------------------------------------ launchers
+uint32_t deflate_slot_stride() { return (uint32_t)((DC::SEG + 64 + 255) & ~255); }
+uint32_t deflate_threads() { return DC::NT; }
+size_t deflate_lds_bytes() { return sizeof(DeflateSmem<DC>); }
+
+hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t sy,
+                            int32_t pt, int32_t kind, uint64_t seed, int32_t plane_no, int32_t z,
+                            int32_t c, int32_t t) {
+    static const int bpps[PT_N] = {1, 1, 2, 2, 4, 4, 4, 8};
+    const uint64_t total = (uint64_t)sx * (uint64_t)sy;
+    uint64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_plane, dim3((uint32_t)blocks), dim3(256), 0, st, out, pitch, sx, sy, pt,
+                       bpps[pt], kind, seed, plane_no, z, c, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                          uint32_t nblocks, uint8_t* out) {
+    if (!ntiles || !nblocks) return hipSuccess;
+    hipLaunchKernelGGL(k_extract, dim3(nblocks), dim3(256), 0, st, d_tiles, ntiles, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowfilter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                            uint32_t nrows, uint8_t* rowfilt) {
+    if (!ntiles || !nrows) return hipSuccess;
+    hipLaunchKernelGGL(k_rowfilter, dim3((nrows + 3) / 4), dim3(256), 0, st, d_tiles, ntiles, nrows,
+                       rowfilt);
+    return hipGetLastError();
+}
+
+hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nseg,
+                          const uint8_t* rowfilt, uint8_t* slots, uint32_t slot_stride,
+                          SegOut* segout) {
+    if (!ntiles || !nseg) return hipSuccess;
+    hipLaunchKernelGGL(k_deflate<DC>, dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles, nseg, rowfilt,
+                       slots, slot_stride, segout);
+    return hipGetLastError();
+}
+
+hipError_t launch_sizes_scan(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                             const SegOut* segout, uint64_t* sizes, uint64_t* offsets) {
+    if (!ntiles) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_sizes, dim3((ntiles + 255) / 256), dim3(256), 0, st, d_tiles, ntiles,
+                       segout, sizes);
+    hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, sizes, ntiles, offsets);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                           const SegOut* segout, const uint8_t* slots, uint32_t slot_stride,
+                           const uint64_t* offsets, uint8_t* out) {
+    if (!ntiles) return hipSuccess;
+    hipLaunchKernelGGL(k_assemble, dim3(ntiles), dim3(256), 0, st, d_tiles, ntiles, segout, slots,
+                       slot_stride, offsets, out);
+    return hipGetLastError();
+}
+
+}  // namespace pbx

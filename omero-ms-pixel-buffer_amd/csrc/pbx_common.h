@@ -77,6 +77,36 @@ struct SegOut {
 
 PBX_HD uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
+PBX_HD void put_be32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+PBX_HD void put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+// TIFF SampleFormat: 1 unsigned, 2 signed, 3 IEEE float.
+PBX_HD uint32_t tiff_sample_format(int32_t pt) {
+    return (pt == PT_FLOAT || pt == PT_DOUBLE) ? 3u
+           : (pt == PT_INT8 || pt == PT_INT16 || pt == PT_INT32) ? 2u : 1u;
+}
+
+// Classic big-endian ("MM") TIFF header + 11-entry IFD; one strip of nbytes at
+// TIFF_DATA_OFFSET (TiffWriter with PixelsBigEndian=true, TileRequestHandler.java:155,182-186).
+// Writes exactly TIFF_DATA_OFFSET bytes.
+PBX_HD void write_tiff_header(uint8_t* p, uint32_t w, uint32_t h, uint32_t bpp, uint32_t sf,
+                              uint32_t compression, uint32_t nbytes) {
+    for (uint32_t i = 0; i < TIFF_DATA_OFFSET; i++) p[i] = 0;
+    p[0] = 'M'; p[1] = 'M'; put_be16(p + 2, 42); put_be32(p + 4, 8);
+    put_be16(p + 8, TIFF_NTAGS);
+    const uint16_t tag[TIFF_NTAGS] = {256, 257, 258, 259, 262, 273, 277, 278, 279, 284, 339};
+    const uint16_t typ[TIFF_NTAGS] = {4, 4, 3, 3, 3, 4, 3, 4, 4, 3, 3};
+    const uint32_t val[TIFF_NTAGS] = {w, h, 8 * bpp, compression, 1, TIFF_DATA_OFFSET, 1, h, nbytes, 1, sf};
+    for (uint32_t k = 0; k < TIFF_NTAGS; k++) {
+        uint8_t* e = p + 10 + 12 * k;
+        put_be16(e, tag[k]); put_be16(e + 2, typ[k]); put_be32(e + 4, 1);
+        if (typ[k] == 3) { put_be16(e + 8, val[k]); } else { put_be32(e + 8, val[k]); }
+    }
+    // next-IFD offset (0) is already zero
+}
+
 // ----------------------------------------------------------------------------- CRC-32 math
 // Standard reflected CRC-32 (poly 0xEDB88320) with zlib's crc32_combine formulation:
 // crc(A||B) = multmodp(x^(8|B|), crc(A)) ^ crc(B).

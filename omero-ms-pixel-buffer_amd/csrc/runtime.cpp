@@ -1,0 +1,719 @@
+// runtime.cpp — host runtime behind include/pbx.h: device context, plane registry (the
+// PixelsService / getPixels stand-in), request validation that mirrors
+// TileRequestHandler.getTile, batch planning, kernel launches and result ownership.
+//
+// Paths below are relative to /root/reference/src/main/java/com/glencoesoftware/omero/ms/pixelbuffer/.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pbx.h"
+#include "pbx_common.h"
+#include "pbx_config.h"
+#include "pbx_kernels.h"
+
+using namespace pbx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(PBX_E_INTERNAL, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                            \
+    } while (0)
+
+const int kBpp[PBX_NPIXEL_TYPES] = {1, 1, 2, 2, 4, 4, 4, 8};
+
+int bpp_of(int32_t pt) { return (pt >= 0 && pt < PBX_NPIXEL_TYPES) ? kBpp[pt] : 0; }
+int log2i(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
+
+struct Plane {
+    uint64_t id = 0;
+    int64_t image_id = 0;
+    int32_t z = 0, c = 0, t = 0, res = 0, pixel_type = 0, size_x = 0, size_y = 0;
+    bool little_endian = false;
+    uint8_t* dev = nullptr;
+    int64_t pitch = 0;
+    size_t bytes = 0;
+};
+
+struct Image {
+    int32_t pixel_type = 0, size_x = 0, size_y = 0;
+    int32_t planes = 0;
+};
+
+// Grow-only caching allocator for device and pinned host blocks (power-of-two classes).
+struct Pool {
+    bool pinned = false;
+    std::mutex mu;
+    std::multimap<size_t, void*> free_blocks;
+    std::unordered_map<void*, size_t> sizes;
+
+    static size_t cls(size_t n) {
+        size_t c = 1 << 20;
+        while (c < n) c <<= 1;
+        return c;
+    }
+    void* get(size_t n, hipError_t* err) {
+        const size_t c = cls(n);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = free_blocks.find(c);
+            if (it != free_blocks.end()) {
+                void* p = it->second;
+                free_blocks.erase(it);
+                return p;
+            }
+        }
+        void* p = nullptr;
+        *err = pinned ? hipHostMalloc(&p, c, hipHostMallocDefault) : hipMalloc(&p, c);
+        if (*err != hipSuccess) {
+            // drop cached blocks and retry once
+            trim();
+            *err = pinned ? hipHostMalloc(&p, c, hipHostMallocDefault) : hipMalloc(&p, c);
+            if (*err != hipSuccess) return nullptr;
+        }
+        std::lock_guard<std::mutex> g(mu);
+        sizes[p] = c;
+        return p;
+    }
+    void put(void* p) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        free_blocks.emplace(sizes[p], p);
+    }
+    void trim() {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto& kv : free_blocks) {
+            if (pinned) (void)hipHostFree(kv.second); else (void)hipFree(kv.second);
+            sizes.erase(kv.second);
+        }
+        free_blocks.clear();
+    }
+    void release_all() {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto& kv : sizes) {
+            if (pinned) (void)hipHostFree(kv.first); else (void)hipFree(kv.first);
+        }
+        sizes.clear();
+        free_blocks.clear();
+    }
+};
+
+}  // namespace
+
+struct pbx_ctx {
+    int device = 0;
+    pbx_config cfg{};
+    hipStream_t stream = nullptr;
+    std::mutex reg_mu;  // plane registry
+    std::mutex run_mu;  // one batch on the stream at a time
+    std::unordered_map<uint64_t, Plane> planes;
+    std::map<std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>, uint64_t> index;
+    std::unordered_map<int64_t, Image> images;
+    uint64_t next_id = 1;
+    Pool dpool, hpool;
+};
+
+namespace {
+
+// Host-side result storage shared by the results of one batch fetch.
+struct HostBlock {
+    std::atomic<int> refs{0};
+    pbx_ctx* ctx = nullptr;
+    void* pinned = nullptr;
+};
+
+}  // namespace
+
+struct pbx_batch {
+    std::vector<pbx_tile_req> reqs;
+    std::vector<int32_t> status, w, h;
+    std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
+    std::vector<uint32_t> ft_req, dt_req;  // request index of each
+    uint32_t ext_blocks = 0, nseg = 0, nrows_filter = 0;
+    uint64_t fixed_bytes = 0, rowfilt_bytes = 0, png_cap = 0;
+    uint64_t in_bytes = 0, stream_bytes = 0;
+    // device buffers (pool blocks)
+    void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_rowfilt = nullptr,
+         *d_slots = nullptr, *d_segout = nullptr, *d_sizes = nullptr, *d_offs = nullptr,
+         *d_png = nullptr;
+    void* h_desc = nullptr;  // pinned staging for descriptors
+    hipEvent_t ev[6] = {};
+    bool launched = false;
+    std::vector<uint64_t> h_offs;
+};
+
+namespace {
+
+int ensure_device(pbx_ctx* ctx) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    return PBX_OK;
+}
+
+// Mirrors TileRequestHandler.getTile (TileRequestHandler.java:80-139) up to the dispatch:
+// returns PBX_OK and the plane, or the status the reference ends with.
+int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane& plane) {
+    w = r.w;
+    h = r.h;
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto im = ctx->images.find(r.image_id);
+    if (im == ctx->images.end()) return fail(PBX_E_NOTFOUND, "Cannot find Image:%lld", (long long)r.image_id);
+    // :92-97 — defaults come from the full-resolution Pixels sizes even with `resolution`
+    if (w == 0) w = im->second.size_x;
+    if (h == 0) h = im->second.size_y;
+    const int bpp = bpp_of(im->second.pixel_type);
+    // :100-103 — int tileSize = w*h*bpp; overflow / negative size -> exception -> null -> 404
+    const int64_t tile_size = (int64_t)w * (int64_t)h * bpp;
+    if (w < 0 || h < 0 || tile_size > 2147483647LL || tile_size <= 0)
+        return fail(PBX_E_NOTFOUND, "invalid tile size %dx%d", w, h);
+    const int32_t res = r.resolution < 0 ? 0 : r.resolution;
+    auto it = ctx->index.find(std::make_tuple(r.image_id, r.z, r.c, r.t, res));
+    if (it == ctx->index.end())
+        return fail(PBX_E_NOTFOUND, "no plane z=%d c=%d t=%d resolution=%d", r.z, r.c, r.t, res);
+    plane = ctx->planes[it->second];
+    // getTileDirect outside the plane throws (upstream PixelBuffer) -> 404
+    if (r.x < 0 || r.y < 0 || (int64_t)r.x + w > plane.size_x || (int64_t)r.y + h > plane.size_y)
+        return fail(PBX_E_NOTFOUND, "region outside plane");
+    switch (r.format) {
+    case PBX_FMT_RAW:
+    case PBX_FMT_TIF:
+        return PBX_OK;
+    case PBX_FMT_PNG:
+        // APNGWriter accepts int8/uint8/int16/uint16 only ("Unsupported image type")
+        if (bpp > 2) return fail(PBX_E_NOTFOUND, "png: unsupported pixel type");
+        return PBX_OK;
+    default:
+        return fail(PBX_E_NOTFOUND, "Unknown output format");  // :125-126
+    }
+}
+
+void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
+    void** bufs[] = {&b->d_ft, &b->d_dt, &b->d_fixed, &b->d_rowfilt, &b->d_slots,
+                     &b->d_segout, &b->d_sizes, &b->d_offs, &b->d_png};
+    for (void** p : bufs) {
+        ctx->dpool.put(*p);
+        *p = nullptr;
+    }
+    if (b->h_desc) ctx->hpool.put(b->h_desc);
+    b->h_desc = nullptr;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+
+extern "C" {
+
+const char* pbx_last_error(void) { return g_err.c_str(); }
+int pbx_abi_version(void) { return PBX_ABI_VERSION; }
+
+int pbx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int pbx_bytes_per_pixel(int32_t pt) { return bpp_of(pt); }
+
+int pbx_format_from_string(const char* f) {
+    if (!f) return PBX_FMT_RAW;
+    if (!strcmp(f, "png")) return PBX_FMT_PNG;
+    if (!strcmp(f, "tif")) return PBX_FMT_TIF;
+    return PBX_FMT_UNKNOWN;
+}
+
+int pbx_pixel_type_from_string(const char* n) {
+    static const char* names[PBX_NPIXEL_TYPES] = {"int8", "uint8", "int16", "uint16",
+                                                  "int32", "uint32", "float", "double"};
+    if (!n) return -1;
+    for (int i = 0; i < PBX_NPIXEL_TYPES; i++)
+        if (!strcmp(n, names[i])) return i;
+    return -1;
+}
+
+int pbx_tile_filename(const pbx_tile_req* r, int32_t w, int32_t h, const char* fmt, char* out,
+                      uint64_t cap) {
+    if (!r || !out) return fail(PBX_E_BADARG, "null argument");
+    return snprintf(out, cap, "image%lld_z%d_c%d_t%d_x%d_y%d_w%d_h%d.%s", (long long)r->image_id,
+                    r->z, r->c, r->t, r->x, r->y, w, h, fmt ? fmt : "bin");
+}
+
+const char* pbx_content_type(const char* f) {
+    if (f && !strcmp(f, "png")) return "image/png";
+    if (f && !strcmp(f, "tif")) return "image/tiff";
+    return "application/octet-stream";
+}
+
+int pbx_config_default(pbx_config* cfg) {
+    if (!cfg) return fail(PBX_E_BADARG, "null config");
+    memset(cfg, 0, sizeof *cfg);
+    cfg->device = -1;
+    cfg->png_filter = PBX_FILTER_NONE;
+    const char* f = getenv("PBX_PNG_FILTER");
+    if (f) cfg->png_filter = atoi(f);
+    const char* td = getenv("PBX_TIFF_DEFLATE");
+    if (td) cfg->tiff_deflate = atoi(td);
+    return PBX_OK;
+}
+
+int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
+    if (!out) return fail(PBX_E_BADARG, "null out");
+    *out = nullptr;
+    pbx_config cfg;
+    if (cfg_in) cfg = *cfg_in; else pbx_config_default(&cfg);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(PBX_E_INTERNAL, "no HIP device available (the tile pipeline runs on MI355X only)");
+    int dev = cfg.device;
+    if (dev < 0) {
+        const char* e = getenv("PBX_DEVICE");
+        const char* lr = getenv("LOCAL_RANK");
+        dev = e ? atoi(e) : lr ? atoi(lr) : 0;
+    }
+    if (dev < 0 || dev >= n) return fail(PBX_E_BADARG, "device %d out of range (%d devices)", dev, n);
+    if (cfg.png_filter < PBX_FILTER_NONE || cfg.png_filter > PBX_FILTER_ADAPTIVE)
+        return fail(PBX_E_BADARG, "bad png_filter %d", cfg.png_filter);
+    pbx_ctx* ctx = new pbx_ctx();
+    ctx->device = dev;
+    ctx->cfg = cfg;
+    ctx->hpool.pinned = true;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(PBX_E_INTERNAL, "init: %s", hipGetErrorString(e));
+    }
+    *out = ctx;
+    return PBX_OK;
+}
+
+void pbx_shutdown(pbx_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->planes) (void)hipFree(kv.second.dev);
+    ctx->dpool.release_all();
+    ctx->hpool.release_all();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int pbx_device_synchronize(pbx_ctx* ctx) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipDeviceSynchronize());
+    return PBX_OK;
+}
+
+int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id) {
+    if (!ctx || !d || !plane_id) return fail(PBX_E_BADARG, "null argument");
+    const int bpp = bpp_of(d->pixel_type);
+    if (!bpp) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
+    if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
+    if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    Plane p;
+    p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
+    p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
+    const int64_t row = (int64_t)d->size_x * bpp;
+    p.pitch = (row + 255) & ~(int64_t)255;
+    p.bytes = (size_t)p.pitch * d->size_y + 256;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
+        if (ctx->index.count(key)) return fail(PBX_E_BADARG, "plane already registered");
+        auto im = ctx->images.find(d->image_id);
+        if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
+            return fail(PBX_E_BADARG, "pixel type differs from the image's");
+        if (d->resolution == 0 && im != ctx->images.end() &&
+            (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
+            return fail(PBX_E_BADARG, "plane size differs from the image's");
+    }
+    HIP_TRY(hipMalloc((void**)&p.dev, p.bytes));
+    if (d->source == PBX_SRC_HOST) {
+        if (!d->host_data || d->host_bytes < (uint64_t)row * d->size_y) {
+            (void)hipFree(p.dev);
+            return fail(PBX_E_BADARG, "host_data too small");
+        }
+        p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
+        HIP_TRY(hipMemcpy2DAsync(p.dev, p.pitch, d->host_data, row, row, d->size_y,
+                                 hipMemcpyHostToDevice, ctx->stream));
+    } else if (d->source == PBX_SRC_GEN_FAKE || d->source == PBX_SRC_GEN_NOISE) {
+        p.little_endian = bpp > 1;
+        HIP_TRY(launch_gen_plane(ctx->stream, p.dev, p.pitch, d->size_x, d->size_y, d->pixel_type,
+                                 d->source == PBX_SRC_GEN_FAKE ? GEN_FAKE : GEN_NOISE, d->seed,
+                                 d->plane_no, d->z, d->c, d->t));
+    } else {
+        (void)hipFree(p.dev);
+        return fail(PBX_E_BADARG, "bad source %d", d->source);
+    }
+    HIP_TRY(hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    p.id = ctx->next_id++;
+    ctx->planes[p.id] = p;
+    ctx->index[std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution)] = p.id;
+    Image& im = ctx->images[d->image_id];
+    if (d->resolution == 0 || im.planes == 0) {  // the Pixels row: full-resolution sizes
+        im.pixel_type = d->pixel_type;
+        im.size_x = d->size_x;
+        im.size_y = d->size_y;
+    }
+    im.planes++;
+    *plane_id = p.id;
+    return PBX_OK;
+}
+
+int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::lock_guard<std::mutex> run(ctx->run_mu);
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->planes.find(id);
+    if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+    Plane p = it->second;
+    ctx->planes.erase(it);
+    ctx->index.erase(std::make_tuple(p.image_id, p.z, p.c, p.t, p.res));
+    auto im = ctx->images.find(p.image_id);
+    if (im != ctx->images.end() && --im->second.planes == 0) ctx->images.erase(im);
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    HIP_TRY(hipFree(p.dev));
+    return PBX_OK;
+}
+
+int pbx_plane_read_be(pbx_ctx* ctx, uint64_t id, void* out, uint64_t bytes) {
+    if (!ctx || !out) return fail(PBX_E_BADARG, "null argument");
+    Plane p;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto it = ctx->planes.find(id);
+        if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane");
+        p = it->second;
+    }
+    const int bpp = bpp_of(p.pixel_type);
+    const int64_t row = (int64_t)p.size_x * bpp;
+    if (bytes < (uint64_t)row * p.size_y) return fail(PBX_E_BADARG, "buffer too small");
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipMemcpy2D(out, row, p.dev, p.pitch, row, p.size_y, hipMemcpyDeviceToHost));
+    if (p.little_endian) {
+        uint8_t* b = (uint8_t*)out;
+        for (int64_t i = 0; i < row * p.size_y; i += bpp) std::reverse(b + i, b + i + bpp);
+    }
+    return PBX_OK;
+}
+
+int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch** out) {
+    if (!ctx || !out || (!reqs && n)) return fail(PBX_E_BADARG, "null argument");
+    if (n > (1u << 26)) return fail(PBX_E_BADARG, "batch too large");
+    pbx_batch* b = new pbx_batch();
+    b->reqs.assign(reqs, reqs + n);
+    b->status.resize(n);
+    b->w.resize(n);
+    b->h.resize(n);
+    const int filter = ctx->cfg.png_filter;
+    const bool tiff_deflate = ctx->cfg.tiff_deflate != 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const pbx_tile_req& r = reqs[i];
+        Plane pl;
+        int32_t w = 0, h = 0;
+        const int st = validate(ctx, r, w, h, pl);
+        b->status[i] = st;
+        b->w[i] = w;
+        b->h[i] = h;
+        if (st != PBX_OK) continue;
+        const int bpp = bpp_of(pl.pixel_type);
+        TileDesc d;
+        memset(&d, 0, sizeof d);
+        d.plane = pl.dev;
+        d.pitch = pl.pitch;
+        d.x = r.x; d.y = r.y; d.w = w; d.h = h;
+        d.bpp = bpp; d.lbpp = log2i(bpp);
+        d.pixel_type = pl.pixel_type;
+        d.flags = pl.little_endian ? TF_SWAP : 0u;
+        const uint64_t tile_bytes = (uint64_t)w * h * bpp;
+        b->in_bytes += tile_bytes;
+        const bool deflate = r.format == PBX_FMT_PNG || (r.format == PBX_FMT_TIF && tiff_deflate);
+        if (!deflate) {
+            if (r.format == PBX_FMT_TIF) d.flags |= TF_TIFF;
+            const uint32_t rb = (uint32_t)w * bpp;
+            d.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(16384 / std::max<uint32_t>(rb, 1)));
+            const uint32_t blks = (uint32_t)((h + d.rows_per_blk - 1) / d.rows_per_blk);
+            d.blk_first = b->ext_blocks;
+            b->ext_blocks += blks;
+            d.out_off = b->fixed_bytes;
+            b->fixed_bytes += ((r.format == PBX_FMT_TIF ? TIFF_DATA_OFFSET : 0) + tile_bytes + 255) & ~255ull;
+            b->ft.push_back(d);
+            b->ft_req.push_back((uint32_t)i);
+        } else {
+            if (r.format == PBX_FMT_PNG) {
+                d.flags |= TF_PNGROWS;
+                if (pl.pixel_type == PBX_INT8 || pl.pixel_type == PBX_INT16) d.flags |= TF_FLIP;
+                d.filter = filter;
+                d.rowlen = 1 + (uint32_t)w * bpp;
+            } else {
+                d.flags |= TF_TIFF;
+                d.filter = 0;
+                d.rowlen = (uint32_t)w * bpp;
+            }
+            d.stream_len = (uint64_t)h * d.rowlen;
+            d.seg_count = deflate_nsegs(d.stream_len);
+            d.seg_len = deflate_seg_len(d.stream_len, d.seg_count);
+            d.seg_first = b->nseg;
+            b->nseg += d.seg_count;
+            if (d.filter == PBX_FILTER_ADAPTIVE && (d.flags & TF_PNGROWS)) {
+                d.rowfilt_off = (uint32_t)b->rowfilt_bytes;
+                b->rowfilt_bytes += (uint64_t)h;
+                d.blk_first = b->nrows_filter;
+                b->nrows_filter += (uint32_t)h;
+            } else {
+                d.blk_first = b->nrows_filter;
+            }
+            b->stream_bytes += d.stream_len;
+            b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
+            b->dt.push_back(d);
+            b->dt_req.push_back((uint32_t)i);
+        }
+    }
+    *out = b;
+    return PBX_OK;
+}
+
+int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
+    if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    hipError_t err = hipSuccess;
+    auto dget = [&](void*& p, size_t n) -> bool {
+        if (p) return true;
+        p = ctx->dpool.get(std::max<size_t>(n, 256), &err);
+        return p != nullptr;
+    };
+    const uint32_t nft = (uint32_t)b->ft.size(), ndt = (uint32_t)b->dt.size();
+    const size_t ft_bytes = nft * sizeof(TileDesc), dt_bytes = ndt * sizeof(TileDesc);
+    if (!b->h_desc) {
+        b->h_desc = ctx->hpool.get(ft_bytes + dt_bytes + 256, &err);
+        if (!b->h_desc) return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
+        if (nft) memcpy(b->h_desc, b->ft.data(), ft_bytes);
+        if (ndt) memcpy((uint8_t*)b->h_desc + ft_bytes, b->dt.data(), dt_bytes);
+    }
+    const uint32_t slot = deflate_slot_stride();
+    if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
+        !dget(b->d_rowfilt, b->rowfilt_bytes) || !dget(b->d_slots, (size_t)b->nseg * slot) ||
+        !dget(b->d_segout, (size_t)b->nseg * sizeof(SegOut)) ||
+        !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
+        !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap))
+        return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
+    if (!b->ev[0])
+        for (auto& e : b->ev) HIP_TRY(hipEventCreate(&e));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipEventRecord(b->ev[0], st));
+    if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
+    if (ndt)
+        HIP_TRY(hipMemcpyAsync(b->d_dt, (uint8_t*)b->h_desc + ft_bytes, dt_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(b->ev[1], st));
+    HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
+    HIP_TRY(hipEventRecord(b->ev[2], st));
+    HIP_TRY(launch_rowfilter(st, (const TileDesc*)b->d_dt, ndt, b->nrows_filter, (uint8_t*)b->d_rowfilt));
+    HIP_TRY(hipEventRecord(b->ev[3], st));
+    HIP_TRY(launch_deflate(st, (const TileDesc*)b->d_dt, ndt, b->nseg, (const uint8_t*)b->d_rowfilt,
+                           (uint8_t*)b->d_slots, slot, (SegOut*)b->d_segout));
+    HIP_TRY(hipEventRecord(b->ev[4], st));
+    HIP_TRY(launch_sizes_scan(st, (const TileDesc*)b->d_dt, ndt, (const SegOut*)b->d_segout,
+                              (uint64_t*)b->d_sizes, (uint64_t*)b->d_offs));
+    HIP_TRY(launch_assemble(st, (const TileDesc*)b->d_dt, ndt, (const SegOut*)b->d_segout,
+                            (const uint8_t*)b->d_slots, slot, (const uint64_t*)b->d_offs,
+                            (uint8_t*)b->d_png));
+    HIP_TRY(hipEventRecord(b->ev[5], st));
+    b->launched = true;
+    return PBX_OK;
+}
+
+int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
+    if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return PBX_OK;
+}
+
+int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
+    if (!ctx || !b || !s) return fail(PBX_E_BADARG, "null argument");
+    memset(s, 0, sizeof *s);
+    s->tiles = b->reqs.size();
+    for (size_t i = 0; i < b->reqs.size(); i++) {
+        if (b->status[i] != PBX_OK) continue;
+        s->ok_tiles++;
+        if (b->reqs[i].format == PBX_FMT_PNG) s->png_tiles++;
+        else if (b->reqs[i].format == PBX_FMT_TIF) s->tif_tiles++;
+        else s->raw_tiles++;
+    }
+    s->in_bytes = b->in_bytes;
+    s->stream_bytes = b->stream_bytes;
+    s->segments = b->nseg;
+    if (b->launched) {
+        if (ensure_device(ctx)) return PBX_E_INTERNAL;
+        HIP_TRY(hipEventSynchronize(b->ev[5]));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); s->ms_extract = ms;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev[2], b->ev[3])); s->ms_filter = ms;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev[3], b->ev[4])); s->ms_deflate = ms;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev[4], b->ev[5])); s->ms_assemble = ms;
+        HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[5])); s->ms_total = ms;
+        const uint32_t ndt = (uint32_t)b->dt.size();
+        if (ndt) {
+            std::vector<uint64_t> offs(ndt + 1);
+            HIP_TRY(hipMemcpy(offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            s->deflate_out_bytes = offs[ndt];
+        }
+        s->out_bytes = s->deflate_out_bytes;
+        for (size_t k = 0; k < b->ft.size(); k++)
+            s->out_bytes += (uint64_t)b->ft[k].w * b->ft[k].h * b->ft[k].bpp +
+                            ((b->ft[k].flags & TF_TIFF) ? TIFF_DATA_OFFSET : 0);
+    }
+    return PBX_OK;
+}
+
+int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
+    if (!ctx || !b || !out) return fail(PBX_E_BADARG, "null argument");
+    const size_t n = b->reqs.size();
+    for (size_t i = 0; i < n; i++) {
+        out[i].status = b->status[i];
+        out[i].format = b->reqs[i].format;
+        out[i].w = b->w[i];
+        out[i].h = b->h[i];
+        out[i].data = nullptr;
+        out[i].len = 0;
+        out[i].owner = nullptr;
+    }
+    if (!b->launched) return PBX_OK;
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const uint32_t ndt = (uint32_t)b->dt.size();
+    b->h_offs.assign(ndt + 1, 0);
+    if (ndt)
+        HIP_TRY(hipMemcpy(b->h_offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    const uint64_t png_total = ndt ? b->h_offs[ndt] : 0;
+    hipError_t err = hipSuccess;
+    HostBlock* hb = new HostBlock();
+    hb->ctx = ctx;
+    hb->pinned = ctx->hpool.get(b->fixed_bytes + png_total + 256, &err);
+    if (!hb->pinned) {
+        delete hb;
+        return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
+    }
+    uint8_t* h = (uint8_t*)hb->pinned;
+    if (b->fixed_bytes)
+        HIP_TRY(hipMemcpyAsync(h, b->d_fixed, b->fixed_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (png_total)
+        HIP_TRY(hipMemcpyAsync(h + b->fixed_bytes, b->d_png, png_total, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int refs = 0;
+    for (size_t k = 0; k < b->ft.size(); k++) {
+        const TileDesc& d = b->ft[k];
+        pbx_result& r = out[b->ft_req[k]];
+        r.data = h + d.out_off;
+        r.len = (uint64_t)d.w * d.h * d.bpp + ((d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : 0);
+        r.owner = hb;
+        refs++;
+    }
+    for (uint32_t k = 0; k < ndt; k++) {
+        pbx_result& r = out[b->dt_req[k]];
+        r.data = h + b->fixed_bytes + b->h_offs[k];
+        r.len = b->h_offs[k + 1] - b->h_offs[k];
+        r.owner = hb;
+        refs++;
+    }
+    if (refs == 0) {
+        ctx->hpool.put(hb->pinned);
+        delete hb;
+    } else {
+        hb->refs.store(refs);
+    }
+    return PBX_OK;
+}
+
+void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
+    if (!ctx || !b) return;
+    (void)hipSetDevice(ctx->device);
+    if (b->launched) (void)hipStreamSynchronize(ctx->stream);
+    free_batch_device(ctx, b);
+    for (auto& e : b->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete b;
+}
+
+void pbx_results_release(pbx_ctx* ctx, pbx_result* res, uint64_t n) {
+    if (!res) return;
+    for (uint64_t i = 0; i < n; i++) {
+        HostBlock* hb = (HostBlock*)res[i].owner;
+        res[i].owner = nullptr;
+        res[i].data = nullptr;
+        if (!hb) continue;
+        if (hb->refs.fetch_sub(1) == 1) {
+            (ctx ? ctx : hb->ctx)->hpool.put(hb->pinned);
+            delete hb;
+        }
+    }
+}
+
+int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out) {
+    if (!ctx || !out || (!reqs && n)) return fail(PBX_E_BADARG, "null argument");
+    std::lock_guard<std::mutex> run(ctx->run_mu);
+    pbx_batch* b = nullptr;
+    int st = pbx_batch_plan(ctx, reqs, n, &b);
+    if (st) return st;
+    st = pbx_batch_launch(ctx, b);
+    if (st == PBX_OK) st = pbx_batch_fetch(ctx, b, out);
+    if (st != PBX_OK) {
+        // a device failure fails every request of the batch with 500 (PixelBufferVerticle.java:141-146)
+        const std::string msg = g_err;
+        for (uint64_t i = 0; i < n; i++) {
+            out[i].status = b->status[i] == PBX_OK ? PBX_E_INTERNAL : b->status[i];
+            out[i].format = reqs[i].format;
+            out[i].w = b->w[i];
+            out[i].h = b->h[i];
+            out[i].data = nullptr;
+            out[i].len = 0;
+            out[i].owner = nullptr;
+        }
+        (void)hipStreamSynchronize(ctx->stream);
+        pbx_batch_destroy(ctx, b);
+        g_err = msg;
+        return st;
+    }
+    pbx_batch_destroy(ctx, b);
+    return PBX_OK;
+}
+
+int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
+    if (!req) return fail(PBX_E_BADARG, "null request");
+    const int st = pbx_get_tiles(ctx, req, 1, out);
+    if (st) return st;
+    return out->status;
+}
+
+}  // extern "C"

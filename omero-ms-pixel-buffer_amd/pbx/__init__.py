@@ -1,0 +1,417 @@
+"""pbx — Python host side of the MI355X /tile pipeline, mirroring the reference's interface.
+
+The reference (glencoesoftware/omero-ms-pixel-buffer, Java) exposes the hot path as
+``TileRequestHandler(pixelsService, tileCtx).getTile(client) -> byte[] | null``
+(src/main/java/com/glencoesoftware/omero/ms/pixelbuffer/TileRequestHandler.java:74-139),
+with the request parsed into a ``TileCtx`` (TileCtx.java:30-92) and replies built by
+``PixelBufferVerticle.getTile`` (PixelBufferVerticle.java:90-147).  This module keeps the
+same names, argument meanings and error behaviour:
+
+* ``TileCtx.from_params`` raises ``ValueError`` for unparsable numbers (Java
+  ``NumberFormatException`` -> HTTP 400, PixelBufferMicroserviceVerticle.java:344-348);
+* ``TileRequestHandler.get_tile`` returns ``None`` for every failure the reference maps
+  to ``null`` (unknown image, bad region, unsupported type/format: 404);
+* ``handle_get_tile`` reproduces the event-bus consumer: status, body and the
+  ``filename`` header.
+
+All compute runs in ``lib/libpbx.so`` (hand-written HIP kernels for gfx950) through the
+plain C-ABI in include/pbx.h.  There is no CPU fallback: loading fails loudly if the
+library is missing, and ``PixelsService`` raises if no HIP device is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from typing import Iterable, List, Mapping, Optional, Sequence, Tuple
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
+
+# enum pbx_status — the HTTP status the reference ends with
+OK, E_BADARG, E_NOTFOUND, E_INTERNAL = 0, 400, 404, 500
+# enum pbx_pixel_type (OMERO PixelType names)
+PIXEL_TYPES = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "float", "double"]
+INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT, DOUBLE = range(8)
+BYTES_PER_PIXEL = [1, 1, 2, 2, 4, 4, 4, 8]
+# enum pbx_format
+FMT_RAW, FMT_PNG, FMT_TIF, FMT_UNKNOWN = range(4)
+# enum pbx_source / byte order / png filter
+SRC_HOST, SRC_GEN_FAKE, SRC_GEN_NOISE = range(3)
+BIG_ENDIAN, LITTLE_ENDIAN = 0, 1
+FILTER_NONE, FILTER_SUB, FILTER_UP, FILTER_AVG, FILTER_PAETH, FILTER_ADAPTIVE = range(6)
+
+
+class PbxConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("png_filter", ctypes.c_int32),
+                ("tiff_deflate", ctypes.c_int32), ("segment_bytes", ctypes.c_int32),
+                ("max_batch_bytes", ctypes.c_uint64)]
+
+
+class PbxPlaneDesc(ctypes.Structure):
+    _fields_ = [("image_id", ctypes.c_int64), ("z", ctypes.c_int32), ("c", ctypes.c_int32),
+                ("t", ctypes.c_int32), ("resolution", ctypes.c_int32),
+                ("pixel_type", ctypes.c_int32), ("size_x", ctypes.c_int32),
+                ("size_y", ctypes.c_int32), ("byte_order", ctypes.c_int32),
+                ("source", ctypes.c_int32), ("host_data", ctypes.c_void_p),
+                ("host_bytes", ctypes.c_uint64), ("seed", ctypes.c_uint64),
+                ("plane_no", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class PbxTileReq(ctypes.Structure):
+    _fields_ = [("image_id", ctypes.c_int64), ("z", ctypes.c_int32), ("c", ctypes.c_int32),
+                ("t", ctypes.c_int32), ("resolution", ctypes.c_int32), ("x", ctypes.c_int32),
+                ("y", ctypes.c_int32), ("w", ctypes.c_int32), ("h", ctypes.c_int32),
+                ("format", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class PbxResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("format", ctypes.c_int32), ("w", ctypes.c_int32),
+                ("h", ctypes.c_int32), ("data", ctypes.POINTER(ctypes.c_uint8)),
+                ("len", ctypes.c_uint64), ("owner", ctypes.c_void_p)]
+
+
+class PbxBatchStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("tiles", "ok_tiles", "png_tiles", "raw_tiles", "tif_tiles", "in_bytes",
+                 "stream_bytes", "out_bytes", "deflate_out_bytes", "segments")] + \
+               [(n, ctypes.c_double) for n in
+                ("ms_extract", "ms_filter", "ms_deflate", "ms_assemble", "ms_total")]
+
+
+# Every symbol include/pbx.h declares (tests check the library exports all of them).
+EXPORTS = [
+    "pbx_config_default", "pbx_init", "pbx_shutdown", "pbx_last_error", "pbx_abi_version",
+    "pbx_device_count", "pbx_plane_register", "pbx_plane_release", "pbx_plane_read_be",
+    "pbx_get_tile", "pbx_get_tiles", "pbx_results_release", "pbx_batch_plan",
+    "pbx_batch_launch", "pbx_batch_sync", "pbx_batch_fetch", "pbx_batch_destroy",
+    "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
+    "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load lib/libpbx.so (build it with `make -C omero-ms-pixel-buffer_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"pbx: native library missing at {LIB_PATH}; run "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+    L.pbx_last_error.restype = ctypes.c_char_p
+    L.pbx_content_type.restype = ctypes.c_char_p
+    L.pbx_content_type.argtypes = [ctypes.c_char_p]
+    L.pbx_format_from_string.argtypes = [ctypes.c_char_p]
+    L.pbx_pixel_type_from_string.argtypes = [ctypes.c_char_p]
+    L.pbx_bytes_per_pixel.argtypes = [i32]
+    L.pbx_config_default.argtypes = [ctypes.POINTER(PbxConfig)]
+    L.pbx_init.argtypes = [ctypes.POINTER(PbxConfig), ctypes.POINTER(vp)]
+    L.pbx_shutdown.argtypes = [vp]
+    L.pbx_shutdown.restype = None
+    L.pbx_device_synchronize.argtypes = [vp]
+    L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
+    L.pbx_plane_release.argtypes = [vp, u64]
+    L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
+    L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
+    L.pbx_get_tiles.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(PbxResult)]
+    L.pbx_results_release.argtypes = [vp, ctypes.POINTER(PbxResult), u64]
+    L.pbx_results_release.restype = None
+    L.pbx_batch_plan.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(vp)]
+    L.pbx_batch_launch.argtypes = [vp, vp]
+    L.pbx_batch_sync.argtypes = [vp, vp]
+    L.pbx_batch_fetch.argtypes = [vp, vp, ctypes.POINTER(PbxResult)]
+    L.pbx_batch_destroy.argtypes = [vp, vp]
+    L.pbx_batch_destroy.restype = None
+    L.pbx_batch_stats_get.argtypes = [vp, vp, ctypes.POINTER(PbxBatchStats)]
+    L.pbx_tile_filename.argtypes = [ctypes.POINTER(PbxTileReq), i32, i32, ctypes.c_char_p,
+                                    ctypes.c_char_p, u64]
+    _lib = L
+    return L
+
+
+class PbxError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"pbx status {status}: {msg}")
+        self.status = status
+
+
+def _check(status: int) -> None:
+    if status != OK:
+        raise PbxError(status, lib().pbx_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    return lib().pbx_device_count()
+
+
+# ------------------------------------------------------------------------- TileCtx
+
+def _parse_int(v: str, bits: int) -> int:
+    """Java Integer.parseInt / Long.parseLong: optional sign, ASCII digits, in range."""
+    if v is None:
+        raise ValueError("null")  # parseInt(null) -> NumberFormatException
+    s = v[1:] if v[:1] in ("+", "-") else v
+    if not s or not s.isascii() or not s.isdigit():
+        raise ValueError(f'For input string: "{v}"')
+    n = int(v)
+    if not -(1 << (bits - 1)) <= n < (1 << (bits - 1)):
+        raise ValueError(f'For input string: "{v}"')
+    return n
+
+
+class TileCtx:
+    """TileCtx.java:30-92 — the request context and the event-bus JSON payload."""
+
+    def __init__(self, image_id: int, z: int, c: int, t: int, x: int = 0, y: int = 0,
+                 w: int = 0, h: int = 0, resolution: Optional[int] = None,
+                 format: Optional[str] = None, omero_session_key: Optional[str] = None):
+        self.imageId = image_id
+        self.z, self.c, self.t = z, c, t
+        self.region = {"x": x, "y": y, "width": w, "height": h}
+        self.resolution = resolution
+        self.format = format
+        self.omeroSessionKey = omero_session_key
+
+    @classmethod
+    def from_params(cls, params: Mapping[str, str], omero_session_key: Optional[str] = None):
+        """TileCtx(MultiMap, String) (TileCtx.java:67-90); ValueError == NumberFormatException."""
+        opt = lambda k: _parse_int(params[k], 32) if params.get(k) is not None else None
+        return cls(_parse_int(params.get("imageId"), 64), _parse_int(params.get("z"), 32),
+                   _parse_int(params.get("c"), 32), _parse_int(params.get("t"), 32),
+                   opt("x") or 0, opt("y") or 0, opt("w") or 0, opt("h") or 0,
+                   opt("resolution"), params.get("format"), omero_session_key)
+
+    def to_json(self) -> str:
+        return json.dumps({"omeroSessionKey": self.omeroSessionKey, "imageId": self.imageId,
+                           "z": self.z, "c": self.c, "t": self.t,
+                           "resolution": self.resolution, "region": self.region,
+                           "format": self.format})
+
+    @classmethod
+    def from_json(cls, body: str) -> "TileCtx":
+        d = json.loads(body)
+        r = d.get("region") or {}
+        for k in ("imageId", "z", "c", "t"):
+            if not isinstance(d.get(k), int):
+                raise ValueError(f"bad {k}")
+        return cls(d["imageId"], d["z"], d["c"], d["t"], r.get("x", 0), r.get("y", 0),
+                   r.get("width", 0), r.get("height", 0), d.get("resolution"),
+                   d.get("format"), d.get("omeroSessionKey"))
+
+    @property
+    def x(self): return self.region["x"]
+
+    @property
+    def y(self): return self.region["y"]
+
+    @property
+    def w(self): return self.region["width"]
+
+    @property
+    def h(self): return self.region["height"]
+
+    def to_req(self) -> PbxTileReq:
+        return PbxTileReq(self.imageId, self.z, self.c, self.t,
+                          -1 if self.resolution is None else self.resolution,
+                          self.x, self.y, self.w, self.h,
+                          lib().pbx_format_from_string(
+                              self.format.encode() if self.format is not None else None), 0)
+
+
+def tile_filename(ctx: TileCtx) -> str:
+    """PixelBufferVerticle.java:118-126 (uses the region after w/h defaulting)."""
+    buf = ctypes.create_string_buffer(512)
+    req = ctx.to_req()
+    lib().pbx_tile_filename(ctypes.byref(req), ctx.w, ctx.h,
+                            ctx.format.encode() if ctx.format is not None else None, buf, 512)
+    return buf.value.decode()
+
+
+def content_type(fmt: Optional[str]) -> str:
+    """PixelBufferMicroserviceVerticle.java:373-379."""
+    return lib().pbx_content_type(fmt.encode() if fmt is not None else None).decode()
+
+
+# --------------------------------------------------------------------- PixelsService
+
+class PixelsService:
+    """Plane registry on one MI355X (the PixelsService / getPixels stand-in).
+
+    Planes live in HBM.  ``register_plane`` takes a numpy array (any byte order) or a
+    synthetic generator ("fake" = Bio-Formats FakeReader style, "noise" = G_NOISE).
+    """
+
+    def __init__(self, device: Optional[int] = None, png_filter: int = FILTER_NONE,
+                 tiff_deflate: bool = False):
+        L = lib()
+        cfg = PbxConfig()
+        _check(L.pbx_config_default(ctypes.byref(cfg)))
+        cfg.device = -1 if device is None else device
+        cfg.png_filter = png_filter
+        cfg.tiff_deflate = 1 if tiff_deflate else 0
+        h = ctypes.c_void_p()
+        _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if self._h:
+            lib().pbx_shutdown(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def register_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int,
+                       size_x: int, size_y: int, data=None, generator: Optional[str] = None,
+                       seed: int = 0, plane_no: int = 0, resolution: int = 0,
+                       big_endian: Optional[bool] = None) -> int:
+        d = PbxPlaneDesc()
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, resolution
+        d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
+        keep = None
+        if generator is not None:
+            d.source = {"fake": SRC_GEN_FAKE, "noise": SRC_GEN_NOISE}[generator]
+            d.seed, d.plane_no = seed, plane_no
+        else:
+            import numpy as np
+            a = np.ascontiguousarray(data)
+            if big_endian is None:
+                big_endian = a.dtype.byteorder == ">" or (
+                    a.dtype.byteorder == "=" and os.sys.byteorder == "big")
+            keep = a.view(np.uint8).reshape(-1)
+            d.source = SRC_HOST
+            d.byte_order = BIG_ENDIAN if big_endian else LITTLE_ENDIAN
+            d.host_data = keep.ctypes.data
+            d.host_bytes = keep.nbytes
+        pid = ctypes.c_uint64()
+        _check(lib().pbx_plane_register(self._h, ctypes.byref(d), ctypes.byref(pid)))
+        del keep
+        return pid.value
+
+    def release_plane(self, plane_id: int) -> None:
+        _check(lib().pbx_plane_release(self._h, plane_id))
+
+    def read_plane_be(self, plane_id: int, nbytes: int) -> bytes:
+        buf = ctypes.create_string_buffer(nbytes)
+        _check(lib().pbx_plane_read_be(self._h, plane_id, buf, nbytes))
+        return buf.raw
+
+    def synchronize(self) -> None:
+        _check(lib().pbx_device_synchronize(self._h))
+
+    # Batched getTile: one set of GPU launches for many requests.
+    def get_tiles(self, ctxs: Sequence[TileCtx]) -> List[Tuple[int, Optional[bytes]]]:
+        n = len(ctxs)
+        reqs = (PbxTileReq * max(n, 1))(*[c.to_req() for c in ctxs])
+        res = (PbxResult * max(n, 1))()
+        st = lib().pbx_get_tiles(self._h, reqs, n, res)
+        out = []
+        try:
+            for i in range(n):
+                r = res[i]
+                body = ctypes.string_at(r.data, r.len) if r.status == OK and r.len else (
+                    b"" if r.status == OK else None)
+                ctxs[i].region["width"], ctxs[i].region["height"] = r.w, r.h
+                out.append((r.status, body))
+        finally:
+            lib().pbx_results_release(self._h, res, n)
+        if st != OK and not out:
+            _check(st)
+        return out
+
+
+class Batch:
+    """Device-resident batch (plan once, launch many): outputs stay in HBM until fetch()."""
+
+    def __init__(self, service: PixelsService, ctxs: Sequence[TileCtx]):
+        self.service = service
+        self.n = len(ctxs)
+        self._reqs = (PbxTileReq * max(self.n, 1))(*[c.to_req() for c in ctxs])
+        h = ctypes.c_void_p()
+        _check(lib().pbx_batch_plan(service.handle, self._reqs, self.n, ctypes.byref(h)))
+        self._h = h
+
+    def launch(self) -> None:
+        _check(lib().pbx_batch_launch(self.service.handle, self._h))
+
+    def sync(self) -> None:
+        _check(lib().pbx_batch_sync(self.service.handle, self._h))
+
+    def stats(self) -> PbxBatchStats:
+        s = PbxBatchStats()
+        _check(lib().pbx_batch_stats_get(self.service.handle, self._h, ctypes.byref(s)))
+        return s
+
+    def fetch(self) -> List[Tuple[int, Optional[bytes]]]:
+        res = (PbxResult * max(self.n, 1))()
+        _check(lib().pbx_batch_fetch(self.service.handle, self._h, res))
+        try:
+            return [(res[i].status, ctypes.string_at(res[i].data, res[i].len)
+                     if res[i].status == OK else None) for i in range(self.n)]
+        finally:
+            lib().pbx_results_release(self.service.handle, res, self.n)
+
+    def close(self) -> None:
+        if self._h:
+            lib().pbx_batch_destroy(self.service.handle, self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------- TileRequestHandler
+
+class TileRequestHandler:
+    """TileRequestHandler.java:53-243 — ``get_tile()`` returns bytes, or None (-> 404)."""
+
+    def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx):
+        self.pixels_service = pixels_service
+        self.tile_ctx = tile_ctx
+
+    def get_tile(self, client=None) -> Optional[bytes]:
+        status, body = self.pixels_service.get_tiles([self.tile_ctx])[0]
+        return body if status == OK else None
+
+    getTile = get_tile
+
+
+def handle_get_tile(service: PixelsService, body: str):
+    """PixelBufferVerticle.getTile (PixelBufferVerticle.java:90-147) over the JSON body.
+
+    Returns (status, payload bytes or message, headers).  400 for an undecodable TileCtx,
+    404 when the handler returns null, 500 for any other failure.
+    """
+    try:
+        ctx = TileCtx.from_json(body)
+    except Exception:
+        return 400, b"Illegal tile context", {}
+    try:
+        tile = TileRequestHandler(service, ctx).get_tile()
+    except PbxError as e:
+        return (400 if e.status == E_BADARG else 500), b"Exception while retrieving tile", {}
+    if tile is None:
+        return 404, f"Cannot find Image:{ctx.imageId}".encode(), {}
+    return 200, tile, {"filename": tile_filename(ctx),
+                       "Content-Type": content_type(ctx.format),
+                       "Content-Length": str(len(tile))}

@@ -1,0 +1,45 @@
+"""ctypes binding of lib/libpbx_emu.so: TEST-ONLY CPU emulation of the deflate workgroup."""
+import ctypes
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "omero-ms-pixel-buffer_amd", "lib", "libpbx_emu.so")
+
+
+class SegOut(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                "nbytes crc crc_op adler_s1 adler_s2 len btype bits".split()]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(LIB_PATH)
+        L.pbxemu_deflate.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(SegOut)]
+        L.pbxemu_nsegs.restype = ctypes.c_uint32
+        L.pbxemu_nsegs.argtypes = [ctypes.c_uint64]
+        L.pbxemu_crc_combine.restype = ctypes.c_uint32
+        L.pbxemu_crc_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        _lib = L
+    return _lib
+
+
+def deflate(data: bytes, rowlen: int):
+    """zlib stream exactly as the GPU pipeline produces it for one tile stream."""
+    data = bytes(data)
+    n = lib().pbxemu_nsegs(len(data))
+    segs = (SegOut * n)()
+    out = ctypes.create_string_buffer(len(data) + 1024 + 16 * n)
+    ol = ctypes.c_uint64()
+    r = lib().pbxemu_deflate(data, len(data), rowlen, out, len(out), ctypes.byref(ol), segs)
+    assert r == 0, r
+    return out.raw[: ol.value], list(segs)
+
+
+def crc_combine(c1, c2, len2):
+    return lib().pbxemu_crc_combine(c1, c2, len2)
