@@ -38,6 +38,8 @@ struct DeflateCfg {
     static constexpr int SUB = SEG / NW;  // positions parsed by one wave
     static constexpr int MAXMW = 256;     // matches kept per wave (then literals only)
     static constexpr int CAP = 32;        // per-lane match length before the wave extends it
+    static constexpr int CRCC = 64;       // CRC chunk bytes per thread (NT*CRCC >= OUTW*4)
+    static constexpr int LOG2_CRCC = 6;
     static constexpr int BUFW = (WIN + SEG + 16) / 4;
     static constexpr int OUTW = (SEG + 64) / 4;
     static constexpr int HSIZE = 1 << HBITS;
@@ -46,20 +48,30 @@ struct DeflateCfg {
     static_assert(SUB <= 65536 && SUB % CH == 0, "sub-segments hold whole thread chunks");
     static_assert(WIN + SEG <= 32768, "deflate distances are limited to 32768");
     static_assert((1 << LOGNT) == NT, "NT must be a power of two in 128..1024");
-    static_assert(NT >= 320, "ph_rank needs one thread per literal/length and distance symbol");
+    static_assert(NT >= 320, "one thread per literal/length and distance symbol");
+    static_assert(NT * CRCC >= OUTW * 4 && NT * CRCC >= SEG + 64, "CRC chunks cover the output");
 };
 
 enum : int {
     M_NL = 0, M_ND, M_HLIT, M_HDIST, M_HCLEN, M_NRLE, M_BTYPE, M_HDRBITS, M_DATABITS, M_NBYTES,
-    M_CRCOP, M_BLKBITS, M_OPK0,  // M_OPK0 .. M_OPK0+9: x^(8*CC*2^k)
-    M_NMISC = M_OPK0 + 11
+    M_CRCOP, M_BLKBITS, M_DYNBITS, M_FIXBITS,
+    M_NMISC
 };
 
-struct HuffWork {
-    uint32_t w[2 * 288];  // weights, then depths
-    uint32_t parent[2 * 288];
+struct HuffWork {  // the 19-symbol code-length code (one thread)
+    uint32_t w[2 * 19];
+    uint32_t parent[2 * 19];
     uint32_t blc[16], next[16];
     uint32_t cllen[19], clcode[19], clfreq[19], clsort[19];
+};
+
+constexpr uint32_t SORTN_ = 512;
+struct HuffScratch {  // aliases the hash table (dead after the parse)
+    uint32_t skey[SORTN_];
+    uint32_t rcnt[SORTN_];      // RLE: symbols emitted by the run starting at i -> offsets
+    uint32_t rec[2][288];       // step s: li0 | qi0 << 10 | cnt << 20
+    uint32_t leafpar[2][288];
+    uint32_t dA[2][288], aA[2][288], dB[2][288], aB[2][288];
 };
 
 template <class C>
@@ -69,7 +81,8 @@ struct DeflateSmem {
     uint32_t mdist[C::NW * C::MAXMW]; // distance - 1
     union {
         uint32_t head[C::HSIZE];      // hash -> first position (atomicMin)
-        uint32_t out[C::OUTW];        // packed output bits
+        HuffScratch hs;               // Huffman construction (after the parse)
+        uint32_t out[C::OUTW];        // packed output bits (after the codes)
     } u;
     uint32_t w_nm[C::NW];             // matches found by each wave
     uint32_t wtot[16];                // block-scan wave totals (device)
@@ -77,10 +90,13 @@ struct DeflateSmem {
     uint32_t t_s1[C::NT], t_s2[C::NT], t_len[C::NT];  // Adler partials
     uint32_t lfreq[288], dfreq[32];
     uint32_t lcode[288], dcode[32];   // bit-reversed code | len << 16
-    uint32_t lsort[288], dsort[32];
+    uint32_t hblc[2][16], hover[2], hstart[2][16], hnext[2][16];
+    uint32_t lbm[16 * 9], dbm[16];    // per-length symbol bitmaps (canonical ranks)
     uint32_t crc_table[256];
     HuffWork hw;
     uint32_t rle[320];                // code-length RLE symbols: sym | extra << 8
+    uint32_t rboff[512];              // bit offset of each RLE symbol inside the header
+    uint32_t rbm[10];                 // run starts over the concatenated code lengths
     uint32_t misc[M_NMISC];
 };
 
@@ -128,6 +144,10 @@ PBX_HD void ph_fill(uint32_t tid, DeflateSmem<C>& S, const Src& src, const SegPa
     if (tid < 288) S.lfreq[tid] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
     if (tid < 256) S.crc_table[tid] = crc_table_entry(tid);
+    if (tid == 0) {
+        S.misc[M_NL] = 0; S.misc[M_ND] = 0; S.misc[M_DYNBITS] = 0; S.misc[M_FIXBITS] = 0;
+        S.misc[M_HLIT] = 257; S.misc[M_HDIST] = 1;
+    }
 }
 
 // ----------------------------------------------------------------------- phase: insert
@@ -329,44 +349,181 @@ PBX_HD uint32_t eff_dfreq(const uint32_t* f, uint32_t s) {
     return s < 2 && v == 0 ? 1u : v;
 }
 
-// ------------------------------------------------------------ phase: rank (parallel sort)
-template <class C>
-PBX_HD void ph_rank(uint32_t tid, DeflateSmem<C>& S) {
-    if (tid < 286) {
-        const uint32_t s = tid, fs = eff_lfreq(S.lfreq, s);
-        if (fs) {
-            uint32_t rank = 0, nz = 0;
-            for (uint32_t j = 0; j < 286; j++) {
-                uint32_t fj = eff_lfreq(S.lfreq, j);
-                nz += fj != 0;
-                rank += fj != 0 && (fj < fs || (fj == fs && j < s));
-            }
-            S.lsort[rank] = s;
-            if (s == 256) S.misc[M_NL] = nz;
+// ====================================================================== Huffman codes
+// Built in parallel phases; the result equals the classic sequential construction
+// (sort by (freq, symbol), two-queue merge with leaves first on ties, zlib's overflow
+// repair at 15 bits, longest codes to the least frequent leaves, canonical codes):
+//   ph_keys     one key per symbol: (freq << 9 | sym), literal/length tree then distances
+//   (sort)      ascending keys: bitonic with wave shuffles on the device, std-sort-like in
+//               the emulator (any correct sort gives the same array)
+//   (twoqueue)  the only serial step: per tree one wave (device: weights in registers,
+//               readlane/writelane) records, per merge step, the queue positions and
+//               how many leaves it took
+//   ph_parents  every step's consumed leaves/internal nodes learn their parent step
+//   ph_jump     pointer jumping (9 rounds): depth of every internal node
+//   ph_leafdepth / ph_fixblc / ph_assign   bit-length counts, overflow repair, lengths
+//   ph_rle      code-length RLE + code-length code + block type (one thread; short)
+//   ph_codes    canonical codes: rank among same-length symbols from per-length bitmaps
+constexpr uint32_t SORTN = SORTN_;
+constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
+
+PBX_HD uint32_t tree_n(const uint32_t* misc, uint32_t T) { return misc[T ? M_ND : M_NL]; }
+PBX_HD uint32_t tree_base(const uint32_t* misc, uint32_t T) { return T ? misc[M_NL] : 0u; }
+PBX_HD uint32_t key_weight(uint32_t key) { return (key >> 9) & 0x3FFFFFu; }
+
+// (tree, index) handled by thread tid in the per-symbol / per-node phases
+PBX_HD bool tree_slot(uint32_t tid, uint32_t& T, uint32_t& i) {
+    if (tid < 288) { T = 0; i = tid; return true; }
+    if (tid < 320) { T = 1; i = tid - 288; return true; }
+    return false;
+}
+
+template <class C, class Ops>
+PBX_HD void ph_keys(uint32_t tid, DeflateSmem<C>& S) {
+    for (uint32_t t = tid; t < SORTN; t += C::NT) {
+        uint32_t key = KEY_NONE;
+        if (t < 286) {
+            const uint32_t f = eff_lfreq(S.lfreq, t);
+            if (f) { key = (f << 9) | t; Ops::add(&S.misc[M_NL], 1u); }
+        } else if (t >= 288 && t < 318) {
+            const uint32_t f = eff_dfreq(S.dfreq, t - 288);
+            if (f) { key = (1u << 31) | (f << 9) | (t - 288); Ops::add(&S.misc[M_ND], 1u); }
         }
-    } else if (tid >= 288 && tid < 288 + 30) {
-        const uint32_t s = tid - 288, fs = eff_dfreq(S.dfreq, s);
-        if (fs) {
-            uint32_t rank = 0, nz = 0;
-            for (uint32_t j = 0; j < 30; j++) {
-                uint32_t fj = eff_dfreq(S.dfreq, j);
-                nz += fj != 0;
-                rank += fj != 0 && (fj < fs || (fj == fs && j < s));
-            }
-            S.dsort[rank] = s;
-            if (s == 0) S.misc[M_ND] = nz;
+        S.u.hs.skey[t] = key;
+    }
+    if (tid < 288) S.lcode[tid] = 0;
+    if (tid < 32) S.dcode[tid] = 0;
+    if (tid < 32) { S.hblc[tid >> 4][tid & 15] = 0; }
+    if (tid < 2) S.hover[tid] = 0;
+    if (tid < 16 * 9) S.lbm[tid] = 0;
+    if (tid < 16) S.dbm[tid] = 0;
+    if (tid < 10) S.rbm[tid] = 0;
+    if (tid < 19) S.hw.clfreq[tid] = 0;
+}
+
+// Serial two-queue merge over sorted leaf weights w(0..n): records every step.
+template <class W>
+PBX_HD void twoqueue_serial(W w, uint32_t n, uint32_t* iw, uint32_t* rec) {
+    uint32_t li = 0, qi = 0, ni = 0;
+    for (uint32_t s = 0; s + 1 < n; s++) {
+        const uint32_t li0 = li, qi0 = qi;
+        uint32_t cnt = 0, sum = 0;
+        for (int k = 0; k < 2; k++) {
+            if (li < n && (qi >= ni || w(li) <= iw[qi])) { sum += w(li); li++; cnt++; }
+            else { sum += iw[qi]; qi++; }
         }
+        iw[ni++] = sum;
+        rec[s] = li0 | (qi0 << 10) | (cnt << 20);
     }
 }
 
-// Length-limited Huffman code lengths (two-queue build + zlib's overflow repair).
-// sorted: n >= 2 used symbols by ascending (freq, symbol).  lens[] is (re)written for
-// the n symbols only; the caller zeroes the rest.
-PBX_HD void huff_lengths(const uint32_t* freq_of_sorted_w, const uint32_t* sorted, uint32_t n,
-                         uint32_t maxbits, uint32_t* lens, uint32_t lens_shift, HuffWork& hw) {
+template <class C>
+PBX_HD void ph_parents(uint32_t tid, DeflateSmem<C>& S) {
+    uint32_t T, s;
+    if (!tree_slot(tid, T, s)) return;
+    const uint32_t n = tree_n(S.misc, T);
+    if (s + 1 >= n) return;
+    HuffScratch& H = S.u.hs;
+    const uint32_t r = H.rec[T][s];
+    const uint32_t li0 = r & 0x3FF, qi0 = (r >> 10) & 0x3FF, cnt = r >> 20;
+    for (uint32_t j = li0; j < li0 + cnt; j++) H.leafpar[T][j] = s;
+    for (uint32_t k = qi0; k < qi0 + 2 - cnt; k++) { H.aA[T][k] = s; H.dA[T][k] = 1; }
+    if (s + 2 == n) { H.aA[T][s] = s; H.dA[T][s] = 0; }  // the root
+}
+
+// Round r of pointer jumping over internal nodes: depth = hops to the root.
+template <class C>
+PBX_HD void ph_jump(uint32_t tid, DeflateSmem<C>& S, int r) {
+    uint32_t T, k;
+    if (!tree_slot(tid, T, k)) return;
+    const uint32_t n = tree_n(S.misc, T);
+    if (k + 1 >= n) return;
+    HuffScratch& H = S.u.hs;
+    const uint32_t* sd = (r & 1) ? H.dB[T] : H.dA[T];
+    const uint32_t* sa = (r & 1) ? H.aB[T] : H.aA[T];
+    uint32_t* dd = (r & 1) ? H.dA[T] : H.dB[T];
+    uint32_t* da = (r & 1) ? H.aA[T] : H.aB[T];
+    const uint32_t a = sa[k];
+    dd[k] = sd[k] + sd[a];
+    da[k] = sa[a];
+}
+constexpr int JUMP_ROUNDS = 9;  // 2^9 > 287 internal nodes; result lands in dB
+
+template <class C, class Ops>
+PBX_HD void ph_leafdepth(uint32_t tid, DeflateSmem<C>& S) {
+    uint32_t T, j;
+    if (!tree_slot(tid, T, j)) return;
+    if (j >= tree_n(S.misc, T)) return;
+    HuffScratch& H = S.u.hs;
+    uint32_t d = H.dB[T][H.leafpar[T][j]] + 1;
+    if (d > 15) { d = 15; Ops::add(&S.hover[T], 1u); }
+    Ops::add(&S.hblc[T][d], 1u);
+}
+
+// Per tree (thread 0: literal/length, thread 64: distance): overflow repair, the length
+// assignment table and canonical first codes.
+template <class C>
+PBX_HD void ph_fixblc(uint32_t tid, DeflateSmem<C>& S) {
+    if (tid != 0 && tid != 64) return;
+    const uint32_t T = tid ? 1 : 0, maxbits = 15;
+    uint32_t* blc = S.hblc[T];
+    int overflow = (int)S.hover[T];
+    while (overflow > 0) {  // zlib trees.c gen_bitlen
+        uint32_t bits = maxbits - 1;
+        while (blc[bits] == 0) bits--;
+        blc[bits]--;
+        blc[bits + 1] += 2;
+        blc[maxbits]--;
+        overflow -= 2;
+    }
+    uint32_t cum = 0;
+    for (uint32_t L = maxbits; L >= 1; L--) { S.hstart[T][L] = cum; cum += blc[L]; }
+    uint32_t code = 0;
+    S.hnext[T][0] = 0;
+    for (uint32_t L = 1; L <= maxbits; L++) {
+        code = (code + (L > 1 ? blc[L - 1] : 0u)) << 1;
+        S.hnext[T][L] = code;
+    }
+}
+
+template <class C, class Ops>
+PBX_HD void ph_assign(uint32_t tid, DeflateSmem<C>& S) {
+    uint32_t T, j;
+    if (!tree_slot(tid, T, j)) return;
+    if (j >= tree_n(S.misc, T)) return;
+    const uint32_t key = S.u.hs.skey[tree_base(S.misc, T) + j];
+    const uint32_t sym = key & 0x1FF;
+    uint32_t L = 15;
+    while (L > 1 && j >= S.hstart[T][L] + S.hblc[T][L]) L--;
+    if (T == 0) {
+        S.lcode[sym] = L << 16;
+        Ops::aor(&S.lbm[L * 9 + (sym >> 5)], 1u << (sym & 31));
+        const uint32_t f = S.lfreq[sym];
+        if (f) {
+            const uint32_t eb = sym >= 257 ? len_sym_ebits(sym) : 0;
+            Ops::add(&S.misc[M_DYNBITS], f * (L + eb));
+            Ops::add(&S.misc[M_FIXBITS], f * (fixed_lit_len(sym) + eb));
+        }
+        Ops::amax(&S.misc[M_HLIT], sym + 1);
+    } else {
+        S.dcode[sym] = L << 16;
+        Ops::aor(&S.dbm[L], 1u << sym);
+        const uint32_t f = S.dfreq[sym];
+        if (f) {
+            const uint32_t eb = dist_sym_ebits(sym);
+            Ops::add(&S.misc[M_DYNBITS], f * (L + eb));
+            Ops::add(&S.misc[M_FIXBITS], f * (5 + eb));
+        }
+        Ops::amax(&S.misc[M_HDIST], sym + 1);
+    }
+}
+
+// Length-limited Huffman lengths for a small alphabet (the 19-symbol code-length code).
+PBX_HD void huff_lengths_small(const uint32_t* wsorted, const uint32_t* sorted, uint32_t n,
+                               uint32_t maxbits, uint32_t* lens, HuffWork& hw) {
     uint32_t* w = hw.w;
     uint32_t* parent = hw.parent;
-    for (uint32_t i = 0; i < n; i++) w[i] = freq_of_sorted_w[i];
+    for (uint32_t i = 0; i < n; i++) w[i] = wsorted[i];
     uint32_t li = 0, qi = n, nxt = n;
     for (uint32_t k = 0; k + 1 < n; k++) {
         uint32_t a, b;
@@ -379,7 +536,7 @@ PBX_HD void huff_lengths(const uint32_t* freq_of_sorted_w, const uint32_t* sorte
     }
     const uint32_t root = 2 * n - 2;
     w[root] = 0;
-    for (uint32_t i = root; i-- > 0;) w[i] = w[parent[i]] + 1;  // depths
+    for (uint32_t i = root; i-- > 0;) w[i] = w[parent[i]] + 1;
     for (uint32_t b = 0; b < 16; b++) hw.blc[b] = 0;
     int overflow = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -397,10 +554,10 @@ PBX_HD void huff_lengths(const uint32_t* freq_of_sorted_w, const uint32_t* sorte
     }
     uint32_t idx = 0;
     for (uint32_t bits = maxbits; bits >= 1; bits--)
-        for (uint32_t c = hw.blc[bits]; c > 0; c--) lens[sorted[idx++]] = bits << lens_shift;
+        for (uint32_t c = hw.blc[bits]; c > 0; c--) lens[sorted[idx++]] = bits << 16;
 }
 
-// Canonical codes from lengths stored as (len << 16) in codes[]; result: rev code | len << 16.
+// Canonical codes from lengths stored as (len << 16); result: rev code | len << 16.
 PBX_HD void huff_codes(uint32_t* codes, uint32_t nsym, uint32_t maxbits, HuffWork& hw) {
     for (uint32_t b = 0; b < 16; b++) hw.blc[b] = 0;
     for (uint32_t s = 0; s < nsym; s++) hw.blc[codes[s] >> 16]++;
@@ -418,105 +575,129 @@ PBX_HD void huff_codes(uint32_t* codes, uint32_t nsym, uint32_t maxbits, HuffWor
 
 PBX_HD uint32_t rle_ebits(uint32_t sym) { return sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0; }
 
-// ----------------------------------------------------------- phase: Huffman (one thread)
+// ----------------------------------------------- code-length RLE (parallel phases)
+// The HLIT + HDIST code lengths are run-length coded (RFC 1951 3.2.7) run by run: a run
+// of zeros becomes 18s (11..138), one 17 (3..10) and plain zeros; a run of v != 0 becomes
+// v then 16s (3..6) and plain v's.  Runs may cross from the literal into the distance
+// lengths.  ph_rle_mark flags run starts, ph_rle_count sizes each run's symbols, an
+// exclusive scan places them, ph_rle_emit writes them.
 template <class C>
-PBX_HD void ph_huff(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
+PBX_HD uint32_t cl_len_at(const DeflateSmem<C>& S, uint32_t i) {
+    const uint32_t hlit = S.misc[M_HLIT];
+    return i < hlit ? S.lcode[i] >> 16 : S.dcode[i - hlit] >> 16;
+}
+
+template <class C, class Ops>
+PBX_HD void ph_rle_mark(uint32_t tid, DeflateSmem<C>& S) {
+    const uint32_t ntot = S.misc[M_HLIT] + S.misc[M_HDIST];
+    if (tid < ntot && (tid == 0 || cl_len_at(S, tid) != cl_len_at(S, tid - 1)))
+        Ops::aor(&S.rbm[tid >> 5], 1u << (tid & 31));
+}
+
+PBX_HD uint32_t rle_nsyms(uint32_t v, uint32_t run) {
+    if (v == 0) {
+        uint32_t n = 0;
+        while (run >= 11) { run -= run < 138 ? run : 138; n++; }
+        if (run >= 3) return n + 1;
+        return n + run;
+    }
+    run--;
+    return 1 + run / 6 + ((run % 6) >= 3 ? 1 : run % 6);
+}
+
+template <class C>
+PBX_HD uint32_t rle_run_len(const DeflateSmem<C>& S, uint32_t i, uint32_t ntot) {
+    uint32_t w = (i + 1) >> 5;
+    uint32_t m = (i + 1) < 320 ? S.rbm[w] & ~((1u << ((i + 1) & 31)) - 1u) : 0u;
+    while (!m && ++w < 10) m = S.rbm[w];
+    const uint32_t nxt = m ? (w << 5) + (uint32_t)__builtin_ctz(m) : ntot;
+    return (nxt < ntot ? nxt : ntot) - i;
+}
+
+template <class C>
+PBX_HD void ph_rle_count(uint32_t tid, DeflateSmem<C>& S) {
+    const uint32_t ntot = S.misc[M_HLIT] + S.misc[M_HDIST];
+    uint32_t cnt = 0;
+    if (tid < ntot && ((S.rbm[tid >> 5] >> (tid & 31)) & 1u))
+        cnt = rle_nsyms(cl_len_at(S, tid), rle_run_len(S, tid, ntot));
+    S.u.hs.rcnt[tid] = cnt;
+}
+
+// requires rcnt = exclusive prefix of the counts and misc[M_NRLE] = their total
+template <class C, class Ops>
+PBX_HD void ph_rle_emit(uint32_t tid, DeflateSmem<C>& S) {
+    const uint32_t ntot = S.misc[M_HLIT] + S.misc[M_HDIST];
+    if (!(tid < ntot && ((S.rbm[tid >> 5] >> (tid & 31)) & 1u))) return;
+    const uint32_t v = cl_len_at(S, tid);
+    uint32_t run = rle_run_len(S, tid, ntot), k = S.u.hs.rcnt[tid];
+    uint32_t* cf = S.hw.clfreq;
+    if (v == 0) {
+        while (run >= 11) {
+            const uint32_t n = run < 138 ? run : 138;
+            S.rle[k++] = 18u | ((n - 11) << 8); Ops::add(&cf[18], 1u); run -= n;
+        }
+        if (run >= 3) { S.rle[k++] = 17u | ((run - 3) << 8); Ops::add(&cf[17], 1u); run = 0; }
+        while (run) { S.rle[k++] = 0; Ops::add(&cf[0], 1u); run--; }
+    } else {
+        S.rle[k++] = v; Ops::add(&cf[v], 1u); run--;
+        while (run >= 3) {
+            const uint32_t n = run < 6 ? run : 6;
+            S.rle[k++] = 16u | ((n - 3) << 8); Ops::add(&cf[16], 1u); run -= n;
+        }
+        while (run) { S.rle[k++] = v; Ops::add(&cf[v], 1u); run--; }
+    }
+}
+
+// Code-length code (19 symbols, max 7 bits; at least two used symbols).  One thread.
+template <class C>
+PBX_HD void ph_clen(uint32_t tid, DeflateSmem<C>& S) {
     if (tid != 0) return;
     HuffWork& hw = S.hw;
-    // literal/length tree
-    const uint32_t nl = S.misc[M_NL], nd = S.misc[M_ND];
-    for (uint32_t s = 0; s < 288; s++) S.lcode[s] = 0;
-    for (uint32_t s = 0; s < 32; s++) S.dcode[s] = 0;
-    // (weights are staged in hw.w itself; huff_lengths' copy is then a no-op)
-    for (uint32_t i = 0; i < nl; i++) hw.w[i] = eff_lfreq(S.lfreq, S.lsort[i]);
-    huff_lengths(hw.w, S.lsort, nl, 15, S.lcode, 16, hw);
-    for (uint32_t i = 0; i < nd; i++) hw.w[i] = eff_dfreq(S.dfreq, S.dsort[i]);
-    huff_lengths(hw.w, S.dsort, nd, 15, S.dcode, 16, hw);
-    // data bits (dynamic and fixed)
-    uint64_t dyn = 0, fix = 0;
-    for (uint32_t s = 0; s < 286; s++) {
-        uint32_t f = S.lfreq[s];
-        if (!f) continue;
-        uint32_t eb = s >= 257 ? len_sym_ebits(s) : 0;
-        dyn += (uint64_t)f * ((S.lcode[s] >> 16) + eb);
-        fix += (uint64_t)f * (fixed_lit_len(s) + eb);
-    }
-    for (uint32_t s = 0; s < 30; s++) {
-        uint32_t f = S.dfreq[s];
-        if (!f) continue;
-        uint32_t eb = dist_sym_ebits(s);
-        dyn += (uint64_t)f * ((S.dcode[s] >> 16) + eb);
-        fix += (uint64_t)f * (5 + eb);
-    }
-    // HLIT / HDIST and the run-length coded code lengths
-    uint32_t hlit = 286;
-    while (hlit > 257 && (S.lcode[hlit - 1] >> 16) == 0) hlit--;
-    uint32_t hdist = 30;
-    while (hdist > 1 && (S.dcode[hdist - 1] >> 16) == 0) hdist--;
-    const uint32_t ntot = hlit + hdist;
-    for (uint32_t s = 0; s < 19; s++) hw.clfreq[s] = 0;
-    uint32_t nr = 0;
-    uint32_t i = 0;
-    while (i < ntot) {
-        uint32_t v = i < hlit ? S.lcode[i] >> 16 : S.dcode[i - hlit] >> 16;
-        uint32_t run = 1;
-        while (i + run < ntot) {
-            uint32_t u = (i + run) < hlit ? S.lcode[i + run] >> 16 : S.dcode[i + run - hlit] >> 16;
-            if (u != v) break;
-            run++;
+    uint32_t* cf = hw.clfreq;
+    uint32_t used = 0, ncl = 0;
+    for (uint32_t s = 0; s < 19; s++) used += cf[s] != 0;
+    for (uint32_t s = 0; s < 19 && used < 2; s++) if (!cf[s]) { cf[s] = 1; used++; }
+    for (uint32_t s = 0; s < 19; s++) {
+        hw.clcode[s] = 0;
+        if (!cf[s]) continue;
+        uint32_t k = ncl++;
+        while (k > 0) {
+            const uint32_t t = hw.clsort[k - 1];
+            if (cf[t] < cf[s] || (cf[t] == cf[s] && t < s)) break;
+            hw.clsort[k] = t;
+            k--;
         }
-        i += run;
-        if (v == 0) {
-            while (run >= 11) {
-                uint32_t n = run < 138 ? run : 138;
-                S.rle[nr++] = 18u | ((n - 11) << 8); hw.clfreq[18]++; run -= n;
-            }
-            if (run >= 3) { S.rle[nr++] = 17u | ((run - 3) << 8); hw.clfreq[17]++; run = 0; }
-            while (run) { S.rle[nr++] = 0; hw.clfreq[0]++; run--; }
-        } else {
-            S.rle[nr++] = v; hw.clfreq[v]++; run--;
-            while (run >= 3) {
-                uint32_t n = run < 6 ? run : 6;
-                S.rle[nr++] = 16u | ((n - 3) << 8); hw.clfreq[16]++; run -= n;
-            }
-            while (run) { S.rle[nr++] = v; hw.clfreq[v]++; run--; }
-        }
+        hw.clsort[k] = s;
     }
-    // code-length code (19 symbols, max 7 bits); same two-symbol minimum as above
-    uint32_t ncl = 0;
-    for (uint32_t s = 0; s < 19; s++) hw.cllen[s] = 0;
-    {
-        uint32_t* cf = hw.clfreq;  // gets the dummies; only the code-length tree reads it
-        uint32_t used = 0;
-        for (uint32_t s = 0; s < 19; s++) used += cf[s] != 0;
-        for (uint32_t s = 0; s < 19 && used < 2; s++) if (!cf[s]) { cf[s] = 1; used++; }
-        // insertion sort by (freq, sym)
-        for (uint32_t s = 0; s < 19; s++) {
-            if (!cf[s]) continue;
-            uint32_t k = ncl++;
-            while (k > 0) {
-                uint32_t t = hw.clsort[k - 1];
-                if (cf[t] < cf[s] || (cf[t] == cf[s] && t < s)) break;
-                hw.clsort[k] = t;
-                k--;
-            }
-            hw.clsort[k] = s;
-        }
-        for (uint32_t k = 0; k < ncl; k++) hw.w[k] = cf[hw.clsort[k]];
-        huff_lengths(hw.w, hw.clsort, ncl, 7, hw.clcode, 16, hw);
-        for (uint32_t s = 0; s < 19; s++) if (!cf[s]) hw.clcode[s] = 0;
-        huff_codes(hw.clcode, 19, 7, hw);
-        for (uint32_t s = 0; s < 19; s++) hw.cllen[s] = hw.clcode[s] >> 16;
-    }
+    uint32_t wsorted[19];
+    for (uint32_t k = 0; k < ncl; k++) wsorted[k] = cf[hw.clsort[k]];
+    huff_lengths_small(wsorted, hw.clsort, ncl, 7, hw.clcode, hw);
+    huff_codes(hw.clcode, 19, 7, hw);
+    for (uint32_t s = 0; s < 19; s++) hw.cllen[s] = hw.clcode[s] >> 16;
     const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
     uint32_t hclen = 19;
     while (hclen > 4 && hw.cllen[order[hclen - 1]] == 0) hclen--;
-    uint64_t hdr = 3 + 5 + 5 + 4 + 3ull * hclen;
-    for (uint32_t k = 0; k < nr; k++) {
-        uint32_t sym = S.rle[k] & 0xFF;
-        hdr += hw.cllen[sym] + rle_ebits(sym);
+    S.misc[M_HCLEN] = hclen;
+}
+
+// Bits of each RLE symbol (for the header offsets) into rboff[0..NT).
+template <class C>
+PBX_HD void ph_rle_bits(uint32_t tid, DeflateSmem<C>& S) {
+    uint32_t b = 0;
+    if (tid < S.misc[M_NRLE]) {
+        const uint32_t sym = S.rle[tid] & 0xFF;
+        b = S.hw.cllen[sym] + rle_ebits(sym);
     }
-    const uint64_t dyn_bits = hdr + dyn, fix_bits = 3 + fix;
+    S.rboff[tid] = b;
+}
+
+// Block type from the three sizes.  Requires rboff = exclusive prefix of RLE bits and
+// misc[M_HDRBITS] = their total.  One thread.
+template <class C>
+PBX_HD void ph_choose(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
+    if (tid != 0) return;
+    const uint64_t hdr = 3 + 5 + 5 + 4 + 3ull * S.misc[M_HCLEN] + S.misc[M_HDRBITS];
+    const uint64_t dyn_bits = hdr + S.misc[M_DYNBITS], fix_bits = 3ull + S.misc[M_FIXBITS];
     auto bytes_of = [&](uint64_t bits) -> uint64_t {
         return sp.last ? (bits + 7) / 8 : (bits + 3 + 7) / 8 + 4;
     };
@@ -525,24 +706,42 @@ PBX_HD void ph_huff(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
     uint64_t best = bytes_of(dyn_bits);
     if (bytes_of(fix_bits) <= best) { btype = 1; best = bytes_of(fix_bits); }
     if (stored_bytes <= best) { btype = 0; best = stored_bytes; }
-    if (btype == 1) {
-        for (uint32_t s = 0; s < 288; s++) S.lcode[s] = fixed_lit_len(s) << 16;
-        for (uint32_t s = 0; s < 32; s++) S.dcode[s] = 5u << 16;
-        huff_codes(S.lcode, 288, 15, hw);
-        huff_codes(S.dcode, 32, 15, hw);
-        S.misc[M_HDRBITS] = 3;
-    } else if (btype == 2) {
-        huff_codes(S.lcode, 288, 15, hw);
-        huff_codes(S.dcode, 32, 15, hw);
-        S.misc[M_HDRBITS] = (uint32_t)hdr;
-    } else {
-        S.misc[M_HDRBITS] = 0;
-    }
+    S.misc[M_HDRBITS] = btype == 2 ? (uint32_t)hdr : btype == 1 ? 3u : 0u;
     S.misc[M_BTYPE] = btype;
-    S.misc[M_HLIT] = hlit;
-    S.misc[M_HDIST] = hdist;
-    S.misc[M_HCLEN] = hclen;
-    S.misc[M_NRLE] = nr;
+}
+
+// Fixed Huffman codes (RFC 1951 3.2.6) in closed form: rev code | len << 16.
+PBX_HD uint32_t fixed_lit_code(uint32_t s) {
+    if (s < 144) return bitrev(0x30 + s, 8) | (8u << 16);
+    if (s < 256) return bitrev(0x190 + (s - 144), 9) | (9u << 16);
+    if (s < 280) return bitrev(s - 256, 7) | (7u << 16);
+    return bitrev(0xC0 + (s - 280), 8) | (8u << 16);
+}
+
+// ------------------------------------------------------------ phase: canonical codes
+template <class C>
+PBX_HD void ph_codes(uint32_t tid, DeflateSmem<C>& S) {
+    uint32_t T, sym;
+    if (!tree_slot(tid, T, sym)) return;
+    const uint32_t bt = S.misc[M_BTYPE];
+    if (bt == 1) {
+        if (T == 0) S.lcode[sym] = fixed_lit_code(sym);
+        else S.dcode[sym] = bitrev(sym, 5) | (5u << 16);
+        return;
+    }
+    if (bt == 0) return;
+    uint32_t* codes = T ? S.dcode : S.lcode;
+    const uint32_t L = codes[sym] >> 16;
+    if (!L) return;
+    uint32_t rank;
+    if (T == 0) {
+        const uint32_t* bm = S.lbm + L * 9;
+        rank = (uint32_t)__builtin_popcount(bm[sym >> 5] & ((1u << (sym & 31)) - 1u));
+        for (uint32_t w = 0; w < (sym >> 5); w++) rank += (uint32_t)__builtin_popcount(bm[w]);
+    } else {
+        rank = (uint32_t)__builtin_popcount(S.dbm[L] & ((1u << sym) - 1u));
+    }
+    codes[sym] = bitrev(S.hnext[T][L] + rank, L) | (L << 16);
 }
 
 template <class C>
@@ -622,22 +821,30 @@ PBX_HD void ph_write(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
         const uint32_t hdr = S.misc[M_HDRBITS];
         WriteF<C, Ops> f{S, {S.u.out, hdr + S.t_a[tid]}};
         walk_tokens<C>(tid, S, sp, f);
+        // header: fields by thread 0, code-length code lengths by threads < HCLEN,
+        // RLE symbols by one thread each at their scanned offsets
+        if (bt == 2) {
+            const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            const uint32_t hclen = S.misc[M_HCLEN];
+            if (tid < hclen) {
+                BitWriter<C, Ops> bw{S.u.out, 17 + 3 * tid};
+                bw.put(S.hw.cllen[order[tid]], 3);
+            }
+            if (tid < S.misc[M_NRLE]) {
+                const uint32_t r = S.rle[tid], sym = r & 0xFF, c = S.hw.clcode[sym];
+                BitWriter<C, Ops> bw{S.u.out, 17 + 3 * hclen + S.rboff[tid]};
+                bw.put(c & 0xFFFF, c >> 16);
+                bw.put(r >> 8, rle_ebits(sym));
+            }
+        }
         if (tid == 0) {
             BitWriter<C, Ops> bw{S.u.out, 0};
             bw.put(sp.last ? 1u : 0u, 1);
             bw.put(bt, 2);
             if (bt == 2) {
-                const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
                 bw.put(S.misc[M_HLIT] - 257, 5);
                 bw.put(S.misc[M_HDIST] - 1, 5);
                 bw.put(S.misc[M_HCLEN] - 4, 4);
-                for (uint32_t k = 0; k < S.misc[M_HCLEN]; k++) bw.put(S.hw.cllen[order[k]], 3);
-                for (uint32_t k = 0; k < S.misc[M_NRLE]; k++) {
-                    const uint32_t r = S.rle[k], sym = r & 0xFF;
-                    const uint32_t c = S.hw.clcode[sym];
-                    bw.put(c & 0xFFFF, c >> 16);
-                    bw.put(r >> 8, rle_ebits(sym));
-                }
             }
             // end of block, then (not last) an empty stored block to reach a byte boundary
             bw.pos = hdr + S.misc[M_DATABITS];
@@ -651,17 +858,7 @@ PBX_HD void ph_write(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp) {
             }
         }
     }
-    // CRC constants for the tree combine (chunks are right-aligned: every right operand
-    // is full, so level k always shifts by x^(8*CC*2^k)).
-    if (tid == C::NT - 1) {
-        const uint32_t cc = (nbytes + C::NT - 1) / C::NT;
-        uint32_t op = crc_x8n(cc);
-        for (int k = 0; k <= C::LOGNT; k++) {
-            S.misc[M_OPK0 + k] = op;
-            op = crc_multmodp(op, op);
-        }
-    }
-    if (tid == C::NT - 2) S.misc[M_CRCOP] = crc_x8n(nbytes);
+    if (tid == C::NT - 1) S.misc[M_CRCOP] = crc_x8n(nbytes);
     if (tid == 0 && bt == 0) S.misc[M_BLKBITS] = 8 * nbytes;
     if (tid == 0) S.misc[M_NBYTES] = nbytes;
 }
@@ -687,11 +884,11 @@ PBX_HD void ph_store(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp, uint8
     } else {
         for (uint32_t j = tid; j < nbytes; j += C::NT) slot[j] = (uint8_t)out_byte(S, sp, j);
     }
-    // Raw CRC (register init 0, no final xor) of a right-aligned chunk: thread t covers
-    // [n - (NT-t)*cc, n - (NT-1-t)*cc).  Leading zero bytes leave a raw CRC unchanged, so a
-    // short or empty chunk counts as a full cc-byte one and every tree level shifts by the
-    // same x^(8*cc*2^k).
-    const uint32_t cc = (nbytes + C::NT - 1) / C::NT;
+    // Raw CRC (register init 0, no final xor) of a right-aligned CRCC-byte chunk: thread t
+    // covers [n - (NT-t)*CRCC, n - (NT-1-t)*CRCC).  Leading zero bytes leave a raw CRC
+    // unchanged, so a short or empty chunk counts as a full one and tree level k shifts by
+    // the constant x^(8*CRCC*2^k).
+    const uint32_t cc = (uint32_t)C::CRCC;
     const int64_t hi = (int64_t)nbytes - (int64_t)(C::NT - 1 - tid) * cc;
     int64_t lo = hi - cc;
     if (lo < 0) lo = 0;
@@ -701,14 +898,15 @@ PBX_HD void ph_store(uint32_t tid, DeflateSmem<C>& S, const SegParams& sp, uint8
 }
 
 // ------------------------------------------------------- phase: tree combine level k
+// op = x^(8 * CRCC * 2^k) = crc_x8pow2(LOG2_CRCC + k)
 template <class C>
-PBX_HD void ph_tree(uint32_t tid, DeflateSmem<C>& S, int k) {
+PBX_HD void ph_tree(uint32_t tid, DeflateSmem<C>& S, int k, uint32_t op) {
     const uint32_t step = 1u << k;
     if ((tid & (2 * step - 1)) == 0 && tid + step < (uint32_t)C::NT) {
         const uint32_t r = tid + step;
         adler_combine(S.t_s1[tid], S.t_s2[tid], S.t_s1[r], S.t_s2[r], S.t_len[r]);
         S.t_len[tid] += S.t_len[r];
-        S.t_a[tid] = crc_combine_op(S.t_a[tid], S.t_a[r], S.misc[M_OPK0 + k]);
+        S.t_a[tid] = crc_combine_op(S.t_a[tid], S.t_a[r], op);
     }
 }
 

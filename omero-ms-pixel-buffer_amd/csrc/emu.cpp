@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -21,6 +22,7 @@ namespace {
 
 struct EmuOps {
     static void amin(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
+    static void amax(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
     static void add(uint32_t* p, uint32_t v) { *p += v; }
     static void aor(uint32_t* p, uint32_t v) { *p |= v; }
 };
@@ -40,14 +42,36 @@ void run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, Se
     for (int t = 0; t < C::NT; t++) ph_insert<C, EmuOps>(t, S, sp);
     for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
     for (int t = 0; t < C::NT; t++) ph_hist<C, EmuOps>(t, S, sp);
-    for (int t = 0; t < C::NT; t++) ph_rank<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_huff<C>(t, S, sp);
+    for (int t = 0; t < C::NT; t++) ph_keys<C, EmuOps>(t, S);
+    std::sort(S.u.hs.skey, S.u.hs.skey + SORTN);
+    {
+        std::vector<uint32_t> iw(SORTN);
+        const uint32_t nl = S.misc[M_NL], nd = S.misc[M_ND];
+        const uint32_t* sk = S.u.hs.skey;
+        twoqueue_serial([&](uint32_t i) { return key_weight(sk[i]); }, nl, iw.data(), S.u.hs.rec[0]);
+        twoqueue_serial([&](uint32_t i) { return key_weight(sk[nl + i]); }, nd, iw.data(), S.u.hs.rec[1]);
+    }
+    for (int t = 0; t < C::NT; t++) ph_parents<C>(t, S);
+    for (int r = 0; r < JUMP_ROUNDS; r++)
+        for (int t = 0; t < C::NT; t++) ph_jump<C>(t, S, r);
+    for (int t = 0; t < C::NT; t++) ph_leafdepth<C, EmuOps>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_fixblc<C>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_assign<C, EmuOps>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_rle_mark<C, EmuOps>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_rle_count<C>(t, S);
+    S.misc[M_NRLE] = scan_excl_add(S.u.hs.rcnt);
+    for (int t = 0; t < C::NT; t++) ph_rle_emit<C, EmuOps>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_clen<C>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_rle_bits<C>(t, S);
+    S.misc[M_HDRBITS] = scan_excl_add(S.rboff);
+    for (int t = 0; t < C::NT; t++) ph_choose<C>(t, S, sp);
+    for (int t = 0; t < C::NT; t++) ph_codes<C>(t, S);
     for (int t = 0; t < C::NT; t++) ph_bits<C>(t, S, sp);
     S.misc[M_DATABITS] = scan_excl_add(S.t_a);
     for (int t = 0; t < C::NT; t++) ph_write<C, EmuOps>(t, S, sp);
     for (int t = 0; t < C::NT; t++) ph_store<C>(t, S, sp, slot);
     for (int k = 0; k < C::LOGNT; k++)
-        for (int t = 0; t < C::NT; t++) ph_tree<C>(t, S, k);
+        for (int t = 0; t < C::NT; t++) ph_tree<C>(t, S, k, crc_x8pow2(C::LOG2_CRCC + k));
     for (int t = 0; t < C::NT; t++) ph_final<C>(t, S, sp, so);
 }
 

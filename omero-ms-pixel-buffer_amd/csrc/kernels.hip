@@ -25,6 +25,7 @@ using DC = DeflateMainCfg;
 
 struct DevOps {
     __device__ static void amin(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+    __device__ static void amax(uint32_t* p, uint32_t v) { atomicMax(p, v); }
     __device__ static void add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
     __device__ static void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 };
@@ -121,13 +122,117 @@ __device__ void ph_parse_dev(uint32_t tid, DeflateSmem<C>& S, const SegParams& s
     if (lane == 0) S.w_nm[w] = nm;
 }
 
+// Ascending bitonic sort of SORTN (= NT) keys, one per thread: wave shuffles for
+// partners inside a wave, LDS + barriers for the 6 cross-wave steps.
 template <class C>
+__device__ void bitonic_sort_keys(uint32_t tid, uint32_t* keys) {
+    static_assert(C::NT == (int)SORTN, "one key per thread");
+    uint32_t v = keys[tid];
+#pragma unroll
+    for (uint32_t k = 2; k <= SORTN; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            uint32_t o;
+            if (j >= 64) {
+                keys[tid] = v;
+                __syncthreads();
+                o = keys[tid ^ j];
+                __syncthreads();
+            } else {
+                o = __shfl_xor(v, (int)j, 64);
+            }
+            const bool up = (tid & k) == 0, lower = (tid & j) == 0;
+            v = (lower == up) ? (v < o ? v : o) : (v < o ? o : v);
+        }
+    }
+    keys[tid] = v;
+}
+
+// The serial Huffman merge on one wave per tree (wave 0: literal/length, wave 1: distance).
+// Queues live in LDS; the wave keeps 64-entry register windows over them (lane i = entry
+// 64*block + i): the leaf read window, the internal-node write window and read window,
+// and the step-record write window.  Every access is one readlane or one lane select;
+// windows move (one LDS access per lane) every 64 entries.  Same records as
+// twoqueue_serial in deflate_seg.h.
+template <class C>
+__device__ void ph_twoqueue_dev(uint32_t tid, DeflateSmem<C>& S) {
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    if (wv > 1) return;
+    const uint32_t T = wv;
+    const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
+    const uint32_t* sk = S.u.hs.skey + base;
+    uint32_t* iq = S.u.hs.dB[T];  // internal weights (dB is free until the jump rounds)
+    uint32_t* rq = S.u.hs.rec[T];
+    const uint32_t INF = 0xFFFFFFFFu;
+    uint32_t lblk = 0, iwblk = 0, irblk = 0xFFFFFFFFu, rblk = 0;
+    uint32_t Wwin = lane < n ? key_weight(sk[lane]) : INF;
+    uint32_t Iw = 0, Ir = 0, Rw = 0;
+    uint32_t li = 0, qi = 0, ni = 0;
+    uint32_t lw = __builtin_amdgcn_readlane(Wwin, 0), iw = INF;
+    for (uint32_t s = 0; s + 1 < n; s++) {
+        const uint32_t rec = li | (qi << 10);
+        uint32_t cnt = 0, sum = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (lw <= iw) {
+                sum += lw; li++; cnt++;
+                if (li < n) {
+                    if ((li >> 6) != lblk) {
+                        lblk = li >> 6;
+                        const uint32_t e = lblk * 64 + lane;
+                        Wwin = e < n ? key_weight(sk[e]) : INF;
+                    }
+                    lw = __builtin_amdgcn_readlane(Wwin, li & 63);
+                } else {
+                    lw = INF;
+                }
+            } else {
+                sum += iw; qi++;
+                if (qi < ni) {
+                    if ((qi >> 6) == iwblk) {
+                        iw = __builtin_amdgcn_readlane(Iw, qi & 63);
+                    } else {
+                        if ((qi >> 6) != irblk) { irblk = qi >> 6; Ir = iq[irblk * 64 + lane]; }
+                        iw = __builtin_amdgcn_readlane(Ir, qi & 63);
+                    }
+                } else {
+                    iw = INF;
+                }
+            }
+        }
+        if ((ni >> 6) != iwblk) {  // the write window moves on: flush it
+            if (iwblk * 64 + lane < 288) iq[iwblk * 64 + lane] = Iw;
+            iwblk = ni >> 6;
+        }
+        Iw = lane == (ni & 63) ? sum : Iw;
+        if (qi == ni) iw = sum;
+        ni++;
+        if ((s >> 6) != rblk) {
+            if (rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
+            rblk = s >> 6;
+        }
+        Rw = lane == (s & 63) ? (rec | (cnt << 20)) : Rw;
+    }
+    if (n > 1 && rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
+}
+
+// PROF: diagnostic build only (PBX_PHASE_PROFILE=1): thread 0 stamps s_memtime after each
+// barrier into stamps[seg * 16 + phase]; no output value depends on a stamp.
+template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT) void k_deflate(const TileDesc* __restrict__ dt, uint32_t ndt,
                                                    uint32_t nseg, const uint8_t* __restrict__ rowfilt,
                                                    uint8_t* __restrict__ slots, uint32_t slot_stride,
-                                                   SegOut* __restrict__ segout) {
+                                                   SegOut* __restrict__ segout,
+                                                   uint64_t* __restrict__ stamps) {
     __shared__ DeflateSmem<C> S;
     const uint32_t tid = threadIdx.x;
+    uint32_t nst = 0;
+    auto stamp = [&]() {
+        if (PROF && tid == 0) stamps[(size_t)xcd_remap(blockIdx.x, gridDim.x) * 16 + nst] = __builtin_amdgcn_s_memtime();
+        nst++;
+    };
+    stamp();
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
     if (seg >= nseg) return;
     const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
@@ -145,31 +250,85 @@ __global__ __launch_bounds__(C::NT) void k_deflate(const TileDesc* __restrict__ 
 
     ph_fill<C>(tid, S, src, sp);
     __syncthreads();
+    stamp();
     ph_insert<C, DevOps>(tid, S, sp);
     __syncthreads();
+    stamp();
     ph_parse_dev<C>(tid, S, sp);
     __syncthreads();
+    stamp();
     ph_hist<C, DevOps>(tid, S, sp);
     __syncthreads();
-    ph_rank<C>(tid, S);
+    stamp();
+    ph_keys<C, DevOps>(tid, S);
     __syncthreads();
-    ph_huff<C>(tid, S, sp);
+    bitonic_sort_keys<C>(tid, S.u.hs.skey);
     __syncthreads();
+    stamp();
+    ph_twoqueue_dev<C>(tid, S);
+    __syncthreads();
+    stamp();
+    ph_parents<C>(tid, S);
+    __syncthreads();
+#pragma unroll 1
+    for (int r = 0; r < JUMP_ROUNDS; r++) {
+        ph_jump<C>(tid, S, r);
+        __syncthreads();
+    }
+    stamp();
+    ph_leafdepth<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_fixblc<C>(tid, S);
+    __syncthreads();
+    ph_assign<C, DevOps>(tid, S);
+    __syncthreads();
+    stamp();
+    ph_rle_mark<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_rle_count<C>(tid, S);
+    __syncthreads();
+    {
+        const uint32_t nr = block_scan_excl_add<C::NT>(S.u.hs.rcnt, S.wtot, tid);
+        if (tid == 0) S.misc[M_NRLE] = nr;
+    }
+    __syncthreads();
+    ph_rle_emit<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_clen<C>(tid, S);
+    __syncthreads();
+    ph_rle_bits<C>(tid, S);
+    __syncthreads();
+    {
+        const uint32_t hb = block_scan_excl_add<C::NT>(S.rboff, S.wtot, tid);
+        if (tid == 0) S.misc[M_HDRBITS] = hb;
+    }
+    __syncthreads();
+    ph_choose<C>(tid, S, sp);
+    __syncthreads();
+    ph_codes<C>(tid, S);
+    __syncthreads();
+    stamp();
     ph_bits<C>(tid, S, sp);
     __syncthreads();
+    stamp();
     const uint32_t total = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
     if (tid == 0) S.misc[M_DATABITS] = total;
     __syncthreads();
+    stamp();
     ph_write<C, DevOps>(tid, S, sp);
     __syncthreads();
+    stamp();
     ph_store<C>(tid, S, sp, slots + (size_t)seg * slot_stride);
     __syncthreads();
-#pragma unroll 1
+    stamp();
+#pragma unroll
     for (int lv = 0; lv < C::LOGNT; lv++) {
-        ph_tree<C>(tid, S, lv);
+        ph_tree<C>(tid, S, lv, crc_x8pow2(C::LOG2_CRCC + lv));
         __syncthreads();
     }
+    stamp();
     ph_final<C>(tid, S, sp, &segout[seg]);
+    stamp();
 }
 
 // ------------------------------------------------------------------- synthetic planes
@@ -435,10 +594,14 @@ hipError_t launch_rowfilter(hipStream_t st, const TileDesc* d_tiles, uint32_t nt
 
 hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nseg,
                           const uint8_t* rowfilt, uint8_t* slots, uint32_t slot_stride,
-                          SegOut* segout) {
+                          SegOut* segout, uint64_t* stamps) {
     if (!ntiles || !nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_deflate<DC>, dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles, nseg, rowfilt,
-                       slots, slot_stride, segout);
+    if (stamps)
+        hipLaunchKernelGGL((k_deflate<DC, true>), dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles,
+                           nseg, rowfilt, slots, slot_stride, segout, stamps);
+    else
+        hipLaunchKernelGGL((k_deflate<DC, false>), dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles,
+                           nseg, rowfilt, slots, slot_stride, segout, stamps);
     return hipGetLastError();
 }
 

@@ -112,34 +112,53 @@ PBX_HD void write_tiff_header(uint8_t* p, uint32_t w, uint32_t h, uint32_t bpp, 
 // crc(A||B) = multmodp(x^(8|B|), crc(A)) ^ crc(B).
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
+// a(x) * b(x) mod P for reflected 32-bit polynomials (zlib multmodp), branch-free.
 PBX_HD uint32_t crc_multmodp(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
-        b = (b & 1) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; i--) {
+        p ^= ((a >> i) & 1u) ? b : 0u;
+        b = (b >> 1) ^ ((b & 1u) ? CRC_POLY : 0u);
     }
     return p;
 }
 
-// x^(2^k) mod P for k = 0..31 is computed by repeated squaring; x^(8n) for a byte count n.
-PBX_HD uint32_t crc_x8n(uint64_t n) {
-    // p = x^0; sq = x^8 (k=3: x^(2^3))
-    uint32_t p = 1u << 31;
-    uint32_t sq = 1u << 30;  // x^1
-    // square x^1 three times -> x^8
-    sq = crc_multmodp(sq, sq);  // x^2
-    sq = crc_multmodp(sq, sq);  // x^4
-    sq = crc_multmodp(sq, sq);  // x^8
-    while (n) {
-        if (n & 1) p = crc_multmodp(sq, p);
-        n >>= 1;
-        if (n) sq = crc_multmodp(sq, sq);
+constexpr uint32_t crc_multmodp_c(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 31; i >= 0; i--) {
+        if ((a >> i) & 1u) p ^= b;
+        b = (b >> 1) ^ ((b & 1u) ? CRC_POLY : 0u);
     }
     return p;
+}
+
+// X8.v[k] = x^(8 * 2^k) mod P: the operator that appends 2^k zero bytes.
+struct X8Table { uint32_t v[40]; };
+constexpr X8Table make_x8() {
+    X8Table t{};
+    uint32_t p = 1u << 30;  // x^1
+    p = crc_multmodp_c(p, p);
+    p = crc_multmodp_c(p, p);
+    p = crc_multmodp_c(p, p);  // x^8
+    t.v[0] = p;
+    for (int k = 1; k < 40; k++) t.v[k] = crc_multmodp_c(t.v[k - 1], t.v[k - 1]);
+    return t;
+}
+
+// x^(8n) mod P (zlib x2nmodp(n, 3)), from compile-time constants.
+PBX_HD uint32_t crc_x8n(uint64_t n) {
+    constexpr X8Table t = make_x8();
+    uint32_t p = 1u << 31;  // x^0
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        if ((n >> k) & 1u) p = crc_multmodp(t.v[k], p);
+    return p;
+}
+
+// Operator of 2^k zero bytes (k < 40), folded to a constant when k is.
+PBX_HD uint32_t crc_x8pow2(int k) {
+    constexpr X8Table t = make_x8();
+    return t.v[k];
 }
 
 PBX_HD uint32_t crc_combine_op(uint32_t crc1, uint32_t crc2, uint32_t op2) {

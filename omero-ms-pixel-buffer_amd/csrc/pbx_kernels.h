@@ -23,7 +23,7 @@ hipError_t launch_rowfilter(hipStream_t st, const TileDesc* d_tiles, uint32_t nt
 // K3-K5: fused filter + LZ77 + Huffman + bit packing, one workgroup per segment.
 hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                           uint32_t nseg, const uint8_t* rowfilt, uint8_t* slots,
-                          uint32_t slot_stride, SegOut* segout);
+                          uint32_t slot_stride, SegOut* segout, uint64_t* stamps = nullptr);
 
 // K7: container sizes, exclusive scan into offsets[0..n] (offsets[n] = total).
 hipError_t launch_sizes_scan(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,

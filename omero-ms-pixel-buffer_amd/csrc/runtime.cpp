@@ -162,7 +162,7 @@ struct pbx_batch {
     // device buffers (pool blocks)
     void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_rowfilt = nullptr,
          *d_slots = nullptr, *d_segout = nullptr, *d_sizes = nullptr, *d_offs = nullptr,
-         *d_png = nullptr;
+         *d_png = nullptr, *d_stamps = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
     hipEvent_t ev[6] = {};
     bool launched = false;
@@ -215,7 +215,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
     void** bufs[] = {&b->d_ft, &b->d_dt, &b->d_fixed, &b->d_rowfilt, &b->d_slots,
-                     &b->d_segout, &b->d_sizes, &b->d_offs, &b->d_png};
+                     &b->d_segout, &b->d_sizes, &b->d_offs, &b->d_png, &b->d_stamps};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -540,8 +540,13 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[2], st));
     HIP_TRY(launch_rowfilter(st, (const TileDesc*)b->d_dt, ndt, b->nrows_filter, (uint8_t*)b->d_rowfilt));
     HIP_TRY(hipEventRecord(b->ev[3], st));
+    // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
+    static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;
+    if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 16 * sizeof(uint64_t)))
+        return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     HIP_TRY(launch_deflate(st, (const TileDesc*)b->d_dt, ndt, b->nseg, (const uint8_t*)b->d_rowfilt,
-                           (uint8_t*)b->d_slots, slot, (SegOut*)b->d_segout));
+                           (uint8_t*)b->d_slots, slot, (SegOut*)b->d_segout,
+                           prof ? (uint64_t*)b->d_stamps : nullptr));
     HIP_TRY(hipEventRecord(b->ev[4], st));
     HIP_TRY(launch_sizes_scan(st, (const TileDesc*)b->d_dt, ndt, (const SegOut*)b->d_segout,
                               (uint64_t*)b->d_sizes, (uint64_t*)b->d_offs));
@@ -557,6 +562,19 @@ int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (b->d_stamps && b->nseg) {  // PBX_PHASE_PROFILE diagnostic: mean cycles per phase
+        std::vector<uint64_t> st((size_t)b->nseg * 16);
+        HIP_TRY(hipMemcpy(st.data(), b->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+        double acc[16] = {0};
+        for (uint32_t s = 0; s < b->nseg; s++)
+            for (int k = 1; k < 16; k++) {
+                const uint64_t a = st[(size_t)s * 16 + k - 1], c = st[(size_t)s * 16 + k];
+                if (c > a && c - a < (1ull << 40)) acc[k] += (double)(c - a);
+            }
+        fprintf(stderr, "[pbx phase cycles/segment]");
+        for (int k = 1; k < 16; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / b->nseg);
+        fprintf(stderr, "\n");
+    }
     return PBX_OK;
 }
 

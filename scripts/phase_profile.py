@@ -1,0 +1,21 @@
+"""Diagnostic: per-phase cycles of the deflate kernel (PBX_PHASE_PROFILE=1 build)."""
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "omero-ms-pixel-buffer_amd"))
+os.environ.setdefault("PBX_PHASE_PROFILE", "1")
+import pbx  # noqa: E402
+
+gen = sys.argv[1] if len(sys.argv) > 1 else "noise"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+svc = pbx.PixelsService(device=0)
+svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
+ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
+        for i in range(n)]
+for _ in range(2):
+    b = pbx.Batch(svc, ctxs)
+    b.launch()
+    b.sync()
+    s = b.stats()
+    print(gen, "deflate ms", round(s.ms_deflate, 3), "segments", s.segments, flush=True)
+    b.close()
