@@ -87,12 +87,16 @@ int pbxemu_threads(void) { return C::NT; }
 // (segments of seg_len_for(len) bytes, window, per-segment blocks, combined Adler-32).
 // rowlen: repeating-row candidate distance.  Per-segment results go to segs (may be NULL,
 // else room for pbxemu_nsegs(len)).  Returns 0, or -1 if cap is too small.
-uint32_t pbxemu_nsegs(uint64_t len) { return deflate_nsegs(len); }
+uint32_t pbxemu_nsegs(uint64_t len) {
+    uint32_t n, l;
+    deflate_split(len, n, l);
+    return n;
+}
 
 int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t* out,
                    uint64_t cap, uint64_t* out_len, SegOut* segs) {
-    const uint32_t nseg = deflate_nsegs(len);
-    const uint32_t seg_len = deflate_seg_len(len, nseg);
+    uint32_t nseg, seg_len;
+    deflate_split(len, nseg, seg_len);
     std::unique_ptr<Smem> S(new Smem());
     std::vector<uint8_t> slot(C::SEG + 256);
     MemStream src{stream};

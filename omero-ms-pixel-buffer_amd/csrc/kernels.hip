@@ -3,9 +3,10 @@
 //   k_gen_plane    synthetic planes in HBM (G_FAKE = Bio-Formats FakeReader, G_NOISE)
 //   k_extract      K1  raw + uncompressed TIFF: PixelBuffer.getTileDirect + big-endian
 //                      (TileRequestHandler.java:104-112,128; TiffWriter via :122-123)
-//   k_rowfilter    K2  per-scanline PNG filter choice (min sum |residual|), adaptive mode
-//   k_deflate      K3/K4 fused getTileDirect + PNG filter + LZ77 (LDS) + Huffman + packing,
-//                      one workgroup per 16 KiB segment (writeImage("png"), :176-199)
+//   k_filter       K1+K2 getTileDirect + big-endian + APNGWriter sign flip + PNG scanline
+//                      filter (adaptive: min sum |residual|) -> per-tile streams in HBM
+//   k_deflate      K3/K4 LZ77 (LDS hash + wave-serial greedy/lazy parse) + Huffman +
+//                      bit packing, one workgroup per 16 KiB segment (writeImage, :176-199)
 //   k_tile_sizes   K7  container size per tile  -> k_scan_offsets: exclusive scan
 //   k_assemble     K5/K6 zlib framing (Adler-32 combine), PNG chunks (CRC-32 combine,
 //                      APNGWriter layout) or deflate-TIFF header, compacted output
@@ -221,7 +222,7 @@ __device__ void ph_twoqueue_dev(uint32_t tid, DeflateSmem<C>& S) {
 // barrier into stamps[seg * 16 + phase]; no output value depends on a stamp.
 template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT) void k_deflate(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                   uint32_t nseg, const uint8_t* __restrict__ rowfilt,
+                                                   uint32_t nseg, const uint8_t* __restrict__ stream,
                                                    uint8_t* __restrict__ slots, uint32_t slot_stride,
                                                    SegOut* __restrict__ segout,
                                                    uint64_t* __restrict__ stamps) {
@@ -237,8 +238,7 @@ __global__ __launch_bounds__(C::NT) void k_deflate(const TileDesc* __restrict__ 
     if (seg >= nseg) return;
     const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
     const TileDesc d = dt[ti];
-    TileStream src;
-    src.init(d, rowfilt);
+    const WordStream src{stream + d.out_off};
     const uint32_t k = seg - d.seg_first;
     const uint64_t s = (uint64_t)k * d.seg_len;
     SegParams sp;
@@ -406,38 +406,168 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
     }
 }
 
-// ------------------------------------------------------------------ PNG row filter
-__global__ __launch_bounds__(256) void k_rowfilter(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                   uint32_t nrows, uint8_t* __restrict__ rowfilt) {
-    const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (gw >= nrows) return;
-    const uint32_t ti = upper_index(ndt, gw, [&](uint32_t i) { return dt[i].blk_first; });
-    const TileDesc d = dt[ti];
-    TileStream ts;
-    ts.init(d, nullptr);
-    const int64_t r = gw - d.blk_first;
-    const uint32_t rb = (uint32_t)d.w * d.bpp, bpp = d.bpp;
-    uint32_t sum[5] = {0, 0, 0, 0, 0};
-    for (uint32_t i = lane; i < rb; i += 64) {
-        const int cur = (int)ts.be(r, i);
-        const int left = i >= bpp ? (int)ts.be(r, i - bpp) : 0;
-        const int up = r > 0 ? (int)ts.be(r - 1, i) : 0;
-        const int ul = (r > 0 && i >= bpp) ? (int)ts.be(r - 1, i - bpp) : 0;
-        const int p = left + up - ul;
-        const int pa = abs(p - left), pb = abs(p - up), pc = abs(p - ul);
-        const int pr = (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
-        const int v[5] = {cur, cur - left, cur - up, cur - ((left + up) >> 1), cur - pr};
-#pragma unroll
-        for (int f = 0; f < 5; f++) sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)(v[f] & 0xFF));
+// ------------------------------------------------------- K1+K2: extract + PNG filter
+// One workgroup per band of FB_ROWS rows of a deflate tile: stage the band's source rows
+// (plus the row above) in LDS as big-endian bytes (16-byte loads, byte swap, APNGWriter
+// sign flip), choose each row's filter (adaptive mode: minimum sum of |signed residual|,
+// one wave per row), then write the band's stream bytes as aligned 16-byte words:
+// FB_ROWS * rowlen is a multiple of 16, so bands never share an output word.
+constexpr int FB_ROWS = 16;
+constexpr int FB_LDS = 64 * 1024;
+
+__device__ __forceinline__ uint4 flip_msb(uint4 q, int bpp) {
+    const uint32_t m = bpp == 1 ? 0x80808080u : 0x00800080u;  // MS byte of each BE sample
+    q.x ^= m; q.y ^= m; q.z ^= m; q.w ^= m;
+    return q;
+}
+
+__device__ __forceinline__ uint32_t filt_byte(int ft, uint32_t cur, uint32_t left, uint32_t up,
+                                             uint32_t ul) {
+    switch (ft) {
+    case 0: return cur;
+    case 1: return (cur - left) & 0xFF;
+    case 2: return (cur - up) & 0xFF;
+    case 3: return (cur - ((left + up) >> 1)) & 0xFF;
+    default: {
+        const int p = (int)left + (int)up - (int)ul;
+        const int pa = abs(p - (int)left), pb = abs(p - (int)up), pc = abs(p - (int)ul);
+        const uint32_t pr = (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
+        return (cur - pr) & 0xFF;
     }
+    }
+}
+
+__device__ uint32_t block_min_filter(uint32_t (&sum)[5], uint32_t* red, uint32_t lane) {
+    (void)red; (void)lane;
+    int best = 0;
+    for (int f = 1; f < 5; f++) if (sum[f] < sum[best]) best = f;
+    return (uint32_t)best;
+}
+
+__global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                uint8_t* __restrict__ stream) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const TileDesc d = dt[ti];
+    const uint32_t r0 = (b - d.blk_first) * FB_ROWS;
+    const uint32_t r1 = r0 + FB_ROWS < (uint32_t)d.h ? r0 + FB_ROWS : (uint32_t)d.h;
+    const uint32_t bpp = d.bpp, rb = (uint32_t)d.w * bpp, rowlen = d.rowlen;
+    const bool png = (d.flags & TF_PNGROWS) != 0;
+    uint8_t* out = stream + d.out_off;
+    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
+    const uint32_t rbp = ((rb + 15) & ~15u) + 16;
+    uint32_t* ftype = (uint32_t*)(sm + FB_LDS - 256);
+    const bool fast = (uint64_t)(FB_ROWS + 1) * rbp + 256 <= (uint64_t)FB_LDS &&
+                      ((((uintptr_t)src0) | (uintptr_t)d.pitch) & 15) == 0;
+    const uint32_t o0 = r0 * rowlen, o1 = r1 * rowlen;
+    if (fast) {
+        const uint32_t nq = r1 - r0 + 1, nc = (rb + 15) >> 4;
+        const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
+        for (uint32_t i = tid; i < nq * nc; i += 256) {
+            const uint32_t q = i / nc, c = i - q * nc;
+            const int64_t row = (int64_t)r0 - 1 + q;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (row >= 0 && png) {
+                v = *(const uint4*)(src0 + row * d.pitch + 16 * c);
+                if (swap) v = swap16(v, bpp);
+                if (flip) v = flip_msb(v, bpp);
+            } else if (row >= 0) {
+                v = *(const uint4*)(src0 + row * d.pitch + 16 * c);
+                if (swap) v = swap16(v, bpp);
+            }
+            *(uint4*)(sm + q * rbp + 16 * c) = v;
+        }
+        __syncthreads();
+        if (png && d.filter == 5) {
+            for (uint32_t q = 1 + wv; q < nq; q += 4) {
+                const uint8_t* L = sm + q * rbp;
+                const uint8_t* U = L - rbp;
+                uint32_t sum[5] = {0, 0, 0, 0, 0};
+                for (uint32_t i = lane; i < rb; i += 64) {
+                    const uint32_t cur = L[i], up = U[i];
+                    const uint32_t left = i >= bpp ? L[i - bpp] : 0u, ul = i >= bpp ? U[i - bpp] : 0u;
 #pragma unroll
-    for (int f = 0; f < 5; f++)
+                    for (int f = 0; f < 5; f++)
+                        sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)filt_byte(f, cur, left, up, ul));
+                }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum[f] += __shfl_xor(sum[f], off, 64);
-    if (lane == 0) {
-        int best = 0;
-        for (int f = 1; f < 5; f++) if (sum[f] < sum[best]) best = f;
-        rowfilt[d.rowfilt_off + r] = (uint8_t)best;
+                for (int f = 0; f < 5; f++)
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) sum[f] += __shfl_xor(sum[f], off, 64);
+                if (lane == 0) ftype[q - 1] = block_min_filter(sum, nullptr, 0);
+            }
+            __syncthreads();
+        }
+        for (uint32_t o = o0 + 16 * tid; o < o1; o += 16 * 256) {
+            uint32_t row = o / rowlen, col = o - row * rowlen;
+            uint32_t w4[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                uint32_t byte = 0;
+                if (o + k < o1) {
+                    const uint8_t* L = sm + (row - r0 + 1) * rbp;
+                    if (png) {
+                        const int ft = d.filter == 5 ? (int)ftype[row - r0] : d.filter;
+                        if (col == 0) {
+                            byte = (uint32_t)ft;
+                        } else {
+                            const uint32_t i = col - 1, cur = L[i];
+                            if (ft == 0) {
+                                byte = cur;
+                            } else {
+                                const uint8_t* U = L - rbp;
+                                byte = filt_byte(ft, cur, i >= bpp ? L[i - bpp] : 0u, U[i],
+                                                 i >= bpp ? U[i - bpp] : 0u);
+                            }
+                        }
+                    } else {
+                        byte = L[col];
+                    }
+                }
+                w4[k >> 2] |= byte << (8 * (k & 3));
+                if (++col == rowlen) { col = 0; row++; }
+            }
+            *(uint4*)(out + o) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+    } else {
+        // wide rows or unaligned regions: bytes straight from the plane
+        TileStream ts;
+        ts.init(d, nullptr);
+        uint32_t* red = (uint32_t*)sm;
+        if (png && d.filter == 5) {
+            for (uint32_t r = r0; r < r1; r++) {
+                if (tid < 5) red[tid] = 0;
+                __syncthreads();
+                uint32_t sum[5] = {0, 0, 0, 0, 0};
+                for (uint32_t i = tid; i < rb; i += 256) {
+                    const uint32_t cur = ts.be(r, i), up = r > 0 ? ts.be(r - 1, i) : 0u;
+                    const uint32_t left = i >= bpp ? ts.be(r, i - bpp) : 0u;
+                    const uint32_t ul = (r > 0 && i >= bpp) ? ts.be(r - 1, i - bpp) : 0u;
+                    for (int f = 0; f < 5; f++)
+                        sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)filt_byte(f, cur, left, up, ul));
+                }
+                for (int f = 0; f < 5; f++) atomicAdd(&red[f], sum[f]);
+                __syncthreads();
+                if (tid == 0) {
+                    int best = 0;
+                    for (int f = 1; f < 5; f++) if (red[f] < red[best]) best = f;
+                    ftype[r - r0] = (uint32_t)best;
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t o = o0 + tid; o < o1; o += 256) {
+            const uint32_t row = o / rowlen, col = o - row * rowlen;
+            uint32_t byte;
+            if (png) {
+                const int ft = d.filter == 5 ? (int)ftype[row - r0] : d.filter;
+                byte = col == 0 ? (uint32_t)ft : ts.filtered(ft, row, col - 1);
+            } else {
+                byte = ts.be(row, col);
+            }
+            out[o] = (uint8_t)byte;
+        }
     }
 }
 
@@ -584,24 +714,25 @@ hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
     return hipGetLastError();
 }
 
-hipError_t launch_rowfilter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                            uint32_t nrows, uint8_t* rowfilt) {
-    if (!ntiles || !nrows) return hipSuccess;
-    hipLaunchKernelGGL(k_rowfilter, dim3((nrows + 3) / 4), dim3(256), 0, st, d_tiles, ntiles, nrows,
-                       rowfilt);
+hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                         uint32_t nblocks, uint8_t* stream) {
+    if (!ntiles || !nblocks) return hipSuccess;
+    hipLaunchKernelGGL(k_filter, dim3(nblocks), dim3(256), FB_LDS, st, d_tiles, ntiles, stream);
     return hipGetLastError();
 }
 
+uint32_t filter_band_rows() { return FB_ROWS; }
+
 hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nseg,
-                          const uint8_t* rowfilt, uint8_t* slots, uint32_t slot_stride,
+                          const uint8_t* stream, uint8_t* slots, uint32_t slot_stride,
                           SegOut* segout, uint64_t* stamps) {
     if (!ntiles || !nseg) return hipSuccess;
     if (stamps)
         hipLaunchKernelGGL((k_deflate<DC, true>), dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles,
-                           nseg, rowfilt, slots, slot_stride, segout, stamps);
+                           nseg, stream, slots, slot_stride, segout, stamps);
     else
         hipLaunchKernelGGL((k_deflate<DC, false>), dim3(nseg), dim3(DC::NT), 0, st, d_tiles, ntiles,
-                           nseg, rowfilt, slots, slot_stride, segout, stamps);
+                           nseg, stream, slots, slot_stride, segout, stamps);
     return hipGetLastError();
 }
 

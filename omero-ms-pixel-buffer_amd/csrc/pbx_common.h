@@ -54,12 +54,12 @@ struct alignas(16) TileDesc {
     int32_t pixel_type;
     uint32_t rowlen;        // stream bytes per row: (png?1:0) + w*bpp
     uint64_t stream_len;    // h * rowlen
-    uint64_t out_off;       // raw/tif: byte offset in the fixed arena; deflate: unused
+    uint64_t out_off;       // raw/tif: offset in the fixed arena; deflate: offset of the stream
     uint32_t seg_first;     // deflate tiles: first segment index in the batch
     uint32_t seg_count;
     uint32_t seg_len;       // nominal segment length (the last may be shorter)
-    uint32_t rowfilt_off;   // offset of this tile's per-row filter bytes in the rowfilt buffer
-    uint32_t blk_first;     // first workgroup (extract) / first row (row filter) of this tile
+    uint32_t rowfilt_off;   // (unused)
+    uint32_t blk_first;     // first workgroup of this tile (extract / filter bands)
     uint32_t rows_per_blk;  // extract: rows handled by one workgroup
 };
 
@@ -294,6 +294,16 @@ struct TileStream {
             if (++col == rowlen) { col = 0; r++; }
         }
         return v;
+    }
+};
+
+// A stream in HBM whose words are read at 4-byte aligned offsets (segment starts and the
+// window are multiples of 16; the buffer has slack after every tile).
+struct WordStream {
+    const uint8_t* p;
+    PBX_HD uint32_t fill_word(uint64_t p0, uint32_t nb) const {
+        const uint32_t v = *(const uint32_t*)(p + p0);
+        return nb >= 4 ? v : v & ((1u << (8 * nb)) - 1u);
     }
 };
 

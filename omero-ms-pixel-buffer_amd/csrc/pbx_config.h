@@ -8,13 +8,17 @@ namespace pbx {
 // 512 threads (8 waves), 16 KiB segments with an 8 KiB look-back window, 4096-entry hash.
 using DeflateMainCfg = DeflateCfg<512, 16384, 8192, 12>;
 
-// Number of segments for a stream of `len` bytes: equal-sized segments of at most SEG.
-inline uint32_t deflate_nsegs(uint64_t len) {
-    const uint64_t seg = (uint64_t)DeflateMainCfg::SEG;
-    return len == 0 ? 1u : (uint32_t)((len + seg - 1) / seg);
-}
-inline uint32_t deflate_seg_len(uint64_t len, uint32_t nseg) {
-    return (uint32_t)((len + nseg - 1) / nseg);
+// Split of a stream of `len` bytes into segments of at most SEG bytes: an equal split
+// rounded up to 16 bytes (segment starts stay 16-byte aligned for vector loads); the
+// count is then recomputed so that the last segment is never empty.
+inline void deflate_split(uint64_t len, uint32_t& nseg, uint32_t& seg_len) {
+    const uint64_t S = (uint64_t)DeflateMainCfg::SEG;
+    if (len == 0) { nseg = 1; seg_len = 16; return; }
+    const uint64_t n0 = (len + S - 1) / S;
+    uint64_t l = ((len + n0 - 1) / n0 + 15) & ~15ull;
+    if (l > S) l = S;
+    seg_len = (uint32_t)l;
+    nseg = (uint32_t)((len + l - 1) / l);
 }
 
 }  // namespace pbx

@@ -16,13 +16,15 @@ hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                           uint32_t nblocks, uint8_t* out);
 
-// K2: per-row PNG filter choice (adaptive mode only): one wave per row.
-hipError_t launch_rowfilter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                            uint32_t nrows, uint8_t* rowfilt);
+// K1+K2: extract + byte swap + sign flip + PNG filter (or raw BE bytes for deflate-TIFF)
+// into the per-tile byte streams the deflate kernel reads.  One workgroup per band.
+hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
+                         uint32_t nblocks, uint8_t* stream);
+uint32_t filter_band_rows();
 
 // K3-K5: fused filter + LZ77 + Huffman + bit packing, one workgroup per segment.
 hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                          uint32_t nseg, const uint8_t* rowfilt, uint8_t* slots,
+                          uint32_t nseg, const uint8_t* stream, uint8_t* slots,
                           uint32_t slot_stride, SegOut* segout, uint64_t* stamps = nullptr);
 
 // K7: container sizes, exclusive scan into offsets[0..n] (offsets[n] = total).

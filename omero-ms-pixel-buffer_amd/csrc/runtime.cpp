@@ -156,11 +156,11 @@ struct pbx_batch {
     std::vector<int32_t> status, w, h;
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
-    uint32_t ext_blocks = 0, nseg = 0, nrows_filter = 0;
-    uint64_t fixed_bytes = 0, rowfilt_bytes = 0, png_cap = 0;
+    uint32_t ext_blocks = 0, nseg = 0, filt_blocks = 0;
+    uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
-    void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_rowfilt = nullptr,
+    void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_stream = nullptr,
          *d_slots = nullptr, *d_segout = nullptr, *d_sizes = nullptr, *d_offs = nullptr,
          *d_png = nullptr, *d_stamps = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
@@ -214,7 +214,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 }
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
-    void** bufs[] = {&b->d_ft, &b->d_dt, &b->d_fixed, &b->d_rowfilt, &b->d_slots,
+    void** bufs[] = {&b->d_ft, &b->d_dt, &b->d_fixed, &b->d_stream, &b->d_slots,
                      &b->d_segout, &b->d_sizes, &b->d_offs, &b->d_png, &b->d_stamps};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
@@ -482,18 +482,13 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                 d.rowlen = (uint32_t)w * bpp;
             }
             d.stream_len = (uint64_t)h * d.rowlen;
-            d.seg_count = deflate_nsegs(d.stream_len);
-            d.seg_len = deflate_seg_len(d.stream_len, d.seg_count);
+            deflate_split(d.stream_len, d.seg_count, d.seg_len);
             d.seg_first = b->nseg;
             b->nseg += d.seg_count;
-            if (d.filter == PBX_FILTER_ADAPTIVE && (d.flags & TF_PNGROWS)) {
-                d.rowfilt_off = (uint32_t)b->rowfilt_bytes;
-                b->rowfilt_bytes += (uint64_t)h;
-                d.blk_first = b->nrows_filter;
-                b->nrows_filter += (uint32_t)h;
-            } else {
-                d.blk_first = b->nrows_filter;
-            }
+            d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
+            b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
+            d.blk_first = b->filt_blocks;
+            b->filt_blocks += (uint32_t)((h + filter_band_rows() - 1) / filter_band_rows());
             b->stream_bytes += d.stream_len;
             b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
             b->dt.push_back(d);
@@ -523,7 +518,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     }
     const uint32_t slot = deflate_slot_stride();
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
-        !dget(b->d_rowfilt, b->rowfilt_bytes) || !dget(b->d_slots, (size_t)b->nseg * slot) ||
+        !dget(b->d_stream, b->stream_cap) || !dget(b->d_slots, (size_t)b->nseg * slot) ||
         !dget(b->d_segout, (size_t)b->nseg * sizeof(SegOut)) ||
         !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
         !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap))
@@ -538,13 +533,13 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
-    HIP_TRY(launch_rowfilter(st, (const TileDesc*)b->d_dt, ndt, b->nrows_filter, (uint8_t*)b->d_rowfilt));
+    HIP_TRY(launch_filter(st, (const TileDesc*)b->d_dt, ndt, b->filt_blocks, (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;
     if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 16 * sizeof(uint64_t)))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
-    HIP_TRY(launch_deflate(st, (const TileDesc*)b->d_dt, ndt, b->nseg, (const uint8_t*)b->d_rowfilt,
+    HIP_TRY(launch_deflate(st, (const TileDesc*)b->d_dt, ndt, b->nseg, (const uint8_t*)b->d_stream,
                            (uint8_t*)b->d_slots, slot, (SegOut*)b->d_segout,
                            prof ? (uint64_t*)b->d_stamps : nullptr));
     HIP_TRY(hipEventRecord(b->ev[4], st));
