@@ -168,6 +168,15 @@ int pbx_bytes_per_pixel(int32_t pixel_type);
 /* Synchronise the context's device (bench/test hook). */
 int pbx_device_synchronize(pbx_ctx* ctx);
 
+/* sizeof of the ABI structs, for bindings to check their layouts: pbx_config,
+ * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats (in that order). */
+int pbx_abi_sizes(uint64_t* sizes, int n);
+
+/* Request sharding across GPUs (one process per GPU, no collectives): the rank that
+ * owns a request, by hash of (image, z, c, t, tile column, tile row) for tile_w x tile_h
+ * tiles.  Identical in every process. */
+int pbx_shard_of(const pbx_tile_req* req, int32_t tile_w, int32_t tile_h, int32_t world);
+
 #ifdef __cplusplus
 }
 #endif

@@ -722,6 +722,24 @@ int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result
     return PBX_OK;
 }
 
+int pbx_abi_sizes(uint64_t* sizes, int n) {
+    const uint64_t v[5] = {sizeof(pbx_config), sizeof(pbx_plane_desc), sizeof(pbx_tile_req),
+                           sizeof(pbx_result), sizeof(pbx_batch_stats)};
+    if (!sizes || n < 0) return fail(PBX_E_BADARG, "null argument");
+    for (int i = 0; i < n && i < 5; i++) sizes[i] = v[i];
+    return 5;
+}
+
+int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {
+    if (!r || world <= 0 || tw <= 0 || th <= 0) return fail(PBX_E_BADARG, "bad argument"), -1;
+    uint64_t k = (uint64_t)r->image_id;
+    const uint64_t parts[5] = {(uint64_t)(uint32_t)r->z, (uint64_t)(uint32_t)r->c,
+                               (uint64_t)(uint32_t)r->t, (uint64_t)(uint32_t)(r->x / tw),
+                               (uint64_t)(uint32_t)(r->y / th)};
+    for (uint64_t p : parts) k = splitmix64(k ^ (p * 0x9E3779B97F4A7C15ull));
+    return (int)(k % (uint64_t)world);
+}
+
 int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
     if (!req) return fail(PBX_E_BADARG, "null request");
     const int st = pbx_get_tiles(ctx, req, 1, out);

@@ -87,6 +87,7 @@ EXPORTS = [
     "pbx_batch_launch", "pbx_batch_sync", "pbx_batch_fetch", "pbx_batch_destroy",
     "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
+    "pbx_abi_sizes", "pbx_shard_of",
 ]
 
 _lib = None
@@ -129,6 +130,8 @@ def lib() -> ctypes.CDLL:
     L.pbx_batch_stats_get.argtypes = [vp, vp, ctypes.POINTER(PbxBatchStats)]
     L.pbx_tile_filename.argtypes = [ctypes.POINTER(PbxTileReq), i32, i32, ctypes.c_char_p,
                                     ctypes.c_char_p, u64]
+    L.pbx_abi_sizes.argtypes = [ctypes.POINTER(u64), ctypes.c_int]
+    L.pbx_shard_of.argtypes = [ctypes.POINTER(PbxTileReq), i32, i32, i32]
     _lib = L
     return L
 
@@ -229,6 +232,20 @@ def tile_filename(ctx: TileCtx) -> str:
     lib().pbx_tile_filename(ctypes.byref(req), ctx.w, ctx.h,
                             ctx.format.encode() if ctx.format is not None else None, buf, 512)
     return buf.value.decode()
+
+
+def shard_of(ctx: TileCtx, world: int, tile_w: int = 512, tile_h: int = 512) -> int:
+    """Rank that serves this request when requests are sharded over `world` GPUs."""
+    req = ctx.to_req()
+    r = lib().pbx_shard_of(ctypes.byref(req), tile_w, tile_h, world)
+    if r < 0:
+        _check(E_BADARG)
+    return r
+
+
+def band_rows(n_rows: int, world: int, rank: int) -> Tuple[int, int]:
+    """Whole-slide split: contiguous tile-row band [lo, hi) of a rank."""
+    return (n_rows * rank) // world, (n_rows * (rank + 1)) // world
 
 
 def content_type(fmt: Optional[str]) -> str:

@@ -1,0 +1,61 @@
+"""Multi-process sharding on the CPU (gloo, world_size 2): the N>1 path of bench.py.
+
+The tile path has no exchange step: every rank serves the requests it owns and the ranks
+only meet at the barrier / max-of-times.  Checks that the shards are disjoint, cover every
+request, and that the max-over-ranks reduction the bench uses works across processes.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "omero-ms-pixel-buffer_amd"))
+    import pbx
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
+            for i in range(4096)]
+    mine = [i for i, c in enumerate(ctxs) if pbx.shard_of(c, world) == rank]
+    # every rank reports its shard; rank 0 checks the union
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    if rank == 0:
+        q.put((gathered, float(t[0])))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharding(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allidx = sorted(i for part in gathered for i in part)
+    assert allidx == list(range(4096))          # disjoint and complete
+    assert all(len(part) > 1500 for part in gathered)
+    assert tmax == float(world)
