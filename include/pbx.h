@@ -149,7 +149,10 @@ typedef struct pbx_batch_stats {
     uint64_t out_bytes;      /* total response bytes */
     uint64_t deflate_out_bytes; /* compressed payload bytes (zlib streams) */
     uint64_t segments;
-    double ms_extract, ms_filter, ms_deflate, ms_assemble, ms_total; /* HIP events, last launch */
+    /* HIP events of the last launch: extract (raw/TIFF), filter (PNG rows), deflate (LZ77 ..
+     * encode, all segments), assemble (container framing), total; then the deflate parts */
+    double ms_extract, ms_filter, ms_deflate, ms_assemble, ms_total;
+    double ms_lz77, ms_huff, ms_encode;
 } pbx_batch_stats;
 int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* out);
 

@@ -1,0 +1,96 @@
+// dev_util.h — small device helpers shared by the gfx950 kernels (wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbx {
+
+struct DevOps {
+    __device__ static void amin(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+    __device__ static void amax(uint32_t* p, uint32_t v) { atomicMax(p, v); }
+    __device__ static void add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+};
+
+// Bijective XCD-aware remap: consecutive logical ids land on the same XCD (shared L2),
+// since workgroups are dealt round-robin over the 8 XCDs.  Speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+    const uint32_t q = n / 8, r = n % 8, x = b % 8, i = b / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+// Largest i with key(i) <= v, for a non-decreasing key (uniform across the workgroup).
+template <class F>
+__device__ __forceinline__ uint32_t upper_index(uint32_t n, uint32_t v, F key) {
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (key(mid) <= v) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+// Exclusive prefix sum of arr[0..NT) in place (one element per thread); returns the total.
+template <int NT>
+__device__ uint32_t block_scan_excl_add(uint32_t* arr, uint32_t* wtot, uint32_t tid) {
+    const uint32_t v = arr[tid], lane = tid & 63, w = tid >> 6;
+    const uint32_t inc = wave_incl_add(v, lane);
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        const uint32_t x = wtot[i];
+        pre += (uint32_t)i < w ? x : 0u;
+        tot += x;
+    }
+    arr[tid] = pre + inc - v;
+    __syncthreads();
+    return tot;
+}
+
+// Exclusive prefix sum of arr[0..N) in place by ONE wave (N/64 consecutive elements per
+// lane); returns the total.
+template <int N>
+__device__ uint32_t wave_scan_excl_add(uint32_t* arr, uint32_t lane) {
+    constexpr int K = N / 64;
+    uint32_t v[K], s = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) { v[k] = arr[lane * K + k]; s += v[k]; }
+    const uint32_t inc = wave_incl_add(s, lane);
+    const uint32_t tot = __shfl(inc, 63, 64);
+    uint32_t run = inc - s;
+#pragma unroll
+    for (int k = 0; k < K; k++) { arr[lane * K + k] = run; run += v[k]; }
+    return tot;
+}
+
+__device__ __forceinline__ uint32_t bswap16x2(uint32_t v) {
+    return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu);
+}
+
+// Swap each big-endian sample of a 16-byte vector to/from little-endian.
+__device__ __forceinline__ uint4 swap16(uint4 q, int bpp) {
+    if (bpp == 2) {
+        q.x = bswap16x2(q.x); q.y = bswap16x2(q.y); q.z = bswap16x2(q.z); q.w = bswap16x2(q.w);
+    } else if (bpp == 4) {
+        q.x = __builtin_bswap32(q.x); q.y = __builtin_bswap32(q.y);
+        q.z = __builtin_bswap32(q.z); q.w = __builtin_bswap32(q.w);
+    } else if (bpp == 8) {
+        const uint32_t a = __builtin_bswap32(q.x), b = __builtin_bswap32(q.y);
+        const uint32_t c = __builtin_bswap32(q.z), d = __builtin_bswap32(q.w);
+        q.x = b; q.y = a; q.z = d; q.w = c;
+    }
+    return q;
+}
+
+}  // namespace pbx

@@ -1,10 +1,10 @@
 // emu.cpp — TEST-ONLY CPU emulation of the segment-deflate workgroup (deflate_seg.h).
 //
 // Builds libpbx_emu.so, which tests/ load to check the deflate algorithm on the CPU:
-// every phase is executed for tid = 0..NT-1 in turn, with the barriers implied between
-// phases.  The phases only communicate through commuting LDS atomics and disjoint
-// writes, so this produces bit-for-bit the bytes the HIP kernel produces; GPU tests
-// compare the two.  Never linked into libpbx.so and never used on the product path.
+// every phase of k_lz77 / k_huff / k_encode is executed for tid = 0..NT-1 (HT for k_huff)
+// in turn, with the barriers implied between phases.  The phases only communicate through
+// commuting LDS atomics and disjoint writes, so this produces bit-for-bit the bytes the
+// HIP kernels produce; GPU tests compare the two.  Never linked into libpbx.so and never used on the product path.
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -28,51 +28,96 @@ struct EmuOps {
 };
 
 using C = DeflateMainCfg;
-using Smem = DeflateSmem<C>;
 
-uint32_t scan_excl_add(uint32_t* a) {
+// One CPU struct holding every member the phases of the three kernels touch.
+struct Smem {
+    uint32_t buf[C::BUFW];
+    uint32_t head[C::HSIZE];
+    uint32_t mpos[C::NW * C::MAXMW];
+    uint16_t mdist[C::NW * C::MAXMW];
+    uint32_t w_nm[C::NW];
+    uint32_t lfreq[288], dfreq[32];
+    HuffScratch hs;
+    uint32_t lcode[288], dcode[32];
+    uint32_t hblc[2][16], hover[2], hstart[2][16], hnext[2][16];
+    uint32_t lbm[16 * 9], dbm[16];
+    HuffWork hw;
+    uint32_t rle[320], rboff[SORTN], rbm[10];
+    uint32_t hdrw[C::HDRW];
+    uint32_t misc[M_NMISC];
+    uint32_t out[C::OUTW];
+    uint32_t crc_table[256];
+    uint32_t t_a[C::NT];
+};
+
+uint32_t scan_excl_add(uint32_t* a, int n) {
     uint32_t run = 0;
-    for (int t = 0; t < C::NT; t++) { uint32_t v = a[t]; a[t] = run; run += v; }
+    for (int t = 0; t < n; t++) { uint32_t v = a[t]; a[t] = run; run += v; }
     return run;
 }
 
+// k_lz77, k_huff and k_encode of one segment, thread by thread; -2 if the encoder's bit
+// count disagrees with the Huffman step's (a broken invariant).
 template <class Src>
-void run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, SegOut* so) {
+int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, SegOut* so) {
+    // ---- k_lz77
     for (int t = 0; t < C::NT; t++) ph_fill<C>(t, S, src, sp);
+    for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, S);
     for (int t = 0; t < C::NT; t++) ph_insert<C, EmuOps>(t, S, sp);
     for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
-    for (int t = 0; t < C::NT; t++) ph_hist<C, EmuOps>(t, S, sp);
-    for (int t = 0; t < C::NT; t++) ph_keys<C, EmuOps>(t, S);
-    std::sort(S.u.hs.skey, S.u.hs.skey + SORTN);
+    uint32_t a1 = 0, a2 = 0;
+    for (int t = 0; t < C::NT; t++) {
+        uint32_t s1, s2, n;
+        ph_hist<C, EmuOps>(t, S, sp, s1, s2, n);
+        adler_combine(a1, a2, s1, s2, n);
+    }
+    // ---- k_huff (one wave)
+    for (int t = 0; t < C::HT; t++) ph_huff_init<C>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_keys<C, EmuOps>(t, S);
+    std::sort(S.hs.skey, S.hs.skey + SORTN);
     {
         std::vector<uint32_t> iw(SORTN);
         const uint32_t nl = S.misc[M_NL], nd = S.misc[M_ND];
-        const uint32_t* sk = S.u.hs.skey;
-        twoqueue_serial([&](uint32_t i) { return key_weight(sk[i]); }, nl, iw.data(), S.u.hs.rec[0]);
-        twoqueue_serial([&](uint32_t i) { return key_weight(sk[nl + i]); }, nd, iw.data(), S.u.hs.rec[1]);
+        const uint32_t* sk = S.hs.skey;
+        twoqueue_serial([&](uint32_t i) { return key_weight(sk[i]); }, nl, iw.data(), S.hs.rec[0]);
+        twoqueue_serial([&](uint32_t i) { return key_weight(sk[nl + i]); }, nd, iw.data(), S.hs.rec[1]);
     }
-    for (int t = 0; t < C::NT; t++) ph_parents<C>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_parents<C>(t, S);
     for (int r = 0; r < JUMP_ROUNDS; r++)
-        for (int t = 0; t < C::NT; t++) ph_jump<C>(t, S, r);
-    for (int t = 0; t < C::NT; t++) ph_leafdepth<C, EmuOps>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_fixblc<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_assign<C, EmuOps>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_rle_mark<C, EmuOps>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_rle_count<C>(t, S);
-    S.misc[M_NRLE] = scan_excl_add(S.u.hs.rcnt);
-    for (int t = 0; t < C::NT; t++) ph_rle_emit<C, EmuOps>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_clen<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_rle_bits<C>(t, S);
-    S.misc[M_HDRBITS] = scan_excl_add(S.rboff);
-    for (int t = 0; t < C::NT; t++) ph_choose<C>(t, S, sp);
-    for (int t = 0; t < C::NT; t++) ph_codes<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_bits<C>(t, S, sp);
-    S.misc[M_DATABITS] = scan_excl_add(S.t_a);
-    for (int t = 0; t < C::NT; t++) ph_write<C, EmuOps>(t, S, sp);
-    for (int t = 0; t < C::NT; t++) ph_store<C>(t, S, sp, slot);
-    for (int k = 0; k < C::LOGNT; k++)
-        for (int t = 0; t < C::NT; t++) ph_tree<C>(t, S, k, crc_x8pow2(C::LOG2_CRCC + k));
-    for (int t = 0; t < C::NT; t++) ph_final<C>(t, S, sp, so);
+        for (int t = 0; t < C::HT; t++) ph_jump<C>(t, S, r);
+    for (int t = 0; t < C::HT; t++) ph_leafdepth<C, EmuOps>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_fixblc<C>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_assign<C, EmuOps>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_rle_mark<C, EmuOps>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_rle_count<C>(t, S);
+    S.misc[M_NRLE] = scan_excl_add(S.hs.rcnt, SORTN);
+    for (int t = 0; t < C::HT; t++) ph_rle_emit<C, EmuOps>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_clen<C>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_rle_bits<C>(t, S);
+    S.misc[M_HDRBITS] = scan_excl_add(S.rboff, SORTN);
+    for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sp.sl, sp.last);
+    for (int t = 0; t < C::HT; t++) ph_codes<C>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, sp.last);
+    // ---- k_encode
+    for (int t = 0; t < C::NT; t++) ph_enc_init<C>(t, S, S.hdrw);
+    for (int t = 0; t < C::NT; t++) S.t_a[t] = ph_bits<C>(t, S, sp);
+    const uint32_t bitsum = scan_excl_add(S.t_a, C::NT);
+    if (S.misc[M_BTYPE] != 0 && bitsum != S.misc[M_DATABITS] - (S.lcode[256] >> 16)) return -2;
+    for (int t = 0; t < C::NT; t++) ph_write<C, EmuOps>(t, S, sp, S.t_a[t]);
+    const uint32_t nbytes = S.misc[M_NBYTES];
+    for (uint32_t j = 0; j < nbytes; j++) slot[j] = (uint8_t)out_byte(S, sp, j);
+    uint32_t raw = 0;
+    const uint32_t opc = crc_x8pow2(C::LOG2_CRCC);
+    for (int t = 0; t < C::NT; t++) raw = crc_multmodp(opc, raw) ^ ph_crc<C>(t, S, sp);
+    so->nbytes = nbytes;
+    so->crc_op = crc_x8n(nbytes);
+    so->crc = crc_from_raw(raw, so->crc_op);
+    so->adler_s1 = a1;
+    so->adler_s2 = a2;
+    so->len = sp.sl;
+    so->btype = S.misc[M_BTYPE];
+    so->bits = S.misc[M_HDRBITS] + S.misc[M_DATABITS];
+    return 0;
 }
 
 }  // namespace
@@ -86,7 +131,8 @@ int pbxemu_threads(void) { return C::NT; }
 // Deflate `len` bytes into a zlib stream exactly as the batch pipeline does for one tile
 // (segments of seg_len_for(len) bytes, window, per-segment blocks, combined Adler-32).
 // rowlen: repeating-row candidate distance.  Per-segment results go to segs (may be NULL,
-// else room for pbxemu_nsegs(len)).  Returns 0, or -1 if cap is too small.
+// else room for pbxemu_nsegs(len)).  Returns 0, -1 if cap is too small, -2 on a broken
+// invariant.
 uint32_t pbxemu_nsegs(uint64_t len) {
     uint32_t n, l;
     deflate_split(len, n, l);
@@ -115,7 +161,7 @@ int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t
         sp.last = k + 1 == nseg;
         memset(S.get(), 0xCD, sizeof(Smem));  // poison: phases must initialise what they read
         SegOut so;
-        run_segment(*S, src, sp, slot.data(), &so);
+        if (run_segment(*S, src, sp, slot.data(), &so)) return -2;
         if (o + so.nbytes > cap) return -1;
         memcpy(out + o, slot.data(), so.nbytes);
         o += so.nbytes;

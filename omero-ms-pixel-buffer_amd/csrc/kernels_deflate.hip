@@ -1,0 +1,644 @@
+// kernels_deflate.hip — gfx950 kernels of the zlib/PNG/TIFF encoder (writeImage,
+// TileRequestHandler.java:176-199), one deflate block per <= 16 KiB segment of a tile's
+// filtered stream (deflate_seg.h):
+//
+//   k_lz77        512 threads / segment: window + segment in LDS, first-occurrence hash,
+//                 wave-serial greedy/lazy parse, symbol histogram, Adler-32 partials
+//   k_huff        ONE WAVE / segment (many per CU): Huffman code lengths and canonical
+//                 codes, code-length RLE, the block header bits, the exact output size
+//   k_seg_sizes   per tile: segment byte offsets and container size -> k_scan_offsets
+//   k_encode      512 threads / segment: bit packing of every token into LDS, CRC-32, and
+//                 the bytes stored straight into the compacted output at their final place
+//   k_frame       per tile: zlib header + Adler-32 (combined), PNG chunks with the IDAT
+//                 CRC-32 combined from the segments (APNGWriter layout), or the TIFF header
+//
+// LDS / ALU / latency-bound integer work; no MFMA.  Splitting the segment's work over three
+// kernels gives each its own occupancy: k_lz77 and k_encode hold ~46-50 KB of LDS
+// (3 workgroups per CU), k_huff ~22 KB per wave, so the serial Huffman merge of many
+// segments overlaps on every CU.
+#include <hip/hip_runtime.h>
+
+#include "deflate_seg.h"
+#include "dev_util.h"
+#include "pbx_common.h"
+#include "pbx_config.h"
+#include "pbx_kernels.h"
+
+namespace pbx {
+
+using DC = DeflateMainCfg;
+
+// ------------------------------------------------------------------- LDS layouts
+template <class C>
+struct LzSmem {
+    alignas(16) uint32_t buf[C::BUFW];
+    uint32_t head[C::HSIZE];
+    uint32_t mpos[C::NW * C::MAXMW];
+    uint16_t mdist[C::NW * C::MAXMW];
+    uint32_t w_nm[C::NW];
+    uint32_t lfreq[288], dfreq[32];
+    uint32_t red[3 * C::NW];
+};
+
+template <class C>
+struct HuffSmem {
+    uint32_t lfreq[288], dfreq[32];
+    HuffScratch hs;
+    uint32_t lcode[288], dcode[32];
+    uint32_t hblc[2][16], hover[2], hstart[2][16], hnext[2][16];
+    uint32_t lbm[16 * 9], dbm[16];
+    HuffWork hw;
+    uint32_t rle[320], rboff[SORTN], rbm[10];
+    uint32_t hdrw[C::HDRW];
+    uint32_t misc[M_NMISC];
+};
+
+template <class C>
+struct EncSmem {
+    alignas(16) uint32_t buf[C::SEGW];
+    uint32_t mpos[C::NW * C::MAXMW];
+    uint16_t mdist[C::NW * C::MAXMW];
+    uint32_t w_nm[C::NW];
+    uint32_t lcode[288], dcode[32];
+    uint32_t out[C::OUTW];
+    uint32_t crc_table[256];
+    uint32_t misc[M_NMISC];
+    uint32_t t_a[C::NT];
+    uint32_t wtot[16];
+    uint32_t red[C::NW];
+};
+
+// Segment geometry from the tile descriptor.
+__device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k, uint32_t win) {
+    SegParams sp;
+    const uint64_t s = (uint64_t)k * d.seg_len;
+    sp.sl = (uint32_t)((d.stream_len - s) < d.seg_len ? (d.stream_len - s) : d.seg_len);
+    sp.wl = (uint32_t)(s < (uint64_t)win ? s : (uint64_t)win);
+    sp.base = s - sp.wl;
+    sp.rowlen = d.rowlen;
+    sp.last = (k + 1 == d.seg_count) ? 1u : 0u;
+    return sp;
+}
+
+// 16-byte loads of nb stream bytes (16-byte aligned source, slack after every tile) into
+// LDS words; bytes past nb and one extra vector are zero.
+template <int NT>
+__device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, uint32_t nb,
+                                             uint32_t tid) {
+    const uint32_t nv = (nb + 15) / 16;
+    for (uint32_t k = tid; k <= nv; k += NT) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < nv) {
+            v = *(const uint4*)(src + 16ull * k);
+            const uint32_t rem = nb - 16 * k;
+            if (rem < 16) {
+                uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int keep = (int)rem - 4 * i;
+                    w[i] = keep >= 4 ? w[i] : keep <= 0 ? 0u : w[i] & ((1u << (8 * keep)) - 1u);
+                }
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        *(uint4*)(dst + 4 * k) = v;
+    }
+}
+
+// ==================================================================== k_lz77
+// Wave-serial greedy parse of one sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).
+template <class C, class SM>
+__device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
+    const uint32_t w = tid >> 6, lane = tid & 63;
+    const uint32_t ss = w * C::SUB;
+    const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
+    uint32_t nm = 0, pos = ss;
+    while (pos < se) {
+        uint32_t L, D;
+        eval_pos<C>(S, sp, pos + lane, se, L, D);
+        const uint64_t mask = __ballot(L >= 3);
+        uint32_t o = 0;
+        while (o < 64) {
+            const uint64_t m = mask >> o;
+            if (!m) { o = 64; break; }
+            const uint32_t k = o + (uint32_t)__builtin_ctzll(m);
+            uint32_t Lk = __builtin_amdgcn_readlane(L, k);
+            const uint32_t Dk = __builtin_amdgcn_readlane(D, k);
+            if (k + 1 < 64) {
+                const uint32_t L1 = __builtin_amdgcn_readlane(L, k + 1);
+                if (L1 > Lk) { o = k + 1; continue; }  // lazy: a longer match starts next
+            }
+            const uint32_t p = pos + k;
+            const uint32_t rem = se - p;
+            const uint32_t maxlen = rem < 258 ? rem : 258;
+            if (Lk >= (uint32_t)C::CAP && Lk < maxlen) {
+                // one wave-wide compare of 4 bytes per lane extends the match past the cap
+                const uint32_t a = sp.wl + p, off = Lk + 4 * lane;
+                const uint32_t x = off < maxlen ? (lds_ld4(S, a - Dk + off) ^ lds_ld4(S, a + off)) : 0u;
+                const uint64_t mm = __ballot(off >= maxlen || x != 0);
+                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+                const uint32_t xf = __builtin_amdgcn_readlane(x, f);
+                const uint32_t of = Lk + 4 * f;
+                const uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
+                Lk = l < maxlen ? l : maxlen;
+            }
+            if (nm < (uint32_t)C::MAXMW) {
+                if (lane == 0) {
+                    S.mpos[w * C::MAXMW + nm] = p | ((Lk - 3) << 16);
+                    S.mdist[w * C::MAXMW + nm] = (uint16_t)(Dk - 1);
+                }
+                nm++;
+            }
+            o = k + Lk;
+        }
+        pos += o;
+    }
+    if (lane == 0) S.w_nm[w] = nm;
+}
+
+template <class C, bool PROF>
+__global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                uint32_t nseg, const uint8_t* __restrict__ stream,
+                                                SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
+                                                uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps) {
+    __shared__ LzSmem<C> S;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
+    uint32_t nst = 0;
+    auto stamp = [&]() {
+        if (PROF && tid == 0) stamps[(size_t)seg * 16 + nst] = __builtin_amdgcn_s_memtime();
+        nst++;
+    };
+    stamp();
+    const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
+    const TileDesc d = dt[ti];
+    const SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
+    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, tid);
+    ph_lz_init<C>(tid, S);
+    __syncthreads();
+    stamp();
+    ph_insert<C, DevOps>(tid, S, sp);
+    __syncthreads();
+    stamp();
+    ph_parse_dev<C>(tid, S, sp);
+    __syncthreads();
+    stamp();
+    uint32_t s1, s2, n;
+    ph_hist<C, DevOps>(tid, S, sp, s1, s2, n);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // Adler-32 partials: wave tree
+        const uint32_t r1 = __shfl_down(s1, off, 64), r2 = __shfl_down(s2, off, 64);
+        const uint32_t rn = __shfl_down(n, off, 64);
+        if ((lane & (2 * off - 1)) == 0 && lane + off < 64) { adler_combine(s1, s2, r1, r2, rn); n += rn; }
+    }
+    if (lane == 0) { S.red[3 * w] = s1; S.red[3 * w + 1] = s2; S.red[3 * w + 2] = n; }
+    __syncthreads();
+    stamp();
+    if (tid == 0) {
+        uint32_t a1 = S.red[0], a2 = S.red[1];
+        for (int k = 1; k < C::NW; k++) adler_combine(a1, a2, S.red[3 * k], S.red[3 * k + 1], S.red[3 * k + 2]);
+        SegInfo& g = info[seg];
+        g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
+        g.adler_s1 = a1; g.adler_s2 = a2;
+    }
+    uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
+    for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) hg[i] = i < 288 ? S.lfreq[i] : S.dfreq[i - 288];
+    uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
+    if (tid < (uint32_t)C::NW) mg[tid] = S.w_nm[tid];
+    for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
+        if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
+            mg[C::NW + i] = S.mpos[i];
+            mg[C::NW + C::NW * C::MAXMW + i] = S.mdist[i];
+        }
+    }
+    stamp();
+}
+
+// ==================================================================== k_huff
+// Ascending sort of 512 keys by one wave: 8 per lane (lane*8 + r), partners at distance
+// j >= 8 by shuffle, j < 8 inside the lane's registers.
+__device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
+    uint32_t v[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = keys[lane * 8 + r];
+#pragma unroll
+    for (uint32_t k = 2; k <= 512; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 8) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const uint32_t o = __shfl_xor(v[r], (int)(j >> 3), 64);
+                    const uint32_t e = lane * 8 + r;
+                    const bool up = (e & k) == 0, lower = (e & j) == 0;
+                    v[r] = (lower == up) ? (v[r] < o ? v[r] : o) : (v[r] < o ? o : v[r]);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    if (r & j) continue;
+                    const int p = r | (int)j;
+                    const uint32_t e = lane * 8 + r;
+                    const uint32_t a = v[r], b = v[p], lo = a < b ? a : b, hi = a < b ? b : a;
+                    if ((e & k) == 0) { v[r] = lo; v[p] = hi; } else { v[r] = hi; v[p] = lo; }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) keys[lane * 8 + r] = v[r];
+}
+
+// The serial Huffman merge of tree T on one wave.  Queues live in LDS; the wave keeps
+// 64-entry register windows over them (lane i = entry 64*block + i): the leaf read window,
+// the internal-node write and read windows, and the step-record window.  Every access is
+// one readlane or one lane select; windows move every 64 entries.  Same records as
+// twoqueue_serial in deflate_seg.h.
+template <class SM>
+__device__ void twoqueue_wave(SM& S, uint32_t T, uint32_t lane) {
+    const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
+    const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
+    const uint32_t* sk = S.hs.skey + base;
+    uint16_t* iq = S.hs.dB[T];  // internal weights (dB is free until the jump rounds)
+    uint32_t* rq = S.hs.rec[T];
+    const uint32_t INF = 0xFFFFFFFFu;
+    uint32_t lblk = 0, iwblk = 0, irblk = 0xFFFFFFFFu, rblk = 0;
+    uint32_t Wwin = lane < n ? key_weight(sk[lane]) : INF;
+    uint32_t Iw = 0, Ir = 0, Rw = 0;
+    uint32_t li = 0, qi = 0, ni = 0;
+    uint32_t lw = __builtin_amdgcn_readlane(Wwin, 0), iw = INF;
+    for (uint32_t s = 0; s + 1 < n; s++) {
+        const uint32_t rec = li | (qi << 10);
+        uint32_t cnt = 0, sum = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (lw <= iw) {
+                sum += lw; li++; cnt++;
+                if (li < n) {
+                    if ((li >> 6) != lblk) {
+                        lblk = li >> 6;
+                        const uint32_t e = lblk * 64 + lane;
+                        Wwin = e < n ? key_weight(sk[e]) : INF;
+                    }
+                    lw = __builtin_amdgcn_readlane(Wwin, li & 63);
+                } else {
+                    lw = INF;
+                }
+            } else {
+                sum += iw; qi++;
+                if (qi < ni) {
+                    if ((qi >> 6) == iwblk) {
+                        iw = __builtin_amdgcn_readlane(Iw, qi & 63);
+                    } else {
+                        if ((qi >> 6) != irblk) { irblk = qi >> 6; Ir = iq[irblk * 64 + lane]; }
+                        iw = __builtin_amdgcn_readlane(Ir, qi & 63);
+                    }
+                } else {
+                    iw = INF;
+                }
+            }
+        }
+        if ((ni >> 6) != iwblk) {  // the write window moves on: flush it
+            if (iwblk * 64 + lane < 288) iq[iwblk * 64 + lane] = Iw;
+            iwblk = ni >> 6;
+        }
+        Iw = lane == (ni & 63) ? sum : Iw;
+        if (qi == ni) iw = sum;
+        ni++;
+        if ((s >> 6) != rblk) {
+            if (rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
+            rblk = s >> 6;
+        }
+        Rw = lane == (s & 63) ? (rec | (cnt << 20)) : Rw;
+    }
+    if (n > 1 && rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
+}
+
+template <class C, bool PROF>
+__global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict__ info,
+                                             const uint32_t* __restrict__ hist,
+                                             uint32_t* __restrict__ codes,
+                                             uint64_t* __restrict__ stamps) {
+    __shared__ HuffSmem<C> S;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
+    uint32_t nst = 0;
+    auto stamp = [&]() {
+        if (PROF && tid == 0) stamps[(size_t)seg * 16 + 6 + nst] = __builtin_amdgcn_s_memtime();
+        nst++;
+    };
+    stamp();
+    const uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
+    for (uint32_t i = tid; i < HIST_WORDS; i += 64) {
+        if (i < 288) S.lfreq[i] = hg[i]; else S.dfreq[i - 288] = hg[i];
+    }
+    const uint32_t sl = info[seg].sl, last = info[seg].last;
+    ph_huff_init<C>(tid, S);
+    __syncthreads();
+    ph_keys<C, DevOps>(tid, S);
+    __syncthreads();
+    sort512_wave(S.hs.skey, tid);
+    __syncthreads();
+    stamp();
+    twoqueue_wave(S, 0, tid);
+    twoqueue_wave(S, 1, tid);
+    __syncthreads();
+    stamp();
+    ph_parents<C>(tid, S);
+    __syncthreads();
+#pragma unroll 1
+    for (int r = 0; r < JUMP_ROUNDS; r++) {
+        ph_jump<C>(tid, S, r);
+        __syncthreads();
+    }
+    ph_leafdepth<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_fixblc<C>(tid, S);
+    __syncthreads();
+    ph_assign<C, DevOps>(tid, S);
+    __syncthreads();
+    stamp();
+    ph_rle_mark<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_rle_count<C>(tid, S);
+    __syncthreads();
+    {
+        const uint32_t nr = wave_scan_excl_add<SORTN>(S.hs.rcnt, tid);
+        if (tid == 0) S.misc[M_NRLE] = nr;
+    }
+    __syncthreads();
+    ph_rle_emit<C, DevOps>(tid, S);
+    __syncthreads();
+    ph_clen<C>(tid, S);
+    __syncthreads();
+    ph_rle_bits<C>(tid, S);
+    __syncthreads();
+    {
+        const uint32_t hb = wave_scan_excl_add<SORTN>(S.rboff, tid);
+        if (tid == 0) S.misc[M_HDRBITS] = hb;
+    }
+    __syncthreads();
+    ph_choose<C>(tid, S, sl, last);
+    __syncthreads();
+    ph_codes<C>(tid, S);
+    ph_header<C, DevOps>(tid, S, last);
+    __syncthreads();
+    stamp();
+    uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
+    for (uint32_t i = tid; i < CODE_WORDS; i += 64)
+        cg[i] = i < 288 ? S.lcode[i] : i < 320 ? S.dcode[i - 288] : S.hdrw[i - 320];
+    if (tid == 0) {
+        SegInfo& g = info[seg];
+        g.btype = S.misc[M_BTYPE];
+        g.hdr_bits = S.misc[M_HDRBITS];
+        g.data_bits = S.misc[M_DATABITS];
+        g.nbytes = S.misc[M_NBYTES];
+    }
+}
+
+// ================================================================ k_seg_sizes
+__device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
+    return (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET + ZLIB_HDR_BYTES + payload + 4
+                               : PNG_IDAT_DATA_OFF + ZLIB_HDR_BYTES + payload + PNG_TAIL_BYTES;
+}
+
+__global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                   SegInfo* __restrict__ info,
+                                                   uint64_t* __restrict__ sizes) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc& d = dt[i];
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        SegInfo& g = info[d.seg_first + k];
+        g.off = off;
+        off += g.nbytes;
+    }
+    sizes[i] = container_bytes(d, off);
+}
+
+__global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restrict__ sizes, uint32_t n,
+                                                       uint64_t* __restrict__ offs) {
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t b = tid * per, e = b + per < n ? b + per : n;
+    uint64_t s = 0;
+    for (uint32_t i = b; i < e; i++) s += sizes[i];
+    part[tid] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[tid] - s;
+    for (uint32_t i = b; i < e; i++) { offs[i] = run; run += sizes[i]; }
+    if (tid == 1023) offs[n] = part[1023];
+}
+
+// ==================================================================== k_encode
+template <class SM>
+__device__ __forceinline__ uint32_t out_word(const SM& S, const SegParams& sp, uint32_t j) {
+    if (S.misc[M_BTYPE] != 0) {
+        const uint32_t w0 = S.out[j >> 2], w1 = S.out[(j >> 2) + 1], sh = (j & 3) * 8;
+        return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+    }
+    return out_byte(S, sp, j) | (out_byte(S, sp, j + 1) << 8) | (out_byte(S, sp, j + 2) << 16) |
+           (out_byte(S, sp, j + 3) << 24);
+}
+
+template <class C, bool PROF>
+__global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                  uint32_t nseg, const uint8_t* __restrict__ stream,
+                                                  SegInfo* __restrict__ info,
+                                                  const uint32_t* __restrict__ mrec,
+                                                  const uint32_t* __restrict__ codes,
+                                                  const uint64_t* __restrict__ offs,
+                                                  uint8_t* __restrict__ out,
+                                                  uint64_t* __restrict__ stamps) {
+    __shared__ EncSmem<C> S;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
+    uint32_t nst = 0;
+    auto stamp = [&]() {
+        if (PROF && tid == 0) stamps[(size_t)seg * 16 + 11 + nst] = __builtin_amdgcn_s_memtime();
+        nst++;
+    };
+    stamp();
+    const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
+    const TileDesc d = dt[ti];
+    SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
+    sp.base += sp.wl;  // the encoder holds the segment only
+    sp.wl = 0;
+    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.sl, tid);
+    const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
+    if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
+    const uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
+    for (uint32_t i = tid; i < 320; i += C::NT) {
+        if (i < 288) S.lcode[i] = cg[i]; else S.dcode[i - 288] = cg[i];
+    }
+    ph_enc_init<C>(tid, S, cg + 320);
+    const SegInfo gi = info[seg];
+    if (tid == 0) {
+        S.misc[M_BTYPE] = gi.btype; S.misc[M_HDRBITS] = gi.hdr_bits;
+        S.misc[M_DATABITS] = gi.data_bits; S.misc[M_NBYTES] = gi.nbytes;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
+        if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
+            S.mpos[i] = mg[C::NW + i];
+            S.mdist[i] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + i];
+        }
+    }
+    __syncthreads();
+    S.t_a[tid] = ph_bits<C>(tid, S, sp);
+    __syncthreads();
+    stamp();
+    const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
+    ph_write<C, DevOps>(tid, S, sp, S.t_a[tid]);
+    __syncthreads();
+    stamp();
+    // CRC-32: raw CRC of right-aligned 64-byte chunks, combined per wave by shuffles with
+    // the constant operators x^(8*64*2^k), then across the waves
+    uint32_t c = ph_crc<C>(tid, S, sp);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const uint32_t r = __shfl_down(c, 1 << k, 64);
+        c = crc_multmodp(crc_x8pow2(C::LOG2_CRCC + k), c) ^ r;
+    }
+    if (lane == 0) S.red[w] = c;
+    // bytes to their final place: unaligned head and tail bytes, aligned words between
+    const uint32_t nbytes = gi.nbytes;
+    const uint32_t zoff = (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+    uint8_t* dst = out + offs[ti] + zoff + ZLIB_HDR_BYTES + gi.off;
+    uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
+    if (head > nbytes) head = nbytes;
+    const uint32_t nwords = (nbytes - head) >> 2;
+    if (tid < head) dst[tid] = (uint8_t)out_byte(S, sp, tid);
+    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, sp, head + 4 * k);
+    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, sp, j);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t raw = S.red[0];
+        const uint32_t opw = crc_x8pow2(C::LOG2_CRCC + 6);  // one wave = 64 chunks
+        for (int k = 1; k < C::NW; k++) raw = crc_multmodp(opw, raw) ^ S.red[k];
+        const uint32_t op = crc_x8n(nbytes);
+        SegInfo& g = info[seg];
+        g.crc = crc_from_raw(raw, op);
+        g.crc_op = op;
+        g.bitsum = bitsum;
+    }
+    stamp();
+}
+
+// ===================================================================== k_frame
+__device__ uint32_t crc_bits(uint32_t c, const uint8_t* p, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        c ^= p[i];
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ CRC_POLY : c >> 1;
+    }
+    return c;
+}
+
+__device__ uint32_t put_chunk(uint8_t* o, const char* type, const uint8_t* data, uint32_t n) {
+    put_be32(o, n);
+    for (int i = 0; i < 4; i++) o[4 + i] = (uint8_t)type[i];
+    for (uint32_t i = 0; i < n; i++) o[8 + i] = data[i];
+    const uint32_t crc = crc_bits(0xFFFFFFFFu, o + 4, 4 + n) ^ 0xFFFFFFFFu;
+    put_be32(o + 8 + n, crc);
+    return 12 + n;
+}
+
+// One thread per tile: everything around the segments' bytes.
+__global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                              const SegInfo* __restrict__ info,
+                                              const uint64_t* __restrict__ offs,
+                                              uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc d = dt[i];
+    uint8_t* base = out + offs[i];
+    const bool tiff = (d.flags & TF_TIFF) != 0;
+    const uint32_t zoff = tiff ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+    uint32_t s1 = 0, s2 = 0, payload = 0;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        const SegInfo& g = info[d.seg_first + k];
+        adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.sl);
+        payload += g.nbytes;
+    }
+    const uint32_t adler = adler_final(s1, s2, d.stream_len);
+    const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;
+    base[zoff] = 0x78;      // CMF: deflate, 32 KiB window
+    base[zoff + 1] = 0x9C;  // FLG: default level (Deflater -1 == 6), check bits
+    put_be32(base + pos, adler);
+    if (tiff) {
+        write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8,
+                          ZLIB_HDR_BYTES + payload + 4);
+        return;
+    }
+    const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+    for (int j = 0; j < 8; j++) base[j] = sig[j];
+    uint32_t o = 8;
+    uint8_t buf[26];
+    put_be32(buf, d.w); put_be32(buf + 4, d.h);
+    buf[8] = (uint8_t)(8 * d.bpp); buf[9] = 0; buf[10] = 0; buf[11] = 0; buf[12] = 0;
+    o += put_chunk(base + o, "IHDR", buf, 13);
+    put_be32(buf, 1); put_be32(buf + 4, 0);  // acTL: 1 frame, 0 plays
+    o += put_chunk(base + o, "acTL", buf, 8);
+    for (int j = 0; j < 26; j++) buf[j] = 0;  // fcTL: seq 0, w, h, offsets 0, delay 0/0, ops 0
+    put_be32(buf + 4, d.w); put_be32(buf + 8, d.h);
+    o += put_chunk(base + o, "fcTL", buf, 26);
+    // IDAT: length, type, zlib stream; CRC over type + data combined from segment CRCs
+    put_be32(base + o, ZLIB_HDR_BYTES + payload + 4);
+    base[o + 4] = 'I'; base[o + 5] = 'D'; base[o + 6] = 'A'; base[o + 7] = 'T';
+    uint32_t c = crc_bits(0xFFFFFFFFu, base + o + 4, 4 + ZLIB_HDR_BYTES) ^ 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < d.seg_count; k++) {
+        const SegInfo& g = info[d.seg_first + k];
+        c = crc_combine_op(c, g.crc, g.crc_op);
+    }
+    c = crc_bits(c ^ 0xFFFFFFFFu, base + pos, 4) ^ 0xFFFFFFFFu;
+    put_be32(base + pos + 4, c);
+    put_chunk(base + pos + 8, "IEND", nullptr, 0);
+}
+
+// ================================================================== launchers
+size_t deflate_lds_bytes(int kernel) {
+    return kernel == 0 ? sizeof(LzSmem<DC>) : kernel == 1 ? sizeof(HuffSmem<DC>) : sizeof(EncSmem<DC>);
+}
+
+hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev) {
+    if (!a.ntiles || !a.nseg) return hipSuccess;
+    const bool prof = a.stamps != nullptr;
+    if (prof)
+        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
+    else
+        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
+    if (ev) (void)hipEventRecord(ev[0], st);
+    if (prof)
+        hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nseg), dim3(64), 0, st, a.nseg, a.info, a.hist,
+                           a.codes, a.stamps);
+    else
+        hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nseg), dim3(64), 0, st, a.nseg, a.info, a.hist,
+                           a.codes, a.stamps);
+    if (ev) (void)hipEventRecord(ev[1], st);
+    hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
+                       a.info, a.sizes);
+    hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
+    if (ev) (void)hipEventRecord(ev[2], st);
+    if (prof)
+        hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+                           a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
+    else
+        hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+                           a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
+    if (ev) (void)hipEventRecord(ev[3], st);
+    hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
+                       a.offs, a.out);
+    return hipGetLastError();
+}
+
+}  // namespace pbx

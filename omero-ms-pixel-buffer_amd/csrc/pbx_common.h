@@ -75,6 +75,18 @@ struct SegOut {
     uint32_t bits;          // bits of the block (diagnostics)
 };
 
+// Per-segment record of the three deflate kernels (64 bytes, in HBM).
+struct SegInfo {
+    uint32_t sl, last, wl, rowlen;       // k_lz77: geometry
+    uint32_t adler_s1, adler_s2;         // k_lz77: Adler-32 partial sums of the sl bytes
+    uint32_t btype, hdr_bits;            // k_huff: block type, header bits
+    uint32_t data_bits, nbytes;          // k_huff: data bits (EOB included), output bytes
+    uint32_t crc, crc_op;                // k_encode: CRC-32 of the output bytes, x^(8*nbytes)
+    uint32_t off;                        // k_seg_sizes: byte offset in the tile's payload
+    uint32_t bitsum;                     // k_encode: token bits (diagnostics)
+    uint32_t pad[2];
+};
+
 PBX_HD uint32_t ceil_div_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
 PBX_HD void put_be32(uint8_t* p, uint32_t v) {

@@ -8,6 +8,12 @@ namespace pbx {
 // 512 threads (8 waves), 16 KiB segments with an 8 KiB look-back window, 4096-entry hash.
 using DeflateMainCfg = DeflateCfg<512, 16384, 8192, 12>;
 
+// Per-segment HBM records between the deflate kernels (32-bit words).
+constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram
+constexpr uint32_t MREC_WORDS =       // per-wave match counts, positions|lengths, distances
+    (DeflateMainCfg::NW + 2 * DeflateMainCfg::NW * DeflateMainCfg::MAXMW + 63) & ~63u;
+constexpr uint32_t CODE_WORDS = 320 + DeflateMainCfg::HDRW;  // codes + block header bits
+
 // Split of a stream of `len` bytes into segments of at most SEG bytes: an equal split
 // rounded up to 16 bytes (segment starts stay 16-byte aligned for vector loads); the
 // count is then recomputed so that the last segment is never empty.

@@ -1,4 +1,5 @@
-// pbx_kernels.h — host-side launchers of the gfx950 kernels (kernels.hip).
+// pbx_kernels.h — host-side launchers of the gfx950 kernels (kernels_io.hip,
+// kernels_deflate.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,27 +18,28 @@ hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
                           uint32_t nblocks, uint8_t* out);
 
 // K1+K2: extract + byte swap + sign flip + PNG filter (or raw BE bytes for deflate-TIFF)
-// into the per-tile byte streams the deflate kernel reads.  One workgroup per band.
+// into the per-tile byte streams the deflate kernels read.  One workgroup per band.
 hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                          uint32_t nblocks, uint8_t* stream);
 uint32_t filter_band_rows();
 
-// K3-K5: fused filter + LZ77 + Huffman + bit packing, one workgroup per segment.
-hipError_t launch_deflate(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                          uint32_t nseg, const uint8_t* stream, uint8_t* slots,
-                          uint32_t slot_stride, SegOut* segout, uint64_t* stamps = nullptr);
-
-// K7: container sizes, exclusive scan into offsets[0..n] (offsets[n] = total).
-hipError_t launch_sizes_scan(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                             const SegOut* segout, uint64_t* sizes, uint64_t* offsets);
-
-// K5/K6: PNG (APNGWriter layout) or deflate-TIFF container, compacted at offsets[i].
-hipError_t launch_assemble(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                           const SegOut* segout, const uint8_t* slots, uint32_t slot_stride,
-                           const uint64_t* offsets, uint8_t* out);
-
-uint32_t deflate_slot_stride();
-uint32_t deflate_threads();
-size_t deflate_lds_bytes();
+// K3-K6: deflate of every tile's stream into its compacted container.
+struct DeflateLaunch {
+    const TileDesc* tiles;  // deflate tiles (seg_first / seg_count / out_off = stream offset)
+    uint32_t ntiles, nseg;
+    const uint8_t* stream;  // filtered streams (16-byte aligned per tile, slack after)
+    SegInfo* info;          // [nseg]
+    uint32_t* hist;         // [nseg * HIST_WORDS]
+    uint32_t* mrec;         // [nseg * MREC_WORDS]
+    uint32_t* codes;        // [nseg * CODE_WORDS]
+    uint64_t* sizes;        // [ntiles] container bytes
+    uint64_t* offs;         // [ntiles + 1] exclusive scan of sizes (offs[ntiles] = total)
+    uint8_t* out;           // compacted containers
+    uint64_t* stamps;       // [nseg * 16] phase clocks (diagnostics) or nullptr
+};
+// k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.  If ev is given,
+// ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.
+hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr);
+size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
 
 }  // namespace pbx

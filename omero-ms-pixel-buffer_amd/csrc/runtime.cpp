@@ -161,10 +161,11 @@ struct pbx_batch {
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
     void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_stream = nullptr,
-         *d_slots = nullptr, *d_segout = nullptr, *d_sizes = nullptr, *d_offs = nullptr,
-         *d_png = nullptr, *d_stamps = nullptr;
+         *d_info = nullptr, *d_hist = nullptr, *d_mrec = nullptr, *d_codes = nullptr,
+         *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
-    hipEvent_t ev[6] = {};
+    // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
+    hipEvent_t ev[9] = {};
     bool launched = false;
     std::vector<uint64_t> h_offs;
 };
@@ -214,8 +215,8 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 }
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
-    void** bufs[] = {&b->d_ft, &b->d_dt, &b->d_fixed, &b->d_stream, &b->d_slots,
-                     &b->d_segout, &b->d_sizes, &b->d_offs, &b->d_png, &b->d_stamps};
+    void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
+                     &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -516,10 +517,11 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
         if (nft) memcpy(b->h_desc, b->ft.data(), ft_bytes);
         if (ndt) memcpy((uint8_t*)b->h_desc + ft_bytes, b->dt.data(), dt_bytes);
     }
-    const uint32_t slot = deflate_slot_stride();
+    const size_t ns = b->nseg;
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
-        !dget(b->d_stream, b->stream_cap) || !dget(b->d_slots, (size_t)b->nseg * slot) ||
-        !dget(b->d_segout, (size_t)b->nseg * sizeof(SegOut)) ||
+        !dget(b->d_stream, b->stream_cap) || !dget(b->d_info, ns * sizeof(SegInfo)) ||
+        !dget(b->d_hist, ns * HIST_WORDS * 4) || !dget(b->d_mrec, ns * MREC_WORDS * 4) ||
+        !dget(b->d_codes, ns * CODE_WORDS * 4) ||
         !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
         !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
@@ -539,16 +541,25 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;
     if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 16 * sizeof(uint64_t)))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
-    HIP_TRY(launch_deflate(st, (const TileDesc*)b->d_dt, ndt, b->nseg, (const uint8_t*)b->d_stream,
-                           (uint8_t*)b->d_slots, slot, (SegOut*)b->d_segout,
-                           prof ? (uint64_t*)b->d_stamps : nullptr));
-    HIP_TRY(hipEventRecord(b->ev[4], st));
-    HIP_TRY(launch_sizes_scan(st, (const TileDesc*)b->d_dt, ndt, (const SegOut*)b->d_segout,
-                              (uint64_t*)b->d_sizes, (uint64_t*)b->d_offs));
-    HIP_TRY(launch_assemble(st, (const TileDesc*)b->d_dt, ndt, (const SegOut*)b->d_segout,
-                            (const uint8_t*)b->d_slots, slot, (const uint64_t*)b->d_offs,
-                            (uint8_t*)b->d_png));
-    HIP_TRY(hipEventRecord(b->ev[5], st));
+    DeflateLaunch a;
+    a.tiles = (const TileDesc*)b->d_dt;
+    a.ntiles = ndt;
+    a.nseg = b->nseg;
+    a.stream = (const uint8_t*)b->d_stream;
+    a.info = (SegInfo*)b->d_info;
+    a.hist = (uint32_t*)b->d_hist;
+    a.mrec = (uint32_t*)b->d_mrec;
+    a.codes = (uint32_t*)b->d_codes;
+    a.sizes = (uint64_t*)b->d_sizes;
+    a.offs = (uint64_t*)b->d_offs;
+    a.out = (uint8_t*)b->d_png;
+    a.stamps = prof ? (uint64_t*)b->d_stamps : nullptr;
+    if (ndt) {
+        HIP_TRY(launch_deflate(st, a, b->ev + 4));
+    } else {
+        for (int k = 4; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
+    }
+    HIP_TRY(hipEventRecord(b->ev[8], st));
     b->launched = true;
     return PBX_OK;
 }
@@ -562,12 +573,14 @@ int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
         HIP_TRY(hipMemcpy(st.data(), b->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
         double acc[16] = {0};
         for (uint32_t s = 0; s < b->nseg; s++)
-            for (int k = 1; k < 16; k++) {
+            for (int k = 1; k < 15; k++) {
+                if (k == 6 || k == 11) continue;  // first stamp of k_huff / k_encode
                 const uint64_t a = st[(size_t)s * 16 + k - 1], c = st[(size_t)s * 16 + k];
                 if (c > a && c - a < (1ull << 40)) acc[k] += (double)(c - a);
             }
         fprintf(stderr, "[pbx phase cycles/segment]");
-        for (int k = 1; k < 16; k++) fprintf(stderr, " %d:%.0f", k, acc[k] / b->nseg);
+        for (int k = 1; k < 15; k++)
+            if (k != 6 && k != 11) fprintf(stderr, " %d:%.0f", k, acc[k] / b->nseg);
         fprintf(stderr, "\n");
     }
     return PBX_OK;
@@ -589,13 +602,17 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
     s->segments = b->nseg;
     if (b->launched) {
         if (ensure_device(ctx)) return PBX_E_INTERNAL;
-        HIP_TRY(hipEventSynchronize(b->ev[5]));
-        float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); s->ms_extract = ms;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev[2], b->ev[3])); s->ms_filter = ms;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev[3], b->ev[4])); s->ms_deflate = ms;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev[4], b->ev[5])); s->ms_assemble = ms;
-        HIP_TRY(hipEventElapsedTime(&ms, b->ev[0], b->ev[5])); s->ms_total = ms;
+        HIP_TRY(hipEventSynchronize(b->ev[8]));
+        auto el = [&](int i, int j, double& out) -> int {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, b->ev[i], b->ev[j]));
+            out = ms;
+            return PBX_OK;
+        };
+        if (el(1, 2, s->ms_extract) || el(2, 3, s->ms_filter) || el(3, 7, s->ms_deflate) ||
+            el(7, 8, s->ms_assemble) || el(0, 8, s->ms_total) || el(3, 4, s->ms_lz77) ||
+            el(4, 5, s->ms_huff) || el(6, 7, s->ms_encode))
+            return PBX_E_INTERNAL;
         const uint32_t ndt = (uint32_t)b->dt.size();
         if (ndt) {
             std::vector<uint64_t> offs(ndt + 1);

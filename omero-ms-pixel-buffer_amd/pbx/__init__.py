@@ -76,7 +76,8 @@ class PbxBatchStats(ctypes.Structure):
                 ("tiles", "ok_tiles", "png_tiles", "raw_tiles", "tif_tiles", "in_bytes",
                  "stream_bytes", "out_bytes", "deflate_out_bytes", "segments")] + \
                [(n, ctypes.c_double) for n in
-                ("ms_extract", "ms_filter", "ms_deflate", "ms_assemble", "ms_total")]
+                ("ms_extract", "ms_filter", "ms_deflate", "ms_assemble", "ms_total",
+                  "ms_lz77", "ms_huff", "ms_encode")]
 
 
 # Every symbol include/pbx.h declares (tests check the library exports all of them).

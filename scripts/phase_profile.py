@@ -17,5 +17,7 @@ for _ in range(2):
     b.launch()
     b.sync()
     s = b.stats()
-    print(gen, "deflate ms", round(s.ms_deflate, 3), "segments", s.segments, flush=True)
+    print(gen, "deflate ms", round(s.ms_deflate, 3), "lz77", round(s.ms_lz77, 3), "huff",
+          round(s.ms_huff, 3), "encode", round(s.ms_encode, 3), "frame", round(s.ms_assemble, 3),
+          "segments", s.segments, "out", s.deflate_out_bytes, flush=True)
     b.close()
