@@ -180,6 +180,15 @@ int pbx_abi_sizes(uint64_t* sizes, int n);
  * tiles.  Identical in every process. */
 int pbx_shard_of(const pbx_tile_req* req, int32_t tile_w, int32_t tile_h, int32_t world);
 
+/* Test hook: the Huffman stage of the deflate pipeline (k_huff) alone, on given symbol
+ * histograms.  hist: nseg x 320 counts (288 literal/length, 32 distance); sl_last: nseg x 2
+ * (segment bytes, final-segment flag).  Out: codes nseg x 480 (288 literal/length and 32
+ * distance codes as bit-reversed code | length << 16, then 160 words of block header bits)
+ * and info nseg x 4 (block type, header bits, data bits, output bytes).  Used by tests/ to
+ * compare the GPU stage with the CPU emulator on adversarial histograms. */
+int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last, uint32_t nseg,
+                     uint32_t* codes, uint32_t* info);
+
 #ifdef __cplusplus
 }
 #endif

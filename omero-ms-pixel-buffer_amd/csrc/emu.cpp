@@ -56,22 +56,8 @@ uint32_t scan_excl_add(uint32_t* a, int n) {
     return run;
 }
 
-// k_lz77, k_huff and k_encode of one segment, thread by thread; -2 if the encoder's bit
-// count disagrees with the Huffman step's (a broken invariant).
-template <class Src>
-int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, SegOut* so) {
-    // ---- k_lz77
-    for (int t = 0; t < C::NT; t++) ph_fill<C>(t, S, src, sp);
-    for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_insert<C, EmuOps>(t, S, sp);
-    for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
-    uint32_t a1 = 0, a2 = 0;
-    for (int t = 0; t < C::NT; t++) {
-        uint32_t s1, s2, n;
-        ph_hist<C, EmuOps>(t, S, sp, s1, s2, n);
-        adler_combine(a1, a2, s1, s2, n);
-    }
-    // ---- k_huff (one wave)
+// k_huff (one wave of HT threads): needs lfreq / dfreq.
+void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_huff_init<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_keys<C, EmuOps>(t, S);
     std::sort(S.hs.skey, S.hs.skey + SORTN);
@@ -95,9 +81,27 @@ int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, Seg
     for (int t = 0; t < C::HT; t++) ph_clen<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_bits<C>(t, S);
     S.misc[M_HDRBITS] = scan_excl_add(S.rboff, SORTN);
-    for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sp.sl, sp.last);
+    for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sl, last);
     for (int t = 0; t < C::HT; t++) ph_codes<C>(t, S);
-    for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, sp.last);
+    for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, last);
+}
+
+// k_lz77, k_huff and k_encode of one segment, thread by thread; -2 if the encoder's bit
+// count disagrees with the Huffman step's (a broken invariant).
+template <class Src>
+int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, SegOut* so) {
+    // ---- k_lz77
+    for (int t = 0; t < C::NT; t++) ph_fill<C>(t, S, src, sp);
+    for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, S);
+    for (int t = 0; t < C::NT; t++) ph_insert<C, EmuOps>(t, S, sp);
+    for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
+    uint32_t a1 = 0, a2 = 0;
+    for (int t = 0; t < C::NT; t++) {
+        uint32_t s1, s2, n;
+        ph_hist<C, EmuOps>(t, S, sp, s1, s2, n);
+        adler_combine(a1, a2, s1, s2, n);
+    }
+    run_huff(S, sp.sl, sp.last);
     // ---- k_encode
     for (int t = 0; t < C::NT; t++) ph_enc_init<C>(t, S, S.hdrw);
     for (int t = 0; t < C::NT; t++) S.t_a[t] = ph_bits<C>(t, S, sp);
@@ -175,6 +179,24 @@ int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t
     out[o++] = (uint8_t)(ad >> 8);
     out[o++] = (uint8_t)ad;
     *out_len = o;
+    return 0;
+}
+
+// The Huffman stage alone on a given histogram (288 + 32 counts): codes 480 words as
+// pbx_test_huffman returns them, info = block type, header bits, data bits, output bytes.
+int pbxemu_huffman(const uint32_t* hist, uint32_t sl, uint32_t last, uint32_t* codes, uint32_t* info) {
+    std::unique_ptr<Smem> S(new Smem());
+    memset(S.get(), 0xCD, sizeof(Smem));
+    for (int i = 0; i < 288; i++) S->lfreq[i] = hist[i];
+    for (int i = 0; i < 32; i++) S->dfreq[i] = hist[288 + i];
+    run_huff(*S, sl, last);
+    for (int i = 0; i < 288; i++) codes[i] = S->lcode[i];
+    for (int i = 0; i < 32; i++) codes[288 + i] = S->dcode[i];
+    for (int i = 0; i < C::HDRW; i++) codes[320 + i] = S->hdrw[i];
+    info[0] = S->misc[M_BTYPE];
+    info[1] = S->misc[M_HDRBITS];
+    info[2] = S->misc[M_DATABITS];
+    info[3] = S->misc[M_NBYTES];
     return 0;
 }
 

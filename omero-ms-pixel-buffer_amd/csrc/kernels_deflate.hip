@@ -27,6 +27,7 @@
 namespace pbx {
 
 using DC = DeflateMainCfg;
+constexpr uint32_t STAMP_STRIDE = 32;  // diagnostics: k_lz77 0.., k_huff 8.., k_encode 24..
 
 // ------------------------------------------------------------------- LDS layouts
 template <class C>
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
     uint32_t nst = 0;
     auto stamp = [&]() {
-        if (PROF && tid == 0) stamps[(size_t)seg * 16 + nst] = __builtin_amdgcn_s_memtime();
+        if (PROF && tid == 0) stamps[(size_t)seg * STAMP_STRIDE + nst] = __builtin_amdgcn_s_memtime();
         nst++;
     };
     stamp();
@@ -249,69 +250,249 @@ __device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
     for (int r = 0; r < 8; r++) keys[lane * 8 + r] = v[r];
 }
 
-// The serial Huffman merge of tree T on one wave.  Queues live in LDS; the wave keeps
-// 64-entry register windows over them (lane i = entry 64*block + i): the leaf read window,
-// the internal-node write and read windows, and the step-record window.  Every access is
-// one readlane or one lane select; windows move every 64 entries.  Same records as
-// twoqueue_serial in deflate_seg.h.
+// The Huffman merge of tree T on one wave, in rounds.  Internal nodes are created in
+// non-decreasing weight order, so once node ni-1 (weight W) exists every node still to come
+// weighs >= W: the remaining leaves of weight <= W and the internal nodes not yet consumed
+// form a fixed prefix of the merged sequence (leaves first on ties), and its consecutive
+// pairs are the next internal nodes, all built at once.  An odd last element waits for the
+// next round; a lone element pairs with the next leaf.  About 16 rounds replace the ~285
+// steps of the serial merge and give exactly its records (twoqueue_serial in deflate_seg.h,
+// which the emulator runs): step s = li0 | qi0 << 10 | cnt << 20.
 template <class SM>
-__device__ void twoqueue_wave(SM& S, uint32_t T, uint32_t lane) {
+__device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
     const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
     const uint32_t* sk = S.hs.skey + base;
-    uint16_t* iq = S.hs.dB[T];  // internal weights (dB is free until the jump rounds)
+    uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the jump rounds)
+    uint16_t* M = &S.hs.aB[0][0];     // merged prefix: leaf index | 0x8000, or internal index
     uint32_t* rq = S.hs.rec[T];
-    const uint32_t INF = 0xFFFFFFFFu;
-    uint32_t lblk = 0, iwblk = 0, irblk = 0xFFFFFFFFu, rblk = 0;
-    uint32_t Wwin = lane < n ? key_weight(sk[lane]) : INF;
-    uint32_t Iw = 0, Ir = 0, Rw = 0;
-    uint32_t li = 0, qi = 0, ni = 0;
-    uint32_t lw = __builtin_amdgcn_readlane(Wwin, 0), iw = INF;
-    for (uint32_t s = 0; s + 1 < n; s++) {
-        const uint32_t rec = li | (qi << 10);
-        uint32_t cnt = 0, sum = 0;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (lw <= iw) {
-                sum += lw; li++; cnt++;
-                if (li < n) {
-                    if ((li >> 6) != lblk) {
-                        lblk = li >> 6;
-                        const uint32_t e = lblk * 64 + lane;
-                        Wwin = e < n ? key_weight(sk[e]) : INF;
-                    }
-                    lw = __builtin_amdgcn_readlane(Wwin, li & 63);
-                } else {
-                    lw = INF;
-                }
-            } else {
-                sum += iw; qi++;
-                if (qi < ni) {
-                    if ((qi >> 6) == iwblk) {
-                        iw = __builtin_amdgcn_readlane(Iw, qi & 63);
-                    } else {
-                        if ((qi >> 6) != irblk) { irblk = qi >> 6; Ir = iq[irblk * 64 + lane]; }
-                        iw = __builtin_amdgcn_readlane(Ir, qi & 63);
-                    }
-                } else {
-                    iw = INF;
-                }
-            }
-        }
-        if ((ni >> 6) != iwblk) {  // the write window moves on: flush it
-            if (iwblk * 64 + lane < 288) iq[iwblk * 64 + lane] = Iw;
-            iwblk = ni >> 6;
-        }
-        Iw = lane == (ni & 63) ? sum : Iw;
-        if (qi == ni) iw = sum;
-        ni++;
-        if ((s >> 6) != rblk) {
-            if (rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
-            rblk = s >> 6;
-        }
-        Rw = lane == (s & 63) ? (rec | (cnt << 20)) : Rw;
+    if (n < 2) return;
+    if (lane == 0) {
+        iq[0] = (uint16_t)(key_weight(sk[0]) + key_weight(sk[1]));
+        rq[0] = 2u << 20;
     }
-    if (n > 1 && rblk * 64 + lane < 288) rq[rblk * 64 + lane] = Rw;
+    uint32_t li = 2, qi = 0, ni = 1;
+    __syncthreads();
+    while (ni + 1 < n) {
+        const uint32_t W = iq[ni - 1];
+        uint32_t a = 0;
+        for (uint32_t c = li; c < n; c += 64) {  // leaves are sorted: count those <= W
+            const uint32_t i = c + lane;
+            const uint64_t m = __ballot(i < n && key_weight(sk[i]) <= W);
+            a += (uint32_t)__builtin_popcountll(m);
+            if (~m) break;
+        }
+        a = __builtin_amdgcn_readfirstlane(a);
+        const uint32_t b = ni - qi, P = a + b;
+        if (P == 1) {  // the lone internal node qi pairs with the next leaf
+            if (lane == 0) {
+                iq[ni] = (uint16_t)(iq[qi] + key_weight(sk[li]));
+                rq[ni] = li | (qi << 10) | (1u << 20);
+            }
+            li++; qi++; ni++;
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t e = lane; e < a; e += 64) {  // leaf li+e: after internal nodes < it
+            const uint32_t w = key_weight(sk[li + e]);
+            uint32_t lo = qi, hi = ni;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (iq[mid] < w) lo = mid + 1; else hi = mid;
+            }
+            M[e + lo - qi] = (uint16_t)((li + e) | 0x8000u);
+        }
+        for (uint32_t e = lane; e < b; e += 64) {  // internal qi+e: after leaves <= it
+            const uint32_t w = iq[qi + e];
+            uint32_t lo = li, hi = li + a;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (key_weight(sk[mid]) <= w) lo = mid + 1; else hi = mid;
+            }
+            M[e + lo - li] = (uint16_t)(qi + e);
+        }
+        __syncthreads();
+        const uint32_t m = P >> 1;
+        // leaves among the first p merged elements, from the element at p
+        auto leaves_before = [&](uint32_t p, uint32_t x) -> uint32_t {
+            return (x & 0x8000u) ? (x & 0x7FFFu) - li : p - (x - qi);
+        };
+        for (uint32_t k = lane; k < m; k += 64) {
+            const uint32_t x0 = M[2 * k], x1 = M[2 * k + 1];
+            const uint32_t w0 = (x0 & 0x8000u) ? key_weight(sk[x0 & 0x7FFFu]) : iq[x0];
+            const uint32_t w1 = (x1 & 0x8000u) ? key_weight(sk[x1 & 0x7FFFu]) : iq[x1];
+            const uint32_t lb = leaves_before(2 * k, x0);
+            const uint32_t cnt = (x0 >> 15) + (x1 >> 15);
+            iq[ni + k] = (uint16_t)(w0 + w1);
+            rq[ni + k] = (li + lb) | ((qi + 2 * k - lb) << 10) | (cnt << 20);
+        }
+        uint32_t lb = a;
+        if (2 * m < P) lb = leaves_before(2 * m, M[2 * m]);
+        lb = __builtin_amdgcn_readfirstlane(lb);
+        li += lb;
+        qi += 2 * m - lb;
+        ni += m;
+        __syncthreads();
+    }
+}
+
+// Code lengths of both trees from the repaired bit-length counts (ph_assign's result):
+// leaf j of a tree gets the length L with end(L+1) <= j < end(L), end(L) = leaves of
+// length >= L.  Sums and maxima by wave reductions instead of same-address LDS atomics.
+template <class SM>
+__device__ void assign_wave(SM& S, uint32_t lane) {
+    uint32_t e0[16], e1[16];
+#pragma unroll
+    for (int L = 1; L < 16; L++) {
+        e0[L] = S.hstart[0][L] + S.hblc[0][L];
+        e1[L] = S.hstart[1][L] + S.hblc[1][L];
+    }
+    const uint32_t nl = S.misc[M_NL], nd = S.misc[M_ND];
+    uint32_t dyn = 0, fix = 0, hlit = 257, hdist = 1;
+#pragma unroll
+    for (int it = 0; it < 5; it++) {
+        const uint32_t i = lane + 64 * it;
+        const uint32_t T = i >= 288 ? 1u : 0u, j = T ? i - 288 : i;
+        if (j >= (T ? nd : nl)) continue;
+        const uint32_t key = S.hs.skey[(T ? nl : 0u) + j], sym = key & 0x1FF;
+        uint32_t L = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) L += j < (T ? e1[l] : e0[l]) ? 1u : 0u;
+        if (T == 0) {
+            S.lcode[sym] = L << 16;
+            atomicOr(&S.lbm[L * 9 + (sym >> 5)], 1u << (sym & 31));
+            const uint32_t f = S.lfreq[sym];
+            const uint32_t eb = sym >= 257 ? len_sym_ebits(sym) : 0;
+            dyn += f * (L + eb);
+            fix += f * (fixed_lit_len(sym) + eb);
+            hlit = sym + 1 > hlit ? sym + 1 : hlit;
+        } else {
+            S.dcode[sym] = L << 16;
+            atomicOr(&S.dbm[L], 1u << sym);
+            const uint32_t f = S.dfreq[sym];
+            const uint32_t eb = dist_sym_ebits(sym);
+            dyn += f * (L + eb);
+            fix += f * (5 + eb);
+            hdist = sym + 1 > hdist ? sym + 1 : hdist;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        dyn += __shfl_xor(dyn, off, 64);
+        fix += __shfl_xor(fix, off, 64);
+        const uint32_t h1 = __shfl_xor(hlit, off, 64), h2 = __shfl_xor(hdist, off, 64);
+        hlit = h1 > hlit ? h1 : hlit;
+        hdist = h2 > hdist ? h2 : hdist;
+    }
+    if (lane == 0) {
+        S.misc[M_DYNBITS] = dyn; S.misc[M_FIXBITS] = fix;
+        S.misc[M_HLIT] = hlit; S.misc[M_HDIST] = hdist;
+    }
+}
+
+// The 19-symbol code-length code on one wave (lane s = symbol s); same result as ph_clen:
+// stable (freq, symbol) order, serial two-queue merge on lane-held arrays, depths, zlib's
+// overflow repair at 7 bits, longest codes to the least frequent, canonical codes.
+template <class SM>
+__device__ void clen_wave(SM& S, uint32_t lane) {
+    const bool sy = lane < 19;
+    uint32_t f = sy ? S.hw.clfreq[lane] : 0u;
+    {   // at least two used symbols: the first unused ones get frequency 1
+        const uint64_t used = __ballot(sy && f != 0);
+        const uint32_t nu = (uint32_t)__builtin_popcountll(used);
+        if (nu < 2) {
+            const uint64_t zero = __ballot(sy && f == 0);
+            const uint32_t zr = (uint32_t)__builtin_popcountll(zero & ((1ull << lane) - 1ull));
+            if (sy && f == 0 && zr < 2 - nu) f = 1;
+        }
+    }
+    const bool used = sy && f != 0;
+    const uint32_t ncl = (uint32_t)__builtin_popcountll(__ballot(used));
+    uint32_t rank = 0;  // position in ascending (freq, symbol) order
+    for (uint32_t t = 0; t < 19; t++) {
+        const uint32_t ft = __builtin_amdgcn_readlane(f, t);
+        rank += (ft != 0 && (ft < f || (ft == f && t < lane))) ? 1u : 0u;
+    }
+    // weights in sorted order: lane p holds the weight of the p-th used symbol
+    uint32_t wv = 0;
+    for (uint32_t t = 0; t < 19; t++) {
+        const uint32_t ft = __builtin_amdgcn_readlane(f, t), rt = __builtin_amdgcn_readlane(rank, t);
+        if (ft != 0 && rt == lane) wv = ft;
+    }
+    // serial two-queue merge (leaves 0..ncl, internal ncl..2ncl-2), parents lane-held
+    uint32_t pv = 0;
+    uint32_t li = 0, qi = ncl, nxt = ncl;
+    for (uint32_t k = 0; k + 1 < ncl; k++) {
+        uint32_t a, b;
+        const uint32_t wl0 = __builtin_amdgcn_readlane(wv, li < 63 ? li : 63);
+        const uint32_t wq0 = __builtin_amdgcn_readlane(wv, qi < 63 ? qi : 63);
+        if (li < ncl && (qi >= nxt || wl0 <= wq0)) a = li++; else a = qi++;
+        const uint32_t wl1 = __builtin_amdgcn_readlane(wv, li < 63 ? li : 63);
+        const uint32_t wq1 = __builtin_amdgcn_readlane(wv, qi < 63 ? qi : 63);
+        if (li < ncl && (qi >= nxt || wl1 <= wq1)) b = li++; else b = qi++;
+        const uint32_t sum = __builtin_amdgcn_readlane(wv, a) + __builtin_amdgcn_readlane(wv, b);
+        wv = lane == nxt ? sum : wv;
+        pv = (lane == a || lane == b) ? nxt : pv;
+        nxt++;
+    }
+    // depths: root 2ncl-2 at 0, then every node below its parent (parents have larger index)
+    uint32_t dv = 0;
+    if (ncl >= 2) {
+        for (int32_t i = (int32_t)(2 * ncl) - 3; i >= 0; i--) {
+            const uint32_t p = __builtin_amdgcn_readlane(pv, (uint32_t)i);
+            const uint32_t d = __builtin_amdgcn_readlane(dv, p) + 1;
+            dv = lane == (uint32_t)i ? d : dv;
+        }
+    }
+    // bit-length counts (lane L holds blc[L]) and overflow repair
+    const bool leaf = lane < ncl;
+    const uint32_t over = (uint32_t)__builtin_popcountll(__ballot(leaf && dv > 7));
+    const uint32_t dcl = dv > 7 ? 7u : dv;
+    uint32_t blc = 0;
+    for (uint32_t L = 1; L <= 7; L++) {
+        const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(leaf && dcl == L));
+        blc = lane == L ? c : blc;
+    }
+    for (int32_t ov = (int32_t)over; ov > 0; ov -= 2) {
+        const uint64_t nz = __ballot(lane >= 1 && lane <= 6 && blc != 0);
+        const uint32_t bits = 63u - (uint32_t)__builtin_clzll(nz);
+        blc += (lane == bits ? 0xFFFFFFFFu : 0u) + (lane == bits + 1 ? 2u : 0u) +
+               (lane == 7 ? 0xFFFFFFFFu : 0u);
+    }
+    // end(L) = sum of blc[L..7]; sorted position p gets #{L : p < end(L)}
+    uint32_t endv = 0;
+    for (uint32_t L = 7; L >= 1; L--) {
+        const uint32_t c = __builtin_amdgcn_readlane(blc, L);
+        endv += lane <= L ? c : 0u;  // lane L accumulates blc[L..7]
+    }
+    // (cross-lane reads stay outside divergent code: a lane inactive in a branch may not
+    // hold its value there)
+    uint32_t len = 0;
+    for (uint32_t L = 1; L <= 7; L++) {
+        const uint32_t eL = __builtin_amdgcn_readlane(endv, L);
+        len += (used && rank < eL) ? 1u : 0u;
+    }
+    // canonical codes (huff_codes)
+    uint32_t code = 0, nextc = 0;
+    for (uint32_t L = 1; L <= 7; L++) {
+        const uint32_t prev = (uint32_t)__builtin_popcountll(__ballot(sy && len == L - 1 && L > 1));
+        nextc = (nextc + prev) << 1;
+        const uint64_t mL = __ballot(sy && len == L);
+        if (len == L) code = nextc + (uint32_t)__builtin_popcountll(mL & ((1ull << lane) - 1ull));
+    }
+    if (sy) {
+        S.hw.cllen[lane] = len;
+        S.hw.clcode[lane] = len ? (bitrev(code, len) | (len << 16)) : 0u;
+        S.hw.clfreq[lane] = f;
+    }
+    __syncthreads();
+    const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 19; k++) o = lane == (uint32_t)k ? order[k] : o;
+    const uint64_t nzo = __ballot(sy && S.hw.cllen[o] != 0);
+    const uint32_t hclen = nzo ? 64u - (uint32_t)__builtin_clzll(nzo) : 0u;
+    if (lane == 0) S.misc[M_HCLEN] = hclen < 4 ? 4u : hclen;
 }
 
 template <class C, bool PROF>
@@ -324,7 +505,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
     uint32_t nst = 0;
     auto stamp = [&]() {
-        if (PROF && tid == 0) stamps[(size_t)seg * 16 + 6 + nst] = __builtin_amdgcn_s_memtime();
+        if (PROF && tid == 0) stamps[(size_t)seg * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
         nst++;
     };
     stamp();
@@ -337,25 +518,30 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     __syncthreads();
     ph_keys<C, DevOps>(tid, S);
     __syncthreads();
+    stamp();
     sort512_wave(S.hs.skey, tid);
     __syncthreads();
     stamp();
-    twoqueue_wave(S, 0, tid);
-    twoqueue_wave(S, 1, tid);
+    huff_rounds_wave(S, 0, tid);
+    huff_rounds_wave(S, 1, tid);
     __syncthreads();
     stamp();
     ph_parents<C>(tid, S);
     __syncthreads();
+    stamp();
 #pragma unroll 1
     for (int r = 0; r < JUMP_ROUNDS; r++) {
         ph_jump<C>(tid, S, r);
         __syncthreads();
     }
+    stamp();
     ph_leafdepth<C, DevOps>(tid, S);
     __syncthreads();
+    stamp();
     ph_fixblc<C>(tid, S);
     __syncthreads();
-    ph_assign<C, DevOps>(tid, S);
+    stamp();
+    assign_wave(S, tid);
     __syncthreads();
     stamp();
     ph_rle_mark<C, DevOps>(tid, S);
@@ -367,10 +553,13 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
         if (tid == 0) S.misc[M_NRLE] = nr;
     }
     __syncthreads();
+    stamp();
     ph_rle_emit<C, DevOps>(tid, S);
     __syncthreads();
-    ph_clen<C>(tid, S);
+    stamp();
+    clen_wave(S, tid);
     __syncthreads();
+    stamp();
     ph_rle_bits<C>(tid, S);
     __syncthreads();
     {
@@ -380,6 +569,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     __syncthreads();
     ph_choose<C>(tid, S, sl, last);
     __syncthreads();
+    stamp();
     ph_codes<C>(tid, S);
     ph_header<C, DevOps>(tid, S, last);
     __syncthreads();
@@ -394,6 +584,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
         g.data_bits = S.misc[M_DATABITS];
         g.nbytes = S.misc[M_NBYTES];
     }
+    stamp();
 }
 
 // ================================================================ k_seg_sizes
@@ -463,7 +654,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
     uint32_t nst = 0;
     auto stamp = [&]() {
-        if (PROF && tid == 0) stamps[(size_t)seg * 16 + 11 + nst] = __builtin_amdgcn_s_memtime();
+        if (PROF && tid == 0) stamps[(size_t)seg * STAMP_STRIDE + 24 + nst] = __builtin_amdgcn_s_memtime();
         nst++;
     };
     stamp();
@@ -606,6 +797,14 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
 // ================================================================== launchers
 size_t deflate_lds_bytes(int kernel) {
     return kernel == 0 ? sizeof(LzSmem<DC>) : kernel == 1 ? sizeof(HuffSmem<DC>) : sizeof(EncSmem<DC>);
+}
+
+hipError_t launch_huffman(hipStream_t st, uint32_t nseg, SegInfo* info, const uint32_t* hist,
+                          uint32_t* codes) {
+    if (nseg)
+        hipLaunchKernelGGL((k_huff<DC, false>), dim3(nseg), dim3(64), 0, st, nseg, info, hist, codes,
+                           nullptr);
+    return hipGetLastError();
 }
 
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev) {

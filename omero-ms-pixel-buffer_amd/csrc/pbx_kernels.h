@@ -35,11 +35,14 @@ struct DeflateLaunch {
     uint64_t* sizes;        // [ntiles] container bytes
     uint64_t* offs;         // [ntiles + 1] exclusive scan of sizes (offs[ntiles] = total)
     uint8_t* out;           // compacted containers
-    uint64_t* stamps;       // [nseg * 16] phase clocks (diagnostics) or nullptr
+    uint64_t* stamps;       // [nseg * 32] phase clocks (diagnostics) or nullptr
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.  If ev is given,
 // ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr);
 size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
+// k_huff alone (test hook): info[].sl / .last must be set.
+hipError_t launch_huffman(hipStream_t st, uint32_t nseg, SegInfo* info, const uint32_t* hist,
+                          uint32_t* codes);
 
 }  // namespace pbx

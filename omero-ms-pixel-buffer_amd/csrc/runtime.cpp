@@ -539,7 +539,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;
-    if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 16 * sizeof(uint64_t)))
+    if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 32 * sizeof(uint64_t)))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     DeflateLaunch a;
     a.tiles = (const TileDesc*)b->d_dt;
@@ -554,6 +554,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.offs = (uint64_t*)b->d_offs;
     a.out = (uint8_t*)b->d_png;
     a.stamps = prof ? (uint64_t*)b->d_stamps : nullptr;
+    if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4));
     } else {
@@ -569,19 +570,23 @@ int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (b->d_stamps && b->nseg) {  // PBX_PHASE_PROFILE diagnostic: mean cycles per phase
-        std::vector<uint64_t> st((size_t)b->nseg * 16);
+        std::vector<uint64_t> st((size_t)b->nseg * 32);
         HIP_TRY(hipMemcpy(st.data(), b->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
-        double acc[16] = {0};
-        for (uint32_t s = 0; s < b->nseg; s++)
-            for (int k = 1; k < 15; k++) {
-                if (k == 6 || k == 11) continue;  // first stamp of k_huff / k_encode
-                const uint64_t a = st[(size_t)s * 16 + k - 1], c = st[(size_t)s * 16 + k];
-                if (c > a && c - a < (1ull << 40)) acc[k] += (double)(c - a);
+        const int base[3] = {0, 8, 24}, lim[3] = {8, 24, 32};
+        const char* name[3] = {"lz77", "huff", "encode"};
+        for (int kk = 0; kk < 3; kk++) {
+            fprintf(stderr, "[pbx %s cycles/segment]", name[kk]);
+            for (int k = base[kk] + 1; k < lim[kk]; k++) {
+                double acc = 0;
+                uint64_t cnt = 0;
+                for (uint32_t s = 0; s < b->nseg; s++) {
+                    const uint64_t a = st[(size_t)s * 32 + k - 1], c = st[(size_t)s * 32 + k];
+                    if (a && c > a && c - a < (1ull << 40)) { acc += (double)(c - a); cnt++; }
+                }
+                if (cnt) fprintf(stderr, " %d:%.0f", k - base[kk], acc / cnt);
             }
-        fprintf(stderr, "[pbx phase cycles/segment]");
-        for (int k = 1; k < 15; k++)
-            if (k != 6 && k != 11) fprintf(stderr, " %d:%.0f", k, acc[k] / b->nseg);
-        fprintf(stderr, "\n");
+            fprintf(stderr, "\n");
+        }
     }
     return PBX_OK;
 }
@@ -745,6 +750,48 @@ int pbx_abi_sizes(uint64_t* sizes, int n) {
     if (!sizes || n < 0) return fail(PBX_E_BADARG, "null argument");
     for (int i = 0; i < n && i < 5; i++) sizes[i] = v[i];
     return 5;
+}
+
+int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last, uint32_t nseg,
+                     uint32_t* codes, uint32_t* info) {
+    if (!ctx || !hist || !sl_last || !codes || !info) return fail(PBX_E_BADARG, "null argument");
+    if (!nseg) return PBX_OK;
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    std::lock_guard<std::mutex> g(ctx->run_mu);
+    std::vector<SegInfo> si(nseg);
+    memset(si.data(), 0, nseg * sizeof(SegInfo));
+    for (uint32_t k = 0; k < nseg; k++) {
+        si[k].sl = sl_last[2 * k];
+        si[k].last = sl_last[2 * k + 1];
+    }
+    hipError_t err = hipSuccess;
+    void* d_info = ctx->dpool.get(nseg * sizeof(SegInfo), &err);
+    void* d_hist = d_info ? ctx->dpool.get((size_t)nseg * HIST_WORDS * 4, &err) : nullptr;
+    void* d_codes = d_hist ? ctx->dpool.get((size_t)nseg * CODE_WORDS * 4, &err) : nullptr;
+    int rc = PBX_OK;
+    if (!d_codes) {
+        rc = fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
+    } else {
+        rc = [&]() -> int {
+            HIP_TRY(hipMemcpy(d_info, si.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_hist, hist, (size_t)nseg * HIST_WORDS * 4, hipMemcpyHostToDevice));
+            HIP_TRY(launch_huffman(ctx->stream, nseg, (SegInfo*)d_info, (const uint32_t*)d_hist,
+                                   (uint32_t*)d_codes));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            HIP_TRY(hipMemcpy(codes, d_codes, (size_t)nseg * CODE_WORDS * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(si.data(), d_info, nseg * sizeof(SegInfo), hipMemcpyDeviceToHost));
+            return PBX_OK;
+        }();
+    }
+    for (void* p : {d_info, d_hist, d_codes}) if (p) ctx->dpool.put(p);
+    if (rc) return rc;
+    for (uint32_t k = 0; k < nseg; k++) {
+        info[4 * k] = si[k].btype;
+        info[4 * k + 1] = si[k].hdr_bits;
+        info[4 * k + 2] = si[k].data_bits;
+        info[4 * k + 3] = si[k].nbytes;
+    }
+    return PBX_OK;
 }
 
 int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {

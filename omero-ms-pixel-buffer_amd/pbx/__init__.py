@@ -88,7 +88,7 @@ EXPORTS = [
     "pbx_batch_launch", "pbx_batch_sync", "pbx_batch_fetch", "pbx_batch_destroy",
     "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
-    "pbx_abi_sizes", "pbx_shard_of",
+    "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman",
 ]
 
 _lib = None
@@ -133,6 +133,8 @@ def lib() -> ctypes.CDLL:
                                     ctypes.c_char_p, u64]
     L.pbx_abi_sizes.argtypes = [ctypes.POINTER(u64), ctypes.c_int]
     L.pbx_shard_of.argtypes = [ctypes.POINTER(PbxTileReq), i32, i32, i32]
+    L.pbx_test_huffman.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 2 + [ctypes.c_uint32] + \
+        [ctypes.c_void_p] * 2
     _lib = L
     return L
 

@@ -23,6 +23,8 @@ def lib():
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(SegOut)]
         L.pbxemu_nsegs.restype = ctypes.c_uint32
         L.pbxemu_nsegs.argtypes = [ctypes.c_uint64]
+        L.pbxemu_huffman.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_void_p]
         L.pbxemu_crc_combine.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         _lib = L
@@ -43,3 +45,15 @@ def deflate(data: bytes, rowlen: int):
 
 def crc_combine(c1, c2, len2):
     return lib().pbxemu_crc_combine(c1, c2, len2)
+
+
+def huffman(hist, sl, last):
+    """Huffman stage alone: (codes[480], info[4]) as uint32 numpy arrays."""
+    import numpy as np
+    h = np.ascontiguousarray(hist, dtype=np.uint32)
+    assert h.shape == (320,)
+    codes = np.zeros(480, np.uint32)
+    info = np.zeros(4, np.uint32)
+    r = lib().pbxemu_huffman(h.ctypes.data, sl, last, codes.ctypes.data, info.ctypes.data)
+    assert r == 0
+    return codes, info
