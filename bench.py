@@ -40,29 +40,47 @@ def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
 
 
 def run_steps(svc, ctxs, steps, warmup, barrier):
-    """Warmup, then `steps` timed plan+launch+sync steps; returns (seconds, last stats)."""
-    for _ in range(warmup):
-        b = pbx.Batch(svc, ctxs)
-        b.launch()
-        b.sync()
-        b.close()
+    """Warmup, then `steps` timed steps; returns (seconds, last stats, mean deflate-chain ms,
+    mean k_extract ms, mean host ms per step).
+
+    Steps are pipelined two deep, as a server feeds its GPU: the host plans and launches
+    batch k+1 (request validation, descriptors, upload) while batch k runs, then waits for
+    batch k.  The request array is built once (the caller's TileCtx list)."""
+    reqs = pbx.make_reqs(ctxs)
+
+    def one_pass(n, record):
+        prev = None
+        host = 0.0
+        out = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            b = pbx.Batch(svc, reqs=reqs)
+            b.launch()
+            host += time.perf_counter() - t0
+            if prev is not None:
+                prev.sync()
+                if record:
+                    out.append(prev.stats())
+                prev.close()
+            prev = b
+        prev.sync()
+        if record:
+            out.append(prev.stats())
+        prev.close()
+        return out, host
+
+    if warmup:
+        one_pass(warmup, False)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats, ms_deflate, ms_extract = None, [], []
-    for _ in range(steps):
-        b = pbx.Batch(svc, ctxs)
-        b.launch()
-        b.sync()
-        s = b.stats()
-        ms_deflate.append(s.ms_deflate)
-        ms_extract.append(s.ms_extract)
-        stats = s
-        b.close()
+    stats, host = one_pass(steps, True)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    return dt, stats, sum(ms_deflate) / len(ms_deflate), sum(ms_extract) / len(ms_extract)
+    n = len(stats)
+    return (dt, stats[-1], sum(s.ms_deflate + s.ms_assemble for s in stats) / n,
+            sum(s.ms_extract for s in stats) / n, 1000.0 * host / n)
 
 
 def fetch_rate(svc, ctxs):
@@ -115,7 +133,7 @@ def main():
     svc.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0,
                        plane_no=rank)
     ctxs = grid_ctxs(iid, "png")
-    dt, st, ms_deflate, _ = run_steps(svc, ctxs, args.steps, args.warmup, barrier)
+    dt, st, ms_deflate, _, host_ms = run_steps(svc, ctxs, args.steps, args.warmup, barrier)
     t = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -141,14 +159,21 @@ def main():
                    "parallelism": f"dp{world} (request sharding, no collectives)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "kernel": "k_deflate",
+                     "traffic": None,
+                     "kernel": "deflate chain k_lz77+k_huff+k_seg_sizes+k_scan_offsets+k_encode+k_frame",
                      "kernel_ms": round(ms_deflate, 3),
-                     "alg_bytes_per_launch": int(alg_bytes)},
+                     "alg_bytes_per_launch": int(alg_bytes),
+                     "alg_bytes_def": "PNG end-to-end w*h*bpp + out_len per tile (SURVEY 8d)"},
         "hbm_gbps_step": round((st.in_bytes + st.deflate_out_bytes) * world * args.steps / dt / 1e9, 1),
         "compressed_bytes_per_tile": round(st.deflate_out_bytes / len(ctxs), 1),
         "kernel_ms": {"extract": round(st.ms_extract, 3), "filter": round(st.ms_filter, 3),
-                      "deflate": round(st.ms_deflate, 3), "assemble": round(st.ms_assemble, 3),
-                      "total": round(st.ms_total, 3)},
+                      "lz77": round(st.ms_lz77, 3), "huff": round(st.ms_huff, 3),
+                      "encode": round(st.ms_encode, 3), "deflate": round(st.ms_deflate, 3),
+                      "frame": round(st.ms_assemble, 3), "total": round(st.ms_total, 3)},
+        "filter_gbps": round((st.in_bytes + st.stream_bytes) / (st.ms_filter * 1e-3) / 1e9, 1),
+        "filter_frac": round((st.in_bytes + st.stream_bytes) / (st.ms_filter * 1e-3) / 1e9
+                             / HBM_PEAK_GBPS, 4),
+        "host_ms_per_step": round(host_ms, 3),
     }
 
     if not args.no_extra:
@@ -157,7 +182,7 @@ def main():
         out["e2e_with_d2h_tiles_per_s"] = round(rate, 1)
         # raw path (BASELINE configs[1]): extraction + byte swap, HBM-bound k_extract
         raw = grid_ctxs(iid, None)
-        dtr, sr, _, ms_ext = run_steps(svc, raw, 5, 1, barrier)
+        dtr, sr, _, ms_ext, _ = run_steps(svc, raw, 5, 1, barrier)
         out["raw_4096x512x512_u16"] = {
             "tiles_per_s": round(len(raw) * 5 * world / dtr, 1),
             "k_extract_ms": round(ms_ext, 3),
@@ -166,7 +191,7 @@ def main():
         # G_FAKE (FakeReader-like gradient) PNG, compressible data
         svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
         fk = grid_ctxs(2, "png")
-        dtf, sf, msf, _ = run_steps(svc, fk, 3, 1, barrier)
+        dtf, sf, msf, _, _ = run_steps(svc, fk, 3, 1, barrier)
         out["png_fake_4096x512x512_u16"] = {
             "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
             "compressed_bytes_per_tile": round(sf.deflate_out_bytes / len(fk), 1),

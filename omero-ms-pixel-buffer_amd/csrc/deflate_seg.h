@@ -51,7 +51,7 @@ struct DeflateCfg {
     static constexpr int CAP = 32;        // per-lane match length before the wave extends it
     static constexpr int CRCC = 64;       // CRC chunk bytes per thread
     static constexpr int LOG2_CRCC = 6;
-    static constexpr int BUFW = (WIN + SEG + 16) / 4;
+    static constexpr int BUFW = (WIN + SEG + 32) / 4;
     static constexpr int SEGW = (SEG + 16) / 4;
     static constexpr int OUTW = (SEG + 64) / 4;
     static constexpr int HDRW = 160;      // dynamic block header bits (<= 17+57+316*14)
@@ -62,6 +62,7 @@ struct DeflateCfg {
     static_assert(WIN + SEG <= 32768, "deflate distances are limited to 32768");
     static_assert((1 << LOGNT) == NT, "NT must be a power of two in 128..1024");
     static_assert(NT * CRCC >= SEG + 64, "CRC chunks cover the output");
+    static_assert(CH % 4 == 0 && WIN % 16 == 0, "Adler chunks are whole aligned words");
     static_assert(HDRW * 32 >= 17 + 57 + 316 * 14, "header buffer holds any dynamic header");
 };
 
@@ -80,17 +81,36 @@ struct SegParams {
     uint32_t last;   // 1 if this segment ends the stream (BFINAL)
 };
 
+// c + sum of the four byte products of a and b (v_dot4_u32_u8 on the device).
+PBX_HD uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+    for (int i = 0; i < 4; i++) c += ((a >> (8 * i)) & 0xFFu) * ((b >> (8 * i)) & 0xFFu);
+    return c;
+#endif
+}
+
 template <class SM>
 PBX_HD uint32_t lds_byte(const SM& S, uint32_t i) {
     return (S.buf[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
 }
 
-// Unaligned little-endian 32-bit read from the byte buffer.
+// Low 32 bits of (hi:lo) >> sh, sh < 32 (v_alignbit_b32 on the device).
+PBX_HD uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+#endif
+}
+
+// Unaligned little-endian 32-bit read from the byte buffer: both words are always read
+// (one ds_read2_b32, no branch on the alignment).
 template <class SM>
 PBX_HD uint32_t lds_ld4(const SM& S, uint32_t i) {
     const uint32_t w0 = S.buf[i >> 2], w1 = S.buf[(i >> 2) + 1];
-    const uint32_t sh = (i & 3) * 8;
-    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+    return funnel32(w1, w0, (i & 3) * 8);
 }
 
 template <class C>
@@ -100,10 +120,18 @@ PBX_HD uint32_t hash3(uint32_t v) {
 
 // ============================================================================ LZ77
 // Src provides fill_word(p0, nb) -> up to 4 stream bytes starting at stream position p0.
+// Buffer bytes the LZ77 phases may read: the window and segment, zero up to the end of
+// the last whole Adler chunk (CH) plus one 16-byte vector.
+template <class C>
+PBX_HD uint32_t lz_fill_bytes(const SegParams& sp) {
+    const uint32_t z = sp.wl + (sp.sl + C::CH - 1) / C::CH * C::CH + 16;
+    return z < (uint32_t)C::BUFW * 4 ? z : (uint32_t)C::BUFW * 4;
+}
+
 template <class C, class SM, class Src>
 PBX_HD void ph_fill(uint32_t tid, SM& S, const Src& src, const SegParams& sp) {
-    const uint32_t nb = sp.wl + sp.sl, nw = (nb + 3) / 4;
-    for (uint32_t k = tid; k < nw + 4; k += C::NT) {
+    const uint32_t nb = sp.wl + sp.sl, nw = (nb + 3) / 4, nz = lz_fill_bytes<C>(sp) / 4;
+    for (uint32_t k = tid; k < nz; k += C::NT) {
         uint32_t v = 0;
         if (k < nw) {
             const uint32_t take = nb - 4 * k;
@@ -126,23 +154,6 @@ PBX_HD void ph_insert(uint32_t tid, SM& S, const SegParams& sp) {
     for (uint32_t i = tid; i + 3 <= nb; i += C::NT) Ops::amin(&S.head[hash3<C>(lds_ld4(S, i))], i);
 }
 
-template <class SM>
-PBX_HD uint32_t match_len(const SM& S, uint32_t j, uint32_t a, uint32_t cur4, uint32_t maxlen) {
-    uint32_t x = lds_ld4(S, j) ^ cur4;
-    uint32_t l;
-    if (x) {
-        l = (uint32_t)__builtin_ctz(x) >> 3;
-    } else {
-        l = 4;
-        while (l < maxlen) {
-            x = lds_ld4(S, j + l) ^ lds_ld4(S, a + l);
-            if (x) { l += (uint32_t)__builtin_ctz(x) >> 3; break; }
-            l += 4;
-        }
-    }
-    return l < maxlen ? l : maxlen;
-}
-
 // Minimum length worth coding at a distance: a 3-byte match 16 KiB back costs more bits
 // than three literals (zlib's TOO_FAR rule, extended one step).
 PBX_HD bool match_pays(uint32_t len, uint32_t dist) {
@@ -152,6 +163,9 @@ PBX_HD bool match_pays(uint32_t len, uint32_t dist) {
 // Best match at segment position p (capped at CAP): candidates, in order, the previous
 // byte (runs), the previous 2-byte sample, the same column one row up, and the first
 // occurrence of the 3-byte hash.  Longest capped length wins; the first wins ties.
+// The first 4 bytes of every candidate are compared without branches (the distance-1 and
+// -2 windows come from the three words around p); only candidates whose 4 bytes all match
+// run the compare loop up to the cap.
 template <class C, class SM>
 PBX_HD void eval_pos(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t& L,
                      uint32_t& D) {
@@ -161,14 +175,37 @@ PBX_HD void eval_pos(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, 
     const uint32_t maxlen = rem < 258 ? rem : 258;
     const uint32_t cap = maxlen < (uint32_t)C::CAP ? maxlen : (uint32_t)C::CAP;
     const uint32_t a = sp.wl + p;
-    const uint32_t cur4 = lds_ld4(S, a);
+    const uint32_t wi = a >> 2, sh = (a & 3) * 8;
+    const uint32_t W0 = S.buf[wi > 0 ? wi - 1 : 0], W1 = S.buf[wi], W2 = S.buf[wi + 1];
+    const uint32_t cur4 = funnel32(W2, W1, sh);
+    const uint32_t m1 = sh >= 8 ? funnel32(W2, W1, sh - 8) : funnel32(W1, W0, sh + 24);
+    const uint32_t m2 = sh >= 16 ? funnel32(W2, W1, sh - 16) : funnel32(W1, W0, sh + 16);
     const uint32_t j = S.head[hash3<C>(cur4)];
     const uint32_t cand[4] = {1u, 2u, sp.rowlen > 2 ? sp.rowlen : 0u, j < a ? a - j : 0u};
+    uint32_t x[4];
+    x[0] = m1 ^ cur4;
+    x[1] = m2 ^ cur4;
+#pragma unroll
+    for (int k = 2; k < 4; k++) {
+        const uint32_t d = cand[k];
+        x[k] = lds_ld4(S, d != 0 && d <= a ? a - d : a) ^ cur4;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint32_t d = cand[k];
         if (d == 0 || d > a) continue;
-        const uint32_t l = match_len(S, a - d, a, cur4, cap);
+        uint32_t l;
+        if (x[k]) {
+            l = (uint32_t)__builtin_ctz(x[k]) >> 3;
+        } else {
+            l = 4;
+            while (l < cap) {
+                const uint32_t y = lds_ld4(S, a - d + l) ^ lds_ld4(S, a + l);
+                if (y) { l += (uint32_t)__builtin_ctz(y) >> 3; break; }
+                l += 4;
+            }
+        }
+        l = l < cap ? l : cap;
         if (l > L && match_pays(l, d)) { L = l; D = d; }
     }
 }
@@ -284,13 +321,19 @@ PBX_HD void ph_hist(uint32_t tid, SM& S, const SegParams& sp, uint32_t& s1, uint
     const uint32_t cs = tid * C::CH;
     s1 = 0; s2 = 0; n = 0;
     if (cs < sp.sl) {
+        // whole words of the chunk (wl and cs are multiples of 4; bytes past the segment
+        // are zero in buf): s2 with weights counted from the full chunk end, then shifted
         const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
         n = ce - cs;
-        for (uint32_t p = cs; p < ce; p++) {
-            const uint32_t b = lds_byte(S, sp.wl + p);
-            s1 += b;
-            s2 += (ce - p) * b;
+        const uint32_t w0 = (sp.wl + cs) >> 2;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)C::CH / 4; k++) {
+            const uint32_t v = S.buf[w0 + k];
+            const uint32_t e = (uint32_t)C::CH - 4 * k;  // weights e, e-1, e-2, e-3
+            s1 = dot4_u8(v, 0x01010101u, s1);
+            s2 = dot4_u8(v, e | ((e - 1) << 8) | ((e - 2) << 16) | ((e - 3) << 24), s2);
         }
+        s2 -= (cs + (uint32_t)C::CH - ce) * s1;
         s1 %= ADLER_BASE;
         s2 %= ADLER_BASE;
     }
@@ -799,11 +842,39 @@ PBX_HD void ph_header(uint32_t tid, SM& S, uint32_t last) {
 // =========================================================================== encode
 // The encode workgroup holds the segment bytes (buf; wl may be 0), the match lists, the
 // code tables, the block header (first HDRW words of out) and M_BTYPE / M_HDRBITS /
-// M_DATABITS / M_NBYTES from the Huffman step.
+// M_DATABITS / M_NBYTES from the Huffman step.  The output bytes are assembled in out
+// (a stored block is copied there too), then CRC'd and stored.
 template <class C, class SM>
 PBX_HD void ph_enc_init(uint32_t tid, SM& S, const uint32_t* hdrw) {
     for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT) S.out[k] = k < (uint32_t)C::HDRW ? hdrw[k] : 0u;
-    for (uint32_t k = tid; k < 256; k += C::NT) S.crc_table[k] = crc_table_entry(k);
+    for (uint32_t k = tid; k < 256; k += C::NT) {  // slicing-by-4 CRC tables
+        const uint32_t t0 = crc_table_entry(k);
+        const uint32_t t1 = (t0 >> 8) ^ crc_table_entry(t0 & 0xFF);
+        const uint32_t t2 = (t1 >> 8) ^ crc_table_entry(t1 & 0xFF);
+        const uint32_t t3 = (t2 >> 8) ^ crc_table_entry(t2 & 0xFF);
+        S.crc_t[0][k] = t0; S.crc_t[1][k] = t1; S.crc_t[2][k] = t2; S.crc_t[3][k] = t3;
+    }
+}
+
+// Stored block (BTYPE 00) bytes into out: BFINAL/BTYPE byte, LEN, NLEN, the segment bytes.
+template <class C, class SM>
+PBX_HD void ph_stored(uint32_t tid, SM& S, const SegParams& sp) {
+    const uint32_t n = 5 + sp.sl, nw = (n + 3) / 4;
+    const uint32_t hdr0 = (sp.last ? 1u : 0u) | ((sp.sl & 0xFFFFu) << 8) | (((~sp.sl) & 0xFFu) << 24);
+    const uint32_t hdr4 = ((~sp.sl) >> 8) & 0xFFu;
+    for (uint32_t k = tid; k < nw; k += C::NT) {
+        uint32_t v = 0;
+        if (k == 0) {
+            v = hdr0;
+        } else {
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t j = 4 * k + i;
+                const uint32_t b = j == 4 ? hdr4 : j < n ? lds_byte(S, sp.wl + j - 5) : 0u;
+                v |= b << (8 * i);
+            }
+        }
+        S.out[k] = v;
+    }
 }
 
 template <class SM>
@@ -828,10 +899,36 @@ PBX_HD uint32_t ph_bits(uint32_t tid, const SM& S, const SegParams& sp) {
     return f.bits;
 }
 
+// Bit writer of one thread's contiguous bit range: whole 32-bit words are plain stores,
+// the first and last (shared with the neighbouring ranges) are OR'd atomically.
+template <class Ops>
+struct RunWriter {
+    uint32_t* out;
+    uint32_t word, first;  // current word index, the range's first word
+    uint32_t nacc;         // bits held in acc (including the leading bits of other ranges)
+    uint64_t acc;
+    PBX_HD RunWriter(uint32_t* o, uint32_t pos)
+        : out(o), word(pos >> 5), first(pos >> 5), nacc(pos & 31), acc(0) {}
+    PBX_HD void put(uint32_t v, uint32_t n) {
+        acc |= (uint64_t)v << nacc;
+        nacc += n;
+        if (nacc >= 32) {
+            const uint32_t w = (uint32_t)acc;
+            if (word == first) Ops::aor(&out[word], w); else out[word] = w;
+            word++;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    PBX_HD void finish() {
+        if (acc) Ops::aor(&out[word], (uint32_t)acc);  // < 32 bits left
+    }
+};
+
 template <class Ops, class SM>
 struct WriteF {
     const SM& S;
-    BitWriter<Ops> bw;
+    RunWriter<Ops> bw;
     PBX_HD void lit(uint32_t b) { const uint32_t c = S.lcode[b]; bw.put(c & 0xFFFF, c >> 16); }
     PBX_HD void match(uint32_t len, uint32_t dist) {
         uint32_t s, e, v;
@@ -853,8 +950,9 @@ PBX_HD void ph_write(uint32_t tid, SM& S, const SegParams& sp, uint32_t bitoff) 
     const uint32_t bt = S.misc[M_BTYPE];
     if (bt == 0) return;
     const uint32_t hdr = S.misc[M_HDRBITS];
-    WriteF<Ops, SM> f{S, {S.out, hdr + bitoff}};
+    WriteF<Ops, SM> f{S, RunWriter<Ops>(S.out, hdr + bitoff)};
     walk_tokens<C>(tid, S, sp, f);
+    f.bw.finish();
     if (tid == 0) {
         const uint32_t eob = S.lcode[256];
         BitWriter<Ops> bw{S.out, hdr + S.misc[M_DATABITS] - (eob >> 16)};
@@ -868,28 +966,34 @@ PBX_HD void ph_write(uint32_t tid, SM& S, const SegParams& sp, uint32_t bitoff) 
 }
 
 template <class SM>
-PBX_HD uint32_t out_byte(const SM& S, const SegParams& sp, uint32_t j) {
-    if (S.misc[M_BTYPE] != 0) return (S.out[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-    if (j == 0) return sp.last ? 1u : 0u;
-    if (j == 1) return sp.sl & 0xFF;
-    if (j == 2) return (sp.sl >> 8) & 0xFF;
-    if (j == 3) return (~sp.sl) & 0xFF;
-    if (j == 4) return (~sp.sl >> 8) & 0xFF;
-    return lds_byte(S, sp.wl + j - 5);
+PBX_HD uint32_t out_byte(const SM& S, uint32_t j) {
+    return (S.out[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
 }
 
-// Raw CRC (register init 0, no final xor) of this thread's right-aligned CRCC-byte chunk:
-// thread t covers [n - (NT-t)*CRCC, n - (NT-1-t)*CRCC).  Leading zero bytes leave a raw CRC
-// unchanged, so short or empty chunks count as full ones and combine level k shifts by the
-// constant x^(8*CRCC*2^k).
+// Raw CRC (register init 0, no final xor) of this thread's right-aligned CRCC-byte chunk of
+// the output left-padded with zero bytes to a multiple of 4 (leading zero bytes leave a raw
+// CRC unchanged): thread t covers [V - (NT-t)*CRCC, V - (NT-1-t)*CRCC) of the padded V bytes,
+// 4 bytes per slicing-by-4 step.  Short or empty chunks count as full ones, so combine
+// level k shifts by the constant x^(8*CRCC*2^k).
 template <class C, class SM>
-PBX_HD uint32_t ph_crc(uint32_t tid, const SM& S, const SegParams& sp) {
+PBX_HD uint32_t ph_crc(uint32_t tid, const SM& S) {
     const uint32_t nbytes = S.misc[M_NBYTES];
-    const int64_t hi = (int64_t)nbytes - (int64_t)(C::NT - 1 - tid) * C::CRCC;
-    int64_t lo = hi - C::CRCC;
+    const uint32_t pad = (4u - (nbytes & 3u)) & 3u, nv = (nbytes + pad) >> 2;
+    const int64_t hi = (int64_t)nv - (int64_t)(C::NT - 1 - tid) * (C::CRCC / 4);
+    int64_t lo = hi - C::CRCC / 4;
     if (lo < 0) lo = 0;
     uint32_t c = 0;
-    for (int64_t j = lo; j < hi; j++) c = crc_update(S.crc_table, c, (uint8_t)out_byte(S, sp, (uint32_t)j));
+    for (int64_t k = lo; k < hi; k++) {
+        const uint32_t w1 = S.out[k];
+        uint32_t v = w1;
+        if (pad) {
+            const uint32_t w0 = k > 0 ? S.out[k - 1] : 0u;
+            v = (w1 << (8 * pad)) | (w0 >> (32 - 8 * pad));
+        }
+        c ^= v;
+        c = S.crc_t[3][c & 0xFF] ^ S.crc_t[2][(c >> 8) & 0xFF] ^ S.crc_t[1][(c >> 16) & 0xFF] ^
+            S.crc_t[0][c >> 24];
+    }
     return c;
 }
 

@@ -46,7 +46,7 @@ struct Smem {
     uint32_t hdrw[C::HDRW];
     uint32_t misc[M_NMISC];
     uint32_t out[C::OUTW];
-    uint32_t crc_table[256];
+    uint32_t crc_t[4][256];
     uint32_t t_a[C::NT];
 };
 
@@ -104,15 +104,17 @@ int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, Seg
     run_huff(S, sp.sl, sp.last);
     // ---- k_encode
     for (int t = 0; t < C::NT; t++) ph_enc_init<C>(t, S, S.hdrw);
+    if (S.misc[M_BTYPE] == 0)
+        for (int t = 0; t < C::NT; t++) ph_stored<C>(t, S, sp);
     for (int t = 0; t < C::NT; t++) S.t_a[t] = ph_bits<C>(t, S, sp);
     const uint32_t bitsum = scan_excl_add(S.t_a, C::NT);
     if (S.misc[M_BTYPE] != 0 && bitsum != S.misc[M_DATABITS] - (S.lcode[256] >> 16)) return -2;
     for (int t = 0; t < C::NT; t++) ph_write<C, EmuOps>(t, S, sp, S.t_a[t]);
     const uint32_t nbytes = S.misc[M_NBYTES];
-    for (uint32_t j = 0; j < nbytes; j++) slot[j] = (uint8_t)out_byte(S, sp, j);
+    for (uint32_t j = 0; j < nbytes; j++) slot[j] = (uint8_t)out_byte(S, j);
     uint32_t raw = 0;
     const uint32_t opc = crc_x8pow2(C::LOG2_CRCC);
-    for (int t = 0; t < C::NT; t++) raw = crc_multmodp(opc, raw) ^ ph_crc<C>(t, S, sp);
+    for (int t = 0; t < C::NT; t++) raw = crc_multmodp(opc, raw) ^ ph_crc<C>(t, S);
     so->nbytes = nbytes;
     so->crc_op = crc_x8n(nbytes);
     so->crc = crc_from_raw(raw, so->crc_op);

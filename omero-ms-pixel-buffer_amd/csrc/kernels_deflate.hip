@@ -62,7 +62,7 @@ struct EncSmem {
     uint32_t w_nm[C::NW];
     uint32_t lcode[288], dcode[32];
     uint32_t out[C::OUTW];
-    uint32_t crc_table[256];
+    uint32_t crc_t[4][256];
     uint32_t misc[M_NMISC];
     uint32_t t_a[C::NT];
     uint32_t wtot[16];
@@ -82,12 +82,12 @@ __device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k, u
 }
 
 // 16-byte loads of nb stream bytes (16-byte aligned source, slack after every tile) into
-// LDS words; bytes past nb and one extra vector are zero.
+// LDS words; bytes from nb up to nz (>= nb + 16, a multiple of 16) are zero.
 template <int NT>
 __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, uint32_t nb,
-                                             uint32_t tid) {
+                                             uint32_t nz, uint32_t tid) {
     const uint32_t nv = (nb + 15) / 16;
-    for (uint32_t k = tid; k <= nv; k += NT) {
+    for (uint32_t k = tid; k < nz / 16; k += NT) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (k < nv) {
             v = *(const uint4*)(src + 16ull * k);
@@ -110,9 +110,11 @@ __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, 
 // Wave-serial greedy parse of one sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).
 template <class C, class SM>
 __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
-    const uint32_t w = tid >> 6, lane = tid & 63;
+    // every loop-carried value is wave-uniform: readfirstlane keeps it in SGPRs, so the
+    // walk below is scalar code, not exec-masked vector code
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t ss = w * C::SUB;
-    const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
+    const uint32_t se = __builtin_amdgcn_readfirstlane(ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl);
     uint32_t nm = 0, pos = ss;
     while (pos < se) {
         uint32_t L, D;
@@ -122,7 +124,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
         while (o < 64) {
             const uint64_t m = mask >> o;
             if (!m) { o = 64; break; }
-            const uint32_t k = o + (uint32_t)__builtin_ctzll(m);
+            const uint32_t k = __builtin_amdgcn_readfirstlane(o + (uint32_t)__builtin_ctzll(m));
             uint32_t Lk = __builtin_amdgcn_readlane(L, k);
             const uint32_t Dk = __builtin_amdgcn_readlane(D, k);
             if (k + 1 < 64) {
@@ -141,7 +143,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
                 const uint32_t xf = __builtin_amdgcn_readlane(x, f);
                 const uint32_t of = Lk + 4 * f;
                 const uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
-                Lk = l < maxlen ? l : maxlen;
+                Lk = __builtin_amdgcn_readfirstlane(l < maxlen ? l : maxlen);
             }
             if (nm < (uint32_t)C::MAXMW) {
                 if (lane == 0) {
@@ -150,9 +152,9 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
                 }
                 nm++;
             }
-            o = k + Lk;
+            o = __builtin_amdgcn_readfirstlane(k + Lk);
         }
-        pos += o;
+        pos = __builtin_amdgcn_readfirstlane(pos + o);
     }
     if (lane == 0) S.w_nm[w] = nm;
 }
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
     const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
     const TileDesc d = dt[ti];
     const SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
-    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, tid);
+    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
     ph_lz_init<C>(tid, S);
     __syncthreads();
     stamp();
@@ -630,14 +632,11 @@ __global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restric
 }
 
 // ==================================================================== k_encode
+// Output bytes j..j+3 (j = any byte offset) from the assembled words.
 template <class SM>
-__device__ __forceinline__ uint32_t out_word(const SM& S, const SegParams& sp, uint32_t j) {
-    if (S.misc[M_BTYPE] != 0) {
-        const uint32_t w0 = S.out[j >> 2], w1 = S.out[(j >> 2) + 1], sh = (j & 3) * 8;
-        return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
-    }
-    return out_byte(S, sp, j) | (out_byte(S, sp, j + 1) << 8) | (out_byte(S, sp, j + 2) << 16) |
-           (out_byte(S, sp, j + 3) << 24);
+__device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
+    const uint32_t w0 = S.out[j >> 2], w1 = S.out[(j >> 2) + 1], sh = (j & 3) * 8;
+    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
 }
 
 template <class C, bool PROF>
@@ -663,7 +662,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
     sp.base += sp.wl;  // the encoder holds the segment only
     sp.wl = 0;
-    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.sl, tid);
+    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.sl, ((sp.sl + 15) & ~15u) + 16, tid);
     const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
     if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
     const uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
@@ -677,6 +676,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
         S.misc[M_DATABITS] = gi.data_bits; S.misc[M_NBYTES] = gi.nbytes;
     }
     __syncthreads();
+    if (gi.btype == 0) ph_stored<C>(tid, S, sp);
     for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
         if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
             S.mpos[i] = mg[C::NW + i];
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     stamp();
     // CRC-32: raw CRC of right-aligned 64-byte chunks, combined per wave by shuffles with
     // the constant operators x^(8*64*2^k), then across the waves
-    uint32_t c = ph_crc<C>(tid, S, sp);
+    uint32_t c = ph_crc<C>(tid, S);
 #pragma unroll
     for (int k = 0; k < 6; k++) {
         const uint32_t r = __shfl_down(c, 1 << k, 64);
@@ -707,9 +707,9 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
     const uint32_t nwords = (nbytes - head) >> 2;
-    if (tid < head) dst[tid] = (uint8_t)out_byte(S, sp, tid);
-    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, sp, head + 4 * k);
-    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, sp, j);
+    if (tid < head) dst[tid] = (uint8_t)out_byte(S, tid);
+    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, head + 4 * k);
+    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, j);
     __syncthreads();
     if (tid == 0) {
         uint32_t raw = S.red[0];

@@ -258,6 +258,116 @@ hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- K1+K2 fast rows (filter None)
+// The stream of a filter-None PNG tile is row r = [0] ++ big-endian row bytes, and of a
+// deflate-TIFF tile the row bytes alone.  Each thread writes aligned 16-byte stream words:
+// 16 bytes of one source row at byte offset s come from two aligned 16-byte loads (byte
+// swap / sign flip applied on the aligned words, where sample boundaries are known) and a
+// funnel shift by s & 15; the ~1/64 of words that straddle a row end are merged bytewise
+// from both rows.  No LDS: neighbouring lanes share the overlapping loads in L1/L2.
+constexpr int RW_NT = 256;
+constexpr int RW_WPT = (int)ROWS_WORDS_PER_BLOCK / RW_NT;
+
+struct Rows16 {
+    const uint8_t* row;  // source row start (16-byte aligned), little- or big-endian samples
+    uint32_t rb, bpp;
+    bool swap, flip;
+    __device__ __forceinline__ uint4 fix(uint4 v) const {
+        if (swap) v = swap16(v, (int)bpp);
+        if (flip) v = flip_msb(v, (int)bpp);
+        return v;
+    }
+    // 16 big-endian row bytes starting at byte s (-16 <= s < rb); bytes outside [0, rb)
+    // are unspecified
+    __device__ __forceinline__ uint4 fetch(int32_t s) const {
+        uint4 lo, hi;
+        uint32_t sh;
+        if (s < 0) {
+            lo = make_uint4(0, 0, 0, 0);
+            hi = fix(*(const uint4*)row);
+            sh = (uint32_t)(s + 16);
+        } else {
+            const uint32_t a = (uint32_t)s & ~15u;
+            lo = fix(*(const uint4*)(row + a));
+            sh = (uint32_t)s & 15u;
+            hi = (sh && a + 16 < rb) ? fix(*(const uint4*)(row + a + 16)) : make_uint4(0, 0, 0, 0);
+        }
+        if (!sh) return lo;
+        const uint32_t q = sh >> 2, t = (sh & 3) * 8;
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+            v[i] = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+        if (!t) return make_uint4(v[0], v[1], v[2], v[3]);
+        return make_uint4((v[0] >> t) | (v[1] << (32 - t)), (v[1] >> t) | (v[2] << (32 - t)),
+                          (v[2] >> t) | (v[3] << (32 - t)), (v[3] >> t) | (v[4] << (32 - t)));
+    }
+};
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t k) {
+    const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+    return (w >> ((k & 3) * 8)) & 0xFFu;
+}
+
+__global__ __launch_bounds__(RW_NT) void k_rows(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                uint8_t* __restrict__ stream) {
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const TileDesc d = dt[ti];
+    const uint32_t fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
+    const uint32_t rowlen = d.rowlen, len = (uint32_t)d.stream_len;
+    const uint32_t nwords = (len + 15) >> 4;
+    Rows16 R;
+    R.rb = rowlen - fb;
+    R.bpp = d.bpp;
+    R.swap = (d.flags & TF_SWAP) != 0;
+    R.flip = (d.flags & TF_FLIP) != 0;
+    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
+    uint8_t* out = stream + d.out_off;
+    const uint32_t w0 = (b - d.blk_first) * ROWS_WORDS_PER_BLOCK;
+#pragma unroll
+    for (int j = 0; j < RW_WPT; j++) {
+        const uint32_t wi = w0 + (uint32_t)j * RW_NT + tid;
+        if (wi >= nwords) break;
+        const uint32_t o = wi << 4;
+        const uint32_t r = o / rowlen, c = o - r * rowlen;
+        R.row = src0 + (int64_t)r * d.pitch;
+        const uint4 x1 = R.fetch((int32_t)c - (int32_t)fb);
+        uint4 v = x1;
+        if (c < fb || c + 16 > rowlen || o + 16 > len) {
+            // filter byte at the row start, or the word runs into the next row / the end
+            uint4 x2 = make_uint4(0, 0, 0, 0);
+            const bool next = c + 16 > rowlen && r + 1 < (uint32_t)d.h;
+            if (next) {
+                Rows16 R2 = R;
+                R2.row = R.row + d.pitch;
+                x2 = R2.fetch((int32_t)c - (int32_t)rowlen - (int32_t)fb);
+            }
+            uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) {
+                const uint32_t p = c + k;
+                uint32_t byte = 0;
+                if (o + k < len) {
+                    if (p < rowlen) byte = p < fb ? 0u : byte_of(x1, k);
+                    else byte = (p - rowlen) < fb ? 0u : byte_of(x2, k);
+                }
+                wv[k >> 2] |= byte << ((k & 3) * 8);
+            }
+            v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+        *(uint4*)(out + o) = v;
+    }
+}
+
+hipError_t launch_rows(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nblocks,
+                       uint8_t* stream) {
+    if (!ntiles || !nblocks) return hipSuccess;
+    hipLaunchKernelGGL(k_rows, dim3(nblocks), dim3(RW_NT), 0, st, d_tiles, ntiles, stream);
+    return hipGetLastError();
+}
+
 hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                          uint32_t nblocks, uint8_t* stream) {
     if (!ntiles || !nblocks) return hipSuccess;

@@ -5,8 +5,12 @@
 
 namespace pbx {
 
-// 512 threads (8 waves), 16 KiB segments with an 8 KiB look-back window, 4096-entry hash.
-using DeflateMainCfg = DeflateCfg<512, 16384, 8192, 12>;
+// 512 threads (8 waves), 16 KiB segments with an 8 KiB look-back window, 2^PBX_HBITS-entry
+// hash (PBX_HBITS overridable for experiments only).
+#ifndef PBX_HBITS
+#define PBX_HBITS 10
+#endif
+using DeflateMainCfg = DeflateCfg<512, 16384, 8192, PBX_HBITS>;
 
 // Per-segment HBM records between the deflate kernels (32-bit words).
 constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram

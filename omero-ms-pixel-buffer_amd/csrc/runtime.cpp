@@ -157,6 +157,7 @@ struct pbx_batch {
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
     uint32_t ext_blocks = 0, nseg = 0, filt_blocks = 0;
+    uint32_t nrows_tiles = 0, rows_blocks = 0;  // dt[0..nrows_tiles): k_rows tiles, the rest banded
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -439,6 +440,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->h.resize(n);
     const int filter = ctx->cfg.png_filter;
     const bool tiff_deflate = ctx->cfg.tiff_deflate != 0;
+    std::vector<TileDesc> dt_rows, dt_band;
+    std::vector<uint32_t> req_rows, req_band;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane pl;
@@ -483,18 +486,35 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                 d.rowlen = (uint32_t)w * bpp;
             }
             d.stream_len = (uint64_t)h * d.rowlen;
-            deflate_split(d.stream_len, d.seg_count, d.seg_len);
-            d.seg_first = b->nseg;
-            b->nseg += d.seg_count;
-            d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
-            b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
-            d.blk_first = b->filt_blocks;
-            b->filt_blocks += (uint32_t)((h + filter_band_rows() - 1) / filter_band_rows());
-            b->stream_bytes += d.stream_len;
-            b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
-            b->dt.push_back(d);
-            b->dt_req.push_back((uint32_t)i);
+            // k_rows (vector funnel copy) serves filter-None rows from 16-byte-aligned
+            // source rows; filtered or odd-shaped tiles go to the banded k_filter
+            const bool rows_ok = d.filter == 0 && d.rowlen >= 32 &&
+                                 ((uint64_t)d.x * bpp % 16) == 0 && d.stream_len < (1ull << 32);
+            (rows_ok ? dt_rows : dt_band).push_back(d);
+            (rows_ok ? req_rows : req_band).push_back((uint32_t)i);
         }
+    }
+    b->nrows_tiles = (uint32_t)dt_rows.size();
+    b->dt = std::move(dt_rows);
+    b->dt.insert(b->dt.end(), dt_band.begin(), dt_band.end());
+    b->dt_req = std::move(req_rows);
+    b->dt_req.insert(b->dt_req.end(), req_band.begin(), req_band.end());
+    for (size_t k = 0; k < b->dt.size(); k++) {
+        TileDesc& d = b->dt[k];
+        deflate_split(d.stream_len, d.seg_count, d.seg_len);
+        d.seg_first = b->nseg;
+        b->nseg += d.seg_count;
+        d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
+        b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
+        if (k < b->nrows_tiles) {
+            d.blk_first = b->rows_blocks;
+            b->rows_blocks += rows_blocks_for(d.stream_len);
+        } else {
+            d.blk_first = b->filt_blocks;
+            b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
+        }
+        b->stream_bytes += d.stream_len;
+        b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
     }
     *out = b;
     return PBX_OK;
@@ -535,7 +555,9 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
-    HIP_TRY(launch_filter(st, (const TileDesc*)b->d_dt, ndt, b->filt_blocks, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_rows(st, (const TileDesc*)b->d_dt, b->nrows_tiles, b->rows_blocks, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter(st, (const TileDesc*)b->d_dt + b->nrows_tiles, ndt - b->nrows_tiles,
+                          b->filt_blocks, (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;

@@ -357,13 +357,24 @@ class PixelsService:
         return out
 
 
+def make_reqs(ctxs: Sequence[TileCtx]):
+    """ctypes array of pbx_tile_req for a request list (reusable across batches)."""
+    return (PbxTileReq * max(len(ctxs), 1))(*[c.to_req() for c in ctxs]) if ctxs else \
+        (PbxTileReq * 1)()
+
+
 class Batch:
     """Device-resident batch (plan once, launch many): outputs stay in HBM until fetch()."""
 
-    def __init__(self, service: PixelsService, ctxs: Sequence[TileCtx]):
+    def __init__(self, service: PixelsService, ctxs: Sequence[TileCtx] = (), reqs=None):
+        """``ctxs``: TileCtx requests; or ``reqs``: a prebuilt ``make_reqs`` array."""
         self.service = service
-        self.n = len(ctxs)
-        self._reqs = (PbxTileReq * max(self.n, 1))(*[c.to_req() for c in ctxs])
+        if reqs is None:
+            self.n = len(ctxs)
+            reqs = make_reqs(ctxs)
+        else:
+            self.n = len(reqs)
+        self._reqs = reqs
         h = ctypes.c_void_p()
         _check(lib().pbx_batch_plan(service.handle, self._reqs, self.n, ctypes.byref(h)))
         self._h = h
