@@ -260,111 +260,106 @@ hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
 
 // ------------------------------------------------------- K1+K2 fast rows (filter None)
 // The stream of a filter-None PNG tile is row r = [0] ++ big-endian row bytes, and of a
-// deflate-TIFF tile the row bytes alone.  Each thread writes aligned 16-byte stream words:
-// 16 bytes of one source row at byte offset s come from two aligned 16-byte loads (byte
-// swap / sign flip applied on the aligned words, where sample boundaries are known) and a
-// funnel shift by s & 15; the ~1/64 of words that straddle a row end are merged bytewise
-// from both rows.  No LDS: neighbouring lanes share the overlapping loads in L1/L2.
-constexpr int RW_NT = 256;
-constexpr int RW_WPT = (int)ROWS_WORDS_PER_BLOCK / RW_NT;
+// deflate-TIFF tile the row bytes alone.  One workgroup per band of RB_ROWS rows (whose
+// stream bytes start and end 16-byte aligned, as RB_ROWS * rowlen is a multiple of 16):
+// the band's source rows are loaded once with aligned 16-byte loads (byte swap and sign
+// flip applied there, where the sample boundaries are known) into LDS rows padded to
+// 16 bytes, then every aligned 16-byte stream word is assembled from 5 LDS words with
+// funnel shifts; the few words that straddle a row end merge two rows with byte masks.
+constexpr int RB_NT = 256;
+constexpr uint32_t RB_ROWS = 16;
 
-struct Rows16 {
-    const uint8_t* row;  // source row start (16-byte aligned), little- or big-endian samples
-    uint32_t rb, bpp;
-    bool swap, flip;
-    __device__ __forceinline__ uint4 fix(uint4 v) const {
-        if (swap) v = swap16(v, (int)bpp);
-        if (flip) v = flip_msb(v, (int)bpp);
-        return v;
-    }
-    // 16 big-endian row bytes starting at byte s (-16 <= s < rb); bytes outside [0, rb)
-    // are unspecified
-    __device__ __forceinline__ uint4 fetch(int32_t s) const {
-        uint4 lo, hi;
-        uint32_t sh;
-        if (s < 0) {
-            lo = make_uint4(0, 0, 0, 0);
-            hi = fix(*(const uint4*)row);
-            sh = (uint32_t)(s + 16);
-        } else {
-            const uint32_t a = (uint32_t)s & ~15u;
-            lo = fix(*(const uint4*)(row + a));
-            sh = (uint32_t)s & 15u;
-            hi = (sh && a + 16 < rb) ? fix(*(const uint4*)(row + a + 16)) : make_uint4(0, 0, 0, 0);
-        }
-        if (!sh) return lo;
-        const uint32_t q = sh >> 2, t = (sh & 3) * 8;
-        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        uint32_t v[5];
-#pragma unroll
-        for (int i = 0; i < 5; i++)
-            v[i] = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
-        if (!t) return make_uint4(v[0], v[1], v[2], v[3]);
-        return make_uint4((v[0] >> t) | (v[1] << (32 - t)), (v[1] >> t) | (v[2] << (32 - t)),
-                          (v[2] >> t) | (v[3] << (32 - t)), (v[3] >> t) | (v[4] << (32 - t)));
-    }
-};
-
-__device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t k) {
-    const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
-    return (w >> ((k & 3) * 8)) & 0xFFu;
+__device__ __forceinline__ uint32_t lds_word4(const uint32_t* rowp, int32_t s, uint32_t i) {
+    // dword i of the 16 bytes of an LDS row starting at byte s (s >= -17): bytes before the
+    // row come from the previous row or the pad and are only ever masked out
+    const int32_t b = s + 4 * (int32_t)i;
+    const int32_t wdx = b >> 2;  // floor
+    const uint32_t w0 = rowp[wdx], w1 = rowp[wdx + 1];
+    return __builtin_amdgcn_alignbit(w1, w0, (uint32_t)(b & 3) * 8);
 }
 
-__global__ __launch_bounds__(RW_NT) void k_rows(const TileDesc* __restrict__ dt, uint32_t ndt,
+// bytes [lo, hi) of dword i (byte index within the 16-byte word) as a mask
+__device__ __forceinline__ uint32_t byte_mask(int32_t lo, int32_t hi, uint32_t i) {
+    const int32_t a = lo - 4 * (int32_t)i, b = hi - 4 * (int32_t)i;
+    const uint32_t ma = a <= 0 ? 0xFFFFFFFFu : a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mb = b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - b)));
+    return ma & mb;
+}
+
+__global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt, uint32_t ndt,
                                                 uint8_t* __restrict__ stream) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lrow[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
     const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
-    const uint32_t rowlen = d.rowlen, len = (uint32_t)d.stream_len;
-    const uint32_t nwords = (len + 15) >> 4;
-    Rows16 R;
-    R.rb = rowlen - fb;
-    R.bpp = d.bpp;
-    R.swap = (d.flags & TF_SWAP) != 0;
-    R.flip = (d.flags & TF_FLIP) != 0;
-    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
-    uint8_t* out = stream + d.out_off;
-    const uint32_t w0 = (b - d.blk_first) * ROWS_WORDS_PER_BLOCK;
+    const uint32_t rowlen = d.rowlen, rb = rowlen - fb, bpp = d.bpp;
+    const uint32_t nc = (rb + 15) >> 4;          // 16-byte chunks per row
+    const uint32_t rw = 4 * nc + 4;               // LDS row stride in words (+16 B pad)
+    const uint32_t r0 = (b - d.blk_first) * RB_ROWS;
+    const uint32_t nr = (uint32_t)d.h - r0 < RB_ROWS ? (uint32_t)d.h - r0 : RB_ROWS;
+    const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
+    const uint8_t* src0 = d.plane + (int64_t)(d.y + r0) * d.pitch + (int64_t)d.x * bpp;
+    // 1. band rows -> LDS (row q at word 4 + q*rw: one pad word before row 0)
+    uint32_t* rows = lrow + 4;
+    for (uint32_t i = tid; i < nr * nc; i += RB_NT) {
+        const uint32_t q = i / nc, c = i - q * nc;
+        uint4 v = *(const uint4*)(src0 + (int64_t)q * d.pitch + 16 * c);
+        if (swap) v = swap16(v, (int)bpp);
+        if (flip) v = flip_msb(v, (int)bpp);
+        *(uint4*)(rows + q * rw + 4 * c) = v;
+    }
+    __syncthreads();
+    // 2. aligned stream words of the band
+    const uint32_t o0 = r0 * rowlen, nb = nr * rowlen, nw = (nb + 15) >> 4;
+    const uint32_t magic = 0xFFFFFFFFu / rowlen;
+    uint8_t* out = stream + d.out_off + o0;
+    for (uint32_t k = tid; k < nw; k += RB_NT) {
+        const uint32_t o = k << 4;
+        uint32_t r = __umulhi(o, magic);
+        if ((r + 1) * rowlen <= o) r++;
+        const uint32_t c = o - r * rowlen;
+        const int32_t s = (int32_t)c - (int32_t)fb;  // data byte of row r at word byte 0
+        const uint32_t* rp = rows + r * rw;
+        uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < RW_WPT; j++) {
-        const uint32_t wi = w0 + (uint32_t)j * RW_NT + tid;
-        if (wi >= nwords) break;
-        const uint32_t o = wi << 4;
-        const uint32_t r = o / rowlen, c = o - r * rowlen;
-        R.row = src0 + (int64_t)r * d.pitch;
-        const uint4 x1 = R.fetch((int32_t)c - (int32_t)fb);
-        uint4 v = x1;
-        if (c < fb || c + 16 > rowlen || o + 16 > len) {
-            // filter byte at the row start, or the word runs into the next row / the end
-            uint4 x2 = make_uint4(0, 0, 0, 0);
-            const bool next = c + 16 > rowlen && r + 1 < (uint32_t)d.h;
-            if (next) {
-                Rows16 R2 = R;
-                R2.row = R.row + d.pitch;
-                x2 = R2.fetch((int32_t)c - (int32_t)rowlen - (int32_t)fb);
-            }
-            uint32_t wv[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < 4; i++) w[i] = lds_word4(rp, s, i);
+        const int32_t k1 = (int32_t)rowlen - (int32_t)c;  // bytes of row r in this word
+        if (s < 0 || k1 < 16 || o + 16 > nb) {
+            // filter byte (row start) / next row's filter byte and data / band end
+            const bool nxt = k1 < 16 && r + 1 < nr;
+            const uint32_t* rq = rows + (r + 1) * rw;
+            const int32_t s2 = s - (int32_t)rowlen;  // data byte of row r+1 at word byte 0
+            const int32_t end = (int32_t)(nb - o) < 16 ? (int32_t)(nb - o) : 16;
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++) {
-                const uint32_t p = c + k;
-                uint32_t byte = 0;
-                if (o + k < len) {
-                    if (p < rowlen) byte = p < fb ? 0u : byte_of(x1, k);
-                    else byte = (p - rowlen) < fb ? 0u : byte_of(x2, k);
-                }
-                wv[k >> 2] |= byte << ((k & 3) * 8);
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t m1 = byte_mask((int32_t)fb - (int32_t)c > 0 ? 1 : 0, k1 < end ? k1 : end, i);
+                uint32_t v = w[i] & m1;
+                if (nxt) v |= lds_word4(rq, s2, i) & byte_mask(k1 + (int32_t)fb, end, i);
+                w[i] = v;
             }
-            v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
-        *(uint4*)(out + o) = v;
+        *(uint4*)(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
+size_t rows_lds_bytes(uint32_t rb) { return 16 + (size_t)RB_ROWS * (4 * ((rb + 15) / 16) + 4) * 4; }
+
 hipError_t launch_rows(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nblocks,
-                       uint8_t* stream) {
+                       uint32_t max_rb, uint8_t* stream) {
     if (!ntiles || !nblocks) return hipSuccess;
-    hipLaunchKernelGGL(k_rows, dim3(nblocks), dim3(RW_NT), 0, st, d_tiles, ntiles, stream);
+    const size_t lds = rows_lds_bytes(max_rb);
+    if (lds > 64 * 1024) {
+        static bool raised = false;  // bands of rows over 4 KiB: allow up to 160 KiB of LDS
+        if (!raised) {
+            const hipError_t e = hipFuncSetAttribute((const void*)k_rows,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     160 * 1024);
+            if (e != hipSuccess) return e;
+            raised = true;
+        }
+    }
+    hipLaunchKernelGGL(k_rows, dim3(nblocks), dim3(RB_NT), lds, st, d_tiles, ntiles, stream);
     return hipGetLastError();
 }
 

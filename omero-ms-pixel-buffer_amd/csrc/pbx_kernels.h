@@ -24,13 +24,12 @@ hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntile
 uint32_t filter_band_rows();
 
 // K1+K2 for filter-None PNG rows and deflate-TIFF rows from 16-byte-aligned source rows:
-// every thread writes aligned 16-byte stream words funnel-shifted from two aligned loads.
+// one workgroup per band of ROWS_BAND rows, staged in LDS, aligned 16-byte stream words.
+constexpr uint32_t ROWS_BAND = 16;
+constexpr uint32_t ROWS_MAX_RB = 8192;  // widest row (bytes) k_rows takes (LDS band <= 132 KB)
 hipError_t launch_rows(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nblocks,
-                       uint8_t* stream);
-constexpr uint32_t ROWS_WORDS_PER_BLOCK = 1024;  // 16-byte words per k_rows workgroup
-inline uint32_t rows_blocks_for(uint64_t stream_len) {
-    return (uint32_t)(((stream_len + 15) / 16 + ROWS_WORDS_PER_BLOCK - 1) / ROWS_WORDS_PER_BLOCK);
-}
+                       uint32_t max_rb, uint8_t* stream);
+inline uint32_t rows_blocks_for(uint32_t h) { return (h + ROWS_BAND - 1) / ROWS_BAND; }
 
 // K3-K6: deflate of every tile's stream into its compacted container.
 struct DeflateLaunch {

@@ -157,7 +157,7 @@ struct pbx_batch {
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
     uint32_t ext_blocks = 0, nseg = 0, filt_blocks = 0;
-    uint32_t nrows_tiles = 0, rows_blocks = 0;  // dt[0..nrows_tiles): k_rows tiles, the rest banded
+    uint32_t nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;  // dt[0..nrows_tiles): k_rows tiles
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -488,8 +488,9 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.stream_len = (uint64_t)h * d.rowlen;
             // k_rows (vector funnel copy) serves filter-None rows from 16-byte-aligned
             // source rows; filtered or odd-shaped tiles go to the banded k_filter
-            const bool rows_ok = d.filter == 0 && d.rowlen >= 32 &&
-                                 ((uint64_t)d.x * bpp % 16) == 0 && d.stream_len < (1ull << 32);
+            const uint32_t rb = (uint32_t)w * bpp;
+            const bool rows_ok = d.filter == 0 && d.rowlen >= 32 && rb <= ROWS_MAX_RB &&
+                                 ((uint64_t)d.x * bpp % 16) == 0;
             (rows_ok ? dt_rows : dt_band).push_back(d);
             (rows_ok ? req_rows : req_band).push_back((uint32_t)i);
         }
@@ -508,7 +509,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
         if (k < b->nrows_tiles) {
             d.blk_first = b->rows_blocks;
-            b->rows_blocks += rows_blocks_for(d.stream_len);
+            b->rows_blocks += rows_blocks_for((uint32_t)d.h);
+            b->rows_max_rb = std::max<uint32_t>(b->rows_max_rb, d.rowlen - ((d.flags & TF_PNGROWS) ? 1u : 0u));
         } else {
             d.blk_first = b->filt_blocks;
             b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
@@ -555,7 +557,8 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
-    HIP_TRY(launch_rows(st, (const TileDesc*)b->d_dt, b->nrows_tiles, b->rows_blocks, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_rows(st, (const TileDesc*)b->d_dt, b->nrows_tiles, b->rows_blocks, b->rows_max_rb,
+                        (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter(st, (const TileDesc*)b->d_dt + b->nrows_tiles, ndt - b->nrows_tiles,
                           b->filt_blocks, (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));

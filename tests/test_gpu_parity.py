@@ -102,6 +102,25 @@ def test_png_decodes_bit_exact(service, oracle, pt, kind):
         assert body[start:start + len(z)] == z
 
 
+@pytest.mark.parametrize("pt", [pbx.UINT16, pbx.INT16, pbx.UINT8])
+def test_png_row_shapes(service, oracle, pt):
+    """Row layouts of the banded row kernel: 2 KiB - 8 KiB rows (large LDS bands), row
+    lengths that are not multiples of 16, band tails, aligned and unaligned starts."""
+    sx, sy = 4200, 41
+    iid, plane = host_plane(service, oracle, pt, sx, sy, kind=2, big_endian=False)
+    bpp = oracle.BPP[pt]
+    regions = [(0, 0, 4096, 20), (0, 1, 2048, 33), (16, 1, 2064, 17), (32, 7, 1000, 34),
+               (8, 0, 777, 41), (0, 0, 31, 16), (0, 0, 15, 3), (4192 // bpp, 2, 8, 39)]
+    ctxs = [pbx.TileCtx(iid, 0, 0, 0, x, y, w, h, format="png") for (x, y, w, h) in regions]
+    res = service.get_tiles(ctxs)
+    for (x, y, w, h), (st, body) in zip(regions, res):
+        assert st == pbx.OK, (x, y, w, h)
+        tile = oracle_tile(oracle, plane, pt, sx, x, y, w, h)
+        stream = oracle.png_filter_stream(np.frombuffer(tile, np.uint8), pt, w, h, 0).tobytes()
+        r, idat = oracle.png_inflate_idat(body, len(stream))
+        assert r == 0 and idat == stream, (pt, x, y, w, h)
+
+
 @pytest.mark.parametrize("pt", [pbx.INT32, pbx.UINT32, pbx.FLOAT, pbx.DOUBLE])
 def test_png_rejects_wide_types(service, oracle, pt):
     iid, _ = host_plane(service, oracle, pt, 40, 30)
