@@ -35,6 +35,13 @@
 #pragma once
 #include "pbx_common.h"
 
+#ifndef PBX_CAP
+#define PBX_CAP 8
+#endif
+#ifndef PBX_PB
+#define PBX_PB 64
+#endif
+
 namespace pbx {
 
 template <int NT_, int SEG_, int WIN_, int HBITS_>
@@ -48,7 +55,8 @@ struct DeflateCfg {
     static constexpr int NW = NT / 64;    // waves
     static constexpr int SUB = SEG / NW;  // positions parsed by one wave
     static constexpr int MAXMW = 256;     // matches kept per wave (then literals only)
-    static constexpr int CAP = 32;        // per-lane match length before the wave extends it
+    static constexpr int CAP = PBX_CAP;   // per-lane match length before the wave extends it
+    static constexpr int PB = PBX_PB;     // positions per parse batch (64 or 128: 1-2 per lane)
     static constexpr int CRCC = 64;       // CRC chunk bytes per thread
     static constexpr int LOG2_CRCC = 6;
     static constexpr int BUFW = (WIN + SEG + 32) / 4;
@@ -164,17 +172,17 @@ PBX_HD bool match_pays(uint32_t len, uint32_t dist) {
 // byte (runs), the previous 2-byte sample, the same column one row up, and the first
 // occurrence of the 3-byte hash.  Longest capped length wins; the first wins ties.
 // The first 4 bytes of every candidate are compared without branches (the distance-1 and
-// -2 windows come from the three words around p); only candidates whose 4 bytes all match
-// run the compare loop up to the cap.
+// -2 windows come from the three words around p, invalid positions read in-bounds words
+// and are masked); only candidates whose 4 bytes all match run the compare loop up to the
+// cap, so on incompressible data the evaluation is straight-line code.
 template <class C, class SM>
 PBX_HD void eval_pos(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t& L,
                      uint32_t& D) {
-    L = 0; D = 0;
-    if (p >= se || se - p < 3) return;
-    const uint32_t rem = se - p;
+    const bool valid = p < se && se - p >= 3;
+    const uint32_t rem = valid ? se - p : 3;
     const uint32_t maxlen = rem < 258 ? rem : 258;
     const uint32_t cap = maxlen < (uint32_t)C::CAP ? maxlen : (uint32_t)C::CAP;
-    const uint32_t a = sp.wl + p;
+    const uint32_t a = sp.wl + (valid ? p : 0u);
     const uint32_t wi = a >> 2, sh = (a & 3) * 8;
     const uint32_t W0 = S.buf[wi > 0 ? wi - 1 : 0], W1 = S.buf[wi], W2 = S.buf[wi + 1];
     const uint32_t cur4 = funnel32(W2, W1, sh);
@@ -183,30 +191,35 @@ PBX_HD void eval_pos(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, 
     const uint32_t j = S.head[hash3<C>(cur4)];
     const uint32_t cand[4] = {1u, 2u, sp.rowlen > 2 ? sp.rowlen : 0u, j < a ? a - j : 0u};
     uint32_t x[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) ok[k] = valid && cand[k] != 0 && cand[k] <= a;
     x[0] = m1 ^ cur4;
     x[1] = m2 ^ cur4;
 #pragma unroll
-    for (int k = 2; k < 4; k++) {
-        const uint32_t d = cand[k];
-        x[k] = lds_ld4(S, d != 0 && d <= a ? a - d : a) ^ cur4;
-    }
+    for (int k = 2; k < 4; k++) x[k] = lds_ld4(S, ok[k] ? a - cand[k] : a) ^ cur4;
+    uint32_t l[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) l[k] = x[k] ? (uint32_t)__builtin_ctz(x[k]) >> 3 : 4u;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const uint32_t d = cand[k];
-        if (d == 0 || d > a) continue;
-        uint32_t l;
-        if (x[k]) {
-            l = (uint32_t)__builtin_ctz(x[k]) >> 3;
-        } else {
-            l = 4;
-            while (l < cap) {
-                const uint32_t y = lds_ld4(S, a - d + l) ^ lds_ld4(S, a + l);
-                if (y) { l += (uint32_t)__builtin_ctz(y) >> 3; break; }
-                l += 4;
+        if (ok[k] && !x[k]) {  // 4 equal bytes: compare on up to the cap
+            uint32_t n = 4;
+            while (n < cap) {
+                const uint32_t y = lds_ld4(S, a - cand[k] + n) ^ lds_ld4(S, a + n);
+                if (y) { n += (uint32_t)__builtin_ctz(y) >> 3; break; }
+                n += 4;
             }
+            l[k] = n;
         }
-        l = l < cap ? l : cap;
-        if (l > L && match_pays(l, d)) { L = l; D = d; }
+    }
+    L = 0; D = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t n = l[k] < cap ? l[k] : cap;
+        const bool take = ok[k] && n > L && match_pays(n, cand[k]);
+        L = take ? n : L;
+        D = take ? cand[k] : D;
     }
 }
 
@@ -237,21 +250,17 @@ PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
     const uint32_t ss = w * C::SUB;
     const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
     uint32_t nm = 0, pos = ss;
-    uint32_t Ls[64], Ds[64];
+    uint32_t Ls[C::PB], Ds[C::PB];
     while (pos < se) {
-        uint64_t mask = 0;
-        for (uint32_t l = 0; l < 64; l++) {
-            eval_pos<C>(S, sp, pos + l, se, Ls[l], Ds[l]);
-            if (Ls[l] >= 3) mask |= 1ull << l;
-        }
+        for (uint32_t l = 0; l < (uint32_t)C::PB; l++) eval_pos<C>(S, sp, pos + l, se, Ls[l], Ds[l]);
         uint32_t o = 0;
-        while (o < 64) {
-            const uint64_t m = mask >> o;
-            if (!m) { o = 64; break; }
-            const uint32_t k = o + (uint32_t)__builtin_ctzll(m);
+        while (o < (uint32_t)C::PB) {
+            uint32_t k = o;
+            while (k < (uint32_t)C::PB && Ls[k] < 3) k++;
+            if (k == (uint32_t)C::PB) { o = C::PB; break; }
             uint32_t L = Ls[k];
             const uint32_t D = Ds[k];
-            if (k + 1 < 64 && Ls[k + 1] > L) { o = k + 1; continue; }  // lazy
+            if (k + 1 < (uint32_t)C::PB && Ls[k + 1] > L) { o = k + 1; continue; }  // lazy
             L = extend_scalar<C>(S, sp, pos + k, se, L, D);
             if (nm < (uint32_t)C::MAXMW) {
                 S.mpos[w * C::MAXMW + nm] = (pos + k) | ((L - 3) << 16);

@@ -110,6 +110,8 @@ __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, 
 // Wave-serial greedy parse of one sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).
 template <class C, class SM>
 __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
+    constexpr int NB = C::PB / 64;  // positions per lane per batch
+    static_assert(NB == 1 || NB == 2, "64 or 128 positions per batch");
     // every loop-carried value is wave-uniform: readfirstlane keeps it in SGPRs, so the
     // walk below is scalar code, not exec-masked vector code
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -117,18 +119,33 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
     const uint32_t se = __builtin_amdgcn_readfirstlane(ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl);
     uint32_t nm = 0, pos = ss;
     while (pos < se) {
-        uint32_t L, D;
-        eval_pos<C>(S, sp, pos + lane, se, L, D);
-        const uint64_t mask = __ballot(L >= 3);
+        uint32_t Lv[NB], Dv[NB];  // positions pos + 64 b + lane
+        uint64_t mv[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) eval_pos<C>(S, sp, pos + 64 * b + lane, se, Lv[b], Dv[b]);
+#pragma unroll
+        for (int b = 0; b < NB; b++) mv[b] = __ballot(Lv[b] >= 3);
+        auto at = [&](const uint32_t (&v)[NB], uint32_t k) {
+            if (NB == 1 || k < 64) return __builtin_amdgcn_readlane(v[0], k & 63);
+            return __builtin_amdgcn_readlane(v[NB - 1], k & 63);
+        };
         uint32_t o = 0;
-        while (o < 64) {
-            const uint64_t m = mask >> o;
-            if (!m) { o = 64; break; }
-            const uint32_t k = __builtin_amdgcn_readfirstlane(o + (uint32_t)__builtin_ctzll(m));
-            uint32_t Lk = __builtin_amdgcn_readlane(L, k);
-            const uint32_t Dk = __builtin_amdgcn_readlane(D, k);
-            if (k + 1 < 64) {
-                const uint32_t L1 = __builtin_amdgcn_readlane(L, k + 1);
+        while (o < (uint32_t)C::PB) {
+            uint32_t k = C::PB;
+#pragma unroll
+            for (int b = NB - 1; b >= 0; b--) {  // first set bit at or after o
+                const uint32_t lo = 64u * b;
+                if (o < lo + 64) {
+                    const uint64_t m = o > lo ? mv[b] >> (o - lo) : mv[b];
+                    if (m) k = (o > lo ? o : lo) + (uint32_t)__builtin_ctzll(m);
+                }
+            }
+            if (k >= (uint32_t)C::PB) { o = C::PB; break; }
+            k = __builtin_amdgcn_readfirstlane(k);
+            uint32_t Lk = at(Lv, k);
+            const uint32_t Dk = at(Dv, k);
+            if (k + 1 < (uint32_t)C::PB) {
+                const uint32_t L1 = at(Lv, k + 1);
                 if (L1 > Lk) { o = k + 1; continue; }  // lazy: a longer match starts next
             }
             const uint32_t p = pos + k;

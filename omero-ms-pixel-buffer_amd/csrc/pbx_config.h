@@ -5,12 +5,16 @@
 
 namespace pbx {
 
-// 512 threads (8 waves), 16 KiB segments with an 8 KiB look-back window, 2^PBX_HBITS-entry
-// hash (PBX_HBITS overridable for experiments only).
+// 512 threads (8 waves), 16 KiB segments with a PBX_WIN-byte look-back window, 2^PBX_HBITS-entry
+// hash (both overridable for experiments only; 4 KiB / 2^10 compress G_NOISE tiles within
+// 0.05% of 8 KiB / 2^12 and fit four LZ77 workgroups per CU).
 #ifndef PBX_HBITS
 #define PBX_HBITS 10
 #endif
-using DeflateMainCfg = DeflateCfg<512, 16384, 8192, PBX_HBITS>;
+#ifndef PBX_WIN
+#define PBX_WIN 4096
+#endif
+using DeflateMainCfg = DeflateCfg<512, 16384, PBX_WIN, PBX_HBITS>;
 
 // Per-segment HBM records between the deflate kernels (32-bit words).
 constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram

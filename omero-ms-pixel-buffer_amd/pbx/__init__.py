@@ -26,7 +26,7 @@ import os
 from typing import Iterable, List, Mapping, Optional, Sequence, Tuple
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
+LIB_PATH = os.environ.get("PBX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
 
 # enum pbx_status — the HTTP status the reference ends with
 OK, E_BADARG, E_NOTFOUND, E_INTERNAL = 0, 400, 404, 500

@@ -19,6 +19,8 @@ for _ in range(n):
     b.launch()
     b.sync()
     s = b.stats()
-    print(gen, "deflate ms", round(s.ms_deflate, 3), "filter ms", round(s.ms_filter, 3), flush=True)
+    print(gen, "deflate ms", round(s.ms_deflate, 3), "lz77", round(s.ms_lz77, 3), "huff",
+          round(s.ms_huff, 3), "encode", round(s.ms_encode, 3), "filter ms", round(s.ms_filter, 3),
+          "out", s.deflate_out_bytes, flush=True)
     b.close()
 svc.close()
