@@ -56,18 +56,35 @@ struct HuffSmem {
 
 template <class C>
 struct EncSmem {
-    alignas(16) uint32_t buf[C::SEGW];
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
     uint32_t lcode[288], dcode[32];
-    uint32_t out[C::OUTW];
+    alignas(16) uint32_t out[C::OUTW];
     uint32_t crc_t[4][256];
     uint32_t misc[M_NMISC];
     uint32_t t_a[C::NT];
     uint32_t wtot[16];
     uint32_t red[C::NW];
 };
+
+// Slicing-by-4 CRC-32 tables, built at compile time into device memory (copied to LDS).
+struct CrcTables {
+    uint32_t t[4][256];
+};
+constexpr uint32_t crc_entry_c(uint32_t n) {
+    uint32_t c = n;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? CRC_POLY ^ (c >> 1) : c >> 1;
+    return c;
+}
+constexpr CrcTables make_crc_tables() {
+    CrcTables T{};
+    for (uint32_t i = 0; i < 256; i++) T.t[0][i] = crc_entry_c(i);
+    for (int k = 1; k < 4; k++)
+        for (uint32_t i = 0; i < 256; i++) T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xFF];
+    return T;
+}
+__constant__ const CrcTables kCrcTables = make_crc_tables();
 
 // Segment geometry from the tile descriptor.
 __device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k, uint32_t win) {
@@ -656,6 +673,65 @@ __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
     return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
 }
 
+// A token's bits packed in one register: value (<= 20 bits) | nbits << 27.
+__device__ __forceinline__ uint32_t slot_of(uint32_t code, uint32_t extra, uint32_t ebits) {
+    const uint32_t n = code >> 16;
+    return (code & 0xFFFFu) | (extra << n) | ((n + ebits) << 27);
+}
+
+// The thread's CH positions as register slots, in stream order: slot i holds the literal
+// or length code (+ extra bits) of a token starting at chunk position i; a match also
+// fills slots i+1 (distance code) and i+2 (distance extra bits), positions it covers.
+// Same tokens as walk_tokens (deflate_seg.h) over the same match lists; the chunk's bytes
+// come from registers instead of LDS.
+template <class C, class SM>
+__device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const SegParams& sp,
+                                            const uint32_t (&cb)[C::CH / 4],
+                                            uint32_t (&slot)[C::CH + 2]) {
+#pragma unroll
+    for (int i = 0; i < C::CH + 2; i++) slot[i] = 0;
+    const uint32_t cs = tid * C::CH;
+    if (cs >= sp.sl) return;
+    const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
+    const uint32_t w = cs / C::SUB;
+    const uint32_t* mp = S.mpos + w * C::MAXMW;
+    const auto* md = S.mdist + w * C::MAXMW;
+    const uint32_t nm = S.w_nm[w];
+    uint32_t lo = 0, hi = nm;  // first match starting at or after cs
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((mp[mid] & 0xFFFFu) < cs) lo = mid + 1; else hi = mid;
+    }
+    uint32_t pos = cs;
+    if (lo > 0) {
+        const uint32_t pe = (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3;
+        if (pe > pos) pos = pe;
+    }
+    uint32_t m = lo;
+    uint32_t nxt = m < nm ? mp[m] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)C::CH; i++) {
+        const uint32_t p = cs + i;
+        if (p < ce && p >= pos) {
+            if (p == (nxt & 0xFFFFu)) {
+                const uint32_t len = (nxt >> 16) + 3, dist = (uint32_t)md[m] + 1;
+                uint32_t sy, e, v;
+                len_code(len, sy, e, v);
+                slot[i] = slot_of(S.lcode[sy], v, e);
+                dist_code(dist, sy, e, v);
+                slot[i + 1] = slot_of(S.dcode[sy], 0, 0);
+                slot[i + 2] = v | (e << 27);
+                pos = p + len;
+                m++;
+                nxt = m < nm ? mp[m] : 0xFFFFFFFFu;
+            } else {
+                const uint32_t b = (cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+                slot[i] = slot_of(S.lcode[b], 0, 0);
+            }
+        }
+    }
+}
+
 template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ dt, uint32_t ndt,
                                                   uint32_t nseg, const uint8_t* __restrict__ stream,
@@ -665,6 +741,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
                                                   const uint64_t* __restrict__ offs,
                                                   uint8_t* __restrict__ out,
                                                   uint64_t* __restrict__ stamps) {
+    static_assert(C::CH == 32, "two 16-byte loads per thread chunk");
     __shared__ EncSmem<C> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
@@ -679,33 +756,85 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
     sp.base += sp.wl;  // the encoder holds the segment only
     sp.wl = 0;
-    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.sl, ((sp.sl + 15) & ~15u) + 16, tid);
+    const SegInfo gi = info[seg];
+    // the thread's chunk bytes (zero past the segment) straight into registers
+    uint32_t cb[C::CH / 4];
+    {
+        const uint32_t cs = tid * C::CH;
+        const uint8_t* src = stream + d.out_off + sp.base + cs;
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
+        if (cs < sp.sl) q0 = *(const uint4*)src;
+        if (cs + 16 < sp.sl) q1 = *(const uint4*)(src + 16);
+        cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
+        cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
+#pragma unroll
+        for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end
+            const int32_t keep = (int32_t)sp.sl - (int32_t)(cs + 4 * k);
+            cb[k] = keep >= 4 ? cb[k] : keep <= 0 ? 0u : cb[k] & ((1u << (8 * keep)) - 1u);
+        }
+    }
     const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
     if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
     const uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
     for (uint32_t i = tid; i < 320; i += C::NT) {
         if (i < 288) S.lcode[i] = cg[i]; else S.dcode[i - 288] = cg[i];
     }
-    ph_enc_init<C>(tid, S, cg + 320);
-    const SegInfo gi = info[seg];
+    for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT) S.out[k] = k < (uint32_t)C::HDRW ? cg[320 + k] : 0u;
+    for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
     if (tid == 0) {
         S.misc[M_BTYPE] = gi.btype; S.misc[M_HDRBITS] = gi.hdr_bits;
         S.misc[M_DATABITS] = gi.data_bits; S.misc[M_NBYTES] = gi.nbytes;
     }
     __syncthreads();
-    if (gi.btype == 0) ph_stored<C>(tid, S, sp);
     for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
         if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
             S.mpos[i] = mg[C::NW + i];
             S.mdist[i] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + i];
         }
     }
+    if (gi.btype == 0) {  // stored block: header byte, LEN, NLEN, then the bytes
+        uint8_t* ob = (uint8_t*)S.out;
+        const uint32_t cs = tid * C::CH;
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
+            if (cs + i < sp.sl) ob[5 + cs + i] = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
+        if (tid == 0) {
+            ob[0] = sp.last ? 1 : 0;
+            ob[1] = (uint8_t)sp.sl; ob[2] = (uint8_t)(sp.sl >> 8);
+            ob[3] = (uint8_t)~sp.sl; ob[4] = (uint8_t)(~sp.sl >> 8);
+        }
+    }
     __syncthreads();
-    S.t_a[tid] = ph_bits<C>(tid, S, sp);
+    uint32_t slot[C::CH + 2];
+    uint32_t nbits = 0;
+    if (gi.btype != 0) {
+        build_slots<C>(tid, S, sp, cb, slot);
+#pragma unroll
+        for (int i = 0; i < C::CH + 2; i++) nbits += slot[i] >> 27;
+    }
+    S.t_a[tid] = nbits;
     __syncthreads();
     stamp();
     const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
-    ph_write<C, DevOps>(tid, S, sp, S.t_a[tid]);
+    if (gi.btype != 0) {
+        RunWriter<DevOps> bw(S.out, gi.hdr_bits + S.t_a[tid]);
+#pragma unroll
+        for (int i = 0; i < C::CH + 2; i++) {
+            const uint32_t n = slot[i] >> 27;
+            if (n) bw.put(slot[i] & 0x7FFFFFFu, n);
+        }
+        bw.finish();
+        if (tid == 0) {  // end of block; a non-final segment ends byte-aligned
+            const uint32_t eob = S.lcode[256];
+            BitWriter<DevOps> ew{S.out, gi.hdr_bits + gi.data_bits - (eob >> 16)};
+            ew.put(eob & 0xFFFF, eob >> 16);
+            if (!sp.last) {
+                ew.put(0, 3);
+                ew.pos = (ew.pos + 7) & ~7u;
+                ew.put(0xFFFF0000u, 32);
+            }
+        }
+    }
     __syncthreads();
     stamp();
     // CRC-32: raw CRC of right-aligned 64-byte chunks, combined per wave by shuffles with

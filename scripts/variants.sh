@@ -1,6 +1,7 @@
 # Time library variants built under omero-ms-pixel-buffer_amd/lib/var_*/ (experiments).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
+shopt -s nullglob
 for d in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_*/libpbx.so; do
   for g in noise fake; do
     echo "== $d $g"
