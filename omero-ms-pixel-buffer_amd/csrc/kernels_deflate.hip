@@ -52,6 +52,8 @@ struct HuffSmem {
     uint32_t rle[320], rboff[SORTN], rbm[10];
     uint32_t hdrw[C::HDRW];
     uint32_t misc[M_NMISC];
+    uint16_t rst[2][290];  // first internal node of every merge round (+ the end)
+    uint32_t nrounds[2];
 };
 
 template <class C>
@@ -302,14 +304,21 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the jump rounds)
     uint16_t* M = &S.hs.aB[0][0];     // merged prefix: leaf index | 0x8000, or internal index
     uint32_t* rq = S.hs.rec[T];
-    if (n < 2) return;
+    uint16_t* rs = S.rst[T];
+    if (n < 2) {
+        if (lane == 0) S.nrounds[T] = 0;
+        return;
+    }
     if (lane == 0) {
         iq[0] = (uint16_t)(key_weight(sk[0]) + key_weight(sk[1]));
         rq[0] = 2u << 20;
+        rs[0] = 0;
     }
-    uint32_t li = 2, qi = 0, ni = 1;
+    uint32_t li = 2, qi = 0, ni = 1, nr = 1;
     __syncthreads();
     while (ni + 1 < n) {
+        if (lane == 0) rs[nr] = (uint16_t)ni;  // this round creates nodes ni..
+        nr++;
         const uint32_t W = iq[ni - 1];
         uint32_t a = 0;
         for (uint32_t c = li; c < n; c += 64) {  // leaves are sorted: count those <= W
@@ -368,6 +377,29 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
         li += lb;
         qi += 2 * m - lb;
         ni += m;
+        __syncthreads();
+    }
+    if (lane == 0) {
+        rs[nr] = (uint16_t)ni;
+        S.nrounds[T] = nr;
+    }
+}
+
+// Depth of every internal node, root first: a node's parent is created in a later merge
+// round, so the rounds taken in reverse order each resolve in one parallel step (instead
+// of pointer jumping).  Result in dB, as ph_jump leaves it.
+template <class SM>
+__device__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(S.nrounds[T]);
+    if (nr == 0) return;
+    uint16_t* dd = S.hs.dB[T];
+    const uint16_t* par = S.hs.aA[T];
+    const uint32_t root = S.rst[T][nr] - 1u;  // the last round creates only the root
+    if (lane == 0) dd[root] = 0;
+    __syncthreads();
+    for (int32_t r = (int32_t)nr - 2; r >= 0; r--) {
+        const uint32_t k0 = S.rst[T][r], k1 = S.rst[T][r + 1];
+        for (uint32_t k = k0 + lane; k < k1; k += 64) dd[k] = (uint16_t)(dd[par[k]] + 1);
         __syncthreads();
     }
 }
@@ -565,11 +597,8 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     ph_parents<C>(tid, S);
     __syncthreads();
     stamp();
-#pragma unroll 1
-    for (int r = 0; r < JUMP_ROUNDS; r++) {
-        ph_jump<C>(tid, S, r);
-        __syncthreads();
-    }
+    depths_wave(S, 0, tid);
+    depths_wave(S, 1, tid);
     stamp();
     ph_leafdepth<C, DevOps>(tid, S);
     __syncthreads();
