@@ -40,12 +40,11 @@ def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
 
 
 def run_steps(svc, ctxs, steps, warmup, barrier):
-    """Warmup, then `steps` timed steps; returns (seconds, last stats, mean deflate-chain ms,
-    mean k_extract ms, mean host ms per step).
+    """Warmup, then `steps` timed steps; returns (seconds, per-step stats, mean host ms).
 
     Steps are pipelined two deep, as a server feeds its GPU: the host plans and launches
     batch k+1 (request validation, descriptors, upload) while batch k runs, then waits for
-    batch k.  The request array is built once (the caller's TileCtx list)."""
+    batch k (its own completion event).  The request array is built once."""
     reqs = pbx.make_reqs(ctxs)
 
     def one_pass(n, record):
@@ -78,20 +77,53 @@ def run_steps(svc, ctxs, steps, warmup, barrier):
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    n = len(stats)
-    return (dt, stats[-1], sum(s.ms_deflate + s.ms_assemble for s in stats) / n,
-            sum(s.ms_extract for s in stats) / n, 1000.0 * host / n)
+    return dt, stats, 1000.0 * host / len(stats)
 
 
-def fetch_rate(svc, ctxs):
-    """End-to-end incl. D2H to pinned host memory (PCIe-inclusive; never the headline)."""
-    b = pbx.Batch(svc, ctxs)
-    t0 = time.perf_counter()
-    b.launch()
-    res = b.fetch()
+def mean(stats, field):
+    return sum(getattr(s, field) for s in stats) / len(stats)
+
+
+def e2e_rate(svc, ctxs, batches=6):
+    """End-to-end incl. D2H into pinned host memory (PCIe-inclusive; never the headline):
+    batches pipelined two deep, batch k's D2H (copy stream) overlapping batch k+1's
+    kernels, after two warmup batches (pinned pool populated)."""
+    reqs = pbx.make_reqs(ctxs)
+    q, nbytes, t0 = [], 0, None
+    for k in range(batches + 2 + 1):
+        if k == 2:
+            torch.cuda.synchronize()
+            t0, nbytes = time.perf_counter(), 0
+        if k < batches + 2:
+            b = pbx.Batch(svc, reqs=reqs)
+            b.launch()
+            q.append(b)
+        if len(q) == 2 or (k == batches + 2 and q):
+            f = q.pop(0)
+            nbytes += f.fetch_into_host()
+            f.close()
+    while q:
+        f = q.pop(0)
+        nbytes += f.fetch_into_host()
+        f.close()
     dt = time.perf_counter() - t0
-    b.close()
-    return len(ctxs) / dt, sum(len(x) for _, x in res if x)
+    return len(ctxs) * batches / dt, nbytes / dt / 1e9
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/*pmc*/traffic.json, written by scripts/pmc_summary.py: FETCH_SIZE doubled
+    per the gfx950 rule + WRITE_SIZE, same workload as this bench's batch)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    k = t.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(seconds=10.0, threads=16):
@@ -107,6 +139,80 @@ def cpu_baseline(seconds=10.0, threads=16):
             "sample": f"{n} tiles 512x512 uint16 G_NOISE -> PNG (filter None, zlib level 6) "
                       f"from a 4096x4096 plane, oracle/pbx_oracle.c on {threads} threads, "
                       f"{sec:.1f} s; avg {nbytes / n:.0f} B/tile"}
+
+
+def extra(out, svc, rank, world, barrier, iid, side):
+    """Secondary lines: the other BASELINE configs (parity-tested in tests/), each timed
+    device-resident like the headline; and the PCIe-inclusive end-to-end rate."""
+    # PCIe-inclusive end-to-end (D2H of every PNG into pinned host memory)
+    rate, gbs = e2e_rate(svc, grid_ctxs(iid, "png"))
+    out["e2e_with_d2h"] = {"tiles_per_s": round(rate, 1), "d2h_gbps": round(gbs, 1)}
+    # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
+    raw = grid_ctxs(iid, None)
+    dtr, sr, _ = run_steps(svc, raw, 5, 1, barrier)
+    ms_ext = mean(sr, "ms_extract")
+    out["raw_4096x512x512_u16"] = {
+        "tiles_per_s": round(len(raw) * 5 * world / dtr, 1),
+        "k_extract_ms": round(ms_ext, 3),
+        "k_extract_gbps": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9, 1),
+        "k_extract_frac": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    # G_FAKE (FakeReader-like gradient) PNG, compressible data
+    svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
+    fk = grid_ctxs(2, "png")
+    dtf, sf, _ = run_steps(svc, fk, 3, 1, barrier)
+    out["png_fake_4096x512x512_u16"] = {
+        "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
+        "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1),
+        "deflate_chain_ms": round(mean(sf, "ms_deflate") + mean(sf, "ms_assemble"), 3)}
+    # configs[2]: 4096 x 1024^2 uint16 PNG from a 65536^2 plane (8 GiB)
+    svc.register_plane(3, 0, 0, 0, pbx.UINT16, 65536, 65536, generator="noise", plane_no=rank)
+    c3 = grid_ctxs(3, "png", tile=1024)
+    dt3, s3, _ = run_steps(svc, c3, 2, 1, barrier)
+    out["c3_png_4096x1024x1024_u16"] = {
+        "tiles_per_s": round(len(c3) * 2 * world / dt3, 1),
+        "compressed_bytes_per_tile": round(s3[-1].deflate_out_bytes / len(c3), 1)}
+    # configs[3]: whole slide 100000^2 uint16, 512^2 tiles (edge 160 px) -> TIFF; this rank's
+    # band of tile rows of one channel (the 5 channels are independent, equal cost)
+    n = (100000 + 511) // 512
+    svc.register_plane(4, 0, 0, 0, pbx.UINT16, 100000, 100000, generator="noise", plane_no=rank)
+    lo, hi = pbx.band_rows(n, world, rank)
+    c4 = [pbx.TileCtx(4, 0, 0, 0, 512 * tx, 512 * ty, min(512, 100000 - 512 * tx),
+                      min(512, 100000 - 512 * ty), format="tif")
+          for ty in range(lo, hi) for tx in range(n)]
+    dt4, s4, _ = run_steps(svc, c4, 2, 1, barrier)
+    out["c4_wholeslide_tif_100k_u16_1ch"] = {
+        "tiles": len(c4) * world, "tiles_per_s": round(len(c4) * 2 * world / dt4, 1),
+        "k_extract_gbps": round(2 * s4[-1].in_bytes / (mean(s4, "ms_extract") * 1e-3) / 1e9, 1)}
+    # configs[4]: mixed stream (uint8/int32/float32 planes 16384^2, w,h in 256..2048,
+    # png/tif/raw), 16384 requests as 8 batches of 2048
+    import random
+    rnd = random.Random(rank)
+    for k, pt in enumerate((pbx.UINT8, pbx.INT32, pbx.FLOAT)):
+        svc.register_plane(10 + k, 0, 0, 0, pt, 16384, 16384, generator="noise", plane_no=rank)
+    reqs5 = []
+    for _ in range(16384):
+        k = rnd.randrange(3)
+        w, h = 256 * rnd.randint(1, 8), 256 * rnd.randint(1, 8)
+        reqs5.append(pbx.TileCtx(10 + k, 0, 0, 0, rnd.randrange(16384 - w + 1),
+                                 rnd.randrange(16384 - h + 1), w, h,
+                                 format=rnd.choice([None, "png", "tif"])))
+    ok = err = 0
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(0, len(reqs5), 2048):
+        b = pbx.Batch(svc, reqs5[j:j + 2048])
+        b.launch()
+        b.sync()
+        s = b.stats()
+        ok += s.ok_tiles
+        err += s.tiles - s.ok_tiles
+        b.close()
+    torch.cuda.synchronize()
+    barrier()
+    dt5 = time.perf_counter() - t0
+    out["c5_mixed_16384_requests"] = {"tiles_per_s": round(ok * world / dt5, 1),
+                                      "ok": ok, "errors_404": err}
 
 
 def main():
@@ -133,7 +239,7 @@ def main():
     svc.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0,
                        plane_no=rank)
     ctxs = grid_ctxs(iid, "png")
-    dt, st, ms_deflate, _, host_ms = run_steps(svc, ctxs, args.steps, args.warmup, barrier)
+    dt, stats, host_ms = run_steps(svc, ctxs, args.steps, args.warmup, barrier)
     t = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -141,12 +247,31 @@ def main():
     tiles_total = len(ctxs) * world * args.steps
     value = tiles_total / dt
     ms_per_step = 1000.0 * dt / args.steps
+    st = stats[-1]
 
-    # roofline of the dominant kernel (k_deflate): algorithmic bytes = tile bytes read
-    # from the plane + compressed bytes written, per launch, / average launch duration
-    deflate_payload = st.deflate_out_bytes - len(ctxs) * 121  # minus PNG framing bytes
-    alg_bytes = st.in_bytes + deflate_payload
-    achieved = alg_bytes / (ms_deflate * 1e-3) / 1e9
+    # Per-kernel algorithmic bytes per launch over the kernel's mean
+    # HIP-event duration on the library's stream:
+    #   k_rows   tile bytes read + filtered stream written (w*h*bpp + h*(1+w*bpp))
+    #   k_lz77   stream bytes read + per-segment symbol histogram written (1280 B)
+    #   k_huff   histograms read + codes/header written per segment (1280 + 1920 B)
+    #   k_encode stream bytes read + compressed bytes written
+    payload = st.deflate_out_bytes - len(ctxs) * 121  # zlib payload (minus PNG framing)
+    seg = st.segments
+    kern = {
+        "k_rows": (mean(stats, "ms_filter"), st.in_bytes + st.stream_bytes),
+        "k_lz77": (mean(stats, "ms_lz77"), st.stream_bytes + 1280 * seg),
+        "k_huff": (mean(stats, "ms_huff"), 3200 * seg),
+        "k_encode": (mean(stats, "ms_encode"), st.stream_bytes + payload),
+    }
+    kernels = {k: {"ms": round(ms, 3), "alg_bytes": int(b),
+                   "gbps": round(b / (ms * 1e-3) / 1e9, 1),
+                   "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+               for k, (ms, b) in kern.items()}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_bytes = kern[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(dom)
+    chain_ms = mean(stats, "ms_deflate") + mean(stats, "ms_assemble")
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -159,43 +284,20 @@ def main():
                    "parallelism": f"dp{world} (request sharding, no collectives)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None,
-                     "kernel": "deflate chain k_lz77+k_huff+k_seg_sizes+k_scan_offsets+k_encode+k_frame",
-                     "kernel_ms": round(ms_deflate, 3),
-                     "alg_bytes_per_launch": int(alg_bytes),
-                     "alg_bytes_def": "PNG end-to-end w*h*bpp + out_len per tile (SURVEY 8d)"},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": dom, "kernel_ms": round(dom_ms, 3),
+                     "alg_bytes_per_launch": int(dom_bytes),
+                     "note": "deflate kernels are LDS/ALU/latency-bound integer work, not "
+                             "HBM-bound; k_rows (the HBM-bound filter kernel) is in kernels"},
+        "kernels": kernels,
+        "deflate_chain_ms": round(chain_ms, 3),
         "hbm_gbps_step": round((st.in_bytes + st.deflate_out_bytes) * world * args.steps / dt / 1e9, 1),
         "compressed_bytes_per_tile": round(st.deflate_out_bytes / len(ctxs), 1),
-        "kernel_ms": {"extract": round(st.ms_extract, 3), "filter": round(st.ms_filter, 3),
-                      "lz77": round(st.ms_lz77, 3), "huff": round(st.ms_huff, 3),
-                      "encode": round(st.ms_encode, 3), "deflate": round(st.ms_deflate, 3),
-                      "frame": round(st.ms_assemble, 3), "total": round(st.ms_total, 3)},
-        "filter_gbps": round((st.in_bytes + st.stream_bytes) / (st.ms_filter * 1e-3) / 1e9, 1),
-        "filter_frac": round((st.in_bytes + st.stream_bytes) / (st.ms_filter * 1e-3) / 1e9
-                             / HBM_PEAK_GBPS, 4),
         "host_ms_per_step": round(host_ms, 3),
     }
 
     if not args.no_extra:
-        # PCIe-inclusive end-to-end (D2H of every PNG to pinned memory)
-        rate, nbytes = fetch_rate(svc, ctxs)
-        out["e2e_with_d2h_tiles_per_s"] = round(rate, 1)
-        # raw path (BASELINE configs[1]): extraction + byte swap, HBM-bound k_extract
-        raw = grid_ctxs(iid, None)
-        dtr, sr, _, ms_ext, _ = run_steps(svc, raw, 5, 1, barrier)
-        out["raw_4096x512x512_u16"] = {
-            "tiles_per_s": round(len(raw) * 5 * world / dtr, 1),
-            "k_extract_ms": round(ms_ext, 3),
-            "k_extract_gbps": round(2 * sr.in_bytes / (ms_ext * 1e-3) / 1e9, 1),
-            "k_extract_frac": round(2 * sr.in_bytes / (ms_ext * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
-        # G_FAKE (FakeReader-like gradient) PNG, compressible data
-        svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
-        fk = grid_ctxs(2, "png")
-        dtf, sf, msf, _, _ = run_steps(svc, fk, 3, 1, barrier)
-        out["png_fake_4096x512x512_u16"] = {
-            "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
-            "compressed_bytes_per_tile": round(sf.deflate_out_bytes / len(fk), 1),
-            "k_deflate_ms": round(msf, 3)}
+        extra(out, svc, rank, world, barrier, iid, side)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(threads=args.cpu_threads)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 1
+#define PBX_ABI_VERSION 2
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -70,6 +70,9 @@ typedef struct pbx_config {
     int32_t tiff_deflate;    /* 0 = uncompressed TIFF (reference default); 1 = Compression=8 */
     int32_t segment_bytes;   /* deflate segment size (bytes of filtered stream); 0 = default */
     uint64_t max_batch_bytes;/* device scratch budget per batch; 0 = default */
+    int32_t coalesce;        /* 1 (default) = concurrent pbx_get_tile calls are coalesced into
+                                batches (one per GPU-busy interval); 0 = one batch per call */
+    int32_t reserved;
 } pbx_config;
 
 typedef struct pbx_ctx pbx_ctx;
@@ -126,7 +129,9 @@ typedef struct pbx_result {
     void* owner;             /* internal */
 } pbx_result;
 
-/* Synchronous single tile: TileRequestHandler.getTile (TileRequestHandler.java:80-139). */
+/* Synchronous single tile: TileRequestHandler.getTile (TileRequestHandler.java:80-139).
+ * Called from many threads at once (the Vert.x worker pool, PixelBufferVerticle.java:109-110),
+ * requests are coalesced: all requests that arrive while the GPU is busy become one batch. */
 int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out);
 /* Synchronous batch: n independent getTile calls executed as one set of GPU launches. */
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out);
@@ -167,6 +172,9 @@ const char* pbx_content_type(const char* format_str);
 int pbx_format_from_string(const char* format_str);
 int pbx_pixel_type_from_string(const char* name);
 int pbx_bytes_per_pixel(int32_t pixel_type);
+
+/* Batches launched and requests served so far by this context (coalescing check). */
+int pbx_ctx_stats_get(pbx_ctx* ctx, uint64_t* batches, uint64_t* requests);
 
 /* Synchronise the context's device (bench/test hook). */
 int pbx_device_synchronize(pbx_ctx* ctx);

@@ -11,9 +11,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -127,12 +131,18 @@ struct Pool {
 
 }  // namespace
 
+struct Coalescer;
+
 struct pbx_ctx {
     int device = 0;
     pbx_config cfg{};
-    hipStream_t stream = nullptr;
-    std::mutex reg_mu;  // plane registry
-    std::mutex run_mu;  // one batch on the stream at a time
+    hipStream_t stream = nullptr;       // kernels (batches run in launch order)
+    hipStream_t copy_stream = nullptr;  // D2H of finished batches, overlapping later kernels
+    std::mutex reg_mu;   // plane registry
+    std::mutex run_mu;   // plan + launch of one batch at a time on the stream
+    std::mutex copy_mu;  // one fetch at a time on the copy stream
+    Coalescer* coal = nullptr;
+    std::atomic<uint64_t> n_batches{0}, n_requests{0};
     std::unordered_map<uint64_t, Plane> planes;
     std::map<std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>, uint64_t> index;
     std::unordered_map<int64_t, Image> images;
@@ -228,6 +238,181 @@ void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
 
 }  // namespace
 
+// One synchronous batch: plan + launch under run_mu (launches stay in order on the
+// kernel stream), then the fetch outside it, so that concurrent callers overlap one
+// batch's D2H with the next batch's kernels.  A device failure fails every request of the
+// batch with 500 (PixelBufferVerticle.java:141-146).
+static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out) {
+    pbx_batch* b = nullptr;
+    int st;
+    {
+        std::lock_guard<std::mutex> run(ctx->run_mu);
+        st = pbx_batch_plan(ctx, reqs, n, &b);
+        if (st) return st;
+        st = pbx_batch_launch(ctx, b);
+    }
+    ctx->n_batches++;
+    ctx->n_requests += n;
+    if (st == PBX_OK) st = pbx_batch_fetch(ctx, b, out);
+    if (st != PBX_OK) {
+        const std::string msg = g_err;
+        for (uint64_t i = 0; i < n; i++) {
+            out[i].status = b->status[i] == PBX_OK ? PBX_E_INTERNAL : b->status[i];
+            out[i].format = reqs[i].format;
+            out[i].w = b->w[i];
+            out[i].h = b->h[i];
+            out[i].data = nullptr;
+            out[i].len = 0;
+            out[i].owner = nullptr;
+        }
+        pbx_batch_destroy(ctx, b);
+        g_err = msg;
+        return st;
+    }
+    pbx_batch_destroy(ctx, b);
+    return PBX_OK;
+}
+
+// Request coalescer behind pbx_get_tile: the reference runs getTile on up to
+// worker_pool_size concurrent Vert.x worker threads, one request each
+// (PixelBufferMicroserviceVerticle.java:117-118,224-233; PixelBufferVerticle.java:109-110).
+// Callers block as before; a launcher thread turns every request queued while the GPU is
+// busy into ONE batch (no fixed time window: an idle GPU takes a lone request at once),
+// with at most DEPTH batches in flight, and a completer thread fetches finished batches
+// (D2H on the copy stream) and wakes their callers.
+struct Coalescer {
+    static constexpr int DEPTH = 2;
+    static constexpr size_t MAX_BATCH = 1 << 16;
+    struct Pending {
+        pbx_tile_req req;
+        pbx_result* out;
+        bool done = false;
+        int rc = PBX_OK;
+        std::string err;
+    };
+    struct Flight {
+        pbx_batch* b;
+        std::vector<Pending*> reqs;
+        int rc;
+        std::string err;
+    };
+    pbx_ctx* ctx;
+    std::mutex mu;
+    std::condition_variable cv_launch, cv_complete, cv_done;
+    std::deque<Pending*> queue;
+    std::deque<Flight> flights;
+    int inflight = 0;
+    bool stop = false;
+    std::thread launcher, completer;
+
+    explicit Coalescer(pbx_ctx* c) : ctx(c) {
+        launcher = std::thread([this] { launch_loop(); });
+        completer = std::thread([this] { complete_loop(); });
+    }
+    ~Coalescer() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv_launch.notify_all();
+        cv_complete.notify_all();
+        launcher.join();
+        completer.join();
+    }
+    int submit(const pbx_tile_req& r, pbx_result* out) {
+        Pending p;
+        p.req = r;
+        p.out = out;
+        std::unique_lock<std::mutex> g(mu);
+        if (stop) return fail(PBX_E_INTERNAL, "context is shutting down");
+        queue.push_back(&p);
+        cv_launch.notify_one();
+        cv_done.wait(g, [&] { return p.done; });
+        if (p.rc != PBX_OK) g_err = p.err;
+        return p.rc;
+    }
+    void launch_loop() {
+        (void)hipSetDevice(ctx->device);
+        for (;;) {
+            std::vector<Pending*> take;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv_launch.wait(g, [&] { return (stop && queue.empty()) || (!queue.empty() && inflight < DEPTH); });
+                if (queue.empty()) break;  // stopping, nothing left
+                while (!queue.empty() && take.size() < MAX_BATCH) {
+                    take.push_back(queue.front());
+                    queue.pop_front();
+                }
+                inflight++;
+            }
+            std::vector<pbx_tile_req> reqs(take.size());
+            for (size_t i = 0; i < take.size(); i++) reqs[i] = take[i]->req;
+            Flight f{nullptr, std::move(take), PBX_OK, {}};
+            {
+                std::lock_guard<std::mutex> run(ctx->run_mu);
+                f.rc = pbx_batch_plan(ctx, reqs.data(), reqs.size(), &f.b);
+                if (f.rc == PBX_OK) f.rc = pbx_batch_launch(ctx, f.b);
+                if (f.rc != PBX_OK) f.err = g_err;
+            }
+            ctx->n_batches++;
+            ctx->n_requests += reqs.size();
+            {
+                std::lock_guard<std::mutex> g(mu);
+                flights.push_back(std::move(f));
+            }
+            cv_complete.notify_one();
+        }
+        std::lock_guard<std::mutex> g(mu);
+        cv_complete.notify_all();
+    }
+    void complete_loop() {
+        (void)hipSetDevice(ctx->device);
+        for (;;) {
+            Flight f;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv_complete.wait(g, [&] { return !flights.empty() || (stop && queue.empty() && inflight == 0); });
+                if (flights.empty()) break;
+                f = std::move(flights.front());
+                flights.pop_front();
+            }
+            const size_t n = f.reqs.size();
+            std::vector<pbx_result> res(n);
+            if (f.rc == PBX_OK) {
+                f.rc = pbx_batch_fetch(ctx, f.b, res.data());
+                if (f.rc != PBX_OK) f.err = g_err;
+            }
+            for (size_t i = 0; i < n; i++) {
+                pbx_result& o = *f.reqs[i]->out;
+                if (f.rc == PBX_OK) {
+                    o = res[i];
+                } else {
+                    const int32_t s = f.b ? f.b->status[i] : PBX_E_INTERNAL;
+                    o.status = s == PBX_OK ? PBX_E_INTERNAL : s;
+                    o.format = f.reqs[i]->req.format;
+                    o.w = f.b ? f.b->w[i] : 0;
+                    o.h = f.b ? f.b->h[i] : 0;
+                    o.data = nullptr;
+                    o.len = 0;
+                    o.owner = nullptr;
+                }
+            }
+            if (f.b) pbx_batch_destroy(ctx, f.b);
+            {
+                std::lock_guard<std::mutex> g(mu);
+                for (Pending* p : f.reqs) {
+                    p->rc = f.rc;
+                    p->err = f.err;
+                    p->done = true;
+                }
+                inflight--;
+            }
+            cv_done.notify_all();
+            cv_launch.notify_one();
+        }
+    }
+};
+
 // ============================================================================ C-ABI
 
 extern "C" {
@@ -277,6 +462,9 @@ int pbx_config_default(pbx_config* cfg) {
     memset(cfg, 0, sizeof *cfg);
     cfg->device = -1;
     cfg->png_filter = PBX_FILTER_NONE;
+    cfg->coalesce = 1;
+    const char* co = getenv("PBX_COALESCE");
+    if (co) cfg->coalesce = atoi(co);
     const char* f = getenv("PBX_PNG_FILTER");
     if (f) cfg->png_filter = atoi(f);
     const char* td = getenv("PBX_TIFF_DEFLATE");
@@ -307,22 +495,28 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     ctx->hpool.pinned = true;
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete ctx;
         return fail(PBX_E_INTERNAL, "init: %s", hipGetErrorString(e));
     }
+    if (cfg.coalesce) ctx->coal = new Coalescer(ctx);
     *out = ctx;
     return PBX_OK;
 }
 
 void pbx_shutdown(pbx_ctx* ctx) {
     if (!ctx) return;
+    delete ctx->coal;  // drains queued requests, joins its threads
+    ctx->coal = nullptr;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->copy_stream);
     for (auto& kv : ctx->planes) (void)hipFree(kv.second.dev);
     ctx->dpool.release_all();
     ctx->hpool.release_all();
     (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->copy_stream);
     delete ctx;
 }
 
@@ -593,7 +787,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
 int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (b->launched) HIP_TRY(hipEventSynchronize(b->ev[8]));
     if (b->d_stamps && b->nseg) {  // PBX_PHASE_PROFILE diagnostic: mean cycles per phase
         std::vector<uint64_t> st((size_t)b->nseg * 32);
         HIP_TRY(hipMemcpy(st.data(), b->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
@@ -671,11 +865,17 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     }
     if (!b->launched) return PBX_OK;
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // Wait for this batch only (later batches may already run on the kernel stream) and
+    // copy on the copy stream, so the D2H overlaps the next batch's kernels.
+    HIP_TRY(hipEventSynchronize(b->ev[8]));
+    std::lock_guard<std::mutex> cg(ctx->copy_mu);
     const uint32_t ndt = (uint32_t)b->dt.size();
     b->h_offs.assign(ndt + 1, 0);
-    if (ndt)
-        HIP_TRY(hipMemcpy(b->h_offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (ndt) {
+        HIP_TRY(hipMemcpyAsync(b->h_offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t),
+                               hipMemcpyDeviceToHost, ctx->copy_stream));
+        HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    }
     const uint64_t png_total = ndt ? b->h_offs[ndt] : 0;
     hipError_t err = hipSuccess;
     HostBlock* hb = new HostBlock();
@@ -687,10 +887,11 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     }
     uint8_t* h = (uint8_t*)hb->pinned;
     if (b->fixed_bytes)
-        HIP_TRY(hipMemcpyAsync(h, b->d_fixed, b->fixed_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(h, b->d_fixed, b->fixed_bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
     if (png_total)
-        HIP_TRY(hipMemcpyAsync(h + b->fixed_bytes, b->d_png, png_total, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipMemcpyAsync(h + b->fixed_bytes, b->d_png, png_total, hipMemcpyDeviceToHost,
+                               ctx->copy_stream));
+    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
     int refs = 0;
     for (size_t k = 0; k < b->ft.size(); k++) {
         const TileDesc& d = b->ft[k];
@@ -719,7 +920,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
 void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return;
     (void)hipSetDevice(ctx->device);
-    if (b->launched) (void)hipStreamSynchronize(ctx->stream);
+    if (b->launched) (void)hipEventSynchronize(b->ev[8]);
     free_batch_device(ctx, b);
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
@@ -742,31 +943,7 @@ void pbx_results_release(pbx_ctx* ctx, pbx_result* res, uint64_t n) {
 
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out) {
     if (!ctx || !out || (!reqs && n)) return fail(PBX_E_BADARG, "null argument");
-    std::lock_guard<std::mutex> run(ctx->run_mu);
-    pbx_batch* b = nullptr;
-    int st = pbx_batch_plan(ctx, reqs, n, &b);
-    if (st) return st;
-    st = pbx_batch_launch(ctx, b);
-    if (st == PBX_OK) st = pbx_batch_fetch(ctx, b, out);
-    if (st != PBX_OK) {
-        // a device failure fails every request of the batch with 500 (PixelBufferVerticle.java:141-146)
-        const std::string msg = g_err;
-        for (uint64_t i = 0; i < n; i++) {
-            out[i].status = b->status[i] == PBX_OK ? PBX_E_INTERNAL : b->status[i];
-            out[i].format = reqs[i].format;
-            out[i].w = b->w[i];
-            out[i].h = b->h[i];
-            out[i].data = nullptr;
-            out[i].len = 0;
-            out[i].owner = nullptr;
-        }
-        (void)hipStreamSynchronize(ctx->stream);
-        pbx_batch_destroy(ctx, b);
-        g_err = msg;
-        return st;
-    }
-    pbx_batch_destroy(ctx, b);
-    return PBX_OK;
+    return run_batch(ctx, reqs, n, out);
 }
 
 int pbx_abi_sizes(uint64_t* sizes, int n) {
@@ -830,10 +1007,17 @@ int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {
 }
 
 int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
-    if (!req) return fail(PBX_E_BADARG, "null request");
-    const int st = pbx_get_tiles(ctx, req, 1, out);
+    if (!ctx || !req || !out) return fail(PBX_E_BADARG, "null argument");
+    const int st = ctx->coal ? ctx->coal->submit(*req, out) : run_batch(ctx, req, 1, out);
     if (st) return st;
     return out->status;
+}
+
+int pbx_ctx_stats_get(pbx_ctx* ctx, uint64_t* batches, uint64_t* requests) {
+    if (!ctx || !batches || !requests) return fail(PBX_E_BADARG, "null argument");
+    *batches = ctx->n_batches.load();
+    *requests = ctx->n_requests.load();
+    return PBX_OK;
 }
 
 }  // extern "C"

@@ -45,7 +45,8 @@ FILTER_NONE, FILTER_SUB, FILTER_UP, FILTER_AVG, FILTER_PAETH, FILTER_ADAPTIVE = 
 class PbxConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("png_filter", ctypes.c_int32),
                 ("tiff_deflate", ctypes.c_int32), ("segment_bytes", ctypes.c_int32),
-                ("max_batch_bytes", ctypes.c_uint64)]
+                ("max_batch_bytes", ctypes.c_uint64), ("coalesce", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class PbxPlaneDesc(ctypes.Structure):
@@ -88,7 +89,7 @@ EXPORTS = [
     "pbx_batch_launch", "pbx_batch_sync", "pbx_batch_fetch", "pbx_batch_destroy",
     "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
-    "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman",
+    "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
 ]
 
 _lib = None
@@ -119,6 +120,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
+    L.pbx_ctx_stats_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.pbx_get_tiles.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(PbxResult)]
     L.pbx_results_release.argtypes = [vp, ctypes.POINTER(PbxResult), u64]
     L.pbx_results_release.restype = None
@@ -266,13 +268,14 @@ class PixelsService:
     """
 
     def __init__(self, device: Optional[int] = None, png_filter: int = FILTER_NONE,
-                 tiff_deflate: bool = False):
+                 tiff_deflate: bool = False, coalesce: bool = True):
         L = lib()
         cfg = PbxConfig()
         _check(L.pbx_config_default(ctypes.byref(cfg)))
         cfg.device = -1 if device is None else device
         cfg.png_filter = png_filter
         cfg.tiff_deflate = 1 if tiff_deflate else 0
+        cfg.coalesce = 1 if coalesce else 0
         h = ctypes.c_void_p()
         _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -335,6 +338,26 @@ class PixelsService:
 
     def synchronize(self) -> None:
         _check(lib().pbx_device_synchronize(self._h))
+
+    # One getTile (pbx_get_tile): safe to call from many threads at once; concurrent
+    # calls are coalesced into batches by the library (ctypes releases the GIL).
+    def get_tile(self, ctx: TileCtx) -> Tuple[int, Optional[bytes]]:
+        req = ctx.to_req()
+        res = PbxResult()
+        lib().pbx_get_tile(self._h, ctypes.byref(req), ctypes.byref(res))
+        try:
+            body = ctypes.string_at(res.data, res.len) if res.status == OK and res.len else (
+                b"" if res.status == OK else None)
+            ctx.region["width"], ctx.region["height"] = res.w, res.h
+        finally:
+            lib().pbx_results_release(self._h, ctypes.byref(res), 1)
+        return res.status, body
+
+    def ctx_stats(self) -> Tuple[int, int]:
+        """(batches launched, requests served) so far."""
+        b, r = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().pbx_ctx_stats_get(self._h, ctypes.byref(b), ctypes.byref(r)))
+        return b.value, r.value
 
     # Batched getTile: one set of GPU launches for many requests.
     def get_tiles(self, ctxs: Sequence[TileCtx]) -> List[Tuple[int, Optional[bytes]]]:
@@ -399,6 +422,15 @@ class Batch:
         finally:
             lib().pbx_results_release(self.service.handle, res, self.n)
 
+    def fetch_into_host(self) -> int:
+        """D2H of every result into library-owned pinned memory, then release it; returns
+        the response bytes (bench: end-to-end rate without Python-side copies)."""
+        res = (PbxResult * max(self.n, 1))()
+        _check(lib().pbx_batch_fetch(self.service.handle, self._h, res))
+        n = sum(res[i].len for i in range(self.n))
+        lib().pbx_results_release(self.service.handle, res, self.n)
+        return n
+
     def close(self) -> None:
         if self._h:
             lib().pbx_batch_destroy(self.service.handle, self._h)
@@ -421,7 +453,7 @@ class TileRequestHandler:
         self.tile_ctx = tile_ctx
 
     def get_tile(self, client=None) -> Optional[bytes]:
-        status, body = self.pixels_service.get_tiles([self.tile_ctx])[0]
+        status, body = self.pixels_service.get_tile(self.tile_ctx)
         return body if status == OK else None
 
     getTile = get_tile

@@ -7,7 +7,10 @@ import os
 import sys
 from collections import defaultdict
 
+import json
+
 base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+traffic_out = sys.argv[2] if len(sys.argv) > 2 else None
 vals = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(base, "pmc[1-9]", "*counter_collection.csv"))):
@@ -36,3 +39,18 @@ for k, cs in sorted(vals.items()):
     if "WRITE_SIZE" in m:
         line.append(f"WRITE_SIZE {m['WRITE_SIZE'] * 1024 / 1e9:.3f} GB")
     print("\n   ".join(line))
+
+if traffic_out:
+    # HBM bytes per launch for bench.py's roofline "traffic" (FETCH_SIZE x2, WRITE_SIZE; KB units)
+    t = {"workload": "scripts/prof_workload.py noise: 4096 x 512x512 uint16 G_NOISE tiles -> PNG",
+         "rule": "fetch = 2 x FETCH_SIZE (gfx950 wide streaming reads), write = WRITE_SIZE; "
+                 "mean per dispatch, separate rocprofv3 --pmc passes",
+         "kernels": {}}
+    for k, cs in sorted(vals.items()):
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
+            w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
+            t["kernels"][k.replace("pbx::", "")] = {"fetch_bytes": int(2 * f * 1024),
+                                                     "write_bytes": int(w * 1024)}
+    with open(traffic_out, "w") as fo:
+        json.dump(t, fo, indent=1)

@@ -1,0 +1,215 @@
+"""GPU parity for the BASELINE.json configs beyond the headline, and the serving path.
+
+* configs[2] (C3): 1024x1024 uint16 PNG tiles;
+* configs[3] (C4): whole-slide, multi-channel uint16, every tile as TIFF, tile-row bands
+  per rank, edge tiles narrower than 512;
+* configs[4] (C5): mixed uint8/int32/float32 stream, 256..2048-px tiles, png/tif/raw;
+* the request coalescer behind pbx_get_tile (many concurrent callers, one batch per
+  GPU-busy interval) and the D2H copy stream.
+
+Everything goes through the C-ABI (libpbx.so); the oracle (oracle/pbx_oracle.c) is the
+checker only.
+"""
+import itertools
+import threading
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import pbx
+
+pytestmark = pytest.mark.gpu
+
+_ids = itertools.count(5000)
+
+
+def _oracle_tile(oracle, kind, pt, x, y, w, h, c=0, plane_no=0):
+    return oracle.gen_region(kind, pt, x, y, w, h, plane_no=plane_no, c=c).tobytes()
+
+
+def test_c3_png_1024_u16(service, oracle):
+    """configs[2] shape: 1024x1024 uint16 PNG tiles from a generated plane (64 tiles of an
+    8192^2 plane); every tile inflates, sampled tiles decode bit-exact, and the IDAT of
+    one equals the oracle's filter-None scanlines."""
+    iid = next(_ids)
+    side = 8192
+    service.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0)
+    ctxs = [pbx.TileCtx(iid, 0, 0, 0, (i % 8) * 1024, (i // 8) * 1024, 1024, 1024,
+                        format="png") for i in range(64)]
+    res = service.get_tiles(ctxs)
+    assert all(st == pbx.OK for st, _ in res)
+    for i, (_, body) in enumerate(res):
+        x, y = (i % 8) * 1024, (i // 8) * 1024
+        if i % 9 == 0:
+            tile = _oracle_tile(oracle, 2, pbx.UINT16, x, y, 1024, 1024)
+            r, px, _ = oracle.png_decode(body)
+            assert r == 0 and px == tile, i
+        else:
+            n = int.from_bytes(body[91:95], "big")
+            assert len(zlib.decompress(body[99:99 + n])) == 1024 * (1 + 2048)
+    tile = oracle.gen_region(2, pbx.UINT16, 0, 0, 1024, 1024)
+    want = oracle.png_filter_stream(tile, pbx.UINT16, 1024, 1024, 0).tobytes()
+    r, raw = oracle.png_inflate_idat(res[0][1], len(want))
+    assert r == 0 and raw == want
+    # compressed size within 1% of zlib level 6 (ImageIO) on the same stream
+    assert len(res[0][1]) < 1.01 * len(zlib.compress(want, 6)) + 200
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_c4_wholeslide_tiff_bands(service, oracle, world):
+    """configs[3] shape, scaled: a 5-channel uint16 slide whose size is not a multiple of
+    512 (edge tiles 160 px, as 100000 = 195*512 + 160), every tile as TIFF; each rank
+    serves its contiguous band of tile rows.  The bands partition the grid, and every
+    TIFF equals the oracle's TIFF of the same tile byte for byte."""
+    iid = next(_ids)
+    side = 3 * 512 + 160
+    ntile = 4
+    for c in range(5):
+        service.register_plane(iid, 0, c, 0, pbx.UINT16, side, side, generator="noise",
+                               seed=0, plane_no=c)
+    seen = set()
+    for rank in range(world):
+        lo, hi = pbx.band_rows(ntile, world, rank)
+        ctxs, keys = [], []
+        for c in range(5):
+            for ty in range(lo, hi):
+                for tx in range(ntile):
+                    w = min(512, side - 512 * tx)
+                    h = min(512, side - 512 * ty)
+                    ctxs.append(pbx.TileCtx(iid, 0, c, 0, 512 * tx, 512 * ty, w, h,
+                                            format="tif"))
+                    keys.append((c, tx, ty, w, h))
+        res = service.get_tiles(ctxs)
+        for (c, tx, ty, w, h), (st, body) in zip(keys, res):
+            assert st == pbx.OK
+            assert (c, tx, ty) not in seen
+            seen.add((c, tx, ty))
+            tile = oracle.gen_region(2, pbx.UINT16, 512 * tx, 512 * ty, w, h, plane_no=c, c=c)
+            assert body == oracle.tiff_encode(tile, pbx.UINT16, w, h)[1], (c, tx, ty)
+    assert len(seen) == 5 * ntile * ntile
+
+
+def test_c5_mixed_stream_full_sizes(service, oracle):
+    """configs[4] shape: uint8/int32/float32 planes; w,h in {256, 512, ..., 2048};
+    png/tif/raw uniformly; PNG of int32/float32 -> 404 (APNGWriter rejects them)."""
+    rng = np.random.default_rng(7)
+    side = 4096
+    planes = {}
+    for pt in (pbx.UINT8, pbx.INT32, pbx.FLOAT):
+        iid = next(_ids)
+        service.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=0)
+        planes[pt] = iid
+    ctxs, meta = [], []
+    for _ in range(96):
+        pt = [pbx.UINT8, pbx.INT32, pbx.FLOAT][rng.integers(3)]
+        w, h = int(rng.integers(1, 9)) * 256, int(rng.integers(1, 9)) * 256
+        x, y = int(rng.integers(0, side - w + 1)), int(rng.integers(0, side - h + 1))
+        fmt = [None, "png", "tif"][rng.integers(3)]
+        ctxs.append(pbx.TileCtx(planes[pt], 0, 0, 0, x, y, w, h, format=fmt))
+        meta.append((pt, x, y, w, h, fmt))
+    res = service.get_tiles(ctxs)
+    for k, ((pt, x, y, w, h, fmt), (st, body)) in enumerate(zip(meta, res)):
+        if fmt == "png" and pt != pbx.UINT8:
+            assert st == pbx.E_NOTFOUND
+            continue
+        assert st == pbx.OK
+        tile = _oracle_tile(oracle, 2, pt, x, y, w, h)
+        if fmt is None:
+            assert body == tile, k
+        elif fmt == "tif":
+            want = oracle.tiff_encode(np.frombuffer(tile, np.uint8).copy(), pt, w, h)[1]
+            assert body == want, k
+        else:
+            r, px, _ = oracle.png_decode(body)
+            assert r == 0 and px == tile, k
+
+
+def _check_result(oracle, pt, ctx, st, body):
+    x, y, w, h, fmt = ctx.x, ctx.y, ctx.w, ctx.h, ctx.format
+    if fmt == "bmp":
+        assert st == pbx.E_NOTFOUND and body is None
+        return
+    assert st == pbx.OK
+    tile = _oracle_tile(oracle, 2, pt, x, y, w, h)
+    if fmt is None:
+        assert body == tile
+    elif fmt == "tif":
+        r, px, _ = oracle.tiff_decode(body, len(tile))
+        assert r == 0 and px == tile
+    else:
+        r, px, _ = oracle.png_decode(body)
+        assert r == 0 and px == tile
+
+
+@pytest.mark.parametrize("coalesce", [True, False])
+def test_concurrent_get_tile(oracle, coalesce):
+    """Vert.x-style serving: 32 threads each call pbx_get_tile (TileRequestHandler.getTile)
+    for their own requests.  With coalescing, requests arriving while the GPU is busy share
+    a batch (fewer batches than requests); every response is still exactly its own tile,
+    and a bad request (unknown format -> 404) does not disturb its batch-mates."""
+    with pbx.PixelsService(coalesce=coalesce) as svc:
+        iid = next(_ids)
+        side = 2048
+        svc.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0)
+        rng = np.random.default_rng(3)
+        ctxs = []
+        for i in range(384):
+            w, h = int(rng.integers(1, 5)) * 128, int(rng.integers(1, 5)) * 128
+            x, y = int(rng.integers(0, side - w + 1)), int(rng.integers(0, side - h + 1))
+            fmt = [None, "png", "tif", "bmp"][i % 4] if i % 17 == 0 else ["png", None, "tif"][i % 3]
+            ctxs.append(pbx.TileCtx(iid, 0, 0, 0, x, y, w, h, format=fmt))
+        b0, r0 = svc.ctx_stats()
+        errors = []
+        barrier = threading.Barrier(32)
+
+        def worker(k):
+            barrier.wait()
+            for j in range(k, len(ctxs), 32):
+                try:
+                    st, body = svc.get_tile(ctxs[j])
+                    _check_result(oracle, pbx.UINT16, ctxs[j], st, body)
+                except AssertionError as e:  # report, don't hang the pool
+                    errors.append((j, repr(e)))
+
+        with ThreadPoolExecutor(32) as ex:
+            list(ex.map(worker, range(32)))
+        assert not errors, errors[:3]
+        b1, r1 = svc.ctx_stats()
+        assert r1 - r0 == len(ctxs)
+        if coalesce:
+            assert b1 - b0 < len(ctxs)
+        else:
+            assert b1 - b0 == len(ctxs)
+        # the reference's single-request handler mirror goes through the same path
+        h = pbx.TileRequestHandler(svc, pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64))
+        assert h.get_tile() == _oracle_tile(oracle, 2, pbx.UINT16, 0, 0, 64, 64)
+        assert pbx.TileRequestHandler(svc, pbx.TileCtx(iid, 0, 0, 0, side, 0, 64, 64)).get_tile() is None
+
+
+def test_pipelined_batches_overlap_d2h(service, oracle):
+    """Batches launched back to back, each fetched (D2H on the copy stream) while the next
+    one runs: every fetch returns its own batch's bytes."""
+    iid = next(_ids)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT16, 4096, 4096, generator="noise", seed=1)
+    batches = []
+    for k in range(4):
+        ctxs = [pbx.TileCtx(iid, 0, 0, 0, 512 * ((i + k) % 8), 512 * ((i // 8 + k) % 8), 512, 512,
+                            format="png" if k % 2 == 0 else None) for i in range(64)]
+        b = pbx.Batch(service, ctxs)
+        b.launch()
+        batches.append((ctxs, b))
+    for ctxs, b in batches:
+        res = b.fetch()
+        b.close()
+        for i in (0, 17, 63):
+            c = ctxs[i]
+            tile = oracle.gen_region(2, pbx.UINT16, c.x, c.y, 512, 512, seed=1).tobytes()
+            st, body = res[i]
+            assert st == pbx.OK
+            if c.format is None:
+                assert body == tile
+            else:
+                r, px, _ = oracle.png_decode(body)
+                assert r == 0 and px == tile
