@@ -197,6 +197,11 @@ int pbx_shard_of(const pbx_tile_req* req, int32_t tile_w, int32_t tile_h, int32_
 int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last, uint32_t nseg,
                      uint32_t* codes, uint32_t* info);
 
+/* Test hook: the LZ77 stage's per-segment outputs of a launched batch (k_lz77: 320
+ * histogram words and the match records per segment, segments in batch order), compared by
+ * tests/ with the CPU emulator.  nseg must equal the batch's segment count. */
+int pbx_test_batch_lz77(pbx_ctx* ctx, pbx_batch* b, uint32_t* hist, uint32_t* mrec, uint64_t nseg);
+
 #ifdef __cplusplus
 }
 #endif

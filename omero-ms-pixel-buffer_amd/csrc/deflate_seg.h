@@ -24,48 +24,48 @@
 // and reductions between phases have a device form (wave shuffles) and an emulator form
 // (loops) with identical results; GPU tests check the GPU bytes against the emulator's.
 //
-// Parse: each wave owns a SUB-byte sub-segment and walks it greedily (with zlib-style
-// one-step lazy matching) in batches of 64 positions: every lane evaluates the match at
-// one position (capped at CAP bytes), the wave picks the greedy path through the batch with
-// ballot/ctz, and a chosen match that reaches the cap is extended by one wave-wide compare
-// of 256 bytes.  The result is exactly the sequential greedy parse of the sub-segment
-// (ph_parse_emu is its scalar twin).  Matches end inside their sub-segment.  Tokens are
-// kept as per-wave match lists; literals are the positions no match covers, so the later
-// phases (histogram, bit counts, bit writing) walk fixed CH-position thread chunks.
+// Parse: each wave owns a SUB-byte sub-segment and parses it greedily with zlib-style
+// one-step lazy matching.  The candidate matches at a position are fixed distances that
+// image scanlines repeat at: the previous byte (runs), the previous 2-byte sample and the
+// same column one row up.  On the device every lane holds 32 consecutive positions and
+// builds, per candidate, a 64-bit mask of "byte equals the byte d back" (its positions
+// plus the next lane's), so match lengths (capped at CAP) and the positions where a match
+// pays are a few bit operations; the wave then walks only the positions that hold a
+// paying match, scalar, and extends a capped match by one wave-wide compare.  The result
+// is exactly the sequential greedy/lazy parse of ph_parse_emu (its scalar twin).  Matches
+// end inside their sub-segment.  Tokens are kept as per-wave match lists; literals are the
+// positions no match covers, so the later phases (histogram, bit counts, bit writing)
+// walk fixed CH-position thread chunks.
 #pragma once
 #include "pbx_common.h"
 
 #ifndef PBX_CAP
-#define PBX_CAP 8
-#endif
-#ifndef PBX_PB
-#define PBX_PB 64
+#define PBX_CAP 32
 #endif
 
 namespace pbx {
 
-template <int NT_, int SEG_, int WIN_, int HBITS_>
+template <int NT_, int SEG_, int WIN_>
 struct DeflateCfg {
     static constexpr int NT = NT_;        // threads per LZ77 / encode workgroup
     static constexpr int SEG = SEG_;      // max segment bytes
     static constexpr int WIN = WIN_;      // max window bytes before the segment
-    static constexpr int HBITS = HBITS_;  // hash table bits
     static constexpr int HT = 64;         // threads of the Huffman workgroup (one wave)
     static constexpr int CH = SEG / NT;   // positions per thread chunk (emission phases)
     static constexpr int NW = NT / 64;    // waves
     static constexpr int SUB = SEG / NW;  // positions parsed by one wave
     static constexpr int MAXMW = 256;     // matches kept per wave (then literals only)
-    static constexpr int CAP = PBX_CAP;   // per-lane match length before the wave extends it
-    static constexpr int PB = PBX_PB;     // positions per parse batch (64 or 128: 1-2 per lane)
+    static constexpr int CAP = PBX_CAP;   // match length found by the masks before the wave extends it
     static constexpr int CRCC = 64;       // CRC chunk bytes per thread
     static constexpr int LOG2_CRCC = 6;
     static constexpr int BUFW = (WIN + SEG + 32) / 4;
     static constexpr int SEGW = (SEG + 16) / 4;
     static constexpr int OUTW = (SEG + 64) / 4;
     static constexpr int HDRW = 160;      // dynamic block header bits (<= 17+57+316*14)
-    static constexpr int HSIZE = 1 << HBITS;
     static constexpr int LOGNT = NT == 1024 ? 10 : NT == 512 ? 9 : NT == 256 ? 8 : 7;
     static_assert(SEG % NT == 0, "SEG must be a multiple of NT");
+    static_assert(CH == 32 && SUB == 64 * CH, "a lane's parse positions are its thread chunk");
+    static_assert(CAP >= 6 && CAP <= 32, "capped lengths come from 64-bit equality masks");
     static_assert(SUB <= 65536 && SUB % CH == 0, "sub-segments hold whole thread chunks");
     static_assert(WIN + SEG <= 32768, "deflate distances are limited to 32768");
     static_assert((1 << LOGNT) == NT, "NT must be a power of two in 128..1024");
@@ -88,6 +88,15 @@ struct SegParams {
     uint32_t rowlen; // repeating-row candidate distance (0 = none)
     uint32_t last;   // 1 if this segment ends the stream (BFINAL)
 };
+
+// Look-back bytes a segment starting at stream offset s keeps before it: enough for the
+// longest candidate distance (one row), 16-byte aligned, at most WIN.
+template <class C>
+PBX_HD uint32_t seg_window(uint64_t s, uint32_t rowlen) {
+    uint32_t need = ((rowlen > 2 ? rowlen : 2u) + 15u) & ~15u;
+    if (need > (uint32_t)C::WIN) need = (uint32_t)C::WIN;
+    return (uint32_t)(s < (uint64_t)need ? s : (uint64_t)need);
+}
 
 // c + sum of the four byte products of a and b (v_dot4_u32_u8 on the device).
 PBX_HD uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
@@ -121,11 +130,6 @@ PBX_HD uint32_t lds_ld4(const SM& S, uint32_t i) {
     return funnel32(w1, w0, (i & 3) * 8);
 }
 
-template <class C>
-PBX_HD uint32_t hash3(uint32_t v) {
-    return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - C::HBITS);
-}
-
 // ============================================================================ LZ77
 // Src provides fill_word(p0, nb) -> up to 4 stream bytes starting at stream position p0.
 // Buffer bytes the LZ77 phases may read: the window and segment, zero up to the end of
@@ -151,79 +155,47 @@ PBX_HD void ph_fill(uint32_t tid, SM& S, const Src& src, const SegParams& sp) {
 
 template <class C, class SM>
 PBX_HD void ph_lz_init(uint32_t tid, SM& S) {
-    for (uint32_t k = tid; k < (uint32_t)C::HSIZE; k += C::NT) S.head[k] = 0xFFFFFFFFu;
     for (uint32_t k = tid; k < 288; k += C::NT) S.lfreq[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
 }
 
-template <class C, class Ops, class SM>
-PBX_HD void ph_insert(uint32_t tid, SM& S, const SegParams& sp) {
-    const uint32_t nb = sp.wl + sp.sl;
-    for (uint32_t i = tid; i + 3 <= nb; i += C::NT) Ops::amin(&S.head[hash3<C>(lds_ld4(S, i))], i);
+// Candidate distances, in priority order (the first wins ties): previous byte, previous
+// 2-byte sample, one row up (0 = none: rows too short to add anything).
+constexpr int NCAND = 3;
+PBX_HD uint32_t cand_dist(const SegParams& sp, int k) {
+    return k == 0 ? 1u : k == 1 ? 2u : (sp.rowlen > 2 ? sp.rowlen : 0u);
 }
 
-// Minimum length worth coding at a distance: a 3-byte match 16 KiB back costs more bits
-// than three literals (zlib's TOO_FAR rule, extended one step).
-PBX_HD bool match_pays(uint32_t len, uint32_t dist) {
-    return len >= 6 || (len >= 4 && dist <= 4096) || (len >= 3 && dist <= 256);
-}
+// Shortest match worth coding at a distance: a 3-byte match far back costs more bits than
+// three literals (zlib's TOO_FAR rule, extended one step).
+PBX_HD uint32_t match_minlen(uint32_t dist) { return dist <= 256 ? 3u : dist <= 4096 ? 4u : 6u; }
 
-// Best match at segment position p (capped at CAP): candidates, in order, the previous
-// byte (runs), the previous 2-byte sample, the same column one row up, and the first
-// occurrence of the 3-byte hash.  Longest capped length wins; the first wins ties.
-// The first 4 bytes of every candidate are compared without branches (the distance-1 and
-// -2 windows come from the three words around p, invalid positions read in-bounds words
-// and are masked); only candidates whose 4 bytes all match run the compare loop up to the
-// cap, so on incompressible data the evaluation is straight-line code.
+// Length of the match of distance d at segment position p, capped at min(CAP, se - p);
+// 0 when the distance reaches before the window.
 template <class C, class SM>
-PBX_HD void eval_pos(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t& L,
-                     uint32_t& D) {
-    const bool valid = p < se && se - p >= 3;
-    const uint32_t rem = valid ? se - p : 3;
-    const uint32_t maxlen = rem < 258 ? rem : 258;
-    const uint32_t cap = maxlen < (uint32_t)C::CAP ? maxlen : (uint32_t)C::CAP;
-    const uint32_t a = sp.wl + (valid ? p : 0u);
-    const uint32_t wi = a >> 2, sh = (a & 3) * 8;
-    const uint32_t W0 = S.buf[wi > 0 ? wi - 1 : 0], W1 = S.buf[wi], W2 = S.buf[wi + 1];
-    const uint32_t cur4 = funnel32(W2, W1, sh);
-    const uint32_t m1 = sh >= 8 ? funnel32(W2, W1, sh - 8) : funnel32(W1, W0, sh + 24);
-    const uint32_t m2 = sh >= 16 ? funnel32(W2, W1, sh - 16) : funnel32(W1, W0, sh + 16);
-    const uint32_t j = S.head[hash3<C>(cur4)];
-    const uint32_t cand[4] = {1u, 2u, sp.rowlen > 2 ? sp.rowlen : 0u, j < a ? a - j : 0u};
-    uint32_t x[4];
-    bool ok[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) ok[k] = valid && cand[k] != 0 && cand[k] <= a;
-    x[0] = m1 ^ cur4;
-    x[1] = m2 ^ cur4;
-#pragma unroll
-    for (int k = 2; k < 4; k++) x[k] = lds_ld4(S, ok[k] ? a - cand[k] : a) ^ cur4;
-    uint32_t l[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) l[k] = x[k] ? (uint32_t)__builtin_ctz(x[k]) >> 3 : 4u;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (ok[k] && !x[k]) {  // 4 equal bytes: compare on up to the cap
-            uint32_t n = 4;
-            while (n < cap) {
-                const uint32_t y = lds_ld4(S, a - cand[k] + n) ^ lds_ld4(S, a + n);
-                if (y) { n += (uint32_t)__builtin_ctz(y) >> 3; break; }
-                n += 4;
-            }
-            l[k] = n;
-        }
-    }
+PBX_HD uint32_t cand_len(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t d) {
+    const uint32_t a = sp.wl + p;
+    if (d == 0 || d > a || p >= se) return 0;
+    const uint32_t lim = se - p < (uint32_t)C::CAP ? se - p : (uint32_t)C::CAP;
+    uint32_t n = 0;
+    while (n < lim && lds_byte(S, a + n) == lds_byte(S, a - d + n)) n++;
+    return n;
+}
+
+// Best paying match at p: longest capped length among the candidates (first wins ties).
+template <class C, class SM>
+PBX_HD void best_match(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t& L,
+                       uint32_t& D) {
     L = 0; D = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t n = l[k] < cap ? l[k] : cap;
-        const bool take = ok[k] && n > L && match_pays(n, cand[k]);
-        L = take ? n : L;
-        D = take ? cand[k] : D;
+    for (int k = 0; k < NCAND; k++) {
+        const uint32_t d = cand_dist(sp, k);
+        const uint32_t n = cand_len<C>(S, sp, p, se, d);
+        if (n >= match_minlen(d) && n > L) { L = n; D = d; }
     }
 }
 
-// Full length of a match of distance D at position p that reached the cap (scalar form).
+// Full length of a match of distance D at position p that reached the cap (scalar form of
+// the wave-wide compare: 4-byte words at offsets L + 4k, up to min(258, se - p)).
 template <class C, class SM>
 PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint32_t se,
                               uint32_t L, uint32_t D) {
@@ -231,7 +203,6 @@ PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint
     const uint32_t maxlen = rem < 258 ? rem : 258;
     if (L < (uint32_t)C::CAP || L >= maxlen) return L;
     const uint32_t a = sp.wl + p;
-    // compare 4-byte words at offsets L + 4k, exactly like the wave-wide form
     for (uint32_t k = 0; k < 64; k++) {
         const uint32_t o = L + 4 * k;
         if (o >= maxlen) return maxlen;
@@ -244,32 +215,26 @@ PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint
     return maxlen;
 }
 
-// Scalar twin of the wave parse (CPU emulator): identical batches, path and lazy rule.
+// The parse of wave w's sub-segment, sequentially (the specification the device's
+// bit-parallel parse reproduces): greedy, one-step lazy on capped lengths.
 template <class C, class SM>
 PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
     const uint32_t ss = w * C::SUB;
     const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
-    uint32_t nm = 0, pos = ss;
-    uint32_t Ls[C::PB], Ds[C::PB];
-    while (pos < se) {
-        for (uint32_t l = 0; l < (uint32_t)C::PB; l++) eval_pos<C>(S, sp, pos + l, se, Ls[l], Ds[l]);
-        uint32_t o = 0;
-        while (o < (uint32_t)C::PB) {
-            uint32_t k = o;
-            while (k < (uint32_t)C::PB && Ls[k] < 3) k++;
-            if (k == (uint32_t)C::PB) { o = C::PB; break; }
-            uint32_t L = Ls[k];
-            const uint32_t D = Ds[k];
-            if (k + 1 < (uint32_t)C::PB && Ls[k + 1] > L) { o = k + 1; continue; }  // lazy
-            L = extend_scalar<C>(S, sp, pos + k, se, L, D);
-            if (nm < (uint32_t)C::MAXMW) {
-                S.mpos[w * C::MAXMW + nm] = (pos + k) | ((L - 3) << 16);
-                S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
-                nm++;
-            }
-            o = k + L;
+    uint32_t nm = 0, p = ss;
+    while (p < se) {
+        uint32_t L, D, L1, D1;
+        best_match<C>(S, sp, p, se, L, D);
+        if (L < 3) { p++; continue; }
+        best_match<C>(S, sp, p + 1, se, L1, D1);
+        if (L1 > L) { p++; continue; }  // lazy: a longer match starts at the next byte
+        L = extend_scalar<C>(S, sp, p, se, L, D);
+        if (nm < (uint32_t)C::MAXMW) {
+            S.mpos[w * C::MAXMW + nm] = p | ((L - 3) << 16);
+            S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
+            nm++;
         }
-        pos += o;
+        p += L;
     }
     S.w_nm[w] = nm;
 }

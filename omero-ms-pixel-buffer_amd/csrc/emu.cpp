@@ -32,7 +32,6 @@ using C = DeflateMainCfg;
 // One CPU struct holding every member the phases of the three kernels touch.
 struct Smem {
     uint32_t buf[C::BUFW];
-    uint32_t head[C::HSIZE];
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
@@ -93,7 +92,6 @@ int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, Seg
     // ---- k_lz77
     for (int t = 0; t < C::NT; t++) ph_fill<C>(t, S, src, sp);
     for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, S);
-    for (int t = 0; t < C::NT; t++) ph_insert<C, EmuOps>(t, S, sp);
     for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
     uint32_t a1 = 0, a2 = 0;
     for (int t = 0; t < C::NT; t++) {
@@ -161,7 +159,7 @@ int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t
         SegParams sp;
         const uint64_t s = (uint64_t)k * seg_len;
         sp.sl = (uint32_t)((len - s) < seg_len ? (len - s) : seg_len);
-        sp.wl = (uint32_t)(s < (uint64_t)C::WIN ? s : (uint64_t)C::WIN);
+        sp.wl = seg_window<C>(s, rowlen);
         sp.base = s - sp.wl;
         sp.rowlen = rowlen;
         sp.last = k + 1 == nseg;
@@ -183,6 +181,49 @@ int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t
     *out_len = o;
     return 0;
 }
+
+// The LZ77 stage alone (k_lz77's outputs) for every segment of a stream: per segment
+// HIST_WORDS histogram words and MREC_WORDS match-record words laid out as k_lz77 writes
+// them (unused match slots are left 0).
+int pbxemu_lz77(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint32_t* hist, uint32_t* mrec) {
+    uint32_t nseg, seg_len;
+    deflate_split(len, nseg, seg_len);
+    std::unique_ptr<Smem> S(new Smem());
+    MemStream src{stream};
+    for (uint32_t k = 0; k < nseg; k++) {
+        SegParams sp;
+        const uint64_t s = (uint64_t)k * seg_len;
+        sp.sl = (uint32_t)((len - s) < seg_len ? (len - s) : seg_len);
+        sp.wl = seg_window<C>(s, rowlen);
+        sp.base = s - sp.wl;
+        sp.rowlen = rowlen;
+        sp.last = k + 1 == nseg;
+        memset(S.get(), 0xCD, sizeof(Smem));
+        for (int t = 0; t < C::NT; t++) ph_fill<C>(t, *S, src, sp);
+        for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, *S);
+        for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, *S, sp);
+        for (int t = 0; t < C::NT; t++) {
+            uint32_t s1, s2, n;
+            ph_hist<C, EmuOps>(t, *S, sp, s1, s2, n);
+        }
+        uint32_t* hg = hist + (size_t)k * HIST_WORDS;
+        for (int i = 0; i < 288; i++) hg[i] = S->lfreq[i];
+        for (int i = 0; i < 32; i++) hg[288 + i] = S->dfreq[i];
+        uint32_t* mg = mrec + (size_t)k * MREC_WORDS;
+        memset(mg, 0, MREC_WORDS * 4);
+        for (int w = 0; w < C::NW; w++) {
+            mg[w] = S->w_nm[w];
+            for (uint32_t m = 0; m < S->w_nm[w]; m++) {
+                mg[C::NW + w * C::MAXMW + m] = S->mpos[w * C::MAXMW + m];
+                mg[C::NW + C::NW * C::MAXMW + w * C::MAXMW + m] = S->mdist[w * C::MAXMW + m];
+            }
+        }
+    }
+    return 0;
+}
+
+uint32_t pbxemu_hist_words(void) { return HIST_WORDS; }
+uint32_t pbxemu_mrec_words(void) { return MREC_WORDS; }
 
 // The Huffman stage alone on a given histogram (288 + 32 counts): codes 480 words as
 // pbx_test_huffman returns them, info = block type, header bits, data bits, output bytes.

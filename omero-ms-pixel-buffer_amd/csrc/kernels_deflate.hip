@@ -33,11 +33,11 @@ constexpr uint32_t STAMP_STRIDE = 32;  // diagnostics: k_lz77 0.., k_huff 8.., k
 template <class C>
 struct LzSmem {
     alignas(16) uint32_t buf[C::BUFW];
-    uint32_t head[C::HSIZE];
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    uint32_t lfreq[288], dfreq[32];
+    alignas(16) uint32_t h8[288 * 4];  // literal/length histogram, 4 interleaved copies (lane & 3)
+    uint32_t dfreq[32];
     uint32_t red[3 * C::NW];
 };
 
@@ -89,11 +89,11 @@ constexpr CrcTables make_crc_tables() {
 __constant__ const CrcTables kCrcTables = make_crc_tables();
 
 // Segment geometry from the tile descriptor.
-__device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k, uint32_t win) {
+__device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k) {
     SegParams sp;
     const uint64_t s = (uint64_t)k * d.seg_len;
     sp.sl = (uint32_t)((d.stream_len - s) < d.seg_len ? (d.stream_len - s) : d.seg_len);
-    sp.wl = (uint32_t)(s < (uint64_t)win ? s : (uint64_t)win);
+    sp.wl = seg_window<DC>(s, d.rowlen);
     sp.base = s - sp.wl;
     sp.rowlen = d.rowlen;
     sp.last = (k + 1 == d.seg_count) ? 1u : 0u;
@@ -126,71 +126,146 @@ __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, 
 }
 
 // ==================================================================== k_lz77
-// Wave-serial greedy parse of one sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).
+// Zero bytes of x as 4 bits (bit j: byte j of x is zero).
+__device__ __forceinline__ uint32_t zero_nibble(uint32_t x) {
+    const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    const uint32_t z = ~(t | x) & 0x80808080u;  // bit 8j+7: byte j == 0
+    return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
+}
+
+// Parse of wave w's sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).  Lane l holds
+// positions p0 = ss + 32 l .. p0 + 31 (its thread chunk).  Per candidate distance d the lane
+// builds E_d, bit i = (byte p0+i == byte p0+i-d), masked to valid positions (< se, d not
+// before the window), and Ex_d = E_d | next lane's E_d << 32: the capped match length at
+// position p0+i is ctz(~(Ex_d >> i)) (<= 64 - i), and the positions where a candidate pays
+// (>= match_minlen(d) equal bytes) are E & E>>1 & E>>2 (& ...).  The wave walks only those
+// positions (M), scalar: lengths at k and k+1 from readlane'd masks, the lazy rule, the
+// wave-wide extension of a capped match.  Each lane also collects the positions of its
+// chunk covered by recorded matches (cover), for the histogram.
 template <class C, class SM>
-__device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp) {
-    constexpr int NB = C::PB / 64;  // positions per lane per batch
-    static_assert(NB == 1 || NB == 2, "64 or 128 positions per batch");
-    // every loop-carried value is wave-uniform: readfirstlane keeps it in SGPRs, so the
-    // walk below is scalar code, not exec-masked vector code
+__device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uint32_t (&cw)[9],
+                             uint32_t& cover, uint32_t& smask) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t ss = w * C::SUB;
     const uint32_t se = __builtin_amdgcn_readfirstlane(ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl);
-    uint32_t nm = 0, pos = ss;
-    while (pos < se) {
-        uint32_t Lv[NB], Dv[NB];  // positions pos + 64 b + lane
-        uint64_t mv[NB];
+    cover = 0;
+    smask = 0;
+    if (ss >= se) {
+        if (lane == 0) S.w_nm[w] = 0;
+        return;
+    }
+    const uint32_t p0 = ss + 32 * lane, a0 = sp.wl + p0;
+    const uint32_t nval = se > p0 ? se - p0 : 0u;
+    smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
+    uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
+    uint32_t M = 0;
 #pragma unroll
-        for (int b = 0; b < NB; b++) eval_pos<C>(S, sp, pos + 64 * b + lane, se, Lv[b], Dv[b]);
+    for (int c = 0; c < NCAND; c++) {
+        const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
+        dd[c] = d;
+        ml[c] = match_minlen(d);
+        uint32_t e = 0;
+        if (d) {
+            if (c < 2) {  // d = 1, 2: the lane's own words shifted by d bytes
+                const uint32_t sh = 32 - 8 * d;
 #pragma unroll
-        for (int b = 0; b < NB; b++) mv[b] = __ballot(Lv[b] >= 3);
-        auto at = [&](const uint32_t (&v)[NB], uint32_t k) {
-            if (NB == 1 || k < 64) return __builtin_amdgcn_readlane(v[0], k & 63);
-            return __builtin_amdgcn_readlane(v[NB - 1], k & 63);
-        };
-        uint32_t o = 0;
-        while (o < (uint32_t)C::PB) {
-            uint32_t k = C::PB;
+                for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh)) << (4 * j);
+            } else {  // one row up: unaligned words at a0 - d
+                const int32_t b = (int32_t)a0 - (int32_t)d;
+                const int32_t r = b >> 2;
+                const uint32_t sh = (uint32_t)(b & 3) * 8;
+                uint32_t rw[9];
 #pragma unroll
-            for (int b = NB - 1; b >= 0; b--) {  // first set bit at or after o
-                const uint32_t lo = 64u * b;
-                if (o < lo + 64) {
-                    const uint64_t m = o > lo ? mv[b] >> (o - lo) : mv[b];
-                    if (m) k = (o > lo ? o : lo) + (uint32_t)__builtin_ctzll(m);
-                }
+                for (int j = 0; j < 9; j++) rw[j] = S.buf[r + j > 0 ? r + j : 0];
+#pragma unroll
+                for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
             }
-            if (k >= (uint32_t)C::PB) { o = C::PB; break; }
-            k = __builtin_amdgcn_readfirstlane(k);
-            uint32_t Lk = at(Lv, k);
-            const uint32_t Dk = at(Dv, k);
-            if (k + 1 < (uint32_t)C::PB) {
-                const uint32_t L1 = at(Lv, k + 1);
-                if (L1 > Lk) { o = k + 1; continue; }  // lazy: a longer match starts next
-            }
-            const uint32_t p = pos + k;
-            const uint32_t rem = se - p;
-            const uint32_t maxlen = rem < 258 ? rem : 258;
-            if (Lk >= (uint32_t)C::CAP && Lk < maxlen) {
-                // one wave-wide compare of 4 bytes per lane extends the match past the cap
-                const uint32_t a = sp.wl + p, off = Lk + 4 * lane;
-                const uint32_t x = off < maxlen ? (lds_ld4(S, a - Dk + off) ^ lds_ld4(S, a + off)) : 0u;
-                const uint64_t mm = __ballot(off >= maxlen || x != 0);
-                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-                const uint32_t xf = __builtin_amdgcn_readlane(x, f);
-                const uint32_t of = Lk + 4 * f;
-                const uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
-                Lk = __builtin_amdgcn_readfirstlane(l < maxlen ? l : maxlen);
-            }
-            if (nm < (uint32_t)C::MAXMW) {
-                if (lane == 0) {
-                    S.mpos[w * C::MAXMW + nm] = p | ((Lk - 3) << 16);
-                    S.mdist[w * C::MAXMW + nm] = (uint16_t)(Dk - 1);
-                }
-                nm++;
-            }
-            o = __builtin_amdgcn_readfirstlane(k + Lk);
+            const uint32_t vm = a0 >= d ? 0xFFFFFFFFu : (d - a0 >= 32 ? 0u : 0xFFFFFFFFu << (d - a0));
+            e &= vm & smask;
         }
-        pos = __builtin_amdgcn_readfirstlane(pos + o);
+        uint32_t nx = __shfl_down(e, 1, 64);
+        nx = lane == 63 ? 0u : nx;
+        exlo[c] = e;
+        exhi[c] = nx;
+        if (d) {
+            const uint64_t x = ((uint64_t)nx << 32) | e;
+            uint64_t r = x & (x >> 1) & (x >> 2);
+            if (ml[c] >= 4) r &= x >> 3;
+            if (ml[c] >= 6) r &= (x >> 4) & (x >> 5);
+            M |= (uint32_t)r;
+        }
+    }
+    const uint64_t B = __ballot(M != 0);
+    const uint32_t lsub = se - ss;
+    uint32_t nm = 0, o = 0;
+    while (o < lsub) {
+        // the first position >= o where a match pays
+        const uint32_t t0 = o >> 5;
+        uint32_t k = 0xFFFFFFFFu;
+        const uint32_t mt = __builtin_amdgcn_readlane(M, t0) & (0xFFFFFFFFu << (o & 31));
+        if (mt) {
+            k = (t0 << 5) + (uint32_t)__builtin_ctz(mt);
+        } else if (t0 < 63) {
+            const uint64_t bb = B & (~0ull << (t0 + 1));
+            if (bb) {
+                const uint32_t t2 = (uint32_t)__builtin_ctzll(bb);
+                k = (t2 << 5) + (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(M, t2));
+            }
+        }
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k >= lsub) break;
+        const uint32_t t = k >> 5, i = k & 31;
+        uint32_t L = 0, D = 0, L1 = 0;
+#pragma unroll
+        for (int c = 0; c < NCAND; c++) {
+            if (!dd[c]) continue;
+            // (readlane returns int: cast through uint32_t, no sign extension)
+            const uint64_t ex = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(exhi[c], t) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(exlo[c], t);
+            uint32_t n0 = (uint32_t)__builtin_ctzll(~(ex >> i));
+            uint32_t n1 = (uint32_t)__builtin_ctzll(~(ex >> (i + 1)));
+            n0 = n0 < (uint32_t)C::CAP ? n0 : (uint32_t)C::CAP;
+            n1 = n1 < (uint32_t)C::CAP ? n1 : (uint32_t)C::CAP;
+            if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; }
+            if (n1 >= ml[c] && n1 > L1) L1 = n1;
+        }
+        L = __builtin_amdgcn_readfirstlane(L);
+        D = __builtin_amdgcn_readfirstlane(D);
+        L1 = __builtin_amdgcn_readfirstlane(L1);
+        if (L < 3 || L1 > L) { o = k + 1; continue; }  // lazy: a longer match starts next
+        const uint32_t p = ss + k;
+        const uint32_t rem = se - p;
+        const uint32_t maxlen = rem < 258 ? rem : 258;
+        if (L >= (uint32_t)C::CAP && L < maxlen) {
+            // one wave-wide compare of 4 bytes per lane extends the match past the cap
+            const uint32_t a = sp.wl + p, off = L + 4 * lane;
+            const uint32_t x = off < maxlen ? (lds_ld4(S, a - D + off) ^ lds_ld4(S, a + off)) : 0u;
+            const uint64_t mm = __ballot(off >= maxlen || x != 0);
+            const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+            const uint32_t xf = __builtin_amdgcn_readlane(x, f);
+            const uint32_t of = L + 4 * f;
+            const uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
+            L = __builtin_amdgcn_readfirstlane(l < maxlen ? l : maxlen);
+        }
+        if (nm < (uint32_t)C::MAXMW) {
+            if (lane == 0) {
+                S.mpos[w * C::MAXMW + nm] = p | ((L - 3) << 16);
+                S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
+                uint32_t sy, e, v;
+                len_code(L, sy, e, v);
+                atomicAdd(&S.h8[sy * 4], 1u);
+                dist_code(D, sy, e, v);
+                atomicAdd(&S.dfreq[sy], 1u);
+            }
+            nm++;
+            // positions [p, p + L) of this lane's chunk are covered
+            const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + L - p0;
+            if (p + L > p0 && p < p0 + 32) {
+                const uint32_t h = hi < 32 ? hi : 32u;
+                cover |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << lo);
+            }
+        }
+        o = k + L;
     }
     if (lane == 0) S.w_nm[w] = nm;
 }
@@ -211,19 +286,45 @@ __global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
     stamp();
     const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
     const TileDesc d = dt[ti];
-    const SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
+    const SegParams sp = seg_params(d, seg - d.seg_first);
     load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
-    ph_lz_init<C>(tid, S);
+    for (uint32_t k = tid; k < 288 * 4; k += C::NT) S.h8[k] = 0;
+    if (tid < 32) S.dfreq[tid] = 0;
     __syncthreads();
     stamp();
-    ph_insert<C, DevOps>(tid, S, sp);
-    __syncthreads();
+    // the thread's chunk words (and the word before it) from LDS
+    const uint32_t cs = tid * C::CH, wi = (sp.wl + cs) >> 2;
+    uint32_t cw[9];
+    cw[0] = wi ? S.buf[wi - 1] : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; j++) cw[j + 1] = S.buf[wi + j];
+    uint32_t cover, smask;
+    ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
     stamp();
-    ph_parse_dev<C>(tid, S, sp);
-    __syncthreads();
-    stamp();
-    uint32_t s1, s2, n;
-    ph_hist<C, DevOps>(tid, S, sp, s1, s2, n);
+    // literal histogram of the chunk (positions no recorded match covers), 4 interleaved
+    // copies against same-address LDS atomics; Adler-32 partial sums from the same words
+    {
+        const uint32_t lit = ~cover & smask, cp = lane & 3u;
+#pragma unroll
+        for (int j = 0; j < 32; j++)
+            if ((lit >> j) & 1u) atomicAdd(&S.h8[((cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu) * 4 + cp], 1u);
+    }
+    if (tid == 0) atomicAdd(&S.h8[256 * 4], 1u);  // end of block
+    uint32_t s1 = 0, s2 = 0, n = 0;
+    if (cs < sp.sl) {
+        const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
+        n = ce - cs;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)C::CH / 4; k++) {
+            const uint32_t v = cw[1 + k];  // bytes past the segment are zero in buf
+            const uint32_t e = (uint32_t)C::CH - 4 * k;
+            s1 = dot4_u8(v, 0x01010101u, s1);
+            s2 = dot4_u8(v, e | ((e - 1) << 8) | ((e - 2) << 16) | ((e - 3) << 24), s2);
+        }
+        s2 -= (cs + (uint32_t)C::CH - ce) * s1;
+        s1 %= ADLER_BASE;
+        s2 %= ADLER_BASE;
+    }
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {  // Adler-32 partials: wave tree
         const uint32_t r1 = __shfl_down(s1, off, 64), r2 = __shfl_down(s2, off, 64);
@@ -241,7 +342,16 @@ __global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
         g.adler_s1 = a1; g.adler_s2 = a2;
     }
     uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
-    for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) hg[i] = i < 288 ? S.lfreq[i] : S.dfreq[i - 288];
+    for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
+        uint32_t v;
+        if (i < 288) {
+            const uint4 a = *(const uint4*)&S.h8[i * 4];
+            v = a.x + a.y + a.z + a.w;
+        } else {
+            v = S.dfreq[i - 288];
+        }
+        hg[i] = v;
+    }
     uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
     if (tid < (uint32_t)C::NW) mg[tid] = S.w_nm[tid];
     for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
@@ -782,7 +892,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     stamp();
     const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
     const TileDesc d = dt[ti];
-    SegParams sp = seg_params(d, seg - d.seg_first, C::WIN);
+    SegParams sp = seg_params(d, seg - d.seg_first);
     sp.base += sp.wl;  // the encoder holds the segment only
     sp.wl = 0;
     const SegInfo gi = info[seg];

@@ -5,16 +5,12 @@
 
 namespace pbx {
 
-// 512 threads (8 waves), 16 KiB segments with a PBX_WIN-byte look-back window, 2^PBX_HBITS-entry
-// hash (both overridable for experiments only; 4 KiB / 2^10 compress G_NOISE tiles within
-// 0.05% of 8 KiB / 2^12 and fit four LZ77 workgroups per CU).
-#ifndef PBX_HBITS
-#define PBX_HBITS 10
-#endif
+// 512 threads (8 waves), 16 KiB segments with at most PBX_WIN look-back bytes (the longest
+// candidate distance is one row; overridable for experiments only).
 #ifndef PBX_WIN
 #define PBX_WIN 4096
 #endif
-using DeflateMainCfg = DeflateCfg<512, 16384, PBX_WIN, PBX_HBITS>;
+using DeflateMainCfg = DeflateCfg<512, 16384, PBX_WIN>;
 
 // Per-segment HBM records between the deflate kernels (32-bit words).
 constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram

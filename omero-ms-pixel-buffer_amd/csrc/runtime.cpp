@@ -996,6 +996,17 @@ int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last
     return PBX_OK;
 }
 
+int pbx_test_batch_lz77(pbx_ctx* ctx, pbx_batch* b, uint32_t* hist, uint32_t* mrec, uint64_t nseg) {
+    if (!ctx || !b || !hist || !mrec) return fail(PBX_E_BADARG, "null argument");
+    if (!b->launched) return fail(PBX_E_BADARG, "batch not launched");
+    if (nseg != b->nseg) return fail(PBX_E_BADARG, "segment count %llu != %u", (unsigned long long)nseg, b->nseg);
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipEventSynchronize(b->ev[8]));
+    HIP_TRY(hipMemcpy(hist, b->d_hist, nseg * HIST_WORDS * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(mrec, b->d_mrec, nseg * MREC_WORDS * 4, hipMemcpyDeviceToHost));
+    return PBX_OK;
+}
+
 int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {
     if (!r || world <= 0 || tw <= 0 || th <= 0) return fail(PBX_E_BADARG, "bad argument"), -1;
     uint64_t k = (uint64_t)r->image_id;

@@ -90,6 +90,7 @@ EXPORTS = [
     "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
+    "pbx_test_batch_lz77",
 ]
 
 _lib = None
@@ -120,6 +121,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
+    L.pbx_test_batch_lz77.argtypes = [vp, vp, vp, vp, u64]
     L.pbx_ctx_stats_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.pbx_get_tiles.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(PbxResult)]
     L.pbx_results_release.argtypes = [vp, ctypes.POINTER(PbxResult), u64]
@@ -421,6 +423,15 @@ class Batch:
                      if res[i].status == OK else None) for i in range(self.n)]
         finally:
             lib().pbx_results_release(self.service.handle, res, self.n)
+
+    def lz77_records(self, nseg: int, hist_words: int, mrec_words: int):
+        """Test hook: (hist, mrec) uint32 arrays of every segment from k_lz77."""
+        import numpy as np
+        h = np.zeros(nseg * hist_words, np.uint32)
+        m = np.zeros(nseg * mrec_words, np.uint32)
+        _check(lib().pbx_test_batch_lz77(self.service.handle, self._h, h.ctypes.data,
+                                         m.ctypes.data, nseg))
+        return h.reshape(nseg, hist_words), m.reshape(nseg, mrec_words)
 
     def fetch_into_host(self) -> int:
         """D2H of every result into library-owned pinned memory, then release it; returns

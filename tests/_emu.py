@@ -25,6 +25,10 @@ def lib():
         L.pbxemu_nsegs.argtypes = [ctypes.c_uint64]
         L.pbxemu_huffman.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.pbxemu_lz77.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                  ctypes.c_void_p, ctypes.c_void_p]
+        L.pbxemu_hist_words.restype = ctypes.c_uint32
+        L.pbxemu_mrec_words.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         _lib = L
@@ -57,3 +61,17 @@ def huffman(hist, sl, last):
     r = lib().pbxemu_huffman(h.ctypes.data, sl, last, codes.ctypes.data, info.ctypes.data)
     assert r == 0
     return codes, info
+
+
+def lz77(data: bytes, rowlen: int):
+    """LZ77 stage alone: (hist[nseg, 320], mrec[nseg, MREC_WORDS]) as k_lz77 writes them."""
+    import numpy as np
+    data = bytes(data)
+    L = lib()
+    n = L.pbxemu_nsegs(len(data))
+    hw, mw = L.pbxemu_hist_words(), L.pbxemu_mrec_words()
+    h = np.zeros(n * hw, np.uint32)
+    m = np.zeros(n * mw, np.uint32)
+    r = L.pbxemu_lz77(data, len(data), rowlen, h.ctypes.data, m.ctypes.data)
+    assert r == 0, r
+    return h.reshape(n, hw), m.reshape(n, mw)

@@ -59,3 +59,38 @@ def test_filtered_streams(oracle, filt):
     s = oracle.png_filter_stream(t, oracle.UINT8, 300, 80, filt).tobytes()
     z, _ = _emu.deflate(s, 301)
     assert zlib.decompress(z) == s
+
+
+@pytest.mark.parametrize("kind", ["random", "periodic", "rows"])
+def test_lz77_records_cover_the_segment(kind):
+    """LZ77 stage records (what k_lz77 writes and the GPU test compares): per segment the
+    literals plus the match lengths cover exactly the segment's bytes, every match lies in
+    its wave's sub-segment, uses a candidate distance (1, 2, one row) and pays."""
+    rng = np.random.default_rng(3)
+    rowlen = 301
+    if kind == "random":
+        s = rng.integers(0, 256, 50000, dtype=np.uint8).tobytes()
+    elif kind == "periodic":
+        s = (bytes(range(5)) * 20000)[:50000]
+    else:
+        row = rng.integers(0, 256, rowlen, dtype=np.uint8).tobytes()
+        s = (row * 200)[:50000]
+    hist, mrec = _emu.lz77(s, rowlen)
+    n = _emu.lib().pbxemu_nsegs(len(s))
+    seg = (-(-len(s) // n) + 15) // 16 * 16
+    nw, mw = 8, 256
+    for k in range(n):
+        sl = min(seg, len(s) - k * seg)
+        lits = int(hist[k][:256].sum())
+        covered = 0
+        for w in range(nw):
+            for m in range(int(mrec[k][w])):
+                pm = int(mrec[k][nw + w * mw + m])
+                d = int(mrec[k][nw + nw * mw + w * mw + m]) + 1
+                p, ln = pm & 0xFFFF, (pm >> 16) + 3
+                assert w * 2048 <= p and p + ln <= min((w + 1) * 2048, sl)
+                assert d in (1, 2, rowlen)
+                assert ln >= (3 if d <= 256 else 4 if d <= 4096 else 6)
+                covered += ln
+        assert lits + covered == sl
+        assert hist[k][256] == 1  # end of block

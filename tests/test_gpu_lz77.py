@@ -1,0 +1,59 @@
+"""GPU LZ77 stage (k_lz77: bit-parallel candidate masks, wave walk of paying positions,
+wave-wide extension, interleaved literal histograms) against the CPU emulator's sequential
+greedy/lazy parse (ph_parse_emu), segment by segment: the symbol histogram and every match
+record must be identical.  Through the C-ABI test hook pbx_test_batch_lz77."""
+import numpy as np
+import pytest
+
+import _emu
+import pbx
+
+pytestmark = pytest.mark.gpu
+
+
+def _streams():
+    """(name, pixel type, w, h, plane array big-endian) cases that stress the parse: noise,
+    long runs, row repeats, short periodic matches, rows longer than the window, tiny rows."""
+    rng = np.random.default_rng(5)
+    out = []
+    yy, xx = np.mgrid[0:96, 0:700]
+    out.append(("noise16", pbx.UINT16, rng.integers(0, 4096, (96, 700)).astype(">u2")))
+    out.append(("runs8", pbx.UINT8, ((xx // 37) % 3 * 50 + (yy // 11) % 2).astype(np.uint8)))
+    out.append(("period3", pbx.UINT8, (xx % 3 * 7 + (rng.random((96, 700)) < 0.05)).astype(np.uint8)))
+    rows = np.tile(rng.integers(0, 65536, (1, 700)), (96, 1)).astype(">u2")
+    rows[::7] = rng.integers(0, 65536, (14, 700))
+    out.append(("rowrep16", pbx.UINT16, rows))
+    out.append(("zeros16", pbx.UINT16, np.zeros((96, 700), ">u2")))
+    wide = rng.integers(0, 3, (24, 2600)).astype(">u2")  # rowlen 5201 > the 4 KiB window
+    wide[1::2] = wide[0::2]
+    out.append(("wide16", pbx.UINT16, wide))
+    out.append(("narrow8", pbx.UINT8, rng.integers(0, 2, (400, 3)).astype(np.uint8)))
+    return out
+
+
+@pytest.mark.parametrize("case", range(7))
+def test_gpu_lz77_matches_emulator(service, case):
+    name, pt, a = _streams()[case]
+    h, w = a.shape
+    iid = 9100 + case
+    service.register_plane(iid, 0, 0, 0, pt, w, h, data=a, big_endian=True)
+    b = pbx.Batch(service, [pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="png")])
+    b.launch()
+    b.sync()
+    nseg = b.stats().segments
+    L = _emu.lib()
+    gh, gm = b.lz77_records(nseg, L.pbxemu_hist_words(), L.pbxemu_mrec_words())
+    b.close()
+    bpp = pbx.BYTES_PER_PIXEL[pt]
+    raw = a.tobytes()
+    stream = b"".join(b"\x00" + raw[r * w * bpp:(r + 1) * w * bpp] for r in range(h))
+    eh, em = _emu.lz77(stream, 1 + w * bpp)
+    assert gh.shape == eh.shape
+    for k in range(nseg):
+        assert (gh[k] == eh[k]).all(), (name, k, np.nonzero(gh[k] != eh[k])[0][:8])
+        nw = 8
+        assert (gm[k][:nw] == em[k][:nw]).all(), (name, k)
+        for wv in range(nw):
+            n = int(em[k][wv])
+            for off in (nw + wv * 256, nw + 8 * 256 + wv * 256):
+                assert (gm[k][off:off + n] == em[k][off:off + n]).all(), (name, k, wv)
