@@ -873,22 +873,20 @@ PBX_HD uint32_t ph_bits(uint32_t tid, const SM& S, const SegParams& sp) {
     return f.bits;
 }
 
-// Bit writer of one thread's contiguous bit range: whole 32-bit words are plain stores,
-// the first and last (shared with the neighbouring ranges) are OR'd atomically.
+// Bit writer of one thread's contiguous bit range: every word is OR'd (the buffer starts zeroed), so the words shared with the neighbouring
+// ranges need no special case and a put of 0 bits is a no-op.
 template <class Ops>
 struct RunWriter {
     uint32_t* out;
-    uint32_t word, first;  // current word index, the range's first word
-    uint32_t nacc;         // bits held in acc (including the leading bits of other ranges)
+    uint32_t word;  // current word index
+    uint32_t nacc;  // bits held in acc (including the leading bits of other ranges)
     uint64_t acc;
-    PBX_HD RunWriter(uint32_t* o, uint32_t pos)
-        : out(o), word(pos >> 5), first(pos >> 5), nacc(pos & 31), acc(0) {}
+    PBX_HD RunWriter(uint32_t* o, uint32_t pos) : out(o), word(pos >> 5), nacc(pos & 31), acc(0) {}
     PBX_HD void put(uint32_t v, uint32_t n) {
         acc |= (uint64_t)v << nacc;
         nacc += n;
         if (nacc >= 32) {
-            const uint32_t w = (uint32_t)acc;
-            if (word == first) Ops::aor(&out[word], w); else out[word] = w;
+            Ops::aor(&out[word], (uint32_t)acc);
             word++;
             acc >>= 32;
             nacc -= 32;

@@ -56,14 +56,16 @@ struct HuffSmem {
     uint32_t nrounds[2];
 };
 
+constexpr int CRC_NIB_LEVELS_ = 7;
 template <class C>
 struct EncSmem {
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    uint32_t lcode[288], dcode[32];
+    uint32_t lcode[289], dcode[32];  // slot form; lcode[288] = no token
     alignas(16) uint32_t out[C::OUTW];
     uint32_t crc_t[4][256];
+    uint32_t crcn[CRC_NIB_LEVELS_][8][16];
     uint32_t misc[M_NMISC];
     uint32_t t_a[C::NT];
     uint32_t wtot[16];
@@ -87,6 +89,59 @@ constexpr CrcTables make_crc_tables() {
     return T;
 }
 __constant__ const CrcTables kCrcTables = make_crc_tables();
+
+// The CRC combine multiplies by constant operators K = x^(8*64*2^k) mod P (k = 0..6: the
+// wave tree over 64-byte chunks, then one wave's 4 KiB).  b -> K*b mod P is GF(2)-linear,
+// so it is 8 lookups in nibble tables T[j][v] = K*(v << 4j) (3.5 KB in LDS) instead of a
+// 32-step shift-and-reduce loop.
+constexpr int CRC_NIB_LEVELS = CRC_NIB_LEVELS_;
+struct CrcNibTables {
+    uint32_t t[CRC_NIB_LEVELS][8][16];
+};
+constexpr CrcNibTables make_crc_nib(int log2c) {
+    CrcNibTables T{};
+    X8Table x = make_x8();
+    for (int k = 0; k < CRC_NIB_LEVELS; k++)
+        for (int j = 0; j < 8; j++)
+            for (uint32_t v = 0; v < 16; v++) T.t[k][j][v] = crc_multmodp_c(x.v[log2c + k], v << (4 * j));
+    return T;
+}
+__constant__ const CrcNibTables kCrcNib = make_crc_nib(DC::LOG2_CRCC);
+
+// x^(8n) mod P for n < 2^15 from two tables: x^(8v) and x^(8*256*v).
+struct CrcPowTables {
+    uint32_t lo[256], hi[128];
+};
+constexpr CrcPowTables make_crc_pow() {
+    CrcPowTables T{};
+    X8Table x = make_x8();
+    for (uint32_t v = 0; v < 256; v++) {
+        uint32_t p = 1u << 31;
+        for (int k = 0; k < 8; k++)
+            if ((v >> k) & 1u) p = crc_multmodp_c(x.v[k], p);
+        T.lo[v] = p;
+    }
+    for (uint32_t v = 0; v < 128; v++) {
+        uint32_t p = 1u << 31;
+        for (int k = 0; k < 7; k++)
+            if ((v >> k) & 1u) p = crc_multmodp_c(x.v[8 + k], p);
+        T.hi[v] = p;
+    }
+    return T;
+}
+__constant__ const CrcPowTables kCrcPow = make_crc_pow();
+
+template <class SM>
+__device__ __forceinline__ uint32_t crc_mul_nib(const SM& S, int k, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r ^= S.crcn[k][j][(b >> (4 * j)) & 0xFu];
+    return r;
+}
+
+__device__ __forceinline__ uint32_t crc_x8n_small(uint32_t n) {  // n < 2^15
+    return crc_multmodp(kCrcPow.lo[n & 0xFFu], kCrcPow.hi[(n >> 8) & 0x7Fu]);
+}
 
 // Segment geometry from the tile descriptor.
 __device__ __forceinline__ SegParams seg_params(const TileDesc& d, uint32_t k) {
@@ -271,7 +326,8 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
 }
 
 template <class C, bool PROF>
-__global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt, uint32_t ndt,
+__global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
+                                                const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, const uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
                                                 uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps) {
@@ -284,7 +340,7 @@ __global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
         nst++;
     };
     stamp();
-    const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
+    const uint32_t ti = seg_tile[seg];
     const TileDesc d = dt[ti];
     const SegParams sp = seg_params(d, seg - d.seg_first);
     load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
@@ -762,6 +818,17 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     stamp();
 }
 
+// ================================================================= k_seg_map
+// The tile of every segment (one thread per tile), so the per-segment kernels find their
+// tile descriptor with one load.
+__global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                 uint32_t* __restrict__ seg_tile) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ndt) return;
+    const uint32_t f = dt[i].seg_first, n = dt[i].seg_count;
+    for (uint32_t k = 0; k < n; k++) seg_tile[f + k] = i;
+}
+
 // ================================================================ k_seg_sizes
 __device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
     return (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET + ZLIB_HDR_BYTES + payload + 4
@@ -812,27 +879,24 @@ __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
     return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
 }
 
-// A token's bits packed in one register: value (<= 20 bits) | nbits << 27.
-__device__ __forceinline__ uint32_t slot_of(uint32_t code, uint32_t extra, uint32_t ebits) {
-    const uint32_t n = code >> 16;
-    return (code & 0xFFFFu) | (extra << n) | ((n + ebits) << 27);
-}
+// A token's bits packed in one register: value (<= 20 bits) | nbits << 27.  The LDS code
+// tables hold literal/length and distance codes in this form (slot 288 = 0 bits).
+__device__ __forceinline__ uint32_t slot_from_code(uint32_t c) { return (c & 0xFFFFu) | ((c >> 16) << 27); }
+constexpr uint32_t SLOT_NONE = 288;
 
 // The thread's CH positions as register slots, in stream order: slot i holds the literal
 // or length code (+ extra bits) of a token starting at chunk position i; a match also
 // fills slots i+1 (distance code) and i+2 (distance extra bits), positions it covers.
-// Same tokens as walk_tokens (deflate_seg.h) over the same match lists; the chunk's bytes
-// come from registers instead of LDS.
+// Same tokens as walk_tokens (deflate_seg.h) over the same match lists.  Literals first,
+// branch-free: covered positions read the empty slot; then the (few) matches starting in
+// the chunk overwrite their three slots.
 template <class C, class SM>
 __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const SegParams& sp,
                                             const uint32_t (&cb)[C::CH / 4],
                                             uint32_t (&slot)[C::CH + 2]) {
-#pragma unroll
-    for (int i = 0; i < C::CH + 2; i++) slot[i] = 0;
     const uint32_t cs = tid * C::CH;
-    if (cs >= sp.sl) return;
     const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
-    const uint32_t w = cs / C::SUB;
+    const uint32_t w = (cs / C::SUB) < (uint32_t)C::NW ? cs / C::SUB : (uint32_t)C::NW - 1;
     const uint32_t* mp = S.mpos + w * C::MAXMW;
     const auto* md = S.mdist + w * C::MAXMW;
     const uint32_t nm = S.w_nm[w];
@@ -841,38 +905,45 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
         const uint32_t mid = (lo + hi) >> 1;
         if ((mp[mid] & 0xFFFFu) < cs) lo = mid + 1; else hi = mid;
     }
-    uint32_t pos = cs;
-    if (lo > 0) {
-        const uint32_t pe = (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3;
-        if (pe > pos) pos = pe;
+    // covered = positions of the chunk inside a match or past the segment
+    const uint32_t nval = ce > cs ? ce - cs : 0u;
+    uint32_t covered = nval >= 32 ? 0u : (0xFFFFFFFFu << nval);
+    auto cover = [&](uint32_t a, uint32_t b) {  // stream positions [a, b) of the chunk
+        const uint32_t l = a > cs ? a - cs : 0u, h = b - cs < 32 ? b - cs : 32u;
+        if (b > cs && l < 32) covered |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << l);
+    };
+    if (lo > 0) cover(mp[lo - 1] & 0xFFFFu, (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3);
+    uint32_t m1 = lo;
+    while (m1 < nm && (mp[m1] & 0xFFFFu) < ce) {
+        cover(mp[m1] & 0xFFFFu, (mp[m1] & 0xFFFFu) + (mp[m1] >> 16) + 3);
+        m1++;
     }
-    uint32_t m = lo;
-    uint32_t nxt = m < nm ? mp[m] : 0xFFFFFFFFu;
 #pragma unroll
-    for (uint32_t i = 0; i < (uint32_t)C::CH; i++) {
-        const uint32_t p = cs + i;
-        if (p < ce && p >= pos) {
-            if (p == (nxt & 0xFFFFu)) {
-                const uint32_t len = (nxt >> 16) + 3, dist = (uint32_t)md[m] + 1;
-                uint32_t sy, e, v;
-                len_code(len, sy, e, v);
-                slot[i] = slot_of(S.lcode[sy], v, e);
-                dist_code(dist, sy, e, v);
-                slot[i + 1] = slot_of(S.dcode[sy], 0, 0);
-                slot[i + 2] = v | (e << 27);
-                pos = p + len;
-                m++;
-                nxt = m < nm ? mp[m] : 0xFFFFFFFFu;
-            } else {
-                const uint32_t b = (cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-                slot[i] = slot_of(S.lcode[b], 0, 0);
-            }
+    for (int i = 0; i < C::CH; i++) {
+        const uint32_t b = (cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+        slot[i] = S.lcode[((covered >> i) & 1u) ? SLOT_NONE : b];
+    }
+    slot[C::CH] = 0;
+    slot[C::CH + 1] = 0;
+    for (uint32_t m = lo; m < m1; m++) {
+        const uint32_t i = (mp[m] & 0xFFFFu) - cs, len = (mp[m] >> 16) + 3, dist = (uint32_t)md[m] + 1;
+        uint32_t sy, e, v;
+        len_code(len, sy, e, v);
+        const uint32_t lc = S.lcode[sy];
+        const uint32_t A = lc + (v << (lc >> 27)) + (e << 27);
+        dist_code(dist, sy, e, v);
+        const uint32_t B = S.dcode[sy], Cx = v | (e << 27);
+#pragma unroll
+        for (int j = 0; j < C::CH + 2; j++) {
+            const uint32_t dj = (uint32_t)j - i;
+            slot[j] = dj == 0 ? A : dj == 1 ? B : dj == 2 ? Cx : slot[j];
         }
     }
 }
 
 template <class C, bool PROF>
-__global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ dt, uint32_t ndt,
+__global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ dt,
+                                                  const uint32_t* __restrict__ seg_tile,
                                                   uint32_t nseg, const uint8_t* __restrict__ stream,
                                                   SegInfo* __restrict__ info,
                                                   const uint32_t* __restrict__ mrec,
@@ -890,7 +961,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
         nst++;
     };
     stamp();
-    const uint32_t ti = upper_index(ndt, seg, [&](uint32_t i) { return dt[i].seg_first; });
+    const uint32_t ti = seg_tile[seg];
     const TileDesc d = dt[ti];
     SegParams sp = seg_params(d, seg - d.seg_first);
     sp.base += sp.wl;  // the encoder holds the segment only
@@ -916,10 +987,12 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
     const uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
     for (uint32_t i = tid; i < 320; i += C::NT) {
-        if (i < 288) S.lcode[i] = cg[i]; else S.dcode[i - 288] = cg[i];
+        if (i < 288) S.lcode[i] = slot_from_code(cg[i]); else S.dcode[i - 288] = slot_from_code(cg[i]);
     }
+    if (tid == 0) S.lcode[SLOT_NONE] = 0;
     for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT) S.out[k] = k < (uint32_t)C::HDRW ? cg[320 + k] : 0u;
     for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
+    for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
     if (tid == 0) {
         S.misc[M_BTYPE] = gi.btype; S.misc[M_HDRBITS] = gi.hdr_bits;
         S.misc[M_DATABITS] = gi.data_bits; S.misc[M_NBYTES] = gi.nbytes;
@@ -958,15 +1031,12 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     if (gi.btype != 0) {
         RunWriter<DevOps> bw(S.out, gi.hdr_bits + S.t_a[tid]);
 #pragma unroll
-        for (int i = 0; i < C::CH + 2; i++) {
-            const uint32_t n = slot[i] >> 27;
-            if (n) bw.put(slot[i] & 0x7FFFFFFu, n);
-        }
+        for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
         bw.finish();
         if (tid == 0) {  // end of block; a non-final segment ends byte-aligned
             const uint32_t eob = S.lcode[256];
-            BitWriter<DevOps> ew{S.out, gi.hdr_bits + gi.data_bits - (eob >> 16)};
-            ew.put(eob & 0xFFFF, eob >> 16);
+            BitWriter<DevOps> ew{S.out, gi.hdr_bits + gi.data_bits - (eob >> 27)};
+            ew.put(eob & 0x7FFFFFFu, eob >> 27);
             if (!sp.last) {
                 ew.put(0, 3);
                 ew.pos = (ew.pos + 7) & ~7u;
@@ -982,7 +1052,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
 #pragma unroll
     for (int k = 0; k < 6; k++) {
         const uint32_t r = __shfl_down(c, 1 << k, 64);
-        c = crc_multmodp(crc_x8pow2(C::LOG2_CRCC + k), c) ^ r;
+        c = crc_mul_nib(S, k, c) ^ r;
     }
     if (lane == 0) S.red[w] = c;
     // bytes to their final place: unaligned head and tail bytes, aligned words between
@@ -998,9 +1068,8 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     __syncthreads();
     if (tid == 0) {
         uint32_t raw = S.red[0];
-        const uint32_t opw = crc_x8pow2(C::LOG2_CRCC + 6);  // one wave = 64 chunks
-        for (int k = 1; k < C::NW; k++) raw = crc_multmodp(opw, raw) ^ S.red[k];
-        const uint32_t op = crc_x8n(nbytes);
+        for (int k = 1; k < C::NW; k++) raw = crc_mul_nib(S, 6, raw) ^ S.red[k];  // one wave = 64 chunks
+        const uint32_t op = crc_x8n_small(nbytes);
         SegInfo& g = info[seg];
         g.crc = crc_from_raw(raw, op);
         g.crc_op = op;
@@ -1095,11 +1164,13 @@ hipError_t launch_huffman(hipStream_t st, uint32_t nseg, SegInfo* info, const ui
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev) {
     if (!a.ntiles || !a.nseg) return hipSuccess;
     const bool prof = a.stamps != nullptr;
+    hipLaunchKernelGGL(k_seg_map, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
+                       a.seg_tile);
     if (prof)
-        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     else
-        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     if (ev) (void)hipEventRecord(ev[0], st);
     if (prof)
@@ -1114,10 +1185,10 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
     if (ev) (void)hipEventRecord(ev[2], st);
     if (prof)
-        hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+        hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
     else
-        hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.ntiles,
+        hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
     if (ev) (void)hipEventRecord(ev[3], st);
     hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,

@@ -173,7 +173,8 @@ struct pbx_batch {
     // device buffers (pool blocks)
     void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_stream = nullptr,
          *d_info = nullptr, *d_hist = nullptr, *d_mrec = nullptr, *d_codes = nullptr,
-         *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr;
+         *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr,
+         *d_segmap = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
@@ -227,7 +228,8 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
     void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
-                     &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps};
+                     &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps,
+                     &b->d_segmap};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -739,7 +741,8 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
         !dget(b->d_hist, ns * HIST_WORDS * 4) || !dget(b->d_mrec, ns * MREC_WORDS * 4) ||
         !dget(b->d_codes, ns * CODE_WORDS * 4) ||
         !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
-        !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap))
+        !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap) ||
+        !dget(b->d_segmap, ns * sizeof(uint32_t)))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     if (!b->ev[0])
         for (auto& e : b->ev) HIP_TRY(hipEventCreate(&e));
@@ -773,6 +776,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.offs = (uint64_t*)b->d_offs;
     a.out = (uint8_t*)b->d_png;
     a.stamps = prof ? (uint64_t*)b->d_stamps : nullptr;
+    a.seg_tile = (uint32_t*)b->d_segmap;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4));
