@@ -67,7 +67,7 @@ struct DeflateCfg {
     static_assert(CH == 32 && SUB == 64 * CH, "a lane's parse positions are its thread chunk");
     static_assert(CAP >= 6 && CAP <= 32, "capped lengths come from 64-bit equality masks");
     static_assert(SUB <= 65536 && SUB % CH == 0, "sub-segments hold whole thread chunks");
-    static_assert(WIN + SEG <= 32768, "deflate distances are limited to 32768");
+    static_assert(WIN <= 32768 && SEG <= 32768, "distances <= one row <= 32768; 16-bit positions");
     static_assert((1 << LOGNT) == NT, "NT must be a power of two in 128..1024");
     static_assert(NT * CRCC >= SEG + 64, "CRC chunks cover the output");
     static_assert(CH % 4 == 0 && WIN % 16 == 0, "Adler chunks are whole aligned words");

@@ -85,42 +85,103 @@ void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, last);
 }
 
-// k_lz77, k_huff and k_encode of one segment, thread by thread; -2 if the encoder's bit
-// count disagrees with the Huffman step's (a broken invariant).
+// Sequential bit writer of one block's tokens (the order k_encode's scan reproduces).
+struct SeqWriter {
+    const Smem& H;  // the block's codes (lcode / dcode: code | len << 16)
+    BitWriter<EmuOps> bw;
+    void lit(uint32_t b) { const uint32_t c = H.lcode[b]; bw.put(c & 0xFFFF, c >> 16); }
+    void match(uint32_t len, uint32_t dist) {
+        uint32_t s, e, v;
+        len_code(len, s, e, v);
+        uint32_t c = H.lcode[s];
+        bw.put(c & 0xFFFF, c >> 16);
+        bw.put(v, e);
+        dist_code(dist, s, e, v);
+        c = H.dcode[s];
+        bw.put(c & 0xFFFF, c >> 16);
+        bw.put(v, e);
+    }
+};
+
+// k_lz77 of one segment, thread by thread (the phases' effects commute): matches, the
+// histogram (one end of block counted) and the Adler-32 partial sums.
 template <class Src>
-int run_segment(Smem& S, const Src& src, const SegParams& sp, uint8_t* slot, SegOut* so) {
-    // ---- k_lz77
+void run_lz77(Smem& S, const Src& src, const SegParams& sp, uint32_t& a1, uint32_t& a2) {
     for (int t = 0; t < C::NT; t++) ph_fill<C>(t, S, src, sp);
     for (int t = 0; t < C::NT; t++) ph_lz_init<C>(t, S);
     for (int w = 0; w < C::NW; w++) ph_parse_emu<C>(w, S, sp);
-    uint32_t a1 = 0, a2 = 0;
+    a1 = 0; a2 = 0;
     for (int t = 0; t < C::NT; t++) {
         uint32_t s1, s2, n;
         ph_hist<C, EmuOps>(t, S, sp, s1, s2, n);
         adler_combine(a1, a2, s1, s2, n);
     }
-    run_huff(S, sp.sl, sp.last);
-    // ---- k_encode
-    for (int t = 0; t < C::NT; t++) ph_enc_init<C>(t, S, S.hdrw);
-    if (S.misc[M_BTYPE] == 0)
-        for (int t = 0; t < C::NT; t++) ph_stored<C>(t, S, sp);
-    for (int t = 0; t < C::NT; t++) S.t_a[t] = ph_bits<C>(t, S, sp);
-    const uint32_t bitsum = scan_excl_add(S.t_a, C::NT);
-    if (S.misc[M_BTYPE] != 0 && bitsum != S.misc[M_DATABITS] - (S.lcode[256] >> 16)) return -2;
-    for (int t = 0; t < C::NT; t++) ph_write<C, EmuOps>(t, S, sp, S.t_a[t]);
-    const uint32_t nbytes = S.misc[M_NBYTES];
-    for (uint32_t j = 0; j < nbytes; j++) slot[j] = (uint8_t)out_byte(S, j);
-    uint32_t raw = 0;
-    const uint32_t opc = crc_x8pow2(C::LOG2_CRCC);
-    for (int t = 0; t < C::NT; t++) raw = crc_multmodp(opc, raw) ^ ph_crc<C>(t, S);
+}
+
+// One deflate block of nsg segments (k_lz77 per segment, k_huff on the summed histogram,
+// k_encode of every segment into the block's bits); out gets the block's bytes.  -1 when
+// cap is too small.
+template <class Src>
+int run_block(std::vector<std::unique_ptr<Smem>>& LZ, Smem& H, const Src& src, const SegParams* sps,
+              uint32_t nsg, uint8_t* out, uint64_t cap, SegOut* so) {
+    uint32_t sl = 0, a1 = 0, a2 = 0;
+    for (uint32_t k = 0; k < nsg; k++) {
+        memset(LZ[k].get(), 0xCD, sizeof(Smem));  // poison: phases must initialise what they read
+        uint32_t s1, s2;
+        run_lz77(*LZ[k], src, sps[k], s1, s2);
+        adler_combine(a1, a2, s1, s2, sps[k].sl);
+        sl += sps[k].sl;
+    }
+    const uint32_t last = sps[nsg - 1].last;
+    memset(&H, 0xCD, sizeof(Smem));
+    for (int i = 0; i < 288; i++) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < nsg; k++) v += LZ[k]->lfreq[i];
+        H.lfreq[i] = i == 256 ? 1u : v;
+    }
+    for (int i = 0; i < 32; i++) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < nsg; k++) v += LZ[k]->dfreq[i];
+        H.dfreq[i] = v;
+    }
+    run_huff(H, sl, last);
+    for (uint32_t k = 0; k < 256; k++) H.crc_t[0][k] = crc_table_entry(k);
+    const uint32_t bt = H.misc[M_BTYPE], nbytes = H.misc[M_NBYTES];
+    if (nbytes > cap) return -1;
+    std::vector<uint32_t> words((nbytes + 8) / 4 + 2, 0);
+    if (bt == 0) {
+        uint8_t* o = (uint8_t*)words.data();
+        o[0] = last ? 1 : 0;
+        o[1] = (uint8_t)sl; o[2] = (uint8_t)(sl >> 8); o[3] = (uint8_t)~sl; o[4] = (uint8_t)(~sl >> 8);
+        uint32_t p = 5;
+        for (uint32_t k = 0; k < nsg; k++)
+            for (uint32_t j = 0; j < sps[k].sl; j++) o[p++] = (uint8_t)lds_byte(*LZ[k], sps[k].wl + j);
+    } else {
+        const uint32_t hdr = H.misc[M_HDRBITS];
+        for (uint32_t w = 0; w < (hdr + 31) / 32; w++) words[w] = H.hdrw[w];
+        SeqWriter f{H, BitWriter<EmuOps>{words.data(), hdr}};
+        for (uint32_t k = 0; k < nsg; k++)
+            for (int t = 0; t < C::NT; t++) walk_tokens<C>((uint32_t)t, *LZ[k], sps[k], f);
+        if (f.bw.pos != hdr + H.misc[M_DATABITS] - (H.lcode[256] >> 16)) return -2;
+        const uint32_t eob = H.lcode[256];
+        f.bw.put(eob & 0xFFFF, eob >> 16);
+        if (!last) {
+            f.bw.put(0, 3);
+            f.bw.pos = (f.bw.pos + 7) & ~7u;
+            f.bw.put(0xFFFF0000u, 32);
+        }
+    }
+    memcpy(out, words.data(), nbytes);
     so->nbytes = nbytes;
     so->crc_op = crc_x8n(nbytes);
-    so->crc = crc_from_raw(raw, so->crc_op);
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < nbytes; j++) c = crc_update(H.crc_t[0], c, out[j]);
+    so->crc = c ^ 0xFFFFFFFFu;
     so->adler_s1 = a1;
     so->adler_s2 = a2;
-    so->len = sp.sl;
-    so->btype = S.misc[M_BTYPE];
-    so->bits = S.misc[M_HDRBITS] + S.misc[M_DATABITS];
+    so->len = sl;
+    so->btype = bt;
+    so->bits = H.misc[M_HDRBITS] + H.misc[M_DATABITS];
     return 0;
 }
 
@@ -143,34 +204,44 @@ uint32_t pbxemu_nsegs(uint64_t len) {
     return n;
 }
 
+uint32_t pbxemu_nblocks(uint64_t len) { return tile_blocks(pbxemu_nsegs(len)); }
+
+// Deflate `len` bytes into a zlib stream exactly as the batch pipeline does for one tile:
+// segments of deflate_split, each with its row-sized window, BLK_SEGS segments per block
+// sharing one Huffman code, combined Adler-32.  rowlen: the row-up candidate distance.
+// Per-block results go to blks (may be NULL, else room for pbxemu_nblocks(len)).  Returns
+// 0, -1 if cap is too small, -2 on a broken invariant.
 int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t* out,
-                   uint64_t cap, uint64_t* out_len, SegOut* segs) {
+                   uint64_t cap, uint64_t* out_len, SegOut* blks) {
     uint32_t nseg, seg_len;
     deflate_split(len, nseg, seg_len);
-    std::unique_ptr<Smem> S(new Smem());
-    std::vector<uint8_t> slot(C::SEG + 256);
+    std::vector<std::unique_ptr<Smem>> LZ;
+    for (uint32_t k = 0; k < BLK_SEGS; k++) LZ.emplace_back(new Smem());
+    std::unique_ptr<Smem> H(new Smem());
     MemStream src{stream};
     uint64_t o = 0;
     if (cap < 2) return -1;
     out[o++] = 0x78;
     out[o++] = 0x9C;
     uint32_t s1 = 0, s2 = 0;
-    for (uint32_t k = 0; k < nseg; k++) {
-        SegParams sp;
-        const uint64_t s = (uint64_t)k * seg_len;
-        sp.sl = (uint32_t)((len - s) < seg_len ? (len - s) : seg_len);
-        sp.wl = seg_window<C>(s, rowlen);
-        sp.base = s - sp.wl;
-        sp.rowlen = rowlen;
-        sp.last = k + 1 == nseg;
-        memset(S.get(), 0xCD, sizeof(Smem));  // poison: phases must initialise what they read
+    for (uint32_t k0 = 0, bi = 0; k0 < nseg; k0 += BLK_SEGS, bi++) {
+        const uint32_t nsg = nseg - k0 < BLK_SEGS ? nseg - k0 : BLK_SEGS;
+        SegParams sps[BLK_SEGS];
+        for (uint32_t q = 0; q < nsg; q++) {
+            SegParams& sp = sps[q];
+            const uint64_t s = (uint64_t)(k0 + q) * seg_len;
+            sp.sl = (uint32_t)((len - s) < seg_len ? (len - s) : seg_len);
+            sp.wl = seg_window<C>(s, rowlen);
+            sp.base = s - sp.wl;
+            sp.rowlen = rowlen;
+            sp.last = k0 + q + 1 == nseg;
+        }
         SegOut so;
-        if (run_segment(*S, src, sp, slot.data(), &so)) return -2;
-        if (o + so.nbytes > cap) return -1;
-        memcpy(out + o, slot.data(), so.nbytes);
+        const int r = run_block(LZ, *H, src, sps, nsg, out + o, cap - o, &so);
+        if (r) return r;
         o += so.nbytes;
         adler_combine(s1, s2, so.adler_s1, so.adler_s2, so.len);
-        if (segs) segs[k] = so;
+        if (blks) blks[bi] = so;
     }
     if (o + 4 > cap) return -1;
     const uint32_t ad = adler_final(s1, s2, len);
@@ -230,7 +301,7 @@ uint32_t pbxemu_mrec_words(void) { return MREC_WORDS; }
 int pbxemu_huffman(const uint32_t* hist, uint32_t sl, uint32_t last, uint32_t* codes, uint32_t* info) {
     std::unique_ptr<Smem> S(new Smem());
     memset(S.get(), 0xCD, sizeof(Smem));
-    for (int i = 0; i < 288; i++) S->lfreq[i] = hist[i];
+    for (int i = 0; i < 288; i++) S->lfreq[i] = i == 256 ? 1u : hist[i];  // one end of block
     for (int i = 0; i < 32; i++) S->dfreq[i] = hist[288 + i];
     run_huff(*S, sl, last);
     for (int i = 0; i < 288; i++) codes[i] = S->lcode[i];

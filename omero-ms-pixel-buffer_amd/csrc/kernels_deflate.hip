@@ -108,9 +108,9 @@ constexpr CrcNibTables make_crc_nib(int log2c) {
 }
 __constant__ const CrcNibTables kCrcNib = make_crc_nib(DC::LOG2_CRCC);
 
-// x^(8n) mod P for n < 2^15 from two tables: x^(8v) and x^(8*256*v).
+// x^(8n) mod P for n < 2^16 from two tables: x^(8v) and x^(8*256*v).
 struct CrcPowTables {
-    uint32_t lo[256], hi[128];
+    uint32_t lo[256], hi[256];
 };
 constexpr CrcPowTables make_crc_pow() {
     CrcPowTables T{};
@@ -121,9 +121,9 @@ constexpr CrcPowTables make_crc_pow() {
             if ((v >> k) & 1u) p = crc_multmodp_c(x.v[k], p);
         T.lo[v] = p;
     }
-    for (uint32_t v = 0; v < 128; v++) {
+    for (uint32_t v = 0; v < 256; v++) {
         uint32_t p = 1u << 31;
-        for (int k = 0; k < 7; k++)
+        for (int k = 0; k < 8; k++)
             if ((v >> k) & 1u) p = crc_multmodp_c(x.v[8 + k], p);
         T.hi[v] = p;
     }
@@ -139,8 +139,8 @@ __device__ __forceinline__ uint32_t crc_mul_nib(const SM& S, int k, uint32_t b) 
     return r;
 }
 
-__device__ __forceinline__ uint32_t crc_x8n_small(uint32_t n) {  // n < 2^15
-    return crc_multmodp(kCrcPow.lo[n & 0xFFu], kCrcPow.hi[(n >> 8) & 0x7Fu]);
+__device__ __forceinline__ uint32_t crc_x8n_small(uint32_t n) {  // n < 2^16
+    return crc_multmodp(kCrcPow.lo[n & 0xFFu], kCrcPow.hi[(n >> 8) & 0xFFu]);
 }
 
 // Segment geometry from the tile descriptor.
@@ -326,7 +326,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
 }
 
 template <class C, bool PROF>
-__global__ __launch_bounds__(C::NT) void k_lz77(const TileDesc* __restrict__ dt,
+__global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, const uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
@@ -729,25 +729,33 @@ __device__ void clen_wave(SM& S, uint32_t lane) {
     if (lane == 0) S.misc[M_HCLEN] = hclen < 4 ? 4u : hclen;
 }
 
+// One Huffman block = the BLK_SEGS (or fewer, at a tile's end) consecutive segments of
+// one tile whose histograms it sums; one wave per block.
 template <class C, bool PROF>
-__global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict__ info,
+__global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict__ blk,
+                                             SegInfo* __restrict__ info,
                                              const uint32_t* __restrict__ hist,
                                              uint32_t* __restrict__ codes,
                                              uint64_t* __restrict__ stamps) {
     __shared__ HuffSmem<C> S;
     const uint32_t tid = threadIdx.x;
-    const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t seg0 = blk[b].seg0, nsg = blk[b].nseg;
     uint32_t nst = 0;
     auto stamp = [&]() {
-        if (PROF && tid == 0) stamps[(size_t)seg * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
+        if (PROF && tid == 0) stamps[(size_t)seg0 * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
         nst++;
     };
     stamp();
-    const uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
     for (uint32_t i = tid; i < HIST_WORDS; i += 64) {
-        if (i < 288) S.lfreq[i] = hg[i]; else S.dfreq[i - 288] = hg[i];
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < nsg; k++) v += hist[(size_t)(seg0 + k) * HIST_WORDS + i];
+        if (i == 256) v = 1;  // one end of block (every segment's histogram counted one)
+        if (i < 288) S.lfreq[i] = v; else S.dfreq[i - 288] = v;
     }
-    const uint32_t sl = info[seg].sl, last = info[seg].last;
+    uint32_t sl = 0;
+    for (uint32_t k = 0; k < nsg; k++) sl += info[seg0 + k].sl;
+    const uint32_t last = info[seg0 + nsg - 1].last;
     ph_huff_init<C>(tid, S);
     __syncthreads();
     ph_keys<C, DevOps>(tid, S);
@@ -805,28 +813,66 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nseg, SegInfo* __restrict_
     ph_header<C, DevOps>(tid, S, last);
     __syncthreads();
     stamp();
-    uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
+    uint32_t* cg = codes + (size_t)b * CODE_WORDS;
     for (uint32_t i = tid; i < CODE_WORDS; i += 64)
         cg[i] = i < 288 ? S.lcode[i] : i < 320 ? S.dcode[i - 288] : S.hdrw[i - 320];
+    // every segment's bit range in the block: [header] tokens of segment 0, 1, ... [EOB]
+    // [empty stored block unless the tile ends here]; a stored block is byte-aligned
+    const uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
+    uint32_t run = bt == 0 ? 40u : hdr;
+    for (uint32_t k = 0; k < nsg; k++) {
+        const uint32_t* hk = hist + (size_t)(seg0 + k) * HIST_WORDS;
+        uint32_t d = 0;
+        if (bt == 0) {
+            d = 8 * info[seg0 + k].sl;
+        } else {
+            for (uint32_t i = tid; i < 320; i += 64) {
+                if (i == 256 || (i >= 286 && i < 288) || i >= 318) continue;
+                const uint32_t f = hk[i];
+                if (!f) continue;
+                const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i - 288]) >> 16;
+                const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i - 288);
+                d += f * (L + eb);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+        }
+        if (tid == 0) {
+            SegInfo& g = info[seg0 + k];
+            g.btype = bt;
+            g.hdr_bits = hdr;
+            g.bit0 = k == 0 ? 0u : run;
+            run += d;
+            g.bit1 = k + 1 < nsg ? run : last ? (bt == 0 ? 8 * nbytes : run + (S.lcode[256] >> 16)) : 8 * nbytes;
+        }
+    }
     if (tid == 0) {
-        SegInfo& g = info[seg];
-        g.btype = S.misc[M_BTYPE];
-        g.hdr_bits = S.misc[M_HDRBITS];
-        g.data_bits = S.misc[M_DATABITS];
-        g.nbytes = S.misc[M_NBYTES];
+        blk[b].nbytes = nbytes;
+        blk[b].data_bits = S.misc[M_DATABITS];
+        blk[b].fin = last;
     }
     stamp();
 }
 
 // ================================================================= k_seg_map
-// The tile of every segment (one thread per tile), so the per-segment kernels find their
-// tile descriptor with one load.
+// Per tile (one thread): the tile of every segment, so the per-segment kernels find their
+// tile descriptor with one load, and the tile's Huffman blocks.
 __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                 uint32_t* __restrict__ seg_tile) {
+                                                 uint32_t* __restrict__ seg_tile,
+                                                 SegInfo* __restrict__ info, BlkInfo* __restrict__ blk) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= ndt) return;
-    const uint32_t f = dt[i].seg_first, n = dt[i].seg_count;
-    for (uint32_t k = 0; k < n; k++) seg_tile[f + k] = i;
+    const uint32_t f = dt[i].seg_first, n = dt[i].seg_count, hb = dt[i].hblk_first;
+    for (uint32_t k = 0; k < n; k++) {
+        seg_tile[f + k] = i;
+        const uint32_t j = k / BLK_SEGS, r = k % BLK_SEGS;
+        info[f + k].blk = hb + j;
+        info[f + k].flags = (r == 0 ? SF_FIRST : 0u) | (r + 1 == BLK_SEGS || k + 1 == n ? SF_LAST : 0u);
+        if (r == 0) {
+            blk[hb + j].seg0 = f + k;
+            blk[hb + j].nseg = n - k < BLK_SEGS ? n - k : BLK_SEGS;
+        }
+    }
 }
 
 // ================================================================ k_seg_sizes
@@ -836,14 +882,15 @@ __device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t 
 }
 
 __global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                   SegInfo* __restrict__ info,
+                                                   BlkInfo* __restrict__ blk,
                                                    uint64_t* __restrict__ sizes) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= ndt) return;
     const TileDesc& d = dt[i];
     uint32_t off = 0;
-    for (uint32_t k = 0; k < d.seg_count; k++) {
-        SegInfo& g = info[d.seg_first + k];
+    const uint32_t nb = tile_blocks(d.seg_count);
+    for (uint32_t k = 0; k < nb; k++) {
+        BlkInfo& g = blk[d.hblk_first + k];
         g.off = off;
         off += g.nbytes;
     }
@@ -941,11 +988,17 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
     }
 }
 
+// One segment's part of its block: the header (first segment), its tokens, and the end of
+// block (+ the empty stored block of a non-final block; last segment) at the bits
+// [bit0, bit1) k_huff assigned.  The bytes it owns entirely go straight to the compacted
+// output; a byte it shares with the previous / next segment of the block (bit0 or bit1 not
+// on a byte boundary) is left to k_frame (SegInfo.part), which ORs the two halves.
 template <class C, bool PROF>
-__global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ dt,
+__global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict__ dt,
                                                   const uint32_t* __restrict__ seg_tile,
                                                   uint32_t nseg, const uint8_t* __restrict__ stream,
                                                   SegInfo* __restrict__ info,
+                                                  const BlkInfo* __restrict__ blk,
                                                   const uint32_t* __restrict__ mrec,
                                                   const uint32_t* __restrict__ codes,
                                                   const uint64_t* __restrict__ offs,
@@ -967,6 +1020,11 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     sp.base += sp.wl;  // the encoder holds the segment only
     sp.wl = 0;
     const SegInfo gi = info[seg];
+    const BlkInfo bi = blk[gi.blk];
+    const bool first = (gi.flags & SF_FIRST) != 0, lastb = (gi.flags & SF_LAST) != 0;
+    const bool final_seg = sp.last != 0;          // the tile's stream ends in this segment
+    const uint32_t byte0 = gi.bit0 >> 3, lb = gi.bit0 & 7u;  // out[] byte 0 = block byte byte0
+    const uint32_t le = gi.bit1 - 8 * byte0;      // end bit in out[]
     // the thread's chunk bytes (zero past the segment) straight into registers
     uint32_t cb[C::CH / 4];
     {
@@ -985,18 +1043,15 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     }
     const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
     if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
-    const uint32_t* cg = codes + (size_t)seg * CODE_WORDS;
+    const uint32_t* cg = codes + (size_t)gi.blk * CODE_WORDS;
     for (uint32_t i = tid; i < 320; i += C::NT) {
         if (i < 288) S.lcode[i] = slot_from_code(cg[i]); else S.dcode[i - 288] = slot_from_code(cg[i]);
     }
     if (tid == 0) S.lcode[SLOT_NONE] = 0;
-    for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT) S.out[k] = k < (uint32_t)C::HDRW ? cg[320 + k] : 0u;
+    for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT)
+        S.out[k] = (first && gi.btype != 0 && k < (uint32_t)C::HDRW) ? cg[320 + k] : 0u;
     for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
     for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
-    if (tid == 0) {
-        S.misc[M_BTYPE] = gi.btype; S.misc[M_HDRBITS] = gi.hdr_bits;
-        S.misc[M_DATABITS] = gi.data_bits; S.misc[M_NBYTES] = gi.nbytes;
-    }
     __syncthreads();
     for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
         if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
@@ -1004,16 +1059,17 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
             S.mdist[i] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + i];
         }
     }
-    if (gi.btype == 0) {  // stored block: header byte, LEN, NLEN, then the bytes
+    if (gi.btype == 0) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; bytes
         uint8_t* ob = (uint8_t*)S.out;
-        const uint32_t cs = tid * C::CH;
+        const uint32_t cs = tid * C::CH, o = first ? 5u : 0u;
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
-            if (cs + i < sp.sl) ob[5 + cs + i] = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
-        if (tid == 0) {
-            ob[0] = sp.last ? 1 : 0;
-            ob[1] = (uint8_t)sp.sl; ob[2] = (uint8_t)(sp.sl >> 8);
-            ob[3] = (uint8_t)~sp.sl; ob[4] = (uint8_t)(~sp.sl >> 8);
+            if (cs + i < sp.sl) ob[o + cs + i] = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
+        if (first && tid == 0) {
+            const uint32_t len = bi.nbytes - 5;  // LEN: every byte of the block's segments
+            ob[0] = (uint8_t)(bi.fin ? 1 : 0);
+            ob[1] = (uint8_t)len; ob[2] = (uint8_t)(len >> 8);
+            ob[3] = (uint8_t)~len; ob[4] = (uint8_t)(~len >> 8);
         }
     }
     __syncthreads();
@@ -1029,15 +1085,16 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
     stamp();
     const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
     if (gi.btype != 0) {
-        RunWriter<DevOps> bw(S.out, gi.hdr_bits + S.t_a[tid]);
+        const uint32_t tb = lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
+        RunWriter<DevOps> bw(S.out, tb + S.t_a[tid]);
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
         bw.finish();
-        if (tid == 0) {  // end of block; a non-final segment ends byte-aligned
+        if (lastb && tid == 0) {  // end of block; a non-final block ends byte-aligned
             const uint32_t eob = S.lcode[256];
-            BitWriter<DevOps> ew{S.out, gi.hdr_bits + gi.data_bits - (eob >> 27)};
+            BitWriter<DevOps> ew{S.out, tb + bitsum};
             ew.put(eob & 0x7FFFFFFu, eob >> 27);
-            if (!sp.last) {
+            if (!final_seg) {
                 ew.put(0, 3);
                 ew.pos = (ew.pos + 7) & ~7u;
                 ew.put(0xFFFF0000u, 32);
@@ -1045,9 +1102,24 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
         }
     }
     __syncthreads();
+    // bytes owned: [o0, o1) of out[]; a partial first byte (lb != 0) and a partial last
+    // byte of a non-final segment are shared with the neighbours (k_frame joins them)
+    const uint32_t o0 = lb ? 1u : 0u;
+    uint32_t o1 = final_seg ? (le + 7) >> 3 : le >> 3;
+    if (o1 < o0) o1 = o0;
+    const bool has_tail = !final_seg && (le & 7u) && !(lb && (le >> 3) == 0);
+    if (tid == 0) {
+        uint32_t part = 0;
+        if (lb) part |= out_byte(S, 0) | SP_HEAD;
+        if (has_tail) part |= (out_byte(S, le >> 3) << 8) | SP_TAIL;
+        S.misc[M_CRCOP] = part;
+        if (lb) ((uint8_t*)S.out)[0] = 0;  // leading zero bytes leave a raw CRC unchanged
+        S.misc[M_NBYTES] = o1;
+    }
+    __syncthreads();
     stamp();
-    // CRC-32: raw CRC of right-aligned 64-byte chunks, combined per wave by shuffles with
-    // the constant operators x^(8*64*2^k), then across the waves
+    // CRC-32 of out[0, o1): raw CRC of right-aligned 64-byte chunks, combined per wave by
+    // shuffles with the constant operators x^(8*64*2^k), then across the waves
     uint32_t c = ph_crc<C>(tid, S);
 #pragma unroll
     for (int k = 0; k < 6; k++) {
@@ -1055,16 +1127,16 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
         c = crc_mul_nib(S, k, c) ^ r;
     }
     if (lane == 0) S.red[w] = c;
-    // bytes to their final place: unaligned head and tail bytes, aligned words between
-    const uint32_t nbytes = gi.nbytes;
+    // owned bytes to their final place: unaligned head and tail bytes, aligned words between
+    const uint32_t nbytes = o1 - o0;
     const uint32_t zoff = (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
-    uint8_t* dst = out + offs[ti] + zoff + ZLIB_HDR_BYTES + gi.off;
+    uint8_t* dst = out + offs[ti] + zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
     const uint32_t nwords = (nbytes - head) >> 2;
-    if (tid < head) dst[tid] = (uint8_t)out_byte(S, tid);
-    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, head + 4 * k);
-    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, j);
+    if (tid < head) dst[tid] = (uint8_t)out_byte(S, o0 + tid);
+    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, o0 + head + 4 * k);
+    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, o0 + j);
     __syncthreads();
     if (tid == 0) {
         uint32_t raw = S.red[0];
@@ -1073,6 +1145,7 @@ __global__ __launch_bounds__(C::NT) void k_encode(const TileDesc* __restrict__ d
         SegInfo& g = info[seg];
         g.crc = crc_from_raw(raw, op);
         g.crc_op = op;
+        g.part = S.misc[M_CRCOP];
         g.bitsum = bitsum;
     }
     stamp();
@@ -1096,9 +1169,11 @@ __device__ uint32_t put_chunk(uint8_t* o, const char* type, const uint8_t* data,
     return 12 + n;
 }
 
-// One thread per tile: everything around the segments' bytes.
+// One thread per tile: everything around the segments' bytes, and the bytes two segments
+// of a block share (SegInfo.part), joined in stream order into the output and the IDAT CRC.
 __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, uint32_t ndt,
                                               const SegInfo* __restrict__ info,
+                                              const BlkInfo* __restrict__ blk,
                                               const uint64_t* __restrict__ offs,
                                               uint8_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -1111,37 +1186,70 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
     for (uint32_t k = 0; k < d.seg_count; k++) {
         const SegInfo& g = info[d.seg_first + k];
         adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.sl);
-        payload += g.nbytes;
     }
+    const uint32_t nb = tile_blocks(d.seg_count);
+    for (uint32_t k = 0; k < nb; k++) payload += blk[d.hblk_first + k].nbytes;
     const uint32_t adler = adler_final(s1, s2, d.stream_len);
     const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;
     base[zoff] = 0x78;      // CMF: deflate, 32 KiB window
     base[zoff + 1] = 0x9C;  // FLG: default level (Deflater -1 == 6), check bits
     put_be32(base + pos, adler);
+    uint32_t o = 8;
+    if (!tiff) {
+        const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+        for (int j = 0; j < 8; j++) base[j] = sig[j];
+        uint8_t buf[26];
+        put_be32(buf, d.w); put_be32(buf + 4, d.h);
+        buf[8] = (uint8_t)(8 * d.bpp); buf[9] = 0; buf[10] = 0; buf[11] = 0; buf[12] = 0;
+        o += put_chunk(base + o, "IHDR", buf, 13);
+        put_be32(buf, 1); put_be32(buf + 4, 0);  // acTL: 1 frame, 0 plays
+        o += put_chunk(base + o, "acTL", buf, 8);
+        for (int j = 0; j < 26; j++) buf[j] = 0;  // fcTL: seq 0, w, h, offsets 0, delay 0/0, ops 0
+        put_be32(buf + 4, d.w); put_be32(buf + 8, d.h);
+        o += put_chunk(base + o, "fcTL", buf, 26);
+        // IDAT: length, type, zlib stream
+        put_be32(base + o, ZLIB_HDR_BYTES + payload + 4);
+        base[o + 4] = 'I'; base[o + 5] = 'D'; base[o + 6] = 'A'; base[o + 7] = 'T';
+    }
+    // CRC over type + zlib stream (PNG), joined from the segments' CRCs and shared bytes
+    uint32_t c = tiff ? 0u : crc_bits(0xFFFFFFFFu, base + o + 4, 4 + ZLIB_HDR_BYTES) ^ 0xFFFFFFFFu;
+    uint8_t* z = base + zoff + ZLIB_HDR_BYTES;
+    for (uint32_t k = 0; k < nb; k++) {
+        const BlkInfo bi = blk[d.hblk_first + k];
+        bool pend = false;
+        uint32_t pv = 0, pidx = 0;
+        auto flush = [&]() {
+            const uint8_t v = (uint8_t)pv;
+            z[bi.off + pidx] = v;
+            if (!tiff) c = crc_bits(c ^ 0xFFFFFFFFu, &v, 1) ^ 0xFFFFFFFFu;
+            pend = false;
+        };
+        for (uint32_t q = 0; q < bi.nseg; q++) {
+            const SegInfo& g = info[bi.seg0 + q];
+            const uint32_t b0 = g.bit0 >> 3, le = g.bit1 - 8 * b0, o0 = (g.bit0 & 7u) ? 1u : 0u;
+            uint32_t o1 = g.last ? (le + 7) >> 3 : le >> 3;
+            if (o1 < o0) o1 = o0;
+            if (g.part & SP_HEAD) {
+                if (!pend) { pend = true; pv = 0; pidx = b0; }
+                pv |= g.part & 0xFFu;
+            }
+            if (o1 > o0) {
+                if (pend) flush();
+                if (!tiff) c = crc_combine_op(c, g.crc, g.crc_op);
+            }
+            if (g.part & SP_TAIL) {
+                if (pend) flush();
+                pend = true;
+                pv = (g.part >> 8) & 0xFFu;
+                pidx = g.bit1 >> 3;
+            }
+        }
+        if (pend) flush();
+    }
     if (tiff) {
         write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8,
                           ZLIB_HDR_BYTES + payload + 4);
         return;
-    }
-    const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
-    for (int j = 0; j < 8; j++) base[j] = sig[j];
-    uint32_t o = 8;
-    uint8_t buf[26];
-    put_be32(buf, d.w); put_be32(buf + 4, d.h);
-    buf[8] = (uint8_t)(8 * d.bpp); buf[9] = 0; buf[10] = 0; buf[11] = 0; buf[12] = 0;
-    o += put_chunk(base + o, "IHDR", buf, 13);
-    put_be32(buf, 1); put_be32(buf + 4, 0);  // acTL: 1 frame, 0 plays
-    o += put_chunk(base + o, "acTL", buf, 8);
-    for (int j = 0; j < 26; j++) buf[j] = 0;  // fcTL: seq 0, w, h, offsets 0, delay 0/0, ops 0
-    put_be32(buf + 4, d.w); put_be32(buf + 8, d.h);
-    o += put_chunk(base + o, "fcTL", buf, 26);
-    // IDAT: length, type, zlib stream; CRC over type + data combined from segment CRCs
-    put_be32(base + o, ZLIB_HDR_BYTES + payload + 4);
-    base[o + 4] = 'I'; base[o + 5] = 'D'; base[o + 6] = 'A'; base[o + 7] = 'T';
-    uint32_t c = crc_bits(0xFFFFFFFFu, base + o + 4, 4 + ZLIB_HDR_BYTES) ^ 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < d.seg_count; k++) {
-        const SegInfo& g = info[d.seg_first + k];
-        c = crc_combine_op(c, g.crc, g.crc_op);
     }
     c = crc_bits(c ^ 0xFFFFFFFFu, base + pos, 4) ^ 0xFFFFFFFFu;
     put_be32(base + pos + 4, c);
@@ -1153,11 +1261,11 @@ size_t deflate_lds_bytes(int kernel) {
     return kernel == 0 ? sizeof(LzSmem<DC>) : kernel == 1 ? sizeof(HuffSmem<DC>) : sizeof(EncSmem<DC>);
 }
 
-hipError_t launch_huffman(hipStream_t st, uint32_t nseg, SegInfo* info, const uint32_t* hist,
-                          uint32_t* codes) {
-    if (nseg)
-        hipLaunchKernelGGL((k_huff<DC, false>), dim3(nseg), dim3(64), 0, st, nseg, info, hist, codes,
-                           nullptr);
+hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* info,
+                          const uint32_t* hist, uint32_t* codes) {
+    if (nblk)
+        hipLaunchKernelGGL((k_huff<DC, false>), dim3(nblk), dim3(64), 0, st, nblk, blk, info, hist,
+                           codes, nullptr);
     return hipGetLastError();
 }
 
@@ -1165,7 +1273,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     if (!a.ntiles || !a.nseg) return hipSuccess;
     const bool prof = a.stamps != nullptr;
     hipLaunchKernelGGL(k_seg_map, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
-                       a.seg_tile);
+                       a.seg_tile, a.info, a.blk);
     if (prof)
         hipLaunchKernelGGL((k_lz77<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
@@ -1174,25 +1282,25 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     if (ev) (void)hipEventRecord(ev[0], st);
     if (prof)
-        hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nseg), dim3(64), 0, st, a.nseg, a.info, a.hist,
-                           a.codes, a.stamps);
+        hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
+                           a.hist, a.codes, a.stamps);
     else
-        hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nseg), dim3(64), 0, st, a.nseg, a.info, a.hist,
-                           a.codes, a.stamps);
+        hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
+                           a.hist, a.codes, a.stamps);
     if (ev) (void)hipEventRecord(ev[1], st);
     hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
-                       a.info, a.sizes);
+                       a.blk, a.sizes);
     hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
     if (ev) (void)hipEventRecord(ev[2], st);
     if (prof)
         hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
+                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
     else
         hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.mrec, a.codes, a.offs, a.out, a.stamps);
+                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
     if (ev) (void)hipEventRecord(ev[3], st);
     hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
-                       a.offs, a.out);
+                       a.blk, a.offs, a.out);
     return hipGetLastError();
 }
 

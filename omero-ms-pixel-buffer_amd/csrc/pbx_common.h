@@ -61,6 +61,8 @@ struct alignas(16) TileDesc {
     uint32_t rowfilt_off;   // (unused)
     uint32_t blk_first;     // first workgroup of this tile (extract / filter bands)
     uint32_t rows_per_blk;  // extract: rows handled by one workgroup
+    uint32_t hblk_first;    // deflate tiles: first Huffman block index in the batch
+    uint32_t pad_[3];
 };
 
 // Per-segment deflate result.
@@ -77,13 +79,24 @@ struct SegOut {
 
 // Per-segment record of the three deflate kernels (64 bytes, in HBM).
 struct SegInfo {
-    uint32_t sl, last, wl, rowlen;       // k_lz77: geometry
+    uint32_t sl, last, wl, rowlen;       // k_lz77: geometry (last: the tile's final segment)
     uint32_t adler_s1, adler_s2;         // k_lz77: Adler-32 partial sums of the sl bytes
-    uint32_t btype, hdr_bits;            // k_huff: block type, header bits
-    uint32_t data_bits, nbytes;          // k_huff: data bits (EOB included), output bytes
-    uint32_t crc, crc_op;                // k_encode: CRC-32 of the output bytes, x^(8*nbytes)
-    uint32_t off;                        // k_seg_sizes: byte offset in the tile's payload
+    uint32_t btype, hdr_bits;            // k_huff: its block's type and header bits
+    uint32_t bit0, bit1;                 // k_huff: the segment's bits [bit0, bit1) of its block
+    uint32_t crc, crc_op;                // k_encode: CRC-32 of the bytes it owns, x^(8*owned)
+    uint32_t blk, flags;                 // k_seg_map: block index; SF_FIRST / SF_LAST in block
+    uint32_t part;                       // k_encode: head | tail << 8 | SP_HEAD | SP_TAIL
     uint32_t bitsum;                     // k_encode: token bits (diagnostics)
+};
+constexpr uint32_t SF_FIRST = 1, SF_LAST = 2;
+constexpr uint32_t SP_HEAD = 1u << 16, SP_TAIL = 1u << 17;
+
+// Per Huffman block (BLK_SEGS consecutive segments of one tile share a code).
+struct BlkInfo {
+    uint32_t seg0, nseg;                 // k_seg_map
+    uint32_t nbytes, data_bits;          // k_huff: block bytes; data bits (EOB included)
+    uint32_t off;                        // k_seg_sizes: byte offset in the tile's zlib payload
+    uint32_t fin;                        // k_huff: the tile's final block (BFINAL)
     uint32_t pad[2];
 };
 

@@ -5,12 +5,28 @@
 
 namespace pbx {
 
-// 512 threads (8 waves), 16 KiB segments with at most PBX_WIN look-back bytes (the longest
-// candidate distance is one row; overridable for experiments only).
+// PBX_NT = 512 threads (8 waves) per segment of up to PBX_SEG = 16 KiB, with at most
+// PBX_WIN look-back bytes (the longest candidate distance is one row); PBX_BLK consecutive
+// segments of a tile form one deflate block with one Huffman code.  Overridable for
+// experiments only.
 #ifndef PBX_WIN
 #define PBX_WIN 4096
 #endif
-using DeflateMainCfg = DeflateCfg<512, 16384, PBX_WIN>;
+#ifndef PBX_NT
+#define PBX_NT 512
+#endif
+#ifndef PBX_SEG
+#define PBX_SEG 16384
+#endif
+#ifndef PBX_BLK
+#define PBX_BLK 2
+#endif
+using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
+constexpr uint32_t BLK_SEGS = PBX_BLK;
+static_assert(BLK_SEGS >= 1 && BLK_SEGS * PBX_SEG <= 65535, "a stored block holds <= 65535 bytes");
+
+// Huffman blocks of a tile of nseg segments.
+PBX_HD uint32_t tile_blocks(uint32_t nseg) { return (nseg + BLK_SEGS - 1) / BLK_SEGS; }
 
 // Per-segment HBM records between the deflate kernels (32-bit words).
 constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram

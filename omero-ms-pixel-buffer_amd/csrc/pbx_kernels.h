@@ -39,7 +39,9 @@ struct DeflateLaunch {
     SegInfo* info;          // [nseg]
     uint32_t* hist;         // [nseg * HIST_WORDS]
     uint32_t* mrec;         // [nseg * MREC_WORDS]
-    uint32_t* codes;        // [nseg * CODE_WORDS]
+    uint32_t* codes;        // [nblk * CODE_WORDS]
+    BlkInfo* blk;           // [nblk] Huffman blocks
+    uint32_t nblk;
     uint64_t* sizes;        // [ntiles] container bytes
     uint64_t* offs;         // [ntiles + 1] exclusive scan of sizes (offs[ntiles] = total)
     uint8_t* out;           // compacted containers
@@ -50,8 +52,8 @@ struct DeflateLaunch {
 // ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr);
 size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
-// k_huff alone (test hook): info[].sl / .last must be set.
-hipError_t launch_huffman(hipStream_t st, uint32_t nseg, SegInfo* info, const uint32_t* hist,
-                          uint32_t* codes);
+// k_huff alone (test hook): blk[].seg0 / .nseg and info[].sl / .last must be set.
+hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* info,
+                          const uint32_t* hist, uint32_t* codes);
 
 }  // namespace pbx

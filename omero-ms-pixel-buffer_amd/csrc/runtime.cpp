@@ -166,7 +166,7 @@ struct pbx_batch {
     std::vector<int32_t> status, w, h;
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
-    uint32_t ext_blocks = 0, nseg = 0, filt_blocks = 0;
+    uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
     uint32_t nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;  // dt[0..nrows_tiles): k_rows tiles
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
@@ -174,7 +174,7 @@ struct pbx_batch {
     void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_stream = nullptr,
          *d_info = nullptr, *d_hist = nullptr, *d_mrec = nullptr, *d_codes = nullptr,
          *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr,
-         *d_segmap = nullptr;
+         *d_segmap = nullptr, *d_blk = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
@@ -229,7 +229,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
     void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
                      &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps,
-                     &b->d_segmap};
+                     &b->d_segmap, &b->d_blk};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -701,6 +701,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         deflate_split(d.stream_len, d.seg_count, d.seg_len);
         d.seg_first = b->nseg;
         b->nseg += d.seg_count;
+        d.hblk_first = b->nblk;
+        b->nblk += tile_blocks(d.seg_count);
         d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
         b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
         if (k < b->nrows_tiles) {
@@ -739,7 +741,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
         !dget(b->d_stream, b->stream_cap) || !dget(b->d_info, ns * sizeof(SegInfo)) ||
         !dget(b->d_hist, ns * HIST_WORDS * 4) || !dget(b->d_mrec, ns * MREC_WORDS * 4) ||
-        !dget(b->d_codes, ns * CODE_WORDS * 4) ||
+        !dget(b->d_codes, (size_t)b->nblk * CODE_WORDS * 4) || !dget(b->d_blk, b->nblk * sizeof(BlkInfo)) ||
         !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
         !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap) ||
         !dget(b->d_segmap, ns * sizeof(uint32_t)))
@@ -777,6 +779,8 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.out = (uint8_t*)b->d_png;
     a.stamps = prof ? (uint64_t*)b->d_stamps : nullptr;
     a.seg_tile = (uint32_t*)b->d_segmap;
+    a.blk = (BlkInfo*)b->d_blk;
+    a.nblk = b->nblk;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4));
@@ -965,14 +969,20 @@ int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     std::lock_guard<std::mutex> g(ctx->run_mu);
     std::vector<SegInfo> si(nseg);
+    std::vector<BlkInfo> bl(nseg);
     memset(si.data(), 0, nseg * sizeof(SegInfo));
-    for (uint32_t k = 0; k < nseg; k++) {
+    memset(bl.data(), 0, nseg * sizeof(BlkInfo));
+    for (uint32_t k = 0; k < nseg; k++) {  // one segment per block
         si[k].sl = sl_last[2 * k];
         si[k].last = sl_last[2 * k + 1];
+        si[k].flags = SF_FIRST | SF_LAST;
+        bl[k].seg0 = k;
+        bl[k].nseg = 1;
     }
     hipError_t err = hipSuccess;
     void* d_info = ctx->dpool.get(nseg * sizeof(SegInfo), &err);
-    void* d_hist = d_info ? ctx->dpool.get((size_t)nseg * HIST_WORDS * 4, &err) : nullptr;
+    void* d_blk = d_info ? ctx->dpool.get(nseg * sizeof(BlkInfo), &err) : nullptr;
+    void* d_hist = d_blk ? ctx->dpool.get((size_t)nseg * HIST_WORDS * 4, &err) : nullptr;
     void* d_codes = d_hist ? ctx->dpool.get((size_t)nseg * CODE_WORDS * 4, &err) : nullptr;
     int rc = PBX_OK;
     if (!d_codes) {
@@ -980,22 +990,24 @@ int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last
     } else {
         rc = [&]() -> int {
             HIP_TRY(hipMemcpy(d_info, si.data(), nseg * sizeof(SegInfo), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d_blk, bl.data(), nseg * sizeof(BlkInfo), hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(d_hist, hist, (size_t)nseg * HIST_WORDS * 4, hipMemcpyHostToDevice));
-            HIP_TRY(launch_huffman(ctx->stream, nseg, (SegInfo*)d_info, (const uint32_t*)d_hist,
-                                   (uint32_t*)d_codes));
+            HIP_TRY(launch_huffman(ctx->stream, nseg, (BlkInfo*)d_blk, (SegInfo*)d_info,
+                                   (const uint32_t*)d_hist, (uint32_t*)d_codes));
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             HIP_TRY(hipMemcpy(codes, d_codes, (size_t)nseg * CODE_WORDS * 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(si.data(), d_info, nseg * sizeof(SegInfo), hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(bl.data(), d_blk, nseg * sizeof(BlkInfo), hipMemcpyDeviceToHost));
             return PBX_OK;
         }();
     }
-    for (void* p : {d_info, d_hist, d_codes}) if (p) ctx->dpool.put(p);
+    for (void* p : {d_info, d_blk, d_hist, d_codes}) if (p) ctx->dpool.put(p);
     if (rc) return rc;
     for (uint32_t k = 0; k < nseg; k++) {
         info[4 * k] = si[k].btype;
         info[4 * k + 1] = si[k].hdr_bits;
-        info[4 * k + 2] = si[k].data_bits;
-        info[4 * k + 3] = si[k].nbytes;
+        info[4 * k + 2] = bl[k].data_bits;
+        info[4 * k + 3] = bl[k].nbytes;
     }
     return PBX_OK;
 }

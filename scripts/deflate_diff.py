@@ -62,7 +62,7 @@ for (w, h, g) in shapes:
         if not (gh[k] == eh[k]).all():
             d = np.nonzero(gh[k] != eh[k])[0]
             print(w, h, g, "seg", k, "HIST diff at", d[:8].tolist(), "gpu", gh[k][d[:8]].tolist(), "emu", eh[k][d[:8]].tolist())
-        nw = 8
+        nw = _emu.lib().pbxemu_threads() // 64
         if not (gm[k][:nw] == em[k][:nw]).all():
             print(w, h, g, "seg", k, "match counts gpu", gm[k][:nw].tolist(), "emu", em[k][:nw].tolist())
             for wv in range(nw):

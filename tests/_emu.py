@@ -23,6 +23,8 @@ def lib():
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(SegOut)]
         L.pbxemu_nsegs.restype = ctypes.c_uint32
         L.pbxemu_nsegs.argtypes = [ctypes.c_uint64]
+        L.pbxemu_nblocks.restype = ctypes.c_uint32
+        L.pbxemu_nblocks.argtypes = [ctypes.c_uint64]
         L.pbxemu_huffman.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_void_p]
         L.pbxemu_lz77.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
@@ -36,9 +38,10 @@ def lib():
 
 
 def deflate(data: bytes, rowlen: int):
-    """zlib stream exactly as the GPU pipeline produces it for one tile stream."""
+    """zlib stream exactly as the GPU pipeline produces it for one tile stream, and the
+    per-block results (SegOut per deflate block)."""
     data = bytes(data)
-    n = lib().pbxemu_nsegs(len(data))
+    n = lib().pbxemu_nblocks(len(data))
     segs = (SegOut * n)()
     out = ctypes.create_string_buffer(len(data) + 1024 + 16 * n)
     ol = ctypes.c_uint64()

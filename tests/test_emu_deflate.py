@@ -78,7 +78,7 @@ def test_lz77_records_cover_the_segment(kind):
     hist, mrec = _emu.lz77(s, rowlen)
     n = _emu.lib().pbxemu_nsegs(len(s))
     seg = (-(-len(s) // n) + 15) // 16 * 16
-    nw, mw = 8, 256
+    nw, mw = _emu.lib().pbxemu_threads() // 64, 256
     for k in range(n):
         sl = min(seg, len(s) - k * seg)
         lits = int(hist[k][:256].sum())

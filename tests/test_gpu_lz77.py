@@ -51,9 +51,9 @@ def test_gpu_lz77_matches_emulator(service, case):
     assert gh.shape == eh.shape
     for k in range(nseg):
         assert (gh[k] == eh[k]).all(), (name, k, np.nonzero(gh[k] != eh[k])[0][:8])
-        nw = 8
+        nw = L.pbxemu_threads() // 64
         assert (gm[k][:nw] == em[k][:nw]).all(), (name, k)
         for wv in range(nw):
             n = int(em[k][wv])
-            for off in (nw + wv * 256, nw + 8 * 256 + wv * 256):
+            for off in (nw + wv * 256, nw + nw * 256 + wv * 256):
                 assert (gm[k][off:off + n] == em[k][off:off + n]).all(), (name, k, wv)
