@@ -158,6 +158,7 @@ typedef struct pbx_batch_stats {
      * encode, all segments), assemble (container framing), total; then the deflate parts */
     double ms_extract, ms_filter, ms_deflate, ms_assemble, ms_total;
     double ms_lz77, ms_huff, ms_encode;
+    uint64_t blocks;         /* deflate blocks (segments sharing one Huffman code) */
 } pbx_batch_stats;
 int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* out);
 

@@ -377,14 +377,20 @@ PBX_HD void ph_huff_init(uint32_t tid, SM& S) {
     for (uint32_t t = tid; t < 288; t += C::HT) S.lcode[t] = 0;
     if (tid < 32) { S.dcode[tid] = 0; S.hblc[tid >> 4][tid & 15] = 0; S.dbm[tid & 15] = 0; }
     for (uint32_t t = tid; t < 16 * 9; t += C::HT) S.lbm[t] = 0;
-    for (uint32_t t = tid; t < (uint32_t)C::HDRW; t += C::HT) S.hdrw[t] = 0;
     if (tid < 2) S.hover[tid] = 0;
-    if (tid < 10) S.rbm[tid] = 0;
-    if (tid < 19) S.hw.clfreq[tid] = 0;
     if (tid == 0) {
         S.misc[M_NL] = 0; S.misc[M_ND] = 0; S.misc[M_DYNBITS] = 0; S.misc[M_FIXBITS] = 0;
         S.misc[M_HLIT] = 257; S.misc[M_HDIST] = 1;
     }
+}
+
+// State of the code-length / header phases, initialised once the code lengths exist (on
+// the device it shares LDS with the tree-building scratch, dead by then).
+template <class C, class SM>
+PBX_HD void ph_rle_init(uint32_t tid, SM& S) {
+    for (uint32_t t = tid; t < (uint32_t)C::HDRW; t += C::HT) S.hdrw[t] = 0;
+    if (tid < 10) S.rbm[tid] = 0;
+    if (tid < 19) S.hw.clfreq[tid] = 0;
 }
 
 template <class C, class Ops, class SM>
@@ -425,7 +431,7 @@ PBX_HD void ph_parents(uint32_t tid, SM& S) {
         tree_slot(i, T, s);
         const uint32_t n = tree_n(S.misc, T);
         if (s + 1 >= n) continue;
-        HuffScratch& H = S.hs;
+        auto& H = S.hs;
         const uint32_t r = H.rec[T][s];
         const uint32_t li0 = r & 0x3FF, qi0 = (r >> 10) & 0x3FF, cnt = r >> 20;
         for (uint32_t j = li0; j < li0 + cnt; j++) H.leafpar[T][j] = s;
@@ -442,7 +448,7 @@ PBX_HD void ph_jump(uint32_t tid, SM& S, int r) {
         tree_slot(i, T, k);
         const uint32_t n = tree_n(S.misc, T);
         if (k + 1 >= n) continue;
-        HuffScratch& H = S.hs;
+        auto& H = S.hs;
         const uint16_t* sd = (r & 1) ? H.dB[T] : H.dA[T];
         const uint16_t* sa = (r & 1) ? H.aB[T] : H.aA[T];
         uint16_t* dd = (r & 1) ? H.dA[T] : H.dB[T];
@@ -460,7 +466,7 @@ PBX_HD void ph_leafdepth(uint32_t tid, SM& S) {
         uint32_t T, j;
         tree_slot(i, T, j);
         if (j >= tree_n(S.misc, T)) continue;
-        HuffScratch& H = S.hs;
+        auto& H = S.hs;
         uint32_t d = H.dB[T][H.leafpar[T][j]] + 1;
         if (d > 15) { d = 15; Ops::add(&S.hover[T], 1u); }
         Ops::add(&S.hblc[T][d], 1u);

@@ -73,6 +73,7 @@ void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_leafdepth<C, EmuOps>(t, S);
     for (int t = 0; t < C::HT; t++) ph_fixblc<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_assign<C, EmuOps>(t, S);
+    for (int t = 0; t < C::HT; t++) ph_rle_init<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_mark<C, EmuOps>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_count<C>(t, S);
     S.misc[M_NRLE] = scan_excl_add(S.hs.rcnt, SORTN);

@@ -41,20 +41,42 @@ struct LzSmem {
     uint32_t red[3 * C::NW];
 };
 
+// The tree-building scratch (keys, merge records, parents, depths, merge rounds) is dead
+// once the code lengths exist; the code-length RLE, the code-length code and the header
+// bits then reuse its bytes, except the RLE counts (rcnt), which already alias the depth
+// arrays inside it.  13.8 KB: 11 one-wave workgroups per CU.
+struct HuffScratchDev {
+    uint32_t skey[SORTN];
+    uint32_t rec[2][288];       // step s: li0 | qi0 << 10 | cnt << 20
+    uint16_t leafpar[2][288];
+    union {
+        struct {
+            uint16_t aA[2][288], dB[2][288], aB[2][288];
+            uint16_t rst[2][290];  // first internal node of every merge round (+ the end)
+        };
+        uint32_t rcnt[SORTN];   // RLE: symbols emitted by the run starting at i -> offsets
+    };
+};
+
 template <class C>
 struct HuffSmem {
     uint32_t lfreq[288], dfreq[32];
-    HuffScratch hs;
     uint32_t lcode[288], dcode[32];
     uint32_t hblc[2][16], hover[2], hstart[2][16], hnext[2][16];
     uint32_t lbm[16 * 9], dbm[16];
-    HuffWork hw;
-    uint32_t rle[320], rboff[SORTN], rbm[10];
-    uint32_t hdrw[C::HDRW];
     uint32_t misc[M_NMISC];
-    uint16_t rst[2][290];  // first internal node of every merge round (+ the end)
     uint32_t nrounds[2];
+    union {
+        HuffScratchDev hs;
+        struct {  // from ph_rle_init on (below hs.rcnt)
+            HuffWork hw;
+            uint32_t rle[320], rboff[SORTN], rbm[10];
+            uint32_t hdrw[C::HDRW];
+        };
+    };
 };
+static_assert(offsetof(HuffScratchDev, rcnt) >= sizeof(HuffWork) + 4 * (320 + SORTN + 10 + DeflateMainCfg::HDRW),
+              "the header-phase arrays stay below the RLE counts");
 
 constexpr int CRC_NIB_LEVELS_ = 7;
 template <class C>
@@ -470,7 +492,7 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the jump rounds)
     uint16_t* M = &S.hs.aB[0][0];     // merged prefix: leaf index | 0x8000, or internal index
     uint32_t* rq = S.hs.rec[T];
-    uint16_t* rs = S.rst[T];
+    uint16_t* rs = S.hs.rst[T];
     if (n < 2) {
         if (lane == 0) S.nrounds[T] = 0;
         return;
@@ -551,6 +573,23 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     }
 }
 
+// Parents from the merge records (ph_parents without the pointer-jumping depths, which the
+// device does not use): leafpar of every leaf, aA of every internal node.
+template <class SM>
+__device__ void parents_wave(SM& S, uint32_t tid) {
+    for (uint32_t i = tid; i < 320; i += 64) {
+        uint32_t T, s;
+        tree_slot(i, T, s);
+        const uint32_t n = tree_n(S.misc, T);
+        if (s + 1 >= n) continue;
+        const uint32_t r = S.hs.rec[T][s];
+        const uint32_t li0 = r & 0x3FF, qi0 = (r >> 10) & 0x3FF, cnt = r >> 20;
+        for (uint32_t j = li0; j < li0 + cnt; j++) S.hs.leafpar[T][j] = (uint16_t)s;
+        for (uint32_t k = qi0; k < qi0 + 2 - cnt; k++) S.hs.aA[T][k] = (uint16_t)s;
+        if (s + 2 == n) S.hs.aA[T][s] = (uint16_t)s;  // the root
+    }
+}
+
 // Depth of every internal node, root first: a node's parent is created in a later merge
 // round, so the rounds taken in reverse order each resolve in one parallel step (instead
 // of pointer jumping).  Result in dB, as ph_jump leaves it.
@@ -560,11 +599,11 @@ __device__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
     if (nr == 0) return;
     uint16_t* dd = S.hs.dB[T];
     const uint16_t* par = S.hs.aA[T];
-    const uint32_t root = S.rst[T][nr] - 1u;  // the last round creates only the root
+    const uint32_t root = S.hs.rst[T][nr] - 1u;  // the last round creates only the root
     if (lane == 0) dd[root] = 0;
     __syncthreads();
     for (int32_t r = (int32_t)nr - 2; r >= 0; r--) {
-        const uint32_t k0 = S.rst[T][r], k1 = S.rst[T][r + 1];
+        const uint32_t k0 = S.hs.rst[T][r], k1 = S.hs.rst[T][r + 1];
         for (uint32_t k = k0 + lane; k < k1; k += 64) dd[k] = (uint16_t)(dd[par[k]] + 1);
         __syncthreads();
     }
@@ -768,7 +807,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     huff_rounds_wave(S, 1, tid);
     __syncthreads();
     stamp();
-    ph_parents<C>(tid, S);
+    parents_wave(S, tid);
     __syncthreads();
     stamp();
     depths_wave(S, 0, tid);
@@ -781,6 +820,8 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     __syncthreads();
     stamp();
     assign_wave(S, tid);
+    __syncthreads();
+    ph_rle_init<C>(tid, S);
     __syncthreads();
     stamp();
     ph_rle_mark<C, DevOps>(tid, S);
@@ -1041,24 +1082,30 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
             cb[k] = keep >= 4 ? cb[k] : keep <= 0 ? 0u : cb[k] & ((1u << (8 * keep)) - 1u);
         }
     }
-    const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
-    if (tid < (uint32_t)C::NW) S.w_nm[tid] = mg[tid];
+    // this wave's match list (a thread's tokens only depend on its own wave's matches)
+    {
+        const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
+        const uint32_t nmw = __builtin_amdgcn_readfirstlane(mg[w]);
+        if (lane == 0) S.w_nm[w] = nmw;
+        for (uint32_t m = lane; m < nmw; m += 64) {
+            S.mpos[w * C::MAXMW + m] = mg[C::NW + w * C::MAXMW + m];
+            S.mdist[w * C::MAXMW + m] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + w * C::MAXMW + m];
+        }
+    }
     const uint32_t* cg = codes + (size_t)gi.blk * CODE_WORDS;
     for (uint32_t i = tid; i < 320; i += C::NT) {
         if (i < 288) S.lcode[i] = slot_from_code(cg[i]); else S.dcode[i - 288] = slot_from_code(cg[i]);
     }
     if (tid == 0) S.lcode[SLOT_NONE] = 0;
-    for (uint32_t k = tid; k < (uint32_t)C::OUTW; k += C::NT)
-        S.out[k] = (first && gi.btype != 0 && k < (uint32_t)C::HDRW) ? cg[320 + k] : 0u;
+    {
+        const bool hdr = first && gi.btype != 0;
+        uint4* o4 = (uint4*)S.out;
+        for (uint32_t k = tid; k < (uint32_t)C::OUTW / 4; k += C::NT)
+            o4[k] = (hdr && 4 * k < (uint32_t)C::HDRW) ? *(const uint4*)(cg + 320 + 4 * k) : make_uint4(0, 0, 0, 0);
+    }
     for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
     for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
     __syncthreads();
-    for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
-        if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
-            S.mpos[i] = mg[C::NW + i];
-            S.mdist[i] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + i];
-        }
-    }
     if (gi.btype == 0) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; bytes
         uint8_t* ob = (uint8_t*)S.out;
         const uint32_t cs = tid * C::CH, o = first ? 5u : 0u;

@@ -832,6 +832,7 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
     s->in_bytes = b->in_bytes;
     s->stream_bytes = b->stream_bytes;
     s->segments = b->nseg;
+    s->blocks = b->nblk;
     if (b->launched) {
         if (ensure_device(ctx)) return PBX_E_INTERNAL;
         HIP_TRY(hipEventSynchronize(b->ev[8]));

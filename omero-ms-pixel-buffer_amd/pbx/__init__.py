@@ -78,7 +78,7 @@ class PbxBatchStats(ctypes.Structure):
                  "stream_bytes", "out_bytes", "deflate_out_bytes", "segments")] + \
                [(n, ctypes.c_double) for n in
                 ("ms_extract", "ms_filter", "ms_deflate", "ms_assemble", "ms_total",
-                  "ms_lz77", "ms_huff", "ms_encode")]
+                  "ms_lz77", "ms_huff", "ms_encode")] + [("blocks", ctypes.c_uint64)]
 
 
 # Every symbol include/pbx.h declares (tests check the library exports all of them).
