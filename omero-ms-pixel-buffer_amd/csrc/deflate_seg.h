@@ -56,8 +56,8 @@ struct DeflateCfg {
     static constexpr int SUB = SEG / NW;  // positions parsed by one wave
     static constexpr int MAXMW = 256;     // matches kept per wave (then literals only)
     static constexpr int CAP = PBX_CAP;   // match length found by the masks before the wave extends it
-    static constexpr int CRCC = 64;       // CRC chunk bytes per thread
-    static constexpr int LOG2_CRCC = 6;
+    static constexpr int CRCC = 32;       // CRC chunk bytes per thread (thread 0: the rest too)
+    static constexpr int LOG2_CRCC = 5;
     static constexpr int BUFW = (WIN + SEG + 32) / 4;
     static constexpr int SEGW = (SEG + 16) / 4;
     static constexpr int OUTW = (SEG + 64) / 4;
@@ -69,7 +69,6 @@ struct DeflateCfg {
     static_assert(SUB <= 65536 && SUB % CH == 0, "sub-segments hold whole thread chunks");
     static_assert(WIN <= 32768 && SEG <= 32768, "distances <= one row <= 32768; 16-bit positions");
     static_assert((1 << LOGNT) == NT, "NT must be a power of two in 128..1024");
-    static_assert(NT * CRCC >= SEG + 64, "CRC chunks cover the output");
     static_assert(CH % 4 == 0 && WIN % 16 == 0, "Adler chunks are whole aligned words");
     static_assert(HDRW * 32 >= 17 + 57 + 316 * 14, "header buffer holds any dynamic header");
 };
@@ -951,15 +950,16 @@ PBX_HD uint32_t out_byte(const SM& S, uint32_t j) {
 // Raw CRC (register init 0, no final xor) of this thread's right-aligned CRCC-byte chunk of
 // the output left-padded with zero bytes to a multiple of 4 (leading zero bytes leave a raw
 // CRC unchanged): thread t covers [V - (NT-t)*CRCC, V - (NT-1-t)*CRCC) of the padded V bytes,
-// 4 bytes per slicing-by-4 step.  Short or empty chunks count as full ones, so combine
-// level k shifts by the constant x^(8*CRCC*2^k).
+// 4 bytes per slicing-by-4 step; thread 0 also takes everything before its chunk.  Short or
+// empty chunks count as full ones and a chunk's operator only depends on the chunks after
+// it, so combine level k shifts by the constant x^(8*CRCC*2^k).
 template <class C, class SM>
 PBX_HD uint32_t ph_crc(uint32_t tid, const SM& S) {
     const uint32_t nbytes = S.misc[M_NBYTES];
     const uint32_t pad = (4u - (nbytes & 3u)) & 3u, nv = (nbytes + pad) >> 2;
     const int64_t hi = (int64_t)nv - (int64_t)(C::NT - 1 - tid) * (C::CRCC / 4);
     int64_t lo = hi - C::CRCC / 4;
-    if (lo < 0) lo = 0;
+    if (lo < 0 || tid == 0) lo = 0;
     uint32_t c = 0;
     for (int64_t k = lo; k < hi; k++) {
         const uint32_t w1 = S.out[k];

@@ -418,6 +418,8 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
         SegInfo& g = info[seg];
         g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
         g.adler_s1 = a1; g.adler_s2 = a2;
+        const uint64_t src = d.out_off + sp.base + sp.wl;
+        g.src_lo = (uint32_t)src; g.src_hi = (uint32_t)(src >> 32);
     }
     uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
     for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
@@ -908,7 +910,9 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
         seg_tile[f + k] = i;
         const uint32_t j = k / BLK_SEGS, r = k % BLK_SEGS;
         info[f + k].blk = hb + j;
-        info[f + k].flags = (r == 0 ? SF_FIRST : 0u) | (r + 1 == BLK_SEGS || k + 1 == n ? SF_LAST : 0u);
+        info[f + k].tile = i;
+        info[f + k].flags = (r == 0 ? SF_FIRST : 0u) | (r + 1 == BLK_SEGS || k + 1 == n ? SF_LAST : 0u) |
+                            ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
         if (r == 0) {
             blk[hb + j].seg0 = f + k;
             blk[hb + j].nseg = n - k < BLK_SEGS ? n - k : BLK_SEGS;
@@ -1029,6 +1033,17 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
     }
 }
 
+// Timing experiments only (scripts/variants.sh): skip parts of k_encode (wrong output).
+#ifndef PBX_ENC_SKIP_WRITE
+#define PBX_ENC_SKIP_WRITE 0
+#endif
+#ifndef PBX_ENC_SKIP_CRC
+#define PBX_ENC_SKIP_CRC 0
+#endif
+#ifndef PBX_ENC_SKIP_STORE
+#define PBX_ENC_SKIP_STORE 0
+#endif
+
 // One segment's part of its block: the header (first segment), its tokens, and the end of
 // block (+ the empty stored block of a non-final block; last segment) at the bits
 // [bit0, bit1) k_huff assigned.  The bytes it owns entirely go straight to the compacted
@@ -1055,13 +1070,16 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         nst++;
     };
     stamp();
-    const uint32_t ti = seg_tile[seg];
-    const TileDesc d = dt[ti];
-    SegParams sp = seg_params(d, seg - d.seg_first);
-    sp.base += sp.wl;  // the encoder holds the segment only
-    sp.wl = 0;
-    const SegInfo gi = info[seg];
+    const SegInfo gi = info[seg];  // everything the encoder needs about its segment / tile
     const BlkInfo bi = blk[gi.blk];
+    const uint32_t ti = gi.tile;
+    SegParams sp;  // the encoder holds the segment only (no window)
+    sp.base = 0;
+    sp.wl = 0;
+    sp.sl = gi.sl;
+    sp.last = gi.last;
+    sp.rowlen = gi.rowlen;
+    const uint8_t* seg_src = stream + (((uint64_t)gi.src_hi << 32) | gi.src_lo);
     const bool first = (gi.flags & SF_FIRST) != 0, lastb = (gi.flags & SF_LAST) != 0;
     const bool final_seg = sp.last != 0;          // the tile's stream ends in this segment
     const uint32_t byte0 = gi.bit0 >> 3, lb = gi.bit0 & 7u;  // out[] byte 0 = block byte byte0
@@ -1070,7 +1088,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     uint32_t cb[C::CH / 4];
     {
         const uint32_t cs = tid * C::CH;
-        const uint8_t* src = stream + d.out_off + sp.base + cs;
+        const uint8_t* src = seg_src + cs;
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
         if (cs < sp.sl) q0 = *(const uint4*)src;
         if (cs + 16 < sp.sl) q1 = *(const uint4*)(src + 16);
@@ -1131,7 +1149,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     __syncthreads();
     stamp();
     const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
-    if (gi.btype != 0) {
+    if (gi.btype != 0 && !PBX_ENC_SKIP_WRITE) {
         const uint32_t tb = lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
         RunWriter<DevOps> bw(S.out, tb + S.t_a[tid]);
 #pragma unroll
@@ -1167,20 +1185,23 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     stamp();
     // CRC-32 of out[0, o1): raw CRC of right-aligned 64-byte chunks, combined per wave by
     // shuffles with the constant operators x^(8*64*2^k), then across the waves
-    uint32_t c = ph_crc<C>(tid, S);
+    uint32_t c = 0;
+    if (!PBX_ENC_SKIP_CRC) {
+        c = ph_crc<C>(tid, S);
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-        const uint32_t r = __shfl_down(c, 1 << k, 64);
-        c = crc_mul_nib(S, k, c) ^ r;
+        for (int k = 0; k < 6; k++) {
+            const uint32_t r = __shfl_down(c, 1 << k, 64);
+            c = crc_mul_nib(S, k, c) ^ r;
+        }
     }
     if (lane == 0) S.red[w] = c;
     // owned bytes to their final place: unaligned head and tail bytes, aligned words between
     const uint32_t nbytes = o1 - o0;
-    const uint32_t zoff = (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+    const uint32_t zoff = (gi.flags & SF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
     uint8_t* dst = out + offs[ti] + zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
-    const uint32_t nwords = (nbytes - head) >> 2;
+    const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
     if (tid < head) dst[tid] = (uint8_t)out_byte(S, o0 + tid);
     for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, o0 + head + 4 * k);
     for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, o0 + j);

@@ -87,8 +87,11 @@ struct SegInfo {
     uint32_t blk, flags;                 // k_seg_map: block index; SF_FIRST / SF_LAST in block
     uint32_t part;                       // k_encode: head | tail << 8 | SP_HEAD | SP_TAIL
     uint32_t bitsum;                     // k_encode: token bits (diagnostics)
+    uint32_t tile;                       // k_seg_map: the segment's tile
+    uint32_t src_lo, src_hi;             // k_lz77: stream-buffer offset of the segment's first byte
+    uint32_t pad_;
 };
-constexpr uint32_t SF_FIRST = 1, SF_LAST = 2;
+constexpr uint32_t SF_FIRST = 1, SF_LAST = 2, SF_TIFF = 4;
 constexpr uint32_t SP_HEAD = 1u << 16, SP_TAIL = 1u << 17;
 
 // Per Huffman block (BLK_SEGS consecutive segments of one tile share a code).
