@@ -971,6 +971,20 @@ __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
     return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
 }
 
+// Timing experiments only (scripts/variants.sh): skip parts of k_encode (wrong output).
+#ifndef PBX_ENC_SKIP_WRITE
+#define PBX_ENC_SKIP_WRITE 0
+#endif
+#ifndef PBX_ENC_SKIP_PATCH
+#define PBX_ENC_SKIP_PATCH 0
+#endif
+#ifndef PBX_ENC_SKIP_CRC
+#define PBX_ENC_SKIP_CRC 0
+#endif
+#ifndef PBX_ENC_SKIP_STORE
+#define PBX_ENC_SKIP_STORE 0
+#endif
+
 // A token's bits packed in one register: value (<= 20 bits) | nbits << 27.  The LDS code
 // tables hold literal/length and distance codes in this form (slot 288 = 0 bits).
 __device__ __forceinline__ uint32_t slot_from_code(uint32_t c) { return (c & 0xFFFFu) | ((c >> 16) << 27); }
@@ -1010,14 +1024,33 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
         cover(mp[m1] & 0xFFFFu, (mp[m1] & 0xFFFFu) + (mp[m1] >> 16) + 3);
         m1++;
     }
-#pragma unroll
-    for (int i = 0; i < C::CH; i++) {
-        const uint32_t b = (cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-        slot[i] = S.lcode[((covered >> i) & 1u) ? SLOT_NONE : b];
+    // the first match starting in the chunk goes in with the literals, branch-free; any
+    // further ones (several short matches in 32 bytes) are patched in after
+    uint32_t i0 = 0xFFu, A = 0, B = 0, Cx = 0;
+    if (lo < m1) {
+        const uint32_t len = (mp[lo] >> 16) + 3, dist = (uint32_t)md[lo] + 1;
+        i0 = (mp[lo] & 0xFFFFu) - cs;
+        uint32_t sy, e, v;
+        len_code(len, sy, e, v);
+        const uint32_t lc = S.lcode[sy];
+        A = lc + (v << (lc >> 27)) + (e << 27);
+        dist_code(dist, sy, e, v);
+        B = S.dcode[sy];
+        Cx = v | (e << 27);
     }
-    slot[C::CH] = 0;
-    slot[C::CH + 1] = 0;
-    for (uint32_t m = lo; m < m1; m++) {
+#pragma unroll
+    for (int i = 0; i < C::CH + 2; i++) {
+        uint32_t lit = 0;
+        if (i < C::CH) {
+            const uint32_t b = (cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+            lit = S.lcode[((covered >> i) & 1u) ? SLOT_NONE : b];
+        }
+        // masks, not ?: chains: the compiler turns those into branches around the lookup
+        const uint32_t di = (uint32_t)i - i0;
+        const uint32_t k0 = 0u - (uint32_t)(di == 0), k1 = 0u - (uint32_t)(di == 1), k2 = 0u - (uint32_t)(di == 2);
+        slot[i] = (lit & ~(k0 | k1 | k2)) | (A & k0) | (B & k1) | (Cx & k2);
+    }
+    for (uint32_t m = lo + 1; m < (PBX_ENC_SKIP_PATCH ? lo : m1); m++) {
         const uint32_t i = (mp[m] & 0xFFFFu) - cs, len = (mp[m] >> 16) + 3, dist = (uint32_t)md[m] + 1;
         uint32_t sy, e, v;
         len_code(len, sy, e, v);
@@ -1032,17 +1065,6 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
         }
     }
 }
-
-// Timing experiments only (scripts/variants.sh): skip parts of k_encode (wrong output).
-#ifndef PBX_ENC_SKIP_WRITE
-#define PBX_ENC_SKIP_WRITE 0
-#endif
-#ifndef PBX_ENC_SKIP_CRC
-#define PBX_ENC_SKIP_CRC 0
-#endif
-#ifndef PBX_ENC_SKIP_STORE
-#define PBX_ENC_SKIP_STORE 0
-#endif
 
 // One segment's part of its block: the header (first segment), its tokens, and the end of
 // block (+ the empty stored block of a non-final block; last segment) at the bits
