@@ -400,16 +400,16 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
             s2 = dot4_u8(v, e | ((e - 1) << 8) | ((e - 2) << 16) | ((e - 3) << 24), s2);
         }
         s2 -= (cs + (uint32_t)C::CH - ce) * s1;
-        s1 %= ADLER_BASE;
-        s2 %= ADLER_BASE;
     }
+    // Adler-32 partials: wave tree on raw sums (one wave covers <= 2048 bytes: s1 < 2^20,
+    // s2 < 2^30, no modular reduction needed), reduced once per wave
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // Adler-32 partials: wave tree
+    for (int off = 1; off < 64; off <<= 1) {
         const uint32_t r1 = __shfl_down(s1, off, 64), r2 = __shfl_down(s2, off, 64);
         const uint32_t rn = __shfl_down(n, off, 64);
-        if ((lane & (2 * off - 1)) == 0 && lane + off < 64) { adler_combine(s1, s2, r1, r2, rn); n += rn; }
+        if ((lane & (2 * off - 1)) == 0 && lane + off < 64) { s2 += rn * s1 + r2; s1 += r1; n += rn; }
     }
-    if (lane == 0) { S.red[3 * w] = s1; S.red[3 * w + 1] = s2; S.red[3 * w + 2] = n; }
+    if (lane == 0) { S.red[3 * w] = s1 % ADLER_BASE; S.red[3 * w + 1] = s2 % ADLER_BASE; S.red[3 * w + 2] = n; }
     __syncthreads();
     stamp();
     if (tid == 0) {
@@ -788,14 +788,28 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         nst++;
     };
     stamp();
-    for (uint32_t i = tid; i < HIST_WORDS; i += 64) {
+    // the segments' histograms, kept in registers for their bit counts at the end
+    uint32_t hreg[BLK_SEGS][5];
+#pragma unroll
+    for (uint32_t k = 0; k < BLK_SEGS; k++)
+#pragma unroll
+        for (int j = 0; j < 5; j++)
+            hreg[k][j] = k < nsg ? hist[(size_t)(seg0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const uint32_t i = tid + 64 * j;
         uint32_t v = 0;
-        for (uint32_t k = 0; k < nsg; k++) v += hist[(size_t)(seg0 + k) * HIST_WORDS + i];
+#pragma unroll
+        for (uint32_t k = 0; k < BLK_SEGS; k++) v += hreg[k][j];
         if (i == 256) v = 1;  // one end of block (every segment's histogram counted one)
         if (i < 288) S.lfreq[i] = v; else S.dfreq[i - 288] = v;
     }
-    uint32_t sl = 0;
-    for (uint32_t k = 0; k < nsg; k++) sl += info[seg0 + k].sl;
+    uint32_t sl = 0, sls[BLK_SEGS];
+#pragma unroll
+    for (uint32_t k = 0; k < BLK_SEGS; k++) {
+        sls[k] = k < nsg ? info[seg0 + k].sl : 0u;
+        sl += sls[k];
+    }
     const uint32_t last = info[seg0 + nsg - 1].last;
     ph_huff_init<C>(tid, S);
     __syncthreads();
@@ -863,16 +877,17 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     // [empty stored block unless the tile ends here]; a stored block is byte-aligned
     const uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
     uint32_t run = bt == 0 ? 40u : hdr;
-    for (uint32_t k = 0; k < nsg; k++) {
-        const uint32_t* hk = hist + (size_t)(seg0 + k) * HIST_WORDS;
+#pragma unroll
+    for (uint32_t k = 0; k < BLK_SEGS; k++) {
+        if (k >= nsg) break;
         uint32_t d = 0;
         if (bt == 0) {
-            d = 8 * info[seg0 + k].sl;
+            d = 8 * sls[k];
         } else {
-            for (uint32_t i = tid; i < 320; i += 64) {
-                if (i == 256 || (i >= 286 && i < 288) || i >= 318) continue;
-                const uint32_t f = hk[i];
-                if (!f) continue;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t i = tid + 64 * j, f = hreg[k][j];
+                if (i == 256 || (i >= 286 && i < 288) || i >= 318 || !f) continue;
                 const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i - 288]) >> 16;
                 const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i - 288);
                 d += f * (L + eb);
