@@ -327,7 +327,9 @@ PBX_HD void ph_hist(uint32_t tid, SM& S, const SegParams& sp, uint32_t& s1, uint
 //   ph_leafdepth / ph_fixblc / ph_assign   bit-length counts, overflow repair, lengths
 //   ph_rle_*    code-length run-length coding; ph_clen: the code-length code
 //   ph_choose   block type by exact size; ph_codes: canonical codes; ph_header: header bits
-constexpr uint32_t SORTN = 512;
+constexpr uint32_t SORTN = 512;  // sorting network width (the device sorts KEYN keys padded)
+constexpr uint32_t KEYN = 320;   // sort keys: 288 literal/length slots, then 32 distance slots
+constexpr uint32_t RLEN = 320;   // code-length RLE slots (HLIT + HDIST <= 316)
 constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
 
 struct HuffWork {  // the 19-symbol code-length code (one thread)
@@ -337,16 +339,13 @@ struct HuffWork {  // the 19-symbol code-length code (one thread)
     uint32_t cllen[19], clcode[19], clfreq[19], clsort[19];
 };
 
-// Node indices, depths and internal weights (<= SEG + 2) fit 16 bits.  The RLE counts
-// reuse the pointer-jumping arrays, which are dead by then.
+// Node indices, depths and internal weights (<= SEG + 2) fit 16 bits.  (The RLE counts,
+// rcnt[RLEN], are a member of the phases' state struct itself.)
 struct HuffScratch {
-    uint32_t skey[SORTN];
+    uint32_t skey[KEYN];
     uint32_t rec[2][288];       // step s: li0 | qi0 << 10 | cnt << 20
     uint16_t leafpar[2][288];
-    union {
-        struct { uint16_t dA[2][288], aA[2][288], dB[2][288], aB[2][288]; };
-        uint32_t rcnt[SORTN];   // RLE: symbols emitted by the run starting at i -> offsets
-    };
+    uint16_t dA[2][288], aA[2][288], dB[2][288], aB[2][288];
 };
 
 // Effective frequencies: every tree gets >= 2 used symbols (zlib's rule, so every decoder
@@ -394,7 +393,7 @@ PBX_HD void ph_rle_init(uint32_t tid, SM& S) {
 
 template <class C, class Ops, class SM>
 PBX_HD void ph_keys(uint32_t tid, SM& S) {
-    for (uint32_t t = tid; t < SORTN; t += C::HT) {
+    for (uint32_t t = tid; t < KEYN; t += C::HT) {
         uint32_t key = KEY_NONE;
         if (t < 286) {
             const uint32_t f = eff_lfreq(S.lfreq, t);
@@ -631,11 +630,11 @@ PBX_HD uint32_t rle_run_len(const SM& S, uint32_t i, uint32_t ntot) {
 template <class C, class SM>
 PBX_HD void ph_rle_count(uint32_t tid, SM& S) {
     const uint32_t ntot = S.misc[M_HLIT] + S.misc[M_HDIST];
-    for (uint32_t i = tid; i < SORTN; i += C::HT) {
+    for (uint32_t i = tid; i < RLEN; i += C::HT) {
         uint32_t cnt = 0;
         if (i < ntot && ((S.rbm[i >> 5] >> (i & 31)) & 1u))
             cnt = rle_nsyms(cl_len_at(S, i), rle_run_len(S, i, ntot));
-        S.hs.rcnt[i] = cnt;
+        S.rcnt[i] = cnt;
     }
 }
 
@@ -646,7 +645,7 @@ PBX_HD void ph_rle_emit(uint32_t tid, SM& S) {
     for (uint32_t i = tid; i < ntot; i += C::HT) {
         if (!((S.rbm[i >> 5] >> (i & 31)) & 1u)) continue;
         const uint32_t v = cl_len_at(S, i);
-        uint32_t run = rle_run_len(S, i, ntot), k = S.hs.rcnt[i];
+        uint32_t run = rle_run_len(S, i, ntot), k = S.rcnt[i];
         uint32_t* cf = S.hw.clfreq;
         if (v == 0) {
             while (run >= 11) {
@@ -698,10 +697,10 @@ PBX_HD void ph_clen(uint32_t tid, SM& S) {
     S.misc[M_HCLEN] = hclen;
 }
 
-// Bits of each RLE symbol (for the header offsets) into rboff[0..SORTN).
+// Bits of each RLE symbol (for the header offsets) into rboff[0..RLEN).
 template <class C, class SM>
 PBX_HD void ph_rle_bits(uint32_t tid, SM& S) {
-    for (uint32_t i = tid; i < SORTN; i += C::HT) {
+    for (uint32_t i = tid; i < RLEN; i += C::HT) {
         uint32_t b = 0;
         if (i < S.misc[M_NRLE]) {
             const uint32_t sym = S.rle[i] & 0xFF;

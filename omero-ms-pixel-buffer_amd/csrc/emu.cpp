@@ -41,7 +41,7 @@ struct Smem {
     uint32_t hblc[2][16], hover[2], hstart[2][16], hnext[2][16];
     uint32_t lbm[16 * 9], dbm[16];
     HuffWork hw;
-    uint32_t rle[320], rboff[SORTN], rbm[10];
+    uint32_t rle[320], rboff[RLEN], rbm[10], rcnt[RLEN];
     uint32_t hdrw[C::HDRW];
     uint32_t misc[M_NMISC];
     uint32_t out[C::OUTW];
@@ -59,7 +59,7 @@ uint32_t scan_excl_add(uint32_t* a, int n) {
 void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_huff_init<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_keys<C, EmuOps>(t, S);
-    std::sort(S.hs.skey, S.hs.skey + SORTN);
+    std::sort(S.hs.skey, S.hs.skey + KEYN);
     {
         std::vector<uint32_t> iw(SORTN);
         const uint32_t nl = S.misc[M_NL], nd = S.misc[M_ND];
@@ -76,11 +76,11 @@ void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_rle_init<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_mark<C, EmuOps>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_count<C>(t, S);
-    S.misc[M_NRLE] = scan_excl_add(S.hs.rcnt, SORTN);
+    S.misc[M_NRLE] = scan_excl_add(S.rcnt, RLEN);
     for (int t = 0; t < C::HT; t++) ph_rle_emit<C, EmuOps>(t, S);
     for (int t = 0; t < C::HT; t++) ph_clen<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_bits<C>(t, S);
-    S.misc[M_HDRBITS] = scan_excl_add(S.rboff, SORTN);
+    S.misc[M_HDRBITS] = scan_excl_add(S.rboff, RLEN);
     for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sl, last);
     for (int t = 0; t < C::HT; t++) ph_codes<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, last);

@@ -14,7 +14,7 @@
 //
 // LDS / ALU / latency-bound integer work; no MFMA.  Splitting the segment's work over three
 // kernels gives each its own occupancy: k_lz77 and k_encode hold ~46-50 KB of LDS
-// (3 workgroups per CU), k_huff ~22 KB per wave, so the serial Huffman merge of many
+// (4 workgroups per CU), k_huff 8.9 KB per wave, so the serial Huffman merge of many
 // segments overlaps on every CU.
 #include <hip/hip_runtime.h>
 
@@ -41,21 +41,26 @@ struct LzSmem {
     uint32_t red[3 * C::NW];
 };
 
+// Per-tree arrays of the literal/length tree (288 slots) and the distance tree (32 slots)
+// back to back: a[T] is tree T's part, as with a [2][288] array, at 320 slots instead of 576.
+template <class E, uint32_t N0, uint32_t N1>
+struct Split2 {
+    E v[N0 + N1];
+    __device__ E* operator[](uint32_t T) { return v + (T ? N0 : 0u); }
+    __device__ const E* operator[](uint32_t T) const { return v + (T ? N0 : 0u); }
+};
+
 // The tree-building scratch (keys, merge records, parents, depths, merge rounds) is dead
-// once the code lengths exist; the code-length RLE, the code-length code and the header
-// bits then reuse its bytes, except the RLE counts (rcnt), which already alias the depth
-// arrays inside it.  13.8 KB: 11 one-wave workgroups per CU.
+// once the code lengths exist; the code-length RLE, the code-length code, the header bits
+// and the RLE counts then reuse its bytes.  The merge rounds' merged prefix (<= 288
+// entries: the queue never holds more than the leaves) lives in leafpar, written only
+// after the rounds.  8.9 KB: 18 one-wave workgroups per CU.
 struct HuffScratchDev {
-    uint32_t skey[SORTN];
-    uint32_t rec[2][288];       // step s: li0 | qi0 << 10 | cnt << 20
-    uint16_t leafpar[2][288];
-    union {
-        struct {
-            uint16_t aA[2][288], dB[2][288], aB[2][288];
-            uint16_t rst[2][290];  // first internal node of every merge round (+ the end)
-        };
-        uint32_t rcnt[SORTN];   // RLE: symbols emitted by the run starting at i -> offsets
-    };
+    uint32_t skey[KEYN];
+    Split2<uint32_t, 288, 32> rec;      // step s: li0 | qi0 << 10 | cnt << 20
+    Split2<uint16_t, 288, 32> leafpar;  // (merge rounds: the merged prefix)
+    Split2<uint16_t, 288, 32> aA, dB;
+    Split2<uint16_t, 290, 34> rst;      // first internal node of every merge round (+ the end)
 };
 
 template <class C>
@@ -68,15 +73,14 @@ struct HuffSmem {
     uint32_t nrounds[2];
     union {
         HuffScratchDev hs;
-        struct {  // from ph_rle_init on (below hs.rcnt)
+        struct {  // from ph_rle_init on
             HuffWork hw;
-            uint32_t rle[320], rboff[SORTN], rbm[10];
+            uint32_t rle[320], rboff[RLEN], rbm[10];
             uint32_t hdrw[C::HDRW];
+            uint32_t rcnt[RLEN];
         };
     };
 };
-static_assert(offsetof(HuffScratchDev, rcnt) >= sizeof(HuffWork) + 4 * (320 + SORTN + 10 + DeflateMainCfg::HDRW),
-              "the header-phase arrays stay below the RLE counts");
 
 constexpr int CRC_NIB_LEVELS_ = 7;
 template <class C>
@@ -444,12 +448,12 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
 }
 
 // ==================================================================== k_huff
-// Ascending sort of 512 keys by one wave: 8 per lane (lane*8 + r), partners at distance
+// Ascending sort of the KEYN keys (padded to 512 with KEY_NONE) by one wave: 8 per lane (lane*8 + r), partners at distance
 // j >= 8 by shuffle, j < 8 inside the lane's registers.
 __device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
     uint32_t v[8];
 #pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = keys[lane * 8 + r];
+    for (int r = 0; r < 8; r++) v[r] = lane * 8 + r < KEYN ? keys[lane * 8 + r] : KEY_NONE;
 #pragma unroll
     for (uint32_t k = 2; k <= 512; k <<= 1) {
 #pragma unroll
@@ -475,7 +479,8 @@ __device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < 8; r++) keys[lane * 8 + r] = v[r];
+    for (int r = 0; r < 8; r++)
+        if (lane * 8 + r < KEYN) keys[lane * 8 + r] = v[r];
 }
 
 // The Huffman merge of tree T on one wave, in rounds.  Internal nodes are created in
@@ -491,8 +496,8 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
     const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
     const uint32_t* sk = S.hs.skey + base;
-    uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the jump rounds)
-    uint16_t* M = &S.hs.aB[0][0];     // merged prefix: leaf index | 0x8000, or internal index
+    uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the depth rounds)
+    uint16_t* M = S.hs.leafpar.v;     // merged prefix: leaf index | 0x8000, or internal index
     uint32_t* rq = S.hs.rec[T];
     uint16_t* rs = S.hs.rst[T];
     if (n < 2) {
@@ -845,7 +850,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     ph_rle_count<C>(tid, S);
     __syncthreads();
     {
-        const uint32_t nr = wave_scan_excl_add<SORTN>(S.hs.rcnt, tid);
+        const uint32_t nr = wave_scan_excl_add<RLEN>(S.rcnt, tid);
         if (tid == 0) S.misc[M_NRLE] = nr;
     }
     __syncthreads();
@@ -859,7 +864,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     ph_rle_bits<C>(tid, S);
     __syncthreads();
     {
-        const uint32_t hb = wave_scan_excl_add<SORTN>(S.rboff, tid);
+        const uint32_t hb = wave_scan_excl_add<RLEN>(S.rboff, tid);
         if (tid == 0) S.misc[M_HDRBITS] = hb;
     }
     __syncthreads();
@@ -998,6 +1003,9 @@ __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
 #endif
 #ifndef PBX_ENC_SKIP_STORE
 #define PBX_ENC_SKIP_STORE 0
+#endif
+#ifndef PBX_ENC_SKIP_TABLES
+#define PBX_ENC_SKIP_TABLES 0
 #endif
 
 // A token's bits packed in one register: value (<= 20 bits) | nbits << 27.  The LDS code
@@ -1158,8 +1166,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         for (uint32_t k = tid; k < (uint32_t)C::OUTW / 4; k += C::NT)
             o4[k] = (hdr && 4 * k < (uint32_t)C::HDRW) ? *(const uint4*)(cg + 320 + 4 * k) : make_uint4(0, 0, 0, 0);
     }
-    for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
-    for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
+    if (!PBX_ENC_SKIP_TABLES) {
+        for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
+        for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
+    }
     __syncthreads();
     if (gi.btype == 0) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; bytes
         uint8_t* ob = (uint8_t*)S.out;
