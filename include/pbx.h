@@ -72,7 +72,8 @@ typedef struct pbx_config {
     uint64_t max_batch_bytes;/* device scratch budget per batch; 0 = default */
     int32_t coalesce;        /* 1 (default) = concurrent pbx_get_tile calls are coalesced into
                                 batches (one per GPU-busy interval); 0 = one batch per call */
-    int32_t reserved;
+    int32_t stage_rows;      /* 0 (default) = the deflate kernels read filter-None rows straight
+                                from the plane; 1 = stage them in a stream buffer first (k_rows) */
 } pbx_config;
 
 typedef struct pbx_ctx pbx_ctx;

@@ -12,6 +12,21 @@ struct DevOps {
     __device__ static void aor(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 };
 
+// Load through a pointer known to be in global memory (plane pointers come from tile
+// descriptors, so the compiler cannot infer their address space and would emit FLAT loads,
+// which also count against lgkmcnt and so stall every later LDS wait on HBM latency).
+// (A native vector type: a uint4 struct copy is lowered to a memcpy that drops the cast.)
+typedef unsigned int pbx_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const void* p) {
+    const pbx_v4u v = *(const __attribute__((address_space(1))) pbx_v4u*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16(void* p, const uint4& v) {
+    pbx_v4u x;
+    x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    *(__attribute__((address_space(1))) pbx_v4u*)p = x;
+}
+
 // Bijective XCD-aware remap: consecutive logical ids land on the same XCD (shared L2),
 // since workgroups are dealt round-robin over the 8 XCDs.  Speed only, never correctness.
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
@@ -91,6 +106,31 @@ __device__ __forceinline__ uint4 swap16(uint4 q, int bpp) {
         q.x = b; q.y = a; q.z = d; q.w = c;
     }
     return q;
+}
+
+// APNGWriter's sign flip of int8 / int16 samples: the MS byte of each big-endian sample.
+__device__ __forceinline__ uint4 flip_msb(uint4 q, int bpp) {
+    const uint32_t m = bpp == 1 ? 0x80808080u : 0x00800080u;
+    q.x ^= m; q.y ^= m; q.z ^= m; q.w ^= m;
+    return q;
+}
+
+// Bytes [bs, bs + 16) of the 32 bytes lo || hi (bs < 16) as 4 words: two levels of mask
+// selects pick the 5 source words, one alignbit each.  (Masks, not ?: over an array: the
+// compiler turns `c ? a[k + 1] : a[k]` into a dynamic index, i.e. scratch memory.)
+__device__ __forceinline__ void funnel16(const uint4& lo, const uint4& hi, uint32_t bs, uint32_t (&w)[4]) {
+    const uint32_t m0 = 0u - ((bs >> 2) & 1u), m1 = 0u - ((bs >> 3) & 1u);
+    auto sel = [](uint32_t m, uint32_t y, uint32_t x) { return (y & m) | (x & ~m); };
+    const uint32_t u0 = sel(m0, lo.y, lo.x), u1 = sel(m0, lo.z, lo.y), u2 = sel(m0, lo.w, lo.z),
+                   u3 = sel(m0, hi.x, lo.w), u4 = sel(m0, hi.y, hi.x), u5 = sel(m0, hi.z, hi.y),
+                   u6 = sel(m0, hi.w, hi.z);
+    const uint32_t t0 = sel(m1, u2, u0), t1 = sel(m1, u3, u1), t2 = sel(m1, u4, u2),
+                   t3 = sel(m1, u5, u3), t4 = sel(m1, u6, u4);
+    const uint32_t sh = (bs & 3u) * 8;
+    w[0] = __builtin_amdgcn_alignbit(t1, t0, sh);
+    w[1] = __builtin_amdgcn_alignbit(t2, t1, sh);
+    w[2] = __builtin_amdgcn_alignbit(t3, t2, sh);
+    w[3] = __builtin_amdgcn_alignbit(t4, t3, sh);
 }
 
 }  // namespace pbx

@@ -206,6 +206,124 @@ __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, 
     }
 }
 
+// Stream bytes of a TF_DIRECT tile assembled in LDS straight from the plane in HBM
+// (getTileDirect + the APNGWriter scanline of filter None, TileRequestHandler.java:107-109,
+// 176-199): the bytes k_rows would have written to a stream buffer.  Row r of the stream is
+// [0] ++ the big-endian row (PNG) or the row alone (deflate-TIFF).  Source rows start 16-byte
+// aligned (the planner checks x * bpp % 16; the pitch is a multiple of 256).
+//
+// One wave per (row, 64 chunks of 16 bytes): lane t loads chunk c = 64 g + t of the row
+// (one coalesced 16-byte load, swapped / sign-flipped in registers) whose bytes land at LDS
+// byte dst = Q + 16 c, Q = the row's first data byte.  The misalignment o = -dst mod 4 is
+// the same for the whole row (a uniform branch), so the lane's bytes are 3 whole LDS words
+// (4 if o = 0) plus an o-byte head and a (4 - o)-byte tail written as byte / short stores;
+// neighbouring lanes share no byte, so no exchange is needed.  Lanes at the buffer edges or
+// with a partial last chunk write byte by byte.  The filter bytes (0) go with chunk 0.  The
+// loads of up to three rows are in flight at once.
+struct DirectRows {
+    const uint8_t* row0;  // region row 0 in the plane
+    int64_t pitch;
+    uint32_t rowlen, rb, fb, h, nc, ngrp;
+    int32_t bpp;
+    bool swap, flip;
+    __device__ __forceinline__ void init(const TileDesc& d) {
+        row0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
+        pitch = d.pitch;
+        fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
+        rowlen = d.rowlen;
+        rb = rowlen - fb;
+        h = (uint32_t)d.h;
+        nc = (rb + 15) >> 4;
+        ngrp = (nc + 63) >> 6;
+        bpp = d.bpp;
+        swap = (d.flags & TF_SWAP) != 0;
+        flip = (d.flags & TF_FLIP) != 0;
+    }
+};
+
+// LDS bytes [0, nb) = stream bytes [B, B + nb) of the tile, zero from nb up to nz (a
+// multiple of 4).  NT threads; wave w takes tasks w, w + NW, ... of (row, chunk group).
+template <int NT>
+__device__ __forceinline__ void fill_direct(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
+                                            uint32_t nz, uint32_t tid) {
+    constexpr uint32_t NW = NT / 64, K = 3;
+    uint8_t* bb = (uint8_t*)buf;
+    uint16_t* bh = (uint16_t*)buf;
+    const uint32_t lane = tid & 63, w = tid >> 6;
+    const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
+    const uint32_t ntask = (rz - ra + 1) * dr.ngrp;
+    auto task = [&](uint32_t k, uint32_t& i, uint32_t& c) {
+        i = dr.ngrp == 1 ? k : k / dr.ngrp;
+        c = (k - i * dr.ngrp) * 64 + lane;
+    };
+    for (uint32_t k0 = w; k0 < ntask; k0 += K * NW) {
+        uint4 v[K];
+#pragma unroll
+        for (uint32_t j = 0; j < K; j++) {  // the loads first
+            const uint32_t k = k0 + j * NW;
+            uint32_t i, c;
+            task(k, i, c);
+            const bool ok = k < ntask && c < dr.nc;
+            v[j] = gload16(dr.row0 + (int64_t)(ok ? ra + i : ra) * dr.pitch + 16 * (ok ? c : 0u));
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < K; j++) {
+            const uint32_t k = k0 + j * NW;
+            if (k >= ntask) break;  // uniform
+            uint32_t i, c;
+            task(k, i, c);
+            uint4 x = v[j];
+            if (dr.swap) x = swap16(x, dr.bpp);
+            if (dr.flip) x = flip_msb(x, dr.bpp);
+            const int32_t Q = (int32_t)((ra + i) * dr.rowlen + dr.fb) - (int32_t)B;
+            const int32_t dst = Q + 16 * (int32_t)c;
+            const uint32_t o = (uint32_t)(-Q) & 3u;  // = -dst mod 4, uniform over the task
+            const bool valid = c < dr.nc;
+            const bool whole = valid && dst >= 0 && dst + 16 <= (int32_t)nb && 16 * (c + 1) <= dr.rb;
+            if (whole) {
+                // LDS words from a0 = dst + o: w[j] = chunk bytes [o + 4j, o + 4j + 4)
+                const uint32_t sh = 8 * o;
+                const uint32_t wm = __builtin_amdgcn_alignbit(x.x, 0u, sh);  // head: top o bytes
+                const uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
+                const uint32_t w1 = __builtin_amdgcn_alignbit(x.z, x.y, sh);
+                const uint32_t w2 = __builtin_amdgcn_alignbit(x.w, x.z, sh);
+                const uint32_t w3 = __builtin_amdgcn_alignbit(0u, x.w, sh);   // tail: low 4 - o bytes
+                const int32_t a0 = dst + (int32_t)o;
+                uint32_t* wp = buf + (a0 >> 2);
+                wp[0] = w0;
+                wp[1] = w1;
+                wp[2] = w2;
+                if (o == 0) {
+                    wp[3] = w3;
+                } else if (o == 1) {
+                    bb[a0 - 1] = (uint8_t)(wm >> 24);
+                    bh[(a0 + 12) >> 1] = (uint16_t)w3;
+                    bb[a0 + 14] = (uint8_t)(w3 >> 16);
+                } else if (o == 2) {
+                    bh[(a0 - 2) >> 1] = (uint16_t)(wm >> 16);
+                    bh[(a0 + 12) >> 1] = (uint16_t)w3;
+                } else {
+                    bb[a0 - 3] = (uint8_t)(wm >> 8);
+                    bh[(a0 - 2) >> 1] = (uint16_t)(wm >> 16);
+                    bb[a0 + 12] = (uint8_t)w3;
+                }
+            } else if (valid && dst + 16 > 0 && dst < (int32_t)nb) {
+                const uint32_t nbc = dr.rb - 16 * c < 16 ? dr.rb - 16 * c : 16u;
+                for (uint32_t q = 0; q < nbc; q++) {
+                    const int32_t at = dst + (int32_t)q;
+                    const uint32_t lo = (q & 4u) ? x.y : x.x, hi = (q & 4u) ? x.w : x.z;
+                    if (at >= 0 && at < (int32_t)nb) bb[at] = (uint8_t)(((q & 8u) ? hi : lo) >> (8 * (q & 3u)));
+                }
+            }
+            if (dr.fb && c == 0 && dst - 1 >= 0 && dst - 1 < (int32_t)nb) bb[dst - 1] = 0;
+        }
+    }
+    // zero tail: bytes [nb, round4(nb)) and words up to nz
+    const uint32_t nb4 = (nb + 3) & ~3u;
+    if (tid < nb4 - nb) bb[nb + tid] = 0;
+    for (uint32_t k = nb4 / 4 + tid; k < nz / 4; k += NT) buf[k] = 0;
+}
+
 // ==================================================================== k_lz77
 // Zero bytes of x as 4 bits (bit j: byte j of x is zero).
 __device__ __forceinline__ uint32_t zero_nibble(uint32_t x) {
@@ -354,7 +472,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
 template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
-                                                uint32_t nseg, const uint8_t* __restrict__ stream,
+                                                uint32_t nseg, uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
                                                 uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps) {
     __shared__ LzSmem<C> S;
@@ -369,10 +487,30 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     const uint32_t ti = seg_tile[seg];
     const TileDesc d = dt[ti];
     const SegParams sp = seg_params(d, seg - d.seg_first);
-    load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
+    const bool direct = (d.flags & TF_DIRECT) != 0;
+    if (PROF) {  // diagnostics: the descriptor's arrival
+        __builtin_amdgcn_s_waitcnt(0);
+        stamp();
+    }
+    if (direct) {
+        DirectRows dr;
+        dr.init(d);
+        fill_direct<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
+    } else {
+        load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
+    }
     for (uint32_t k = tid; k < 288 * 4; k += C::NT) S.h8[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
+    if (PROF) {  // diagnostics: wave 0's fill done
+        __builtin_amdgcn_s_waitcnt(0);
+        stamp();
+    }
     __syncthreads();
+    if (direct) {  // the segment's stream bytes for k_encode (16-byte words; slack after every tile)
+        uint8_t* o = stream + d.out_off + sp.base + sp.wl;
+        for (uint32_t k = tid; k < (sp.sl + 15) / 16; k += C::NT)
+            *(uint4*)(o + 16 * k) = *(const uint4*)(S.buf + sp.wl / 4 + 4 * k);
+    }
     stamp();
     // the thread's chunk words (and the word before it) from LDS
     const uint32_t cs = tid * C::CH, wi = (sp.wl + cs) >> 2;
@@ -1124,7 +1262,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     sp.sl = gi.sl;
     sp.last = gi.last;
     sp.rowlen = gi.rowlen;
-    const uint8_t* seg_src = stream + (((uint64_t)gi.src_hi << 32) | gi.src_lo);
+    const uint64_t seg_off = ((uint64_t)gi.src_hi << 32) | gi.src_lo;
     const bool first = (gi.flags & SF_FIRST) != 0, lastb = (gi.flags & SF_LAST) != 0;
     const bool final_seg = sp.last != 0;          // the tile's stream ends in this segment
     const uint32_t byte0 = gi.bit0 >> 3, lb = gi.bit0 & 7u;  // out[] byte 0 = block byte byte0
@@ -1133,10 +1271,12 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     uint32_t cb[C::CH / 4];
     {
         const uint32_t cs = tid * C::CH;
-        const uint8_t* src = seg_src + cs;
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
-        if (cs < sp.sl) q0 = *(const uint4*)src;
-        if (cs + 16 < sp.sl) q1 = *(const uint4*)(src + 16);
+        {
+            const uint8_t* src = stream + seg_off + cs;
+            if (cs < sp.sl) q0 = *(const uint4*)src;
+            if (cs + 16 < sp.sl) q1 = *(const uint4*)(src + 16);
+        }
         cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
         cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
 #pragma unroll

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
         const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
         for (uint32_t i = tid; i < nv; i += 256) {
             const uint32_t r = r0 + i / n16, v = i % n16;
-            uint4 q = *(const uint4*)(src0 + (int64_t)r * d.pitch + 16 * v);
+            uint4 q = gload16(src0 + (int64_t)r * d.pitch + 16 * v);
             if (swap) q = swap16(q, d.bpp);
             *(uint4*)(base + (size_t)r * rb + 16 * v) = q;
         }
@@ -80,12 +80,6 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
 // FB_ROWS * rowlen is a multiple of 16, so bands never share an output word.
 constexpr int FB_ROWS = 16;
 constexpr int FB_LDS = 64 * 1024;
-
-__device__ __forceinline__ uint4 flip_msb(uint4 q, int bpp) {
-    const uint32_t m = bpp == 1 ? 0x80808080u : 0x00800080u;  // MS byte of each BE sample
-    q.x ^= m; q.y ^= m; q.z ^= m; q.w ^= m;
-    return q;
-}
 
 __device__ __forceinline__ uint32_t filt_byte(int ft, uint32_t cur, uint32_t left, uint32_t up,
                                              uint32_t ul) {
@@ -135,11 +129,11 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
             const int64_t row = (int64_t)r0 - 1 + q;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (row >= 0 && png) {
-                v = *(const uint4*)(src0 + row * d.pitch + 16 * c);
+                v = gload16(src0 + row * d.pitch + 16 * c);
                 if (swap) v = swap16(v, bpp);
                 if (flip) v = flip_msb(v, bpp);
             } else if (row >= 0) {
-                v = *(const uint4*)(src0 + row * d.pitch + 16 * c);
+                v = gload16(src0 + row * d.pitch + 16 * c);
                 if (swap) v = swap16(v, bpp);
             }
             *(uint4*)(sm + q * rbp + 16 * c) = v;
@@ -304,7 +298,7 @@ __global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt,
     uint32_t* rows = lrow + 4;
     for (uint32_t i = tid; i < nr * nc; i += RB_NT) {
         const uint32_t q = i / nc, c = i - q * nc;
-        uint4 v = *(const uint4*)(src0 + (int64_t)q * d.pitch + 16 * c);
+        uint4 v = gload16(src0 + (int64_t)q * d.pitch + 16 * c);
         if (swap) v = swap16(v, (int)bpp);
         if (flip) v = flip_msb(v, (int)bpp);
         *(uint4*)(rows + q * rw + 4 * c) = v;

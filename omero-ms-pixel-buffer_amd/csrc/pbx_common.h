@@ -28,6 +28,8 @@ enum : uint32_t {
     TF_FLIP = 2u,      // PNG int8/int16: flip the sign bit of the MS byte (APNGWriter)
     TF_PNGROWS = 4u,   // stream rows carry a leading PNG filter-type byte
     TF_TIFF = 8u,      // container is TIFF (else PNG) for deflate tiles
+    TF_DIRECT = 16u,   // filter-None rows, 16-byte aligned source, bpp <= 4: k_lz77
+                       // assembles the stream from the plane (no k_rows pass)
 };
 
 // PNG container layout (APNGWriter: sig, IHDR, acTL, fcTL, IDAT, IEND).

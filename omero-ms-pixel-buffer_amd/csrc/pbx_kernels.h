@@ -35,7 +35,8 @@ inline uint32_t rows_blocks_for(uint32_t h) { return (h + ROWS_BAND - 1) / ROWS_
 struct DeflateLaunch {
     const TileDesc* tiles;  // deflate tiles (seg_first / seg_count / out_off = stream offset)
     uint32_t ntiles, nseg;
-    const uint8_t* stream;  // filtered streams (16-byte aligned per tile, slack after)
+    uint8_t* stream;        // filtered streams (16-byte aligned per tile, slack after); k_lz77
+                            // writes those of TF_DIRECT tiles
     SegInfo* info;          // [nseg]
     uint32_t* hist;         // [nseg * HIST_WORDS]
     uint32_t* mrec;         // [nseg * MREC_WORDS]

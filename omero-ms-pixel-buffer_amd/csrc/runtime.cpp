@@ -167,7 +167,8 @@ struct pbx_batch {
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
     uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
-    uint32_t nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;  // dt[0..nrows_tiles): k_rows tiles
+    // dt = [direct tiles | k_rows tiles | k_filter tiles]
+    uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -467,6 +468,8 @@ int pbx_config_default(pbx_config* cfg) {
     cfg->coalesce = 1;
     const char* co = getenv("PBX_COALESCE");
     if (co) cfg->coalesce = atoi(co);
+    const char* sr = getenv("PBX_STAGE_ROWS");
+    if (sr) cfg->stage_rows = atoi(sr);
     const char* f = getenv("PBX_PNG_FILTER");
     if (f) cfg->png_filter = atoi(f);
     const char* td = getenv("PBX_TIFF_DEFLATE");
@@ -636,8 +639,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->h.resize(n);
     const int filter = ctx->cfg.png_filter;
     const bool tiff_deflate = ctx->cfg.tiff_deflate != 0;
-    std::vector<TileDesc> dt_rows, dt_band;
-    std::vector<uint32_t> req_rows, req_band;
+    std::vector<TileDesc> dt_direct, dt_rows, dt_band;
+    std::vector<uint32_t> req_direct, req_rows, req_band;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane pl;
@@ -682,19 +685,30 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                 d.rowlen = (uint32_t)w * bpp;
             }
             d.stream_len = (uint64_t)h * d.rowlen;
-            // k_rows (vector funnel copy) serves filter-None rows from 16-byte-aligned
-            // source rows; filtered or odd-shaped tiles go to the banded k_filter
+            // Filter-None rows from 16-byte-aligned source rows are read by k_lz77 straight
+            // from the plane (TF_DIRECT: no k_rows; k_lz77 writes the stream for k_encode);
+            // cfg.stage_rows routes them through k_rows (vector funnel copy) instead.
+            // Filtered or odd-shaped tiles go to the banded k_filter.
             const uint32_t rb = (uint32_t)w * bpp;
             const bool rows_ok = d.filter == 0 && d.rowlen >= 32 && rb <= ROWS_MAX_RB &&
                                  ((uint64_t)d.x * bpp % 16) == 0;
-            (rows_ok ? dt_rows : dt_band).push_back(d);
-            (rows_ok ? req_rows : req_band).push_back((uint32_t)i);
+            if (rows_ok && bpp <= 4 && !ctx->cfg.stage_rows) {
+                d.flags |= TF_DIRECT;
+                dt_direct.push_back(d);
+                req_direct.push_back((uint32_t)i);
+            } else {
+                (rows_ok ? dt_rows : dt_band).push_back(d);
+                (rows_ok ? req_rows : req_band).push_back((uint32_t)i);
+            }
         }
     }
+    b->ndirect_tiles = (uint32_t)dt_direct.size();
     b->nrows_tiles = (uint32_t)dt_rows.size();
-    b->dt = std::move(dt_rows);
+    b->dt = std::move(dt_direct);
+    b->dt.insert(b->dt.end(), dt_rows.begin(), dt_rows.end());
     b->dt.insert(b->dt.end(), dt_band.begin(), dt_band.end());
-    b->dt_req = std::move(req_rows);
+    b->dt_req = std::move(req_direct);
+    b->dt_req.insert(b->dt_req.end(), req_rows.begin(), req_rows.end());
     b->dt_req.insert(b->dt_req.end(), req_band.begin(), req_band.end());
     for (size_t k = 0; k < b->dt.size(); k++) {
         TileDesc& d = b->dt[k];
@@ -703,9 +717,12 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         b->nseg += d.seg_count;
         d.hblk_first = b->nblk;
         b->nblk += tile_blocks(d.seg_count);
+        b->stream_bytes += d.stream_len;
+        b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
         d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
         b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
-        if (k < b->nrows_tiles) {
+        if (k < b->ndirect_tiles) continue;  // k_lz77 assembles it from the plane
+        if (k < b->ndirect_tiles + b->nrows_tiles) {
             d.blk_first = b->rows_blocks;
             b->rows_blocks += rows_blocks_for((uint32_t)d.h);
             b->rows_max_rb = std::max<uint32_t>(b->rows_max_rb, d.rowlen - ((d.flags & TF_PNGROWS) ? 1u : 0u));
@@ -713,8 +730,6 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.blk_first = b->filt_blocks;
             b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
         }
-        b->stream_bytes += d.stream_len;
-        b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
     }
     *out = b;
     return PBX_OK;
@@ -756,9 +771,9 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
-    HIP_TRY(launch_rows(st, (const TileDesc*)b->d_dt, b->nrows_tiles, b->rows_blocks, b->rows_max_rb,
-                        (uint8_t*)b->d_stream));
-    HIP_TRY(launch_filter(st, (const TileDesc*)b->d_dt + b->nrows_tiles, ndt - b->nrows_tiles,
+    const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;
+    HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles, ndt - b->ndirect_tiles - b->nrows_tiles,
                           b->filt_blocks, (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
@@ -769,7 +784,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.tiles = (const TileDesc*)b->d_dt;
     a.ntiles = ndt;
     a.nseg = b->nseg;
-    a.stream = (const uint8_t*)b->d_stream;
+    a.stream = (uint8_t*)b->d_stream;
     a.info = (SegInfo*)b->d_info;
     a.hist = (uint32_t*)b->d_hist;
     a.mrec = (uint32_t*)b->d_mrec;

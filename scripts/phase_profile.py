@@ -8,10 +8,15 @@ import pbx  # noqa: E402
 
 gen = sys.argv[1] if len(sys.argv) > 1 else "noise"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-svc = pbx.PixelsService(device=0)
-svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
-ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
-        for i in range(n)]
+layout = sys.argv[3] if len(sys.argv) > 3 else "grid"  # "tall": one 512-px column of tiles
+svc = pbx.PixelsService(device=0, stage_rows=os.environ.get("PBX_STAGE_ROWS", "0") == "1")
+if layout == "tall":
+    svc.register_plane(1, 0, 0, 0, pbx.UINT16, 512, 512 * 4096, generator=gen)
+    ctxs = [pbx.TileCtx(1, 0, 0, 0, 0, i * 512, 512, 512, format="png") for i in range(n)]
+else:
+    svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
+    ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
+            for i in range(n)]
 for _ in range(2):
     b = pbx.Batch(svc, ctxs)
     b.launch()

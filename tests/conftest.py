@@ -30,6 +30,21 @@ def service():
 
 
 @pytest.fixture(scope="session")
+def staged_service():
+    """Filter-None rows staged in a stream buffer by k_rows (the default reads the plane
+    directly inside the deflate kernels)."""
+    import pbx
+    s = pbx.PixelsService(stage_rows=True)
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="session", params=["direct", "staged"])
+def png_service(request, service, staged_service):
+    return service if request.param == "direct" else staged_service
+
+
+@pytest.fixture(scope="session")
 def adaptive_service():
     import pbx
     s = pbx.PixelsService(png_filter=pbx.FILTER_ADAPTIVE, tiff_deflate=True)

@@ -77,7 +77,8 @@ PNG_TYPES = [pbx.INT8, pbx.UINT8, pbx.INT16, pbx.UINT16]
 
 @pytest.mark.parametrize("pt", PNG_TYPES)
 @pytest.mark.parametrize("kind", [1, 2])
-def test_png_decodes_bit_exact(service, oracle, pt, kind):
+def test_png_decodes_bit_exact(png_service, oracle, pt, kind):
+    service = png_service
     sx, sy = 700, 333
     iid, plane = host_plane(service, oracle, pt, sx, sy, kind=kind, big_endian=False)
     regions = [(0, 0, 512, 300), (3, 5, 1, 1), (0, 0, 1, 333), (11, 2, 513, 257), (0, 0, 0, 0),
@@ -102,12 +103,15 @@ def test_png_decodes_bit_exact(service, oracle, pt, kind):
         assert body[start:start + len(z)] == z
 
 
+@pytest.mark.parametrize("big_endian", [False, True])
 @pytest.mark.parametrize("pt", [pbx.UINT16, pbx.INT16, pbx.UINT8])
-def test_png_row_shapes(service, oracle, pt):
-    """Row layouts of the banded row kernel: 2 KiB - 8 KiB rows (large LDS bands), row
-    lengths that are not multiples of 16, band tails, aligned and unaligned starts."""
+def test_png_row_shapes(png_service, oracle, pt, big_endian):
+    """Row layouts of the direct plane reader and of the banded row kernel: 2 KiB - 8 KiB
+    rows (large LDS bands), row lengths that are not multiples of 16, band tails, aligned
+    and unaligned starts."""
+    service = png_service
     sx, sy = 4200, 41
-    iid, plane = host_plane(service, oracle, pt, sx, sy, kind=2, big_endian=False)
+    iid, plane = host_plane(service, oracle, pt, sx, sy, kind=2, big_endian=big_endian)
     bpp = oracle.BPP[pt]
     regions = [(0, 0, 4096, 20), (0, 1, 2048, 33), (16, 1, 2064, 17), (32, 7, 1000, 34),
                (8, 0, 777, 41), (0, 0, 31, 16), (0, 0, 15, 3), (4192 // bpp, 2, 8, 39)]
