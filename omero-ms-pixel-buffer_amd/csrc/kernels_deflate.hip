@@ -213,12 +213,10 @@ __device__ __forceinline__ void load_bytes16(uint32_t* dst, const uint8_t* src, 
 // aligned (the planner checks x * bpp % 16; the pitch is a multiple of 256).
 //
 // One wave per (row, 64 chunks of 16 bytes): lane t loads chunk c = 64 g + t of the row
-// (one coalesced 16-byte load, swapped / sign-flipped in registers) whose bytes land at LDS
-// byte dst = Q + 16 c, Q = the row's first data byte.  The misalignment o = -dst mod 4 is
-// the same for the whole row (a uniform branch), so the lane's bytes are 3 whole LDS words
-// (4 if o = 0) plus an o-byte head and a (4 - o)-byte tail written as byte / short stores;
-// neighbouring lanes share no byte, so no exchange is needed.  Lanes at the buffer edges or
-// with a partial last chunk write byte by byte.  The filter bytes (0) go with chunk 0.  The
+// (one coalesced 16-byte load, swapped / sign-flipped in registers) and stores it at LDS
+// byte Q + 16 c, Q = the row's first data byte, with ONE unaligned ds_write_b128 (gfx950
+// LDS takes byte-aligned accesses; chunks never share a byte).  Lanes at the buffer edges or
+// with a partial last chunk write byte by byte; the filter bytes (0) go with chunk 0.  The
 // loads of up to three rows are in flight at once.
 struct DirectRows {
     const uint8_t* row0;  // region row 0 in the plane
@@ -243,70 +241,47 @@ struct DirectRows {
 
 // LDS bytes [0, nb) = stream bytes [B, B + nb) of the tile, zero from nb up to nz (a
 // multiple of 4).  NT threads; wave w takes tasks w, w + NW, ... of (row, chunk group).
-template <int NT>
+template <int NT, class Stamp>
 __device__ __forceinline__ void fill_direct(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
-                                            uint32_t nz, uint32_t tid) {
+                                            uint32_t nz, uint32_t tid, Stamp&& stamp) {
     constexpr uint32_t NW = NT / 64, K = 3;
     uint8_t* bb = (uint8_t*)buf;
-    uint16_t* bh = (uint16_t*)buf;
-    const uint32_t lane = tid & 63, w = tid >> 6;
+    const uint32_t lane = tid & 63;
+    // task = (row, group of 64 chunks): everything but the lane's chunk offset is uniform
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
     const uint32_t ntask = (rz - ra + 1) * dr.ngrp;
-    auto task = [&](uint32_t k, uint32_t& i, uint32_t& c) {
-        i = dr.ngrp == 1 ? k : k / dr.ngrp;
-        c = (k - i * dr.ngrp) * 64 + lane;
-    };
     for (uint32_t k0 = w; k0 < ntask; k0 += K * NW) {
         uint4 v[K];
+        const uint8_t* rp[K];
+        int32_t q0[K];
+        uint32_t c0[K];
 #pragma unroll
         for (uint32_t j = 0; j < K; j++) {  // the loads first
-            const uint32_t k = k0 + j * NW;
-            uint32_t i, c;
-            task(k, i, c);
-            const bool ok = k < ntask && c < dr.nc;
-            v[j] = gload16(dr.row0 + (int64_t)(ok ? ra + i : ra) * dr.pitch + 16 * (ok ? c : 0u));
+            const uint32_t k = k0 + j * NW < ntask ? k0 + j * NW : k0;
+            const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
+            c0[j] = (k - i * dr.ngrp) * 64;
+            rp[j] = dr.row0 + (int64_t)(ra + i) * dr.pitch + 16 * c0[j];
+            q0[j] = (int32_t)((ra + i) * dr.rowlen + dr.fb) - (int32_t)B + 16 * (int32_t)c0[j];
+            v[j] = gload16(rp[j] + 16 * (c0[j] + lane < dr.nc ? lane : 0u));
         }
+        if (k0 == w) stamp(false);  // diagnostics: the first loads issued
 #pragma unroll
         for (uint32_t j = 0; j < K; j++) {
-            const uint32_t k = k0 + j * NW;
-            if (k >= ntask) break;  // uniform
-            uint32_t i, c;
-            task(k, i, c);
+            if (k0 + j * NW >= ntask) break;  // uniform
             uint4 x = v[j];
             if (dr.swap) x = swap16(x, dr.bpp);
             if (dr.flip) x = flip_msb(x, dr.bpp);
-            const int32_t Q = (int32_t)((ra + i) * dr.rowlen + dr.fb) - (int32_t)B;
-            const int32_t dst = Q + 16 * (int32_t)c;
-            const uint32_t o = (uint32_t)(-Q) & 3u;  // = -dst mod 4, uniform over the task
+            const uint32_t c = c0[j] + lane;
+            const int32_t dst = q0[j] + 16 * (int32_t)lane;  // LDS byte of the chunk's first byte
             const bool valid = c < dr.nc;
-            const bool whole = valid && dst >= 0 && dst + 16 <= (int32_t)nb && 16 * (c + 1) <= dr.rb;
-            if (whole) {
-                // LDS words from a0 = dst + o: w[j] = chunk bytes [o + 4j, o + 4j + 4)
-                const uint32_t sh = 8 * o;
-                const uint32_t wm = __builtin_amdgcn_alignbit(x.x, 0u, sh);  // head: top o bytes
-                const uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
-                const uint32_t w1 = __builtin_amdgcn_alignbit(x.z, x.y, sh);
-                const uint32_t w2 = __builtin_amdgcn_alignbit(x.w, x.z, sh);
-                const uint32_t w3 = __builtin_amdgcn_alignbit(0u, x.w, sh);   // tail: low 4 - o bytes
-                const int32_t a0 = dst + (int32_t)o;
-                uint32_t* wp = buf + (a0 >> 2);
-                wp[0] = w0;
-                wp[1] = w1;
-                wp[2] = w2;
-                if (o == 0) {
-                    wp[3] = w3;
-                } else if (o == 1) {
-                    bb[a0 - 1] = (uint8_t)(wm >> 24);
-                    bh[(a0 + 12) >> 1] = (uint16_t)w3;
-                    bb[a0 + 14] = (uint8_t)(w3 >> 16);
-                } else if (o == 2) {
-                    bh[(a0 - 2) >> 1] = (uint16_t)(wm >> 16);
-                    bh[(a0 + 12) >> 1] = (uint16_t)w3;
-                } else {
-                    bb[a0 - 3] = (uint8_t)(wm >> 8);
-                    bh[(a0 - 2) >> 1] = (uint16_t)(wm >> 16);
-                    bb[a0 + 12] = (uint8_t)w3;
-                }
+            if (valid && dst >= 0 && dst + 16 <= (int32_t)nb && 16 * (c + 1) <= dr.rb) {
+                // one unaligned 16-byte LDS store (gfx950 DS access is unaligned-capable)
+#ifdef PBX_LZ_ALIGNED_FILL  // timing experiment only: aligned stores (wrong output)
+                __builtin_memcpy(bb + (dst & ~15), &x, 16);
+#else
+                __builtin_memcpy(bb + dst, &x, 16);
+#endif
             } else if (valid && dst + 16 > 0 && dst < (int32_t)nb) {
                 const uint32_t nbc = dr.rb - 16 * c < 16 ? dr.rb - 16 * c : 16u;
                 for (uint32_t q = 0; q < nbc; q++) {
@@ -318,6 +293,7 @@ __device__ __forceinline__ void fill_direct(uint32_t* buf, const DirectRows& dr,
             if (dr.fb && c == 0 && dst - 1 >= 0 && dst - 1 < (int32_t)nb) bb[dst - 1] = 0;
         }
     }
+    stamp(true);  // diagnostics: the rows stored
     // zero tail: bytes [nb, round4(nb)) and words up to nz
     const uint32_t nb4 = (nb + 3) & ~3u;
     if (tid < nb4 - nb) bb[nb + tid] = 0;
@@ -485,19 +461,34 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     };
     stamp();
     const uint32_t ti = seg_tile[seg];
-    const TileDesc d = dt[ti];
+    TileDesc d;
+    {  // the whole descriptor in one round of scalar loads: the fence keeps the compiler from
+       // sinking the plane fields' loads past the branches into a second dependent round
+        uint4 q[sizeof(TileDesc) / 16];
+#pragma unroll
+        for (uint32_t i = 0; i < sizeof(TileDesc) / 16; i++) q[i] = ((const uint4*)(dt + ti))[i];
+        asm volatile("" : "+s"(q[0].x), "+s"(q[0].y), "+s"(q[0].z), "+s"(q[0].w), "+s"(q[1].x), "+s"(q[1].y),
+                     "+s"(q[1].z), "+s"(q[1].w), "+s"(q[2].x), "+s"(q[2].y), "+s"(q[2].z), "+s"(q[2].w),
+                     "+s"(q[3].x), "+s"(q[3].y), "+s"(q[3].z), "+s"(q[3].w), "+s"(q[4].x), "+s"(q[4].y));
+        __builtin_memcpy(&d, q, sizeof d);
+    }
     const SegParams sp = seg_params(d, seg - d.seg_first);
     const bool direct = (d.flags & TF_DIRECT) != 0;
-    if (PROF) {  // diagnostics: the descriptor's arrival
-        __builtin_amdgcn_s_waitcnt(0);
-        stamp();
-    }
+    DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
+    dr.init(d);
     if (direct) {
-        DirectRows dr;
-        dr.init(d);
-        fill_direct<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
+        uint32_t nfs = 0;
+        fill_direct<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid,
+                           [&](bool wait) {  // diagnostics: 2 sub-phase stamps (PROF only)
+                               if (!PROF || nfs >= 2) return;
+                               if (wait) __builtin_amdgcn_s_waitcnt(0);
+                               stamp();
+                               nfs++;
+                           });
+        if (PROF && nfs < 2) { stamp(); if (nfs < 1) stamp(); }
     } else {
         load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
+        if (PROF) { stamp(); stamp(); }
     }
     for (uint32_t k = tid; k < 288 * 4; k += C::NT) S.h8[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
@@ -506,7 +497,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
         stamp();
     }
     __syncthreads();
-    if (direct) {  // the segment's stream bytes for k_encode (16-byte words; slack after every tile)
+#ifndef PBX_LZ_SKIP_STORE
+#define PBX_LZ_SKIP_STORE 0  // timing experiments only (scripts/variants.sh): wrong output
+#endif
+    if (direct && !PBX_LZ_SKIP_STORE) {  // the segment's stream bytes for k_encode (16-byte words; slack after every tile)
         uint8_t* o = stream + d.out_off + sp.base + sp.wl;
         for (uint32_t k = tid; k < (sp.sl + 15) / 16; k += C::NT)
             *(uint4*)(o + 16 * k) = *(const uint4*)(S.buf + sp.wl / 4 + 4 * k);

@@ -13,6 +13,9 @@ svc = pbx.PixelsService(device=0, stage_rows=os.environ.get("PBX_STAGE_ROWS", "0
 if layout == "tall":
     svc.register_plane(1, 0, 0, 0, pbx.UINT16, 512, 512 * 4096, generator=gen)
     ctxs = [pbx.TileCtx(1, 0, 0, 0, 0, i * 512, 512, 512, format="png") for i in range(n)]
+elif layout == "same":  # every request the same tile: the plane reads hit the caches
+    svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
+    ctxs = [pbx.TileCtx(1, 0, 0, 0, 0, 0, 512, 512, format="png") for i in range(n)]
 else:
     svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
     ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
