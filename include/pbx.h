@@ -37,7 +37,8 @@ enum pbx_status {
     PBX_OK = 0,
     PBX_E_BADARG = 400,
     PBX_E_NOTFOUND = 404,
-    PBX_E_INTERNAL = 500
+    PBX_E_INTERNAL = 500,
+    PBX_E_PENDING = 504      /* pbx_wait: the batch is still running (not a tile status) */
 };
 
 /* OMERO pixel types (ome.xml.model.enums.PixelType; TileRequestHandler.java:100-101,164-165). */
@@ -107,6 +108,14 @@ typedef struct pbx_plane_desc {
 
 int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* desc, uint64_t* plane_id);
 int pbx_plane_release(pbx_ctx* ctx, uint64_t plane_id);
+/* Resolution pyramid on the GPU (the lower levels
+ * PixelBuffer.setResolutionLevel selects, TileRequestHandler.java:89-91): registers `levels`
+ * planes of the same (image, z, c, t) at resolutions r+1 .. r+levels (r = the plane's), each
+ * the 2x2 box mean of the one above (sizes rounded up; the last column / row repeated for odd
+ * sizes; integers (sum + 2) >> 2 on the exact sum, arithmetic for signed types; float/double
+ * ((a + b) + (c + d)) * 0.25), in the plane's byte order.  ids[k] = the plane id of level
+ * r+1+k (ids may be NULL).  Tiles of a level are served with pbx_tile_req.resolution. */
+int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t plane_id, int32_t levels, uint64_t* ids);
 /* Copy a registered plane back to the host, samples in big-endian order (test hook). */
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
 
@@ -137,6 +146,17 @@ int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out);
 /* Synchronous batch: n independent getTile calls executed as one set of GPU launches. */
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out);
 void pbx_results_release(pbx_ctx* ctx, pbx_result* results, uint64_t n);
+
+/* Batched async: pbx_submit plans and launches n independent getTile
+ * requests and returns at once; pbx_wait blocks until the batch has finished (timeout_us < 0:
+ * no limit; 0: poll), fills out[0..n) (the array given to pbx_submit) exactly like
+ * pbx_get_tiles and frees the ticket.  On PBX_E_PENDING the ticket stays valid: call again.
+ * Batches run in submission order on the context's stream; results are released with
+ * pbx_results_release. */
+typedef struct pbx_ticket pbx_ticket;
+int pbx_submit(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out,
+               pbx_ticket** ticket);
+int pbx_wait(pbx_ctx* ctx, pbx_ticket* ticket, int64_t timeout_us);
 
 /* Device-resident batches: plan once, launch asynchronously on the context's stream,
  * outputs stay in HBM until pbx_batch_fetch.  Used by callers that pipeline requests

@@ -9,6 +9,8 @@
 // HBM-bound byte work: 16-byte loads/stores, byte swaps in registers, no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev_util.h"
 #include "pbx_common.h"
 #include "pbx_kernels.h"
@@ -33,6 +35,85 @@ __global__ __launch_bounds__(256) void k_gen_plane(uint8_t* __restrict__ out, in
         default: *(uint64_t*)p = v; break;
         }
     }
+}
+
+// ------------------------------------------------------------------ resolution pyramid
+// One level of the on-GPU pyramid (the levels PixelBuffer.setResolutionLevel
+// selects, TileRequestHandler.java:89-91): out(x, y) = mean of in(2x..2x+1, 2y..2y+1), the
+// last column / row repeated when the input size is odd.  Integers: (sum + 2) >> 2 on the
+// exact 64-bit sum (arithmetic shift for signed types: floor((sum + 2) / 4)); float/double:
+// ((a + b) + (c + d)) * 0.25 in the sample's precision.  One thread per output sample; a
+// horizontal pair of input samples is one aligned 2*bpp-byte load (rows are 256-aligned).
+template <class T>
+__device__ __forceinline__ T ds_swap(T v, bool be) {
+    if constexpr (sizeof(T) == 1) {
+        return v;
+    } else if constexpr (sizeof(T) == 2) {
+        if (!be) return v;
+        const uint16_t u = __builtin_bit_cast(uint16_t, v);
+        return __builtin_bit_cast(T, (uint16_t)((u >> 8) | (u << 8)));
+    } else if constexpr (sizeof(T) == 4) {
+        return be ? __builtin_bit_cast(T, __builtin_bswap32(__builtin_bit_cast(uint32_t, v))) : v;
+    } else {
+        return be ? __builtin_bit_cast(T, __builtin_bswap64(__builtin_bit_cast(uint64_t, v))) : v;
+    }
+}
+
+template <class T>
+__device__ __forceinline__ T ds_mean4(T a, T b, T c, T d) {
+    if constexpr (std::is_floating_point<T>::value) {
+        return ((a + b) + (c + d)) * (T)0.25;
+    } else {
+        const int64_t s = (int64_t)a + (int64_t)b + (int64_t)c + (int64_t)d;
+        return (T)((s + 2) >> 2);
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_downsample(const uint8_t* __restrict__ src, int64_t spitch,
+                                                    int32_t sx, int32_t sy, uint8_t* __restrict__ dst,
+                                                    int64_t dpitch, int32_t dx, int32_t dy, bool be) {
+    const uint64_t total = (uint64_t)dx * (uint64_t)dy;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int32_t y = (int32_t)(i / (uint64_t)dx), x = (int32_t)(i - (uint64_t)y * dx);
+        const int32_t y0 = 2 * y, y1 = 2 * y + 1 < sy ? 2 * y + 1 : sy - 1;
+        const bool pair = 2 * x + 1 < sx;
+        const T* r0 = (const T*)(src + (int64_t)y0 * spitch) + 2 * x;
+        const T* r1 = (const T*)(src + (int64_t)y1 * spitch) + 2 * x;
+        T a, b, c, d;
+        if (pair) {
+            using P = HIP_vector_type<T, 2>;
+            const P p0 = *(const P*)r0, p1 = *(const P*)r1;
+            a = p0.x; b = p0.y; c = p1.x; d = p1.y;
+        } else {
+            a = b = r0[0];
+            c = d = r1[0];
+        }
+        const T m = ds_mean4(ds_swap(a, be), ds_swap(b, be), ds_swap(c, be), ds_swap(d, be));
+        ((T*)(dst + (int64_t)y * dpitch))[x] = ds_swap(m, be);
+    }
+}
+
+hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch, int32_t sx, int32_t sy,
+                             uint8_t* dst, int64_t dpitch, int32_t dx, int32_t dy, int32_t pixel_type,
+                             bool be) {
+    const uint64_t total = (uint64_t)dx * (uint64_t)dy;
+    uint64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (!blocks) return hipSuccess;
+    const dim3 g((uint32_t)blocks), b(256);
+    switch (pixel_type) {
+    case PT_INT8: hipLaunchKernelGGL(k_downsample<int8_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_UINT8: hipLaunchKernelGGL(k_downsample<uint8_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_INT16: hipLaunchKernelGGL(k_downsample<int16_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_UINT16: hipLaunchKernelGGL(k_downsample<uint16_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_INT32: hipLaunchKernelGGL(k_downsample<int32_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_UINT32: hipLaunchKernelGGL(k_downsample<uint32_t>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    case PT_FLOAT: hipLaunchKernelGGL(k_downsample<float>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    default: hipLaunchKernelGGL(k_downsample<double>, g, b, 0, st, src, spitch, sx, sy, dst, dpitch, dx, dy, be); break;
+    }
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------ extraction

@@ -14,6 +14,11 @@ hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t
                             int32_t z, int32_t c, int32_t t);
 
 // K1: raw / uncompressed-TIFF tiles (getTileDirect + big-endian; TIFF header in front).
+// Resolution pyramid level: dst (dx x dy) = 2x2 box mean of src (sx x sy), edge samples
+// repeated for odd sizes; samples big-endian in memory when `be`.
+hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch, int32_t sx, int32_t sy,
+                             uint8_t* dst, int64_t dpitch, int32_t dx, int32_t dy, int32_t pixel_type,
+                             bool be);
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                           uint32_t nblocks, uint8_t* out);
 

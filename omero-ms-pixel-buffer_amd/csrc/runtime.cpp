@@ -591,6 +591,57 @@ int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id
     return PBX_OK;
 }
 
+int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t* ids) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    if (levels < 1 || levels > 30) return fail(PBX_E_BADARG, "bad level count %d", levels);
+    Plane src;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto it = ctx->planes.find(id);
+        if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+        src = it->second;
+        for (int32_t k = 1; k <= levels; k++)
+            if (ctx->index.count(std::make_tuple(src.image_id, src.z, src.c, src.t, src.res + k)))
+                return fail(PBX_E_BADARG, "resolution %d already registered", src.res + k);
+    }
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    const int bpp = bpp_of(src.pixel_type);
+    std::vector<Plane> made;
+    auto undo = [&](int code) {
+        for (Plane& q : made) (void)hipFree(q.dev);
+        return code;
+    };
+    Plane prev = src;
+    for (int32_t k = 1; k <= levels; k++) {
+        Plane p = prev;
+        p.res = src.res + k;
+        p.size_x = (prev.size_x + 1) / 2;
+        p.size_y = (prev.size_y + 1) / 2;
+        p.pitch = ((int64_t)p.size_x * bpp + 255) & ~(int64_t)255;
+        p.bytes = (size_t)p.pitch * p.size_y + 256;
+        hipError_t e = hipMalloc((void**)&p.dev, p.bytes);
+        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
+        made.push_back(p);
+        e = launch_downsample(ctx->stream, prev.dev, prev.pitch, prev.size_x, prev.size_y, p.dev, p.pitch,
+                              p.size_x, p.size_y, p.pixel_type, !p.little_endian && bpp > 1);
+        if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * p.size_y, 0, 256, ctx->stream);
+        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
+        prev = p;
+    }
+    const hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    for (size_t k = 0; k < made.size(); k++) {
+        Plane& p = made[k];
+        p.id = ctx->next_id++;
+        ctx->planes[p.id] = p;
+        ctx->index[std::make_tuple(p.image_id, p.z, p.c, p.t, p.res)] = p.id;
+        ctx->images[p.image_id].planes++;
+        if (ids) ids[k] = p.id;
+    }
+    return PBX_OK;
+}
+
 int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     std::lock_guard<std::mutex> run(ctx->run_mu);
@@ -968,6 +1019,74 @@ void pbx_results_release(pbx_ctx* ctx, pbx_result* res, uint64_t n) {
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out) {
     if (!ctx || !out || (!reqs && n)) return fail(PBX_E_BADARG, "null argument");
     return run_batch(ctx, reqs, n, out);
+}
+
+struct pbx_ticket {
+    pbx_batch* b = nullptr;
+    pbx_result* out = nullptr;
+    int launch_status = PBX_OK;
+    std::string launch_err;
+};
+
+int pbx_submit(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out, pbx_ticket** ticket) {
+    if (!ctx || !out || !ticket || (!reqs && n)) return fail(PBX_E_BADARG, "null argument");
+    *ticket = nullptr;
+    pbx_batch* b = nullptr;
+    int st;
+    {
+        std::lock_guard<std::mutex> run(ctx->run_mu);
+        st = pbx_batch_plan(ctx, reqs, n, &b);
+        if (st) return st;
+        st = pbx_batch_launch(ctx, b);
+    }
+    ctx->n_batches++;
+    ctx->n_requests += n;
+    pbx_ticket* t = new pbx_ticket();
+    t->b = b;
+    t->out = out;
+    t->launch_status = st;
+    if (st != PBX_OK) t->launch_err = g_err;
+    *ticket = t;
+    return PBX_OK;
+}
+
+int pbx_wait(pbx_ctx* ctx, pbx_ticket* t, int64_t timeout_us) {
+    if (!ctx || !t) return fail(PBX_E_BADARG, "null argument");
+    pbx_batch* b = t->b;
+    if (t->launch_status == PBX_OK && b->launched && timeout_us >= 0) {
+        if (ensure_device(ctx)) return PBX_E_INTERNAL;
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+        for (;;) {
+            const hipError_t q = hipEventQuery(b->ev[8]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) {
+                t->launch_status = fail(PBX_E_INTERNAL, "hipEventQuery: %s", hipGetErrorString(q));
+                t->launch_err = g_err;
+                break;
+            }
+            if (std::chrono::steady_clock::now() >= until) return PBX_E_PENDING;
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    int st = t->launch_status;
+    if (st == PBX_OK) st = pbx_batch_fetch(ctx, b, t->out);
+    if (st != PBX_OK) {  // every request of the batch fails with 500 (or its own 4xx)
+        const std::string msg = t->launch_status != PBX_OK ? t->launch_err : g_err;
+        for (size_t i = 0; i < b->reqs.size(); i++) {
+            pbx_result& r = t->out[i];
+            r.status = b->status[i] == PBX_OK ? PBX_E_INTERNAL : b->status[i];
+            r.format = b->reqs[i].format;
+            r.w = b->w[i];
+            r.h = b->h[i];
+            r.data = nullptr;
+            r.len = 0;
+            r.owner = nullptr;
+        }
+        g_err = msg;
+    }
+    pbx_batch_destroy(ctx, b);
+    delete t;
+    return st;
 }
 
 int pbx_abi_sizes(uint64_t* sizes, int n) {

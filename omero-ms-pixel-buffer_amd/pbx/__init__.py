@@ -29,7 +29,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PBX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
 
 # enum pbx_status — the HTTP status the reference ends with
-OK, E_BADARG, E_NOTFOUND, E_INTERNAL = 0, 400, 404, 500
+OK, E_BADARG, E_NOTFOUND, E_INTERNAL, E_PENDING = 0, 400, 404, 500, 504
 # enum pbx_pixel_type (OMERO PixelType names)
 PIXEL_TYPES = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "float", "double"]
 INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT, DOUBLE = range(8)
@@ -90,7 +90,7 @@ EXPORTS = [
     "pbx_batch_stats_get", "pbx_tile_filename", "pbx_content_type", "pbx_format_from_string",
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
-    "pbx_test_batch_lz77",
+    "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
 ]
 
 _lib = None
@@ -120,10 +120,14 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
+    L.pbx_plane_build_pyramid.argtypes = [vp, u64, i32, ctypes.POINTER(u64)]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
     L.pbx_test_batch_lz77.argtypes = [vp, vp, vp, vp, u64]
     L.pbx_ctx_stats_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.pbx_get_tiles.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(PbxResult)]
+    L.pbx_submit.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(PbxResult),
+                             ctypes.POINTER(vp)]
+    L.pbx_wait.argtypes = [vp, vp, ctypes.c_int64]
     L.pbx_results_release.argtypes = [vp, ctypes.POINTER(PbxResult), u64]
     L.pbx_results_release.restype = None
     L.pbx_batch_plan.argtypes = [vp, ctypes.POINTER(PbxTileReq), u64, ctypes.POINTER(vp)]
@@ -334,6 +338,13 @@ class PixelsService:
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))
 
+    def build_pyramid(self, plane_id: int, levels: int) -> List[int]:
+        """Resolution levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
+        returns their plane ids.  Tiles of level k: TileCtx(..., resolution=k)."""
+        ids = (ctypes.c_uint64 * max(levels, 1))()
+        _check(lib().pbx_plane_build_pyramid(self._h, plane_id, levels, ids))
+        return list(ids)[:levels]
+
     def read_plane_be(self, plane_id: int, nbytes: int) -> bytes:
         buf = ctypes.create_string_buffer(nbytes)
         _check(lib().pbx_plane_read_be(self._h, plane_id, buf, nbytes))
@@ -378,6 +389,45 @@ class PixelsService:
                 out.append((r.status, body))
         finally:
             lib().pbx_results_release(self._h, res, n)
+        if st != OK and not out:
+            _check(st)
+        return out
+
+
+    # Batched async: submit returns at once, Ticket.wait() collects (pbx_submit / pbx_wait).
+    def submit(self, ctxs: Sequence[TileCtx]) -> "Ticket":
+        return Ticket(self, ctxs)
+
+
+class Ticket:
+    """A submitted batch of getTile requests (pbx_submit); wait() returns what get_tiles would."""
+
+    def __init__(self, service: PixelsService, ctxs: Sequence[TileCtx]):
+        self.service, self.ctxs, self.n = service, list(ctxs), len(ctxs)
+        self._reqs = make_reqs(self.ctxs)
+        self._res = (PbxResult * max(self.n, 1))()
+        h = ctypes.c_void_p()
+        _check(lib().pbx_submit(service._h, self._reqs, self.n, self._res, ctypes.byref(h)))
+        self._t = h
+
+    def wait(self, timeout_us: int = -1) -> Optional[List[Tuple[int, Optional[bytes]]]]:
+        """Results, or None if the batch is still running after timeout_us (then call again)."""
+        if self._t is None:
+            raise RuntimeError("pbx: ticket already collected")
+        st = lib().pbx_wait(self.service._h, self._t, timeout_us)
+        if st == E_PENDING:
+            return None
+        self._t = None
+        out = []
+        try:
+            for i in range(self.n):
+                r = self._res[i]
+                body = ctypes.string_at(r.data, r.len) if r.status == OK and r.len else (
+                    b"" if r.status == OK else None)
+                self.ctxs[i].region["width"], self.ctxs[i].region["height"] = r.w, r.h
+                out.append((r.status, body))
+        finally:
+            lib().pbx_results_release(self.service._h, self._res, self.n)
         if st != OK and not out:
             _check(st)
         return out

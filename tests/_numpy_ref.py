@@ -46,3 +46,19 @@ def region(kind, pt, x0, y0, w, h, seed=0, plane_no=0, z=0, c=0, t=0):
         v = (256 + ((x >> 5) + (y >> 5)) % 16 * 48 + (r & np.uint64(0xFF)).astype(np.int64)
              + ((r >> np.uint64(8)) & np.uint64(0xFF)).astype(np.int64))
     return np.ascontiguousarray(_cast(pt, v)).tobytes()
+
+
+def downsample(a):
+    """One level of the resolution pyramid (include/pbx.h pbx_plane_build_pyramid), restated
+    independently of csrc/kernels_io.hip: the 2x2 box mean, the last column / row repeated
+    for odd sizes; integers (exact sum + 2) >> 2 (floor for signed), floats
+    ((a + b) + (c + d)) * 0.25 in the array's precision.  `a`: 2-D array (any byte order)."""
+    if a.shape[1] % 2:
+        a = np.concatenate([a, a[:, -1:]], axis=1)
+    if a.shape[0] % 2:
+        a = np.concatenate([a, a[-1:, :]], axis=0)
+    p, q, r, s = a[0::2, 0::2], a[0::2, 1::2], a[1::2, 0::2], a[1::2, 1::2]
+    if a.dtype.kind == "f":
+        return ((p + q) + (r + s)) * a.dtype.type(0.25)
+    tot = p.astype(np.int64) + q.astype(np.int64) + r.astype(np.int64) + s.astype(np.int64)
+    return ((tot + 2) >> 2).astype(a.dtype)

@@ -213,3 +213,82 @@ def test_pipelined_batches_overlap_d2h(service, oracle):
             else:
                 r, px, _ = oracle.png_decode(body)
                 assert r == 0 and px == tile
+
+
+def test_submit_wait(service, oracle):
+    """Batched async C-ABI (pbx_submit / pbx_wait): several batches in flight,
+    polled with a zero timeout and collected out of order; each returns its own tiles, and
+    a bad request fails alone with the reference's 404."""
+    iid = next(_ids)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT16, 2048, 2048, generator="noise", seed=3)
+    sets = []
+    for k in range(3):
+        ctxs = [pbx.TileCtx(iid, 0, 0, 0, 256 * ((i + k) % 8), 256 * (i // 8), 256, 256,
+                            format=("png", None, "tif")[k]) for i in range(32)]
+        ctxs.append(pbx.TileCtx(iid, 0, 0, 0, 2000, 0, 256, 256))  # out of bounds -> 404
+        sets.append((ctxs, service.submit(ctxs)))
+    first = sets[0][1].wait(0)  # a poll: the results, or None while the batch runs
+    got = {0: first} if first is not None else {}
+    for k in (2, 1, 0):
+        if k not in got:
+            got[k] = sets[k][1].wait()
+    for k, (ctxs, t) in enumerate(sets):
+        res = got[k]
+        assert len(res) == len(ctxs)
+        assert res[-1] == (pbx.E_NOTFOUND, None)
+        for i in (0, 9, 31):
+            c = ctxs[i]
+            tile = oracle.gen_region(2, pbx.UINT16, c.x, c.y, 256, 256, seed=3).tobytes()
+            st, body = res[i]
+            assert st == pbx.OK
+            if k == 0:
+                r, px, _ = oracle.png_decode(body)
+            elif k == 1:
+                r, px = 0, body
+            else:
+                r, px, _ = oracle.tiff_decode(body, len(tile))
+            assert r == 0 and px == tile, (k, i)
+        with pytest.raises(RuntimeError):
+            t.wait()
+
+
+@pytest.mark.parametrize("pt", range(8))
+@pytest.mark.parametrize("source", ["host_be", "gen"])
+def test_resolution_pyramid(service, oracle, pt, source):
+    """On-GPU resolution pyramid (row f3): every level equals the numpy restatement of the
+    2x2 box mean applied level by level (bit-exact, floats included), and tiles of a level
+    are served through the ordinary getTile path with `resolution` (raw and PNG)."""
+    import _numpy_ref as R
+    iid = next(_ids)
+    sx, sy = 301, 97
+    dt = R.DTYPES_BE[pt]
+    be = oracle.gen_region(2, pt, 0, 0, sx, sy, seed=7)
+    if source == "host_be":
+        pid = service.register_plane(iid, 0, 0, 0, pt, sx, sy, data=be, big_endian=True)
+    else:
+        pid = service.register_plane(iid, 0, 0, 0, pt, sx, sy, generator="noise", seed=7)
+    ids = service.build_pyramid(pid, 4)
+    want = np.frombuffer(be.tobytes(), dt).reshape(sy, sx)
+    for k, lid in enumerate(ids, start=1):
+        want = R.downsample(want)
+        h, w = want.shape
+        got = service.read_plane_be(lid, w * h * oracle.BPP[pt])
+        assert got == want.astype(dt).tobytes(), (pt, source, k)
+    # tiles of level 2 (76 x 25): raw bytes and (8/16-bit types) PNG pixels
+    lvl = R.downsample(R.downsample(np.frombuffer(be.tobytes(), dt).reshape(sy, sx))).astype(dt)
+    ctxs = [pbx.TileCtx(iid, 0, 0, 0, 3, 2, 40, 20, resolution=2),
+            pbx.TileCtx(iid, 0, 0, 0, 0, 0, 76, 25, resolution=2, format="png"),
+            pbx.TileCtx(iid, 0, 0, 0, 70, 20, 10, 10, resolution=2)]  # past the level -> 404
+    (s1, raw), (s2, png), (s3, _) = service.get_tiles(ctxs)
+    assert s1 == pbx.OK and raw == lvl[2:22, 3:43].tobytes()
+    assert s3 == pbx.E_NOTFOUND
+    if pt in (pbx.INT8, pbx.UINT8, pbx.INT16, pbx.UINT16):
+        assert s2 == pbx.OK
+        r, px, _ = oracle.png_decode(png)
+        bpp = oracle.BPP[pt]
+        flip = bytearray(lvl.tobytes())
+        if pt in (pbx.INT8, pbx.INT16):
+            flip[0::bpp] = bytes(b ^ 0x80 for b in flip[0::bpp])
+        assert r == 0 and px == bytes(flip)
+    else:
+        assert s2 == pbx.E_NOTFOUND  # APNGWriter rejects 32/64-bit types
