@@ -166,6 +166,18 @@ def extra(out, svc, rank, world, barrier, iid, side):
             "tiles_per_s": round(len(grid_ctxs(iid, "png")) * 5 * world / dts, 1),
             "k_rows_ms": round(mean(sst, "ms_filter"), 3),
             "k_lz77_ms": round(mean(sst, "ms_lz77"), 3)}
+    # Row f3: on-GPU resolution pyramid of the headline plane (6 levels of 2x2 box means);
+    # algorithmic bytes = every level read once + every lower level written once
+    pid = svc.register_plane(5, 0, 0, 0, pbx.UINT16, side, side, generator="noise", plane_no=rank)
+    _, pms = svc.build_pyramid(pid, 6, timing=True)
+    pb, wl = 0, side
+    for _ in range(6):
+        pb += 2 * wl * wl + 2 * ((wl + 1) // 2) ** 2
+        wl = (wl + 1) // 2
+    out["pyramid_6_levels_32768sq_u16"] = {
+        "kernel_ms": round(pms, 3), "alg_bytes": pb,
+        "gbps": round(pb / (pms * 1e-3) / 1e9, 1),
+        "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
     # G_FAKE (FakeReader-like gradient) PNG, compressible data
     svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
     fk = grid_ctxs(2, "png")

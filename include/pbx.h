@@ -114,8 +114,10 @@ int pbx_plane_release(pbx_ctx* ctx, uint64_t plane_id);
  * the 2x2 box mean of the one above (sizes rounded up; the last column / row repeated for odd
  * sizes; integers (sum + 2) >> 2 on the exact sum, arithmetic for signed types; float/double
  * ((a + b) + (c + d)) * 0.25), in the plane's byte order.  ids[k] = the plane id of level
- * r+1+k (ids may be NULL).  Tiles of a level are served with pbx_tile_req.resolution. */
-int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t plane_id, int32_t levels, uint64_t* ids);
+ * r+1+k (ids may be NULL).  Tiles of a level are served with pbx_tile_req.resolution.
+ * kernel_ms (may be NULL): device time of the downsampling kernels (HIP events). */
+int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t plane_id, int32_t levels, uint64_t* ids,
+                            double* kernel_ms);
 /* Copy a registered plane back to the host, samples in big-endian order (test hook). */
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
 

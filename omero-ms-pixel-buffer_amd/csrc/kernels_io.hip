@@ -42,8 +42,7 @@ __global__ __launch_bounds__(256) void k_gen_plane(uint8_t* __restrict__ out, in
 // selects, TileRequestHandler.java:89-91): out(x, y) = mean of in(2x..2x+1, 2y..2y+1), the
 // last column / row repeated when the input size is odd.  Integers: (sum + 2) >> 2 on the
 // exact 64-bit sum (arithmetic shift for signed types: floor((sum + 2) / 4)); float/double:
-// ((a + b) + (c + d)) * 0.25 in the sample's precision.  One thread per output sample; a
-// horizontal pair of input samples is one aligned 2*bpp-byte load (rows are 256-aligned).
+// ((a + b) + (c + d)) * 0.25 in the sample's precision.
 template <class T>
 __device__ __forceinline__ T ds_swap(T v, bool be) {
     if constexpr (sizeof(T) == 1) {
@@ -69,36 +68,52 @@ __device__ __forceinline__ T ds_mean4(T a, T b, T c, T d) {
     }
 }
 
+// One level: a thread makes N = 8 / sizeof(T) output samples of a row from one aligned
+// 16-byte load per input row (input rows are 256-aligned, so group g starts at byte 16 g) and
+// stores them as one 8-byte word; the last, partial group of a row goes sample by sample.
 template <class T>
 __global__ __launch_bounds__(256) void k_downsample(const uint8_t* __restrict__ src, int64_t spitch,
                                                     int32_t sx, int32_t sy, uint8_t* __restrict__ dst,
                                                     int64_t dpitch, int32_t dx, int32_t dy, bool be) {
-    const uint64_t total = (uint64_t)dx * (uint64_t)dy;
+    constexpr int N = 8 / sizeof(T);
+    const uint64_t ngx = ((uint64_t)dx + N - 1) / N, total = ngx * (uint64_t)dy;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-        const int32_t y = (int32_t)(i / (uint64_t)dx), x = (int32_t)(i - (uint64_t)y * dx);
+        const int32_t y = (int32_t)(i / ngx), g = (int32_t)(i - (uint64_t)y * ngx), x0 = g * N;
         const int32_t y0 = 2 * y, y1 = 2 * y + 1 < sy ? 2 * y + 1 : sy - 1;
-        const bool pair = 2 * x + 1 < sx;
-        const T* r0 = (const T*)(src + (int64_t)y0 * spitch) + 2 * x;
-        const T* r1 = (const T*)(src + (int64_t)y1 * spitch) + 2 * x;
-        T a, b, c, d;
-        if (pair) {
-            using P = HIP_vector_type<T, 2>;
-            const P p0 = *(const P*)r0, p1 = *(const P*)r1;
-            a = p0.x; b = p0.y; c = p1.x; d = p1.y;
+        const uint8_t* r0 = src + (int64_t)y0 * spitch;
+        const uint8_t* r1 = src + (int64_t)y1 * spitch;
+        T* out = (T*)(dst + (int64_t)y * dpitch) + x0;
+        if (2 * x0 + 2 * N <= sx) {
+            const uint4 va = gload16(r0 + 16 * g), vb = gload16(r1 + 16 * g);
+            T a[2 * N], b[2 * N], m[N];
+            __builtin_memcpy(a, &va, 16);
+            __builtin_memcpy(b, &vb, 16);
+#pragma unroll
+            for (int j = 0; j < N; j++)
+                m[j] = ds_swap(ds_mean4(ds_swap(a[2 * j], be), ds_swap(a[2 * j + 1], be),
+                                        ds_swap(b[2 * j], be), ds_swap(b[2 * j + 1], be)), be);
+            uint2 w;
+            __builtin_memcpy(&w, m, 8);
+            *(uint2*)out = w;
         } else {
-            a = b = r0[0];
-            c = d = r1[0];
+            for (int32_t j = 0; j < N && x0 + j < dx; j++) {
+                const int32_t xa = 2 * (x0 + j), xb = xa + 1 < sx ? xa + 1 : sx - 1;
+                const T* p0 = (const T*)r0;
+                const T* p1 = (const T*)r1;
+                out[j] = ds_swap(ds_mean4(ds_swap(p0[xa], be), ds_swap(p0[xb], be), ds_swap(p1[xa], be),
+                                          ds_swap(p1[xb], be)), be);
+            }
         }
-        const T m = ds_mean4(ds_swap(a, be), ds_swap(b, be), ds_swap(c, be), ds_swap(d, be));
-        ((T*)(dst + (int64_t)y * dpitch))[x] = ds_swap(m, be);
     }
 }
 
 hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch, int32_t sx, int32_t sy,
                              uint8_t* dst, int64_t dpitch, int32_t dx, int32_t dy, int32_t pixel_type,
                              bool be) {
-    const uint64_t total = (uint64_t)dx * (uint64_t)dy;
+    static const int bpps[PT_N] = {1, 1, 2, 2, 4, 4, 4, 8};
+    const uint64_t n = 8 / bpps[pixel_type];
+    const uint64_t total = ((uint64_t)dx + n - 1) / n * (uint64_t)dy;
     uint64_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     if (!blocks) return hipSuccess;

@@ -591,7 +591,7 @@ int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id
     return PBX_OK;
 }
 
-int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t* ids) {
+int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t* ids, double* kernel_ms) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     if (levels < 1 || levels > 30) return fail(PBX_E_BADARG, "bad level count %d", levels);
     Plane src;
@@ -612,24 +612,55 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
         return code;
     };
     Plane prev = src;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (kernel_ms) {
+        HIP_TRY(hipEventCreate(&ev0));
+        HIP_TRY(hipEventCreate(&ev1));
+    }
+    auto fin_events = [&]() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    };
     for (int32_t k = 1; k <= levels; k++) {
         Plane p = prev;
-        p.res = src.res + k;
         p.size_x = (prev.size_x + 1) / 2;
         p.size_y = (prev.size_y + 1) / 2;
         p.pitch = ((int64_t)p.size_x * bpp + 255) & ~(int64_t)255;
         p.bytes = (size_t)p.pitch * p.size_y + 256;
         hipError_t e = hipMalloc((void**)&p.dev, p.bytes);
-        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
+        if (e != hipSuccess) {
+            fin_events();
+            return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
+        }
+        p.res = src.res + k;
         made.push_back(p);
-        e = launch_downsample(ctx->stream, prev.dev, prev.pitch, prev.size_x, prev.size_y, p.dev, p.pitch,
-                              p.size_x, p.size_y, p.pixel_type, !p.little_endian && bpp > 1);
-        if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * p.size_y, 0, 256, ctx->stream);
-        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
         prev = p;
     }
+    if (ev0) HIP_TRY(hipEventRecord(ev0, ctx->stream));
+    prev = src;
+    for (int32_t k = 1; k <= levels; k++) {
+        const Plane& p = made[k - 1];
+        hipError_t e = launch_downsample(ctx->stream, prev.dev, prev.pitch, prev.size_x, prev.size_y, p.dev, p.pitch,
+                              p.size_x, p.size_y, p.pixel_type, !p.little_endian && bpp > 1);
+        if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * p.size_y, 0, 256, ctx->stream);
+        if (e != hipSuccess) {
+            fin_events();
+            return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
+        }
+        prev = p;
+    }
+    if (ev1) HIP_TRY(hipEventRecord(ev1, ctx->stream));
     const hipError_t e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
+    if (e != hipSuccess) {
+        fin_events();
+        return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
+    }
+    if (kernel_ms) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev0, ev1);
+        *kernel_ms = ms;
+    }
+    fin_events();
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     for (size_t k = 0; k < made.size(); k++) {
         Plane& p = made[k];

@@ -120,7 +120,8 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
-    L.pbx_plane_build_pyramid.argtypes = [vp, u64, i32, ctypes.POINTER(u64)]
+    L.pbx_plane_build_pyramid.argtypes = [vp, u64, i32, ctypes.POINTER(u64),
+                                          ctypes.POINTER(ctypes.c_double)]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
     L.pbx_test_batch_lz77.argtypes = [vp, vp, vp, vp, u64]
     L.pbx_ctx_stats_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
@@ -338,12 +339,14 @@ class PixelsService:
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))
 
-    def build_pyramid(self, plane_id: int, levels: int) -> List[int]:
+    def build_pyramid(self, plane_id: int, levels: int, timing: bool = False):
         """Resolution levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
-        returns their plane ids.  Tiles of level k: TileCtx(..., resolution=k)."""
+        returns their plane ids (and the kernels' device ms with timing=True).  Tiles of
+        level k: TileCtx(..., resolution=k)."""
         ids = (ctypes.c_uint64 * max(levels, 1))()
-        _check(lib().pbx_plane_build_pyramid(self._h, plane_id, levels, ids))
-        return list(ids)[:levels]
+        ms = ctypes.c_double(0.0)
+        _check(lib().pbx_plane_build_pyramid(self._h, plane_id, levels, ids, ctypes.byref(ms)))
+        return (list(ids)[:levels], ms.value) if timing else list(ids)[:levels]
 
     def read_plane_be(self, plane_id: int, nbytes: int) -> bytes:
         buf = ctypes.create_string_buffer(nbytes)
