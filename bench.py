@@ -141,6 +141,62 @@ def cpu_baseline(seconds=10.0, threads=16):
                       f"{sec:.1f} s; avg {nbytes / n:.0f} B/tile"}
 
 
+def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    import _zarr
+    pid = svc.register_plane(20, 0, 0, 0, pbx.UINT16, side, side, generator="noise", plane_no=rank)
+    plane = np.frombuffer(svc.read_plane_be(pid, side * side * 2), ">u2").reshape(side, side)
+    svc.release_plane(pid)
+    grid = _zarr.chunk_grid(plane, chunk, chunk)
+    res = {}
+    for name, comp, kw in (("blosc_lz4", "blosc", {}), ("zlib1", "zlib", {"level": 1})):
+        with ThreadPoolExecutor(16) as ex:
+            if comp == "blosc":
+                chunks = list(ex.map(lambda c: _zarr.blosc_encode(c.tobytes(), 2), grid))
+            else:
+                chunks = list(ex.map(lambda c: _zarr.zlib_encode(c.tobytes(), 1), grid))
+        cbytes = sum(len(c) for c in chunks)
+        dec, plc, wall = [], [], []
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            pid, (md, mp) = svc.register_zarr_plane(21, 0, 0, 0, pbx.UINT16, side, side, chunk, chunk,
+                                                    comp, chunks, timing=True)
+            t1 = time.perf_counter()
+            if r:
+                dec.append(md)
+                plc.append(mp)
+                wall.append(t1 - t0)
+            svc.release_plane(pid)
+        raw = side * side * 2
+        md, mp = sum(dec) / reps, sum(plc) / reps
+        line = {"chunks": len(chunks), "compressed_bytes": cbytes, "decoded_bytes": raw,
+                "decode_ms": round(md, 3), "place_ms": round(mp, 3),
+                "decoded_gbps": round(raw / ((md + mp) * 1e-3) / 1e9, 1),
+                "chunks_per_s": round(len(chunks) * world / ((md + mp) * 1e-3), 1),
+                "decode_alg_gbps": round((cbytes + raw) / (md * 1e-3) / 1e9, 1),
+                "place_gbps": round(2 * raw / (mp * 1e-3) / 1e9, 1),
+                "register_wall_ms_incl_upload": round(1e3 * sum(wall) / reps, 1)}
+        if rank == 0 and world == 1:
+            import _oracle as O
+            L = O.lib()
+            import ctypes
+            L.pbxo_zarr_bench.restype = ctypes.c_double
+            L.pbxo_zarr_bench.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p,
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+            n = 256  # bounded sample: a quarter of the chunks
+            sub = chunks[:n]
+            offs = np.concatenate([[0], np.cumsum([len(c) for c in sub])]).astype(np.uint64)
+            sec = L.pbxo_zarr_bench({"blosc": 1, "zlib": 2}[comp], b"".join(sub), offs.ctypes.data,
+                                    n, chunk * chunk * 2, 16)
+            line["cpu_baseline"] = {"value": round(n * chunk * chunk * 2 / sec / 1e9, 2), "unit": "GB/s",
+                                    "chunks_per_s": round(n / sec, 1), "cores": 16, "kind": "port",
+                                    "sample": f"{n} of the same chunks, oracle/zarr_oracle.c "
+                                              f"(c-blosc frame restatement / zlib 1.2.11) on 16 threads"}
+        res[name] = line
+    return res
+
+
 def extra(out, svc, rank, world, barrier, iid, side):
     """Secondary lines: the other BASELINE configs (parity-tested in tests/), each timed
     device-resident like the headline; and the PCIe-inclusive end-to-end rate."""
@@ -178,6 +234,11 @@ def extra(out, svc, rank, world, barrier, iid, side):
         "kernel_ms": round(pms, 3), "alg_bytes": pb,
         "gbps": round(pb / (pms * 1e-3) / 1e9, 1),
         "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    # Row f2: NGFF/Zarr chunk decode into HBM (pbx_plane_register_zarr) of a 16384^2 uint16
+    # G_NOISE plane stored as 512^2 chunks (1,024 chunks); blosc-lz4 (shuffle, the NGFF
+    # writers' default) and zlib-1.  Timed: the decode kernels and the placement kernel
+    # (HIP events); the chunk upload is PCIe and reported apart.
+    out["zarr_decode_16384sq_u16_512chunks"] = zarr_lines(svc, rank, world)
     # G_FAKE (FakeReader-like gradient) PNG, compressible data
     svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
     fk = grid_ctxs(2, "png")

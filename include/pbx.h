@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 2
+#define PBX_ABI_VERSION 3
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -118,6 +118,33 @@ int pbx_plane_release(pbx_ctx* ctx, uint64_t plane_id);
  * kernel_ms (may be NULL): device time of the downsampling kernels (HIP events). */
 int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t plane_id, int32_t levels, uint64_t* ids,
                             double* kernel_ms);
+/* NGFF / Zarr v2 planes: the reference's pixels service is ZarrPixelsService
+ * (PixelBufferVerticle.java:29,56; beanRefContext.xml:51; config.yaml:18), which reads Zarr
+ * chunks through omero-zarr-pixel-buffer 0.6.1 / JZarr (build.gradle:57) on every
+ * getTileDirect.  Here the chunks of one (z, c, t, resolution) plane are uploaded once and
+ * decoded on the GPU (one wave per compressed stream) straight into a resident HBM plane,
+ * which then serves tiles like any registered plane.  Codec = the .zarray "compressor":
+ * null, blosc (c-blosc 1.x frames: lz4 / lz4hc / zlib, byte shuffle or none, split or not),
+ * zlib.  Other blosc codecs (blosclz, zstd, snappy, bit shuffle) and blosc2 frames -> 400. */
+enum pbx_zarr_codec { PBX_ZARR_RAW = 0, PBX_ZARR_BLOSC = 1, PBX_ZARR_ZLIB = 2 };
+
+typedef struct pbx_zarr_chunks {
+    int32_t chunk_x, chunk_y;   /* .zarray "chunks" (the x and y extents; edge chunks are full) */
+    int32_t codec;              /* enum pbx_zarr_codec */
+    int32_t reserved;
+    const uint8_t* data;        /* the chunk files concatenated, C order over the chunk grid */
+    const uint64_t* offsets;    /* gx*gy + 1 entries (gx = ceil(size_x/chunk_x), ...); chunk
+                                   i = cy*gx + cx is data[offsets[i] .. offsets[i+1]); an empty
+                                   range is a missing chunk (every sample = fill) */
+    uint64_t fill_bits;         /* .zarray fill_value as the sample's bit pattern */
+} pbx_zarr_chunks;
+
+/* desc: image/z/c/t/resolution/pixel_type/size as pbx_plane_register; byte_order = the
+ * .zarray dtype's ('<' little, '>' / '|' big); source/host_data are ignored.
+ * kernel_ms (may be NULL): [0] device ms of the decode kernels, [1] of the placement kernel.
+ * A malformed or unsupported chunk fails the whole plane with 400 (nothing registered). */
+int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* desc, const pbx_zarr_chunks* chunks,
+                            uint64_t* plane_id, double* kernel_ms);
 /* Copy a registered plane back to the host, samples in big-endian order (test hook). */
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
 

@@ -1,0 +1,524 @@
+// kernels_zarr.hip — NGFF/Zarr v2 chunk decode into a resident HBM plane:
+// the step before getTileDirect when the reference's pixels service is ZarrPixelsService
+// (PixelBufferVerticle.java:29,56; beanRefContext.xml:51; omero-zarr-pixel-buffer 0.6.1,
+// build.gradle:57).  Chunk formats are restated in oracle/zarr_oracle.c.
+//
+//   k_zarr_lz4      one wave per compressed stream (a blosc split): LZ4 block decode
+//   k_zarr_inflate  one wave per zlib stream (Zarr "zlib" chunks, blosc-zlib splits)
+//   k_zarr_copy     one wave per stored stream (blosc splits kept raw)
+//   k_zarr_place    per chunk rows: blosc byte-unshuffle + placement into the pitched plane,
+//                   fill value for missing chunks
+//
+// Decoders keep the wave's last ZR output bytes in an LDS ring (the match source for every
+// distance <= ZR) and flush completed 64-byte lines to HBM, so a match never waits on the
+// wave's own global stores; a longer distance reads HBM after a workgroup fence (rare for
+// image chunks: rows are at most a few KB apart).  Sequence/Huffman parsing is wave-uniform:
+// the input is held as a 256-byte window, one dword per lane, read with readlane; a Huffman
+// symbol is decoded by lanes 0..14 testing the 15 code lengths at once (canonical ranges),
+// one ballot picks the length.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dev_util.h"
+#include "pbx_common.h"
+#include "pbx_kernels.h"
+
+namespace pbx {
+
+constexpr uint32_t ZR = 8192, ZM = ZR - 1;  // LDS output ring per wave
+constexpr uint32_t ZWAVES = 4;              // waves per workgroup
+
+// Dynamic LDS of the decoders, addressed by offset (a pointer into LDS kept in a struct would
+// become a FLAT pointer; a selected one, a stack slot).  Per wave: ring, then (inflate) tables.
+extern __shared__ uint8_t zlds[];
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Input window of ZWIN bytes in LDS (wave-uniform reads are LDS reads: a VGPR window would
+// put an s_waitcnt vmcnt(0) -- which on gfx9 also waits for every pending flush store --
+// in front of each use).  Reloaded by one 16-byte load per lane.  The device source buffer
+// has ZSLACK bytes after its last stream, so window loads never leave the allocation.
+constexpr uint32_t ZWIN = 1024;  // the runtime leaves 4 KiB of slack after the streams
+
+struct InWin {
+    const uint8_t* in;
+    uint32_t wo, base, lane;  // LDS offset of the window, stream offset it starts at
+    __device__ void load(uint32_t q) {
+        base = q;
+        uint4 v;
+        __builtin_memcpy(&v, in + q + 16 * lane, 16);
+        *(uint4*)(zlds + wo + 16 * lane) = v;
+    }
+    __device__ uint32_t byte(uint32_t q) {
+        if (q - base > ZWIN - 1) load(q);
+        return rfl(zlds[wo + q - base]);
+    }
+    // 32 bits starting at byte q (little-endian)
+    __device__ uint32_t dword(uint32_t q) {
+        if (q - base > ZWIN - 4) load(q);
+        const uint32_t r = wo + q - base;
+        return rfl((uint32_t)zlds[r] | (uint32_t)zlds[r + 1] << 8 | (uint32_t)zlds[r + 2] << 16 |
+                   (uint32_t)zlds[r + 3] << 24);
+    }
+    // byte q + lane for every lane
+    __device__ uint32_t lane_byte(uint32_t q) {
+        if (q - base > ZWIN - 64) load(q);
+        return zlds[wo + q - base + lane];
+    }
+};
+
+// Output through the LDS ring (offset rb, 256-aligned); bytes [flushed, op) are in the ring
+// only.  Completed 256-byte runs go to HBM as one dword store per lane.
+struct OutRing {
+    uint32_t rb;
+    uint8_t* out;
+    uint32_t op, flushed, olen, lane;
+    __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
+    __device__ void flush(uint32_t upto) {
+        while (upto - flushed >= 256u) {
+            const uint32_t v = *(const uint32_t*)(zlds + rb + ((flushed + 4 * lane) & ZM));
+            __builtin_memcpy(out + flushed + 4 * lane, &v, 4);
+            flushed += 256;
+        }
+    }
+    __device__ void finish() {
+        for (uint32_t k = flushed; k < op; k += 64)
+            if (k + lane < op) out[k + lane] = ring(k + lane);
+        flushed = op;
+    }
+    // out[op .. op+len) = out[op-off .. op-off+len) (overlapping: period off)
+    __device__ bool match(uint32_t off, uint32_t len) {
+        if (off == 0 || off > op || len > olen - op) return false;
+        const uint32_t rep = off < 64 ? lane % off : lane;
+        if (off > ZR) {
+            // a far source lies below `flushed`: wait for this wave's stores, read HBM
+            for (uint32_t k = 0; k < len; k += 64) {
+                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                const uint32_t v = *(const __attribute__((address_space(1))) uint8_t*)(out + p - off + rep);
+                if (lane < n) ring(p + lane) = (uint8_t)v;
+                flush(p + n);
+            }
+        } else {
+            for (uint32_t k = 0; k < len; k += 64) {
+                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
+                const uint32_t v = ring(p - off + rep);
+                if (lane < n) ring(p + lane) = (uint8_t)v;
+                flush(p + n);
+            }
+        }
+        op += len;
+        return true;
+    }
+    __device__ void put1(uint32_t v) {
+        if (lane == 0) ring(op) = (uint8_t)v;
+        op++;
+        flush(op);
+    }
+};
+
+// ------------------------------------------------------------------------------ LZ4
+__global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st, uint32_t n,
+                                                  const uint8_t* __restrict__ src,
+                                                  uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t si = blockIdx.x * ZWAVES + w;
+    if (si >= n) return;
+    const ZStream t = st[si];
+    const uint32_t ilen = rfl(t.csize);
+    const uint32_t wb = w * (ZR + ZWIN);
+    InWin win{src + t.src_off, wb + ZR, 0, lane};
+    win.load(0);
+    OutRing o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+    uint32_t ip = 0, bad = 0;
+    for (;;) {
+        if (ip >= ilen) { bad = 1; break; }
+        const uint32_t tok = win.byte(ip++);
+        uint32_t ll = tok >> 4;
+        if (ll == 15) {
+            uint32_t b;
+            do {
+                if (ip >= ilen) { bad = 2; break; }
+                b = win.byte(ip++);
+                ll += b;
+            } while (b == 255);
+            if (bad) break;
+        }
+        if (ll > ilen - ip || ll > o.olen - o.op) { bad = 3; break; }
+        for (uint32_t k = 0; k < ll; k += 64) {
+            const uint32_t q = ip + k, nb = ll - k < 64 ? ll - k : 64;
+            const uint32_t v = win.lane_byte(q);
+            if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+            o.flush(o.op + k + nb);
+        }
+        ip += ll;
+        o.op += ll;
+        if (ip == ilen) break;
+        if (ilen - ip < 2) { bad = 4; break; }
+        const uint32_t off = win.byte(ip) | win.byte(ip + 1) << 8;
+        ip += 2;
+        uint32_t ml = tok & 15;
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                if (ip >= ilen) { bad = 5; break; }
+                b = win.byte(ip++);
+                ml += b;
+            } while (b == 255);
+            if (bad) break;
+        }
+        if (!o.match(off, ml + 4)) { bad = 6; break; }
+    }
+    if (!bad && o.op != o.olen) bad = 7;
+    o.finish();
+    if (lane == 0) err[si] = bad;
+}
+
+// ---------------------------------------------------------------------------- inflate
+// Canonical Huffman table held by lanes 1..15 (code length L = lane + 1 for lane < 15):
+// first code, count and the index of its first symbol in the sorted symbol list.
+struct HTab {
+    uint32_t first, count, offs;
+    uint32_t syms;  // LDS byte offset of the sorted symbol list (uint16)
+};
+__device__ __forceinline__ uint16_t& lds16(uint32_t byte_off) {
+    return *(uint16_t*)(zlds + byte_off);
+}
+__device__ __forceinline__ uint32_t& lds32(uint32_t byte_off) {
+    return *(uint32_t*)(zlds + byte_off);
+}
+
+struct BitIn {
+    InWin win;
+    uint64_t buf;
+    uint32_t cnt, ipos, ilen;
+    __device__ void refill() {
+        if (cnt <= 32) {
+            // past the stream's end (corrupt input) feed zeros instead of reading on: the
+            // decoder stops at the output bound and the consumed-bytes check fails the stream
+            if (ipos <= ilen + 8) buf |= (uint64_t)win.dword(ipos) << cnt;
+            cnt += 32;
+            ipos += 4;
+        }
+    }
+    __device__ uint32_t bits(uint32_t k) {  // k <= 32 - (bits guaranteed by a refill)
+        const uint32_t v = (uint32_t)buf & ((k == 32) ? 0xffffffffu : ((1u << k) - 1u));
+        buf >>= k;
+        cnt -= k;
+        return v;
+    }
+    __device__ uint32_t consumed_bytes() const { return ipos - cnt / 8; }
+};
+
+// Build the table of n code lengths lens[0..n) (LDS); returns false if over-subscribed.
+__device__ bool build_table(HTab& h, uint32_t lens /* LDS offset */, uint32_t n, uint32_t lane,
+                            uint32_t next /* LDS offset of 16 counters */) {
+    const uint32_t L = lane + 1;
+    uint32_t cnt = 0;
+    if (L <= 15)
+        for (uint32_t s = 0; s < n; s++) cnt += zlds[lens + s] == L;
+    // first code of length L: code = (code + count[L-1]) << 1 from L = 1; offs = sum count[<L]
+    uint32_t code = 0, off = 0, left = 1;
+    bool over = false;
+    for (uint32_t l = 1; l <= 15; l++) {
+        const uint32_t c = rdl(cnt, l - 1);
+        left = (left << 1);
+        if (c > left) over = true;
+        left -= c > left ? left : c;
+        if (l == L) { h.first = code; h.offs = off; }
+        code = (code + c) << 1;
+        off += c;
+    }
+    h.count = L <= 15 ? cnt : 0;
+    if (L > 15) { h.first = 0; h.offs = 0; }
+    if (lane < 16) lds32(next + 4 * lane) = 0;
+    __builtin_amdgcn_wave_barrier();
+    // sorted symbol list: rank of s among the symbols of its length, in symbol order
+    for (uint32_t g = 0; g < n; g += 64) {
+        const uint32_t s = g + lane;
+        const uint32_t ln = s < n ? zlds[lens + s] : 0;
+        const uint64_t lt = (lane ? (~0ull >> (64 - lane)) : 0ull);
+        for (uint32_t l = 1; l <= 15; l++) {
+            const uint64_t m = __ballot(ln == l);
+            if (!m) continue;
+            const uint32_t base = lds32(next + 4 * l);
+            if (ln == l) lds16(h.syms + 2 * (rdl(h.offs, l - 1) + base + __popcll(m & lt))) = (uint16_t)s;
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) lds32(next + 4 * l) = base + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return !over;
+}
+
+// Decode one symbol (the bit buffer holds >= 15 bits); returns -1 on an invalid code.
+__device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
+    const uint32_t rev = __builtin_bitreverse32((uint32_t)bi.buf & 0x7fffu) >> 17;  // 15 bits, MSB-first
+    const uint32_t L = lane + 1;
+    const uint32_t code = L <= 15 ? rev >> (15 - L) : 0;
+    const bool ok = L <= 15 && (code - h.first) < h.count;
+    const uint64_t m = __ballot(ok);
+    if (!m) return -1;
+    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+    const uint32_t idx = rdl(h.offs + code - h.first, l);
+    bi.bits(l + 1);
+    return lds16(h.syms + 2 * idx);
+}
+
+__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
+                                   3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                     193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097,
+                                     6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                   6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+constexpr uint32_t ZLENS = 352;
+
+// Per-wave LDS of k_zarr_inflate (byte offsets from the wave's base)
+constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR, ZI_DSYMS = ZI_LSYMS + 2 * 288,
+                   ZI_LENS = ZI_DSYMS + 2 * 32, ZI_NEXT = ZI_LENS + ZLENS, ZI_BYTES = ZI_NEXT + 64;
+
+__global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict__ st, uint32_t n,
+                                                      const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t si = blockIdx.x * ZWAVES + w;
+    if (si >= n) return;
+    const uint32_t wb = w * (ZI_BYTES + ZWIN);
+    const uint32_t LENS = wb + ZI_LENS, NEXT = wb + ZI_NEXT;
+    const ZStream t = st[si];
+    BitIn bi{{src + t.src_off, wb + ZI_BYTES, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
+    bi.win.load(0);
+    OutRing o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
+    HTab lt{0, 0, 0, wb + ZI_LSYMS}, dt{0, 0, 0, wb + ZI_DSYMS};
+    uint32_t bad = 0;
+    bi.refill();
+    if (t.kind == ZS_ZLIB) {  // RFC 1950 header: CM = 8, CINFO <= 7, no preset dictionary
+        const uint32_t cmf = bi.bits(8), flg = bi.bits(8);
+        if ((cmf & 15) != 8 || (cmf >> 4) > 7 || (flg & 0x20) || ((cmf << 8) | flg) % 31) bad = 10;
+    }
+    uint32_t final = 0;
+    while (!bad && !final) {
+        bi.refill();
+        final = bi.bits(1);
+        const uint32_t type = bi.bits(2);
+        if (type == 0) {  // stored
+            bi.bits(bi.cnt & 7);
+            bi.refill();
+            const uint32_t len = bi.bits(16), nlen = bi.bits(16);
+            if ((len ^ 0xffffu) != nlen) { bad = 11; break; }
+            // the remaining whole bytes of the bit buffer come first
+            uint32_t done = 0;
+            while (done < len && bi.cnt >= 8 && o.op < o.olen) { o.put1(bi.bits(8)); done++; }
+            if (done < len && bi.cnt >= 8) { bad = 12; break; }
+            const uint32_t q = bi.ipos, rest = len - done;
+            if (q + rest > bi.ilen || rest > o.olen - o.op) { bad = 12; break; }
+            for (uint32_t k = 0; k < rest; k += 64) {
+                const uint32_t nb = rest - k < 64 ? rest - k : 64;
+                const uint32_t v = bi.win.lane_byte(q + k);
+                if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+                o.flush(o.op + k + nb);
+            }
+            o.op += rest;
+            bi.ipos = q + rest;
+            bi.buf = 0;
+            bi.cnt = 0;
+            continue;
+        }
+        if (type == 3) { bad = 13; break; }
+        if (type == 1) {  // fixed codes
+            for (uint32_t s = lane; s < 320; s += 64)
+                zlds[LENS + s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+            __builtin_amdgcn_wave_barrier();
+            build_table(lt, LENS, 288, lane, NEXT);
+            build_table(dt, LENS + 288, 30, lane, NEXT);
+        } else {  // dynamic
+            bi.refill();
+            const uint32_t hlit = bi.bits(5) + 257, hdist = bi.bits(5) + 1, hclen = bi.bits(4) + 4;
+            if (hlit > 286 || hdist > 30) { bad = 14; break; }
+            for (uint32_t s = lane; s < 19; s += 64) zlds[LENS + s] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t k = 0; k < hclen; k++) {
+                bi.refill();
+                const uint32_t v = bi.bits(3);
+                if (lane == 0) zlds[LENS + c_clord[k]] = (uint8_t)v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            HTab ct{0, 0, 0, wb + ZI_LSYMS};
+            if (!build_table(ct, LENS, 19, lane, NEXT)) { bad = 15; break; }
+            // code lengths for litlen + dist go to lens[19..] first, then move down
+            uint32_t k = 0, prev = 0;
+            while (k < hlit + hdist) {
+                bi.refill();
+                const int sym = decode_sym(ct, bi, lane);
+                if (sym < 0) { bad = 16; break; }
+                uint32_t rep = 1, val = (uint32_t)sym;
+                if (sym == 16) {
+                    if (k == 0) { bad = 17; break; }
+                    rep = 3 + bi.bits(2); val = prev;
+                } else if (sym == 17) { rep = 3 + bi.bits(3); val = 0; }
+                else if (sym == 18) { rep = 11 + bi.bits(7); val = 0; }
+                if (k + rep > hlit + hdist) { bad = 18; break; }
+                for (uint32_t r = lane; r < rep; r += 64) zlds[LENS + 19 + k + r] = (uint8_t)val;
+                __builtin_amdgcn_wave_barrier();
+                k += rep;
+                prev = val;
+            }
+            if (bad) break;
+            for (uint32_t s = lane; s < 320; s += 64) {
+                const uint8_t v = s < hlit + hdist ? zlds[LENS + 19 + s] : 0;
+                __builtin_amdgcn_wave_barrier();
+                zlds[LENS + s] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            // litlen = lens[0..hlit) zero-padded to 288; dist lengths moved to lens[288..320)
+            {
+                const uint8_t dv = lane < hdist ? zlds[LENS + hlit + lane] : 0;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t s = hlit + lane; s < ZLENS; s += 64) zlds[LENS + s] = 0;
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 32) zlds[LENS + 288 + lane] = dv;
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (!build_table(lt, LENS, 288, lane, NEXT)) { bad = 19; break; }
+            if (!build_table(dt, LENS + 288, 30, lane, NEXT)) { bad = 20; break; }
+        }
+        // block data
+        for (;;) {
+            bi.refill();
+            const int sym = decode_sym(lt, bi, lane);
+            if (sym < 0) { bad = 21; break; }
+            if (sym < 256) {
+                if (o.op >= o.olen) { bad = 22; break; }
+                o.put1((uint32_t)sym);
+                continue;
+            }
+            if (sym == 256) break;
+            const uint32_t ls = (uint32_t)sym - 257;
+            if (ls >= 29) { bad = 23; break; }
+            bi.refill();
+            const uint32_t len = c_lbase[ls] + bi.bits(c_lext[ls]);
+            bi.refill();
+            const int ds = decode_sym(dt, bi, lane);
+            if (ds < 0 || ds >= 30) { bad = 24; break; }
+            bi.refill();
+            const uint32_t dist = c_dbase[ds] + bi.bits(c_dext[ds]);
+            if (!o.match(dist, len)) { bad = 25; break; }
+        }
+        if (!bad && bi.consumed_bytes() > bi.ilen) bad = 26;
+    }
+    if (!bad && o.op != o.olen) bad = 27;
+    o.finish();
+    if (lane == 0) err[si] = bad;
+}
+
+// ------------------------------------------------------------------------------ stored
+__global__ __launch_bounds__(256) void k_zarr_copy(const ZStream* __restrict__ st, uint32_t n,
+                                                   const uint8_t* __restrict__ src,
+                                                   uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t si = blockIdx.x * ZWAVES + w;
+    if (si >= n) return;
+    const ZStream t = st[si];
+    const uint8_t* in = src + t.src_off;
+    uint8_t* out = dst + t.dst_off;
+    const uint32_t len = t.dlen;
+    uint32_t k = 0;
+    if ((((uintptr_t)out) & 3) == 0)
+        for (; k + 256 <= len; k += 256) {
+            const uint32_t v = ld_u32_unaligned(in + k + 4 * lane);
+            *(uint32_t*)(out + k + 4 * lane) = v;
+        }
+    for (; k < len; k += 64)
+        if (k + lane < len) out[k + lane] = in[k + lane];
+    if (lane == 0) err[si] = t.csize < t.dlen ? 30u : 0u;
+}
+
+// ------------------------------------------------------------------------------- place
+// One workgroup per (chunk, band of ZP_ROWS chunk rows).  Each thread makes one sample:
+// blosc byte-unshuffle (typesize ts within blocks of `blocksize` bytes) + copy into the
+// plane (samples stay in the array's byte order); missing chunks get the fill bytes.
+constexpr uint32_t ZP_ROWS = 8;
+
+__global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ ch, uint32_t bands,
+                                                    const uint8_t* __restrict__ scratch,
+                                                    const uint8_t* __restrict__ input,
+                                                    uint8_t* __restrict__ plane, int64_t pitch,
+                                                    int32_t sx, int32_t sy, int32_t cw, int32_t chh,
+                                                    uint32_t bpp, uint64_t fill) {
+    const ZChunk c = ch[blockIdx.x / bands];
+    const uint32_t band = blockIdx.x % bands;
+    const int32_t r0 = (int32_t)(band * ZP_ROWS);
+    const int32_t w = sx - c.x0 < cw ? sx - c.x0 : cw;
+    const int32_t h = sy - c.y0 < chh ? sy - c.y0 : chh;
+    const int32_t r1 = r0 + (int32_t)ZP_ROWS < h ? r0 + (int32_t)ZP_ROWS : h;
+    const uint8_t* s = (c.flags & ZC_INPUT ? input : scratch) + c.src;
+    const uint32_t ts = c.typesize, bs = c.blocksize, nb = c.nbytes;
+    for (int32_t r = r0; r < r1; r++) {
+        uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
+        for (int32_t col = (int32_t)threadIdx.x; col < w; col += 256) {
+            const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
+            for (uint32_t j = 0; j < bpp; j++) {
+                uint32_t v;
+                if (c.flags & ZC_MISSING) {
+                    v = (uint32_t)(fill >> (8 * j)) & 0xffu;
+                } else if (ts > 1) {
+                    const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
+                    const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
+                    const uint32_t ne = bsize / ts;
+                    const uint32_t pos = within < ne * ts ? blk * bs + (within % ts) * ne + within / ts : B;
+                    v = s[pos];
+                } else {
+                    v = s[e * bpp + j];
+                }
+                o[(int64_t)col * bpp + j] = (uint8_t)v;
+            }
+        }
+    }
+}
+
+hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t n_lz4,
+                              uint32_t n_infl, uint32_t n_copy, const uint8_t* src, uint8_t* scratch,
+                              uint32_t* err) {
+    // streams are ordered: lz4 first, then inflate, then copy
+    if (n_lz4)
+        hipLaunchKernelGGL(k_zarr_lz4, dim3((n_lz4 + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZR + ZWIN), st,
+                           d_streams, n_lz4, src, scratch, err);
+    if (n_infl)
+        hipLaunchKernelGGL(k_zarr_inflate, dim3((n_infl + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZI_BYTES + ZWIN), st,
+                           d_streams + n_lz4, n_infl, src, scratch, err + n_lz4);
+    if (n_copy)
+        hipLaunchKernelGGL(k_zarr_copy, dim3((n_copy + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), 0, st,
+                           d_streams + n_lz4 + n_infl, n_copy, src, scratch, err + n_lz4 + n_infl);
+    return hipGetLastError();
+}
+
+hipError_t launch_zarr_place(hipStream_t st, const ZChunk* d_chunks, uint32_t nchunks,
+                             const uint8_t* scratch, const uint8_t* input, uint8_t* plane,
+                             int64_t pitch, int32_t sx, int32_t sy, int32_t cw, int32_t chh,
+                             uint32_t bpp, uint64_t fill) {
+    const uint32_t bands = ((uint32_t)chh + ZP_ROWS - 1) / ZP_ROWS;
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_zarr_place, dim3(nchunks * bands), dim3(256), 0, st, d_chunks, bands,
+                       scratch, input, plane, pitch, sx, sy, cw, chh, bpp, fill);
+    return hipGetLastError();
+}
+
+}  // namespace pbx

@@ -62,4 +62,27 @@ size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
 hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* info,
                           const uint32_t* hist, uint32_t* codes);
 
+// NGFF/Zarr chunk decode (kernels_zarr.hip).  One wave per stream.
+enum : uint32_t { ZS_LZ4 = 0, ZS_ZLIB = 1, ZS_COPY = 2 };
+struct ZStream {
+    uint64_t src_off;  // compressed bytes in the uploaded chunk buffer
+    uint64_t dst_off;  // decoded bytes in the scratch buffer
+    uint32_t csize, dlen, kind, pad;
+};
+enum : uint32_t { ZC_MISSING = 1u, ZC_INPUT = 2u };
+struct ZChunk {
+    uint64_t src;                         // decoded chunk: scratch offset (or input offset if ZC_INPUT)
+    uint32_t nbytes, blocksize, typesize; // blosc geometry (typesize 1 = not shuffled)
+    uint32_t flags;                       // ZC_*
+    int32_t x0, y0;                       // chunk origin in the plane
+};
+// Streams ordered lz4 | inflate | copy; err[i] = 0 or a decoder error code per stream.
+hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t n_lz4,
+                              uint32_t n_infl, uint32_t n_copy, const uint8_t* src, uint8_t* scratch,
+                              uint32_t* err);
+hipError_t launch_zarr_place(hipStream_t st, const ZChunk* d_chunks, uint32_t nchunks,
+                             const uint8_t* scratch, const uint8_t* input, uint8_t* plane,
+                             int64_t pitch, int32_t sx, int32_t sy, int32_t cw, int32_t chh,
+                             uint32_t bpp, uint64_t fill);
+
 }  // namespace pbx

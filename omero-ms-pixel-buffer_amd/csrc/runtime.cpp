@@ -673,6 +673,238 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
     return PBX_OK;
 }
 
+// ------------------------------------------------------------------ NGFF / Zarr planes
+namespace {
+
+uint32_t rd_le32(const uint8_t* p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+// Host plan of one plane's chunks: metadata only (blosc headers, block starts and split
+// sizes); every byte of chunk data is decoded on the GPU.  Frame layout: oracle/zarr_oracle.c.
+struct ZarrPlan {
+    std::vector<ZStream> lz4, infl, copy;
+    std::vector<ZChunk> chunks;
+    uint64_t scratch = 0;
+};
+
+int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPlan& P) {
+    const int64_t gx = (d->size_x + z->chunk_x - 1) / z->chunk_x;
+    const int64_t gy = (d->size_y + z->chunk_y - 1) / z->chunk_y;
+    const uint64_t cb = (uint64_t)z->chunk_x * z->chunk_y * bpp;
+    if (cb > 0x7fffffffull) return fail(PBX_E_BADARG, "chunk of %llu bytes too large", (unsigned long long)cb);
+    const uint64_t total = z->offsets[gx * gy];
+    for (int64_t i = 0; i < gx * gy; i++) {
+        const uint64_t o = z->offsets[i], len = z->offsets[i + 1] - o;
+        if (z->offsets[i + 1] < o || z->offsets[i + 1] > total)
+            return fail(PBX_E_BADARG, "chunk %lld: bad offsets", (long long)i);
+        ZChunk c{};
+        c.x0 = (int32_t)((i % gx) * z->chunk_x);
+        c.y0 = (int32_t)((i / gx) * z->chunk_y);
+        c.nbytes = (uint32_t)cb;
+        c.blocksize = (uint32_t)cb;
+        c.typesize = 1;
+        if (len == 0) {
+            c.flags = ZC_MISSING;
+            P.chunks.push_back(c);
+            continue;
+        }
+        if (z->codec == PBX_ZARR_RAW) {
+            if (len < cb) return fail(PBX_E_BADARG, "chunk %lld: %llu bytes < %llu", (long long)i,
+                                      (unsigned long long)len, (unsigned long long)cb);
+            c.src = o;
+            c.flags = ZC_INPUT;
+            P.chunks.push_back(c);
+            continue;
+        }
+        const uint64_t dst = P.scratch;
+        if (z->codec == PBX_ZARR_ZLIB) {
+            if (len > 0xffffffffull) return fail(PBX_E_BADARG, "chunk %lld too large", (long long)i);
+            P.infl.push_back(ZStream{o, dst, (uint32_t)len, (uint32_t)cb, ZS_ZLIB, 0});
+            c.src = dst;
+            P.chunks.push_back(c);
+            P.scratch += (cb + 255) & ~255ull;
+            continue;
+        }
+        // blosc 1.x frame
+        const uint8_t* f = z->data + o;
+        if (len < 16) return fail(PBX_E_BADARG, "chunk %lld: short blosc header", (long long)i);
+        const uint32_t ver = f[0], flags = f[2], ts = f[3] ? f[3] : 1;
+        const uint32_t nbytes = rd_le32(f + 4), bs = rd_le32(f + 8), cbytes = rd_le32(f + 12);
+        if (ver > 2) return fail(PBX_E_BADARG, "chunk %lld: blosc format version %u (blosc2?)", (long long)i, ver);
+        if (nbytes != cb) return fail(PBX_E_BADARG, "chunk %lld: blosc nbytes %u != chunk bytes %llu",
+                                      (long long)i, nbytes, (unsigned long long)cb);
+        if (cbytes > len || cbytes < 16) return fail(PBX_E_BADARG, "chunk %lld: blosc cbytes %u", (long long)i, cbytes);
+        if (flags & 0x2) {  // memcpyed: the unshuffled chunk follows the header
+            if (16ull + nbytes > cbytes) return fail(PBX_E_BADARG, "chunk %lld: short memcpyed frame", (long long)i);
+            c.src = o + 16;
+            c.flags = ZC_INPUT;
+            P.chunks.push_back(c);
+            continue;
+        }
+        if (flags & 0x4) return fail(PBX_E_BADARG, "chunk %lld: blosc bit shuffle is not supported", (long long)i);
+        const uint32_t codec = flags >> 5;
+        if (codec != 1 && codec != 3)
+            return fail(PBX_E_BADARG, "chunk %lld: blosc codec %u not supported (lz4/lz4hc/zlib only)",
+                        (long long)i, codec);
+        if (bs == 0 || bs > nbytes || (bs % ts)) return fail(PBX_E_BADARG, "chunk %lld: blosc blocksize %u", (long long)i, bs);
+        const uint32_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
+        if (16ull + 4ull * nblocks > cbytes) return fail(PBX_E_BADARG, "chunk %lld: short block table", (long long)i);
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const bool is_left = leftover && b == nblocks - 1;
+            const uint32_t bsize = is_left ? leftover : bs;
+            const bool split = !(flags & 0x10) && ts <= 16 && bsize / ts >= 128 && !is_left;
+            const uint32_t nsp = split ? ts : 1, neb = bsize / nsp;
+            if (neb * nsp != bsize) return fail(PBX_E_BADARG, "chunk %lld: block %u not a multiple of typesize", (long long)i, b);
+            uint64_t pos = rd_le32(f + 16 + 4 * b);
+            for (uint32_t s = 0; s < nsp; s++) {
+                if (pos + 4 > cbytes) return fail(PBX_E_BADARG, "chunk %lld: block %u truncated", (long long)i, b);
+                const uint32_t cs = rd_le32(f + pos);
+                pos += 4;
+                if (pos + cs > cbytes || cs > neb || cs == 0)
+                    return fail(PBX_E_BADARG, "chunk %lld: block %u split %u size %u", (long long)i, b, s, cs);
+                const ZStream zs{o + pos, dst + (uint64_t)b * bs + (uint64_t)s * neb, cs, neb,
+                                 cs == neb ? ZS_COPY : (codec == 1 ? ZS_LZ4 : ZS_ZLIB), 0};
+                (cs == neb ? P.copy : codec == 1 ? P.lz4 : P.infl).push_back(zs);
+                pos += cs;
+            }
+        }
+        c.src = dst;
+        c.blocksize = bs;
+        c.typesize = (flags & 0x1) ? ts : 1;
+        P.chunks.push_back(c);
+        P.scratch += (cb + 255) & ~255ull;
+    }
+    return PBX_OK;
+}
+
+}  // namespace
+
+int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zarr_chunks* z,
+                            uint64_t* plane_id, double* kernel_ms) {
+    if (!ctx || !d || !z || !plane_id || !z->offsets || (!z->data && z->codec != PBX_ZARR_RAW))
+        return fail(PBX_E_BADARG, "null argument");
+    const int bpp = bpp_of(d->pixel_type);
+    if (!bpp) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
+    if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
+    if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
+    if (z->chunk_x <= 0 || z->chunk_y <= 0) return fail(PBX_E_BADARG, "bad chunk shape");
+    if (z->codec < PBX_ZARR_RAW || z->codec > PBX_ZARR_ZLIB) return fail(PBX_E_BADARG, "bad codec %d", z->codec);
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
+        if (ctx->index.count(key)) return fail(PBX_E_BADARG, "plane already registered");
+        auto im = ctx->images.find(d->image_id);
+        if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
+            return fail(PBX_E_BADARG, "pixel type differs from the image's");
+        if (d->resolution == 0 && im != ctx->images.end() &&
+            (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
+            return fail(PBX_E_BADARG, "plane size differs from the image's");
+    }
+    ZarrPlan P;
+    if (int rc = zarr_plan(d, z, bpp, P)) return rc;
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    const int64_t gx = (d->size_x + z->chunk_x - 1) / z->chunk_x, gy = (d->size_y + z->chunk_y - 1) / z->chunk_y;
+    const uint64_t in_bytes = z->offsets[gx * gy];
+    Plane p;
+    p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
+    p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
+    p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
+    p.pitch = ((int64_t)d->size_x * bpp + 255) & ~(int64_t)255;
+    p.bytes = (size_t)p.pitch * d->size_y + 256;
+    // fill bytes in the stored byte order
+    uint64_t fill = 0;
+    for (int j = 0; j < bpp; j++) {
+        const uint64_t byte = (z->fill_bits >> (8 * j)) & 0xff;
+        fill |= byte << (8 * (p.little_endian || bpp == 1 ? j : bpp - 1 - j));
+    }
+    const uint32_t nstreams = (uint32_t)(P.lz4.size() + P.infl.size() + P.copy.size());
+    std::vector<ZStream> all;
+    all.reserve(nstreams);
+    all.insert(all.end(), P.lz4.begin(), P.lz4.end());
+    all.insert(all.end(), P.infl.begin(), P.infl.end());
+    all.insert(all.end(), P.copy.begin(), P.copy.end());
+    uint8_t *d_in = nullptr, *d_scr = nullptr;
+    ZStream* d_st = nullptr;
+    ZChunk* d_ch = nullptr;
+    uint32_t* d_err = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    auto cleanup = [&]() {
+        if (d_in) (void)hipFree(d_in);
+        if (d_scr) (void)hipFree(d_scr);
+        if (d_st) (void)hipFree(d_st);
+        if (d_ch) (void)hipFree(d_ch);
+        if (d_err) (void)hipFree(d_err);
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    };
+    hipError_t e = hipMalloc((void**)&p.dev, p.bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_in, in_bytes + 4096);  // decoder window over-read slack (>= ZSLACK)
+    if (e == hipSuccess && P.scratch) e = hipMalloc((void**)&d_scr, P.scratch);
+    if (e == hipSuccess && nstreams) e = hipMalloc((void**)&d_st, sizeof(ZStream) * nstreams);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_ch, sizeof(ZChunk) * P.chunks.size());
+    if (e == hipSuccess) e = hipMalloc((void**)&d_err, sizeof(uint32_t) * (nstreams + 1));
+    for (auto& x : ev) if (e == hipSuccess) e = hipEventCreate(&x);
+    if (e == hipSuccess && in_bytes) e = hipMemcpyAsync(d_in, z->data, in_bytes, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_in + in_bytes, 0, 4096, ctx->stream);
+    if (e == hipSuccess && nstreams)
+        e = hipMemcpyAsync(d_st, all.data(), sizeof(ZStream) * nstreams, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_ch, P.chunks.data(), sizeof(ZChunk) * P.chunks.size(), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_err, 0, sizeof(uint32_t) * (nstreams + 1), ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ev[0], ctx->stream);
+    if (e == hipSuccess)
+        e = launch_zarr_decode(ctx->stream, d_st, (uint32_t)P.lz4.size(), (uint32_t)P.infl.size(),
+                               (uint32_t)P.copy.size(), d_in, d_scr, d_err);
+    if (e == hipSuccess) e = hipEventRecord(ev[1], ctx->stream);
+    if (e == hipSuccess)
+        e = launch_zarr_place(ctx->stream, d_ch, (uint32_t)P.chunks.size(), d_scr, d_in, p.dev, p.pitch,
+                              d->size_x, d->size_y, z->chunk_x, z->chunk_y, (uint32_t)bpp, fill);
+    if (e == hipSuccess) e = hipEventRecord(ev[2], ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    std::vector<uint32_t> err(nstreams + 1, 0);
+    if (e == hipSuccess && nstreams)
+        e = hipMemcpy(err.data(), d_err, sizeof(uint32_t) * nstreams, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        cleanup();
+        (void)hipFree(p.dev);
+        return fail(PBX_E_INTERNAL, "zarr decode: %s", hipGetErrorString(e));
+    }
+    for (uint32_t s = 0; s < nstreams; s++)
+        if (err[s]) {
+            cleanup();
+            (void)hipFree(p.dev);
+            return fail(PBX_E_BADARG, "corrupt chunk stream %u (%s, decoder code %u)", s,
+                        s < P.lz4.size() ? "lz4" : s < P.lz4.size() + P.infl.size() ? "zlib" : "stored", err[s]);
+        }
+    if (kernel_ms) {
+        float a = 0, b = 0;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        kernel_ms[0] = a;
+        kernel_ms[1] = b;
+    }
+    cleanup();
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
+    if (ctx->index.count(key)) {
+        (void)hipFree(p.dev);
+        return fail(PBX_E_BADARG, "plane already registered");
+    }
+    p.id = ctx->next_id++;
+    ctx->planes[p.id] = p;
+    ctx->index[key] = p.id;
+    Image& im = ctx->images[d->image_id];
+    if (d->resolution == 0 || im.planes == 0) {
+        im.pixel_type = d->pixel_type;
+        im.size_x = d->size_x;
+        im.size_y = d->size_y;
+    }
+    im.planes++;
+    *plane_id = p.id;
+    return PBX_OK;
+}
+
 int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     std::lock_guard<std::mutex> run(ctx->run_mu);

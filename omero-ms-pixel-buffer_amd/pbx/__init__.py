@@ -59,6 +59,19 @@ class PbxPlaneDesc(ctypes.Structure):
                 ("plane_no", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class PbxZarrChunks(ctypes.Structure):
+    _fields_ = [("chunk_x", ctypes.c_int32), ("chunk_y", ctypes.c_int32),
+                ("codec", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("data", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("fill_bits", ctypes.c_uint64)]
+
+
+ZARR_RAW, ZARR_BLOSC, ZARR_ZLIB = 0, 1, 2
+ZARR_CODECS = {None: ZARR_RAW, "blosc": ZARR_BLOSC, "zlib": ZARR_ZLIB}
+_ZARR_DTYPES = {"i1": INT8, "u1": UINT8, "i2": INT16, "u2": UINT16, "i4": INT32, "u4": UINT32,
+                "f4": FLOAT, "f8": DOUBLE}
+
+
 class PbxTileReq(ctypes.Structure):
     _fields_ = [("image_id", ctypes.c_int64), ("z", ctypes.c_int32), ("c", ctypes.c_int32),
                 ("t", ctypes.c_int32), ("resolution", ctypes.c_int32), ("x", ctypes.c_int32),
@@ -91,6 +104,7 @@ EXPORTS = [
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
     "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
+    "pbx_plane_register_zarr",
 ]
 
 _lib = None
@@ -121,6 +135,9 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
     L.pbx_plane_build_pyramid.argtypes = [vp, u64, i32, ctypes.POINTER(u64),
+                                          ctypes.POINTER(ctypes.c_double)]
+    L.pbx_plane_register_zarr.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc),
+                                          ctypes.POINTER(PbxZarrChunks), ctypes.POINTER(u64),
                                           ctypes.POINTER(ctypes.c_double)]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
     L.pbx_test_batch_lz77.argtypes = [vp, vp, vp, vp, u64]
@@ -335,6 +352,73 @@ class PixelsService:
         _check(lib().pbx_plane_register(self._h, ctypes.byref(d), ctypes.byref(pid)))
         del keep
         return pid.value
+
+    def register_zarr_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int,
+                            size_x: int, size_y: int, chunk_x: int, chunk_y: int,
+                            codec: Optional[str], chunks: Sequence[Optional[bytes]],
+                            big_endian: bool = True, fill_bits: int = 0, resolution: int = 0,
+                            timing: bool = False):
+        """Register a plane from its Zarr v2 chunks (C order over the chunk grid; None or
+        b"" = missing chunk -> fill), decoded on the GPU (pbx_plane_register_zarr).  codec is
+        the .zarray compressor id: None, "blosc" or "zlib".  Returns the plane id (and the
+        decode / placement kernels' device ms with timing=True)."""
+        import numpy as np
+        if codec not in ZARR_CODECS:
+            raise PbxError(400, "unsupported Zarr compressor %r" % (codec,))
+        lens = np.array([len(b) if b else 0 for b in chunks], dtype=np.uint64)
+        offsets = np.zeros(len(chunks) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offsets[1:])
+        data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
+        d = PbxPlaneDesc()
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, resolution
+        d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
+        d.byte_order = BIG_ENDIAN if big_endian else LITTLE_ENDIAN
+        zc = PbxZarrChunks()
+        zc.chunk_x, zc.chunk_y, zc.codec = chunk_x, chunk_y, ZARR_CODECS[codec]
+        zc.data, zc.offsets, zc.fill_bits = data.ctypes.data, offsets.ctypes.data, fill_bits
+        pid = ctypes.c_uint64()
+        ms = (ctypes.c_double * 2)()
+        _check(lib().pbx_plane_register_zarr(self._h, ctypes.byref(d), ctypes.byref(zc),
+                                             ctypes.byref(pid), ms))
+        return (pid.value, (ms[0], ms[1])) if timing else pid.value
+
+    def register_zarr_array(self, array_dir: str, image_id: int, z: int, c: int, t: int,
+                            resolution: int = 0) -> int:
+        """One (t, c, z) plane of an NGFF multiscale dataset (a Zarr v2 array directory with
+        shape [..., y, x], NGFF order t, c, z, y, x) — what ZarrPixelBuffer reads through
+        JZarr (omero-zarr-pixel-buffer 0.6.1, build.gradle:57).  Chunks of the plane are read
+        from disk here and decoded on the GPU."""
+        import json
+        with open(os.path.join(array_dir, ".zarray")) as f:
+            meta = json.load(f)
+        if meta.get("zarr_format") != 2 or meta.get("order", "C") != "C" or meta.get("filters"):
+            raise PbxError(400, "only Zarr v2 C-order arrays without filters are supported")
+        shape, chunk = meta["shape"], meta["chunks"]
+        dt = meta["dtype"]
+        if dt[1:] not in _ZARR_DTYPES:
+            raise PbxError(400, "unsupported dtype %s" % dt)
+        comp = meta.get("compressor")
+        codec = None if comp is None else comp.get("id")
+        lead = [t, c, z][-(len(shape) - 2):] if len(shape) > 2 else []
+        lead_idx = [v // cs for v, cs in zip(lead, chunk[:-2])]
+        sep = meta.get("dimension_separator", ".")
+        sy, sx, cy_, cx_ = shape[-2], shape[-1], chunk[-2], chunk[-1]
+        gy, gx = -(-sy // cy_), -(-sx // cx_)
+        if any(cs != 1 for cs in chunk[:-2]):
+            raise PbxError(400, "chunks spanning several planes are not supported")
+        chunks = []
+        for j in range(gy):
+            for i in range(gx):
+                key = sep.join(str(v) for v in lead_idx + [j, i])
+                path = os.path.join(array_dir, key)
+                chunks.append(open(path, "rb").read() if os.path.exists(path) else None)
+        fill = meta.get("fill_value") or 0
+        import numpy as np
+        native = np.dtype(dt).newbyteorder("=")
+        fill_bits = int(np.array([fill], dtype=native).view("u%d" % native.itemsize)[0])
+        return self.register_zarr_plane(image_id, z, c, t, _ZARR_DTYPES[dt[1:]], sx, sy, cx_, cy_,
+                                        codec, chunks, big_endian=dt[0] != "<",
+                                        fill_bits=fill_bits, resolution=resolution)
 
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))

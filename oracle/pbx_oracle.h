@@ -109,6 +109,24 @@ const char* pbxo_content_type(const char* format);
 double pbxo_bench(int kind, int pixel_type, int format, int32_t plane_w, int32_t plane_h,
                   int32_t w, int32_t h, int tiles, int threads, uint64_t* out_bytes);
 
+/* Zarr v2 chunk decode (oracle/zarr_oracle.c).  Codecs = include/pbx.h
+ * enum pbx_zarr_codec. */
+enum { PBXO_ZARR_RAW = 0, PBXO_ZARR_BLOSC = 1, PBXO_ZARR_ZLIB = 2 };
+int pbxo_lz4_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen);
+int pbxo_blosc_info(const uint8_t* in, size_t len, uint32_t* nbytes, uint32_t* blocksize,
+                    uint32_t* typesize, uint32_t* flags);
+int pbxo_blosc_decode(const uint8_t* in, size_t len, uint8_t* out, size_t cap, size_t* out_len);
+int pbxo_zarr_decode_chunk(int codec, const uint8_t* in, size_t len, uint8_t* out, size_t nbytes);
+/* Assemble a plane (row-major, size_x*bpp bytes per row) from the C-order chunk grid:
+ * chunk i's bytes are data[offsets[i] .. offsets[i+1]); an empty range is a missing chunk
+ * (every sample = the bpp bytes at fill).  Returns 0 on success. */
+int pbxo_zarr_plane(int codec, int bpp, int32_t size_x, int32_t size_y, int32_t chunk_x,
+                    int32_t chunk_y, const uint8_t* data, const uint64_t* offsets,
+                    const uint8_t* fill, uint8_t* plane);
+/* CPU baseline: decode every chunk on `threads` threads; returns wall seconds (-1 on error). */
+double pbxo_zarr_bench(int codec, const uint8_t* data, const uint64_t* offsets, size_t nchunks,
+                       size_t chunk_bytes, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,271 @@
+"""NGFF / Zarr v2 chunk decode into HBM (pbx_plane_register_zarr).
+
+CPU (not gpu): the oracle's frame/codec restatement (oracle/zarr_oracle.c) against the
+c-blosc 1.21 / zlib fixtures in tests/golden/zarr (made by imagecodecs, script committed),
+and the test-side frame writer (tests/_zarr.py) byte-identical to c-blosc's frames.
+GPU: every fixture decoded on the GPU equals the fixture's raw bytes; multi-chunk planes
+(edge chunks, missing chunks with fill values, every codec) equal the oracle's assembly of
+the same chunks byte for byte; tiles served from a Zarr plane equal the oracle's tiles;
+malformed or unsupported chunks fail with 400 and register nothing.
+"""
+import ctypes
+import itertools
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import _zarr
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden", "zarr")
+MANIFEST = json.load(open(os.path.join(GOLD, "manifest.json")))
+CASES = MANIFEST["cases"]
+CODEC = {"blosc": 1, "zlib": 2, None: 0}
+PT = {"i1": 0, "u1": 1, "i2": 2, "u2": 3, "i4": 4, "u4": 5, "f4": 6, "f8": 7}
+
+_ids = itertools.count(5000)
+
+
+def fixture(name):
+    enc = open(os.path.join(GOLD, name + ".enc"), "rb").read()
+    raw = open(os.path.join(GOLD, name + ".raw"), "rb").read()
+    return enc, raw
+
+
+def oracle_decode(oracle, codec, enc, nbytes):
+    L = oracle.lib()
+    out = ctypes.create_string_buffer(max(nbytes, 1))
+    rc = L.pbxo_zarr_decode_chunk(CODEC[codec], enc, ctypes.c_size_t(len(enc)), out,
+                                  ctypes.c_size_t(nbytes))
+    return rc, out.raw[:nbytes]
+
+
+def oracle_plane(oracle, codec, bpp, sx, sy, cx, cy, chunks, fill_bytes):
+    L = oracle.lib()
+    lens = [len(c) if c else 0 for c in chunks]
+    offs = (ctypes.c_uint64 * (len(chunks) + 1))(*np.concatenate([[0], np.cumsum(lens)]).astype(int).tolist())
+    data = b"".join(c for c in chunks if c) or b"\0"
+    out = ctypes.create_string_buffer(sx * sy * bpp)
+    rc = L.pbxo_zarr_plane(CODEC[codec], bpp, sx, sy, cx, cy, data, offs, fill_bytes, out)
+    assert rc == 0
+    return out.raw
+
+
+# ----------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_decodes_fixture(oracle, case):
+    enc, raw = fixture(case["name"])
+    rc, out = oracle_decode(oracle, case["codec"], enc, len(raw))
+    if case["name"].startswith("unsupported"):
+        assert rc != 0
+    else:
+        assert rc == 0 and out == raw
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["codec"] == "blosc"
+                                  and c["params"]["compressor"] in ("lz4", "zlib")
+                                  and c["params"]["shuffle"] in (0, 1)],
+                         ids=lambda c: c["name"])
+def test_frame_writer_matches_cblosc(case):
+    enc, raw = fixture(case["name"])
+    p = case["params"]
+    mine = _zarr.blosc_encode(raw, np.dtype(case["dtype"]).itemsize, clevel=p["level"],
+                              shuffle=bool(p["shuffle"]), codec=p["compressor"])
+    assert mine == enc
+
+
+def test_oracle_plane_assembly(oracle):
+    plane = _zarr.noise_plane(300, 200, ">u2", seed=3)
+    chunks = _zarr.encode_chunks(plane, 64, 48, "blosc")
+    chunks[5] = None
+    got = np.frombuffer(oracle_plane(oracle, "blosc", 2, 200, 300, 48, 64, chunks,
+                                     (7).to_bytes(2, "big")), ">u2").reshape(300, 200)
+    want = plane.copy()
+    gx = -(-200 // 48)
+    cy, cx = divmod(5, gx)
+    want[cy * 64:(cy + 1) * 64, cx * 48:(cx + 1) * 48] = 7
+    assert np.array_equal(got, want)
+
+
+# ----------------------------------------------------------------------------- GPU
+gpu = pytest.mark.gpu
+
+
+def plane_be(service, pid, dtype, h, w):
+    raw = service.read_plane_be(pid, h * w * np.dtype(dtype).itemsize)
+    return np.frombuffer(raw, np.dtype(dtype).newbyteorder(">")).reshape(h, w)
+
+
+@gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_decodes_fixture(service, case):
+    import pbx
+    enc, raw = fixture(case["name"])
+    h, w = case["shape"]
+    dt = np.dtype(case["dtype"])
+    iid = next(_ids)
+    args = (iid, 0, 0, 0, PT[dt.str[1:]], w, h, w, h, case["codec"], [enc])
+    if case["name"].startswith("unsupported"):
+        with pytest.raises(pbx.PbxError) as ei:
+            service.register_zarr_plane(*args, big_endian=dt.str[0] != "<")
+        assert ei.value.status == 400
+        return
+    pid = service.register_zarr_plane(*args, big_endian=dt.str[0] != "<")
+    got = plane_be(service, pid, dt, h, w)
+    want = np.frombuffer(raw, dt).reshape(h, w)
+    assert np.array_equal(got.view(np.uint8), want.astype(dt.newbyteorder(">")).view(np.uint8))
+    service.release_plane(pid)
+
+
+@gpu
+@pytest.mark.parametrize("codec,kw", [
+    ("blosc", dict(codec="lz4", clevel=5)),
+    ("blosc", dict(codec="lz4", clevel=9, shuffle=False)),
+    ("blosc", dict(codec="lz4", clevel=1, blocksize=4096)),
+    ("blosc", dict(codec="zlib", clevel=5)),
+    ("blosc", dict(codec="lz4", clevel=5, split=False)),
+    ("zlib", dict(level=1)),
+    ("zlib", dict(level=6)),
+    ("zlib", dict(level=9)),
+    (None, {}),
+], ids=["lz4", "lz4-noshuffle-l9", "lz4-4k-blocks", "blosc-zlib", "lz4-nosplit", "zlib1", "zlib6",
+        "zlib9", "raw"])
+@pytest.mark.parametrize("dtype", [">u2", "<u2", "u1", ">f4", "<i4", ">f8"])
+def test_gpu_plane_multichunk(service, oracle, codec, kw, dtype):
+    h, w, cy, cx = 333, 517, 96, 128  # edge chunks in both directions
+    dt = np.dtype(dtype)
+    plane = _zarr.noise_plane(h, w, dtype, seed=len(dtype) + h)
+    if dt.kind == "f":
+        plane = (plane.astype(np.float64) * 0.25).astype(dtype)
+    chunks = _zarr.encode_chunks(plane, cy, cx, codec, **kw)
+    chunks[1] = None       # missing chunks read as fill_value
+    chunks[-1] = b""
+    fill_val = np.array([3], dtype=dt.newbyteorder("="))
+    fill_bits = int(fill_val.view("u%d" % dt.itemsize)[0])
+    iid = next(_ids)
+    pid, (ms_dec, ms_place) = service.register_zarr_plane(
+        iid, 0, 0, 0, PT[dt.str[1:]], w, h, cx, cy, codec, chunks,
+        big_endian=dt.str[0] != "<", fill_bits=fill_bits, timing=True)
+    assert ms_dec >= 0 and ms_place >= 0
+    want = oracle_plane(oracle, codec, dt.itemsize, w, h, cx, cy, chunks,
+                        fill_val.astype(dt).tobytes())
+    want = np.frombuffer(want, dt).reshape(h, w)
+    got = plane_be(service, pid, dt, h, w)
+    assert np.array_equal(got.view(np.uint8), want.astype(dt.newbyteorder(">")).view(np.uint8))
+    service.release_plane(pid)
+
+
+@gpu
+def test_gpu_zarr_tiles_png_raw_tif(service, oracle):
+    """Tiles served from a Zarr-decoded plane equal the oracle's tiles of the same pixels."""
+    import pbx
+    h, w = 1024, 1536
+    plane = _zarr.noise_plane(h, w, ">u2", seed=11)
+    chunks = _zarr.encode_chunks(plane, 512, 512, "blosc")
+    iid = next(_ids)
+    pid = service.register_zarr_plane(iid, 0, 0, 0, pbx.UINT16, w, h, 512, 512, "blosc", chunks)
+    be = plane.tobytes()
+    ctxs = [pbx.TileCtx(iid, 0, 0, 0, 256, 256, 512, 512, format="png"),
+            pbx.TileCtx(iid, 0, 0, 0, 1000, 700, 536, 324),
+            pbx.TileCtx(iid, 0, 0, 0, 0, 0, 300, 200, format="tif")]
+    (s1, png), (s2, raw), (s3, tif) = service.get_tiles(ctxs)
+    assert (s1, s2, s3) == (0, 0, 0)
+    r, px, _ = oracle.png_decode(png)
+    assert r == 0 and px == oracle.extract_be(np.frombuffer(be, np.uint8), True, pbx.UINT16, w * 2,
+                                              256, 256, 512, 512).tobytes()
+    assert raw == oracle.extract_be(np.frombuffer(be, np.uint8), True, pbx.UINT16, w * 2,
+                                    1000, 700, 536, 324).tobytes()
+    r, px, _ = oracle.tiff_decode(tif, 300 * 200 * 2)
+    assert r == 0 and px == oracle.extract_be(np.frombuffer(be, np.uint8), True, pbx.UINT16, w * 2,
+                                              0, 0, 300, 200).tobytes()
+    service.release_plane(pid)
+
+
+@gpu
+def test_gpu_ngff_directory(service, oracle, tmp_path):
+    """register_zarr_array reads an NGFF (t, c, z, y, x) array directory like JZarr does."""
+    import pbx
+    t_, c_, z_, h, w = 1, 2, 3, 400, 600
+    arr = tmp_path / "0"
+    arr.mkdir()
+    meta = {"zarr_format": 2, "shape": [t_, c_, z_, h, w], "chunks": [1, 1, 1, 256, 256],
+            "dtype": ">u2", "order": "C", "fill_value": 0, "filters": None,
+            "dimension_separator": "/",
+            "compressor": {"id": "blosc", "cname": "lz4", "clevel": 5, "shuffle": 1, "blocksize": 0}}
+    (arr / ".zarray").write_text(json.dumps(meta))
+    planes = {}
+    for c in range(c_):
+        for z in range(z_):
+            p = _zarr.noise_plane(h, w, ">u2", seed=10 * c + z)
+            planes[(c, z)] = p
+            for k, ch in enumerate(_zarr.encode_chunks(p, 256, 256, "blosc")):
+                j, i = divmod(k, 3)
+                d = arr / "0" / str(c) / str(z) / str(j)
+                d.mkdir(parents=True, exist_ok=True)
+                (d / str(i)).write_bytes(ch)
+    iid = next(_ids)
+    pid = service.register_zarr_array(str(arr), iid, 2, 1, 0)
+    got = plane_be(service, pid, ">u2", h, w)
+    assert np.array_equal(got, planes[(1, 2)])
+    st, raw = service.get_tile(pbx.TileCtx(iid, 2, 1, 0, 100, 50, 64, 32))
+    assert st == 0 and raw == planes[(1, 2)][50:82, 100:164].tobytes()
+    service.release_plane(pid)
+
+
+@gpu
+@pytest.mark.parametrize("damage", ["truncate", "flip", "bad_offset"])
+def test_gpu_corrupt_chunk_is_400(service, damage):
+    import pbx
+    plane = _zarr.noise_plane(256, 256, ">u2", seed=1)
+    chunks = _zarr.encode_chunks(plane, 128, 128, "blosc")
+    c = bytearray(chunks[2])
+    if damage == "truncate":
+        c = c[:len(c) // 2]
+    elif damage == "flip":
+        # corrupt LZ4 sequences inside the first split (after header, block table, csize)
+        for k in range(40, min(len(c), 400), 7):
+            c[k] ^= 0xA5
+    else:
+        c[16:20] = (len(c) + 100).to_bytes(4, "little")
+    chunks[2] = bytes(c)
+    iid = next(_ids)
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_plane(iid, 0, 0, 0, pbx.UINT16, 256, 256, 128, 128, "blosc", chunks)
+    assert ei.value.status == 400
+    # nothing registered: the same key registers cleanly afterwards
+    good = _zarr.encode_chunks(plane, 128, 128, "blosc")
+    pid = service.register_zarr_plane(iid, 0, 0, 0, pbx.UINT16, 256, 256, 128, 128, "blosc", good)
+    assert np.array_equal(plane_be(service, pid, ">u2", 256, 256), plane)
+    service.release_plane(pid)
+
+
+@gpu
+def test_gpu_corrupt_zlib_is_400(service):
+    import pbx
+    plane = _zarr.noise_plane(128, 128, ">u2", seed=2)
+    enc = bytearray(zlib.compress(plane.tobytes(), 6))
+    for k in range(20, 200, 5):
+        enc[k] ^= 0x3C
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 128, 128, 128, 128, "zlib",
+                                    [bytes(enc)])
+    assert ei.value.status == 400
+
+
+@gpu
+@pytest.mark.parametrize("compressor,kw", [("blosc", {}), ("zlib", {"level": 1}), ("blosc", {"codec": "zlib"})],
+                         ids=["blosc-lz4", "zlib1", "blosc-zlib"])
+def test_gpu_zarr_full_size(service, compressor, kw):
+    """A 8192^2 uint16 plane of 512^2 chunks (256 chunks; blosc: 1,024 streams)."""
+    import pbx
+    h = w = 8192
+    plane = _zarr.noise_plane(h, w, ">u2", seed=5)
+    chunks = _zarr.encode_chunks(plane, 512, 512, compressor, **kw)
+    pid, (ms_dec, ms_place) = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, w, h,
+                                                          512, 512, compressor, chunks, timing=True)
+    assert np.array_equal(plane_be(service, pid, ">u2", h, w), plane)
+    print("%s: decode %.3f ms, place %.3f ms" % (compressor, ms_dec, ms_place))
+    service.release_plane(pid)
