@@ -72,6 +72,19 @@ struct InWin {
         return rfl((uint32_t)zlds[r] | (uint32_t)zlds[r + 1] << 8 | (uint32_t)zlds[r + 2] << 16 |
                    (uint32_t)zlds[r + 3] << 24);
     }
+    // bytes q .. q+15 as four little-endian words (one LDS round trip: five aligned dword
+    // reads, shifted in scalar registers)
+    __device__ void peek16(uint32_t q, uint32_t (&d)[4]) {
+        if (q - base > ZWIN - 20) load(q);
+        const uint32_t a = wo + q - base, sh = (a & 3) * 8;
+        const uint32_t* p = (const uint32_t*)(zlds + (a & ~3u));
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = rfl(p[k]);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            d[k] = sh ? (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> sh) : w[k];
+    }
     // byte q + lane for every lane
     __device__ uint32_t lane_byte(uint32_t q) {
         if (q - base > ZWIN - 64) load(q);
@@ -133,7 +146,7 @@ struct OutRing {
 __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st, uint32_t n,
                                                   const uint8_t* __restrict__ src,
                                                   uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);  // wave-uniform (SGPR) state
     const uint32_t si = blockIdx.x * ZWAVES + w;
     if (si >= n) return;
     const ZStream t = st[si];
@@ -143,43 +156,66 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
     win.load(0);
     OutRing o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
     uint32_t ip = 0, bad = 0;
+    // the sequence header (token, length bytes, offset) usually lies in these 16 bytes; the
+    // next one is fetched while a short match's ring read is in flight (one LDS round trip
+    // per sequence)
+    uint32_t h[4];
+    win.peek16(0, h);
     for (;;) {
         if (ip >= ilen) { bad = 1; break; }
-        const uint32_t tok = win.byte(ip++);
-        uint32_t ll = tok >> 4;
+        auto hb = [&](uint32_t k) -> uint32_t {  // byte ip + k (k uniform)
+            if (k >= 16) return win.byte(ip + k);
+            const uint32_t d = k < 4 ? h[0] : k < 8 ? h[1] : k < 12 ? h[2] : h[3];
+            return (d >> ((k & 3) * 8)) & 0xffu;
+        };
+        const uint32_t tok = h[0] & 0xffu;
+        uint32_t k = 1, ll = tok >> 4;
         if (ll == 15) {
             uint32_t b;
             do {
-                if (ip >= ilen) { bad = 2; break; }
-                b = win.byte(ip++);
+                if (ip + k >= ilen) { bad = 2; break; }
+                b = hb(k++);
                 ll += b;
             } while (b == 255);
             if (bad) break;
         }
-        if (ll > ilen - ip || ll > o.olen - o.op) { bad = 3; break; }
-        for (uint32_t k = 0; k < ll; k += 64) {
-            const uint32_t q = ip + k, nb = ll - k < 64 ? ll - k : 64;
-            const uint32_t v = win.lane_byte(q);
-            if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
-            o.flush(o.op + k + nb);
+        const uint32_t ls = ip + k;
+        if (ll > ilen - ls || ll > o.olen - o.op) { bad = 3; break; }
+        for (uint32_t c = 0; c < ll; c += 64) {
+            const uint32_t nb = ll - c < 64 ? ll - c : 64;
+            const uint32_t v = win.lane_byte(ls + c);
+            if (lane < nb) o.ring(o.op + c + lane) = (uint8_t)v;
+            o.flush(o.op + c + nb);
         }
-        ip += ll;
         o.op += ll;
-        if (ip == ilen) break;
-        if (ilen - ip < 2) { bad = 4; break; }
-        const uint32_t off = win.byte(ip) | win.byte(ip + 1) << 8;
-        ip += 2;
+        if (ls + ll == ilen) { ip = ilen; break; }
+        if (ilen - (ls + ll) < 2) { bad = 4; break; }
         uint32_t ml = tok & 15;
+        k += ll;  // offset at ip + k
+        const uint32_t off = hb(k) | hb(k + 1) << 8;
+        k += 2;
         if (ml == 15) {
             uint32_t b;
             do {
-                if (ip >= ilen) { bad = 5; break; }
-                b = win.byte(ip++);
+                if (ip + k >= ilen) { bad = 5; break; }
+                b = hb(k++);
                 ml += b;
             } while (b == 255);
             if (bad) break;
         }
-        if (!o.match(off, ml + 4)) { bad = 6; break; }
+        ip += k;
+        const uint32_t len = ml + 4;
+        if (len <= 64 && off <= ZR && off != 0 && off <= o.op && len <= o.olen - o.op) {
+            const uint32_t rep = off < 64 ? lane % off : lane;
+            const uint32_t v = o.ring(o.op - off + rep);
+            win.peek16(ip, h);
+            if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
+            o.op += len;
+            o.flush(o.op);
+        } else {
+            if (!o.match(off, len)) { bad = 6; break; }
+            win.peek16(ip, h);
+        }
     }
     if (!bad && o.op != o.olen) bad = 7;
     o.finish();
@@ -275,7 +311,7 @@ __device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
     const uint32_t l = (uint32_t)__builtin_ctzll(m);
     const uint32_t idx = rdl(h.offs + code - h.first, l);
     bi.bits(l + 1);
-    return lds16(h.syms + 2 * idx);
+    return (int)rfl(lds16(h.syms + 2 * idx));
 }
 
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -298,7 +334,7 @@ constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR, ZI_DSYMS = ZI_LSYMS + 2 * 288,
 __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict__ st, uint32_t n,
                                                       const uint8_t* __restrict__ src,
                                                       uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);  // wave-uniform (SGPR) state
     const uint32_t si = blockIdx.x * ZWAVES + w;
     if (si >= n) return;
     const uint32_t wb = w * (ZI_BYTES + ZWIN);
@@ -433,7 +469,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
 __global__ __launch_bounds__(256) void k_zarr_copy(const ZStream* __restrict__ st, uint32_t n,
                                                    const uint8_t* __restrict__ src,
                                                    uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);  // wave-uniform (SGPR) state
     const uint32_t si = blockIdx.x * ZWAVES + w;
     if (si >= n) return;
     const ZStream t = st[si];

@@ -12,3 +12,5 @@ timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo bench 
 cat $O/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extra > $O/prof_bench.json 2> $O/prof.log && echo prof ok || { echo prof FAIL; tail -30 $O/prof.log; exit 1; }
 find $O/prof -name "*stats*"
+# row f2: kernel trace of the Zarr decode workload (k_zarr_*)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_zarr -o zarr --output-format csv -- python3 scripts/zarr_bench.py > $O/prof_zarr.json 2> $O/prof_zarr.log && echo zarr prof ok || { echo zarr prof FAIL; tail -30 $O/prof_zarr.log; exit 1; }

@@ -26,7 +26,7 @@ CASES = MANIFEST["cases"]
 CODEC = {"blosc": 1, "zlib": 2, None: 0}
 PT = {"i1": 0, "u1": 1, "i2": 2, "u2": 3, "i4": 4, "u4": 5, "f4": 6, "f8": 7}
 
-_ids = itertools.count(5000)
+_ids = itertools.count(900000)  # disjoint from the other test files (shared service)
 
 
 def fixture(name):
