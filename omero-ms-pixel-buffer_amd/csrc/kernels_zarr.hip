@@ -27,6 +27,7 @@ namespace pbx {
 
 constexpr uint32_t ZR = 8192, ZM = ZR - 1;  // LDS output ring per wave
 constexpr uint32_t ZWAVES = 4;              // waves per workgroup
+constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
 
 // Dynamic LDS of the decoders, addressed by offset (a pointer into LDS kept in a struct would
 // become a FLAT pointer; a selected one, a stack slot).  Per wave: ring, then (inflate) tables.
@@ -100,11 +101,14 @@ struct OutRing {
     uint32_t op, flushed, olen, lane;
     __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
     __device__ void flush(uint32_t upto) {
-        while (upto - flushed >= 256u) {
-            const uint32_t v = *(const uint32_t*)(zlds + rb + ((flushed + 4 * lane) & ZM));
-            __builtin_memcpy(out + flushed + 4 * lane, &v, 4);
-            flushed += 256;
+        uint32_t f = rfl(flushed);  // keep the ring state in SGPRs (scalar branches)
+        upto = rfl(upto);
+        while (upto - f >= 256u) {
+            const uint32_t v = *(const uint32_t*)(zlds + rb + ((f + 4 * lane) & ZM));
+            __builtin_memcpy(out + f + 4 * lane, &v, 4);
+            f += 256;
         }
+        flushed = f;
     }
     __device__ void finish() {
         for (uint32_t k = flushed; k < op; k += 64)
@@ -137,7 +141,7 @@ struct OutRing {
     }
     __device__ void put1(uint32_t v) {
         if (lane == 0) ring(op) = (uint8_t)v;
-        op++;
+        op = rfl(op) + 1;
         flush(op);
     }
 };
@@ -314,6 +318,36 @@ __device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
     return (int)rfl(lds16(h.syms + 2 * idx));
 }
 
+// First-level table of a built code: lut[next 9 stream bits] = sym | len << 9 for codes of
+// <= 9 bits (every extension of the bit-reversed code), 0xFFFF (-> decode_sym) otherwise.
+__device__ void build_lut(const HTab& h, uint32_t lens, uint32_t lut, uint32_t lane) {
+    for (uint32_t e = lane; e < (1u << ZLUT); e += 64) lds16(lut + 2 * e) = 0xFFFF;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = rdl(h.offs + h.count, 14);  // symbols with a code
+    for (uint32_t g = 0; g < total; g += 64) {  // uniform trip count: the shuffles see all lanes
+        const uint32_t j = g + lane;
+        const uint32_t sym = j < total ? lds16(h.syms + 2 * j) : 0u;
+        const uint32_t len = j < total ? zlds[lens + sym] : 0u;
+        const uint32_t src = len ? len - 1 : 0;
+        const uint32_t first = (uint32_t)__shfl((int)h.first, (int)src, 64);
+        const uint32_t offs = (uint32_t)__shfl((int)h.offs, (int)src, 64);
+        if (len == 0 || len > ZLUT) continue;
+        const uint32_t rev = __builtin_bitreverse32(first + (j - offs)) >> (32 - len);
+        for (uint32_t k = 0; k < (1u << (ZLUT - len)); k++)
+            lds16(lut + 2 * (rev | (k << len))) = (uint16_t)(sym | len << 9);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int decode_fast(const HTab& h, uint32_t lut, BitIn& bi, uint32_t lane) {
+    const uint32_t e = rfl(lds16(lut + 2 * ((uint32_t)bi.buf & ((1u << ZLUT) - 1))));
+    if (e != 0xFFFF) {
+        bi.bits(e >> 9);
+        return (int)(e & 511);
+    }
+    return decode_sym(h, bi, lane);
+}
+
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
@@ -329,7 +363,9 @@ constexpr uint32_t ZLENS = 352;
 
 // Per-wave LDS of k_zarr_inflate (byte offsets from the wave's base)
 constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR, ZI_DSYMS = ZI_LSYMS + 2 * 288,
-                   ZI_LENS = ZI_DSYMS + 2 * 32, ZI_NEXT = ZI_LENS + ZLENS, ZI_BYTES = ZI_NEXT + 64;
+                   ZI_LENS = ZI_DSYMS + 2 * 32, ZI_NEXT = ZI_LENS + ZLENS,
+                   ZI_LLUT = ZI_NEXT + 64, ZI_DLUT = ZI_LLUT + 2 * (1u << ZLUT),
+                   ZI_BYTES = ZI_DLUT + 2 * (1u << ZLUT);
 
 __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict__ st, uint32_t n,
                                                       const uint8_t* __restrict__ src,
@@ -385,6 +421,8 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             __builtin_amdgcn_wave_barrier();
             build_table(lt, LENS, 288, lane, NEXT);
             build_table(dt, LENS + 288, 30, lane, NEXT);
+            build_lut(lt, LENS, wb + ZI_LLUT, lane);
+            build_lut(dt, LENS + 288, wb + ZI_DLUT, lane);
         } else {  // dynamic
             bi.refill();
             const uint32_t hlit = bi.bits(5) + 257, hdist = bi.bits(5) + 1, hclen = bi.bits(4) + 4;
@@ -435,11 +473,13 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             }
             if (!build_table(lt, LENS, 288, lane, NEXT)) { bad = 19; break; }
             if (!build_table(dt, LENS + 288, 30, lane, NEXT)) { bad = 20; break; }
+            build_lut(lt, LENS, wb + ZI_LLUT, lane);
+            build_lut(dt, LENS + 288, wb + ZI_DLUT, lane);
         }
         // block data
         for (;;) {
             bi.refill();
-            const int sym = decode_sym(lt, bi, lane);
+            const int sym = decode_fast(lt, wb + ZI_LLUT, bi, lane);
             if (sym < 0) { bad = 21; break; }
             if (sym < 256) {
                 if (o.op >= o.olen) { bad = 22; break; }
@@ -452,7 +492,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             bi.refill();
             const uint32_t len = c_lbase[ls] + bi.bits(c_lext[ls]);
             bi.refill();
-            const int ds = decode_sym(dt, bi, lane);
+            const int ds = decode_fast(dt, wb + ZI_DLUT, bi, lane);
             if (ds < 0 || ds >= 30) { bad = 24; break; }
             bi.refill();
             const uint32_t dist = c_dbase[ds] + bi.bits(c_dext[ds]);
@@ -507,13 +547,58 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
     const int32_t r1 = r0 + (int32_t)ZP_ROWS < h ? r0 + (int32_t)ZP_ROWS : h;
     const uint8_t* s = (c.flags & ZC_INPUT ? input : scratch) + c.src;
     const uint32_t ts = c.typesize, bs = c.blocksize, nb = c.nbytes;
+    const bool missing = (c.flags & ZC_MISSING) != 0;
     for (int32_t r = r0; r < r1; r++) {
         uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
-        for (int32_t col = (int32_t)threadIdx.x; col < w; col += 256) {
+        // fast path: 4 samples per thread, one (unaligned) dword load per byte plane
+        int32_t done = 0;
+        if (!missing && (ts == 1 || ts == bpp) && (bpp == 1 || bpp == 2 || bpp == 4)) {
+            const int32_t w4 = w & ~3;
+            for (int32_t c4 = 4 * (int32_t)threadIdx.x; c4 < w4; c4 += 1024) {
+                const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)c4;
+                uint32_t out[4];
+                if (ts == 1) {
+                    if (bpp == 1) __builtin_memcpy(out, s + e, 4);
+                    else if (bpp == 2) __builtin_memcpy(out, s + (size_t)e * 2, 8);
+                    else __builtin_memcpy(out, s + (size_t)e * 4, 16);
+                } else {
+                    const uint32_t B = e * bpp, blk = B / bs;
+                    const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
+                    const uint32_t ne = bsize / ts, ie = (B - blk * bs) / ts;
+                    if (ie + 3 >= ne) {  // the 4 samples straddle a block: byte path below
+                        for (int32_t col = c4; col < c4 + 4; col++)
+                            for (uint32_t j = 0; j < bpp; j++) {
+                                const uint32_t Bj = ((uint32_t)r * (uint32_t)cw + (uint32_t)col) * bpp + j;
+                                const uint32_t bk = Bj / bs, wi = Bj - bk * bs;
+                                const uint32_t bz = nb - bk * bs < bs ? nb - bk * bs : bs, nz = bz / ts;
+                                o[(int64_t)col * bpp + j] = s[wi < nz * ts ? bk * bs + (wi % ts) * nz + wi / ts : Bj];
+                            }
+                        continue;
+                    }
+                    const uint8_t* q = s + blk * bs + ie;
+                    uint32_t p[4];
+                    for (uint32_t j = 0; j < bpp; j++) p[j] = ld_u32_unaligned(q + j * ne);
+                    if (bpp == 2) {
+                        out[0] = (p[0] & 0xff) | (p[1] & 0xff) << 8 | (p[0] & 0xff00) << 8 | (p[1] & 0xff00) << 16;
+                        out[1] = (p[0] >> 16 & 0xff) | (p[1] >> 16 & 0xff) << 8 | (p[0] >> 24) << 16 | (p[1] >> 24) << 24;
+                    } else {  // bpp == 4
+                        for (uint32_t i = 0; i < 4; i++)
+                            out[i] = (p[0] >> (8 * i) & 0xff) | (p[1] >> (8 * i) & 0xff) << 8 |
+                                     (p[2] >> (8 * i) & 0xff) << 16 | (p[3] >> (8 * i) & 0xff) << 24;
+                    }
+                }
+                uint8_t* d = o + (int64_t)c4 * bpp;
+                if (bpp == 1) __builtin_memcpy(d, out, 4);
+                else if (bpp == 2) __builtin_memcpy(d, out, 8);
+                else __builtin_memcpy(d, out, 16);
+            }
+            done = w4;
+        }
+        for (int32_t col = done + (int32_t)threadIdx.x; col < w; col += 256) {
             const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
             for (uint32_t j = 0; j < bpp; j++) {
                 uint32_t v;
-                if (c.flags & ZC_MISSING) {
+                if (missing) {
                     v = (uint32_t)(fill >> (8 * j)) & 0xffu;
                 } else if (ts > 1) {
                     const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
