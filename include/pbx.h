@@ -145,6 +145,12 @@ typedef struct pbx_zarr_chunks {
  * A malformed or unsupported chunk fails the whole plane with 400 (nothing registered). */
 int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* desc, const pbx_zarr_chunks* chunks,
                             uint64_t* plane_id, double* kernel_ms);
+/* n planes (e.g. every (z, c, t) plane of an NGFF resolution level) decoded by ONE set of
+ * launches: descs[k] / chunks[k] as above, plane_ids[k] receives plane k's id.  More planes
+ * per call = more compressed streams in flight (one wave each), which is what hides the
+ * serial decode latency.  All planes are registered, or none (400/500). */
+int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* descs,
+                             const pbx_zarr_chunks* chunks, uint64_t* plane_ids, double* kernel_ms);
 /* Copy a registered plane back to the host, samples in big-endian order (test hook). */
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
 

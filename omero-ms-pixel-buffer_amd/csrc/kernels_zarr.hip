@@ -25,7 +25,8 @@
 
 namespace pbx {
 
-constexpr uint32_t ZR = 8192, ZM = ZR - 1;  // LDS output ring per wave
+constexpr uint32_t ZR = 8192;                // LDS output ring per wave (inflate)
+constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
 constexpr uint32_t ZWAVES = 4;              // waves per workgroup
 constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
 
@@ -69,22 +70,20 @@ struct InWin {
     // 32 bits starting at byte q (little-endian)
     __device__ uint32_t dword(uint32_t q) {
         if (q - base > ZWIN - 4) load(q);
-        const uint32_t r = wo + q - base;
-        return rfl((uint32_t)zlds[r] | (uint32_t)zlds[r + 1] << 8 | (uint32_t)zlds[r + 2] << 16 |
-                   (uint32_t)zlds[r + 3] << 24);
+        uint32_t v;
+        __builtin_memcpy(&v, zlds + wo + q - base, 4);  // one unaligned ds_read_b32
+        return rfl(v);
     }
-    // bytes q .. q+15 as four little-endian words (one LDS round trip: five aligned dword
-    // reads, shifted in scalar registers)
+    // bytes q .. q+15 as four little-endian words: one unaligned ds_read_b128 (gfx950 LDS
+    // takes byte-aligned accesses)
     __device__ void peek16(uint32_t q, uint32_t (&d)[4]) {
-        if (q - base > ZWIN - 20) load(q);
-        const uint32_t a = wo + q - base, sh = (a & 3) * 8;
-        const uint32_t* p = (const uint32_t*)(zlds + (a & ~3u));
-        uint32_t w[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) w[k] = rfl(p[k]);
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            d[k] = sh ? (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> sh) : w[k];
+        if (q - base > ZWIN - 16) load(q);
+        uint4 v;
+        __builtin_memcpy(&v, zlds + wo + q - base, 16);
+        d[0] = rfl(v.x);
+        d[1] = rfl(v.y);
+        d[2] = rfl(v.z);
+        d[3] = rfl(v.w);
     }
     // byte q + lane for every lane
     __device__ uint32_t lane_byte(uint32_t q) {
@@ -95,7 +94,9 @@ struct InWin {
 
 // Output through the LDS ring (offset rb, 256-aligned); bytes [flushed, op) are in the ring
 // only.  Completed 256-byte runs go to HBM as one dword store per lane.
+template <uint32_t RING>
 struct OutRing {
+    static constexpr uint32_t ZM = RING - 1, ZR = RING;
     uint32_t rb;
     uint8_t* out;
     uint32_t op, flushed, olen, lane;
@@ -155,10 +156,14 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
     if (si >= n) return;
     const ZStream t = st[si];
     const uint32_t ilen = rfl(t.csize);
-    const uint32_t wb = w * (ZR + ZWIN);
-    InWin win{src + t.src_off, wb + ZR, 0, lane};
+    const uint32_t wb = w * (ZR_LZ4 + ZWIN);
+    InWin win{src + t.src_off, wb + ZR_LZ4, 0, lane};
     win.load(0);
-    OutRing o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+#ifdef PBX_ZARR_CLOCKS  // diagnostic build: shader clocks and real time of stream 0
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t nseq = 0;
+#endif
     uint32_t ip = 0, bad = 0;
     // the sequence header (token, length bytes, offset) usually lies in these 16 bytes; the
     // next one is fetched while a short match's ring read is in flight (one LDS round trip
@@ -208,8 +213,11 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
             if (bad) break;
         }
         ip += k;
+#ifdef PBX_ZARR_CLOCKS
+        nseq++;
+#endif
         const uint32_t len = ml + 4;
-        if (len <= 64 && off <= ZR && off != 0 && off <= o.op && len <= o.olen - o.op) {
+        if (len <= 64 && off <= ZR_LZ4 && off != 0 && off <= o.op && len <= o.olen - o.op) {
             const uint32_t rep = off < 64 ? lane % off : lane;
             const uint32_t v = o.ring(o.op - off + rep);
             win.peek16(ip, h);
@@ -223,6 +231,13 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
     }
     if (!bad && o.op != o.olen) bad = 7;
     o.finish();
+#ifdef PBX_ZARR_CLOCKS
+    if (lane == 0 && (si == 0 || si == 1)) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        printf("lz4 stream %u: %u sequences, %u bytes, %llu shader clocks, %llu realtime ticks\n", si, nseq,
+               o.op, (unsigned long long)(t1 - t0), (unsigned long long)(r1 - r0));
+    }
+#endif
     if (lane == 0) err[si] = bad;
 }
 
@@ -378,7 +393,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
     const ZStream t = st[si];
     BitIn bi{{src + t.src_off, wb + ZI_BYTES, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
     bi.win.load(0);
-    OutRing o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR> o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
     HTab lt{0, 0, 0, wb + ZI_LSYMS}, dt{0, 0, 0, wb + ZI_DSYMS};
     uint32_t bad = 0;
     bi.refill();
@@ -534,14 +549,19 @@ __global__ __launch_bounds__(256) void k_zarr_copy(const ZStream* __restrict__ s
 constexpr uint32_t ZP_ROWS = 8;
 
 __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ ch, uint32_t bands,
+                                                    const ZPlane* __restrict__ planes,
                                                     const uint8_t* __restrict__ scratch,
-                                                    const uint8_t* __restrict__ input,
-                                                    uint8_t* __restrict__ plane, int64_t pitch,
-                                                    int32_t sx, int32_t sy, int32_t cw, int32_t chh,
-                                                    uint32_t bpp, uint64_t fill) {
+                                                    const uint8_t* __restrict__ input) {
     const ZChunk c = ch[blockIdx.x / bands];
+    const ZPlane& zp = planes[c.plane];
+    uint8_t* const plane = zp.dev;
+    const int64_t pitch = zp.pitch;
+    const int32_t sx = zp.sx, sy = zp.sy, cw = zp.cw, chh = zp.chh;
+    const uint32_t bpp = zp.bpp;
+    const uint64_t fill = zp.fill;
     const uint32_t band = blockIdx.x % bands;
     const int32_t r0 = (int32_t)(band * ZP_ROWS);
+    if (r0 >= chh) return;  // bands cover the tallest chunk of the set
     const int32_t w = sx - c.x0 < cw ? sx - c.x0 : cw;
     const int32_t h = sy - c.y0 < chh ? sy - c.y0 : chh;
     const int32_t r1 = r0 + (int32_t)ZP_ROWS < h ? r0 + (int32_t)ZP_ROWS : h;
@@ -620,7 +640,7 @@ hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t
                               uint32_t* err) {
     // streams are ordered: lz4 first, then inflate, then copy
     if (n_lz4)
-        hipLaunchKernelGGL(k_zarr_lz4, dim3((n_lz4 + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZR + ZWIN), st,
+        hipLaunchKernelGGL(k_zarr_lz4, dim3((n_lz4 + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZR_LZ4 + ZWIN), st,
                            d_streams, n_lz4, src, scratch, err);
     if (n_infl)
         hipLaunchKernelGGL(k_zarr_inflate, dim3((n_infl + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZI_BYTES + ZWIN), st,
@@ -632,13 +652,12 @@ hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t
 }
 
 hipError_t launch_zarr_place(hipStream_t st, const ZChunk* d_chunks, uint32_t nchunks,
-                             const uint8_t* scratch, const uint8_t* input, uint8_t* plane,
-                             int64_t pitch, int32_t sx, int32_t sy, int32_t cw, int32_t chh,
-                             uint32_t bpp, uint64_t fill) {
-    const uint32_t bands = ((uint32_t)chh + ZP_ROWS - 1) / ZP_ROWS;
+                             const ZPlane* d_planes, int32_t max_chunk_y, const uint8_t* scratch,
+                             const uint8_t* input) {
+    const uint32_t bands = ((uint32_t)max_chunk_y + ZP_ROWS - 1) / ZP_ROWS;
     if (!nchunks) return hipSuccess;
     hipLaunchKernelGGL(k_zarr_place, dim3(nchunks * bands), dim3(256), 0, st, d_chunks, bands,
-                       scratch, input, plane, pitch, sx, sy, cw, chh, bpp, fill);
+                       d_planes, scratch, input);
     return hipGetLastError();
 }
 

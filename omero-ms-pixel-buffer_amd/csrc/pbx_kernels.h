@@ -75,14 +75,21 @@ struct ZChunk {
     uint32_t nbytes, blocksize, typesize; // blosc geometry (typesize 1 = not shuffled)
     uint32_t flags;                       // ZC_*
     int32_t x0, y0;                       // chunk origin in the plane
+    uint32_t plane, pad;                  // index into the ZPlane table of the launch
+};
+struct ZPlane {                           // a destination plane of one decode launch
+    uint8_t* dev;
+    int64_t pitch;
+    int32_t sx, sy, cw, chh;              // plane and chunk shape
+    uint32_t bpp, pad;
+    uint64_t fill;                        // fill bytes in stored order (missing chunks)
 };
 // Streams ordered lz4 | inflate | copy; err[i] = 0 or a decoder error code per stream.
 hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t n_lz4,
                               uint32_t n_infl, uint32_t n_copy, const uint8_t* src, uint8_t* scratch,
                               uint32_t* err);
 hipError_t launch_zarr_place(hipStream_t st, const ZChunk* d_chunks, uint32_t nchunks,
-                             const uint8_t* scratch, const uint8_t* input, uint8_t* plane,
-                             int64_t pitch, int32_t sx, int32_t sy, int32_t cw, int32_t chh,
-                             uint32_t bpp, uint64_t fill);
+                             const ZPlane* d_planes, int32_t max_chunk_y, const uint8_t* scratch,
+                             const uint8_t* input);
 
 }  // namespace pbx

@@ -688,7 +688,8 @@ struct ZarrPlan {
     uint64_t scratch = 0;
 };
 
-int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPlan& P) {
+int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, uint64_t in_base,
+              uint32_t plane_idx, ZarrPlan& P) {
     const int64_t gx = (d->size_x + z->chunk_x - 1) / z->chunk_x;
     const int64_t gy = (d->size_y + z->chunk_y - 1) / z->chunk_y;
     const uint64_t cb = (uint64_t)z->chunk_x * z->chunk_y * bpp;
@@ -696,9 +697,11 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
     const uint64_t total = z->offsets[gx * gy];
     for (int64_t i = 0; i < gx * gy; i++) {
         const uint64_t o = z->offsets[i], len = z->offsets[i + 1] - o;
+        const uint64_t ob = o + in_base;  // device offset in the launch's upload buffer
         if (z->offsets[i + 1] < o || z->offsets[i + 1] > total)
             return fail(PBX_E_BADARG, "chunk %lld: bad offsets", (long long)i);
         ZChunk c{};
+        c.plane = plane_idx;
         c.x0 = (int32_t)((i % gx) * z->chunk_x);
         c.y0 = (int32_t)((i / gx) * z->chunk_y);
         c.nbytes = (uint32_t)cb;
@@ -712,7 +715,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
         if (z->codec == PBX_ZARR_RAW) {
             if (len < cb) return fail(PBX_E_BADARG, "chunk %lld: %llu bytes < %llu", (long long)i,
                                       (unsigned long long)len, (unsigned long long)cb);
-            c.src = o;
+            c.src = ob;
             c.flags = ZC_INPUT;
             P.chunks.push_back(c);
             continue;
@@ -720,7 +723,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
         const uint64_t dst = P.scratch;
         if (z->codec == PBX_ZARR_ZLIB) {
             if (len > 0xffffffffull) return fail(PBX_E_BADARG, "chunk %lld too large", (long long)i);
-            P.infl.push_back(ZStream{o, dst, (uint32_t)len, (uint32_t)cb, ZS_ZLIB, 0});
+            P.infl.push_back(ZStream{ob, dst, (uint32_t)len, (uint32_t)cb, ZS_ZLIB, 0});
             c.src = dst;
             P.chunks.push_back(c);
             P.scratch += (cb + 255) & ~255ull;
@@ -737,7 +740,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
         if (cbytes > len || cbytes < 16) return fail(PBX_E_BADARG, "chunk %lld: blosc cbytes %u", (long long)i, cbytes);
         if (flags & 0x2) {  // memcpyed: the unshuffled chunk follows the header
             if (16ull + nbytes > cbytes) return fail(PBX_E_BADARG, "chunk %lld: short memcpyed frame", (long long)i);
-            c.src = o + 16;
+            c.src = ob + 16;
             c.flags = ZC_INPUT;
             P.chunks.push_back(c);
             continue;
@@ -763,7 +766,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
                 pos += 4;
                 if (pos + cs > cbytes || cs > neb || cs == 0)
                     return fail(PBX_E_BADARG, "chunk %lld: block %u split %u size %u", (long long)i, b, s, cs);
-                const ZStream zs{o + pos, dst + (uint64_t)b * bs + (uint64_t)s * neb, cs, neb,
+                const ZStream zs{ob + pos, dst + (uint64_t)b * bs + (uint64_t)s * neb, cs, neb,
                                  cs == neb ? ZS_COPY : (codec == 1 ? ZS_LZ4 : ZS_ZLIB), 0};
                 (cs == neb ? P.copy : codec == 1 ? P.lz4 : P.infl).push_back(zs);
                 pos += cs;
@@ -780,43 +783,70 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, ZarrPl
 
 }  // namespace
 
-int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zarr_chunks* z,
-                            uint64_t* plane_id, double* kernel_ms) {
-    if (!ctx || !d || !z || !plane_id || !z->offsets || (!z->data && z->codec != PBX_ZARR_RAW))
-        return fail(PBX_E_BADARG, "null argument");
-    const int bpp = bpp_of(d->pixel_type);
-    if (!bpp) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
-    if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
-    if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
-    if (z->chunk_x <= 0 || z->chunk_y <= 0) return fail(PBX_E_BADARG, "bad chunk shape");
-    if (z->codec < PBX_ZARR_RAW || z->codec > PBX_ZARR_ZLIB) return fail(PBX_E_BADARG, "bad codec %d", z->codec);
-    {
-        std::lock_guard<std::mutex> g(ctx->reg_mu);
-        auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
-        if (ctx->index.count(key)) return fail(PBX_E_BADARG, "plane already registered");
-        auto im = ctx->images.find(d->image_id);
-        if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
-            return fail(PBX_E_BADARG, "pixel type differs from the image's");
-        if (d->resolution == 0 && im != ctx->images.end() &&
-            (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
-            return fail(PBX_E_BADARG, "plane size differs from the image's");
+int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
+                             const pbx_zarr_chunks* zs, uint64_t* plane_ids, double* kernel_ms) {
+    if (!ctx || !ds || !zs || !plane_ids || n == 0) return fail(PBX_E_BADARG, "null argument");
+    std::vector<std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>> keys;
+    for (uint64_t k = 0; k < n; k++) {
+        const pbx_plane_desc* d = &ds[k];
+        const pbx_zarr_chunks* z = &zs[k];
+        if (!z->offsets || (!z->data && z->codec != PBX_ZARR_RAW)) return fail(PBX_E_BADARG, "null argument");
+        if (!bpp_of(d->pixel_type)) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
+        if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
+        if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
+        if (z->chunk_x <= 0 || z->chunk_y <= 0) return fail(PBX_E_BADARG, "bad chunk shape");
+        if (z->codec < PBX_ZARR_RAW || z->codec > PBX_ZARR_ZLIB) return fail(PBX_E_BADARG, "bad codec %d", z->codec);
+        keys.emplace_back(d->image_id, d->z, d->c, d->t, d->resolution);
     }
+    {
+        auto sorted = keys;
+        std::sort(sorted.begin(), sorted.end());
+        if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+            return fail(PBX_E_BADARG, "the same plane twice in one call");
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        for (uint64_t k = 0; k < n; k++) {
+            const pbx_plane_desc* d = &ds[k];
+            if (ctx->index.count(keys[k])) return fail(PBX_E_BADARG, "plane already registered");
+            auto im = ctx->images.find(d->image_id);
+            if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
+                return fail(PBX_E_BADARG, "pixel type differs from the image's");
+            if (d->resolution == 0 && im != ctx->images.end() &&
+                (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
+                return fail(PBX_E_BADARG, "plane size differs from the image's");
+        }
+    }
+    // host plan: metadata of every chunk of every plane, one upload buffer, one scratch
     ZarrPlan P;
-    if (int rc = zarr_plan(d, z, bpp, P)) return rc;
+    std::vector<uint64_t> in_base(n + 1, 0);
+    int32_t max_cy = 0;
+    for (uint64_t k = 0; k < n; k++) {
+        const pbx_plane_desc* d = &ds[k];
+        const pbx_zarr_chunks* z = &zs[k];
+        const int64_t gx = (d->size_x + z->chunk_x - 1) / z->chunk_x, gy = (d->size_y + z->chunk_y - 1) / z->chunk_y;
+        if (int rc = zarr_plan(d, z, bpp_of(d->pixel_type), in_base[k], (uint32_t)k, P)) return rc;
+        in_base[k + 1] = in_base[k] + ((z->offsets[gx * gy] + 15) & ~15ull);
+        max_cy = std::max(max_cy, z->chunk_y);
+    }
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    const int64_t gx = (d->size_x + z->chunk_x - 1) / z->chunk_x, gy = (d->size_y + z->chunk_y - 1) / z->chunk_y;
-    const uint64_t in_bytes = z->offsets[gx * gy];
-    Plane p;
-    p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
-    p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
-    p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
-    p.pitch = ((int64_t)d->size_x * bpp + 255) & ~(int64_t)255;
-    p.bytes = (size_t)p.pitch * d->size_y + 256;
-    // fill bytes in the stored byte order
-    uint64_t fill = 0;
-    for (int j = 0; j < bpp; j++) {
-        const uint64_t byte = (z->fill_bits >> (8 * j)) & 0xff;
-        fill |= byte << (8 * (p.little_endian || bpp == 1 ? j : bpp - 1 - j));
+    const uint64_t in_bytes = in_base[n];
+    std::vector<Plane> ps(n);
+    std::vector<ZPlane> zp(n);
+    for (uint64_t k = 0; k < n; k++) {
+        const pbx_plane_desc* d = &ds[k];
+        const int bpp = bpp_of(d->pixel_type);
+        Plane& p = ps[k];
+        p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
+        p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
+        p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
+        p.pitch = ((int64_t)d->size_x * bpp + 255) & ~(int64_t)255;
+        p.bytes = (size_t)p.pitch * d->size_y + 256;
+        uint64_t fill = 0;  // fill bytes in the stored byte order
+        for (int j = 0; j < bpp; j++) {
+            const uint64_t byte = (zs[k].fill_bits >> (8 * j)) & 0xff;
+            fill |= byte << (8 * (p.little_endian || bpp == 1 ? j : bpp - 1 - j));
+        }
+        zp[k] = ZPlane{nullptr, p.pitch, d->size_x, d->size_y, zs[k].chunk_x, zs[k].chunk_y,
+                       (uint32_t)bpp, 0, fill};
     }
     const uint32_t nstreams = (uint32_t)(P.lz4.size() + P.infl.size() + P.copy.size());
     std::vector<ZStream> all;
@@ -827,29 +857,46 @@ int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zar
     uint8_t *d_in = nullptr, *d_scr = nullptr;
     ZStream* d_st = nullptr;
     ZChunk* d_ch = nullptr;
+    ZPlane* d_pl = nullptr;
     uint32_t* d_err = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    auto cleanup = [&]() {
+    auto cleanup = [&](bool planes_too) {
         if (d_in) (void)hipFree(d_in);
         if (d_scr) (void)hipFree(d_scr);
         if (d_st) (void)hipFree(d_st);
         if (d_ch) (void)hipFree(d_ch);
+        if (d_pl) (void)hipFree(d_pl);
         if (d_err) (void)hipFree(d_err);
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (planes_too)
+            for (Plane& p : ps) if (p.dev) (void)hipFree(p.dev);
     };
-    hipError_t e = hipMalloc((void**)&p.dev, p.bytes);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_in, in_bytes + 4096);  // decoder window over-read slack (>= ZSLACK)
+    hipError_t e = hipSuccess;
+    for (uint64_t k = 0; k < n && e == hipSuccess; k++) {
+        e = hipMalloc((void**)&ps[k].dev, ps[k].bytes);
+        zp[k].dev = ps[k].dev;
+    }
+    if (e == hipSuccess) e = hipMalloc((void**)&d_in, in_bytes + 4096);  // decoder window over-read slack
     if (e == hipSuccess && P.scratch) e = hipMalloc((void**)&d_scr, P.scratch);
     if (e == hipSuccess && nstreams) e = hipMalloc((void**)&d_st, sizeof(ZStream) * nstreams);
     if (e == hipSuccess) e = hipMalloc((void**)&d_ch, sizeof(ZChunk) * P.chunks.size());
+    if (e == hipSuccess) e = hipMalloc((void**)&d_pl, sizeof(ZPlane) * n);
     if (e == hipSuccess) e = hipMalloc((void**)&d_err, sizeof(uint32_t) * (nstreams + 1));
     for (auto& x : ev) if (e == hipSuccess) e = hipEventCreate(&x);
-    if (e == hipSuccess && in_bytes) e = hipMemcpyAsync(d_in, z->data, in_bytes, hipMemcpyHostToDevice, ctx->stream);
+    for (uint64_t k = 0; k < n && e == hipSuccess; k++) {
+        const uint64_t len = in_base[k + 1] - in_base[k];
+        const int64_t gx = (ds[k].size_x + zs[k].chunk_x - 1) / zs[k].chunk_x;
+        const int64_t gy = (ds[k].size_y + zs[k].chunk_y - 1) / zs[k].chunk_y;
+        const uint64_t used = zs[k].offsets[gx * gy];
+        if (used) e = hipMemcpyAsync(d_in + in_base[k], zs[k].data, used, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess && len > used) e = hipMemsetAsync(d_in + in_base[k] + used, 0, len - used, ctx->stream);
+    }
     if (e == hipSuccess) e = hipMemsetAsync(d_in + in_bytes, 0, 4096, ctx->stream);
     if (e == hipSuccess && nstreams)
         e = hipMemcpyAsync(d_st, all.data(), sizeof(ZStream) * nstreams, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(d_ch, P.chunks.data(), sizeof(ZChunk) * P.chunks.size(), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_pl, zp.data(), sizeof(ZPlane) * n, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d_err, 0, sizeof(uint32_t) * (nstreams + 1), ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ev[0], ctx->stream);
     if (e == hipSuccess)
@@ -857,23 +904,21 @@ int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zar
                                (uint32_t)P.copy.size(), d_in, d_scr, d_err);
     if (e == hipSuccess) e = hipEventRecord(ev[1], ctx->stream);
     if (e == hipSuccess)
-        e = launch_zarr_place(ctx->stream, d_ch, (uint32_t)P.chunks.size(), d_scr, d_in, p.dev, p.pitch,
-                              d->size_x, d->size_y, z->chunk_x, z->chunk_y, (uint32_t)bpp, fill);
+        e = launch_zarr_place(ctx->stream, d_ch, (uint32_t)P.chunks.size(), d_pl, max_cy, d_scr, d_in);
     if (e == hipSuccess) e = hipEventRecord(ev[2], ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream);
+    for (uint64_t k = 0; k < n && e == hipSuccess; k++)
+        e = hipMemsetAsync(ps[k].dev + (size_t)ps[k].pitch * ps[k].size_y, 0, 256, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     std::vector<uint32_t> err(nstreams + 1, 0);
     if (e == hipSuccess && nstreams)
         e = hipMemcpy(err.data(), d_err, sizeof(uint32_t) * nstreams, hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
-        cleanup();
-        (void)hipFree(p.dev);
+        cleanup(true);
         return fail(PBX_E_INTERNAL, "zarr decode: %s", hipGetErrorString(e));
     }
     for (uint32_t s = 0; s < nstreams; s++)
         if (err[s]) {
-            cleanup();
-            (void)hipFree(p.dev);
+            cleanup(true);
             return fail(PBX_E_BADARG, "corrupt chunk stream %u (%s, decoder code %u)", s,
                         s < P.lz4.size() ? "lz4" : s < P.lz4.size() + P.infl.size() ? "zlib" : "stored", err[s]);
         }
@@ -884,25 +929,34 @@ int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zar
         kernel_ms[0] = a;
         kernel_ms[1] = b;
     }
-    cleanup();
+    cleanup(false);
     std::lock_guard<std::mutex> g(ctx->reg_mu);
-    auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
-    if (ctx->index.count(key)) {
-        (void)hipFree(p.dev);
-        return fail(PBX_E_BADARG, "plane already registered");
+    for (uint64_t k = 0; k < n; k++)
+        if (ctx->index.count(keys[k])) {
+            for (Plane& p : ps) (void)hipFree(p.dev);
+            return fail(PBX_E_BADARG, "plane already registered");
+        }
+    for (uint64_t k = 0; k < n; k++) {
+        const pbx_plane_desc* d = &ds[k];
+        Plane& p = ps[k];
+        p.id = ctx->next_id++;
+        ctx->planes[p.id] = p;
+        ctx->index[keys[k]] = p.id;
+        Image& im = ctx->images[d->image_id];
+        if (d->resolution == 0 || im.planes == 0) {
+            im.pixel_type = d->pixel_type;
+            im.size_x = d->size_x;
+            im.size_y = d->size_y;
+        }
+        im.planes++;
+        plane_ids[k] = p.id;
     }
-    p.id = ctx->next_id++;
-    ctx->planes[p.id] = p;
-    ctx->index[key] = p.id;
-    Image& im = ctx->images[d->image_id];
-    if (d->resolution == 0 || im.planes == 0) {
-        im.pixel_type = d->pixel_type;
-        im.size_x = d->size_x;
-        im.size_y = d->size_y;
-    }
-    im.planes++;
-    *plane_id = p.id;
     return PBX_OK;
+}
+
+int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zarr_chunks* z,
+                            uint64_t* plane_id, double* kernel_ms) {
+    return pbx_planes_register_zarr(ctx, 1, d, z, plane_id, kernel_ms);
 }
 
 int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {

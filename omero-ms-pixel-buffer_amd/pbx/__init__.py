@@ -104,7 +104,7 @@ EXPORTS = [
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
     "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
-    "pbx_plane_register_zarr",
+    "pbx_plane_register_zarr", "pbx_planes_register_zarr",
 ]
 
 _lib = None
@@ -139,6 +139,9 @@ def lib() -> ctypes.CDLL:
     L.pbx_plane_register_zarr.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc),
                                           ctypes.POINTER(PbxZarrChunks), ctypes.POINTER(u64),
                                           ctypes.POINTER(ctypes.c_double)]
+    L.pbx_planes_register_zarr.argtypes = [vp, u64, ctypes.POINTER(PbxPlaneDesc),
+                                           ctypes.POINTER(PbxZarrChunks), ctypes.POINTER(u64),
+                                           ctypes.POINTER(ctypes.c_double)]
     L.pbx_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult)]
     L.pbx_test_batch_lz77.argtypes = [vp, vp, vp, vp, u64]
     L.pbx_ctx_stats_get.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
@@ -381,6 +384,40 @@ class PixelsService:
         _check(lib().pbx_plane_register_zarr(self._h, ctypes.byref(d), ctypes.byref(zc),
                                              ctypes.byref(pid), ms))
         return (pid.value, (ms[0], ms[1])) if timing else pid.value
+
+    def register_zarr_planes(self, planes: Sequence[dict], timing: bool = False):
+        """Several Zarr planes decoded by one set of GPU launches (pbx_planes_register_zarr):
+        each dict holds register_zarr_plane's arguments (image_id, z, c, t, pixel_type,
+        size_x, size_y, chunk_x, chunk_y, codec, chunks[, big_endian, fill_bits,
+        resolution]).  All are registered or none.  Returns the plane ids (and the kernels'
+        device ms with timing=True)."""
+        import numpy as np
+        n = len(planes)
+        descs = (PbxPlaneDesc * n)()
+        zcs = (PbxZarrChunks * n)()
+        keep = []
+        for k, p in enumerate(planes):
+            if p["codec"] not in ZARR_CODECS:
+                raise PbxError(400, "unsupported Zarr compressor %r" % (p["codec"],))
+            chunks = p["chunks"]
+            lens = np.array([len(b) if b else 0 for b in chunks], dtype=np.uint64)
+            offsets = np.zeros(len(chunks) + 1, dtype=np.uint64)
+            np.cumsum(lens, out=offsets[1:])
+            data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
+            keep += [offsets, data]
+            d = descs[k]
+            d.image_id, d.z, d.c, d.t = p["image_id"], p["z"], p["c"], p["t"]
+            d.resolution = p.get("resolution", 0)
+            d.pixel_type, d.size_x, d.size_y = p["pixel_type"], p["size_x"], p["size_y"]
+            d.byte_order = BIG_ENDIAN if p.get("big_endian", True) else LITTLE_ENDIAN
+            zc = zcs[k]
+            zc.chunk_x, zc.chunk_y, zc.codec = p["chunk_x"], p["chunk_y"], ZARR_CODECS[p["codec"]]
+            zc.data, zc.offsets, zc.fill_bits = data.ctypes.data, offsets.ctypes.data, p.get("fill_bits", 0)
+        ids = (ctypes.c_uint64 * n)()
+        ms = (ctypes.c_double * 2)()
+        _check(lib().pbx_planes_register_zarr(self._h, n, descs, zcs, ids, ms))
+        del keep
+        return (list(ids), (ms[0], ms[1])) if timing else list(ids)
 
     def register_zarr_array(self, array_dir: str, image_id: int, z: int, c: int, t: int,
                             resolution: int = 0) -> int:

@@ -269,3 +269,40 @@ def test_gpu_zarr_full_size(service, compressor, kw):
     assert np.array_equal(plane_be(service, pid, ">u2", h, w), plane)
     print("%s: decode %.3f ms, place %.3f ms" % (compressor, ms_dec, ms_place))
     service.release_plane(pid)
+
+
+@gpu
+def test_gpu_planes_one_launch(service, oracle):
+    """Several planes (mixed codecs and dtypes) decoded by one pbx_planes_register_zarr call;
+    a corrupt chunk in any of them registers none."""
+    import pbx
+    specs, wants = [], []
+    for k, (comp, kw, dtype, cy, cx) in enumerate([("blosc", {}, ">u2", 128, 128),
+                                                    ("zlib", {"level": 6}, "<u2", 96, 200),
+                                                    ("blosc", {"codec": "zlib"}, ">f4", 64, 64),
+                                                    (None, {}, "u1", 100, 100)]):
+        dt = np.dtype(dtype)
+        plane = _zarr.noise_plane(300, 260, dtype, seed=40 + k)
+        chunks = _zarr.encode_chunks(plane, cy, cx, comp, **kw)
+        chunks[0] = None
+        iid = next(_ids)
+        specs.append(dict(image_id=iid, z=k, c=0, t=0, pixel_type=PT[dt.str[1:]], size_x=260,
+                          size_y=300, chunk_x=cx, chunk_y=cy, codec=comp, chunks=chunks,
+                          big_endian=dt.str[0] != "<", fill_bits=0))
+        want = plane.copy()
+        want[:cy, :cx] = 0
+        wants.append(want)
+    bad = [dict(sp) for sp in specs]
+    ch = list(bad[1]["chunks"])
+    ch[3] = ch[3][:len(ch[3]) // 3]
+    bad[1]["chunks"] = ch
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_planes(bad)
+    assert ei.value.status == 400
+    ids, (ms_dec, ms_place) = service.register_zarr_planes(specs, timing=True)
+    assert len(ids) == 4 and ms_dec > 0
+    for pid, sp, want in zip(ids, specs, wants):
+        dt = want.dtype
+        got = plane_be(service, pid, dt, 300, 260)
+        assert np.array_equal(got.view(np.uint8), want.astype(dt.newbyteorder(">")).view(np.uint8))
+        service.release_plane(pid)
