@@ -178,6 +178,34 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
             return (d >> ((k & 3) * 8)) & 0xffu;
         };
         const uint32_t tok = h[0] & 0xffu;
+        {
+            // common sequence: no length-extension bytes, <= 13 literals, so the literals and
+            // the offset all lie in the 16 header bytes already in SGPRs
+            const uint32_t ll0 = tok >> 4, ml0 = tok & 15;
+            if (ll0 <= 13 && ml0 < 15 && ilen - ip >= 3 + ll0 && ll0 <= o.olen - o.op) {
+                if (ll0) {
+                    const uint32_t bsel = 1 + lane, ws = bsel >> 2;
+                    const uint32_t wv = ws == 0 ? h[0] : ws == 1 ? h[1] : ws == 2 ? h[2] : h[3];
+                    if (lane < ll0) o.ring(o.op + lane) = (uint8_t)(wv >> ((bsel & 3) * 8));
+                    o.op += ll0;  // flushed with the match below (the ring has room)
+                }
+                const uint32_t off = hb(1 + ll0) | hb(2 + ll0) << 8, len = ml0 + 4;
+                ip += 3 + ll0;
+                if (off != 0 && off <= ZR_LZ4 && off <= o.op && len <= o.olen - o.op) {
+                    const uint32_t rep = off < 64 ? lane % off : lane;
+                    const uint32_t v = o.ring(o.op - off + rep);
+                    win.peek16(ip, h);
+                    if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
+                    o.op += len;
+                    o.flush(o.op);
+                } else {
+                    o.flush(o.op);
+                    if (!o.match(off, len)) { bad = 6; break; }
+                    win.peek16(ip, h);
+                }
+                continue;
+            }
+        }
         uint32_t k = 1, ll = tok >> 4;
         if (ll == 15) {
             uint32_t b;
