@@ -143,7 +143,9 @@ struct OutRing {
     __device__ void put1(uint32_t v) {
         if (lane == 0) ring(op) = (uint8_t)v;
         op = rfl(op) + 1;
-        flush(op);
+        // `flushed` is a multiple of 256 and every other writer flushes as it goes, so a
+        // single byte completes a run exactly when op reaches a multiple of 256
+        if ((op & 255u) == 0) flush(op);
     }
 };
 
