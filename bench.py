@@ -194,26 +194,30 @@ def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
                                     "sample": f"{n} of the same chunks, oracle/zarr_oracle.c "
                                               f"(c-blosc frame restatement / zlib 1.2.11) on 16 threads"}
         res[name] = line
-    # the same blosc-lz4 chunks for 4 planes (4 x 512 MiB) in ONE pbx_planes_register_zarr
-    # call: 4x the streams in flight hide the per-stream decode latency
-    with ThreadPoolExecutor(16) as ex:
-        chunks = list(ex.map(lambda c: _zarr.blosc_encode(c.tobytes(), 2), grid))
-    specs = [dict(image_id=22, z=k, c=0, t=0, pixel_type=pbx.UINT16, size_x=side, size_y=side,
-                  chunk_x=chunk, chunk_y=chunk, codec="blosc", chunks=chunks) for k in range(4)]
-    dec, plc = [], []
-    for r in range(reps + 1):
-        ids, (md, mp) = svc.register_zarr_planes(specs, timing=True)
-        if r:
-            dec.append(md)
-            plc.append(mp)
-        for pid in ids:
-            svc.release_plane(pid)
-    md, mp = sum(dec) / reps, sum(plc) / reps
-    raw = 4 * side * side * 2
-    res["blosc_lz4_4_planes_one_launch"] = {
-        "chunks": 4 * len(chunks), "decoded_bytes": raw, "decode_ms": round(md, 3),
-        "place_ms": round(mp, 3), "decoded_gbps": round(raw / ((md + mp) * 1e-3) / 1e9, 1),
-        "chunks_per_s": round(4 * len(chunks) * world / ((md + mp) * 1e-3), 1)}
+    # the same chunks for 4 planes (4 x 512 MiB) in ONE pbx_planes_register_zarr call: 4x the
+    # streams in flight hide the per-stream decode latency
+    for name, comp in (("blosc_lz4", "blosc"), ("zlib1", "zlib")):
+        with ThreadPoolExecutor(16) as ex:
+            if comp == "blosc":
+                chunks = list(ex.map(lambda c: _zarr.blosc_encode(c.tobytes(), 2), grid))
+            else:
+                chunks = list(ex.map(lambda c: _zarr.zlib_encode(c.tobytes(), 1), grid))
+        specs = [dict(image_id=22, z=k, c=0, t=0, pixel_type=pbx.UINT16, size_x=side, size_y=side,
+                      chunk_x=chunk, chunk_y=chunk, codec=comp, chunks=chunks) for k in range(4)]
+        dec, plc = [], []
+        for r in range(reps + 1):
+            ids, (md, mp) = svc.register_zarr_planes(specs, timing=True)
+            if r:
+                dec.append(md)
+                plc.append(mp)
+            for pid in ids:
+                svc.release_plane(pid)
+        md, mp = sum(dec) / reps, sum(plc) / reps
+        raw = 4 * side * side * 2
+        res[name + "_4_planes_one_launch"] = {
+            "chunks": 4 * len(chunks), "decoded_bytes": raw, "decode_ms": round(md, 3),
+            "place_ms": round(mp, 3), "decoded_gbps": round(raw / ((md + mp) * 1e-3) / 1e9, 1),
+            "chunks_per_s": round(4 * len(chunks) * world / ((md + mp) * 1e-3), 1)}
     return res
 
 

@@ -9,13 +9,14 @@
 //   k_zarr_place    per chunk rows: blosc byte-unshuffle + placement into the pitched plane,
 //                   fill value for missing chunks
 //
-// Decoders keep the wave's last ZR output bytes in an LDS ring (the match source for every
-// distance <= ZR) and flush completed 64-byte lines to HBM, so a match never waits on the
-// wave's own global stores; a longer distance reads HBM after a workgroup fence (rare for
-// image chunks: rows are at most a few KB apart).  Sequence/Huffman parsing is wave-uniform:
-// the input is held as a 256-byte window, one dword per lane, read with readlane; a Huffman
-// symbol is decoded by lanes 0..14 testing the 15 code lengths at once (canonical ranges),
-// one ballot picks the length.
+// Decoders keep the wave's last 4 KiB of output in an LDS ring (the match source for every
+// distance <= 4 KiB) and flush completed 256-byte runs to HBM (one dword store per lane), so
+// a match never waits on the wave's own global stores; a longer distance reads HBM after a
+// workgroup fence.  Parse state is wave-uniform and lives in SGPRs (the wave index goes
+// through readfirstlane).  The input is an LDS window of 1 KiB (one 16-byte load per lane);
+// an LZ4 sequence header is one unaligned ds_read_b128 peek.  A Huffman symbol comes from a
+// 512-entry first-level table (codes <= 9 bits) or, for longer codes, from lanes 0..14 testing
+// the 15 code lengths at once (canonical ranges) with one ballot picking the length.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,7 +26,7 @@
 
 namespace pbx {
 
-constexpr uint32_t ZR = 8192;                // LDS output ring per wave (inflate)
+constexpr uint32_t ZR_INF = 4096;            // LDS output ring per wave (inflate): 16 waves/CU
 constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
 constexpr uint32_t ZWAVES = 4;              // waves per workgroup
 constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
@@ -407,7 +408,7 @@ __constant__ uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12,
 constexpr uint32_t ZLENS = 352;
 
 // Per-wave LDS of k_zarr_inflate (byte offsets from the wave's base)
-constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR, ZI_DSYMS = ZI_LSYMS + 2 * 288,
+constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR_INF, ZI_DSYMS = ZI_LSYMS + 2 * 288,
                    ZI_LENS = ZI_DSYMS + 2 * 32, ZI_NEXT = ZI_LENS + ZLENS,
                    ZI_LLUT = ZI_NEXT + 64, ZI_DLUT = ZI_LLUT + 2 * (1u << ZLUT),
                    ZI_BYTES = ZI_DLUT + 2 * (1u << ZLUT);
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
     const ZStream t = st[si];
     BitIn bi{{src + t.src_off, wb + ZI_BYTES, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
     bi.win.load(0);
-    OutRing<ZR> o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR_INF> o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
     HTab lt{0, 0, 0, wb + ZI_LSYMS}, dt{0, 0, 0, wb + ZI_DSYMS};
     uint32_t bad = 0;
     bi.refill();
