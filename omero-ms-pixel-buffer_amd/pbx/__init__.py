@@ -23,7 +23,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
-from typing import Iterable, List, Mapping, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PBX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
@@ -287,6 +287,51 @@ def content_type(fmt: Optional[str]) -> str:
 
 # --------------------------------------------------------------------- PixelsService
 
+def zarr_array_meta(array_dir: str) -> dict:
+    """The .zarray of a Zarr v2 array directory, checked for what the GPU decode supports."""
+    import json
+    with open(os.path.join(array_dir, ".zarray")) as f:
+        meta = json.load(f)
+    if meta.get("zarr_format") != 2 or meta.get("order", "C") != "C" or meta.get("filters"):
+        raise PbxError(400, "only Zarr v2 C-order arrays without filters are supported")
+    if meta["dtype"][1:] not in _ZARR_DTYPES:
+        raise PbxError(400, "unsupported dtype %s" % meta["dtype"])
+    if len(meta["shape"]) < 2 or len(meta["shape"]) > 5 or any(cs != 1 for cs in meta["chunks"][:-2]):
+        raise PbxError(400, "need shape [..., y, x] with one plane per chunk")
+    return meta
+
+
+def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, resolution: int = 0,
+                    meta: Optional[dict] = None) -> dict:
+    """register_zarr_planes() arguments for plane (z, c, t) of an NGFF array directory (NGFF
+    axis order t, c, z, y, x; fewer leading axes drop from the left): chunk files named by
+    dimension_separator "." or "/", absent files = fill_value."""
+    import numpy as np
+    meta = meta or zarr_array_meta(array_dir)
+    shape, chunk, dt = meta["shape"], meta["chunks"], meta["dtype"]
+    comp = meta.get("compressor")
+    k = len(shape) - 2
+    lead, dropped = [t, c, z][3 - k:], [t, c, z][:3 - k]
+    if any(dropped):
+        raise PbxError(404, "plane (z=%d, c=%d, t=%d) outside the array" % (z, c, t))
+    for v, n in zip(lead, shape[:-2]):
+        if not 0 <= v < n:
+            raise PbxError(404, "plane (z=%d, c=%d, t=%d) outside the array" % (z, c, t))
+    sep = meta.get("dimension_separator", ".")
+    sy, sx, cy, cx = shape[-2], shape[-1], chunk[-2], chunk[-1]
+    chunks = []
+    for j in range(-(-sy // cy)):
+        for i in range(-(-sx // cx)):
+            path = os.path.join(array_dir, sep.join(str(v) for v in lead + [j, i]))
+            chunks.append(open(path, "rb").read() if os.path.exists(path) else None)
+    native = np.dtype(dt).newbyteorder("=")
+    fill_bits = int(np.array([meta.get("fill_value") or 0], dtype=native).view("u%d" % native.itemsize)[0])
+    return dict(image_id=image_id, z=z, c=c, t=t, resolution=resolution,
+                pixel_type=_ZARR_DTYPES[dt[1:]], size_x=sx, size_y=sy, chunk_x=cx, chunk_y=cy,
+                codec=None if comp is None else comp.get("id"), chunks=chunks,
+                big_endian=dt[0] != "<", fill_bits=fill_bits)
+
+
 class PixelsService:
     """Plane registry on one MI355X (the PixelsService / getPixels stand-in).
 
@@ -425,37 +470,22 @@ class PixelsService:
         shape [..., y, x], NGFF order t, c, z, y, x) — what ZarrPixelBuffer reads through
         JZarr (omero-zarr-pixel-buffer 0.6.1, build.gradle:57).  Chunks of the plane are read
         from disk here and decoded on the GPU."""
-        import json
-        with open(os.path.join(array_dir, ".zarray")) as f:
-            meta = json.load(f)
-        if meta.get("zarr_format") != 2 or meta.get("order", "C") != "C" or meta.get("filters"):
-            raise PbxError(400, "only Zarr v2 C-order arrays without filters are supported")
-        shape, chunk = meta["shape"], meta["chunks"]
-        dt = meta["dtype"]
-        if dt[1:] not in _ZARR_DTYPES:
-            raise PbxError(400, "unsupported dtype %s" % dt)
-        comp = meta.get("compressor")
-        codec = None if comp is None else comp.get("id")
-        lead = [t, c, z][-(len(shape) - 2):] if len(shape) > 2 else []
-        lead_idx = [v // cs for v, cs in zip(lead, chunk[:-2])]
-        sep = meta.get("dimension_separator", ".")
-        sy, sx, cy_, cx_ = shape[-2], shape[-1], chunk[-2], chunk[-1]
-        gy, gx = -(-sy // cy_), -(-sx // cx_)
-        if any(cs != 1 for cs in chunk[:-2]):
-            raise PbxError(400, "chunks spanning several planes are not supported")
-        chunks = []
-        for j in range(gy):
-            for i in range(gx):
-                key = sep.join(str(v) for v in lead_idx + [j, i])
-                path = os.path.join(array_dir, key)
-                chunks.append(open(path, "rb").read() if os.path.exists(path) else None)
-        fill = meta.get("fill_value") or 0
-        import numpy as np
-        native = np.dtype(dt).newbyteorder("=")
-        fill_bits = int(np.array([fill], dtype=native).view("u%d" % native.itemsize)[0])
-        return self.register_zarr_plane(image_id, z, c, t, _ZARR_DTYPES[dt[1:]], sx, sy, cx_, cy_,
-                                        codec, chunks, big_endian=dt[0] != "<",
-                                        fill_bits=fill_bits, resolution=resolution)
+        sp = zarr_plane_spec(array_dir, image_id, z, c, t, resolution)
+        return self.register_zarr_planes([sp])[0]
+
+    def register_zarr_array_planes(self, array_dir: str, image_id: int,
+                                   planes: Optional[Sequence[Tuple[int, int, int]]] = None,
+                                   resolution: int = 0) -> Dict[Tuple[int, int, int], int]:
+        """Every (z, c, t) plane of an NGFF array (or the given ones) decoded by ONE set of GPU
+        launches (pbx_planes_register_zarr).  Returns {(z, c, t): plane id}."""
+        meta = zarr_array_meta(array_dir)
+        lead = list(meta["shape"][:-2])
+        lead = [1] * (3 - len(lead)) + lead  # (t, c, z) extents
+        if planes is None:
+            planes = [(z, c, t) for t in range(lead[0]) for c in range(lead[1]) for z in range(lead[2])]
+        specs = [zarr_plane_spec(array_dir, image_id, z, c, t, resolution, meta) for z, c, t in planes]
+        ids = self.register_zarr_planes(specs)
+        return dict(zip([tuple(p) for p in planes], ids))
 
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))

@@ -90,6 +90,49 @@ def test_oracle_plane_assembly(oracle):
     assert np.array_equal(got, want)
 
 
+def _write_ngff(root, shape, chunks, dtype, sep, compressor, fill=0, skip=()):
+    """A Zarr v2 array directory; returns {lead index tuple: plane array}."""
+    root.mkdir(parents=True, exist_ok=True)
+    meta = {"zarr_format": 2, "shape": list(shape), "chunks": list(chunks), "dtype": dtype,
+            "order": "C", "fill_value": fill, "filters": None, "dimension_separator": sep,
+            "compressor": None if compressor is None else {"id": compressor}}
+    (root / ".zarray").write_text(json.dumps(meta))
+    planes = {}
+    for lead in np.ndindex(*shape[:-2]):
+        p = _zarr.noise_plane(shape[-2], shape[-1], dtype, seed=sum(lead) + 7)
+        planes[lead] = p
+        gx = -(-shape[-1] // chunks[-1])
+        for k, ch in enumerate(_zarr.encode_chunks(p, chunks[-2], chunks[-1], compressor)):
+            j, i = divmod(k, gx)
+            if (lead, j, i) in skip:
+                continue
+            path = root / sep.join(str(v) for v in list(lead) + [j, i])
+            path.parent.mkdir(parents=True, exist_ok=True)
+            path.write_bytes(ch)
+    return planes
+
+
+@pytest.mark.parametrize("ndim,sep", [(5, "/"), (3, "."), (2, ".")])
+def test_ngff_plane_spec(tmp_path, ndim, sep):
+    """NGFF array reading on the host (which chunk files belong to a plane, dtype, fill)."""
+    import pbx
+    shape = [2, 3, 4, 70, 90][5 - ndim:]
+    chunks = [1] * (ndim - 2) + [32, 40]
+    lead0 = tuple([1, 2, 3][3 - (ndim - 2):]) if ndim > 2 else ()
+    planes = _write_ngff(tmp_path / "a", shape, chunks, "<u2", sep, "zlib", fill=9,
+                         skip={(lead0, 1, 2)})
+    z, c, t = (3 if ndim >= 3 else 0), (2 if ndim >= 4 else 0), (1 if ndim >= 5 else 0)
+    sp = pbx.zarr_plane_spec(str(tmp_path / "a"), 77, z, c, t)
+    assert (sp["size_x"], sp["size_y"], sp["chunk_x"], sp["chunk_y"]) == (90, 70, 40, 32)
+    assert sp["pixel_type"] == pbx.UINT16 and sp["big_endian"] is False and sp["fill_bits"] == 9
+    assert sp["codec"] == "zlib" and len(sp["chunks"]) == 3 * 3
+    assert sp["chunks"][1 * 3 + 2] is None  # the skipped chunk file
+    dec = zlib.decompress(sp["chunks"][0])
+    assert dec == _zarr.chunk_grid(planes[lead0], 32, 40)[0].tobytes()
+    with pytest.raises(pbx.PbxError):
+        pbx.zarr_plane_spec(str(tmp_path / "a"), 77, 99 if ndim >= 3 else 0, c, t + (ndim < 3))
+
+
 # ----------------------------------------------------------------------------- GPU
 gpu = pytest.mark.gpu
 
@@ -305,4 +348,21 @@ def test_gpu_planes_one_launch(service, oracle):
         dt = want.dtype
         got = plane_be(service, pid, dt, 300, 260)
         assert np.array_equal(got.view(np.uint8), want.astype(dt.newbyteorder(">")).view(np.uint8))
+        service.release_plane(pid)
+
+
+@gpu
+def test_gpu_ngff_all_planes_one_call(service, tmp_path):
+    """register_zarr_array_planes: every (z, c, t) plane of an NGFF array in one launch."""
+    import pbx
+    planes = _write_ngff(tmp_path / "img", [2, 2, 3, 200, 300], [1, 1, 1, 128, 128], ">u2", "/",
+                         "blosc")
+    iid = next(_ids)
+    ids = service.register_zarr_array_planes(str(tmp_path / "img"), iid)
+    assert len(ids) == 12
+    for (z, c, t), pid in ids.items():
+        assert np.array_equal(plane_be(service, pid, ">u2", 200, 300), planes[(t, c, z)])
+    st, raw = service.get_tile(pbx.TileCtx(iid, 2, 1, 1, 10, 20, 30, 40))
+    assert st == 0 and raw == planes[(1, 1, 2)][20:60, 10:40].tobytes()
+    for pid in ids.values():
         service.release_plane(pid)
