@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void k_zarr_copy(const ZStream* __restrict__ s
 // One workgroup per (chunk, band of ZP_ROWS chunk rows).  Each thread makes one sample:
 // blosc byte-unshuffle (typesize ts within blocks of `blocksize` bytes) + copy into the
 // plane (samples stay in the array's byte order); missing chunks get the fill bytes.
-constexpr uint32_t ZP_ROWS = 8;
+constexpr uint32_t ZP_ROWS = 16;
 
 __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ ch, uint32_t bands,
                                                     const ZPlane* __restrict__ planes,
@@ -599,13 +599,16 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
     const uint8_t* s = (c.flags & ZC_INPUT ? input : scratch) + c.src;
     const uint32_t ts = c.typesize, bs = c.blocksize, nb = c.nbytes;
     const bool missing = (c.flags & ZC_MISSING) != 0;
-    for (int32_t r = r0; r < r1; r++) {
-        uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
-        // fast path: 4 samples per thread, one (unaligned) dword load per byte plane
-        int32_t done = 0;
-        if (!missing && (ts == 1 || ts == bpp) && (bpp == 1 || bpp == 2 || bpp == 4)) {
-            const int32_t w4 = w & ~3;
-            for (int32_t c4 = 4 * (int32_t)threadIdx.x; c4 < w4; c4 += 1024) {
+    const bool fast = !missing && (ts == 1 || ts == bpp) && (bpp == 1 || bpp == 2 || bpp == 4);
+    const int32_t w4 = fast ? (w & ~3) : 0;
+    // fast path: 4 samples per thread, one (unaligned) dword load per byte plane; the band's
+    // (row, 4-sample group) pairs are spread over all 256 threads
+    if (w4 > 0) {
+        const int32_t groups = w4 >> 2, total = (r1 - r0) * groups;
+        for (int32_t g = (int32_t)threadIdx.x; g < total; g += 256) {
+            const int32_t r = r0 + g / groups, c4 = 4 * (g - (g / groups) * groups);
+            uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
+            {
                 const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)c4;
                 uint32_t out[4];
                 if (ts == 1) {
@@ -643,9 +646,11 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
                 else if (bpp == 2) __builtin_memcpy(d, out, 8);
                 else __builtin_memcpy(d, out, 16);
             }
-            done = w4;
         }
-        for (int32_t col = done + (int32_t)threadIdx.x; col < w; col += 256) {
+    }
+    for (int32_t r = r0; r < r1; r++) {
+        uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
+        for (int32_t col = w4 + (int32_t)threadIdx.x; col < w; col += 256) {
             const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
             for (uint32_t j = 0; j < bpp; j++) {
                 uint32_t v;
