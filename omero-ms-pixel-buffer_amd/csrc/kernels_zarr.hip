@@ -525,6 +525,11 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
         // block data
         for (;;) {
             bi.refill();
+            // distance-table entries at every bit offset of the buffer, gathered in the same
+            // LDS round trip as the literal/length lookup: a match's distance code then costs
+            // a readlane instead of a second dependent round trip
+            const uint32_t cnt0 = bi.cnt;
+            const uint32_t dv = lds16(wb + ZI_DLUT + 2 * ((uint32_t)(bi.buf >> lane) & ((1u << ZLUT) - 1)));
             const int sym = decode_fast(lt, wb + ZI_LLUT, bi, lane);
             if (sym < 0) { bad = 21; break; }
             if (sym < 256) {
@@ -535,10 +540,17 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             if (sym == 256) break;
             const uint32_t ls = (uint32_t)sym - 257;
             if (ls >= 29) { bad = 23; break; }
-            bi.refill();
+            // >= 17 bits are left after a <= 15-bit code (refill leaves >= 32): no refill
             const uint32_t len = c_lbase[ls] + bi.bits(c_lext[ls]);
-            bi.refill();
-            const int ds = decode_fast(dt, wb + ZI_DLUT, bi, lane);
+            int ds;
+            const uint32_t de = rdl(dv, cnt0 - bi.cnt);
+            if (de != 0xFFFF && (de >> 9) <= bi.cnt) {
+                bi.bits(de >> 9);
+                ds = (int)(de & 511);
+            } else {
+                bi.refill();
+                ds = decode_fast(dt, wb + ZI_DLUT, bi, lane);
+            }
             if (ds < 0 || ds >= 30) { bad = 24; break; }
             bi.refill();
             const uint32_t dist = c_dbase[ds] + bi.bits(c_dext[ds]);
