@@ -803,6 +803,14 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
         std::sort(sorted.begin(), sorted.end());
         if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
             return fail(PBX_E_BADARG, "the same plane twice in one call");
+        for (uint64_t a = 0; a < n; a++)  // planes of one image agree with each other too
+            for (uint64_t b = a + 1; b < n; b++)
+                if (ds[a].image_id == ds[b].image_id &&
+                    (ds[a].pixel_type != ds[b].pixel_type ||
+                     (ds[a].resolution == 0 && ds[b].resolution == 0 &&
+                      (ds[a].size_x != ds[b].size_x || ds[a].size_y != ds[b].size_y))))
+                    return fail(PBX_E_BADARG, "planes of image %lld disagree on type or size",
+                                (long long)ds[a].image_id);
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         for (uint64_t k = 0; k < n; k++) {
             const pbx_plane_desc* d = &ds[k];

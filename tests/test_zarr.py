@@ -342,6 +342,10 @@ def test_gpu_planes_one_launch(service, oracle):
     with pytest.raises(pbx.PbxError) as ei:
         service.register_zarr_planes(bad)
     assert ei.value.status == 400
+    clash = [dict(specs[0]), dict(specs[0], z=9, size_x=259)]  # same image, other size
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_planes(clash)
+    assert ei.value.status == 400
     ids, (ms_dec, ms_place) = service.register_zarr_planes(specs, timing=True)
     assert len(ids) == 4 and ms_dec > 0
     for pid, sp, want in zip(ids, specs, wants):
