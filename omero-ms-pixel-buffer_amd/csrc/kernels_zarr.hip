@@ -195,7 +195,13 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
                 const uint32_t off = hb(1 + ll0) | hb(2 + ll0) << 8, len = ml0 + 4;
                 ip += 3 + ll0;
                 if (off != 0 && off <= ZR_LZ4 && off <= o.op && len <= o.olen - o.op) {
-                    const uint32_t rep = off < 64 ? lane % off : lane;
+                    // lane % off for off < 64 without an integer division: lane / off is
+                    // exact to within 1/63 in float, so +0.001 never crosses an integer
+                    uint32_t rep = lane;
+                    if (off < 64) {
+                        const float inv = __builtin_amdgcn_rcpf((float)off);
+                        rep = lane - off * (uint32_t)((float)lane * inv + 0.001f);
+                    }
                     const uint32_t v = o.ring(o.op - off + rep);
                     win.peek16(ip, h);
                     if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
