@@ -118,9 +118,16 @@ struct OutRing {
         flushed = op;
     }
     // out[op .. op+len) = out[op-off .. op-off+len) (overlapping: period off)
+    // lane % off for off < 64 without an integer division: lane / off is exact to within 1/63
+    // in float, so +0.001 never crosses an integer
+    __device__ uint32_t period_lane(uint32_t off) const {
+        if (off >= 64) return lane;
+        const float inv = __builtin_amdgcn_rcpf((float)off);
+        return lane - off * (uint32_t)((float)lane * inv + 0.001f);
+    }
     __device__ bool match(uint32_t off, uint32_t len) {
         if (off == 0 || off > op || len > olen - op) return false;
-        const uint32_t rep = off < 64 ? lane % off : lane;
+        const uint32_t rep = period_lane(off);
         if (off > ZR) {
             // a far source lies below `flushed`: wait for this wave's stores, read HBM
             for (uint32_t k = 0; k < len; k += 64) {
@@ -195,13 +202,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
                 const uint32_t off = hb(1 + ll0) | hb(2 + ll0) << 8, len = ml0 + 4;
                 ip += 3 + ll0;
                 if (off != 0 && off <= ZR_LZ4 && off <= o.op && len <= o.olen - o.op) {
-                    // lane % off for off < 64 without an integer division: lane / off is
-                    // exact to within 1/63 in float, so +0.001 never crosses an integer
-                    uint32_t rep = lane;
-                    if (off < 64) {
-                        const float inv = __builtin_amdgcn_rcpf((float)off);
-                        rep = lane - off * (uint32_t)((float)lane * inv + 0.001f);
-                    }
+                    const uint32_t rep = o.period_lane(off);
                     const uint32_t v = o.ring(o.op - off + rep);
                     win.peek16(ip, h);
                     if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
 #endif
         const uint32_t len = ml + 4;
         if (len <= 64 && off <= ZR_LZ4 && off != 0 && off <= o.op && len <= o.olen - o.op) {
-            const uint32_t rep = off < 64 ? lane % off : lane;
+            const uint32_t rep = o.period_lane(off);
             const uint32_t v = o.ring(o.op - off + rep);
             win.peek16(ip, h);
             if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
