@@ -10,13 +10,19 @@ left in HBM.  Inputs are resident before the timed region; D2H is reported separ
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU); ranks only meet at the
-barrier and the max-over-ranks of the step time (gloo, CPU tensors).
+One rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one rank.
+Otherwise `--gpus N` with N > 1 makes this process a launcher that touches no GPU: it
+starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment),
+and only rank 0 prints the JSON line.  Ranks only meet at the barrier and the max-over-ranks
+of the step time (gloo, CPU tensors): no collective on the data path.  `--dry-run` runs the
+rank plumbing (launch, barrier, max) without any HIP call (CPU test of the N > 1 path).
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -241,12 +247,107 @@ def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
     return res
 
 
+class ServeStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("requests", "ok", "bytes", "batches")] + \
+               [(n, ctypes.c_double) for n in ("seconds", "p50_us", "p90_us", "p99_us", "max_us",
+                                               "mean_us")]
+
+
+def serve_lines(svc, iid, threads=(32, 128, 512)):
+    """The served path as the reference drives it: T worker threads (Vert.x
+    worker_pool_size, PixelBufferMicroserviceVerticle.java:117-118,224-233), each blocking in
+    one getTile at a time -> pbx_get_tile (coalesced into GPU batches), D2H and the JNI-style
+    copy of every body included.  Native threads (lib/libpbx_servebench.so), no Python in the
+    loop.  512x512 uint16 PNG tiles of the headline plane."""
+    L = ctypes.CDLL(os.path.join(ROOT, "omero-ms-pixel-buffer_amd", "lib", "libpbx_servebench.so"))
+    L.pbx_serve_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ServeStats)]
+    ctxs = grid_ctxs(iid, "png")
+    reqs = pbx.make_reqs(ctxs)
+    res = {}
+    for t in threads:
+        s = ServeStats()
+        total = max(8192, 16 * t)
+        rc = L.pbx_serve_bench(svc.handle, reqs, len(ctxs), t, total, 2 * t, ctypes.byref(s))
+        if rc != 0:
+            raise RuntimeError(f"pbx_serve_bench: {rc}")
+        res[f"threads_{t}"] = {
+            "tiles_per_s": round(s.ok / s.seconds, 1), "requests": s.requests, "ok": s.ok,
+            "requests_per_batch": round(s.requests / max(s.batches, 1), 1),
+            "p50_ms": round(s.p50_us / 1e3, 3), "p90_ms": round(s.p90_us / 1e3, 3),
+            "p99_ms": round(s.p99_us / 1e3, 3), "max_ms": round(s.max_us / 1e3, 3),
+            "d2h_gbps": round(s.bytes / s.seconds / 1e9, 1)}
+    return res
+
+
+def run_stream(svc, req_chunks, barrier, warmup=1, steps=1):
+    """Timed passes over a request stream cut into batches (pipelined two deep: batch k+1
+    planned and launched while k runs); returns (seconds for `steps` passes, last stats)."""
+    def one_pass():
+        stats, prev = [], None
+        for r in list(req_chunks) + [None]:
+            b = None
+            if r is not None:
+                b = pbx.Batch(svc, reqs=r)
+                b.launch()
+            if prev is not None:
+                prev.sync()
+                stats.append(prev.stats())
+                prev.close()
+            prev = b
+        return stats
+    for _ in range(warmup):
+        one_pass()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        stats = one_pass()
+    torch.cuda.synchronize()
+    barrier()
+    return (time.perf_counter() - t0) / steps, stats
+
+
+def wholeslide_line(svc, rank, world, barrier, steps=2, side=100000, channels=5, tile=512,
+                    band_batch_rows=49):
+    """configs[3]: this rank's tile-row band of all 5 channels of a 100000^2 uint16 slide as
+    TIFF (uncompressed = the reference's TiffWriter default, or Compression=8 when the
+    service deflates TIFF), in batches of `band_batch_rows` tile rows (bounded arenas)."""
+    n = (side + tile - 1) // tile
+    pids = [svc.register_plane(4, 0, c, 0, pbx.UINT16, side, side, generator="noise",
+                               plane_no=c) for c in range(channels)]
+    lo, hi = pbx.band_rows(n, world, rank)
+    chunks, ntiles = [], 0
+    for c in range(channels):
+        for r0 in range(lo, hi, band_batch_rows):
+            ctxs = [pbx.TileCtx(4, 0, c, 0, tile * tx, tile * ty, min(tile, side - tile * tx),
+                                min(tile, side - tile * ty), format="tif")
+                    for ty in range(r0, min(hi, r0 + band_batch_rows)) for tx in range(n)]
+            ntiles += len(ctxs)
+            chunks.append(pbx.make_reqs(ctxs))
+    dt, stats = run_stream(svc, chunks, barrier, warmup=1, steps=steps)
+    in_bytes = sum(s.in_bytes for s in stats)
+    out_bytes = sum(s.out_bytes for s in stats)
+    line = {"tiles_this_rank": ntiles, "tiles_all_ranks": n * n * channels,
+            "tiles_per_s": round(ntiles * world / dt, 1), "ms_per_pass": round(dt * 1e3, 2),
+            "pixel_bytes": in_bytes, "response_bytes": out_bytes,
+            "d2h_bytes_saved_vs_uncompressed": int(in_bytes + ntiles * 160 - out_bytes)}
+    ext = sum(s.ms_extract for s in stats)
+    if out_bytes >= in_bytes:  # uncompressed: the HBM-bound k_extract does all the work
+        line["k_extract_gbps"] = round(2 * in_bytes / (ext * 1e-3) / 1e9, 1)
+    for pid in pids:
+        svc.release_plane(pid)
+    return line
+
+
 def extra(out, svc, rank, world, barrier, iid, side):
     """Secondary lines: the other BASELINE configs (parity-tested in tests/), each timed
     device-resident like the headline; and the PCIe-inclusive end-to-end rate."""
     # PCIe-inclusive end-to-end (D2H of every PNG into pinned host memory)
     rate, gbs = e2e_rate(svc, grid_ctxs(iid, "png"))
     out["e2e_with_d2h"] = {"tiles_per_s": round(rate, 1), "d2h_gbps": round(gbs, 1)}
+    # the served path: concurrent single-tile callers through the coalescer
+    out["served_get_tile_512x512_u16_png"] = serve_lines(svc, iid)
     # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
     raw = grid_ctxs(iid, None)
     dtr, sr, _ = run_steps(svc, raw, 5, 2, barrier)
@@ -298,18 +399,14 @@ def extra(out, svc, rank, world, barrier, iid, side):
     out["c3_png_4096x1024x1024_u16"] = {
         "tiles_per_s": round(len(c3) * 2 * world / dt3, 1),
         "compressed_bytes_per_tile": round(s3[-1].deflate_out_bytes / len(c3), 1)}
-    # configs[3]: whole slide 100000^2 uint16, 512^2 tiles (edge 160 px) -> TIFF; this rank's
-    # band of tile rows of one channel (the 5 channels are independent, equal cost)
-    n = (100000 + 511) // 512
-    svc.register_plane(4, 0, 0, 0, pbx.UINT16, 100000, 100000, generator="noise", plane_no=rank)
-    lo, hi = pbx.band_rows(n, world, rank)
-    c4 = [pbx.TileCtx(4, 0, 0, 0, 512 * tx, 512 * ty, min(512, 100000 - 512 * tx),
-                      min(512, 100000 - 512 * ty), format="tif")
-          for ty in range(lo, hi) for tx in range(n)]
-    dt4, s4, _ = run_steps(svc, c4, 3, 2, barrier)
-    out["c4_wholeslide_tif_100k_u16_1ch"] = {
-        "tiles": len(c4) * world, "tiles_per_s": round(len(c4) * 3 * world / dt4, 1),
-        "k_extract_gbps": round(2 * s4[-1].in_bytes / (mean(s4, "ms_extract") * 1e-3) / 1e9, 1)}
+    # configs[3]: whole slide 100000^2 x 5 channels uint16, 512^2 tiles (edge 160 px) -> TIFF.
+    # Every rank holds the 5 channels and serves its contiguous band of tile rows of each
+    # (SURVEY.md §8(e)); over all ranks the bands cover the whole slide (192,080 tiles).
+    out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
+    svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
+    with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
+        out["c4_wholeslide_tif_deflate_100k_u16_5ch"] = wholeslide_line(sd, rank, world, barrier,
+                                                                        steps=1)
     # configs[4]: mixed stream (uint8/int32/float32 planes 16384^2, w,h in 256..2048,
     # png/tif/raw), 16384 requests as 8 batches of 2048
     import random
@@ -354,6 +451,59 @@ def extra(out, svc, rank, world, barrier, iid, side):
                                       "ok": ok, "errors_404": err}
 
 
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: start N rank processes of this script and wait.
+
+    This process never touches the GPU (it only imported torch; nothing here initialises
+    HIP), so the ranks are plain child processes, not an exec.  If one rank fails, the
+    others (which would wait at the barrier forever) are terminated by PID."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:
+                    q.terminate()
+    return rc
+
+
+def dry_run(args, world, rank):
+    """The N > 1 plumbing without HIP: rendezvous, barrier, timed no-op steps, max-over-ranks."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    met = torch.ones(1, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(met)
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "tiles/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "ranks_met": int(met[0]), "max_step_s": float(t[0])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -362,11 +512,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (launch, barrier, max), no HIP call")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)",
+              file=sys.stderr)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 3
+#define PBX_ABI_VERSION 4
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -94,7 +94,9 @@ int pbx_device_count(void);
 typedef struct pbx_plane_desc {
     int64_t image_id;
     int32_t z, c, t;
-    int32_t resolution;      /* 0 = full resolution (PixelBuffer.setResolutionLevel, :89-91) */
+    int32_t resolution;      /* STORED pyramid level: 0 = full resolution, k = k-th downsampled
+                                level (the NGFF multiscales dataset index).  Requests use
+                                OMERO's numbering instead: see pbx_tile_req.resolution. */
     int32_t pixel_type;      /* enum pbx_pixel_type */
     int32_t size_x, size_y;
     int32_t byte_order;      /* enum pbx_byte_order of host_data (ignored for generators) */
@@ -154,11 +156,20 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* des
 /* Copy a registered plane back to the host, samples in big-endian order (test hook). */
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t plane_id, void* out, uint64_t bytes);
 
+/* TileCtx.resolution == null (TileCtx.java:86-88): the pixel buffer's default level. */
+#define PBX_RESOLUTION_NONE (-1)
+
 /* TileCtx (TileCtx.java:36-54, parsed at :67-90). */
 typedef struct pbx_tile_req {
     int64_t image_id;
     int32_t z, c, t;
-    int32_t resolution;      /* -1 = not given */
+    int32_t resolution;      /* OMERO PixelBuffer.setResolutionLevel numbering
+                                (TileRequestHandler.java:89-91): with L stored levels,
+                                L-1 = full resolution, 0 = the smallest level; stored level
+                                = L-1-resolution.  PBX_RESOLUTION_NONE = not given (full
+                                resolution).  Outside [0, L), or any other negative value:
+                                setResolutionLevel throws -> getTile null -> 404.  A binding
+                                maps a given negative Integer to a value < -1. */
     int32_t x, y, w, h;      /* w/h == 0 -> plane size (TileRequestHandler.java:92-97) */
     int32_t format;          /* enum pbx_format */
     int32_t reserved;
@@ -232,6 +243,10 @@ int pbx_bytes_per_pixel(int32_t pixel_type);
 
 /* Batches launched and requests served so far by this context (coalescing check). */
 int pbx_ctx_stats_get(pbx_ctx* ctx, uint64_t* batches, uint64_t* requests);
+
+/* Free the context's cached (currently unused) device and pinned batch buffers; buffers
+ * of batches still alive stay (torch.cuda.empty_cache analogue). */
+int pbx_release_cached(pbx_ctx* ctx);
 
 /* Synchronise the context's device (bench/test hook). */
 int pbx_device_synchronize(pbx_ctx* ctx);

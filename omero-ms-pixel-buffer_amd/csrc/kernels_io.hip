@@ -9,6 +9,7 @@
 // HBM-bound byte work: 16-byte loads/stores, byte swaps in registers, no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <type_traits>
 
 #include "dev_util.h"
@@ -440,14 +441,20 @@ hipError_t launch_rows(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
     if (!ntiles || !nblocks) return hipSuccess;
     const size_t lds = rows_lds_bytes(max_rb);
     if (lds > 64 * 1024) {
-        static bool raised = false;  // bands of rows over 4 KiB: allow up to 160 KiB of LDS
-        if (!raised) {
-            const hipError_t e = hipFuncSetAttribute((const void*)k_rows,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     160 * 1024);
-            if (e != hipSuccess) return e;
-            raised = true;
-        }
+        // bands of rows over 4 KiB: allow up to 160 KiB of LDS.  The attribute belongs to the
+        // current device, so it is raised once per device (thread-safe).
+        constexpr int kMaxDev = 64;
+        static std::once_flag once[kMaxDev];
+        static hipError_t res[kMaxDev];
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+        std::call_once(once[dev], [&] {
+            res[dev] = hipFuncSetAttribute((const void*)k_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        });
+        if (res[dev] != hipSuccess) return res[dev];
     }
     hipLaunchKernelGGL(k_rows, dim3(nblocks), dim3(RB_NT), lds, st, d_tiles, ntiles, stream);
     return hipGetLastError();

@@ -453,7 +453,10 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             uint32_t done = 0;
             while (done < len && bi.cnt >= 8 && o.op < o.olen) { o.put1(bi.bits(8)); done++; }
             if (done < len && bi.cnt >= 8) { bad = 12; break; }
-            const uint32_t q = bi.ipos, rest = len - done;
+            // a block shorter than the buffered bytes (LEN 0..3: e.g. the empty stored block
+            // of a sync flush) leaves whole bytes of what FOLLOWS it in the buffer: rewind
+            // the input over them (cnt is a multiple of 8 here) instead of dropping them
+            const uint32_t q = bi.ipos - bi.cnt / 8, rest = len - done;
             if (q + rest > bi.ilen || rest > o.olen - o.op) { bad = 12; break; }
             for (uint32_t k = 0; k < rest; k += 64) {
                 const uint32_t nb = rest - k < 64 ? rest - k : 64;

@@ -69,18 +69,30 @@ struct Plane {
 struct Image {
     int32_t pixel_type = 0, size_x = 0, size_y = 0;
     int32_t planes = 0;
+    std::map<int32_t, int32_t> level_planes;  // stored pyramid level -> registered planes
+    // PixelBuffer.getResolutionLevels(): the number of stored levels (0 .. max)
+    int32_t levels() const { return level_planes.empty() ? 0 : level_planes.rbegin()->first + 1; }
 };
 
 // Grow-only caching allocator for device and pinned host blocks (power-of-two classes).
 struct Pool {
-    bool pinned = false;
+    bool pinned = false;  // pinned host blocks: power-of-two classes from 4 MiB (few, reused)
     std::mutex mu;
     std::multimap<size_t, void*> free_blocks;
     std::unordered_map<void*, size_t> sizes;
 
-    static size_t cls(size_t n) {
-        size_t c = 1 << 20;
+    // size classes: 1 MiB, then 2^k x {1, 1.25, 1.5, 1.75} (at most 25% slack per block)
+    size_t cls(size_t n) const {
+        size_t c = pinned ? (4u << 20) : (1u << 20);
+        if (n <= c) return c;
+        if (pinned) {
+            while (c < n) c <<= 1;
+            return c;
+        }
         while (c < n) c <<= 1;
+        const size_t q = c >> 3;  // c/8: the steps between c/2 and c
+        for (size_t k = 5; k <= 8; k++)
+            if (k * q >= n) return k * q;
         return c;
     }
     void* get(size_t n, hipError_t* err) {
@@ -190,6 +202,50 @@ int ensure_device(pbx_ctx* ctx) {
     return PBX_OK;
 }
 
+using PlaneKey = std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>;
+PlaneKey key_of(const Plane& p) { return std::make_tuple(p.image_id, p.z, p.c, p.t, p.res); }
+
+// Checks, under reg_mu, that a plane may join the registry: its key is free and it agrees
+// with the image record (the Pixels row: pixel type; full-resolution size).
+int registry_check(pbx_ctx* ctx, const Plane& p) {
+    if (ctx->index.count(key_of(p))) return fail(PBX_E_BADARG, "plane already registered");
+    auto im = ctx->images.find(p.image_id);
+    if (im == ctx->images.end()) return PBX_OK;
+    if (im->second.pixel_type != p.pixel_type) return fail(PBX_E_BADARG, "pixel type differs from the image's");
+    if (p.res == 0 && im->second.level_planes.count(0) &&
+        (im->second.size_x != p.size_x || im->second.size_y != p.size_y))
+        return fail(PBX_E_BADARG, "plane size differs from the image's");
+    return PBX_OK;
+}
+
+// Inserts planes into the registry, all or none, re-checking every key under reg_mu at
+// insertion time (a concurrent registration of the same key loses with 400 instead of
+// both succeeding).  On failure the caller still owns (and frees) the planes' memory.
+int registry_insert(pbx_ctx* ctx, std::vector<Plane>& ps, uint64_t* ids) {
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    for (size_t k = 0; k < ps.size(); k++) {
+        if (int rc = registry_check(ctx, ps[k])) return rc;
+        for (size_t j = 0; j < k; j++)
+            if (key_of(ps[j]) == key_of(ps[k])) return fail(PBX_E_BADARG, "the same plane twice in one call");
+    }
+    for (size_t k = 0; k < ps.size(); k++) {
+        Plane& p = ps[k];
+        p.id = ctx->next_id++;
+        ctx->planes[p.id] = p;
+        ctx->index[key_of(p)] = p.id;
+        Image& im = ctx->images[p.image_id];
+        if (p.res == 0 || im.planes == 0) {  // the Pixels row: full-resolution sizes
+            im.pixel_type = p.pixel_type;
+            im.size_x = p.size_x;
+            im.size_y = p.size_y;
+        }
+        im.planes++;
+        im.level_planes[p.res]++;
+        if (ids) ids[k] = p.id;
+    }
+    return PBX_OK;
+}
+
 // Mirrors TileRequestHandler.getTile (TileRequestHandler.java:80-139) up to the dispatch:
 // returns PBX_OK and the plane, or the status the reference ends with.
 int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane& plane) {
@@ -198,6 +254,19 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     auto im = ctx->images.find(r.image_id);
     if (im == ctx->images.end()) return fail(PBX_E_NOTFOUND, "Cannot find Image:%lld", (long long)r.image_id);
+    // :89-91 — pixelBuffer.setResolutionLevel(resolution) when given.  OMERO numbers levels
+    // the other way round from storage: resolution getResolutionLevels()-1 is the full
+    // resolution and 0 the smallest (omero-zarr-pixel-buffer's ZarrPixelBuffer maps it to
+    // NGFF dataset levels-1-resolution; a level outside [0, levels) throws
+    // IllegalArgumentException, which getTile turns into null -> 404).  Stored level 0 is
+    // the full resolution.  Not given (PBX_RESOLUTION_NONE): the buffer's default, full res.
+    int32_t level = 0;
+    if (r.resolution != PBX_RESOLUTION_NONE) {
+        const int32_t nlev = im->second.levels();
+        if (r.resolution < 0 || r.resolution >= nlev)
+            return fail(PBX_E_NOTFOUND, "This image has only %d resolution levels", nlev);
+        level = nlev - 1 - r.resolution;
+    }
     // :92-97 — defaults come from the full-resolution Pixels sizes even with `resolution`
     if (w == 0) w = im->second.size_x;
     if (h == 0) h = im->second.size_y;
@@ -206,10 +275,9 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
     const int64_t tile_size = (int64_t)w * (int64_t)h * bpp;
     if (w < 0 || h < 0 || tile_size > 2147483647LL || tile_size <= 0)
         return fail(PBX_E_NOTFOUND, "invalid tile size %dx%d", w, h);
-    const int32_t res = r.resolution < 0 ? 0 : r.resolution;
-    auto it = ctx->index.find(std::make_tuple(r.image_id, r.z, r.c, r.t, res));
+    auto it = ctx->index.find(std::make_tuple(r.image_id, r.z, r.c, r.t, level));
     if (it == ctx->index.end())
-        return fail(PBX_E_NOTFOUND, "no plane z=%d c=%d t=%d resolution=%d", r.z, r.c, r.t, res);
+        return fail(PBX_E_NOTFOUND, "no plane z=%d c=%d t=%d level=%d", r.z, r.c, r.t, level);
     plane = ctx->planes[it->second];
     // getTileDirect outside the plane throws (upstream PixelBuffer) -> 404
     if (r.x < 0 || r.y < 0 || (int64_t)r.x + w > plane.size_x || (int64_t)r.y + h > plane.size_y)
@@ -284,7 +352,6 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
 // with at most DEPTH batches in flight, and a completer thread fetches finished batches
 // (D2H on the copy stream) and wakes their callers.
 struct Coalescer {
-    static constexpr int DEPTH = 2;
     static constexpr size_t MAX_BATCH = 1 << 16;
     struct Pending {
         pbx_tile_req req;
@@ -292,6 +359,7 @@ struct Coalescer {
         bool done = false;
         int rc = PBX_OK;
         std::string err;
+        std::condition_variable cv;  // this caller only: no thundering herd per batch
     };
     struct Flight {
         pbx_batch* b;
@@ -301,7 +369,14 @@ struct Coalescer {
     };
     pbx_ctx* ctx;
     std::mutex mu;
-    std::condition_variable cv_launch, cv_complete, cv_done;
+    std::condition_variable cv_launch, cv_complete;
+    // Batches in flight (launched, not yet fetched): up to `depth` ($PBX_COALESCE_DEPTH), but
+    // the k-th concurrent batch only once `launch_min[k]` requests wait, so that few callers
+    // get few, larger batches and many callers get a deeper pipeline (measured:
+    // scripts/serve_sweep.py).
+    int depth = 3;
+    size_t launch_min[8] = {1, 4, 32, 64, 128, 256, 512, 1024};
+    bool may_launch() const { return !queue.empty() && inflight < depth && queue.size() >= launch_min[inflight]; }
     std::deque<Pending*> queue;
     std::deque<Flight> flights;
     int inflight = 0;
@@ -309,6 +384,7 @@ struct Coalescer {
     std::thread launcher, completer;
 
     explicit Coalescer(pbx_ctx* c) : ctx(c) {
+        if (const char* d = getenv("PBX_COALESCE_DEPTH")) depth = std::min(8, std::max(1, atoi(d)));
         launcher = std::thread([this] { launch_loop(); });
         completer = std::thread([this] { complete_loop(); });
     }
@@ -330,7 +406,7 @@ struct Coalescer {
         if (stop) return fail(PBX_E_INTERNAL, "context is shutting down");
         queue.push_back(&p);
         cv_launch.notify_one();
-        cv_done.wait(g, [&] { return p.done; });
+        p.cv.wait(g, [&] { return p.done; });
         if (p.rc != PBX_OK) g_err = p.err;
         return p.rc;
     }
@@ -340,7 +416,7 @@ struct Coalescer {
             std::vector<Pending*> take;
             {
                 std::unique_lock<std::mutex> g(mu);
-                cv_launch.wait(g, [&] { return (stop && queue.empty()) || (!queue.empty() && inflight < DEPTH); });
+                cv_launch.wait(g, [&] { return (stop && queue.empty()) || may_launch(); });
                 if (queue.empty()) break;  // stopping, nothing left
                 while (!queue.empty() && take.size() < MAX_BATCH) {
                     take.push_back(queue.front());
@@ -407,10 +483,10 @@ struct Coalescer {
                     p->rc = f.rc;
                     p->err = f.err;
                     p->done = true;
+                    p->cv.notify_one();  // under mu: the caller cannot return (and free p) first
                 }
                 inflight--;
             }
-            cv_done.notify_all();
             cv_launch.notify_one();
         }
     }
@@ -525,6 +601,17 @@ void pbx_shutdown(pbx_ctx* ctx) {
     delete ctx;
 }
 
+int pbx_release_cached(pbx_ctx* ctx) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::lock_guard<std::mutex> run(ctx->run_mu);
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    ctx->dpool.trim();
+    ctx->hpool.trim();
+    return PBX_OK;
+}
+
 int pbx_device_synchronize(pbx_ctx* ctx) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
@@ -547,14 +634,7 @@ int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id
     p.bytes = (size_t)p.pitch * d->size_y + 256;
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
-        auto key = std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution);
-        if (ctx->index.count(key)) return fail(PBX_E_BADARG, "plane already registered");
-        auto im = ctx->images.find(d->image_id);
-        if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
-            return fail(PBX_E_BADARG, "pixel type differs from the image's");
-        if (d->resolution == 0 && im != ctx->images.end() &&
-            (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
-            return fail(PBX_E_BADARG, "plane size differs from the image's");
+        if (int rc = registry_check(ctx, p)) return rc;
     }
     HIP_TRY(hipMalloc((void**)&p.dev, p.bytes));
     if (d->source == PBX_SRC_HOST) {
@@ -574,26 +654,26 @@ int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id
         (void)hipFree(p.dev);
         return fail(PBX_E_BADARG, "bad source %d", d->source);
     }
-    HIP_TRY(hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    std::lock_guard<std::mutex> g(ctx->reg_mu);
-    p.id = ctx->next_id++;
-    ctx->planes[p.id] = p;
-    ctx->index[std::make_tuple(d->image_id, d->z, d->c, d->t, d->resolution)] = p.id;
-    Image& im = ctx->images[d->image_id];
-    if (d->resolution == 0 || im.planes == 0) {  // the Pixels row: full-resolution sizes
-        im.pixel_type = d->pixel_type;
-        im.size_x = d->size_x;
-        im.size_y = d->size_y;
+    hipError_t e = hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(p.dev);
+        return fail(PBX_E_INTERNAL, "plane upload: %s", hipGetErrorString(e));
     }
-    im.planes++;
-    *plane_id = p.id;
+    std::vector<Plane> one{p};
+    if (int rc = registry_insert(ctx, one, plane_id)) {  // lost a race for the same key
+        (void)hipFree(p.dev);
+        return rc;
+    }
     return PBX_OK;
 }
 
 int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t* ids, double* kernel_ms) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     if (levels < 1 || levels > 30) return fail(PBX_E_BADARG, "bad level count %d", levels);
+    // run_mu from the source lookup through the last kernel: pbx_plane_release takes it
+    // before freeing a plane, so the source cannot be freed under the downsampling kernels.
+    std::lock_guard<std::mutex> run(ctx->run_mu);
     Plane src;
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
@@ -607,70 +687,53 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     const int bpp = bpp_of(src.pixel_type);
     std::vector<Plane> made;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     auto undo = [&](int code) {
         for (Plane& q : made) (void)hipFree(q.dev);
-        return code;
-    };
-    Plane prev = src;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (kernel_ms) {
-        HIP_TRY(hipEventCreate(&ev0));
-        HIP_TRY(hipEventCreate(&ev1));
-    }
-    auto fin_events = [&]() {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        return code;
     };
+    hipError_t e = hipSuccess;
+    if (kernel_ms) {
+        e = hipEventCreate(&ev0);
+        if (e == hipSuccess) e = hipEventCreate(&ev1);
+        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "hipEventCreate: %s", hipGetErrorString(e)));
+    }
+    Plane prev = src;
     for (int32_t k = 1; k <= levels; k++) {
         Plane p = prev;
         p.size_x = (prev.size_x + 1) / 2;
         p.size_y = (prev.size_y + 1) / 2;
         p.pitch = ((int64_t)p.size_x * bpp + 255) & ~(int64_t)255;
         p.bytes = (size_t)p.pitch * p.size_y + 256;
-        hipError_t e = hipMalloc((void**)&p.dev, p.bytes);
-        if (e != hipSuccess) {
-            fin_events();
-            return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
-        }
+        p.dev = nullptr;
+        e = hipMalloc((void**)&p.dev, p.bytes);
+        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
         p.res = src.res + k;
         made.push_back(p);
         prev = p;
     }
-    if (ev0) HIP_TRY(hipEventRecord(ev0, ctx->stream));
+    if (ev0) e = hipEventRecord(ev0, ctx->stream);
     prev = src;
-    for (int32_t k = 1; k <= levels; k++) {
+    for (int32_t k = 1; k <= levels && e == hipSuccess; k++) {
         const Plane& p = made[k - 1];
-        hipError_t e = launch_downsample(ctx->stream, prev.dev, prev.pitch, prev.size_x, prev.size_y, p.dev, p.pitch,
+        e = launch_downsample(ctx->stream, prev.dev, prev.pitch, prev.size_x, prev.size_y, p.dev, p.pitch,
                               p.size_x, p.size_y, p.pixel_type, !p.little_endian && bpp > 1);
         if (e == hipSuccess) e = hipMemsetAsync(p.dev + (size_t)p.pitch * p.size_y, 0, 256, ctx->stream);
-        if (e != hipSuccess) {
-            fin_events();
-            return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
-        }
         prev = p;
     }
-    if (ev1) HIP_TRY(hipEventRecord(ev1, ctx->stream));
-    const hipError_t e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) {
-        fin_events();
-        return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
-    }
+    if (ev1 && e == hipSuccess) e = hipEventRecord(ev1, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "downsample: %s", hipGetErrorString(e)));
     if (kernel_ms) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, ev0, ev1);
         *kernel_ms = ms;
     }
-    fin_events();
-    std::lock_guard<std::mutex> g(ctx->reg_mu);
-    for (size_t k = 0; k < made.size(); k++) {
-        Plane& p = made[k];
-        p.id = ctx->next_id++;
-        ctx->planes[p.id] = p;
-        ctx->index[std::make_tuple(p.image_id, p.z, p.c, p.t, p.res)] = p.id;
-        ctx->images[p.image_id].planes++;
-        if (ids) ids[k] = p.id;
-    }
-    return PBX_OK;
+    if (int rc = registry_insert(ctx, made, ids)) return undo(rc);  // keys re-checked here
+    made.clear();
+    return undo(PBX_OK);  // events only
 }
 
 // ------------------------------------------------------------------ NGFF / Zarr planes
@@ -938,26 +1001,9 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
         kernel_ms[1] = b;
     }
     cleanup(false);
-    std::lock_guard<std::mutex> g(ctx->reg_mu);
-    for (uint64_t k = 0; k < n; k++)
-        if (ctx->index.count(keys[k])) {
-            for (Plane& p : ps) (void)hipFree(p.dev);
-            return fail(PBX_E_BADARG, "plane already registered");
-        }
-    for (uint64_t k = 0; k < n; k++) {
-        const pbx_plane_desc* d = &ds[k];
-        Plane& p = ps[k];
-        p.id = ctx->next_id++;
-        ctx->planes[p.id] = p;
-        ctx->index[keys[k]] = p.id;
-        Image& im = ctx->images[d->image_id];
-        if (d->resolution == 0 || im.planes == 0) {
-            im.pixel_type = d->pixel_type;
-            im.size_x = d->size_x;
-            im.size_y = d->size_y;
-        }
-        im.planes++;
-        plane_ids[k] = p.id;
+    if (int rc = registry_insert(ctx, ps, plane_ids)) {  // keys re-checked at insertion
+        for (Plane& p : ps) (void)hipFree(p.dev);
+        return rc;
     }
     return PBX_OK;
 }
@@ -977,7 +1023,10 @@ int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
     ctx->planes.erase(it);
     ctx->index.erase(std::make_tuple(p.image_id, p.z, p.c, p.t, p.res));
     auto im = ctx->images.find(p.image_id);
-    if (im != ctx->images.end() && --im->second.planes == 0) ctx->images.erase(im);
+    if (im != ctx->images.end()) {
+        if (--im->second.level_planes[p.res] == 0) im->second.level_planes.erase(p.res);
+        if (--im->second.planes == 0) ctx->images.erase(im);
+    }
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     HIP_TRY(hipFree(p.dev));

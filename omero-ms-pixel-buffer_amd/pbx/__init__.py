@@ -104,7 +104,7 @@ EXPORTS = [
     "pbx_pixel_type_from_string", "pbx_bytes_per_pixel", "pbx_device_synchronize",
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
     "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
-    "pbx_plane_register_zarr", "pbx_planes_register_zarr",
+    "pbx_plane_register_zarr", "pbx_planes_register_zarr", "pbx_release_cached",
 ]
 
 _lib = None
@@ -131,6 +131,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_shutdown.argtypes = [vp]
     L.pbx_shutdown.restype = None
     L.pbx_device_synchronize.argtypes = [vp]
+    L.pbx_release_cached.argtypes = [vp]
     L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
     L.pbx_plane_release.argtypes = [vp, u64]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
@@ -198,6 +199,17 @@ def _parse_int(v: str, bits: int) -> int:
     return n
 
 
+RESOLUTION_NONE = -1  # PBX_RESOLUTION_NONE: TileCtx.resolution == null
+
+
+def _req_resolution(r: Optional[int]) -> int:
+    """TileCtx.resolution -> pbx_tile_req.resolution (OMERO numbering, include/pbx.h): null ->
+    PBX_RESOLUTION_NONE; a given negative level (setResolutionLevel throws -> 404) -> -2."""
+    if r is None:
+        return RESOLUTION_NONE
+    return r if r >= 0 else -2
+
+
 class TileCtx:
     """TileCtx.java:30-92 — the request context and the event-bus JSON payload."""
 
@@ -251,7 +263,7 @@ class TileCtx:
 
     def to_req(self) -> PbxTileReq:
         return PbxTileReq(self.imageId, self.z, self.c, self.t,
-                          -1 if self.resolution is None else self.resolution,
+                          _req_resolution(self.resolution),
                           self.x, self.y, self.w, self.h,
                           lib().pbx_format_from_string(
                               self.format.encode() if self.format is not None else None), 0)
@@ -301,7 +313,7 @@ def zarr_array_meta(array_dir: str) -> dict:
     return meta
 
 
-def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, resolution: int = 0,
+def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, level: int = 0,
                     meta: Optional[dict] = None) -> dict:
     """register_zarr_planes() arguments for plane (z, c, t) of an NGFF array directory (NGFF
     axis order t, c, z, y, x; fewer leading axes drop from the left): chunk files named by
@@ -326,7 +338,7 @@ def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, resol
             chunks.append(open(path, "rb").read() if os.path.exists(path) else None)
     native = np.dtype(dt).newbyteorder("=")
     fill_bits = int(np.array([meta.get("fill_value") or 0], dtype=native).view("u%d" % native.itemsize)[0])
-    return dict(image_id=image_id, z=z, c=c, t=t, resolution=resolution,
+    return dict(image_id=image_id, z=z, c=c, t=t, level=level,
                 pixel_type=_ZARR_DTYPES[dt[1:]], size_x=sx, size_y=sy, chunk_x=cx, chunk_y=cy,
                 codec=None if comp is None else comp.get("id"), chunks=chunks,
                 big_endian=dt[0] != "<", fill_bits=fill_bits)
@@ -376,10 +388,13 @@ class PixelsService:
 
     def register_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int,
                        size_x: int, size_y: int, data=None, generator: Optional[str] = None,
-                       seed: int = 0, plane_no: int = 0, resolution: int = 0,
+                       seed: int = 0, plane_no: int = 0, level: int = 0,
                        big_endian: Optional[bool] = None) -> int:
+        """``level`` is the STORED pyramid level (0 = full resolution, the NGFF dataset
+        index); requests name levels in OMERO's numbering (TileCtx.resolution, levels-1 =
+        full resolution)."""
         d = PbxPlaneDesc()
-        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, resolution
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, level
         d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
         keep = None
         if generator is not None:
@@ -404,7 +419,7 @@ class PixelsService:
     def register_zarr_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int,
                             size_x: int, size_y: int, chunk_x: int, chunk_y: int,
                             codec: Optional[str], chunks: Sequence[Optional[bytes]],
-                            big_endian: bool = True, fill_bits: int = 0, resolution: int = 0,
+                            big_endian: bool = True, fill_bits: int = 0, level: int = 0,
                             timing: bool = False):
         """Register a plane from its Zarr v2 chunks (C order over the chunk grid; None or
         b"" = missing chunk -> fill), decoded on the GPU (pbx_plane_register_zarr).  codec is
@@ -418,7 +433,7 @@ class PixelsService:
         np.cumsum(lens, out=offsets[1:])
         data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
         d = PbxPlaneDesc()
-        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, resolution
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, level
         d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
         d.byte_order = BIG_ENDIAN if big_endian else LITTLE_ENDIAN
         zc = PbxZarrChunks()
@@ -434,7 +449,7 @@ class PixelsService:
         """Several Zarr planes decoded by one set of GPU launches (pbx_planes_register_zarr):
         each dict holds register_zarr_plane's arguments (image_id, z, c, t, pixel_type,
         size_x, size_y, chunk_x, chunk_y, codec, chunks[, big_endian, fill_bits,
-        resolution]).  All are registered or none.  Returns the plane ids (and the kernels'
+        level]).  All are registered or none.  Returns the plane ids (and the kernels'
         device ms with timing=True)."""
         import numpy as np
         n = len(planes)
@@ -452,7 +467,7 @@ class PixelsService:
             keep += [offsets, data]
             d = descs[k]
             d.image_id, d.z, d.c, d.t = p["image_id"], p["z"], p["c"], p["t"]
-            d.resolution = p.get("resolution", 0)
+            d.resolution = p.get("level", 0)
             d.pixel_type, d.size_x, d.size_y = p["pixel_type"], p["size_x"], p["size_y"]
             d.byte_order = BIG_ENDIAN if p.get("big_endian", True) else LITTLE_ENDIAN
             zc = zcs[k]
@@ -465,17 +480,17 @@ class PixelsService:
         return (list(ids), (ms[0], ms[1])) if timing else list(ids)
 
     def register_zarr_array(self, array_dir: str, image_id: int, z: int, c: int, t: int,
-                            resolution: int = 0) -> int:
+                            level: int = 0) -> int:
         """One (t, c, z) plane of an NGFF multiscale dataset (a Zarr v2 array directory with
         shape [..., y, x], NGFF order t, c, z, y, x) — what ZarrPixelBuffer reads through
         JZarr (omero-zarr-pixel-buffer 0.6.1, build.gradle:57).  Chunks of the plane are read
         from disk here and decoded on the GPU."""
-        sp = zarr_plane_spec(array_dir, image_id, z, c, t, resolution)
+        sp = zarr_plane_spec(array_dir, image_id, z, c, t, level)
         return self.register_zarr_planes([sp])[0]
 
     def register_zarr_array_planes(self, array_dir: str, image_id: int,
                                    planes: Optional[Sequence[Tuple[int, int, int]]] = None,
-                                   resolution: int = 0) -> Dict[Tuple[int, int, int], int]:
+                                   level: int = 0) -> Dict[Tuple[int, int, int], int]:
         """Every (z, c, t) plane of an NGFF array (or the given ones) decoded by ONE set of GPU
         launches (pbx_planes_register_zarr).  Returns {(z, c, t): plane id}."""
         meta = zarr_array_meta(array_dir)
@@ -483,7 +498,7 @@ class PixelsService:
         lead = [1] * (3 - len(lead)) + lead  # (t, c, z) extents
         if planes is None:
             planes = [(z, c, t) for t in range(lead[0]) for c in range(lead[1]) for z in range(lead[2])]
-        specs = [zarr_plane_spec(array_dir, image_id, z, c, t, resolution, meta) for z, c, t in planes]
+        specs = [zarr_plane_spec(array_dir, image_id, z, c, t, level, meta) for z, c, t in planes]
         ids = self.register_zarr_planes(specs)
         return dict(zip([tuple(p) for p in planes], ids))
 
@@ -491,9 +506,10 @@ class PixelsService:
         _check(lib().pbx_plane_release(self._h, plane_id))
 
     def build_pyramid(self, plane_id: int, levels: int, timing: bool = False):
-        """Resolution levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
-        returns their plane ids (and the kernels' device ms with timing=True).  Tiles of
-        level k: TileCtx(..., resolution=k)."""
+        """Stored levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
+        returns their plane ids (and the kernels' device ms with timing=True).  With L
+        stored levels, tiles of stored level k are TileCtx(..., resolution=L-1-k) (OMERO's
+        numbering, include/pbx.h)."""
         ids = (ctypes.c_uint64 * max(levels, 1))()
         ms = ctypes.c_double(0.0)
         _check(lib().pbx_plane_build_pyramid(self._h, plane_id, levels, ids, ctypes.byref(ms)))
@@ -506,6 +522,10 @@ class PixelsService:
 
     def synchronize(self) -> None:
         _check(lib().pbx_device_synchronize(self._h))
+
+    def release_cached(self) -> None:
+        """Free cached batch buffers (device and pinned) no live batch uses."""
+        _check(lib().pbx_release_cached(self._h))
 
     # One getTile (pbx_get_tile): safe to call from many threads at once; concurrent
     # calls are coalesced into batches by the library (ctypes releases the GIL).

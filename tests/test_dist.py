@@ -43,6 +43,24 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_ranks(world):
+    """`bench.py --gpus N` (no torchrun) starts N ranks itself; they meet at the barrier and
+    rank 0 alone prints the JSON line with n_gpus == N (dry run: no HIP call)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+                          "--dry-run", "--steps", "3"], env=env, capture_output=True, text=True,
+                         timeout=180)
+    assert out.returncode == 0, out.stderr
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == world and rec["ranks_met"] == world and rec["steps"] == 3
+
+
 @pytest.mark.parametrize("world", [2])
 def test_gloo_sharding(world):
     port = _free_port()

@@ -268,20 +268,25 @@ def test_resolution_pyramid(service, oracle, pt, source):
     else:
         pid = service.register_plane(iid, 0, 0, 0, pt, sx, sy, generator="noise", seed=7)
     ids = service.build_pyramid(pid, 4)
-    want = np.frombuffer(be.tobytes(), dt).reshape(sy, sx)
+    want = want0 = np.frombuffer(be.tobytes(), dt).reshape(sy, sx)
     for k, lid in enumerate(ids, start=1):
         want = R.downsample(want)
         h, w = want.shape
         got = service.read_plane_be(lid, w * h * oracle.BPP[pt])
         assert got == want.astype(dt).tobytes(), (pt, source, k)
-    # tiles of level 2 (76 x 25): raw bytes and (8/16-bit types) PNG pixels
+    # tiles of stored level 2 (76 x 25) = OMERO resolution 5-1-2 = 2 of the 5 levels: raw
+    # bytes and (8/16-bit types) PNG pixels; resolution 4 = the full-resolution plane
     lvl = R.downsample(R.downsample(np.frombuffer(be.tobytes(), dt).reshape(sy, sx))).astype(dt)
     ctxs = [pbx.TileCtx(iid, 0, 0, 0, 3, 2, 40, 20, resolution=2),
             pbx.TileCtx(iid, 0, 0, 0, 0, 0, 76, 25, resolution=2, format="png"),
-            pbx.TileCtx(iid, 0, 0, 0, 70, 20, 10, 10, resolution=2)]  # past the level -> 404
-    (s1, raw), (s2, png), (s3, _) = service.get_tiles(ctxs)
+            pbx.TileCtx(iid, 0, 0, 0, 70, 20, 10, 10, resolution=2),  # past the level -> 404
+            pbx.TileCtx(iid, 0, 0, 0, 3, 2, 40, 20, resolution=4),
+            pbx.TileCtx(iid, 0, 0, 0, 0, 0, 19, 7, resolution=0)]     # stored level 4: 19 x 7
+    (s1, raw), (s2, png), (s3, _), (s4, full), (s5, small) = service.get_tiles(ctxs)
     assert s1 == pbx.OK and raw == lvl[2:22, 3:43].tobytes()
     assert s3 == pbx.E_NOTFOUND
+    assert s4 == pbx.OK and full == want0[2:22, 3:43].astype(dt).tobytes()
+    assert s5 == pbx.OK and small == want.astype(dt).tobytes()  # the smallest level, whole
     if pt in (pbx.INT8, pbx.UINT8, pbx.INT16, pbx.UINT16):
         assert s2 == pbx.OK
         r, px, _ = oracle.png_decode(png)

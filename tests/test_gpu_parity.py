@@ -177,7 +177,8 @@ def test_error_statuses(service, oracle):
         (pbx.TileCtx(iid, 0, 0, 0, -1, 0, 4, 4), pbx.E_NOTFOUND),
         (pbx.TileCtx(iid, 0, 0, 0, 10, 0, 0, 4), pbx.E_NOTFOUND),             # w default + x
         (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, format="jpg"), pbx.E_NOTFOUND),  # unknown fmt
-        (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, resolution=1), pbx.E_NOTFOUND),  # no level 1
+        (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, resolution=1), pbx.E_NOTFOUND),  # 1 level only
+        (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, resolution=0), pbx.OK),          # = full res
         (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, format="png"), pbx.OK),
         (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 65536, 65536), pbx.E_NOTFOUND),       # int overflow
     ]
@@ -196,15 +197,34 @@ def test_error_statuses(service, oracle):
 
 
 def test_resolution_levels(service, oracle):
+    """OMERO's resolution numbering (TileRequestHandler.java:89-91 -> setResolutionLevel):
+    with L stored levels, resolution L-1 is the full-resolution plane and 0 the smallest
+    (omero-zarr-pixel-buffer maps it to NGFF dataset L-1-resolution); an absent resolution
+    serves full resolution; w/h defaulting uses the full-resolution Pixels size (:92-97);
+    a level outside [0, L) -> setResolutionLevel throws -> null -> 404."""
     iid, plane = host_plane(service, oracle, pbx.UINT8, 64, 64)
-    lvl = oracle.gen_region(1, pbx.UINT8, 0, 0, 32, 32)
-    service.register_plane(iid, 0, 0, 0, pbx.UINT8, 32, 32, data=lvl, resolution=1)
-    res = service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 0, 0, 16, 16, resolution=1),
-                             pbx.TileCtx(iid, 0, 0, 0, 0, 0, 0, 0, resolution=1)])
-    assert res[0][0] == pbx.OK
-    assert res[0][1] == oracle.extract_be(lvl, True, pbx.UINT8, 32, 0, 0, 16, 16).tobytes()
-    # w/h default to the full-resolution Pixels size (64) -> outside level 1 -> 404
-    assert res[1][0] == pbx.E_NOTFOUND
+    lvl1 = oracle.gen_region(1, pbx.UINT8, 0, 0, 32, 32)
+    lvl2 = oracle.gen_region(2, pbx.UINT8, 0, 0, 16, 16, seed=9)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT8, 32, 32, data=lvl1, level=1)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT8, 16, 16, data=lvl2, level=2)
+    full = oracle.extract_be(plane, True, pbx.UINT8, 64, 0, 0, 16, 16).tobytes()
+    res = service.get_tiles([
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 16, 16, resolution=2),     # L-1: full resolution
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 16, 16),                   # absent: full resolution
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 16, 16, resolution=1),     # stored level 1
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 16, 16, resolution=0),     # smallest (stored 2)
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 0, 0, resolution=2),       # w/h -> 64 x 64, full res
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 0, 0, resolution=1),       # w/h -> 64: outside 32^2
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, resolution=3),       # only 3 levels -> 404
+        pbx.TileCtx(iid, 0, 0, 0, 0, 0, 4, 4, resolution=-1),      # given negative -> 404
+    ])
+    st = [s for s, _ in res]
+    assert st == [pbx.OK, pbx.OK, pbx.OK, pbx.OK, pbx.OK, pbx.E_NOTFOUND, pbx.E_NOTFOUND,
+                  pbx.E_NOTFOUND], st
+    assert res[0][1] == full and res[1][1] == full
+    assert res[2][1] == oracle.extract_be(lvl1, True, pbx.UINT8, 32, 0, 0, 16, 16).tobytes()
+    assert res[3][1] == lvl2.tobytes()
+    assert res[4][1] == plane.tobytes()
 
 
 # ------------------------------------------------------------- adaptive filter / deflate TIFF

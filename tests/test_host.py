@@ -35,7 +35,7 @@ def test_abi_struct_sizes_match_bindings():
 
 def test_enums_and_names():
     L = pbx.lib()
-    assert L.pbx_abi_version() == 3
+    assert L.pbx_abi_version() == 4
     assert L.pbx_format_from_string(None) == pbx.FMT_RAW
     assert L.pbx_format_from_string(b"png") == pbx.FMT_PNG
     assert L.pbx_format_from_string(b"tif") == pbx.FMT_TIF

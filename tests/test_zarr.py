@@ -370,3 +370,39 @@ def test_gpu_ngff_all_planes_one_call(service, tmp_path):
     assert st == 0 and raw == planes[(1, 1, 2)][20:60, 10:40].tobytes()
     for pid in ids.values():
         service.release_plane(pid)
+
+
+def _flushed_zlib(raw, level, piece_sizes):
+    """A zlib stream whose pieces are separated by Z_SYNC_FLUSH (each flush ends with an
+    empty stored block: LEN 0 after byte alignment), or at level 0 stored blocks of 1..3
+    bytes: blocks shorter than the bytes the decoder's bit buffer holds."""
+    co = zlib.compressobj(level)
+    out, pos, k = [], 0, 0
+    while pos < len(raw):
+        n = piece_sizes[k % len(piece_sizes)]
+        out.append(co.compress(raw[pos:pos + n]))
+        out.append(co.flush(zlib.Z_SYNC_FLUSH))
+        pos += n
+        k += 1
+    out.append(co.flush())
+    return b"".join(out)
+
+
+@gpu
+@pytest.mark.parametrize("level,pieces", [(6, [777, 1, 4096, 3]), (0, [1, 2, 3]), (1, [2, 5000]),
+                                          (0, [65535, 1])],
+                         ids=["l6-sync", "l0-tiny-stored", "l1-sync", "l0-max-stored"])
+def test_gpu_inflate_sync_flush_and_tiny_stored_blocks(service, oracle, level, pieces):
+    """Stored blocks of 0..3 bytes (sync flushes; level 0 pieces) decode exactly like zlib's
+    inflate (the oracle's uncompress): the bytes buffered past such a block are not lost."""
+    import pbx
+    h, w = 64, 96
+    plane = _zarr.noise_plane(h, w, ">u2", seed=17)
+    raw = plane.tobytes()
+    enc = _flushed_zlib(raw, level, pieces)
+    assert zlib.decompress(enc) == raw
+    rc, want = oracle_decode(oracle, "zlib", enc, len(raw))
+    assert rc == 0 and want == raw
+    pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, w, h, w, h, "zlib", [enc])
+    assert np.array_equal(plane_be(service, pid, ">u2", h, w), plane)
+    service.release_plane(pid)
