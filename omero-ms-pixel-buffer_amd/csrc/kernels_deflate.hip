@@ -30,13 +30,21 @@ using DC = DeflateMainCfg;
 constexpr uint32_t STAMP_STRIDE = 32;  // diagnostics: k_lz77 0.., k_huff 8.., k_encode 24..
 
 // ------------------------------------------------------------------- LDS layouts
+// A match record of k_lz77 in LDS: position in the wave's sub-segment (11 bits), length - 3
+// (8 bits), candidate index (2 bits: distance 1, 2 or one row), unpacked into the mrec form
+// (pos | (len - 3) << 16, dist - 1) when written to HBM.  4 KB less than two arrays: the room
+// for 8 histogram copies at 4 workgroups per CU.
+constexpr uint32_t LZ_HCOPIES = 8;
 template <class C>
 struct LzSmem {
+    static_assert(C::SUB == 2048, "11-bit sub-segment positions in the packed match records");
     alignas(16) uint32_t buf[C::BUFW];
-    uint32_t mpos[C::NW * C::MAXMW];
-    uint16_t mdist[C::NW * C::MAXMW];
+    uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    alignas(16) uint32_t h8[288 * 4];  // literal/length histogram, 4 interleaved copies (lane & 3)
+    // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
+    // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
+    alignas(16) uint32_t h8[288 * LZ_HCOPIES];
+    uint32_t hdummy[64];  // per-lane sink of the branch-free histogram (covered positions)
     uint32_t dfreq[32];
     uint32_t red[3 * C::NW];
 };
@@ -83,13 +91,24 @@ struct HuffSmem {
 };
 
 constexpr int CRC_NIB_LEVELS_ = 7;
+// Output word k of the encoder lives at LDS word osk(k).  A skew (k + k / 32: the CRC phase's
+// lanes, 8 consecutive words each, then hit 32 banks instead of 4) was measured slower.
+#ifdef PBX_ENC_SKEW  // timing experiment (measured 3% slower: the CRC's reads are not the cost)
+__device__ __forceinline__ uint32_t osk(uint32_t k) { return k + (k >> 5); }
+#else
+__device__ __forceinline__ uint32_t osk(uint32_t k) { return k; }
+#endif
 template <class C>
 struct EncSmem {
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
     uint32_t lcode[289], dcode[32];  // slot form; lcode[288] = no token
-    alignas(16) uint32_t out[C::OUTW];
+#ifdef PBX_ENC_SKEW
+    alignas(16) uint32_t out[(C::OUTW + C::OUTW / 32 + 2 + 3) & ~3];  // word k at osk(k)
+#else
+    alignas(16) uint32_t out[(C::OUTW + 3) & ~3];
+#endif
     uint32_t crc_t[4][256];
     uint32_t crcn[CRC_NIB_LEVELS_][8][16];
     uint32_t misc[M_NMISC];
@@ -240,60 +259,93 @@ struct DirectRows {
 };
 
 // LDS bytes [0, nb) = stream bytes [B, B + nb) of the tile, zero from nb up to nz (a
-// multiple of 4).  NT threads; wave w takes tasks w, w + NW, ... of (row, chunk group).
-template <int NT, class Stamp>
-__device__ __forceinline__ void fill_direct(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
-                                            uint32_t nz, uint32_t tid, Stamp&& stamp) {
-    constexpr uint32_t NW = NT / 64, K = 3;
+// multiple of 4).  NT threads; wave w takes tasks w, w + NW, ... of (row, chunk group), K
+// tasks per batch (the loads of a batch are in flight together).  Split in two so that the
+// first batch's loads can be issued one segment ahead (k_lz77's prefetch): fill_issue loads
+// batch 0 into registers, fill_finish stores it and does the other batches.
+template <uint32_t K>
+struct FillPre {
+    uint4 v[K];
+};
+
+struct FillGeom {
+    uint32_t ra, ntask;
+    __device__ __forceinline__ FillGeom(const DirectRows& dr, uint32_t B, uint32_t nb) {
+        ra = B / dr.rowlen;
+        const uint32_t rz = (B + nb - 1) / dr.rowlen;
+        ntask = (rz - ra + 1) * dr.ngrp;
+    }
+};
+
+template <int NT, uint32_t K>
+__device__ __forceinline__ void fill_loads(uint4 (&v)[K], const DirectRows& dr, const FillGeom& g,
+                                           uint32_t k0, uint32_t lane) {
+    constexpr uint32_t NW = NT / 64;
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++) {
+        const uint32_t k = k0 + j * NW < g.ntask ? k0 + j * NW : k0;
+        const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
+        const uint32_t c0 = (k - i * dr.ngrp) * 64;
+        const uint8_t* rp = dr.row0 + (int64_t)(g.ra + i) * dr.pitch + 16 * c0;
+        v[j] = gload16(rp + 16 * (c0 + lane < dr.nc ? lane : 0u));
+    }
+}
+
+template <int NT, uint32_t K>
+__device__ __forceinline__ void fill_stores(const uint4 (&v)[K], uint8_t* bb, const DirectRows& dr,
+                                            const FillGeom& g, uint32_t B, uint32_t nb, uint32_t k0,
+                                            uint32_t lane) {
+    constexpr uint32_t NW = NT / 64;
+#pragma unroll
+    for (uint32_t j = 0; j < K; j++) {
+        const uint32_t k = k0 + j * NW;
+        if (k >= g.ntask) break;  // uniform
+        const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
+        const uint32_t c0 = (k - i * dr.ngrp) * 64;
+        const int32_t q0 = (int32_t)((g.ra + i) * dr.rowlen + dr.fb) - (int32_t)B + 16 * (int32_t)c0;
+        uint4 x = v[j];
+        if (dr.swap) x = swap16(x, dr.bpp);
+        if (dr.flip) x = flip_msb(x, dr.bpp);
+        const uint32_t c = c0 + lane;
+        const int32_t dst = q0 + 16 * (int32_t)lane;  // LDS byte of the chunk's first byte
+        const bool valid = c < dr.nc;
+        if (valid && dst >= 0 && dst + 16 <= (int32_t)nb && 16 * (c + 1) <= dr.rb) {
+            // one unaligned 16-byte LDS store (gfx950 DS access is unaligned-capable)
+            __builtin_memcpy(bb + dst, &x, 16);
+        } else if (valid && dst + 16 > 0 && dst < (int32_t)nb) {
+            const uint32_t nbc = dr.rb - 16 * c < 16 ? dr.rb - 16 * c : 16u;
+            for (uint32_t q = 0; q < nbc; q++) {
+                const int32_t at = dst + (int32_t)q;
+                const uint32_t lo = (q & 4u) ? x.y : x.x, hi = (q & 4u) ? x.w : x.z;
+                if (at >= 0 && at < (int32_t)nb) bb[at] = (uint8_t)(((q & 8u) ? hi : lo) >> (8 * (q & 3u)));
+            }
+        }
+        if (dr.fb && c == 0 && dst - 1 >= 0 && dst - 1 < (int32_t)nb) bb[dst - 1] = 0;
+    }
+}
+
+template <int NT, uint32_t K>
+__device__ __forceinline__ void fill_issue(FillPre<K>& pf, const DirectRows& dr, uint32_t B, uint32_t nb,
+                                           uint32_t tid) {
+    const FillGeom g(dr, B, nb);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (w < g.ntask) fill_loads<NT, K>(pf.v, dr, g, w, tid & 63);
+}
+
+template <int NT, uint32_t K>
+__device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf, const DirectRows& dr,
+                                            uint32_t B, uint32_t nb, uint32_t nz, uint32_t tid) {
+    constexpr uint32_t NW = NT / 64;
     uint8_t* bb = (uint8_t*)buf;
     const uint32_t lane = tid & 63;
-    // task = (row, group of 64 chunks): everything but the lane's chunk offset is uniform
+    const FillGeom g(dr, B, nb);
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
-    const uint32_t ntask = (rz - ra + 1) * dr.ngrp;
-    for (uint32_t k0 = w; k0 < ntask; k0 += K * NW) {
+    if (w < g.ntask) fill_stores<NT, K>(pf.v, bb, dr, g, B, nb, w, lane);
+    for (uint32_t k0 = w + K * NW; k0 < g.ntask; k0 += K * NW) {  // batches past the prefetched one
         uint4 v[K];
-        const uint8_t* rp[K];
-        int32_t q0[K];
-        uint32_t c0[K];
-#pragma unroll
-        for (uint32_t j = 0; j < K; j++) {  // the loads first
-            const uint32_t k = k0 + j * NW < ntask ? k0 + j * NW : k0;
-            const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
-            c0[j] = (k - i * dr.ngrp) * 64;
-            rp[j] = dr.row0 + (int64_t)(ra + i) * dr.pitch + 16 * c0[j];
-            q0[j] = (int32_t)((ra + i) * dr.rowlen + dr.fb) - (int32_t)B + 16 * (int32_t)c0[j];
-            v[j] = gload16(rp[j] + 16 * (c0[j] + lane < dr.nc ? lane : 0u));
-        }
-        if (k0 == w) stamp(false);  // diagnostics: the first loads issued
-#pragma unroll
-        for (uint32_t j = 0; j < K; j++) {
-            if (k0 + j * NW >= ntask) break;  // uniform
-            uint4 x = v[j];
-            if (dr.swap) x = swap16(x, dr.bpp);
-            if (dr.flip) x = flip_msb(x, dr.bpp);
-            const uint32_t c = c0[j] + lane;
-            const int32_t dst = q0[j] + 16 * (int32_t)lane;  // LDS byte of the chunk's first byte
-            const bool valid = c < dr.nc;
-            if (valid && dst >= 0 && dst + 16 <= (int32_t)nb && 16 * (c + 1) <= dr.rb) {
-                // one unaligned 16-byte LDS store (gfx950 DS access is unaligned-capable)
-#ifdef PBX_LZ_ALIGNED_FILL  // timing experiment only: aligned stores (wrong output)
-                __builtin_memcpy(bb + (dst & ~15), &x, 16);
-#else
-                __builtin_memcpy(bb + dst, &x, 16);
-#endif
-            } else if (valid && dst + 16 > 0 && dst < (int32_t)nb) {
-                const uint32_t nbc = dr.rb - 16 * c < 16 ? dr.rb - 16 * c : 16u;
-                for (uint32_t q = 0; q < nbc; q++) {
-                    const int32_t at = dst + (int32_t)q;
-                    const uint32_t lo = (q & 4u) ? x.y : x.x, hi = (q & 4u) ? x.w : x.z;
-                    if (at >= 0 && at < (int32_t)nb) bb[at] = (uint8_t)(((q & 8u) ? hi : lo) >> (8 * (q & 3u)));
-                }
-            }
-            if (dr.fb && c == 0 && dst - 1 >= 0 && dst - 1 < (int32_t)nb) bb[dst - 1] = 0;
-        }
+        fill_loads<NT, K>(v, dr, g, k0, lane);
+        fill_stores<NT, K>(v, bb, dr, g, B, nb, k0, lane);
     }
-    stamp(true);  // diagnostics: the rows stored
     // zero tail: bytes [nb, round4(nb)) and words up to nz
     const uint32_t nb4 = (nb + 3) & ~3u;
     if (tid < nb4 - nb) bb[nb + tid] = 0;
@@ -390,7 +442,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= lsub) break;
         const uint32_t t = k >> 5, i = k & 31;
-        uint32_t L = 0, D = 0, L1 = 0;
+        uint32_t L = 0, D = 0, Dc = 0, L1 = 0;
 #pragma unroll
         for (int c = 0; c < NCAND; c++) {
             if (!dd[c]) continue;
@@ -401,11 +453,12 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             uint32_t n1 = (uint32_t)__builtin_ctzll(~(ex >> (i + 1)));
             n0 = n0 < (uint32_t)C::CAP ? n0 : (uint32_t)C::CAP;
             n1 = n1 < (uint32_t)C::CAP ? n1 : (uint32_t)C::CAP;
-            if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; }
+            if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; Dc = (uint32_t)c; }
             if (n1 >= ml[c] && n1 > L1) L1 = n1;
         }
         L = __builtin_amdgcn_readfirstlane(L);
         D = __builtin_amdgcn_readfirstlane(D);
+        Dc = __builtin_amdgcn_readfirstlane(Dc);
         L1 = __builtin_amdgcn_readfirstlane(L1);
         if (L < 3 || L1 > L) { o = k + 1; continue; }  // lazy: a longer match starts next
         const uint32_t p = ss + k;
@@ -424,11 +477,10 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         }
         if (nm < (uint32_t)C::MAXMW) {
             if (lane == 0) {
-                S.mpos[w * C::MAXMW + nm] = p | ((L - 3) << 16);
-                S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
+                S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
                 uint32_t sy, e, v;
                 len_code(L, sy, e, v);
-                atomicAdd(&S.h8[sy * 4], 1u);
+                atomicAdd(&S.h8[sy * LZ_HCOPIES], 1u);
                 dist_code(D, sy, e, v);
                 atomicAdd(&S.dfreq[sy], 1u);
             }
@@ -445,6 +497,66 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     if (lane == 0) S.w_nm[w] = nm;
 }
 
+// The whole descriptor in one round of scalar loads: the fence keeps the compiler from
+// sinking the plane fields' loads past the branches into a second dependent round.
+__device__ __forceinline__ TileDesc load_desc(const TileDesc* p) {
+    uint4 q[sizeof(TileDesc) / 16];
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(TileDesc) / 16; i++) q[i] = ((const uint4*)p)[i];
+    asm volatile("" : "+s"(q[0].x), "+s"(q[0].y), "+s"(q[0].z), "+s"(q[0].w), "+s"(q[1].x), "+s"(q[1].y),
+                 "+s"(q[1].z), "+s"(q[1].w), "+s"(q[2].x), "+s"(q[2].y), "+s"(q[2].z), "+s"(q[2].w),
+                 "+s"(q[3].x), "+s"(q[3].y), "+s"(q[3].z), "+s"(q[3].w), "+s"(q[4].x), "+s"(q[4].y));
+    TileDesc d;
+    __builtin_memcpy(&d, q, sizeof d);
+    return d;
+}
+
+constexpr uint32_t LZ_PF = 3;  // load tasks (rows x 64 chunks) per wave in flight at once
+
+// A finished segment's results, from LDS to HBM: SegInfo (geometry, Adler-32 partials from
+// S.red), the symbol histogram (the 8 copies summed), the match records (unpacked).
+template <class C>
+__device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, const SegParams& sp, uint64_t src,
+                                             SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
+                                             uint32_t* __restrict__ mrec, uint32_t tid) {
+    if (tid == 0) {
+        uint32_t a1 = S.red[0], a2 = S.red[1];
+        for (int k = 1; k < C::NW; k++) adler_combine(a1, a2, S.red[3 * k], S.red[3 * k + 1], S.red[3 * k + 2]);
+        SegInfo& g = info[seg];
+        g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
+        g.adler_s1 = a1; g.adler_s2 = a2;
+        g.src_lo = (uint32_t)src; g.src_hi = (uint32_t)(src >> 32);
+    }
+    uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
+    for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
+        uint32_t v;
+        if (i < 288) {
+            const uint4 a = *(const uint4*)&S.h8[i * LZ_HCOPIES];
+            const uint4 b = *(const uint4*)&S.h8[i * LZ_HCOPIES + 4];
+            v = (a.x + a.y) + (a.z + a.w) + (b.x + b.y) + (b.z + b.w);
+        } else {
+            v = S.dfreq[i - 288];
+        }
+        hg[i] = v;
+    }
+    uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
+    if (tid < (uint32_t)C::NW) mg[tid] = S.w_nm[tid];
+    for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
+        if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
+            const uint32_t r = S.mrl[i], c = r >> 19;
+            const uint32_t pos = (i / C::MAXMW) * C::SUB + (r & 2047u);
+            const uint32_t dist = c == 0 ? 1u : c == 1 ? 2u : sp.rowlen;
+            mg[C::NW + i] = pos | (((r >> 11) & 255u) << 16);
+            mg[C::NW + C::NW * C::MAXMW + i] = dist - 1;
+        }
+    }
+}
+
+// One workgroup per segment.  (A persistent variant -- a contiguous run of segments per
+// workgroup, the next segment's plane rows prefetched into registers while the current one is
+// parsed -- needed more registers than 8 waves per SIMD allow and spilled; the fill is
+// issue-bound rather than latency-bound anyway: the same cycles with every plane read a cache
+// hit, profiles/r01_s4_phase_direct_sametile.log.)
 template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
@@ -460,37 +572,22 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
         nst++;
     };
     stamp();
-    const uint32_t ti = seg_tile[seg];
-    TileDesc d;
-    {  // the whole descriptor in one round of scalar loads: the fence keeps the compiler from
-       // sinking the plane fields' loads past the branches into a second dependent round
-        uint4 q[sizeof(TileDesc) / 16];
-#pragma unroll
-        for (uint32_t i = 0; i < sizeof(TileDesc) / 16; i++) q[i] = ((const uint4*)(dt + ti))[i];
-        asm volatile("" : "+s"(q[0].x), "+s"(q[0].y), "+s"(q[0].z), "+s"(q[0].w), "+s"(q[1].x), "+s"(q[1].y),
-                     "+s"(q[1].z), "+s"(q[1].w), "+s"(q[2].x), "+s"(q[2].y), "+s"(q[2].z), "+s"(q[2].w),
-                     "+s"(q[3].x), "+s"(q[3].y), "+s"(q[3].z), "+s"(q[3].w), "+s"(q[4].x), "+s"(q[4].y));
-        __builtin_memcpy(&d, q, sizeof d);
-    }
+    const TileDesc d = load_desc(dt + seg_tile[seg]);
     const SegParams sp = seg_params(d, seg - d.seg_first);
     const bool direct = (d.flags & TF_DIRECT) != 0;
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
     dr.init(d);
+    const uint32_t nz = lz_fill_bytes<C>(sp) & ~15u;
     if (direct) {
-        uint32_t nfs = 0;
-        fill_direct<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid,
-                           [&](bool wait) {  // diagnostics: 2 sub-phase stamps (PROF only)
-                               if (!PROF || nfs >= 2) return;
-                               if (wait) __builtin_amdgcn_s_waitcnt(0);
-                               stamp();
-                               nfs++;
-                           });
-        if (PROF && nfs < 2) { stamp(); if (nfs < 1) stamp(); }
+        FillPre<LZ_PF> pf;
+        fill_issue<C::NT, LZ_PF>(pf, dr, (uint32_t)sp.base, sp.wl + sp.sl, tid);
+        if (PROF) stamp();  // diagnostics: the first loads issued
+        fill_finish<C::NT, LZ_PF>(pf, S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid);
     } else {
-        load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, lz_fill_bytes<C>(sp) & ~15u, tid);
-        if (PROF) { stamp(); stamp(); }
+        load_bytes16<C::NT>(S.buf, stream + d.out_off + sp.base, sp.wl + sp.sl, nz, tid);
+        if (PROF) stamp();
     }
-    for (uint32_t k = tid; k < 288 * 4; k += C::NT) S.h8[k] = 0;
+    for (uint32_t k = tid; k < 288 * LZ_HCOPIES; k += C::NT) S.h8[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
     if (PROF) {  // diagnostics: wave 0's fill done
         __builtin_amdgcn_s_waitcnt(0);
@@ -515,15 +612,19 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     uint32_t cover, smask;
     ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
     stamp();
-    // literal histogram of the chunk (positions no recorded match covers), 4 interleaved
-    // copies against same-address LDS atomics; Adler-32 partial sums from the same words
+    // literal histogram of the chunk (positions no recorded match covers), 8 interleaved
+    // copies against same-address LDS atomics, branch-free: a covered position adds into the
+    // lane's own sink word.  Adler-32 partial sums from the same words.
     {
-        const uint32_t lit = ~cover & smask, cp = lane & 3u;
+        const uint32_t lit = ~cover & smask, cp = lane & (LZ_HCOPIES - 1);
+        const uint32_t sink = (uint32_t)(&S.hdummy[lane] - S.h8);
 #pragma unroll
-        for (int j = 0; j < 32; j++)
-            if ((lit >> j) & 1u) atomicAdd(&S.h8[((cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu) * 4 + cp], 1u);
+        for (int j = 0; j < 32; j++) {
+            const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+            atomicAdd(&S.h8[((lit >> j) & 1u) ? bt * LZ_HCOPIES + cp : sink], 1u);
+        }
     }
-    if (tid == 0) atomicAdd(&S.h8[256 * 4], 1u);  // end of block
+    if (tid == 0) atomicAdd(&S.h8[256 * LZ_HCOPIES], 1u);  // end of block
     uint32_t s1 = 0, s2 = 0, n = 0;
     if (cs < sp.sl) {
         const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
@@ -548,34 +649,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     if (lane == 0) { S.red[3 * w] = s1 % ADLER_BASE; S.red[3 * w + 1] = s2 % ADLER_BASE; S.red[3 * w + 2] = n; }
     __syncthreads();
     stamp();
-    if (tid == 0) {
-        uint32_t a1 = S.red[0], a2 = S.red[1];
-        for (int k = 1; k < C::NW; k++) adler_combine(a1, a2, S.red[3 * k], S.red[3 * k + 1], S.red[3 * k + 2]);
-        SegInfo& g = info[seg];
-        g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
-        g.adler_s1 = a1; g.adler_s2 = a2;
-        const uint64_t src = d.out_off + sp.base + sp.wl;
-        g.src_lo = (uint32_t)src; g.src_hi = (uint32_t)(src >> 32);
-    }
-    uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
-    for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
-        uint32_t v;
-        if (i < 288) {
-            const uint4 a = *(const uint4*)&S.h8[i * 4];
-            v = a.x + a.y + a.z + a.w;
-        } else {
-            v = S.dfreq[i - 288];
-        }
-        hg[i] = v;
-    }
-    uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
-    if (tid < (uint32_t)C::NW) mg[tid] = S.w_nm[tid];
-    for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
-        if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
-            mg[C::NW + i] = S.mpos[i];
-            mg[C::NW + C::NW * C::MAXMW + i] = S.mdist[i];
-        }
-    }
+    lz_write_out<C>(S, seg, sp, d.out_off + sp.base + sp.wl, info, hist, mrec, tid);
     stamp();
 }
 
@@ -1116,11 +1190,77 @@ __global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restric
 }
 
 // ==================================================================== k_encode
-// Output bytes j..j+3 (j = any byte offset) from the assembled words.
+// Output bytes j..j+3 (j = any byte offset) from the assembled (skewed) words.
 template <class SM>
 __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
-    const uint32_t w0 = S.out[j >> 2], w1 = S.out[(j >> 2) + 1], sh = (j & 3) * 8;
+    const uint32_t w0 = S.out[osk(j >> 2)], w1 = S.out[osk((j >> 2) + 1)], sh = (j & 3) * 8;
     return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+}
+template <class SM>
+__device__ __forceinline__ uint32_t out_byte_sk(const SM& S, uint32_t j) {
+    return (S.out[osk(j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+}
+template <class SM>
+__device__ __forceinline__ uint8_t* out_byte_ptr(SM& S, uint32_t j) {
+    return (uint8_t*)&S.out[osk(j >> 2)] + (j & 3);
+}
+
+// Bit writers over the skewed output words (deflate_seg.h RunWriter / BitWriter semantics:
+// every word is OR'd into a zeroed buffer, so words shared with the neighbouring bit ranges
+// need no special case).  (A branch-free put -- OR zero when no word completes -- measured
+// slower: on compressible data many lanes then OR into the same few words.)
+struct SkRunWriter {
+    uint32_t* out;
+    uint32_t word, nacc;
+    uint64_t acc;
+    __device__ SkRunWriter(uint32_t* o, uint32_t pos) : out(o), word(pos >> 5), nacc(pos & 31), acc(0) {}
+    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+        acc |= (uint64_t)v << nacc;
+        nacc += n;
+        if (nacc >= 32) {
+            atomicOr(&out[osk(word)], (uint32_t)acc);
+            word++;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (acc) atomicOr(&out[osk(word)], (uint32_t)acc);
+    }
+};
+struct SkBitWriter {
+    uint32_t* out;
+    uint32_t pos;
+    __device__ void put(uint32_t v, uint32_t n) {
+        if (!n) return;
+        const uint32_t w = pos >> 5, sh = pos & 31;
+        atomicOr(&out[osk(w)], v << sh);
+        if (sh + n > 32) atomicOr(&out[osk(w + 1)], v >> (32 - sh));
+        pos += n;
+    }
+};
+
+// ph_crc (deflate_seg.h) over the skewed words.
+template <class C, class SM>
+__device__ __forceinline__ uint32_t crc_chunk_sk(uint32_t tid, const SM& S) {
+    const uint32_t nbytes = S.misc[M_NBYTES];
+    const uint32_t pad = (4u - (nbytes & 3u)) & 3u, nv = (nbytes + pad) >> 2;
+    const int64_t hi = (int64_t)nv - (int64_t)(C::NT - 1 - tid) * (C::CRCC / 4);
+    int64_t lo = hi - C::CRCC / 4;
+    if (lo < 0 || tid == 0) lo = 0;
+    uint32_t c = 0;
+    for (int64_t k = lo; k < hi; k++) {
+        const uint32_t w1 = S.out[osk((uint32_t)k)];
+        uint32_t v = w1;
+        if (pad) {
+            const uint32_t w0 = k > 0 ? S.out[osk((uint32_t)k - 1)] : 0u;
+            v = (w1 << (8 * pad)) | (w0 >> (32 - 8 * pad));
+        }
+        c ^= v;
+        c = S.crc_t[3][c & 0xFF] ^ S.crc_t[2][(c >> 8) & 0xFF] ^ S.crc_t[1][(c >> 16) & 0xFF] ^
+            S.crc_t[0][c >> 24];
+    }
+    return c;
 }
 
 // Timing experiments only (scripts/variants.sh): skip parts of k_encode (wrong output).
@@ -1294,28 +1434,28 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         if (i < 288) S.lcode[i] = slot_from_code(cg[i]); else S.dcode[i - 288] = slot_from_code(cg[i]);
     }
     if (tid == 0) S.lcode[SLOT_NONE] = 0;
-    {
-        const bool hdr = first && gi.btype != 0;
+    {  // zero the (skewed) output words; the block header goes in after the barrier
         uint4* o4 = (uint4*)S.out;
-        for (uint32_t k = tid; k < (uint32_t)C::OUTW / 4; k += C::NT)
-            o4[k] = (hdr && 4 * k < (uint32_t)C::HDRW) ? *(const uint4*)(cg + 320 + 4 * k) : make_uint4(0, 0, 0, 0);
+        for (uint32_t k = tid; k < (uint32_t)(sizeof(S.out) / 16); k += C::NT) o4[k] = make_uint4(0, 0, 0, 0);
     }
+    const uint32_t hdrw = (first && gi.btype != 0 && tid < (uint32_t)C::HDRW) ? cg[320 + tid] : 0u;
     if (!PBX_ENC_SKIP_TABLES) {
         for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
         for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
     }
     __syncthreads();
+    stamp();  // diagnostics: loads and tables in LDS
+    if (hdrw) S.out[osk(tid)] = hdrw;
     if (gi.btype == 0) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; bytes
-        uint8_t* ob = (uint8_t*)S.out;
         const uint32_t cs = tid * C::CH, o = first ? 5u : 0u;
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
-            if (cs + i < sp.sl) ob[o + cs + i] = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
+            if (cs + i < sp.sl) *out_byte_ptr(S, o + cs + i) = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
         if (first && tid == 0) {
             const uint32_t len = bi.nbytes - 5;  // LEN: every byte of the block's segments
-            ob[0] = (uint8_t)(bi.fin ? 1 : 0);
-            ob[1] = (uint8_t)len; ob[2] = (uint8_t)(len >> 8);
-            ob[3] = (uint8_t)~len; ob[4] = (uint8_t)(~len >> 8);
+            *out_byte_ptr(S, 0) = (uint8_t)(bi.fin ? 1 : 0);
+            *out_byte_ptr(S, 1) = (uint8_t)len; *out_byte_ptr(S, 2) = (uint8_t)(len >> 8);
+            *out_byte_ptr(S, 3) = (uint8_t)~len; *out_byte_ptr(S, 4) = (uint8_t)(~len >> 8);
         }
     }
     __syncthreads();
@@ -1326,19 +1466,23 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) nbits += slot[i] >> 27;
     }
+    if (PROF) {  // diagnostics: slots built (wave 0)
+        __builtin_amdgcn_s_waitcnt(0);
+        stamp();
+    }
     S.t_a[tid] = nbits;
     __syncthreads();
     stamp();
     const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
     if (gi.btype != 0 && !PBX_ENC_SKIP_WRITE) {
         const uint32_t tb = lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
-        RunWriter<DevOps> bw(S.out, tb + S.t_a[tid]);
+        SkRunWriter bw(S.out, tb + S.t_a[tid]);
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
         bw.finish();
         if (lastb && tid == 0) {  // end of block; a non-final block ends byte-aligned
             const uint32_t eob = S.lcode[256];
-            BitWriter<DevOps> ew{S.out, tb + bitsum};
+            SkBitWriter ew{S.out, tb + bitsum};
             ew.put(eob & 0x7FFFFFFu, eob >> 27);
             if (!final_seg) {
                 ew.put(0, 3);
@@ -1356,10 +1500,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     const bool has_tail = !final_seg && (le & 7u) && !(lb && (le >> 3) == 0);
     if (tid == 0) {
         uint32_t part = 0;
-        if (lb) part |= out_byte(S, 0) | SP_HEAD;
-        if (has_tail) part |= (out_byte(S, le >> 3) << 8) | SP_TAIL;
+        if (lb) part |= out_byte_sk(S, 0) | SP_HEAD;
+        if (has_tail) part |= (out_byte_sk(S, le >> 3) << 8) | SP_TAIL;
         S.misc[M_CRCOP] = part;
-        if (lb) ((uint8_t*)S.out)[0] = 0;  // leading zero bytes leave a raw CRC unchanged
+        if (lb) *out_byte_ptr(S, 0) = 0;  // leading zero bytes leave a raw CRC unchanged
         S.misc[M_NBYTES] = o1;
     }
     __syncthreads();
@@ -1368,7 +1512,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     // shuffles with the constant operators x^(8*64*2^k), then across the waves
     uint32_t c = 0;
     if (!PBX_ENC_SKIP_CRC) {
-        c = ph_crc<C>(tid, S);
+        c = crc_chunk_sk<C>(tid, S);
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const uint32_t r = __shfl_down(c, 1 << k, 64);
@@ -1383,9 +1527,9 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
     const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
-    if (tid < head) dst[tid] = (uint8_t)out_byte(S, o0 + tid);
+    if (tid < head) dst[tid] = (uint8_t)out_byte_sk(S, o0 + tid);
     for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, o0 + head + 4 * k);
-    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte(S, o0 + j);
+    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_sk(S, o0 + j);
     __syncthreads();
     if (tid == 0) {
         uint32_t raw = S.red[0];
@@ -1523,11 +1667,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     const bool prof = a.stamps != nullptr;
     hipLaunchKernelGGL(k_seg_map, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
                        a.seg_tile, a.info, a.blk);
+    const uint32_t lz_grid = a.nseg;
     if (prof)
-        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
+        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     else
-        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
+        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     if (ev) (void)hipEventRecord(ev[0], st);
     if (prof)

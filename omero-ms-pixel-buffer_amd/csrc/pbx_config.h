@@ -19,7 +19,7 @@ namespace pbx {
 #define PBX_SEG 16384
 #endif
 #ifndef PBX_BLK
-#define PBX_BLK 2
+#define PBX_BLK 3
 #endif
 using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
 constexpr uint32_t BLK_SEGS = PBX_BLK;

@@ -53,6 +53,7 @@ struct DeflateLaunch {
     uint8_t* out;           // compacted containers
     uint64_t* stamps;       // [nseg * 32] phase clocks (diagnostics) or nullptr
     uint32_t* seg_tile;     // [nseg] tile of every segment (k_seg_map)
+    uint32_t cus = 256;     // compute units of the device (persistent grids)
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.  If ev is given,
 // ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.

@@ -147,6 +147,7 @@ struct Coalescer;
 
 struct pbx_ctx {
     int device = 0;
+    int cus = 256;                      // compute units (persistent kernel grids)
     pbx_config cfg{};
     hipStream_t stream = nullptr;       // kernels (batches run in launch order)
     hipStream_t copy_stream = nullptr;  // D2H of finished batches, overlapping later kernels
@@ -575,6 +576,7 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     ctx->cfg = cfg;
     ctx->hpool.pinned = true;
     hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1221,6 +1223,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.seg_tile = (uint32_t*)b->d_segmap;
     a.blk = (BlkInfo*)b->d_blk;
     a.nblk = b->nblk;
+    a.cus = (uint32_t)ctx->cus;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4));
