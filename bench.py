@@ -163,11 +163,12 @@ def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
             else:
                 chunks = list(ex.map(lambda c: _zarr.zlib_encode(c.tobytes(), 1), grid))
         cbytes = sum(len(c) for c in chunks)
+        packed = pbx.pack_chunks(chunks)  # the C-ABI's form: the chunk files back to back
         dec, plc, wall = [], [], []
         for r in range(reps + 1):
             t0 = time.perf_counter()
             pid, (md, mp) = svc.register_zarr_plane(21, 0, 0, 0, pbx.UINT16, side, side, chunk, chunk,
-                                                    comp, chunks, timing=True)
+                                                    comp, packed, timing=True)
             t1 = time.perf_counter()
             if r:
                 dec.append(md)

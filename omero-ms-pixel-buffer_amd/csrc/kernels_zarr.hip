@@ -596,10 +596,28 @@ __global__ __launch_bounds__(256) void k_zarr_copy(const ZStream* __restrict__ s
 }
 
 // ------------------------------------------------------------------------------- place
-// One workgroup per (chunk, band of ZP_ROWS chunk rows).  Each thread makes one sample:
-// blosc byte-unshuffle (typesize ts within blocks of `blocksize` bytes) + copy into the
-// plane (samples stay in the array's byte order); missing chunks get the fill bytes.
+// One workgroup per (chunk, band of ZP_ROWS chunk rows).  Blosc byte-unshuffle (typesize ts
+// within blocks of `blocksize` bytes) + copy into the pitched plane (samples stay in the
+// array's byte order); missing chunks get the fill bytes.  Fast path: each thread makes one
+// aligned 16-byte group of a plane row (16 / bpp samples): unshuffled chunks are one 16-byte
+// load, shuffled ones one load of 16 / bpp bytes from each byte plane, interleaved with byte
+// permutes (v_perm_b32).  Groups straddling a blosc block, row tails and unaligned rows take
+// the sample-by-sample path.
 constexpr uint32_t ZP_ROWS = 16;
+
+__device__ __forceinline__ uint32_t zperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);  // bytes 0-3 of lo, 4-7 of hi
+}
+
+// byte j of sample `col` of row r of the chunk (after unshuffling)
+__device__ __forceinline__ uint32_t zsample_byte(const uint8_t* s, uint32_t ts, uint32_t bs, uint32_t nb,
+                                                 uint32_t e, uint32_t bpp, uint32_t j) {
+    if (ts <= 1) return s[(size_t)e * bpp + j];
+    const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
+    const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
+    const uint32_t ne = bsize / ts;
+    return s[within < ne * ts ? blk * bs + (within % ts) * ne + within / ts : B];
+}
 
 __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ ch, uint32_t bands,
                                                     const ZPlane* __restrict__ planes,
@@ -621,72 +639,64 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
     const uint8_t* s = (c.flags & ZC_INPUT ? input : scratch) + c.src;
     const uint32_t ts = c.typesize, bs = c.blocksize, nb = c.nbytes;
     const bool missing = (c.flags & ZC_MISSING) != 0;
-    const bool fast = !missing && (ts == 1 || ts == bpp) && (bpp == 1 || bpp == 2 || bpp == 4);
-    const int32_t w4 = fast ? (w & ~3) : 0;
-    // fast path: 4 samples per thread, one (unaligned) dword load per byte plane; the band's
-    // (row, 4-sample group) pairs are spread over all 256 threads
-    if (w4 > 0) {
-        const int32_t groups = w4 >> 2, total = (r1 - r0) * groups;
+    const uint32_t G = 16 / bpp;  // samples per 16-byte group
+    uint8_t* const base = plane + (int64_t)c.y0 * pitch + (int64_t)c.x0 * bpp;
+    const bool aligned = ((((uintptr_t)base) | (uintptr_t)pitch) & 15) == 0;
+    const bool fast = aligned && (ts <= 1 || ts == bpp) && bpp <= 4;
+    const int32_t wg = fast ? (w / (int32_t)G) * (int32_t)G : 0;  // samples in whole groups
+    if (wg > 0) {
+        const int32_t groups = wg / (int32_t)G, total = (r1 - r0) * groups;
         for (int32_t g = (int32_t)threadIdx.x; g < total; g += 256) {
-            const int32_t r = r0 + g / groups, c4 = 4 * (g - (g / groups) * groups);
-            uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
-            {
-                const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)c4;
-                uint32_t out[4];
-                if (ts == 1) {
-                    if (bpp == 1) __builtin_memcpy(out, s + e, 4);
-                    else if (bpp == 2) __builtin_memcpy(out, s + (size_t)e * 2, 8);
-                    else __builtin_memcpy(out, s + (size_t)e * 4, 16);
+            const int32_t rr = g / groups, r = r0 + rr, col = (int32_t)G * (g - rr * groups);
+            uint4 o;
+            if (missing) {
+                uint32_t f = 0;
+                for (uint32_t j = 0; j < 4; j++) f |= (uint32_t)(fill >> (8 * (j % bpp)) & 0xffu) << (8 * j);
+                o = make_uint4(f, f, f, f);
+            } else {
+                const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
+                if (ts <= 1 || bpp == 1) {
+                    __builtin_memcpy(&o, s + (size_t)e * bpp, 16);
                 } else {
                     const uint32_t B = e * bpp, blk = B / bs;
                     const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
                     const uint32_t ne = bsize / ts, ie = (B - blk * bs) / ts;
-                    if (ie + 3 >= ne) {  // the 4 samples straddle a block: byte path below
-                        for (int32_t col = c4; col < c4 + 4; col++)
-                            for (uint32_t j = 0; j < bpp; j++) {
-                                const uint32_t Bj = ((uint32_t)r * (uint32_t)cw + (uint32_t)col) * bpp + j;
-                                const uint32_t bk = Bj / bs, wi = Bj - bk * bs;
-                                const uint32_t bz = nb - bk * bs < bs ? nb - bk * bs : bs, nz = bz / ts;
-                                o[(int64_t)col * bpp + j] = s[wi < nz * ts ? bk * bs + (wi % ts) * nz + wi / ts : Bj];
-                            }
-                        continue;
-                    }
-                    const uint8_t* q = s + blk * bs + ie;
-                    uint32_t p[4];
-                    for (uint32_t j = 0; j < bpp; j++) p[j] = ld_u32_unaligned(q + j * ne);
-                    if (bpp == 2) {
-                        out[0] = (p[0] & 0xff) | (p[1] & 0xff) << 8 | (p[0] & 0xff00) << 8 | (p[1] & 0xff00) << 16;
-                        out[1] = (p[0] >> 16 & 0xff) | (p[1] >> 16 & 0xff) << 8 | (p[0] >> 24) << 16 | (p[1] >> 24) << 24;
-                    } else {  // bpp == 4
-                        for (uint32_t i = 0; i < 4; i++)
-                            out[i] = (p[0] >> (8 * i) & 0xff) | (p[1] >> (8 * i) & 0xff) << 8 |
-                                     (p[2] >> (8 * i) & 0xff) << 16 | (p[3] >> (8 * i) & 0xff) << 24;
+                    if (ie + G > ne) {  // the group straddles a block (or its leftover bytes)
+                        uint32_t v[4] = {0, 0, 0, 0};
+                        for (uint32_t q = 0; q < 16; q++)
+                            v[q >> 2] |= zsample_byte(s, ts, bs, nb, e + q / bpp, bpp, q % bpp) << (8 * (q & 3));
+                        o = make_uint4(v[0], v[1], v[2], v[3]);
+                    } else {
+                        const uint8_t* q = s + (size_t)blk * bs + ie;
+                        if (bpp == 2) {  // 8 samples: 8 bytes of each byte plane
+                            uint2 p0, p1;
+                            __builtin_memcpy(&p0, q, 8);
+                            __builtin_memcpy(&p1, q + ne, 8);
+                            o = make_uint4(zperm(p1.x, p0.x, 0x05010400u), zperm(p1.x, p0.x, 0x07030602u),
+                                           zperm(p1.y, p0.y, 0x05010400u), zperm(p1.y, p0.y, 0x07030602u));
+                        } else {  // bpp == 4: 4 samples, a 4 x 4 byte transpose
+                            uint32_t a, b2, c2, d;
+                            __builtin_memcpy(&a, q, 4);
+                            __builtin_memcpy(&b2, q + ne, 4);
+                            __builtin_memcpy(&c2, q + 2 * ne, 4);
+                            __builtin_memcpy(&d, q + 3 * ne, 4);
+                            const uint32_t t0 = zperm(b2, a, 0x05010400u), t1 = zperm(d, c2, 0x05010400u);
+                            const uint32_t t2 = zperm(b2, a, 0x07030602u), t3 = zperm(d, c2, 0x07030602u);
+                            o = make_uint4(zperm(t1, t0, 0x05040100u), zperm(t1, t0, 0x07060302u),
+                                           zperm(t3, t2, 0x05040100u), zperm(t3, t2, 0x07060302u));
+                        }
                     }
                 }
-                uint8_t* d = o + (int64_t)c4 * bpp;
-                if (bpp == 1) __builtin_memcpy(d, out, 4);
-                else if (bpp == 2) __builtin_memcpy(d, out, 8);
-                else __builtin_memcpy(d, out, 16);
             }
+            *(uint4*)(base + (int64_t)r * pitch + (int64_t)col * bpp) = o;
         }
     }
-    for (int32_t r = r0; r < r1; r++) {
-        uint8_t* o = plane + (int64_t)(c.y0 + r) * pitch + (int64_t)c.x0 * bpp;
-        for (int32_t col = w4 + (int32_t)threadIdx.x; col < w; col += 256) {
+    for (int32_t r = r0; r < r1; r++) {  // the rest of every row, sample by sample
+        uint8_t* o = base + (int64_t)r * pitch;
+        for (int32_t col = wg + (int32_t)threadIdx.x; col < w; col += 256) {
             const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
             for (uint32_t j = 0; j < bpp; j++) {
-                uint32_t v;
-                if (missing) {
-                    v = (uint32_t)(fill >> (8 * j)) & 0xffu;
-                } else if (ts > 1) {
-                    const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
-                    const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
-                    const uint32_t ne = bsize / ts;
-                    const uint32_t pos = within < ne * ts ? blk * bs + (within % ts) * ne + within / ts : B;
-                    v = s[pos];
-                } else {
-                    v = s[e * bpp + j];
-                }
+                const uint32_t v = missing ? (uint32_t)(fill >> (8 * j)) & 0xffu : zsample_byte(s, ts, bs, nb, e, bpp, j);
                 o[(int64_t)col * bpp + j] = (uint8_t)v;
             }
         }

@@ -19,6 +19,7 @@
 #include <string>
 #include <thread>
 #include <tuple>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -738,6 +739,57 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
     return undo(PBX_OK);  // events only
 }
 
+// ------------------------------------------------------------- staged host -> HBM upload
+namespace {
+
+// Copies host bytes (pageable caller memory) to HBM through pinned staging blocks of the
+// context's pinned pool: each piece is copied into a pinned block by several host threads
+// (one thread's memcpy is the bottleneck otherwise) and DMA'd asynchronously on `st` while
+// the next piece is being staged.  Returns once every piece is staged and its DMA queued; the
+// pinned blocks go back to the pool after their copies completed.
+int upload_staged(pbx_ctx* ctx, uint8_t* dev, const uint8_t* host, uint64_t bytes, hipStream_t st) {
+    constexpr uint64_t PIECE = 32ull << 20;
+    constexpr int NBUF = 3;
+    if (bytes < (4ull << 20)) {  // small: one pageable copy
+        HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, st));
+        return PBX_OK;
+    }
+    void* blk[NBUF] = {};
+    hipEvent_t ev[NBUF] = {};
+    bool used[NBUF] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < NBUF && e == hipSuccess; i++) {
+        blk[i] = ctx->hpool.get(PIECE, &e);
+        if (blk[i]) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    }
+    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (uint64_t off = 0, p = 0; off < bytes && e == hipSuccess; off += PIECE, p++) {
+        const int b = (int)(p % NBUF);
+        const uint64_t n = std::min(PIECE, bytes - off);
+        if (used[b]) e = hipEventSynchronize(ev[b]);  // the block's previous DMA is done
+        if (e != hipSuccess) break;
+        uint8_t* dst = (uint8_t*)blk[b];
+        const uint64_t per = (n + nth - 1) / nth;
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nth && t * per < n; t++)
+            th.emplace_back([=] { memcpy(dst + t * per, host + off + t * per, std::min(per, n - t * per)); });
+        memcpy(dst, host + off, std::min(per, n));
+        for (auto& x : th) x.join();
+        e = hipMemcpyAsync(dev + off, dst, n, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(ev[b], st);
+        used[b] = true;
+    }
+    for (int i = 0; i < NBUF; i++) {
+        if (used[i]) (void)hipEventSynchronize(ev[i]);
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+        if (blk[i]) ctx->hpool.put(blk[i]);
+    }
+    if (e != hipSuccess) return fail(PBX_E_INTERNAL, "staged upload: %s", hipGetErrorString(e));
+    return PBX_OK;
+}
+
+}  // namespace
+
 // ------------------------------------------------------------------ NGFF / Zarr planes
 namespace {
 
@@ -933,36 +985,47 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     ZPlane* d_pl = nullptr;
     uint32_t* d_err = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    // launch scratch (input, decoded chunks, tables) comes from the context's device pool and
+    // goes back to it: only the planes themselves are new allocations
     auto cleanup = [&](bool planes_too) {
-        if (d_in) (void)hipFree(d_in);
-        if (d_scr) (void)hipFree(d_scr);
-        if (d_st) (void)hipFree(d_st);
-        if (d_ch) (void)hipFree(d_ch);
-        if (d_pl) (void)hipFree(d_pl);
-        if (d_err) (void)hipFree(d_err);
-        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        for (void* q : {(void*)d_in, (void*)d_scr, (void*)d_st, (void*)d_ch, (void*)d_pl, (void*)d_err})
+            if (q) ctx->dpool.put(q);
+        for (auto& x : ev) if (x) (void)hipEventDestroy(x);
         if (planes_too)
             for (Plane& p : ps) if (p.dev) (void)hipFree(p.dev);
     };
     hipError_t e = hipSuccess;
+    auto dget = [&](auto*& ptr, size_t bytes) {
+        if (e != hipSuccess) return;
+        ptr = (std::remove_reference_t<decltype(ptr)>)ctx->dpool.get(std::max<size_t>(bytes, 256), &e);
+    };
     for (uint64_t k = 0; k < n && e == hipSuccess; k++) {
         e = hipMalloc((void**)&ps[k].dev, ps[k].bytes);
         zp[k].dev = ps[k].dev;
     }
-    if (e == hipSuccess) e = hipMalloc((void**)&d_in, in_bytes + 4096);  // decoder window over-read slack
-    if (e == hipSuccess && P.scratch) e = hipMalloc((void**)&d_scr, P.scratch);
-    if (e == hipSuccess && nstreams) e = hipMalloc((void**)&d_st, sizeof(ZStream) * nstreams);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_ch, sizeof(ZChunk) * P.chunks.size());
-    if (e == hipSuccess) e = hipMalloc((void**)&d_pl, sizeof(ZPlane) * n);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_err, sizeof(uint32_t) * (nstreams + 1));
+    dget(d_in, in_bytes + 4096);  // decoder window over-read slack
+    if (P.scratch) dget(d_scr, P.scratch);
+    if (nstreams) dget(d_st, sizeof(ZStream) * nstreams);
+    dget(d_ch, sizeof(ZChunk) * P.chunks.size());
+    dget(d_pl, sizeof(ZPlane) * n);
+    dget(d_err, sizeof(uint32_t) * (nstreams + 1));
     for (auto& x : ev) if (e == hipSuccess) e = hipEventCreate(&x);
+    if (e != hipSuccess) {
+        cleanup(true);
+        return fail(PBX_E_INTERNAL, "zarr decode: %s", hipGetErrorString(e));
+    }
     for (uint64_t k = 0; k < n && e == hipSuccess; k++) {
         const uint64_t len = in_base[k + 1] - in_base[k];
         const int64_t gx = (ds[k].size_x + zs[k].chunk_x - 1) / zs[k].chunk_x;
         const int64_t gy = (ds[k].size_y + zs[k].chunk_y - 1) / zs[k].chunk_y;
         const uint64_t used = zs[k].offsets[gx * gy];
-        if (used) e = hipMemcpyAsync(d_in + in_base[k], zs[k].data, used, hipMemcpyHostToDevice, ctx->stream);
-        if (e == hipSuccess && len > used) e = hipMemsetAsync(d_in + in_base[k] + used, 0, len - used, ctx->stream);
+        if (used) {
+            if (int rc = upload_staged(ctx, d_in + in_base[k], zs[k].data, used, ctx->stream)) {
+                cleanup(true);
+                return rc;
+            }
+        }
+        if (len > used) e = hipMemsetAsync(d_in + in_base[k] + used, 0, len - used, ctx->stream);
     }
     if (e == hipSuccess) e = hipMemsetAsync(d_in + in_bytes, 0, 4096, ctx->stream);
     if (e == hipSuccess && nstreams)

@@ -344,6 +344,17 @@ def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, level
                 big_endian=dt[0] != "<", fill_bits=fill_bits)
 
 
+def pack_chunks(chunks: Sequence[Optional[bytes]]):
+    """Chunk files of one plane as the C-ABI takes them: (uint8 data, uint64 offsets[n+1]),
+    the files concatenated in C order over the chunk grid (None / b"" = missing chunk)."""
+    import numpy as np
+    lens = np.array([len(b) if b else 0 for b in chunks], dtype=np.uint64)
+    offsets = np.zeros(len(chunks) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
+    return data, offsets
+
+
 class PixelsService:
     """Plane registry on one MI355X (the PixelsService / getPixels stand-in).
 
@@ -422,16 +433,13 @@ class PixelsService:
                             big_endian: bool = True, fill_bits: int = 0, level: int = 0,
                             timing: bool = False):
         """Register a plane from its Zarr v2 chunks (C order over the chunk grid; None or
-        b"" = missing chunk -> fill), decoded on the GPU (pbx_plane_register_zarr).  codec is
+        b"" = missing chunk -> fill; or pack_chunks()' (data, offsets) pair), decoded on the GPU
+        (pbx_plane_register_zarr).  codec is
         the .zarray compressor id: None, "blosc" or "zlib".  Returns the plane id (and the
         decode / placement kernels' device ms with timing=True)."""
-        import numpy as np
         if codec not in ZARR_CODECS:
             raise PbxError(400, "unsupported Zarr compressor %r" % (codec,))
-        lens = np.array([len(b) if b else 0 for b in chunks], dtype=np.uint64)
-        offsets = np.zeros(len(chunks) + 1, dtype=np.uint64)
-        np.cumsum(lens, out=offsets[1:])
-        data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
+        data, offsets = chunks if isinstance(chunks, tuple) else pack_chunks(chunks)
         d = PbxPlaneDesc()
         d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, level
         d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
@@ -460,10 +468,7 @@ class PixelsService:
             if p["codec"] not in ZARR_CODECS:
                 raise PbxError(400, "unsupported Zarr compressor %r" % (p["codec"],))
             chunks = p["chunks"]
-            lens = np.array([len(b) if b else 0 for b in chunks], dtype=np.uint64)
-            offsets = np.zeros(len(chunks) + 1, dtype=np.uint64)
-            np.cumsum(lens, out=offsets[1:])
-            data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
+            data, offsets = chunks if isinstance(chunks, tuple) else pack_chunks(chunks)
             keep += [offsets, data]
             d = descs[k]
             d.image_id, d.z, d.c, d.t = p["image_id"], p["z"], p["c"], p["t"]
