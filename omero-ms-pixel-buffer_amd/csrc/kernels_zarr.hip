@@ -23,139 +23,9 @@
 #include "dev_util.h"
 #include "pbx_common.h"
 #include "pbx_kernels.h"
+#include "zarr_dev.h"
 
 namespace pbx {
-
-constexpr uint32_t ZR_INF = 4096;            // LDS output ring per wave (inflate): 16 waves/CU
-constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
-constexpr uint32_t ZWAVES = 4;              // waves per workgroup
-constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
-
-// Dynamic LDS of the decoders, addressed by offset (a pointer into LDS kept in a struct would
-// become a FLAT pointer; a selected one, a stack slot).  Per wave: ring, then (inflate) tables.
-extern __shared__ uint8_t zlds[];
-
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
-    uint32_t v;
-    __builtin_memcpy(&v, p, 4);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t rfl(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-// Input window of ZWIN bytes in LDS (wave-uniform reads are LDS reads: a VGPR window would
-// put an s_waitcnt vmcnt(0) -- which on gfx9 also waits for every pending flush store --
-// in front of each use).  Reloaded by one 16-byte load per lane.  The device source buffer
-// has ZSLACK bytes after its last stream, so window loads never leave the allocation.
-constexpr uint32_t ZWIN = 1024;  // the runtime leaves 4 KiB of slack after the streams
-
-struct InWin {
-    const uint8_t* in;
-    uint32_t wo, base, lane;  // LDS offset of the window, stream offset it starts at
-    __device__ void load(uint32_t q) {
-        base = q;
-        uint4 v;
-        __builtin_memcpy(&v, in + q + 16 * lane, 16);
-        *(uint4*)(zlds + wo + 16 * lane) = v;
-    }
-    __device__ uint32_t byte(uint32_t q) {
-        if (q - base > ZWIN - 1) load(q);
-        return rfl(zlds[wo + q - base]);
-    }
-    // 32 bits starting at byte q (little-endian)
-    __device__ uint32_t dword(uint32_t q) {
-        if (q - base > ZWIN - 4) load(q);
-        uint32_t v;
-        __builtin_memcpy(&v, zlds + wo + q - base, 4);  // one unaligned ds_read_b32
-        return rfl(v);
-    }
-    // bytes q .. q+15 as four little-endian words: one unaligned ds_read_b128 (gfx950 LDS
-    // takes byte-aligned accesses)
-    __device__ void peek16(uint32_t q, uint32_t (&d)[4]) {
-        if (q - base > ZWIN - 16) load(q);
-        uint4 v;
-        __builtin_memcpy(&v, zlds + wo + q - base, 16);
-        d[0] = rfl(v.x);
-        d[1] = rfl(v.y);
-        d[2] = rfl(v.z);
-        d[3] = rfl(v.w);
-    }
-    // byte q + lane for every lane
-    __device__ uint32_t lane_byte(uint32_t q) {
-        if (q - base > ZWIN - 64) load(q);
-        return zlds[wo + q - base + lane];
-    }
-};
-
-// Output through the LDS ring (offset rb, 256-aligned); bytes [flushed, op) are in the ring
-// only.  Completed 256-byte runs go to HBM as one dword store per lane.
-template <uint32_t RING>
-struct OutRing {
-    static constexpr uint32_t ZM = RING - 1, ZR = RING;
-    uint32_t rb;
-    uint8_t* out;
-    uint32_t op, flushed, olen, lane;
-    __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
-    __device__ void flush(uint32_t upto) {
-        uint32_t f = rfl(flushed);  // keep the ring state in SGPRs (scalar branches)
-        upto = rfl(upto);
-        while (upto - f >= 256u) {
-            const uint32_t v = *(const uint32_t*)(zlds + rb + ((f + 4 * lane) & ZM));
-            __builtin_memcpy(out + f + 4 * lane, &v, 4);
-            f += 256;
-        }
-        flushed = f;
-    }
-    __device__ void finish() {
-        for (uint32_t k = flushed; k < op; k += 64)
-            if (k + lane < op) out[k + lane] = ring(k + lane);
-        flushed = op;
-    }
-    // out[op .. op+len) = out[op-off .. op-off+len) (overlapping: period off)
-    // lane % off for off < 64 without an integer division: lane / off is exact to within 1/63
-    // in float, so +0.001 never crosses an integer
-    __device__ uint32_t period_lane(uint32_t off) const {
-        if (off >= 64) return lane;
-        const float inv = __builtin_amdgcn_rcpf((float)off);
-        return lane - off * (uint32_t)((float)lane * inv + 0.001f);
-    }
-    __device__ bool match(uint32_t off, uint32_t len) {
-        if (off == 0 || off > op || len > olen - op) return false;
-        const uint32_t rep = period_lane(off);
-        if (off > ZR) {
-            // a far source lies below `flushed`: wait for this wave's stores, read HBM
-            for (uint32_t k = 0; k < len; k += 64) {
-                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                const uint32_t v = *(const __attribute__((address_space(1))) uint8_t*)(out + p - off + rep);
-                if (lane < n) ring(p + lane) = (uint8_t)v;
-                flush(p + n);
-            }
-        } else {
-            for (uint32_t k = 0; k < len; k += 64) {
-                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
-                const uint32_t v = ring(p - off + rep);
-                if (lane < n) ring(p + lane) = (uint8_t)v;
-                flush(p + n);
-            }
-        }
-        op += len;
-        return true;
-    }
-    __device__ void put1(uint32_t v) {
-        if (lane == 0) ring(op) = (uint8_t)v;
-        op = rfl(op) + 1;
-        // `flushed` is a multiple of 256 and every other writer flushes as it goes, so a
-        // single byte completes a run exactly when op reaches a multiple of 256
-        if ((op & 255u) == 0) flush(op);
-    }
-};
 
 // ------------------------------------------------------------------------------ LZ4
 __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st, uint32_t n,
@@ -276,6 +146,69 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
                o.op, (unsigned long long)(t1 - t0), (unsigned long long)(r1 - r0));
     }
 #endif
+    if (lane == 0) err[si] = bad;
+}
+
+// --------------------------------------------------------------------------- BloscLZ
+// c-blosc 1.21's internal codec (format restated in oracle/zarr_oracle.c): control byte < 32
+// = ctrl + 1 literals; else a match of (ctrl >> 5) + 2 bytes (7: + 255-terminated extension
+// bytes) at distance ((ctrl & 31) << 8) + next byte + 1, or 16-bit big-endian + 8192 when
+// those are 31 and 255.  A match is only copied when another control byte follows.
+__global__ __launch_bounds__(256) void k_zarr_blosclz(const ZStream* __restrict__ st, uint32_t n,
+                                                      const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);  // wave-uniform (SGPR) state
+    const uint32_t si = blockIdx.x * ZWAVES + w;
+    if (si >= n) return;
+    const ZStream t = st[si];
+    const uint32_t ilen = rfl(t.csize);
+    const uint32_t wb = w * (ZR_LZ4 + ZWIN);
+    InWin win{src + t.src_off, wb + ZR_LZ4, 0, lane};
+    win.load(0);
+    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+    uint32_t ip = 0, bad = ilen == 0 ? 1u : 0u;
+    uint32_t ctrl = bad ? 0u : win.byte(ip++) & 31u;
+    while (!bad) {
+        if (ctrl >= 32) {
+            uint32_t len = (ctrl >> 5) - 1, code = 0;
+            const uint32_t ofs = (ctrl & 31u) << 8;
+            if (len == 6) {
+                do {
+                    if (ip + 1 >= ilen) { bad = 2; break; }
+                    code = win.byte(ip++);
+                    len += code;
+                } while (code == 255);
+                if (bad) break;
+            } else if (ip + 1 >= ilen) {
+                bad = 3;
+                break;
+            }
+            code = win.byte(ip++);
+            len += 3;
+            uint32_t dist = ofs + code + 1;
+            if (code == 255 && ofs == (31u << 8)) {  // 16-bit distance
+                if (ip + 1 >= ilen) { bad = 4; break; }
+                dist = (win.byte(ip) << 8 | win.byte(ip + 1)) + 8192;
+                ip += 2;
+            }
+            if (len > o.olen - o.op || dist > o.op) { bad = 5; break; }
+            if (ip >= ilen) break;
+            ctrl = win.byte(ip++);
+            if (!o.match(dist, len)) { bad = 6; break; }
+        } else {
+            const uint32_t nl = ctrl + 1;  // <= 32 literals: one lane step
+            if (nl > o.olen - o.op || ip + nl > ilen) { bad = 7; break; }
+            const uint32_t v = win.lane_byte(ip);
+            if (lane < nl) o.ring(o.op + lane) = (uint8_t)v;
+            o.op += nl;
+            o.flush(o.op);
+            ip += nl;
+            if (ip >= ilen) break;
+            ctrl = win.byte(ip++);
+        }
+    }
+    if (!bad && o.op != o.olen) bad = 8;
+    o.finish();
     if (lane == 0) err[si] = bad;
 }
 
@@ -609,9 +542,21 @@ __device__ __forceinline__ uint32_t zperm(uint32_t hi, uint32_t lo, uint32_t sel
     return __builtin_amdgcn_perm(hi, lo, sel);  // bytes 0-3 of lo, 4-7 of hi
 }
 
-// byte j of sample `col` of row r of the chunk (after unshuffling)
+// byte j of sample e of the chunk (after unshuffling; bit: the bit-shuffle layout of
+// oracle/zarr_oracle.c -- a block of n = bsize / ts elements, n % 8 == 0, is ts * 8 bit rows of
+// n / 8 bytes, row j * 8 + k holding bit k of byte j of every element; other blocks are raw)
 __device__ __forceinline__ uint32_t zsample_byte(const uint8_t* s, uint32_t ts, uint32_t bs, uint32_t nb,
-                                                 uint32_t e, uint32_t bpp, uint32_t j) {
+                                                 uint32_t e, uint32_t bpp, uint32_t j, bool bit = false) {
+    if (bit) {
+        const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
+        const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs, ne = bsize / ts;
+        if (bsize < ts || (ne & 7u) || within >= ne * ts) return s[B];
+        const uint32_t i = within / ts, jj = within - i * ts, row = ne >> 3;
+        const uint8_t* r = s + (size_t)blk * bs + (size_t)jj * 8 * row + (i >> 3);
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 8; k++) v |= ((r[(size_t)k * row] >> (i & 7u)) & 1u) << k;
+        return v;
+    }
     if (ts <= 1) return s[(size_t)e * bpp + j];
     const uint32_t B = e * bpp + j, blk = B / bs, within = B - blk * bs;
     const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs;
@@ -639,9 +584,48 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
     const uint8_t* s = (c.flags & ZC_INPUT ? input : scratch) + c.src;
     const uint32_t ts = c.typesize, bs = c.blocksize, nb = c.nbytes;
     const bool missing = (c.flags & ZC_MISSING) != 0;
+    const bool bit = (c.flags & ZC_BITSHUF) != 0;
     const uint32_t G = 16 / bpp;  // samples per 16-byte group
     uint8_t* const base = plane + (int64_t)c.y0 * pitch + (int64_t)c.x0 * bpp;
     const bool aligned = ((((uintptr_t)base) | (uintptr_t)pitch) & 15) == 0;
+    if (bit && !missing) {
+        // bit shuffle: a thread makes 8 samples of a row (8 elements share each bit-row byte):
+        // per byte j of the sample, the 8 bit rows' bytes -> an 8 x 8 bit transpose
+        const int32_t w8 = (ts == bpp && (cw & 7) == 0) ? (w & ~7) : 0;
+        const int32_t groups = w8 >> 3, total = (r1 - r0) * groups;
+        for (int32_t g = (int32_t)threadIdx.x; g < total; g += 256) {
+            const int32_t rr = g / groups, r = r0 + rr, col = 8 * (g - rr * groups);
+            const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
+            const uint32_t B = e * bpp, blk = B / bs;
+            const uint32_t bsize = nb - blk * bs < bs ? nb - blk * bs : bs, ne = bsize / ts;
+            uint8_t* o = base + (int64_t)r * pitch + (int64_t)col * bpp;
+            const uint32_t i = (B - blk * bs) / ts;  // element index in the block (multiple of 8)
+            if (bsize < ts || (ne & 7u) || i + 8 > ne) {
+                for (uint32_t q = 0; q < 8 * bpp; q++) o[q] = (uint8_t)zsample_byte(s, ts, bs, nb, e + q / bpp, bpp, q % bpp, true);
+                continue;
+            }
+            const uint32_t row = ne >> 3;
+            const uint8_t* rb = s + (size_t)blk * bs + (i >> 3);
+            for (uint32_t j = 0; j < bpp; j++) {
+                // x byte k = bit row (j, k)'s byte: bit m of it = bit k of element m's byte j
+                uint64_t x = 0;
+                for (uint32_t k = 0; k < 8; k++) x |= (uint64_t)rb[(size_t)(j * 8 + k) * row] << (8 * k);
+                // 8 x 8 bit transpose (delta swaps): afterwards byte m, bit k = old byte k, bit m
+                uint64_t tt = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull; x ^= tt ^ (tt << 7);
+                tt = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull; x ^= tt ^ (tt << 14);
+                tt = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= tt ^ (tt << 28);
+                for (uint32_t m = 0; m < 8; m++) o[m * bpp + j] = (uint8_t)(x >> (8 * m));
+            }
+        }
+        for (int32_t r = r0; r < r1; r++) {  // row tails (and chunks whose width is not 8k)
+            uint8_t* o = base + (int64_t)r * pitch;
+            for (int32_t col = w8 + (int32_t)threadIdx.x; col < w; col += 256) {
+                const uint32_t e = (uint32_t)r * (uint32_t)cw + (uint32_t)col;
+                for (uint32_t j = 0; j < bpp; j++) o[(int64_t)col * bpp + j] = (uint8_t)zsample_byte(s, ts, bs, nb, e, bpp, j, true);
+            }
+        }
+        return;
+    }
     const bool fast = aligned && (ts <= 1 || ts == bpp) && bpp <= 4;
     const int32_t wg = fast ? (w / (int32_t)G) * (int32_t)G : 0;  // samples in whole groups
     if (wg > 0) {
@@ -703,19 +687,28 @@ __global__ __launch_bounds__(256) void k_zarr_place(const ZChunk* __restrict__ c
     }
 }
 
-hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t n_lz4,
-                              uint32_t n_infl, uint32_t n_copy, const uint8_t* src, uint8_t* scratch,
-                              uint32_t* err) {
-    // streams are ordered: lz4 first, then inflate, then copy
-    if (n_lz4)
-        hipLaunchKernelGGL(k_zarr_lz4, dim3((n_lz4 + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZR_LZ4 + ZWIN), st,
-                           d_streams, n_lz4, src, scratch, err);
-    if (n_infl)
-        hipLaunchKernelGGL(k_zarr_inflate, dim3((n_infl + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), ZWAVES * (ZI_BYTES + ZWIN), st,
-                           d_streams + n_lz4, n_infl, src, scratch, err + n_lz4);
-    if (n_copy)
-        hipLaunchKernelGGL(k_zarr_copy, dim3((n_copy + ZWAVES - 1) / ZWAVES), dim3(64 * ZWAVES), 0, st,
-                           d_streams + n_lz4 + n_infl, n_copy, src, scratch, err + n_lz4 + n_infl);
+hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, const uint32_t* counts,
+                              const uint8_t* src, uint8_t* scratch, uint8_t* zstd_lit, uint32_t* err) {
+    // streams are ordered by kind: lz4, inflate, copy, blosclz, zstd
+    uint32_t first = 0;
+    for (uint32_t k = 0; k < ZS_NKINDS; k++) {
+        const uint32_t n = counts[k];
+        const ZStream* s = d_streams + first;
+        uint32_t* e = err + first;
+        first += n;
+        if (!n) continue;
+        const dim3 g((n + ZWAVES - 1) / ZWAVES), b(64 * ZWAVES);
+        switch (k) {
+        case ZS_LZ4: hipLaunchKernelGGL(k_zarr_lz4, g, b, ZWAVES * (ZR_LZ4 + ZWIN), st, s, n, src, scratch, e); break;
+        case ZS_ZLIB: hipLaunchKernelGGL(k_zarr_inflate, g, b, ZWAVES * (ZI_BYTES + ZWIN), st, s, n, src, scratch, e); break;
+        case ZS_COPY: hipLaunchKernelGGL(k_zarr_copy, g, b, 0, st, s, n, src, scratch, e); break;
+        case ZS_BLOSCLZ: hipLaunchKernelGGL(k_zarr_blosclz, g, b, ZWAVES * (ZR_LZ4 + ZWIN), st, s, n, src, scratch, e); break;
+        default: {
+            hipError_t r = launch_zarr_zstd(st, s, n, src, scratch, zstd_lit, e);
+            if (r != hipSuccess) return r;
+        }
+        }
+    }
     return hipGetLastError();
 }
 

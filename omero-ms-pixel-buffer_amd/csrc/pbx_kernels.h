@@ -64,16 +64,17 @@ hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* 
                           const uint32_t* hist, uint32_t* codes);
 
 // NGFF/Zarr chunk decode (kernels_zarr.hip).  One wave per stream.
-enum : uint32_t { ZS_LZ4 = 0, ZS_ZLIB = 1, ZS_COPY = 2 };
+enum : uint32_t { ZS_LZ4 = 0, ZS_ZLIB = 1, ZS_COPY = 2, ZS_BLOSCLZ = 3, ZS_ZSTD = 4, ZS_NKINDS = 5 };
 struct ZStream {
     uint64_t src_off;  // compressed bytes in the uploaded chunk buffer
     uint64_t dst_off;  // decoded bytes in the scratch buffer
     uint32_t csize, dlen, kind, pad;
 };
-enum : uint32_t { ZC_MISSING = 1u, ZC_INPUT = 2u };
+enum : uint32_t { ZC_MISSING = 1u, ZC_INPUT = 2u, ZC_BITSHUF = 4u };
 struct ZChunk {
     uint64_t src;                         // decoded chunk: scratch offset (or input offset if ZC_INPUT)
-    uint32_t nbytes, blocksize, typesize; // blosc geometry (typesize 1 = not shuffled)
+    uint32_t nbytes, blocksize, typesize; // blosc geometry (typesize 1 = not byte-shuffled;
+                                          // with ZC_BITSHUF the bit-shuffle element size)
     uint32_t flags;                       // ZC_*
     int32_t x0, y0;                       // chunk origin in the plane
     uint32_t plane, pad;                  // index into the ZPlane table of the launch
@@ -85,10 +86,14 @@ struct ZPlane {                           // a destination plane of one decode l
     uint32_t bpp, pad;
     uint64_t fill;                        // fill bytes in stored order (missing chunks)
 };
-// Streams ordered lz4 | inflate | copy; err[i] = 0 or a decoder error code per stream.
-hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, uint32_t n_lz4,
-                              uint32_t n_infl, uint32_t n_copy, const uint8_t* src, uint8_t* scratch,
-                              uint32_t* err);
+// Streams ordered by kind (ZS_LZ4 | ZS_ZLIB | ZS_COPY | ZS_BLOSCLZ | ZS_ZSTD), counts[k] of
+// kind k; err[i] = 0 or a decoder error code per stream.
+// zstd_lit: zstd_scratch_bytes(counts[ZS_ZSTD]) bytes (a block's literals per zstd frame).
+hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, const uint32_t* counts,
+                              const uint8_t* src, uint8_t* scratch, uint8_t* zstd_lit, uint32_t* err);
+size_t zstd_scratch_bytes(uint32_t nstreams);
+hipError_t launch_zarr_zstd(hipStream_t st, const ZStream* d_streams, uint32_t n, const uint8_t* src,
+                            uint8_t* scratch, uint8_t* litbuf, uint32_t* err);
 hipError_t launch_zarr_place(hipStream_t st, const ZChunk* d_chunks, uint32_t nchunks,
                              const ZPlane* d_planes, int32_t max_chunk_y, const uint8_t* scratch,
                              const uint8_t* input);

@@ -800,7 +800,7 @@ uint32_t rd_le32(const uint8_t* p) {
 // Host plan of one plane's chunks: metadata only (blosc headers, block starts and split
 // sizes); every byte of chunk data is decoded on the GPU.  Frame layout: oracle/zarr_oracle.c.
 struct ZarrPlan {
-    std::vector<ZStream> lz4, infl, copy;
+    std::vector<ZStream> kind[ZS_NKINDS];  // streams by decoder (enum ZS_*)
     std::vector<ZChunk> chunks;
     uint64_t scratch = 0;
 };
@@ -840,7 +840,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, uint64
         const uint64_t dst = P.scratch;
         if (z->codec == PBX_ZARR_ZLIB) {
             if (len > 0xffffffffull) return fail(PBX_E_BADARG, "chunk %lld too large", (long long)i);
-            P.infl.push_back(ZStream{ob, dst, (uint32_t)len, (uint32_t)cb, ZS_ZLIB, 0});
+            P.kind[ZS_ZLIB].push_back(ZStream{ob, dst, (uint32_t)len, (uint32_t)cb, ZS_ZLIB, 0});
             c.src = dst;
             P.chunks.push_back(c);
             P.scratch += (cb + 255) & ~255ull;
@@ -851,7 +851,7 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, uint64
         if (len < 16) return fail(PBX_E_BADARG, "chunk %lld: short blosc header", (long long)i);
         const uint32_t ver = f[0], flags = f[2], ts = f[3] ? f[3] : 1;
         const uint32_t nbytes = rd_le32(f + 4), bs = rd_le32(f + 8), cbytes = rd_le32(f + 12);
-        if (ver > 2) return fail(PBX_E_BADARG, "chunk %lld: blosc format version %u (blosc2?)", (long long)i, ver);
+        if (ver != 2) return fail(PBX_E_BADARG, "chunk %lld: blosc format version %u (c-blosc 1.x writes 2)", (long long)i, ver);
         if (nbytes != cb) return fail(PBX_E_BADARG, "chunk %lld: blosc nbytes %u != chunk bytes %llu",
                                       (long long)i, nbytes, (unsigned long long)cb);
         if (cbytes > len || cbytes < 16) return fail(PBX_E_BADARG, "chunk %lld: blosc cbytes %u", (long long)i, cbytes);
@@ -862,11 +862,11 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, uint64
             P.chunks.push_back(c);
             continue;
         }
-        if (flags & 0x4) return fail(PBX_E_BADARG, "chunk %lld: blosc bit shuffle is not supported", (long long)i);
-        const uint32_t codec = flags >> 5;
-        if (codec != 1 && codec != 3)
-            return fail(PBX_E_BADARG, "chunk %lld: blosc codec %u not supported (lz4/lz4hc/zlib only)",
+        const uint32_t codec = flags >> 5;  // 0 blosclz, 1 lz4 / lz4hc, 2 snappy, 3 zlib, 4 zstd
+        if (codec != 0 && codec != 1 && codec != 3 && codec != 4)
+            return fail(PBX_E_BADARG, "chunk %lld: blosc codec %u not supported (blosclz/lz4/lz4hc/zlib/zstd)",
                         (long long)i, codec);
+        static const uint32_t kind_of[5] = {ZS_BLOSCLZ, ZS_LZ4, 0, ZS_ZLIB, ZS_ZSTD};
         if (bs == 0 || bs > nbytes || (bs % ts)) return fail(PBX_E_BADARG, "chunk %lld: blosc blocksize %u", (long long)i, bs);
         const uint32_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
         if (16ull + 4ull * nblocks > cbytes) return fail(PBX_E_BADARG, "chunk %lld: short block table", (long long)i);
@@ -883,15 +883,19 @@ int zarr_plan(const pbx_plane_desc* d, const pbx_zarr_chunks* z, int bpp, uint64
                 pos += 4;
                 if (pos + cs > cbytes || cs > neb || cs == 0)
                     return fail(PBX_E_BADARG, "chunk %lld: block %u split %u size %u", (long long)i, b, s, cs);
-                const ZStream zs{ob + pos, dst + (uint64_t)b * bs + (uint64_t)s * neb, cs, neb,
-                                 cs == neb ? ZS_COPY : (codec == 1 ? ZS_LZ4 : ZS_ZLIB), 0};
-                (cs == neb ? P.copy : codec == 1 ? P.lz4 : P.infl).push_back(zs);
+                const uint32_t k = cs == neb ? ZS_COPY : kind_of[codec];
+                P.kind[k].push_back(ZStream{ob + pos, dst + (uint64_t)b * bs + (uint64_t)s * neb, cs, neb, k, 0});
                 pos += cs;
             }
         }
         c.src = dst;
         c.blocksize = bs;
-        c.typesize = (flags & 0x1) ? ts : 1;
+        if (flags & 0x4) {  // bit shuffle (takes precedence over the byte-shuffle bit)
+            c.flags |= ZC_BITSHUF;
+            c.typesize = ts;
+        } else {
+            c.typesize = (flags & 0x1) ? ts : 1;
+        }
         P.chunks.push_back(c);
         P.scratch += (cb + 255) & ~255ull;
     }
@@ -973,13 +977,14 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
         zp[k] = ZPlane{nullptr, p.pitch, d->size_x, d->size_y, zs[k].chunk_x, zs[k].chunk_y,
                        (uint32_t)bpp, 0, fill};
     }
-    const uint32_t nstreams = (uint32_t)(P.lz4.size() + P.infl.size() + P.copy.size());
+    uint32_t counts[ZS_NKINDS], nstreams = 0;
     std::vector<ZStream> all;
-    all.reserve(nstreams);
-    all.insert(all.end(), P.lz4.begin(), P.lz4.end());
-    all.insert(all.end(), P.infl.begin(), P.infl.end());
-    all.insert(all.end(), P.copy.begin(), P.copy.end());
-    uint8_t *d_in = nullptr, *d_scr = nullptr;
+    for (uint32_t k = 0; k < ZS_NKINDS; k++) {
+        counts[k] = (uint32_t)P.kind[k].size();
+        nstreams += counts[k];
+        all.insert(all.end(), P.kind[k].begin(), P.kind[k].end());
+    }
+    uint8_t *d_in = nullptr, *d_scr = nullptr, *d_lit = nullptr;
     ZStream* d_st = nullptr;
     ZChunk* d_ch = nullptr;
     ZPlane* d_pl = nullptr;
@@ -988,7 +993,7 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     // launch scratch (input, decoded chunks, tables) comes from the context's device pool and
     // goes back to it: only the planes themselves are new allocations
     auto cleanup = [&](bool planes_too) {
-        for (void* q : {(void*)d_in, (void*)d_scr, (void*)d_st, (void*)d_ch, (void*)d_pl, (void*)d_err})
+        for (void* q : {(void*)d_in, (void*)d_scr, (void*)d_lit, (void*)d_st, (void*)d_ch, (void*)d_pl, (void*)d_err})
             if (q) ctx->dpool.put(q);
         for (auto& x : ev) if (x) (void)hipEventDestroy(x);
         if (planes_too)
@@ -1005,6 +1010,7 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     }
     dget(d_in, in_bytes + 4096);  // decoder window over-read slack
     if (P.scratch) dget(d_scr, P.scratch);
+    if (counts[ZS_ZSTD]) dget(d_lit, zstd_scratch_bytes(counts[ZS_ZSTD]));
     if (nstreams) dget(d_st, sizeof(ZStream) * nstreams);
     dget(d_ch, sizeof(ZChunk) * P.chunks.size());
     dget(d_pl, sizeof(ZPlane) * n);
@@ -1036,8 +1042,7 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     if (e == hipSuccess) e = hipMemsetAsync(d_err, 0, sizeof(uint32_t) * (nstreams + 1), ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ev[0], ctx->stream);
     if (e == hipSuccess)
-        e = launch_zarr_decode(ctx->stream, d_st, (uint32_t)P.lz4.size(), (uint32_t)P.infl.size(),
-                               (uint32_t)P.copy.size(), d_in, d_scr, d_err);
+        e = launch_zarr_decode(ctx->stream, d_st, counts, d_in, d_scr, d_lit, d_err);
     if (e == hipSuccess) e = hipEventRecord(ev[1], ctx->stream);
     if (e == hipSuccess)
         e = launch_zarr_place(ctx->stream, d_ch, (uint32_t)P.chunks.size(), d_pl, max_cy, d_scr, d_in);
@@ -1054,9 +1059,11 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     }
     for (uint32_t s = 0; s < nstreams; s++)
         if (err[s]) {
+            static const char* names[ZS_NKINDS] = {"lz4", "zlib", "stored", "blosclz", "zstd"};
+            uint32_t k = 0, first = 0;
+            while (s >= first + counts[k]) first += counts[k++];
             cleanup(true);
-            return fail(PBX_E_BADARG, "corrupt chunk stream %u (%s, decoder code %u)", s,
-                        s < P.lz4.size() ? "lz4" : s < P.lz4.size() + P.infl.size() ? "zlib" : "stored", err[s]);
+            return fail(PBX_E_BADARG, "corrupt chunk stream %u (%s, decoder code %u)", s, names[k], err[s]);
         }
     if (kernel_ms) {
         float a = 0, b = 0;

@@ -1,0 +1,142 @@
+// zarr_dev.h — device helpers shared by the Zarr chunk decoders (kernels_zarr.hip,
+// kernels_zstd.hip): the per-wave LDS input window and output ring.  Everything about a
+// stream's parse is wave-uniform and kept in SGPRs (readfirstlane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbx {
+
+constexpr uint32_t ZR_INF = 4096;            // LDS output ring per wave (inflate): 16 waves/CU
+constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
+constexpr uint32_t ZWAVES = 4;              // waves per workgroup
+constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
+
+// Dynamic LDS of the decoders, addressed by offset (a pointer into LDS kept in a struct would
+// become a FLAT pointer; a selected one, a stack slot).  Per wave: ring, then (inflate) tables.
+extern __shared__ uint8_t zlds[];
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Input window of ZWIN bytes in LDS (wave-uniform reads are LDS reads: a VGPR window would
+// put an s_waitcnt vmcnt(0) -- which on gfx9 also waits for every pending flush store --
+// in front of each use).  Reloaded by one 16-byte load per lane.  The device source buffer
+// has ZSLACK bytes after its last stream, so window loads never leave the allocation.
+constexpr uint32_t ZWIN = 1024;  // the runtime leaves 4 KiB of slack after the streams
+
+struct InWin {
+    const uint8_t* in;
+    uint32_t wo, base, lane;  // LDS offset of the window, stream offset it starts at
+    __device__ void load(uint32_t q) {
+        base = q;
+        uint4 v;
+        __builtin_memcpy(&v, in + q + 16 * lane, 16);
+        *(uint4*)(zlds + wo + 16 * lane) = v;
+    }
+    __device__ uint32_t byte(uint32_t q) {
+        if (q - base > ZWIN - 1) load(q);
+        return rfl(zlds[wo + q - base]);
+    }
+    // 32 bits starting at byte q (little-endian)
+    __device__ uint32_t dword(uint32_t q) {
+        if (q - base > ZWIN - 4) load(q);
+        uint32_t v;
+        __builtin_memcpy(&v, zlds + wo + q - base, 4);  // one unaligned ds_read_b32
+        return rfl(v);
+    }
+    // bytes q .. q+15 as four little-endian words: one unaligned ds_read_b128 (gfx950 LDS
+    // takes byte-aligned accesses)
+    __device__ void peek16(uint32_t q, uint32_t (&d)[4]) {
+        if (q - base > ZWIN - 16) load(q);
+        uint4 v;
+        __builtin_memcpy(&v, zlds + wo + q - base, 16);
+        d[0] = rfl(v.x);
+        d[1] = rfl(v.y);
+        d[2] = rfl(v.z);
+        d[3] = rfl(v.w);
+    }
+    // byte q + lane for every lane
+    __device__ uint32_t lane_byte(uint32_t q) {
+        if (q - base > ZWIN - 64) load(q);
+        return zlds[wo + q - base + lane];
+    }
+};
+
+// Output through the LDS ring (offset rb, 256-aligned); bytes [flushed, op) are in the ring
+// only.  Completed 256-byte runs go to HBM as one dword store per lane.
+template <uint32_t RING>
+struct OutRing {
+    static constexpr uint32_t ZM = RING - 1, ZR = RING;
+    uint32_t rb;
+    uint8_t* out;
+    uint32_t op, flushed, olen, lane;
+    __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
+    __device__ void flush(uint32_t upto) {
+        uint32_t f = rfl(flushed);  // keep the ring state in SGPRs (scalar branches)
+        upto = rfl(upto);
+        while (upto - f >= 256u) {
+            const uint32_t v = *(const uint32_t*)(zlds + rb + ((f + 4 * lane) & ZM));
+            __builtin_memcpy(out + f + 4 * lane, &v, 4);
+            f += 256;
+        }
+        flushed = f;
+    }
+    __device__ void finish() {
+        for (uint32_t k = flushed; k < op; k += 64)
+            if (k + lane < op) out[k + lane] = ring(k + lane);
+        flushed = op;
+    }
+    // out[op .. op+len) = out[op-off .. op-off+len) (overlapping: period off)
+    // lane % off for off < 64 without an integer division: lane / off is exact to within 1/63
+    // in float, so +0.001 never crosses an integer
+    __device__ uint32_t period_lane(uint32_t off) const {
+        if (off >= 64) return lane;
+        const float inv = __builtin_amdgcn_rcpf((float)off);
+        return lane - off * (uint32_t)((float)lane * inv + 0.001f);
+    }
+    __device__ bool match(uint32_t off, uint32_t len) {
+        if (off == 0 || off > op || len > olen - op) return false;
+        const uint32_t rep = period_lane(off);
+        if (off > ZR) {
+            // a far source lies below `flushed`: wait for this wave's stores, read HBM
+            for (uint32_t k = 0; k < len; k += 64) {
+                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                const uint32_t v = *(const __attribute__((address_space(1))) uint8_t*)(out + p - off + rep);
+                if (lane < n) ring(p + lane) = (uint8_t)v;
+                flush(p + n);
+            }
+        } else {
+            for (uint32_t k = 0; k < len; k += 64) {
+                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
+                const uint32_t v = ring(p - off + rep);
+                if (lane < n) ring(p + lane) = (uint8_t)v;
+                flush(p + n);
+            }
+        }
+        op += len;
+        return true;
+    }
+    __device__ void put1(uint32_t v) {
+        if (lane == 0) ring(op) = (uint8_t)v;
+        op = rfl(op) + 1;
+        // `flushed` is a multiple of 256 and every other writer flushes as it goes, so a
+        // single byte completes a run exactly when op reaches a multiple of 256
+        if ((op & 255u) == 0) flush(op);
+    }
+};
+
+
+}  // namespace pbx

@@ -113,6 +113,9 @@ double pbxo_bench(int kind, int pixel_type, int format, int32_t plane_w, int32_t
  * enum pbx_zarr_codec. */
 enum { PBXO_ZARR_RAW = 0, PBXO_ZARR_BLOSC = 1, PBXO_ZARR_ZLIB = 2 };
 int pbxo_lz4_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen);
+int pbxo_blosclz_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen);
+/* -2 when the system libzstd cannot be loaded */
+int pbxo_zstd_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen);
 int pbxo_blosc_info(const uint8_t* in, size_t len, uint32_t* nbytes, uint32_t* blocksize,
                     uint32_t* typesize, uint32_t* flags);
 int pbxo_blosc_decode(const uint8_t* in, size_t len, uint8_t* out, size_t cap, size_t* out_len);

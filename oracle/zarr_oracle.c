@@ -25,9 +25,22 @@
  *     Byte shuffle within a block of bsize bytes: byte j of element i sits at j*(bsize/ts)+i.
  *   - LZ4 block format: sequences [token][lit-len ext][literals][offset u16 LE][match ext];
  *     match length = low nibble + 4 (+ ext bytes), the last sequence has literals only.
+ *   - BloscLZ (c-blosc 1.21's internal codec, FastLZ-derived): a control byte; < 32: a run
+ *     of ctrl + 1 literals; else a match of length (ctrl >> 5) + 2 (7 -> 255-terminated
+ *     extension bytes added), distance ((ctrl & 31) << 8) + next byte + 1, or when those two
+ *     are 31 and 255, a 16-bit big-endian distance + 8192.  The first control byte's top
+ *     three bits carry the level.  A match is only copied when another control byte follows
+ *     (streams end with literals).
+ *   - Zstandard (RFC 8878) inside blosc: one zstd frame per split; decoded here with the
+ *     system libzstd (1.4.8, loaded at run time), as zlib is with the system zlib.
+ *   - Bit shuffle (flag 0x4, format version 2): a block of n = bsize / ts elements with
+ *     n % 8 == 0 is stored as ts * 8 bit rows of n / 8 bytes: row j * 8 + k holds bit k of byte
+ *     j of every element, element i at bit i % 8 of byte i / 8; other blocks are stored as is.
  * Pinned by fixtures encoded with c-blosc 1.21.0 / zlib via imagecodecs 2021.8.26
- * (tests/golden/zarr/make_zarr_golden.py) and round trips through the system liblz4.
+ * (tests/golden/zarr/make_zarr_golden.py), round trips through the system liblz4, and (CPU
+ * tests) the c-blosc 1.21.0 library's own decoder on frames it encoded.
  */
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -80,6 +93,90 @@ int pbxo_lz4_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen) {
     return op == olen ? 0 : -1;
 }
 
+int pbxo_blosclz_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen) {
+    size_t ip = 0, op = 0;
+    if (ilen == 0) return -1;
+    uint32_t ctrl = in[ip++] & 31u;
+    for (;;) {
+        if (ctrl >= 32) {
+            size_t len = (ctrl >> 5) - 1;
+            size_t ofs = (size_t)(ctrl & 31u) << 8;
+            if (len == 6) {
+                unsigned code;
+                do {
+                    if (ip + 1 >= ilen) return -1;
+                    code = in[ip++];
+                    len += code;
+                } while (code == 255);
+            } else if (ip + 1 >= ilen) {
+                return -1;
+            }
+            const unsigned code = in[ip++];
+            len += 3;
+            size_t dist = ofs + code + 1;
+            if (code == 255 && ofs == (31u << 8)) {  /* 16-bit distance */
+                if (ip + 1 >= ilen) return -1;
+                dist = ((size_t)in[ip] << 8 | in[ip + 1]) + 8191 + 1;
+                ip += 2;
+            }
+            if (op + len > olen || dist > op) return -1;
+            if (ip >= ilen) break;  /* (c-blosc: a match is copied only if a control byte follows) */
+            ctrl = in[ip++];
+            for (size_t k = 0; k < len; k++) out[op + k] = out[op + k - dist];  /* overlap-safe */
+            op += len;
+        } else {
+            const size_t n = ctrl + 1;
+            if (op + n > olen || ip + n > ilen) return -1;
+            memcpy(out + op, in + ip, n);
+            op += n;
+            ip += n;
+            if (ip >= ilen) break;
+            ctrl = in[ip++];
+        }
+    }
+    return op == olen ? 0 : -1;
+}
+
+/* libzstd (system 1.4.8), resolved at run time: the oracle builds without its header. */
+typedef size_t (*zstd_decompress_fn)(void*, size_t, const void*, size_t);
+typedef unsigned (*zstd_iserror_fn)(size_t);
+static zstd_decompress_fn p_zstd_decompress;
+static zstd_iserror_fn p_zstd_iserror;
+
+static int zstd_load(void) {
+    if (p_zstd_decompress) return 0;
+    void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return -1;
+    p_zstd_iserror = (zstd_iserror_fn)dlsym(h, "ZSTD_isError");
+    p_zstd_decompress = (zstd_decompress_fn)dlsym(h, "ZSTD_decompress");
+    return p_zstd_decompress && p_zstd_iserror ? 0 : -1;
+}
+
+int pbxo_zstd_decode(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen) {
+    if (zstd_load()) return -2;
+    const size_t n = p_zstd_decompress(out, olen, in, ilen);
+    if (p_zstd_iserror(n)) return -1;
+    return n == olen ? 0 : -1;
+}
+
+/* bit unshuffle of one block (format version 2): see the header comment */
+static void bitunshuffle_block(const uint8_t* in, uint8_t* out, uint32_t bsize, uint32_t ts) {
+    const uint32_t n = bsize / ts;
+    if (n % 8) {
+        memcpy(out, in, bsize);
+        return;
+    }
+    const uint32_t row = n / 8;
+    memset(out, 0, (size_t)n * ts);
+    for (uint32_t j = 0; j < ts; j++)
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint8_t* r = in + (size_t)(j * 8 + k) * row;
+            for (uint32_t i = 0; i < n; i++)
+                out[(size_t)i * ts + j] |= (uint8_t)(((r[i >> 3] >> (i & 7)) & 1u) << k);
+        }
+    memcpy(out + (size_t)n * ts, in + (size_t)n * ts, bsize - n * ts);
+}
+
 static int zlib_exact(const uint8_t* in, size_t ilen, uint8_t* out, size_t olen) {
     uLongf n = (uLongf)olen;
     if (uncompress(out, &n, in, (uLong)ilen) != Z_OK) return -1;
@@ -108,12 +205,13 @@ int pbxo_blosc_decode(const uint8_t* in, size_t len, uint8_t* out, size_t cap, s
         memcpy(out, in + 16, nbytes);
         return 0;
     }
-    if (bs == 0 || (flags & 0x4)) return -1;  /* bit shuffle: not restated */
+    if (bs == 0 || in[0] != 2) return -1;  /* c-blosc 1.x frames (format version 2) */
     const uint32_t codec = flags >> 5;
-    if (codec != 1 && codec != 3) return -1;  /* lz4 / zlib only */
+    if (codec != 0 && codec != 1 && codec != 3 && codec != 4) return -1;  /* no snappy */
     const uint32_t nblocks = (nbytes + bs - 1) / bs, leftover = nbytes % bs;
     if (16 + 4 * (size_t)nblocks > cbytes) return -1;
-    uint8_t* tmp = (flags & 0x1) && ts > 1 ? (uint8_t*)malloc(bs) : NULL;
+    const int bitshuf = (flags & 0x4) != 0, byteshuf = !bitshuf && (flags & 0x1) && ts > 1;
+    uint8_t* tmp = byteshuf || bitshuf ? (uint8_t*)malloc(bs) : NULL;
     int rc = 0;
     for (uint32_t b = 0; b < nblocks && !rc; b++) {
         const int is_left = leftover && b == nblocks - 1;
@@ -128,11 +226,16 @@ int pbxo_blosc_decode(const uint8_t* in, size_t len, uint8_t* out, size_t cap, s
             pos += 4;
             if (pos + cs > cbytes || cs > neb) { rc = -1; break; }
             if (cs == neb) memcpy(dst + (size_t)s * neb, in + pos, neb);
+            else if (codec == 0) rc = pbxo_blosclz_decode(in + pos, cs, dst + (size_t)s * neb, neb);
             else if (codec == 1) rc = pbxo_lz4_decode(in + pos, cs, dst + (size_t)s * neb, neb);
-            else rc = zlib_exact(in + pos, cs, dst + (size_t)s * neb, neb);
+            else if (codec == 3) rc = zlib_exact(in + pos, cs, dst + (size_t)s * neb, neb);
+            else rc = pbxo_zstd_decode(in + pos, cs, dst + (size_t)s * neb, neb);
             pos += cs;
         }
-        if (!rc && tmp) {  /* byte unshuffle of this block */
+        if (!rc && bitshuf) {
+            if (bsize >= ts) bitunshuffle_block(tmp, out + (size_t)b * bs, bsize, ts);
+            else memcpy(out + (size_t)b * bs, tmp, bsize);
+        } else if (!rc && tmp) {  /* byte unshuffle of this block */
             const uint32_t ne = bsize / ts;
             uint8_t* o = out + (size_t)b * bs;
             for (uint32_t j = 0; j < ts; j++)

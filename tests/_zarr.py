@@ -115,13 +115,60 @@ def chunk_grid(plane: np.ndarray, chunk_y: int, chunk_x: int):
     return out
 
 
+# The real c-blosc 1.21.0 (the image's /opt/conda libblosc, the library imagecodecs and
+# numcodecs wrap), used to ENCODE test chunks with every codec and shuffle mode (blosclz,
+# lz4, lz4hc, zlib, zstd; no / byte / bit shuffle) and, in CPU tests, to decode them as a
+# second reference next to oracle/zarr_oracle.c.  Test infrastructure only.
+CBLOSC_PATH = "/opt/conda/lib/libblosc.so.1"
+_cb = None
+
+
+def cblosc():
+    """ctypes handle of c-blosc 1.21 or None when the image lacks it."""
+    global _cb
+    if _cb is None:
+        import os
+        if not os.path.exists(CBLOSC_PATH):
+            _cb = False
+            return None
+        L = ctypes.CDLL(CBLOSC_PATH)
+        L.blosc_compress_ctx.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+        L.blosc_decompress_ctx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _cb = L
+    return _cb or None
+
+
+def cblosc_encode(raw: bytes, typesize: int, cname: str = "lz4", clevel: int = 5, shuffle: int = 1,
+                  blocksize: int = 0) -> bytes:
+    """blosc_compress_ctx (shuffle 0 none, 1 byte, 2 bit)."""
+    L = cblosc()
+    out = ctypes.create_string_buffer(len(raw) + 64)
+    n = L.blosc_compress_ctx(clevel, shuffle, typesize, len(raw), raw, out, len(out), cname.encode(),
+                             blocksize, 1)
+    assert n > 0, (cname, n)
+    return out.raw[:n]
+
+
+def cblosc_decode(enc: bytes, nbytes: int) -> bytes:
+    L = cblosc()
+    out = ctypes.create_string_buffer(max(nbytes, 1))
+    n = L.blosc_decompress_ctx(enc, out, nbytes, 1)
+    assert n == nbytes, n
+    return out.raw[:nbytes]
+
+
 def encode_chunks(plane: np.ndarray, chunk_y: int, chunk_x: int, compressor, **kw):
     """Chunk files of a plane for the .zarray compressor id (None, "blosc", "zlib");
-    kw: blosc_encode options (codec, clevel, shuffle, blocksize, split) or zlib level."""
+    kw: blosc_encode options (codec, clevel, shuffle, blocksize, split) or zlib level; with
+    cname=... the chunks come from the real c-blosc (cblosc_encode options)."""
     out = []
     for c in chunk_grid(plane, chunk_y, chunk_x):
         raw = c.tobytes()
-        if compressor == "blosc":
+        if compressor == "blosc" and "cname" in kw:
+            out.append(cblosc_encode(raw, c.dtype.itemsize, **kw))
+        elif compressor == "blosc":
             out.append(blosc_encode(raw, c.dtype.itemsize, **kw))
         elif compressor == "zlib":
             out.append(zlib_encode(raw, kw.get("level", 1)))

@@ -44,20 +44,33 @@ CASES = [
     ("zlib_l6_u16_smooth_256x256", (256, 256), ">u2", "smooth", "zlib", dict(level=6)),
     ("zlib_l9_u8_128x100", (128, 100), "u1", "smooth", "zlib", dict(level=9)),
     ("zlib_l6_u16_noise_128x128", (128, 128), ">u2", "noise", "zlib", dict(level=6)),
-    # codecs the GPU path rejects with 400 (the oracle rejects them too)
-    ("unsupported_blosc_zstd_u16_64x64", (64, 64), ">u2", "smooth", "blosc", dict(compressor="zstd", level=5, shuffle=1)),
-    ("unsupported_blosc_blosclz_u16_128x128", (128, 128), ">u2", "smooth", "blosc", dict(compressor="blosclz", level=5, shuffle=1)),
-    ("unsupported_blosc_bitshuffle_u16_128x128", (128, 128), ">u2", "smooth", "blosc", dict(compressor="lz4", level=5, shuffle=2)),
+    # blosc-zstd, blosclz and bit shuffle (round 1 rejected these with 400; decoded since round 2)
+    ("blosc_zstd_u16_64x64", (64, 64), ">u2", "smooth", "blosc", dict(compressor="zstd", level=5, shuffle=1)),
+    ("blosc_blosclz_u16_128x128", (128, 128), ">u2", "smooth", "blosc", dict(compressor="blosclz", level=5, shuffle=1)),
+    ("blosc_lz4_bitshuffle_u16_128x128", (128, 128), ">u2", "smooth", "blosc", dict(compressor="lz4", level=5, shuffle=2)),
+    ("blosc_zstd_u16_600x500", (600, 500), ">u2", "noise", "blosc", dict(compressor="zstd", level=5, shuffle=1)),
+    ("blosc_zstd_l1_f32_256x256", (256, 256), ">f4", "noise", "blosc", dict(compressor="zstd", level=1, shuffle=1)),
+    ("blosc_zstd_l9_u8_300x200", (300, 200), "u1", "smooth", "blosc", dict(compressor="zstd", level=9, shuffle=0)),
+    ("blosc_zstd_bitshuffle_u16_512x512", (512, 512), ">u2", "noise", "blosc", dict(compressor="zstd", level=5, shuffle=2)),
+    ("blosc_blosclz_u16_600x500", (600, 500), ">u2", "noise", "blosc", dict(compressor="blosclz", level=5, shuffle=1)),
+    ("blosc_blosclz_l9_u8_256x256", (256, 256), "u1", "smooth", "blosc", dict(compressor="blosclz", level=9, shuffle=0)),
+    ("blosc_blosclz_i32_le_100x97", (100, 97), "<i4", "smooth", "blosc", dict(compressor="blosclz", level=5, shuffle=1)),
+    ("blosc_blosclz_bitshuffle_f32_128x130", (128, 130), ">f4", "noise", "blosc", dict(compressor="blosclz", level=5, shuffle=2)),
+    ("blosc_lz4_bitshuffle_u8_333x101", (333, 101), "u1", "noise", "blosc", dict(compressor="lz4", level=5, shuffle=2)),
+    ("blosc_lz4_bitshuffle_f64_100x77", (100, 77), ">f8", "smooth", "blosc", dict(compressor="lz4", level=5, shuffle=2)),
+    ("blosc_zlib_bitshuffle_u16_257x255", (257, 255), ">u2", "noise", "blosc", dict(compressor="zlib", level=5, shuffle=2)),
 ]
 
 
 def main():
-    manifest = {"generator": "imagecodecs %s, %s" % (ic.__version__, ic.blosc_version()), "cases": []}
+    manifest = {"generator": "imagecodecs %s, %s, %s" % (ic.__version__, ic.blosc_version(), ic.zstd_version()),
+                "cases": []}
     for i, (name, shape, dtype, kind, codec, params) in enumerate(CASES):
         a = image(shape[0], shape[1], dtype, seed=i, kind=kind)
         raw = a.tobytes()
         if codec == "blosc":
             enc = ic.blosc_encode(raw, typesize=a.dtype.itemsize, numthreads=1, **params)
+            assert ic.blosc_decode(enc) == raw
         else:
             enc = ic.zlib_encode(raw, level=params["level"])
         with open(os.path.join(HERE, name + ".enc"), "wb") as f:
