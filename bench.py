@@ -156,12 +156,22 @@ def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
     svc.release_plane(pid)
     grid = _zarr.chunk_grid(plane, chunk, chunk)
     res = {}
-    for name, comp, kw in (("blosc_lz4", "blosc", {}), ("zlib1", "zlib", {"level": 1})):
+    codecs = [("blosc_lz4", "blosc", {}), ("zlib1", "zlib", {"level": 1})]
+    if _zarr.cblosc() is not None:  # chunks written by the real c-blosc 1.21
+        codecs += [("blosc_zstd5", "blosc", {"cname": "zstd", "clevel": 5, "shuffle": 1}),
+                   ("blosc_blosclz5", "blosc", {"cname": "blosclz", "clevel": 5, "shuffle": 1}),
+                   ("blosc_lz4_bitshuffle", "blosc", {"cname": "lz4", "clevel": 5, "shuffle": 2})]
+
+    def enc(c, comp, kw):
+        if comp == "zlib":
+            return _zarr.zlib_encode(c.tobytes(), 1)
+        if "cname" in kw:
+            return _zarr.cblosc_encode(c.tobytes(), 2, kw["cname"], kw["clevel"], kw["shuffle"])
+        return _zarr.blosc_encode(c.tobytes(), 2)
+
+    for name, comp, kw in codecs:
         with ThreadPoolExecutor(16) as ex:
-            if comp == "blosc":
-                chunks = list(ex.map(lambda c: _zarr.blosc_encode(c.tobytes(), 2), grid))
-            else:
-                chunks = list(ex.map(lambda c: _zarr.zlib_encode(c.tobytes(), 1), grid))
+            chunks = list(ex.map(lambda c: enc(c, comp, kw), grid))
         cbytes = sum(len(c) for c in chunks)
         packed = pbx.pack_chunks(chunks)  # the C-ABI's form: the chunk files back to back
         dec, plc, wall = [], [], []

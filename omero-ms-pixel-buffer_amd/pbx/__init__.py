@@ -313,18 +313,34 @@ def zarr_array_meta(array_dir: str) -> dict:
     return meta
 
 
+def _lead_axes(ndim: int, axes: Optional[Sequence[str]]) -> List[str]:
+    """Names of the leading (non-y/x) axes of an array: the NGFF multiscales "axes" when given
+    (0.4: time, then channel, then space), else t, c, z with missing ones dropped from the left."""
+    if axes is not None:
+        names = [a["name"] if isinstance(a, dict) else a for a in axes]
+        if len(names) != ndim or [n.lower() for n in names[-2:]] != ["y", "x"]:
+            raise PbxError(400, "axes %r do not end in y, x" % (names,))
+        lead = [n.lower() for n in names[:-2]]
+        if any(n not in ("t", "c", "z") for n in lead) or len(set(lead)) != len(lead):
+            raise PbxError(400, "unsupported axes %r" % (names,))
+        return lead
+    return ["t", "c", "z"][3 - (ndim - 2):]
+
+
 def zarr_plane_spec(array_dir: str, image_id: int, z: int, c: int, t: int, level: int = 0,
-                    meta: Optional[dict] = None) -> dict:
-    """register_zarr_planes() arguments for plane (z, c, t) of an NGFF array directory (NGFF
-    axis order t, c, z, y, x; fewer leading axes drop from the left): chunk files named by
-    dimension_separator "." or "/", absent files = fill_value."""
+                    meta: Optional[dict] = None, axes: Optional[Sequence] = None) -> dict:
+    """register_zarr_planes() arguments for plane (z, c, t) of an NGFF array directory (axes:
+    the multiscales "axes" of the image, else NGFF order t, c, z, y, x with fewer leading axes
+    dropped from the left): chunk files named by dimension_separator "." or "/", absent
+    files = fill_value.  `level` is the stored pyramid level (0 = full resolution)."""
     import numpy as np
     meta = meta or zarr_array_meta(array_dir)
     shape, chunk, dt = meta["shape"], meta["chunks"], meta["dtype"]
     comp = meta.get("compressor")
-    k = len(shape) - 2
-    lead, dropped = [t, c, z][3 - k:], [t, c, z][:3 - k]
-    if any(dropped):
+    names = _lead_axes(len(shape), axes)
+    want = {"t": t, "c": c, "z": z}
+    lead = [want[n] for n in names]
+    if any(want[n] for n in ("t", "c", "z") if n not in names):
         raise PbxError(404, "plane (z=%d, c=%d, t=%d) outside the array" % (z, c, t))
     for v, n in zip(lead, shape[:-2]):
         if not 0 <= v < n:
@@ -353,6 +369,20 @@ def pack_chunks(chunks: Sequence[Optional[bytes]]):
     np.cumsum(lens, out=offsets[1:])
     data = np.frombuffer(b"".join(b for b in chunks if b) or b"\0", dtype=np.uint8)
     return data, offsets
+
+
+def ngff_multiscales(image_dir: str):
+    """(multiscales[0], image directory) of an NGFF image (.zattrs, NGFF 0.1-0.4); a
+    bioformats2raw container root (attribute "bioformats2raw.layout") resolves to series 0."""
+    import json
+    with open(os.path.join(image_dir, ".zattrs")) as f:
+        attrs = json.load(f)
+    if "multiscales" not in attrs and "bioformats2raw.layout" in attrs:
+        return ngff_multiscales(os.path.join(image_dir, "0"))
+    ms = attrs.get("multiscales")
+    if not ms or not ms[0].get("datasets"):
+        raise PbxError(400, "no multiscales datasets in %s/.zattrs" % image_dir)
+    return ms[0], image_dir
 
 
 class PixelsService:
@@ -493,19 +523,50 @@ class PixelsService:
         sp = zarr_plane_spec(array_dir, image_id, z, c, t, level)
         return self.register_zarr_planes([sp])[0]
 
+    @staticmethod
+    def _array_planes(meta: dict, axes) -> List[Tuple[int, int, int]]:
+        names = _lead_axes(len(meta["shape"]), axes)
+        ext = {"t": 1, "c": 1, "z": 1}
+        ext.update(dict(zip(names, meta["shape"][:-2])))
+        return [(z, c, t) for t in range(ext["t"]) for c in range(ext["c"]) for z in range(ext["z"])]
+
     def register_zarr_array_planes(self, array_dir: str, image_id: int,
                                    planes: Optional[Sequence[Tuple[int, int, int]]] = None,
-                                   level: int = 0) -> Dict[Tuple[int, int, int], int]:
+                                   level: int = 0, axes=None) -> Dict[Tuple[int, int, int], int]:
         """Every (z, c, t) plane of an NGFF array (or the given ones) decoded by ONE set of GPU
         launches (pbx_planes_register_zarr).  Returns {(z, c, t): plane id}."""
         meta = zarr_array_meta(array_dir)
-        lead = list(meta["shape"][:-2])
-        lead = [1] * (3 - len(lead)) + lead  # (t, c, z) extents
         if planes is None:
-            planes = [(z, c, t) for t in range(lead[0]) for c in range(lead[1]) for z in range(lead[2])]
-        specs = [zarr_plane_spec(array_dir, image_id, z, c, t, level, meta) for z, c, t in planes]
+            planes = self._array_planes(meta, axes)
+        specs = [zarr_plane_spec(array_dir, image_id, z, c, t, level, meta, axes) for z, c, t in planes]
         ids = self.register_zarr_planes(specs)
         return dict(zip([tuple(p) for p in planes], ids))
+
+    def register_ngff_image(self, image_dir: str, image_id: int,
+                            planes: Optional[Sequence[Tuple[int, int, int]]] = None
+                            ) -> Dict[int, Dict[Tuple[int, int, int], int]]:
+        """A whole NGFF multiscale image -- what ZarrPixelsService opens for an image
+        (omero-zarr-pixel-buffer 0.6.1, build.gradle:57; PixelBufferVerticle.java:29,56) -- in
+        ONE set of GPU launches: .zattrs "multiscales"[0] lists the datasets from full
+        resolution down; dataset k becomes stored level k of every (z, c, t) plane (or of the
+        given ones).  A bioformats2raw container (root .zattrs with "bioformats2raw.layout")
+        is opened at its series 0.  Requests then select levels with OMERO's numbering:
+        TileCtx.resolution = levels - 1 - k (TileRequestHandler.java:89-91).  All levels are
+        registered, or none.  Returns {level: {(z, c, t): plane id}}."""
+        ms, root = ngff_multiscales(image_dir)
+        axes = ms.get("axes")
+        specs, keys = [], []
+        for k, ds in enumerate(ms["datasets"]):
+            adir = os.path.join(root, ds["path"])
+            meta = zarr_array_meta(adir)
+            for z, c, t in (planes if planes is not None else self._array_planes(meta, axes)):
+                specs.append(zarr_plane_spec(adir, image_id, z, c, t, k, meta, axes))
+                keys.append((k, (z, c, t)))
+        ids = self.register_zarr_planes(specs)
+        out: Dict[int, Dict[Tuple[int, int, int], int]] = {}
+        for (k, p), pid in zip(keys, ids):
+            out.setdefault(k, {})[p] = pid
+        return out
 
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))

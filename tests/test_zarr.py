@@ -491,3 +491,73 @@ def test_gpu_cblosc_rejects(service, damage):
         service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 128, 128, 128, 128, "blosc",
                                     [bytes(enc)])
     assert ei.value.status == 400
+
+
+def _write_ngff_image(root, levels, dtype=">u2", axes=("t", "c", "z", "y", "x"), lead=(1, 2, 3),
+                      h=600, w=500, chunk=(128, 96), compressor="blosc", b2r=False):
+    """An NGFF multiscale image: dataset k = 2^k-downsampled planes (numpy box means of the
+    level above, as a writer would produce), .zattrs multiscales with the given axes; with
+    b2r, inside a bioformats2raw container (root/.zattrs layout 3, series 0)."""
+    import pathlib
+    root = pathlib.Path(root)
+    img = root / "0" if b2r else root
+    img.mkdir(parents=True, exist_ok=True)
+    if b2r:
+        (root / ".zattrs").write_text(json.dumps({"bioformats2raw.layout": 3}))
+    datasets, arrays = [], []
+    for k in range(levels):
+        hk, wk = -(-h // 2 ** k), -(-w // 2 ** k)
+        shape = list(lead) + [hk, wk]
+        planes = _write_ngff(img / str(k), shape, [1] * len(lead) + list(chunk), dtype, "/", compressor)
+        arrays.append(planes)
+        datasets.append({"path": str(k), "coordinateTransformations": [{"type": "scale", "scale": [1.0] * len(lead) + [2.0 ** k] * 2}]})
+    ms = {"multiscales": [{"version": "0.4", "name": "img", "axes": [{"name": a} for a in axes],
+                           "datasets": datasets}]}
+    (img / ".zattrs").write_text(json.dumps(ms))
+    return arrays
+
+
+@pytest.mark.parametrize("axes,lead", [(("t", "c", "z", "y", "x"), (1, 2, 3)), (("c", "y", "x"), (2,)),
+                                       (("z", "y", "x"), (3,))])
+def test_ngff_axes_planes(tmp_path, axes, lead):
+    """Plane enumeration and chunk paths follow the multiscales "axes" (CPU)."""
+    import pbx
+    _write_ngff_image(tmp_path / "img", 2, axes=axes, lead=lead, h=70, w=50, chunk=(32, 32))
+    ms, root = pbx.ngff_multiscales(str(tmp_path / "img"))
+    meta = pbx.zarr_array_meta(os.path.join(root, "1"))
+    planes = pbx.PixelsService._array_planes(meta, ms["axes"])
+    n = int(np.prod(lead))
+    assert len(planes) == n
+    for z, c, t in planes:
+        sp = pbx.zarr_plane_spec(os.path.join(root, "1"), 1, z, c, t, 1, meta, ms["axes"])
+        assert sp["level"] == 1 and (sp["size_y"], sp["size_x"]) == (35, 25)
+        assert all(ch is not None for ch in sp["chunks"])
+
+
+@gpu
+@pytest.mark.parametrize("b2r", [False, True], ids=["ngff", "bioformats2raw"])
+def test_gpu_ngff_pyramid_one_call(service, tmp_path, b2r):
+    """A whole 3-level NGFF image (2 channels x 3 z) registers with ONE call; tiles follow
+    OMERO's resolution numbering (resolution 2 = dataset 0 = full resolution, 0 = the
+    smallest), absent resolution = full resolution, w/h defaults to the full-resolution size."""
+    import pbx
+    arrays = _write_ngff_image(tmp_path / "img", 3, b2r=b2r)
+    iid = next(_ids)
+    reg = service.register_ngff_image(str(tmp_path / "img"), iid)
+    assert sorted(reg) == [0, 1, 2] and all(len(v) == 6 for v in reg.values())
+    z, c = 2, 1
+    ctxs = [pbx.TileCtx(iid, z, c, 0, 100, 50, 64, 32),                   # full resolution
+            pbx.TileCtx(iid, z, c, 0, 100, 50, 64, 32, resolution=2),     # = dataset 0
+            pbx.TileCtx(iid, z, c, 0, 10, 20, 64, 32, resolution=1),      # dataset 1
+            pbx.TileCtx(iid, z, c, 0, 3, 4, 100, 60, resolution=0),       # dataset 2 (150 x 125)
+            pbx.TileCtx(iid, z, c, 0, 0, 0, 0, 0, resolution=0),          # w/h 500 x 600 > level
+            pbx.TileCtx(iid, z, c, 0, 0, 0, 16, 16, resolution=3)]        # no 4th level
+    res = service.get_tiles(ctxs)
+    lv = [arrays[k][(0, c, z)] for k in range(3)]
+    assert res[0] == (0, lv[0][50:82, 100:164].tobytes()) == res[1]
+    assert res[2] == (0, lv[1][20:52, 10:74].tobytes())
+    assert res[3] == (0, lv[2][4:64, 3:103].tobytes())
+    assert res[4][0] == pbx.E_NOTFOUND and res[5][0] == pbx.E_NOTFOUND
+    for lvl in reg.values():
+        for pid in lvl.values():
+            service.release_plane(pid)
