@@ -75,6 +75,9 @@ typedef struct pbx_config {
                                 batches (one per GPU-busy interval); 0 = one batch per call */
     int32_t stage_rows;      /* 0 (default) = the deflate kernels read filter-None rows straight
                                 from the plane; 1 = stage them in a stream buffer first (k_rows) */
+    int32_t tiff_tile;       /* 0 (reference) = TIFF as one strip; T = tiled TIFF (TIFF 6.0 s.15)
+                                of T x T tiles, edge tiles zero-padded; T a multiple of 16 in
+                                [16, 4096]; with tiff_deflate every tile is its own zlib stream */
 } pbx_config;
 
 typedef struct pbx_ctx pbx_ctx;

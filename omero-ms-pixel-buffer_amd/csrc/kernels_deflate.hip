@@ -1123,6 +1123,12 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     stamp();
 }
 
+// Container bytes before the zlib stream: TIFF header, PNG chunks up to the IDAT data, or
+// (tiled TIFF) the response header in front of its first sub-tile only.
+__device__ __forceinline__ uint32_t container_zoff(const TileDesc& d) {
+    return (d.flags & TF_TILED) ? d.tiff_hdr : (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+}
+
 // ================================================================= k_seg_map
 // Per tile (one thread): the tile of every segment, so the per-segment kernels find their
 // tile descriptor with one load, and the tile's Huffman blocks.
@@ -1132,11 +1138,13 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= ndt) return;
     const uint32_t f = dt[i].seg_first, n = dt[i].seg_count, hb = dt[i].hblk_first;
+    const uint32_t zoff = container_zoff(dt[i]);
     for (uint32_t k = 0; k < n; k++) {
         seg_tile[f + k] = i;
         const uint32_t j = k / BLK_SEGS, r = k % BLK_SEGS;
         info[f + k].blk = hb + j;
         info[f + k].tile = i;
+        info[f + k].zoff = zoff;
         info[f + k].flags = (r == 0 ? SF_FIRST : 0u) | (r + 1 == BLK_SEGS || k + 1 == n ? SF_LAST : 0u) |
                             ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
         if (r == 0) {
@@ -1148,8 +1156,7 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
 
 // ================================================================ k_seg_sizes
 __device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
-    return (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET + ZLIB_HDR_BYTES + payload + 4
-                               : PNG_IDAT_DATA_OFF + ZLIB_HDR_BYTES + payload + PNG_TAIL_BYTES;
+    return container_zoff(d) + ZLIB_HDR_BYTES + payload + ((d.flags & TF_TIFF) ? 4 : PNG_TAIL_BYTES);
 }
 
 __global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ dt, uint32_t ndt,
@@ -1522,8 +1529,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     if (lane == 0) S.red[w] = c;
     // owned bytes to their final place: unaligned head and tail bytes, aligned words between
     const uint32_t nbytes = o1 - o0;
-    const uint32_t zoff = (gi.flags & SF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
-    uint8_t* dst = out + offs[ti] + zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
+    uint8_t* dst = out + offs[ti] + gi.zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
     const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
@@ -1574,7 +1580,7 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
     const TileDesc d = dt[i];
     uint8_t* base = out + offs[i];
     const bool tiff = (d.flags & TF_TIFF) != 0;
-    const uint32_t zoff = tiff ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+    const uint32_t zoff = container_zoff(d);
     uint32_t s1 = 0, s2 = 0, payload = 0;
     for (uint32_t k = 0; k < d.seg_count; k++) {
         const SegInfo& g = info[d.seg_first + k];
@@ -1639,6 +1645,7 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
         }
         if (pend) flush();
     }
+    if (d.flags & TF_TILED) return;  // header and tile arrays: k_tiff_tiled
     if (tiff) {
         write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8,
                           ZLIB_HDR_BYTES + payload + 4);

@@ -142,13 +142,14 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
     const uint32_t r0 = (b - d.blk_first) * d.rows_per_blk;
     const uint32_t r1 = r0 + d.rows_per_blk < (uint32_t)d.h ? r0 + d.rows_per_blk : (uint32_t)d.h;
     uint8_t* base = out + d.out_off;
-    if (d.flags & TF_TIFF) {
+    if ((d.flags & (TF_TIFF | TF_TILED)) == TF_TIFF) {  // tiled: header by k_tiff_tiled
         if (r0 == 0 && tid == 0)
             write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 1, rb * d.h);
         base += TIFF_DATA_OFFSET;
     }
     const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
-    const bool fast = (((uintptr_t)src0 | (uintptr_t)base | (uintptr_t)d.pitch | rb) & 15u) == 0;
+    // padded edge sub-tiles of a tiled TIFF go byte by byte (zeros outside the region)
+    const bool fast = !d.vw && (((uintptr_t)src0 | (uintptr_t)base | (uintptr_t)d.pitch | rb) & 15u) == 0;
     const bool swap = (d.flags & TF_SWAP) != 0;
     if (fast) {
         const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
     const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
     const uint32_t rbp = ((rb + 15) & ~15u) + 16;
     uint32_t* ftype = (uint32_t*)(sm + FB_LDS - 256);
-    const bool fast = (uint64_t)(FB_ROWS + 1) * rbp + 256 <= (uint64_t)FB_LDS &&
+    const bool fast = !d.vw && (uint64_t)(FB_ROWS + 1) * rbp + 256 <= (uint64_t)FB_LDS &&
                       ((((uintptr_t)src0) | (uintptr_t)d.pitch) & 15) == 0;
     const uint32_t o0 = r0 * rowlen, o1 = r1 * rowlen;
     if (fast) {
@@ -328,7 +329,53 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
     }
 }
 
+// ------------------------------------------------------------- tiled-TIFF headers
+// One workgroup per tiled-TIFF response: header, IFD and the TileOffsets / TileByteCounts
+// arrays (TIFF 6.0 section 15).  Uncompressed sub-tiles all hold t*t*bpp bytes; deflate
+// sub-tiles k are the containers [offs[first+k], offs[first+k+1]) of the deflate arena, the
+// first one preceded by the header.
+__global__ __launch_bounds__(256) void k_tiff_tiled(const TiledHdr* __restrict__ th, uint32_t nth,
+                                                    uint8_t* __restrict__ fixed,
+                                                    const uint64_t* __restrict__ offs,
+                                                    uint8_t* __restrict__ zout) {
+    const TiledHdr j = th[blockIdx.x];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t D = tiff_tiled_data_offset(j.n);
+    const uint64_t sub = (uint64_t)j.t * j.t * j.bpp;
+    uint8_t* p = j.comp == 1 ? fixed + j.off : zout + offs[j.first];
+    auto entry = [&](uint32_t k, uint32_t& off, uint32_t& cnt) {
+        if (j.comp == 1) {
+            off = (uint32_t)(D + k * sub);
+            cnt = (uint32_t)sub;
+        } else {
+            const uint64_t a = offs[j.first + k] - offs[j.first], e = offs[j.first + k + 1] - offs[j.first];
+            off = (uint32_t)(k ? a : D);
+            cnt = (uint32_t)(e - off);
+        }
+    };
+    if (tid == 0) {
+        uint32_t off0, cnt0;
+        entry(0, off0, cnt0);
+        write_tiff_tiled_ifd(p, j.w, j.h, j.t, j.bpp, j.sf, j.comp, j.n, off0, cnt0);
+    }
+    if (j.n > 1) {
+        for (uint32_t k = tid; k < j.n; k += 256) {
+            uint32_t off, cnt;
+            entry(k, off, cnt);
+            tiff_tiled_entry(p, j.n, k, off, cnt);
+        }
+        for (uint64_t i = TIFF_TILED_ARRAYS + 8ull * j.n + tid; i < D; i += 256) p[i] = 0;
+    }
+}
+
 // ------------------------------------------------------------------------ launchers
+hipError_t launch_tiff_tiled(hipStream_t st, const TiledHdr* d_th, uint32_t nth, uint8_t* fixed,
+                             const uint64_t* offs, uint8_t* zout) {
+    if (!nth) return hipSuccess;
+    hipLaunchKernelGGL(k_tiff_tiled, dim3(nth), dim3(256), 0, st, d_th, nth, fixed, offs, zout);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t sy,
                             int32_t pt, int32_t kind, uint64_t seed, int32_t plane_no, int32_t z,
                             int32_t c, int32_t t) {

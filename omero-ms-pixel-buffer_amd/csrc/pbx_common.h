@@ -30,6 +30,7 @@ enum : uint32_t {
     TF_TIFF = 8u,      // container is TIFF (else PNG) for deflate tiles
     TF_DIRECT = 16u,   // filter-None rows, 16-byte aligned source, bpp <= 4: k_lz77
                        // assembles the stream from the plane (no k_rows pass)
+    TF_TILED = 32u,    // one T x T sub-tile of a tiled-TIFF response (header by k_tiff_tiled)
 };
 
 // PNG container layout (APNGWriter: sig, IHDR, acTL, fcTL, IDAT, IEND).
@@ -64,7 +65,10 @@ struct alignas(16) TileDesc {
     uint32_t blk_first;     // first workgroup of this tile (extract / filter bands)
     uint32_t rows_per_blk;  // extract: rows handled by one workgroup
     uint32_t hblk_first;    // deflate tiles: first Huffman block index in the batch
-    uint32_t pad_[3];
+    uint32_t vw, vh;        // tiled-TIFF edge sub-tile: valid w x h inside the padded w x h
+                            // geometry (bytes outside read as 0); 0 = no padding
+    uint32_t tiff_hdr;      // tiled TIFF: header bytes before this sub-tile's data (first
+                            // sub-tile of a response only)
 };
 
 // Per-segment deflate result.
@@ -91,7 +95,7 @@ struct SegInfo {
     uint32_t bitsum;                     // k_encode: token bits (diagnostics)
     uint32_t tile;                       // k_seg_map: the segment's tile
     uint32_t src_lo, src_hi;             // k_lz77: stream-buffer offset of the segment's first byte
-    uint32_t pad_;
+    uint32_t zoff;                       // k_seg_map: container bytes before the zlib stream
 };
 constexpr uint32_t SF_FIRST = 1, SF_LAST = 2, SF_TIFF = 4;
 constexpr uint32_t SP_HEAD = 1u << 16, SP_TAIL = 1u << 17;
@@ -136,6 +140,52 @@ PBX_HD void write_tiff_header(uint8_t* p, uint32_t w, uint32_t h, uint32_t bpp, 
     }
     // next-IFD offset (0) is already zero
 }
+
+// Tiled TIFF (TIFF 6.0 section 15): header + 12-entry IFD at 8 (ends at 158); with n > 1
+// sub-tiles the TileOffsets array at 160 and TileByteCounts at 160 + 4n; sub-tile data from
+// the 16-byte aligned offset tiff_tiled_data_offset(n), row-major over the region, every
+// sub-tile T x T samples (edge sub-tiles zero-padded), raw or one zlib stream each.
+constexpr uint32_t TIFF_TILED_NTAGS = 12;
+constexpr uint32_t TIFF_TILED_ARRAYS = 160;
+
+PBX_HD uint64_t tiff_tiled_data_offset(uint64_t n) {
+    return n > 1 ? (TIFF_TILED_ARRAYS + 8 * n + 15) & ~15ull : TIFF_TILED_ARRAYS;
+}
+
+// Header and IFD (bytes [0, 160)); for n == 1 the one offset / byte count sit in the entries,
+// else the caller writes tiff_tiled_entry(k) for every sub-tile.
+PBX_HD void write_tiff_tiled_ifd(uint8_t* p, uint32_t w, uint32_t h, uint32_t t, uint32_t bpp,
+                                 uint32_t sf, uint32_t compression, uint32_t n, uint32_t off0,
+                                 uint32_t cnt0) {
+    for (uint32_t i = 0; i < TIFF_TILED_ARRAYS; i++) p[i] = 0;
+    p[0] = 'M'; p[1] = 'M'; put_be16(p + 2, 42); put_be32(p + 4, 8);
+    put_be16(p + 8, TIFF_TILED_NTAGS);
+    const uint16_t tag[TIFF_TILED_NTAGS] = {256, 257, 258, 259, 262, 277, 284, 322, 323, 324, 325, 339};
+    const uint16_t typ[TIFF_TILED_NTAGS] = {4, 4, 3, 3, 3, 3, 3, 4, 4, 4, 4, 3};
+    const uint32_t val[TIFF_TILED_NTAGS] = {w, h, 8 * bpp, compression, 1, 1, 1, t, t,
+                                            n > 1 ? TIFF_TILED_ARRAYS : off0,
+                                            n > 1 ? TIFF_TILED_ARRAYS + 4 * n : cnt0, sf};
+    for (uint32_t k = 0; k < TIFF_TILED_NTAGS; k++) {
+        uint8_t* e = p + 10 + 12 * k;
+        put_be16(e, tag[k]); put_be16(e + 2, typ[k]);
+        put_be32(e + 4, (tag[k] == 324 || tag[k] == 325) ? n : 1u);
+        if (typ[k] == 3) { put_be16(e + 8, val[k]); } else { put_be32(e + 8, val[k]); }
+    }
+}
+
+// Sub-tile k's TileOffsets / TileByteCounts entries (n > 1).
+PBX_HD void tiff_tiled_entry(uint8_t* p, uint32_t n, uint32_t k, uint32_t off, uint32_t cnt) {
+    put_be32(p + TIFF_TILED_ARRAYS + 4 * k, off);
+    put_be32(p + TIFF_TILED_ARRAYS + 4 * n + 4 * k, cnt);
+}
+
+// A tiled-TIFF response's header job (k_tiff_tiled).  comp 1: the response starts at `off`
+// in the fixed arena and every sub-tile is t*t*bpp bytes; comp 8: its sub-tiles are deflate
+// tiles first..first+n-1 and the response starts at their first container.
+struct alignas(16) TiledHdr {
+    uint64_t off;
+    uint32_t first, n, w, h, t, bpp, sf, comp;
+};
 
 // ----------------------------------------------------------------------------- CRC-32 math
 // Standard reflected CRC-32 (poly 0xEDB88320) with zlib's crc32_combine formulation:
@@ -274,14 +324,19 @@ struct TileStream {
     uint32_t rowlen, flags;
     int32_t filter;
     const uint8_t* rowfilt;
+    uint32_t vrb, vh;  // valid row bytes / rows (tiled-TIFF edge sub-tiles; else unbounded)
 
     PBX_HD void init(const TileDesc& d, const uint8_t* rowfilt_base) {
         plane = d.plane; pitch = d.pitch; x = d.x; y = d.y; bpp = d.bpp; lbpp = d.lbpp;
         rowlen = d.rowlen; flags = d.flags; filter = d.filter;
         rowfilt = rowfilt_base ? rowfilt_base + d.rowfilt_off : nullptr;
+        vrb = d.vw ? d.vw * (uint32_t)d.bpp : 0xFFFFFFFFu;
+        vh = d.vw ? d.vh : 0xFFFFFFFFu;
     }
-    // Big-endian byte i of tile row r, after the APNGWriter sign flip.
+    // Big-endian byte i of tile row r, after the APNGWriter sign flip; 0 in the padding of
+    // a tiled-TIFF edge sub-tile.
     PBX_HD uint32_t be(int64_t r, uint32_t i) const {
+        if ((uint64_t)r >= vh || i >= vrb) return 0u;
         uint32_t s = i >> lbpp, b = i & (uint32_t)(bpp - 1);
         uint32_t sb = (flags & TF_SWAP) ? (uint32_t)(bpp - 1) - b : b;
         uint32_t v = plane[(int64_t)(y + r) * pitch + ((int64_t)x + s) * bpp + sb];

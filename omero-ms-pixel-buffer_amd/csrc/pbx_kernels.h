@@ -21,6 +21,10 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
                              bool be);
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                           uint32_t nblocks, uint8_t* out);
+// Tiled-TIFF headers (IFD + TileOffsets/TileByteCounts), one workgroup per response: after
+// k_extract for uncompressed responses (in `fixed`), after k_frame for deflate ones (`zout`).
+hipError_t launch_tiff_tiled(hipStream_t st, const TiledHdr* d_th, uint32_t nth, uint8_t* fixed,
+                             const uint64_t* offs, uint8_t* zout);
 
 // K1+K2: extract + byte swap + sign flip + PNG filter (or raw BE bytes for deflate-TIFF)
 // into the per-tile byte streams the deflate kernels read.  One workgroup per band.

@@ -180,6 +180,8 @@ struct pbx_batch {
     std::vector<int32_t> status, w, h;
     std::vector<TileDesc> ft, dt;          // fixed-size (raw / TIFF) and deflate tiles
     std::vector<uint32_t> ft_req, dt_req;  // request index of each
+    std::vector<TiledHdr> th;              // tiled-TIFF responses (their sub-tiles carry TF_TILED)
+    std::vector<uint32_t> th_req;
     uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
     // dt = [direct tiles | k_rows tiles | k_filter tiles]
     uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
@@ -189,7 +191,7 @@ struct pbx_batch {
     void *d_ft = nullptr, *d_dt = nullptr, *d_fixed = nullptr, *d_stream = nullptr,
          *d_info = nullptr, *d_hist = nullptr, *d_mrec = nullptr, *d_codes = nullptr,
          *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr,
-         *d_segmap = nullptr, *d_blk = nullptr;
+         *d_segmap = nullptr, *d_blk = nullptr, *d_th = nullptr;
     void* h_desc = nullptr;  // pinned staging for descriptors
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
@@ -300,7 +302,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
     void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
                      &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps,
-                     &b->d_segmap, &b->d_blk};
+                     &b->d_segmap, &b->d_blk, &b->d_th};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -552,6 +554,8 @@ int pbx_config_default(pbx_config* cfg) {
     if (f) cfg->png_filter = atoi(f);
     const char* td = getenv("PBX_TIFF_DEFLATE");
     if (td) cfg->tiff_deflate = atoi(td);
+    const char* tt = getenv("PBX_TIFF_TILE");
+    if (tt) cfg->tiff_tile = atoi(tt);
     return PBX_OK;
 }
 
@@ -560,6 +564,10 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     *out = nullptr;
     pbx_config cfg;
     if (cfg_in) cfg = *cfg_in; else pbx_config_default(&cfg);
+    if (cfg.png_filter < PBX_FILTER_NONE || cfg.png_filter > PBX_FILTER_ADAPTIVE)
+        return fail(PBX_E_BADARG, "bad png_filter %d", cfg.png_filter);
+    if (cfg.tiff_tile && (cfg.tiff_tile < 16 || cfg.tiff_tile > 4096 || cfg.tiff_tile % 16))
+        return fail(PBX_E_BADARG, "bad tiff_tile %d (0, or a multiple of 16 in [16, 4096])", cfg.tiff_tile);
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
         return fail(PBX_E_INTERNAL, "no HIP device available (the tile pipeline runs on MI355X only)");
@@ -570,8 +578,6 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
         dev = e ? atoi(e) : lr ? atoi(lr) : 0;
     }
     if (dev < 0 || dev >= n) return fail(PBX_E_BADARG, "device %d out of range (%d devices)", dev, n);
-    if (cfg.png_filter < PBX_FILTER_NONE || cfg.png_filter > PBX_FILTER_ADAPTIVE)
-        return fail(PBX_E_BADARG, "bad png_filter %d", cfg.png_filter);
     pbx_ctx* ctx = new pbx_ctx();
     ctx->device = dev;
     ctx->cfg = cfg;
@@ -1136,8 +1142,11 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->h.resize(n);
     const int filter = ctx->cfg.png_filter;
     const bool tiff_deflate = ctx->cfg.tiff_deflate != 0;
-    std::vector<TileDesc> dt_direct, dt_rows, dt_band;
-    std::vector<uint32_t> req_direct, req_rows, req_band;
+    const int32_t tiff_tile = ctx->cfg.tiff_tile;
+    // deflate sub-tiles of a tiled TIFF stay consecutive (one response = one run of the
+    // deflate arena): they go to k_filter, after the other banded tiles
+    std::vector<TileDesc> dt_direct, dt_rows, dt_band, dt_tiled;
+    std::vector<uint32_t> req_direct, req_rows, req_band, req_tiled;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane pl;
@@ -1159,6 +1168,61 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         const uint64_t tile_bytes = (uint64_t)w * h * bpp;
         b->in_bytes += tile_bytes;
         const bool deflate = r.format == PBX_FMT_PNG || (r.format == PBX_FMT_TIF && tiff_deflate);
+        if (r.format == PBX_FMT_TIF && tiff_tile) {
+            // Tiled TIFF: the region as ntx x nty sub-tiles of T x T samples (edge ones
+            // zero-padded), each raw or its own zlib stream, behind one header
+            const uint32_t T = (uint32_t)tiff_tile;
+            const uint32_t ntx = ((uint32_t)w + T - 1) / T, nty = ((uint32_t)h + T - 1) / T;
+            const uint64_t nsub = (uint64_t)ntx * nty, sub = (uint64_t)T * T * bpp;
+            const uint64_t D = tiff_tiled_data_offset(nsub);
+            if (D + nsub * sub > 0xFFFFFFFFull) {  // classic TIFF: 32-bit offsets
+                b->status[i] = fail(PBX_E_BADARG, "tiled TIFF response over 4 GiB");
+                b->in_bytes -= tile_bytes;
+                continue;
+            }
+            TiledHdr th;
+            memset(&th, 0, sizeof th);
+            th.n = (uint32_t)nsub;
+            th.w = (uint32_t)w; th.h = (uint32_t)h; th.t = T; th.bpp = (uint32_t)bpp;
+            th.sf = tiff_sample_format(pl.pixel_type);
+            th.comp = deflate ? 8u : 1u;
+            if (!deflate) {
+                th.off = b->fixed_bytes;
+                b->fixed_bytes += (D + nsub * sub + 255) & ~255ull;
+            } else {
+                th.first = (uint32_t)dt_tiled.size();  // rebased below
+            }
+            d.flags |= TF_TIFF | TF_TILED;
+            for (uint32_t ty = 0; ty < nty; ty++)
+                for (uint32_t tx = 0; tx < ntx; tx++) {
+                    TileDesc s = d;
+                    const uint32_t k = ty * ntx + tx;
+                    s.x = r.x + (int32_t)(tx * T);
+                    s.y = r.y + (int32_t)(ty * T);
+                    s.w = s.h = (int32_t)T;
+                    const uint32_t vw = std::min<uint32_t>(T, (uint32_t)w - tx * T);
+                    const uint32_t vh = std::min<uint32_t>(T, (uint32_t)h - ty * T);
+                    if (vw < T || vh < T) { s.vw = vw; s.vh = vh; }
+                    s.tiff_hdr = k == 0 ? (uint32_t)D : 0u;
+                    if (!deflate) {
+                        s.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(16384 / (T * bpp)));
+                        s.blk_first = b->ext_blocks;
+                        b->ext_blocks += (T + s.rows_per_blk - 1) / s.rows_per_blk;
+                        s.out_off = th.off + D + k * sub;
+                        b->ft.push_back(s);
+                        b->ft_req.push_back((uint32_t)i);
+                    } else {
+                        s.filter = 0;
+                        s.rowlen = T * (uint32_t)bpp;
+                        s.stream_len = (uint64_t)T * s.rowlen;
+                        dt_tiled.push_back(s);
+                        req_tiled.push_back((uint32_t)i);
+                    }
+                }
+            b->th.push_back(th);
+            b->th_req.push_back((uint32_t)i);
+            continue;
+        }
         if (!deflate) {
             if (r.format == PBX_FMT_TIF) d.flags |= TF_TIFF;
             const uint32_t rb = (uint32_t)w * bpp;
@@ -1204,9 +1268,14 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->dt = std::move(dt_direct);
     b->dt.insert(b->dt.end(), dt_rows.begin(), dt_rows.end());
     b->dt.insert(b->dt.end(), dt_band.begin(), dt_band.end());
+    b->dt.insert(b->dt.end(), dt_tiled.begin(), dt_tiled.end());
     b->dt_req = std::move(req_direct);
     b->dt_req.insert(b->dt_req.end(), req_rows.begin(), req_rows.end());
     b->dt_req.insert(b->dt_req.end(), req_band.begin(), req_band.end());
+    b->dt_req.insert(b->dt_req.end(), req_tiled.begin(), req_tiled.end());
+    const uint32_t tiled0 = (uint32_t)(b->dt.size() - dt_tiled.size());
+    for (TiledHdr& th : b->th)
+        if (th.comp == 8) th.first += tiled0;
     for (size_t k = 0; k < b->dt.size(); k++) {
         TileDesc& d = b->dt[k];
         deflate_split(d.stream_len, d.seg_count, d.seg_len);
@@ -1215,7 +1284,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         d.hblk_first = b->nblk;
         b->nblk += tile_blocks(d.seg_count);
         b->stream_bytes += d.stream_len;
-        b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + 128 + d.stream_len + 16ull * d.seg_count + 255) & ~255ull;
+        b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + d.tiff_hdr + 128 + d.stream_len + 16ull * d.seg_count + 255) &
+                      ~255ull;
         d.out_off = b->stream_cap;  // the tile's filtered stream in the stream buffer
         b->stream_cap += (d.stream_len + 256 + 255) & ~255ull;
         if (k < b->ndirect_tiles) continue;  // k_lz77 assembles it from the plane
@@ -1241,13 +1311,15 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
         p = ctx->dpool.get(std::max<size_t>(n, 256), &err);
         return p != nullptr;
     };
-    const uint32_t nft = (uint32_t)b->ft.size(), ndt = (uint32_t)b->dt.size();
-    const size_t ft_bytes = nft * sizeof(TileDesc), dt_bytes = ndt * sizeof(TileDesc);
+    const uint32_t nft = (uint32_t)b->ft.size(), ndt = (uint32_t)b->dt.size(), nth = (uint32_t)b->th.size();
+    const size_t ft_bytes = nft * sizeof(TileDesc), dt_bytes = ndt * sizeof(TileDesc),
+                 th_bytes = nth * sizeof(TiledHdr);
     if (!b->h_desc) {
-        b->h_desc = ctx->hpool.get(ft_bytes + dt_bytes + 256, &err);
+        b->h_desc = ctx->hpool.get(ft_bytes + dt_bytes + th_bytes + 256, &err);
         if (!b->h_desc) return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
         if (nft) memcpy(b->h_desc, b->ft.data(), ft_bytes);
         if (ndt) memcpy((uint8_t*)b->h_desc + ft_bytes, b->dt.data(), dt_bytes);
+        if (nth) memcpy((uint8_t*)b->h_desc + ft_bytes + dt_bytes, b->th.data(), th_bytes);
     }
     const size_t ns = b->nseg;
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
@@ -1256,7 +1328,7 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
         !dget(b->d_codes, (size_t)b->nblk * CODE_WORDS * 4) || !dget(b->d_blk, b->nblk * sizeof(BlkInfo)) ||
         !dget(b->d_sizes, (ndt + 1) * sizeof(uint64_t)) ||
         !dget(b->d_offs, (ndt + 1) * sizeof(uint64_t)) || !dget(b->d_png, b->png_cap) ||
-        !dget(b->d_segmap, ns * sizeof(uint32_t)))
+        !dget(b->d_segmap, ns * sizeof(uint32_t)) || !dget(b->d_th, th_bytes))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     if (!b->ev[0])
         for (auto& e : b->ev) HIP_TRY(hipEventCreate(&e));
@@ -1265,6 +1337,9 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
     if (ndt)
         HIP_TRY(hipMemcpyAsync(b->d_dt, (uint8_t*)b->h_desc + ft_bytes, dt_bytes, hipMemcpyHostToDevice, st));
+    if (nth)
+        HIP_TRY(hipMemcpyAsync(b->d_th, (uint8_t*)b->h_desc + ft_bytes + dt_bytes, th_bytes,
+                               hipMemcpyHostToDevice, st));
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
@@ -1300,6 +1375,8 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     } else {
         for (int k = 4; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
     }
+    HIP_TRY(launch_tiff_tiled(st, (const TiledHdr*)b->d_th, nth, (uint8_t*)b->d_fixed, (const uint64_t*)b->d_offs,
+                              (uint8_t*)b->d_png));
     HIP_TRY(hipEventRecord(b->ev[8], st));
     b->launched = true;
     return PBX_OK;
@@ -1368,7 +1445,8 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
         s->out_bytes = s->deflate_out_bytes;
         for (size_t k = 0; k < b->ft.size(); k++)
             s->out_bytes += (uint64_t)b->ft[k].w * b->ft[k].h * b->ft[k].bpp +
-                            ((b->ft[k].flags & TF_TIFF) ? TIFF_DATA_OFFSET : 0);
+                            ((b->ft[k].flags & TF_TILED) ? b->ft[k].tiff_hdr
+                             : (b->ft[k].flags & TF_TIFF) ? TIFF_DATA_OFFSET : 0);
     }
     return PBX_OK;
 }
@@ -1417,6 +1495,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     int refs = 0;
     for (size_t k = 0; k < b->ft.size(); k++) {
         const TileDesc& d = b->ft[k];
+        if (d.flags & TF_TILED) continue;
         pbx_result& r = out[b->ft_req[k]];
         r.data = h + d.out_off;
         r.len = (uint64_t)d.w * d.h * d.bpp + ((d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : 0);
@@ -1424,9 +1503,23 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
         refs++;
     }
     for (uint32_t k = 0; k < ndt; k++) {
+        if (b->dt[k].flags & TF_TILED) continue;
         pbx_result& r = out[b->dt_req[k]];
         r.data = h + b->fixed_bytes + b->h_offs[k];
         r.len = b->h_offs[k + 1] - b->h_offs[k];
+        r.owner = hb;
+        refs++;
+    }
+    for (size_t k = 0; k < b->th.size(); k++) {  // tiled TIFF: header + all sub-tiles
+        const TiledHdr& t = b->th[k];
+        pbx_result& r = out[b->th_req[k]];
+        if (t.comp == 1) {
+            r.data = h + t.off;
+            r.len = tiff_tiled_data_offset(t.n) + (uint64_t)t.n * t.t * t.t * t.bpp;
+        } else {
+            r.data = h + b->fixed_bytes + b->h_offs[t.first];
+            r.len = b->h_offs[t.first + t.n] - b->h_offs[t.first];
+        }
         r.owner = hb;
         refs++;
     }

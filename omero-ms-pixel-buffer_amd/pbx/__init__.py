@@ -46,7 +46,7 @@ class PbxConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("png_filter", ctypes.c_int32),
                 ("tiff_deflate", ctypes.c_int32), ("segment_bytes", ctypes.c_int32),
                 ("max_batch_bytes", ctypes.c_uint64), ("coalesce", ctypes.c_int32),
-                ("stage_rows", ctypes.c_int32)]
+                ("stage_rows", ctypes.c_int32), ("tiff_tile", ctypes.c_int32)]
 
 
 class PbxPlaneDesc(ctypes.Structure):
@@ -393,7 +393,8 @@ class PixelsService:
     """
 
     def __init__(self, device: Optional[int] = None, png_filter: int = FILTER_NONE,
-                 tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False):
+                 tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False,
+                 tiff_tile: Optional[int] = None):
         L = lib()
         cfg = PbxConfig()
         _check(L.pbx_config_default(ctypes.byref(cfg)))
@@ -402,6 +403,8 @@ class PixelsService:
         cfg.tiff_deflate = 1 if tiff_deflate else 0
         cfg.coalesce = 1 if coalesce else 0
         cfg.stage_rows = 1 if stage_rows else 0
+        if tiff_tile is not None:  # else $PBX_TIFF_TILE or 0 (one strip, the reference's)
+            cfg.tiff_tile = int(tiff_tile)
         h = ctypes.c_void_p()
         _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

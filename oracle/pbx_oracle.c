@@ -468,6 +468,110 @@ static uint32_t tiff_value(const uint8_t* tif, size_t len, const uint8_t* e, int
     return tget(base + (size_t)idx * sz, be, sz);
 }
 
+/* Tiled TIFF (TIFF 6.0 section 15: TileWidth 322, TileLength 323, TileOffsets 324,
+ * TileByteCounts 325): tiles row-major over the image, each tw x tl samples (edge tiles
+ * padded), raw or one zlib stream; only the part inside the image is kept. */
+static int tiff_decode_tiles(const uint8_t* tif, size_t len, int be, uint8_t* out, size_t cap,
+                             int32_t w, int32_t h, int32_t bits, int32_t comp, uint32_t spp,
+                             uint32_t planar, uint32_t tw, uint32_t tl, uint32_t ntiles,
+                             const uint8_t* toffs, const uint8_t* tcnts) {
+    if (!toffs || !tcnts || !tw || !tl || spp != 1 || planar != 1 || bits % 8 || w <= 0 || h <= 0)
+        return -4;
+    if (tw % 16 || tl % 16) return -11;  /* TIFF 6.0: tile sizes are multiples of 16 */
+    const size_t bpp = (size_t)bits / 8, rb = (size_t)w * bpp, trb = (size_t)tw * bpp;
+    const uint32_t ntx = ((uint32_t)w + tw - 1) / tw, nty = ((uint32_t)h + tl - 1) / tl;
+    if (ntiles != ntx * nty || tget(tcnts + 4, be, 4) != ntiles) return -12;
+    if (cap < rb * (size_t)h) return -5;
+    const size_t tbytes = trb * tl;
+    uint8_t* tile = (uint8_t*)malloc(tbytes + 1);
+    if (!tile) return -13;
+    for (uint32_t k = 0; k < ntiles; k++) {
+        uint32_t off = tiff_value(tif, len, toffs, be, k), cnt = tiff_value(tif, len, tcnts, be, k);
+        if ((size_t)off + cnt > len) { free(tile); return -6; }
+        if (comp == 1) {
+            if (cnt < tbytes) { free(tile); return -7; }
+            memcpy(tile, tif + off, tbytes);
+        } else if (comp == 8 || comp == 32946) {
+            size_t got = 0;
+            if (pbxo_zlib_inflate(tif + off, cnt, tile, tbytes + 1, &got) || got != tbytes) {
+                free(tile);
+                return -8;
+            }
+        } else {
+            free(tile);
+            return -9;
+        }
+        const uint32_t tx = k % ntx, ty = k / ntx;
+        const size_t x0 = (size_t)tx * tw, y0 = (size_t)ty * tl;
+        const size_t vw = (size_t)w - x0 < tw ? (size_t)w - x0 : tw;
+        const size_t vh = (size_t)h - y0 < tl ? (size_t)h - y0 : tl;
+        for (size_t r = 0; r < vh; r++) memcpy(out + (y0 + r) * rb + x0 * bpp, tile + r * trb, vw * bpp);
+    }
+    free(tile);
+    return 0;
+}
+
+static void wbe16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static void wbe32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+/* Tiled-TIFF writer: the layout DESIGN.md §3 specifies for tiled responses ("MM", 12-entry
+ * IFD at 8, TileOffsets at 160 and TileByteCounts at 160 + 4n when n > 1, tile data from the
+ * 16-byte aligned end of the arrays), tiles zero-padded to t x t, raw (comp 1) or each a
+ * zlib stream at level 6 (comp 8).  Returns 0, -1 on bad arguments, -2 if cap is short. */
+int pbxo_tiff_tiled_write(const uint8_t* tile_be, int32_t w, int32_t h, int32_t bpp, int32_t sf,
+                          int32_t t, int32_t comp, uint8_t* out, size_t cap, size_t* out_len) {
+    if (w <= 0 || h <= 0 || t <= 0 || t % 16 || (comp != 1 && comp != 8) || bpp <= 0) return -1;
+    const uint32_t ntx = ((uint32_t)w + t - 1) / t, nty = ((uint32_t)h + t - 1) / t, n = ntx * nty;
+    const size_t D = n > 1 ? (160 + 8 * (size_t)n + 15) & ~(size_t)15 : 160;
+    const size_t rb = (size_t)w * bpp, trb = (size_t)t * bpp, tbytes = trb * t;
+    if (cap < D) return -2;
+    memset(out, 0, D);
+    uint8_t* tile = (uint8_t*)malloc(tbytes);
+    if (!tile) return -1;
+    size_t pos = D;
+    uint32_t off0 = 0, cnt0 = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const size_t x0 = (size_t)(k % ntx) * t, y0 = (size_t)(k / ntx) * t;
+        const size_t vw = (size_t)w - x0 < (size_t)t ? (size_t)w - x0 : (size_t)t;
+        const size_t vh = (size_t)h - y0 < (size_t)t ? (size_t)h - y0 : (size_t)t;
+        memset(tile, 0, tbytes);
+        for (size_t r = 0; r < vh; r++) memcpy(tile + r * trb, tile_be + (y0 + r) * rb + x0 * bpp, vw * bpp);
+        size_t cnt;
+        if (comp == 1) {
+            if (pos + tbytes > cap) { free(tile); return -2; }
+            memcpy(out + pos, tile, tbytes);
+            cnt = tbytes;
+        } else {
+            uLongf dl = (uLongf)(cap - pos);
+            if (compress2(out + pos, &dl, tile, (uLong)tbytes, 6) != Z_OK) { free(tile); return -2; }
+            cnt = dl;
+        }
+        if (n > 1) {
+            wbe32(out + 160 + 4 * (size_t)k, (uint32_t)pos);
+            wbe32(out + 160 + 4 * (size_t)n + 4 * (size_t)k, (uint32_t)cnt);
+        } else {
+            off0 = (uint32_t)pos; cnt0 = (uint32_t)cnt;
+        }
+        pos += cnt;
+    }
+    free(tile);
+    out[0] = 'M'; out[1] = 'M'; wbe16(out + 2, 42); wbe32(out + 4, 8); wbe16(out + 8, 12);
+    const uint16_t tag[12] = {256, 257, 258, 259, 262, 277, 284, 322, 323, 324, 325, 339};
+    const uint16_t typ[12] = {4, 4, 3, 3, 3, 3, 3, 4, 4, 4, 4, 3};
+    const uint32_t val[12] = {(uint32_t)w, (uint32_t)h, 8u * bpp, (uint32_t)comp, 1, 1, 1, (uint32_t)t,
+                              (uint32_t)t, n > 1 ? 160u : off0, n > 1 ? 160u + 4 * n : cnt0, (uint32_t)sf};
+    for (int k = 0; k < 12; k++) {
+        uint8_t* e = out + 10 + 12 * k;
+        wbe16(e, tag[k]); wbe16(e + 2, typ[k]);
+        wbe32(e + 4, (tag[k] == 324 || tag[k] == 325) ? n : 1u);
+        if (typ[k] == 3) wbe16(e + 8, val[k]); else wbe32(e + 8, val[k]);
+    }
+    *out_len = pos;
+    return 0;
+}
+
 int pbxo_tiff_decode(const uint8_t* tif, size_t len, uint8_t* out, size_t cap, int32_t* w,
                      int32_t* h, int32_t* bits, int32_t* sf, int32_t* comp, int32_t* big_endian) {
     if (len < 8) return -1;
@@ -480,8 +584,8 @@ int pbxo_tiff_decode(const uint8_t* tif, size_t len, uint8_t* out, size_t cap, i
     if ((size_t)ifd + 2 > len) return -3;
     uint32_t nt = tget(tif + ifd, be, 2);
     if ((size_t)ifd + 2 + nt * 12 + 4 > len) return -3;
-    uint32_t rps = 0, nstrips = 0, spp = 1, planar = 1;
-    const uint8_t *offs = NULL, *cnts = NULL;
+    uint32_t rps = 0, nstrips = 0, spp = 1, planar = 1, tw = 0, tl = 0, ntiles = 0;
+    const uint8_t *offs = NULL, *cnts = NULL, *toffs = NULL, *tcnts = NULL;
     *w = *h = 0; *bits = 0; *sf = 1; *comp = 1; *big_endian = be;
     for (uint32_t i = 0; i < nt; i++) {
         const uint8_t* e = tif + ifd + 2 + 12 * i;
@@ -496,10 +600,17 @@ int pbxo_tiff_decode(const uint8_t* tif, size_t len, uint8_t* out, size_t cap, i
         case 278: rps = tiff_value(tif, len, e, be, 0); break;
         case 279: cnts = e; break;
         case 284: planar = tiff_value(tif, len, e, be, 0); break;
+        case 322: tw = tiff_value(tif, len, e, be, 0); break;
+        case 323: tl = tiff_value(tif, len, e, be, 0); break;
+        case 324: toffs = e; ntiles = tget(e + 4, be, 4); break;
+        case 325: tcnts = e; break;
         case 339: *sf = (int32_t)tiff_value(tif, len, e, be, 0); break;
         default: break;
         }
     }
+    if (toffs || tw || tl)
+        return tiff_decode_tiles(tif, len, be, out, cap, *w, *h, *bits, *comp, spp, planar, tw, tl,
+                                 ntiles, toffs, tcnts);
     if (!offs || !cnts || spp != 1 || planar != 1 || *bits % 8) return -4;
     if (rps == 0) rps = (uint32_t)*h;
     size_t rb = (size_t)(*w) * (*bits / 8), total = rb * (size_t)(*h), o = 0;

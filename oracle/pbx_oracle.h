@@ -67,6 +67,11 @@ int pbxo_tiff_encode(const uint8_t* tile_be, int pixel_type, int32_t w, int32_t 
                      uint8_t* out, size_t cap, size_t* len);
 size_t pbxo_png_max_size(int pixel_type, int32_t w, int32_t h);
 size_t pbxo_tiff_size(int pixel_type, int32_t w, int32_t h);
+/* Tiled TIFF of t x t tiles (t a multiple of 16; edge tiles zero-padded), compression 1
+ * or 8 (zlib level 6 per tile), in the layout the tiled-TIFF option of the pipeline writes
+ * (not part of the reference: its TiffWriter writes one strip). */
+int pbxo_tiff_tiled_write(const uint8_t* tile_be, int32_t w, int32_t h, int32_t bpp, int32_t sf,
+                          int32_t t, int32_t comp, uint8_t* out, size_t cap, size_t* len);
 
 /* TileRequestHandler.getTile (TileRequestHandler.java:80-139) over one registered plane.
  * The plane is the whole (z,c,t) plane of an image of size_x x size_y.  Region w/h == 0
@@ -85,8 +90,9 @@ int pbxo_png_decode(const uint8_t* png, size_t len, uint8_t* out, size_t cap,
 /* Inflate the concatenated IDAT payload: the filtered stream.  Returns 0 on success. */
 int pbxo_png_inflate_idat(const uint8_t* png, size_t len, uint8_t* out, size_t cap,
                           size_t* out_len);
-/* Baseline TIFF ("MM" or "II"), compression 1 or 8 (zlib), any strip layout.  Writes
- * samples in the file's byte order.  Returns 0 on success. */
+/* Baseline TIFF ("MM" or "II"), compression 1 or 8 (zlib), any strip layout or tiled
+ * (TileWidth/TileLength/TileOffsets/TileByteCounts).  Writes samples in the file's byte
+ * order.  Returns 0 on success. */
 int pbxo_tiff_decode(const uint8_t* tif, size_t len, uint8_t* out, size_t cap,
                      int32_t* w, int32_t* h, int32_t* bits, int32_t* sample_format,
                      int32_t* compression, int32_t* big_endian);

@@ -62,6 +62,9 @@ def lib():
         L.pbxo_tiff_decode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, i32p, i32p,
                                        i32p, i32p, i32p, i32p]
         L.pbxo_zlib_inflate.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, szp]
+        L.pbxo_tiff_tiled_write.argtypes = [u8p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, u8p,
+                                            ctypes.c_size_t, szp]
         L.pbxo_crc32.restype = ctypes.c_uint32
         L.pbxo_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
         L.pbxo_adler32.restype = ctypes.c_uint32
@@ -172,6 +175,19 @@ def tiff_decode(buf, cap):
         return r, None, meta
     n = meta["w"] * meta["h"] * meta["bits"] // 8
     return 0, bytes(out[:n]), meta
+
+
+def tiff_tiled_write(tile_be, w, h, bpp, sf, t, comp):
+    """Tiled TIFF of the big-endian tile bytes (the pipeline's tiled-TIFF layout)."""
+    a = np.ascontiguousarray(np.frombuffer(bytes(tile_be), np.uint8))
+    ntx, nty = -(-w // t), -(-h // t)
+    cap = 256 + 8 * ntx * nty + 2 * ntx * nty * (t * t * bpp + 64)
+    out = np.zeros(cap, np.uint8)
+    n = ctypes.c_size_t()
+    r = lib().pbxo_tiff_tiled_write(_p(a), w, h, bpp, sf, t, comp, _p(out), cap, ctypes.byref(n))
+    if r != 0:
+        raise ValueError(f"pbxo_tiff_tiled_write: {r}")
+    return bytes(out[: n.value])
 
 
 def zlib_inflate(buf, cap):
