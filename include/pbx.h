@@ -129,8 +129,8 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t plane_id, int32_t levels, uin
  * getTileDirect.  Here the chunks of one (z, c, t, resolution) plane are uploaded once and
  * decoded on the GPU (one wave per compressed stream) straight into a resident HBM plane,
  * which then serves tiles like any registered plane.  Codec = the .zarray "compressor":
- * null, blosc (c-blosc 1.x frames: lz4 / lz4hc / zlib, byte shuffle or none, split or not),
- * zlib.  Other blosc codecs (blosclz, zstd, snappy, bit shuffle) and blosc2 frames -> 400. */
+ * null, blosc (c-blosc 1.x frames: blosclz / lz4 / lz4hc / zlib / zstd, byte shuffle, bit
+ * shuffle or none, split or not), zlib.  snappy and blosc2 frames -> 400. */
 enum pbx_zarr_codec { PBX_ZARR_RAW = 0, PBX_ZARR_BLOSC = 1, PBX_ZARR_ZLIB = 2 };
 
 typedef struct pbx_zarr_chunks {

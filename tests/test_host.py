@@ -33,6 +33,20 @@ def test_abi_struct_sizes_match_bindings():
                                                       pbx.PbxBatchStats)]
 
 
+def test_jni_shim_matches_abi():
+    """jni/: every native method of PbxNative.java has its JNI function in pbx_jni.c, and
+    every pbx_* call there is a symbol libpbx.so exports (no JDK here to compile it)."""
+    java = open(os.path.join(ROOT, "jni", "PbxNative.java")).read()
+    c = open(os.path.join(ROOT, "jni", "pbx_jni.c")).read()
+    natives = set(re.findall(r"static native \S+ (\w+)\(", java))
+    assert natives >= {"init", "shutdown", "registerPlane", "registerZarr", "getTile"}
+    defined = set(re.findall(r"Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_(\w+)\(", c))
+    assert natives == defined
+    body = re.sub(r"/\*.*?\*/", "", c, flags=re.S)
+    called = set(re.findall(r"\b(pbx_[a-z_0-9]+)\s*\(", body))
+    assert called and called <= set(header_functions())
+
+
 def test_enums_and_names():
     L = pbx.lib()
     assert L.pbx_abi_version() == 4
