@@ -716,6 +716,24 @@ PBX_HD uint32_t block_nbytes(uint32_t btype, uint64_t bits, uint32_t sl, uint32_
     return last ? (uint32_t)((bits + 7) / 8) : (uint32_t)((bits + 3 + 7) / 8 + 4);
 }
 
+// Whether every segment's share of a Huffman-coded block (its bits [bit0, bit1): the header
+// for the first, its tokens, the end of block and the empty stored block for the last)
+// fits the encoder's per-segment output buffer: at most SEG bytes of bits.  With several
+// segments per block one can exceed its stored size when the code was shaped by the
+// others; such a block is stored instead (k_huff and the CPU emulation decide alike).
+template <class C>
+PBX_HD bool seg_shares_fit(const uint32_t* dk, uint32_t nsg, uint32_t hdr, uint32_t eob_len, uint32_t last,
+                           uint32_t nbytes) {
+    uint64_t run = hdr;
+    for (uint32_t k = 0; k < nsg; k++) {
+        const uint64_t b0 = k == 0 ? 0 : run;
+        run += dk[k];
+        const uint64_t b1 = k + 1 < nsg ? run : last ? run + eob_len : 8ull * nbytes;
+        if (b1 - b0 > 8ull * (uint64_t)C::SEG) return false;
+    }
+    return true;
+}
+
 // Block type from the three sizes.  Requires rboff = exclusive prefix of RLE bits and
 // misc[M_HDRBITS] = their total.  One thread.  Leaves M_HDRBITS = header bits of the
 // chosen block, M_DATABITS = its data bits (EOB included) and M_NBYTES = the segment's

@@ -146,6 +146,20 @@ int run_block(std::vector<std::unique_ptr<Smem>>& LZ, Smem& H, const Src& src, c
         H.dfreq[i] = v;
     }
     run_huff(H, sl, last);
+    if (H.misc[M_BTYPE] != 0) {  // k_huff's per-segment capacity rule (seg_shares_fit)
+        uint32_t dk[BLK_SEGS];
+        for (uint32_t k = 0; k < nsg; k++) {
+            BitsF<Smem> f{H, 0};
+            for (int t = 0; t < C::NT; t++) walk_tokens<C>((uint32_t)t, *LZ[k], sps[k], f);
+            dk[k] = f.bits;
+        }
+        if (!seg_shares_fit<C>(dk, nsg, H.misc[M_HDRBITS], H.lcode[256] >> 16, last, H.misc[M_NBYTES])) {
+            H.misc[M_BTYPE] = 0;
+            H.misc[M_HDRBITS] = 0;
+            H.misc[M_DATABITS] = 0;
+            H.misc[M_NBYTES] = block_nbytes(0, 0, sl, last);
+        }
+    }
     for (uint32_t k = 0; k < 256; k++) H.crc_t[0][k] = crc_table_entry(k);
     const uint32_t bt = H.misc[M_BTYPE], nbytes = H.misc[M_NBYTES];
     if (nbytes > cap) return -1;

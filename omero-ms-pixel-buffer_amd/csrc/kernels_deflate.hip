@@ -90,32 +90,22 @@ struct HuffSmem {
     };
 };
 
-constexpr int CRC_NIB_LEVELS_ = 7;
-// Output word k of the encoder lives at LDS word osk(k).  A skew (k + k / 32: the CRC phase's
-// lanes, 8 consecutive words each, then hit 32 banks instead of 4) was measured slower.
-#ifdef PBX_ENC_SKEW  // timing experiment (measured 3% slower: the CRC's reads are not the cost)
-__device__ __forceinline__ uint32_t osk(uint32_t k) { return k + (k >> 5); }
-#else
-__device__ __forceinline__ uint32_t osk(uint32_t k) { return k; }
-#endif
+// CRC combine levels: x^(8*32*2^k) for k = 0..5 (the wave tree over 32-byte chunks) and
+// k = 6..8 (1, 2, 4 waves of 2 KiB: a wave's distance to the segment end).
+constexpr int CRC_NIB_LEVELS_ = 9;
 template <class C>
 struct EncSmem {
     uint32_t mpos[C::NW * C::MAXMW];
     uint16_t mdist[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
     uint32_t lcode[289], dcode[32];  // slot form; lcode[288] = no token
-#ifdef PBX_ENC_SKEW
-    alignas(16) uint32_t out[(C::OUTW + C::OUTW / 32 + 2 + 3) & ~3];  // word k at osk(k)
-#else
     alignas(16) uint32_t out[(C::OUTW + 3) & ~3];
-#endif
-    uint32_t crc_t[4][256];
-    uint32_t crcn[CRC_NIB_LEVELS_][8][16];
-    uint32_t misc[M_NMISC];
-    uint32_t t_a[C::NT];
+    alignas(16) uint32_t crc_t[4][256];
+    alignas(16) uint32_t crcn[CRC_NIB_LEVELS_][8][16];
     uint32_t wtot[16];
     uint32_t red[C::NW];
 };
+static_assert(sizeof(EncSmem<DC>) <= 40 * 1024, "four encode workgroups per CU (160 KiB LDS)");
 
 // Slicing-by-4 CRC-32 tables, built at compile time into device memory (copied to LDS).
 struct CrcTables {
@@ -135,10 +125,10 @@ constexpr CrcTables make_crc_tables() {
 }
 __constant__ const CrcTables kCrcTables = make_crc_tables();
 
-// The CRC combine multiplies by constant operators K = x^(8*64*2^k) mod P (k = 0..6: the
-// wave tree over 64-byte chunks, then one wave's 4 KiB).  b -> K*b mod P is GF(2)-linear,
-// so it is 8 lookups in nibble tables T[j][v] = K*(v << 4j) (3.5 KB in LDS) instead of a
-// 32-step shift-and-reduce loop.
+// The CRC combine multiplies by constant operators K = x^(8*32*2^k) mod P (k = 0..5: the
+// wave tree over 32-byte chunks; k = 6..8: 1, 2 and 4 waves of 2 KiB).  b -> K*b mod P is
+// GF(2)-linear, so it is 8 lookups in nibble tables T[j][v] = K*(v << 4j) (4.5 KB in LDS)
+// instead of a 32-step shift-and-reduce loop.
 constexpr int CRC_NIB_LEVELS = CRC_NIB_LEVELS_;
 struct CrcNibTables {
     uint32_t t[CRC_NIB_LEVELS][8][16];
@@ -1086,26 +1076,36 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         cg[i] = i < 288 ? S.lcode[i] : i < 320 ? S.dcode[i - 288] : S.hdrw[i - 320];
     // every segment's bit range in the block: [header] tokens of segment 0, 1, ... [EOB]
     // [empty stored block unless the tile ends here]; a stored block is byte-aligned
-    const uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
+    // the segments' token bits under the block's code (wave-uniform)
+    uint32_t dk[BLK_SEGS];
+#pragma unroll
+    for (uint32_t k = 0; k < BLK_SEGS; k++) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t i = tid + 64 * j, f = hreg[k][j];
+            if (i == 256 || (i >= 286 && i < 288) || i >= 318 || !f) continue;
+            const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i - 288]) >> 16;
+            const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i - 288);
+            d += f * (L + eb);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+        dk[k] = d;
+    }
+    // a segment's share of a Huffman-coded block must fit k_encode's output buffer
+    // (deflate_seg.h seg_share_fits); else the block is stored
+    uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
+    uint32_t dbits = S.misc[M_DATABITS];
+    if (bt != 0 && !seg_shares_fit<C>(dk, nsg, hdr, S.lcode[256] >> 16, last, nbytes)) {
+        bt = 0; hdr = 0; dbits = 0;
+        nbytes = block_nbytes(0, 0, sl, last);
+    }
     uint32_t run = bt == 0 ? 40u : hdr;
 #pragma unroll
     for (uint32_t k = 0; k < BLK_SEGS; k++) {
         if (k >= nsg) break;
-        uint32_t d = 0;
-        if (bt == 0) {
-            d = 8 * sls[k];
-        } else {
-#pragma unroll
-            for (int j = 0; j < 5; j++) {
-                const uint32_t i = tid + 64 * j, f = hreg[k][j];
-                if (i == 256 || (i >= 286 && i < 288) || i >= 318 || !f) continue;
-                const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i - 288]) >> 16;
-                const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i - 288);
-                d += f * (L + eb);
-            }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-        }
+        const uint32_t d = bt == 0 ? 8 * sls[k] : dk[k];
         if (tid == 0) {
             SegInfo& g = info[seg0 + k];
             g.btype = bt;
@@ -1117,7 +1117,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     }
     if (tid == 0) {
         blk[b].nbytes = nbytes;
-        blk[b].data_bits = S.misc[M_DATABITS];
+        blk[b].data_bits = dbits;
         blk[b].fin = last;
     }
     stamp();
@@ -1197,75 +1197,87 @@ __global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restric
 }
 
 // ==================================================================== k_encode
-// Output bytes j..j+3 (j = any byte offset) from the assembled (skewed) words.
+// Output bytes j..j+3 (j = any byte offset) from the assembled words.
 template <class SM>
 __device__ __forceinline__ uint32_t out_word(const SM& S, uint32_t j) {
-    const uint32_t w0 = S.out[osk(j >> 2)], w1 = S.out[osk((j >> 2) + 1)], sh = (j & 3) * 8;
+    const uint32_t w0 = S.out[j >> 2], w1 = S.out[(j >> 2) + 1], sh = (j & 3) * 8;
     return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
 }
 template <class SM>
-__device__ __forceinline__ uint32_t out_byte_sk(const SM& S, uint32_t j) {
-    return (S.out[osk(j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+__device__ __forceinline__ uint32_t out_byte_at(const SM& S, uint32_t j) {
+    return (S.out[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
 }
 template <class SM>
 __device__ __forceinline__ uint8_t* out_byte_ptr(SM& S, uint32_t j) {
-    return (uint8_t*)&S.out[osk(j >> 2)] + (j & 3);
+    return (uint8_t*)&S.out[j >> 2] + (j & 3);
 }
 
-// Bit writers over the skewed output words (deflate_seg.h RunWriter / BitWriter semantics:
+// Bit writers over the LDS output words (deflate_seg.h RunWriter / BitWriter semantics:
 // every word is OR'd into a zeroed buffer, so words shared with the neighbouring bit ranges
 // need no special case).  (A branch-free put -- OR zero when no word completes -- measured
 // slower: on compressible data many lanes then OR into the same few words.)
-struct SkRunWriter {
+struct LdsRunWriter {
     uint32_t* out;
     uint32_t word, nacc;
     uint64_t acc;
-    __device__ SkRunWriter(uint32_t* o, uint32_t pos) : out(o), word(pos >> 5), nacc(pos & 31), acc(0) {}
+    __device__ LdsRunWriter(uint32_t* o, uint32_t pos) : out(o), word(pos >> 5), nacc(pos & 31), acc(0) {}
     __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
         acc |= (uint64_t)v << nacc;
         nacc += n;
         if (nacc >= 32) {
-            atomicOr(&out[osk(word)], (uint32_t)acc);
+            atomicOr(&out[word], (uint32_t)acc);
             word++;
             acc >>= 32;
             nacc -= 32;
         }
     }
     __device__ __forceinline__ void finish() {
-        if (acc) atomicOr(&out[osk(word)], (uint32_t)acc);
+        if (acc) atomicOr(&out[word], (uint32_t)acc);
     }
 };
-struct SkBitWriter {
+struct LdsBitWriter {
     uint32_t* out;
     uint32_t pos;
     __device__ void put(uint32_t v, uint32_t n) {
         if (!n) return;
         const uint32_t w = pos >> 5, sh = pos & 31;
-        atomicOr(&out[osk(w)], v << sh);
-        if (sh + n > 32) atomicOr(&out[osk(w + 1)], v >> (32 - sh));
+        atomicOr(&out[w], v << sh);
+        if (sh + n > 32) atomicOr(&out[w + 1], v >> (32 - sh));
         pos += n;
     }
 };
 
-// ph_crc (deflate_seg.h) over the skewed words.
+// Slicing-by-4 CRC step over one little-endian word.
+template <class SM>
+__device__ __forceinline__ uint32_t crc_word(const SM& S, uint32_t c, uint32_t v) {
+    c ^= v;
+    return S.crc_t[3][c & 0xFF] ^ S.crc_t[2][(c >> 8) & 0xFF] ^ S.crc_t[1][(c >> 16) & 0xFF] ^
+           S.crc_t[0][c >> 24];
+}
+
+// ph_crc (deflate_seg.h) over out[0, 4 nv) with nv a multiple of 8 words: the segment's
+// bytes sit after P leading zero bytes (P = -bytes mod 32), so every thread's right-aligned
+// 32-byte chunk starts on a 32-byte boundary and is two 16-byte LDS reads (no realignment,
+// no stride-8 word reads).  Byte zb (the head byte shared with the previous segment, or
+// ~0u) reads as zero.
 template <class C, class SM>
-__device__ __forceinline__ uint32_t crc_chunk_sk(uint32_t tid, const SM& S) {
-    const uint32_t nbytes = S.misc[M_NBYTES];
-    const uint32_t pad = (4u - (nbytes & 3u)) & 3u, nv = (nbytes + pad) >> 2;
-    const int64_t hi = (int64_t)nv - (int64_t)(C::NT - 1 - tid) * (C::CRCC / 4);
-    int64_t lo = hi - C::CRCC / 4;
-    if (lo < 0 || tid == 0) lo = 0;
+__device__ __forceinline__ uint32_t crc_chunk_aligned(uint32_t tid, const SM& S, uint32_t nv, uint32_t zb) {
+    const int32_t hi = (int32_t)nv - (int32_t)(C::NT - 1 - tid) * (C::CRCC / 4);
     uint32_t c = 0;
-    for (int64_t k = lo; k < hi; k++) {
-        const uint32_t w1 = S.out[osk((uint32_t)k)];
-        uint32_t v = w1;
-        if (pad) {
-            const uint32_t w0 = k > 0 ? S.out[osk((uint32_t)k - 1)] : 0u;
-            v = (w1 << (8 * pad)) | (w0 >> (32 - 8 * pad));
+    auto step = [&](uint32_t k) {  // words k..k+3
+        const uint4 q = *(const uint4*)&S.out[k];
+        uint32_t v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            if (k + j == (zb >> 2)) v[j] &= ~(0xFFu << (8 * (zb & 3)));
+            c = crc_word(S, c, v[j]);
         }
-        c ^= v;
-        c = S.crc_t[3][c & 0xFF] ^ S.crc_t[2][(c >> 8) & 0xFF] ^ S.crc_t[1][(c >> 16) & 0xFF] ^
-            S.crc_t[0][c >> 24];
+    };
+    if (tid == 0) {
+        for (int32_t k = 0; k < hi; k += 4) step((uint32_t)k);  // its chunk and everything before
+    } else if (hi >= (int32_t)(C::CRCC / 4)) {
+        step((uint32_t)hi - 8);
+        step((uint32_t)hi - 4);
     }
     return c;
 }
@@ -1282,9 +1294,6 @@ __device__ __forceinline__ uint32_t crc_chunk_sk(uint32_t tid, const SM& S) {
 #endif
 #ifndef PBX_ENC_SKIP_STORE
 #define PBX_ENC_SKIP_STORE 0
-#endif
-#ifndef PBX_ENC_SKIP_TABLES
-#define PBX_ENC_SKIP_TABLES 0
 #endif
 
 // A token's bits packed in one register: value (<= 20 bits) | nbits << 27.  The LDS code
@@ -1373,6 +1382,13 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
 // [bit0, bit1) k_huff assigned.  The bytes it owns entirely go straight to the compacted
 // output; a byte it shares with the previous / next segment of the block (bit0 or bit1 not
 // on a byte boundary) is left to k_frame (SegInfo.part), which ORs the two halves.
+//
+// Four barriers: (1) inputs in LDS and the output words zeroed (the block header already
+// in them), (2) the bit offsets scanned, (3) every token written, (4) the waves' CRCs.
+// Everything the segment needs is loaded up front in two dependent rounds (the record and
+// the match counts, then the bytes, matches and codes); the CRC tables, needed last, are
+// loaded while the slots are built.  The segment's bytes go P = -bytes mod 32 bytes into
+// out[], so the CRC chunks are 32-byte aligned.
 template <class C, bool PROF>
 __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict__ dt,
                                                   const uint32_t* __restrict__ seg_tile,
@@ -1384,9 +1400,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
                                                   const uint64_t* __restrict__ offs,
                                                   uint8_t* __restrict__ out,
                                                   uint64_t* __restrict__ stamps) {
-    static_assert(C::CH == 32, "two 16-byte loads per thread chunk");
+    static_assert(C::CH == 32 && C::CRCC == 32, "two 16-byte loads per thread chunk");
     __shared__ EncSmem<C> S;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
     uint32_t nst = 0;
     auto stamp = [&]() {
@@ -1394,8 +1411,25 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         nst++;
     };
     stamp();
-    const SegInfo gi = info[seg];  // everything the encoder needs about its segment / tile
-    const BlkInfo bi = blk[gi.blk];
+    // round 1: the segment record and this wave's match count (scalar loads, issued together:
+    // the empty asm uses make the compiler wait for all of them at one point)
+    const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
+    SegInfo gi;  // everything the encoder needs about its segment / tile
+    uint32_t nmw;
+    {
+        nmw = mg[w];
+        static_assert(sizeof(SegInfo) == 80, "five 16-byte words");
+        const uint4* src = (const uint4*)&info[seg];
+        const uint4 g0 = src[0], g1 = src[1], g2 = src[2], g3 = src[3], g4 = src[4];
+        asm volatile("" ::"s"(g0.x), "s"(g0.y), "s"(g0.z), "s"(g0.w), "s"(g1.x), "s"(g1.y), "s"(g1.z),
+                     "s"(g1.w), "s"(g2.x), "s"(g2.y), "s"(g2.z), "s"(g2.w), "s"(g3.x), "s"(g3.y),
+                     "s"(g3.z), "s"(g3.w), "s"(g4.x), "s"(g4.y), "s"(g4.z), "s"(g4.w));
+        __builtin_memcpy((uint4*)&gi, &g0, 16);
+        __builtin_memcpy((uint4*)&gi + 1, &g1, 16);
+        __builtin_memcpy((uint4*)&gi + 2, &g2, 16);
+        __builtin_memcpy((uint4*)&gi + 3, &g3, 16);
+        __builtin_memcpy((uint4*)&gi + 4, &g4, 16);
+    }
     const uint32_t ti = gi.tile;
     SegParams sp;  // the encoder holds the segment only (no window)
     sp.base = 0;
@@ -1406,90 +1440,123 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     const uint64_t seg_off = ((uint64_t)gi.src_hi << 32) | gi.src_lo;
     const bool first = (gi.flags & SF_FIRST) != 0, lastb = (gi.flags & SF_LAST) != 0;
     const bool final_seg = sp.last != 0;          // the tile's stream ends in this segment
-    const uint32_t byte0 = gi.bit0 >> 3, lb = gi.bit0 & 7u;  // out[] byte 0 = block byte byte0
-    const uint32_t le = gi.bit1 - 8 * byte0;      // end bit in out[]
-    // the thread's chunk bytes (zero past the segment) straight into registers
+    const bool stored = gi.btype == 0;
+    const uint32_t byte0 = gi.bit0 >> 3, lb = gi.bit0 & 7u;  // block byte byte0 = out[] byte P
+    const uint32_t le = gi.bit1 - 8 * byte0;      // end bit, relative to byte P
+    // bytes owned: [o0, o1) after byte P; a partial first byte (lb != 0) and a partial last
+    // byte of a non-final segment are shared with the neighbours (k_frame joins them)
+    const uint32_t o0 = lb ? 1u : 0u;
+    uint32_t o1 = final_seg ? (le + 7) >> 3 : le >> 3;
+    if (o1 < o0) o1 = o0;
+    const uint32_t P = (0u - o1) & 31u, SH = 8 * P;  // leading zero bytes: P + o1 = 0 mod 32
+    // round 2: the thread's chunk bytes (zero past the segment: loads past it read the
+    // segment start instead, no branch), the wave's matches, the block's codes and header
     uint32_t cb[C::CH / 4];
     {
         const uint32_t cs = tid * C::CH;
-        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
-        {
-            const uint8_t* src = stream + seg_off + cs;
-            if (cs < sp.sl) q0 = *(const uint4*)src;
-            if (cs + 16 < sp.sl) q1 = *(const uint4*)(src + 16);
-        }
+        const uint4 q0 = *(const uint4*)(stream + seg_off + (cs < sp.sl ? cs : 0u));
+        const uint4 q1 = *(const uint4*)(stream + seg_off + (cs + 16 < sp.sl ? cs + 16 : 0u));
         cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
         cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
 #pragma unroll
-        for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end
+        for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end, branch-free
             const int32_t keep = (int32_t)sp.sl - (int32_t)(cs + 4 * k);
-            cb[k] = keep >= 4 ? cb[k] : keep <= 0 ? 0u : cb[k] & ((1u << (8 * keep)) - 1u);
+            const uint32_t kb = keep <= 0 ? 0u : keep >= 4 ? 32u : 8u * (uint32_t)keep;
+            cb[k] &= (uint32_t)((1ull << kb) - 1ull);
         }
     }
-    // this wave's match list (a thread's tokens only depend on its own wave's matches)
-    {
-        const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
-        const uint32_t nmw = __builtin_amdgcn_readfirstlane(mg[w]);
-        if (lane == 0) S.w_nm[w] = nmw;
-        for (uint32_t m = lane; m < nmw; m += 64) {
-            S.mpos[w * C::MAXMW + m] = mg[C::NW + w * C::MAXMW + m];
-            S.mdist[w * C::MAXMW + m] = (uint16_t)mg[C::NW + C::NW * C::MAXMW + w * C::MAXMW + m];
-        }
-    }
+    const BlkInfo bi = blk[gi.blk];       // scalar loads, needed at the end
+    const uint64_t tile_off = offs[ti];
     const uint32_t* cg = codes + (size_t)gi.blk * CODE_WORDS;
-    for (uint32_t i = tid; i < 320; i += C::NT) {
-        if (i < 288) S.lcode[i] = slot_from_code(cg[i]); else S.dcode[i - 288] = slot_from_code(cg[i]);
+    const uint32_t craw = cg[tid < 320 ? tid : 319u];  // unconditional: no branch, no early wait
+    // the block header (first segment of a Huffman block): word tid, OR-ed in at bit SH + 32 tid
+    const bool hdr = first && !stored;
+    const uint32_t hraw = cg[320 + (tid < (uint32_t)C::HDRW ? tid : (uint32_t)C::HDRW - 1)];
+    {
+        static_assert(C::MAXMW == 256, "four match slots per lane");
+        const uint32_t* gp = mg + C::NW + w * C::MAXMW;
+        const uint32_t* gd = mg + C::NW + C::NW * C::MAXMW + w * C::MAXMW;
+        uint32_t vp[4], vd[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t m = lane + 64 * j;
+            vp[j] = m < nmw ? gp[m] : 0u;
+            vd[j] = m < nmw ? gd[m] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t m = lane + 64 * j;
+            if (m < nmw) {
+                S.mpos[w * C::MAXMW + m] = vp[j];
+                S.mdist[w * C::MAXMW + m] = (uint16_t)vd[j];
+            }
+        }
     }
+    if (lane == 0) S.w_nm[w] = nmw;
+    if (tid < 288) S.lcode[tid] = slot_from_code(craw); else if (tid < 320) S.dcode[tid - 288] = slot_from_code(craw);
     if (tid == 0) S.lcode[SLOT_NONE] = 0;
-    {  // zero the (skewed) output words; the block header goes in after the barrier
+    {   // zero the output words
         uint4* o4 = (uint4*)S.out;
         for (uint32_t k = tid; k < (uint32_t)(sizeof(S.out) / 16); k += C::NT) o4[k] = make_uint4(0, 0, 0, 0);
     }
-    const uint32_t hdrw = (first && gi.btype != 0 && tid < (uint32_t)C::HDRW) ? cg[320 + tid] : 0u;
-    if (!PBX_ENC_SKIP_TABLES) {
-        for (uint32_t k = tid; k < 1024; k += C::NT) (&S.crc_t[0][0])[k] = (&kCrcTables.t[0][0])[k];
-        for (uint32_t k = tid; k < CRC_NIB_LEVELS * 128; k += C::NT) (&S.crcn[0][0][0])[k] = (&kCrcNib.t[0][0][0])[k];
-    }
     __syncthreads();
-    stamp();  // diagnostics: loads and tables in LDS
-    if (hdrw) S.out[osk(tid)] = hdrw;
-    if (gi.btype == 0) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; bytes
-        const uint32_t cs = tid * C::CH, o = first ? 5u : 0u;
-#pragma unroll
-        for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
-            if (cs + i < sp.sl) *out_byte_ptr(S, o + cs + i) = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
-        if (first && tid == 0) {
-            const uint32_t len = bi.nbytes - 5;  // LEN: every byte of the block's segments
-            *out_byte_ptr(S, 0) = (uint8_t)(bi.fin ? 1 : 0);
-            *out_byte_ptr(S, 1) = (uint8_t)len; *out_byte_ptr(S, 2) = (uint8_t)(len >> 8);
-            *out_byte_ptr(S, 3) = (uint8_t)~len; *out_byte_ptr(S, 4) = (uint8_t)(~len >> 8);
-        }
-    }
-    __syncthreads();
+    stamp();  // diagnostics: inputs in LDS
     uint32_t slot[C::CH + 2];
     uint32_t nbits = 0;
-    if (gi.btype != 0) {
+    if (!stored) {
         build_slots<C>(tid, S, sp, cb, slot);
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) nbits += slot[i] >> 27;
+    }
+    // the CRC tables (needed after barrier 3): loaded now, stored before barrier 2
+    {
+        constexpr uint32_t NT4 = 256, NN4 = CRC_NIB_LEVELS * 32;
+        for (uint32_t k = tid; k < NT4 + NN4; k += C::NT) {
+            if (k < NT4) ((uint4*)&S.crc_t[0][0])[k] = ((const uint4*)&kCrcTables.t[0][0])[k];
+            else ((uint4*)&S.crcn[0][0][0])[k - NT4] = ((const uint4*)&kCrcNib.t[0][0][0])[k - NT4];
+        }
     }
     if (PROF) {  // diagnostics: slots built (wave 0)
         __builtin_amdgcn_s_waitcnt(0);
         stamp();
     }
-    S.t_a[tid] = nbits;
+    // exclusive scan of the token bits over the workgroup (one barrier)
+    const uint32_t inc = wave_incl_add(nbits, lane);
+    if (lane == 63) S.wtot[w] = inc;
     __syncthreads();
     stamp();
-    const uint32_t bitsum = block_scan_excl_add<C::NT>(S.t_a, S.wtot, tid);
-    if (gi.btype != 0 && !PBX_ENC_SKIP_WRITE) {
-        const uint32_t tb = lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
-        SkRunWriter bw(S.out, tb + S.t_a[tid]);
+    uint32_t pre = 0, bitsum = 0;
+#pragma unroll
+    for (int i = 0; i < C::NW; i++) {
+        const uint32_t x = S.wtot[i];
+        pre += (uint32_t)i < w ? x : 0u;
+        bitsum += x;
+    }
+    if (stored) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; the bytes
+        const uint32_t cs = tid * C::CH, o = P + (first ? 5u : 0u);
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
+            if (cs + i < sp.sl) *out_byte_ptr(S, o + cs + i) = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
+        if (first && tid == 0) {
+            const uint32_t len = bi.nbytes - 5;  // LEN: every byte of the block's segments
+            *out_byte_ptr(S, P) = (uint8_t)(bi.fin ? 1 : 0);
+            *out_byte_ptr(S, P + 1) = (uint8_t)len; *out_byte_ptr(S, P + 2) = (uint8_t)(len >> 8);
+            *out_byte_ptr(S, P + 3) = (uint8_t)~len; *out_byte_ptr(S, P + 4) = (uint8_t)(~len >> 8);
+        }
+    } else if (!PBX_ENC_SKIP_WRITE) {
+        if (hdr && tid < (uint32_t)C::HDRW && hraw) {  // header word tid at bit SH + 32 tid
+            const uint32_t q = (SH >> 5) + tid, r = SH & 31;
+            atomicOr(&S.out[q], hraw << r);
+            if (r) atomicOr(&S.out[q + 1], hraw >> (32 - r));
+        }
+        const uint32_t tb = SH + lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
+        LdsRunWriter bw(S.out, tb + pre + inc - nbits);
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
         bw.finish();
         if (lastb && tid == 0) {  // end of block; a non-final block ends byte-aligned
             const uint32_t eob = S.lcode[256];
-            SkBitWriter ew{S.out, tb + bitsum};
+            LdsBitWriter ew{S.out, tb + bitsum};
             ew.put(eob & 0x7FFFFFFu, eob >> 27);
             if (!final_seg) {
                 ew.put(0, 3);
@@ -1499,52 +1566,51 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         }
     }
     __syncthreads();
-    // bytes owned: [o0, o1) of out[]; a partial first byte (lb != 0) and a partial last
-    // byte of a non-final segment are shared with the neighbours (k_frame joins them)
-    const uint32_t o0 = lb ? 1u : 0u;
-    uint32_t o1 = final_seg ? (le + 7) >> 3 : le >> 3;
-    if (o1 < o0) o1 = o0;
-    const bool has_tail = !final_seg && (le & 7u) && !(lb && (le >> 3) == 0);
-    if (tid == 0) {
-        uint32_t part = 0;
-        if (lb) part |= out_byte_sk(S, 0) | SP_HEAD;
-        if (has_tail) part |= (out_byte_sk(S, le >> 3) << 8) | SP_TAIL;
-        S.misc[M_CRCOP] = part;
-        if (lb) *out_byte_ptr(S, 0) = 0;  // leading zero bytes leave a raw CRC unchanged
-        S.misc[M_NBYTES] = o1;
-    }
-    __syncthreads();
     stamp();
-    // CRC-32 of out[0, o1): raw CRC of right-aligned 64-byte chunks, combined per wave by
-    // shuffles with the constant operators x^(8*64*2^k), then across the waves
+    // CRC-32 of out[P, P + o1) (the shared head byte as zero): raw CRC of the 32-byte chunks,
+    // combined per wave by shuffles with the constant operators x^(8*32*2^k), then every
+    // wave's by x^(8*2048*(NW-1-w)) (its distance to the end), XOR-ed by thread 0.  Waves
+    // whose chunks are all empty skip it.
+    const uint32_t nv = (P + o1) >> 2;
+    const bool wact = nv >= 8u * (uint32_t)(C::NT - 64 * w - 63);
     uint32_t c = 0;
-    if (!PBX_ENC_SKIP_CRC) {
-        c = crc_chunk_sk<C>(tid, S);
+    if (!PBX_ENC_SKIP_CRC && wact) {
+        c = crc_chunk_aligned<C>(tid, S, nv, lb ? P : 0xFFFFFFFFu);
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const uint32_t r = __shfl_down(c, 1 << k, 64);
             c = crc_mul_nib(S, k, c) ^ r;
         }
+        const uint32_t d = (uint32_t)C::NW - 1 - w;  // waves after this one
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if ((d >> k) & 1u) c = crc_mul_nib(S, 6 + k, c);
     }
     if (lane == 0) S.red[w] = c;
     // owned bytes to their final place: unaligned head and tail bytes, aligned words between
     const uint32_t nbytes = o1 - o0;
-    uint8_t* dst = out + offs[ti] + gi.zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
+    uint8_t* dst = out + tile_off + gi.zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
     uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
     if (head > nbytes) head = nbytes;
     const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
-    if (tid < head) dst[tid] = (uint8_t)out_byte_sk(S, o0 + tid);
-    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, o0 + head + 4 * k);
-    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_sk(S, o0 + j);
+    const uint32_t b0 = P + o0;
+    if (tid < head) dst[tid] = (uint8_t)out_byte_at(S, b0 + tid);
+    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, b0 + head + 4 * k);
+    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_at(S, b0 + j);
     __syncthreads();
     if (tid == 0) {
-        uint32_t raw = S.red[0];
-        for (int k = 1; k < C::NW; k++) raw = crc_mul_nib(S, 6, raw) ^ S.red[k];  // one wave = 64 chunks
+        uint32_t raw = 0;
+#pragma unroll
+        for (int k = 0; k < C::NW; k++) raw ^= S.red[k];
+        const bool has_tail = !final_seg && (le & 7u) && !(lb && (le >> 3) == 0);
+        uint32_t part = 0;
+        if (lb) part |= out_byte_at(S, P) | SP_HEAD;
+        if (has_tail) part |= (out_byte_at(S, P + (le >> 3)) << 8) | SP_TAIL;
         const uint32_t op = crc_x8n_small(nbytes);
         SegInfo& g = info[seg];
         g.crc = crc_from_raw(raw, op);
         g.crc_op = op;
-        g.part = S.misc[M_CRCOP];
+        g.part = part;
         g.bitsum = bitsum;
     }
     stamp();

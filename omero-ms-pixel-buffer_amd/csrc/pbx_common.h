@@ -83,7 +83,7 @@ struct SegOut {
     uint32_t bits;          // bits of the block (diagnostics)
 };
 
-// Per-segment record of the three deflate kernels (64 bytes, in HBM).
+// Per-segment record of the three deflate kernels (80 bytes, in HBM).
 struct SegInfo {
     uint32_t sl, last, wl, rowlen;       // k_lz77: geometry (last: the tile's final segment)
     uint32_t adler_s1, adler_s2;         // k_lz77: Adler-32 partial sums of the sl bytes

@@ -94,3 +94,21 @@ def test_lz77_records_cover_the_segment(kind):
                 covered += ln
         assert lits + covered == sl
         assert hist[k][256] == 1  # end of block
+
+
+def skewed_block_stream(seed=7):
+    """Three 16 KiB segments (one Huffman block): bytes 0..127 in the first two, 128..255 in
+    the third, no repeats.  The block's code favours the first two, so the third's share of
+    a Huffman-coded block would exceed 16 KiB: the block must be stored."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 128, 2 * 16384, dtype=np.uint8)
+    b = rng.integers(128, 256, 16384, dtype=np.uint8)
+    return np.concatenate([a, b]).tobytes()
+
+
+def test_segment_share_over_capacity_is_stored():
+    data = skewed_block_stream()
+    z, blks = _emu.deflate(data, 256)
+    assert zlib.decompress(z) == data
+    assert blks[0].btype == 0  # stored: a coded block would overflow the third segment

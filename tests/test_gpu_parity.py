@@ -322,3 +322,20 @@ def test_mixed_batch(service, oracle):
         else:
             r, px, _ = oracle.png_decode(body)
             assert r == 0 and px == tile
+
+
+def test_tiff_deflate_segment_capacity(adaptive_service):
+    """A Huffman block (3 segments) whose code would give one segment more than 16 KiB of
+    bits is stored (k_huff's seg_shares_fit): the GPU stream equals the CPU emulation byte
+    for byte and decodes exactly."""
+    from test_emu_deflate import skewed_block_stream
+    data = skewed_block_stream()
+    iid = next(_ids)
+    plane = np.frombuffer(data, np.uint8).reshape(192, 256)
+    adaptive_service.register_plane(iid, 0, 0, 0, pbx.UINT8, 256, 192, data=plane, big_endian=True)
+    (st, body), = adaptive_service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 0, 0, 256, 192, format="tif")])
+    assert st == pbx.OK
+    z, blks = _emu.deflate(data, 256)
+    assert blks[0].btype == 0
+    assert body[160:] == z
+    assert zlib.decompress(body[160:]) == data
