@@ -90,21 +90,27 @@ struct HuffSmem {
     };
 };
 
-// CRC combine levels: x^(8*32*2^k) for k = 0..5 (the wave tree over 32-byte chunks) and
-// k = 6..8 (1, 2, 4 waves of 2 KiB: a wave's distance to the segment end).
-constexpr int CRC_NIB_LEVELS_ = 9;
+// The CRC combine tables of k_encode (words): per-lane distance operators x^(8*32*m) (TA,
+// m = 0..7 chunks) and x^(8*256*m) (TB, 8-chunk steps), then the wave-distance operators
+// x^(8*2048*2^k) (TW, k = 0..2), each as nibble tables (crc_lane_tables below).
+constexpr uint32_t CRCX_TA = 0, CRCX_TB = 1024, CRCX_TW = 2048, CRCX_WORDS = 2048 + 3 * 128;
 template <class C>
 struct EncSmem {
-    uint32_t mpos[C::NW * C::MAXMW];
-    uint16_t mdist[C::NW * C::MAXMW];
+    union {
+        struct {
+            uint32_t mpos[C::NW * C::MAXMW];
+            uint16_t mdist[C::NW * C::MAXMW];
+        };
+        alignas(16) uint32_t crcx[CRCX_WORDS];  // CRC combine tables once the slots are built
+    };
     uint32_t w_nm[C::NW];
     uint32_t lcode[289], dcode[32];  // slot form; lcode[288] = no token
     alignas(16) uint32_t out[(C::OUTW + 3) & ~3];
     alignas(16) uint32_t crc_t[4][256];
-    alignas(16) uint32_t crcn[CRC_NIB_LEVELS_][8][16];
     uint32_t wtot[16];
     uint32_t red[C::NW];
 };
+static_assert(CRCX_WORDS * 4 <= DC::NW * DC::MAXMW * 6, "the CRC combine tables fit the match lists' room");
 static_assert(sizeof(EncSmem<DC>) <= 40 * 1024, "four encode workgroups per CU (160 KiB LDS)");
 
 // Slicing-by-4 CRC-32 tables, built at compile time into device memory (copied to LDS).
@@ -125,23 +131,39 @@ constexpr CrcTables make_crc_tables() {
 }
 __constant__ const CrcTables kCrcTables = make_crc_tables();
 
-// The CRC combine multiplies by constant operators K = x^(8*32*2^k) mod P (k = 0..5: the
-// wave tree over 32-byte chunks; k = 6..8: 1, 2 and 4 waves of 2 KiB).  b -> K*b mod P is
-// GF(2)-linear, so it is 8 lookups in nibble tables T[j][v] = K*(v << 4j) (4.5 KB in LDS)
-// instead of a 32-step shift-and-reduce loop.
-constexpr int CRC_NIB_LEVELS = CRC_NIB_LEVELS_;
-struct CrcNibTables {
-    uint32_t t[CRC_NIB_LEVELS][8][16];
+// The CRC combine multiplies by constant operators K mod P.  b -> K*b mod P is GF(2)-linear,
+// so it is 8 lookups in nibble tables T[j][v] = K*(v << 4j) instead of a 32-step
+// shift-and-reduce loop.  A thread's chunk CRC is moved to the end of its wave's 2 KiB by
+// x^(8*32*dl), dl = 63 - lane = 8 mb + ma: TA (operator ma) then TB (operator mb), both laid
+// out [j][v][m] (lanes of one lookup use different m: the layout spreads them over banks);
+// the wave's XOR is moved to the segment end by TW levels k (x^(8*2048*2^k), [k][j][v]).
+struct CrcLaneTables {
+    uint32_t t[CRCX_WORDS];
 };
-constexpr CrcNibTables make_crc_nib(int log2c) {
-    CrcNibTables T{};
-    X8Table x = make_x8();
-    for (int k = 0; k < CRC_NIB_LEVELS; k++)
-        for (int j = 0; j < 8; j++)
-            for (uint32_t v = 0; v < 16; v++) T.t[k][j][v] = crc_multmodp_c(x.v[log2c + k], v << (4 * j));
+constexpr uint32_t crc_pow_c(uint32_t base, uint32_t m) {  // base^m mod P
+    uint32_t p = 1u << 31;
+    for (uint32_t i = 0; i < m; i++) p = crc_multmodp_c(base, p);
+    return p;
+}
+constexpr CrcLaneTables make_crc_lane_tables() {
+    CrcLaneTables T{};
+    const X8Table x = make_x8();
+    static_assert(DC::CRCC == 32, "x.v[5] = 32 bytes, x.v[8] = 256, x.v[11] = 2048");
+    for (uint32_t m = 0; m < 8; m++) {
+        const uint32_t ka = crc_pow_c(x.v[5], m), kb = crc_pow_c(x.v[8], m);
+        for (uint32_t j = 0; j < 8; j++)
+            for (uint32_t v = 0; v < 16; v++) {
+                T.t[CRCX_TA + j * 128 + v * 8 + m] = crc_multmodp_c(ka, v << (4 * j));
+                T.t[CRCX_TB + j * 128 + v * 8 + m] = crc_multmodp_c(kb, v << (4 * j));
+            }
+    }
+    for (uint32_t k = 0; k < 3; k++)
+        for (uint32_t j = 0; j < 8; j++)
+            for (uint32_t v = 0; v < 16; v++)
+                T.t[CRCX_TW + k * 128 + j * 16 + v] = crc_multmodp_c(x.v[11 + k], v << (4 * j));
     return T;
 }
-__constant__ const CrcNibTables kCrcNib = make_crc_nib(DC::LOG2_CRCC);
+__constant__ const CrcLaneTables kCrcLane = make_crc_lane_tables();
 
 // x^(8n) mod P for n < 2^16 from two tables: x^(8v) and x^(8*256*v).
 struct CrcPowTables {
@@ -166,12 +188,28 @@ constexpr CrcPowTables make_crc_pow() {
 }
 __constant__ const CrcPowTables kCrcPow = make_crc_pow();
 
-template <class SM>
-__device__ __forceinline__ uint32_t crc_mul_nib(const SM& S, int k, uint32_t b) {
+// b * (operator m of a [j][v][m] table at t)
+__device__ __forceinline__ uint32_t crc_mul_lane(const uint32_t* t, uint32_t m, uint32_t b) {
     uint32_t r = 0;
 #pragma unroll
-    for (int j = 0; j < 8; j++) r ^= S.crcn[k][j][(b >> (4 * j)) & 0xFu];
+    for (int j = 0; j < 8; j++) r ^= t[j * 128 + ((b >> (4 * j)) & 0xFu) * 8 + m];
     return r;
+}
+// b * (the operator of a [j][v] table at t)
+__device__ __forceinline__ uint32_t crc_mul_tab(const uint32_t* t, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r ^= t[j * 16 + ((b >> (4 * j)) & 0xFu)];
+    return r;
+}
+// XOR of x over the wave (row scans by DPP shifts, then the four row totals), uniform.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) ^ (uint32_t)__builtin_amdgcn_readlane((int)x, 31) ^
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 47) ^ (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 __device__ __forceinline__ uint32_t crc_x8n_small(uint32_t n) {  // n < 2^16
@@ -391,9 +429,37 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                 const int32_t b = (int32_t)a0 - (int32_t)d;
                 const int32_t r = b >> 2;
                 const uint32_t sh = (uint32_t)(b & 3) * 8;
-                uint32_t rw[9];
+                // words r .. r+8 from three aligned 16-byte reads (lanes 32 bytes apart: a
+                // 2-way conflict per read instead of 8-way on 9 word reads); r mod 4 is the
+                // same in every lane (a0 - 32 lane is), so the selection is uniform.  Quads
+                // before the buffer (positions the window mask drops) read quad 0.
+                const int32_t r4 = r & ~3;
+                uint32_t q12[12];
 #pragma unroll
-                for (int j = 0; j < 9; j++) rw[j] = S.buf[r + j > 0 ? r + j : 0];
+                for (int k = 0; k < 3; k++) {
+                    const int32_t at = r4 + 4 * k;
+                    const uint4 v = *(const uint4*)&S.buf[at > 0 ? at : 0];
+                    q12[4 * k] = v.x; q12[4 * k + 1] = v.y; q12[4 * k + 2] = v.z; q12[4 * k + 3] = v.w;
+                }
+                uint32_t rw[9];
+                switch (__builtin_amdgcn_readfirstlane((uint32_t)(r - r4))) {
+                case 0:
+#pragma unroll
+                    for (int j = 0; j < 9; j++) rw[j] = q12[j];
+                    break;
+                case 1:
+#pragma unroll
+                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 1];
+                    break;
+                case 2:
+#pragma unroll
+                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 2];
+                    break;
+                default:
+#pragma unroll
+                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 3];
+                    break;
+                }
 #pragma unroll
                 for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
             }
@@ -568,7 +634,11 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
     dr.init(d);
     const uint32_t nz = lz_fill_bytes<C>(sp) & ~15u;
-    if (direct) {
+#ifndef PBX_LZ_SKIP_FILL
+#define PBX_LZ_SKIP_FILL 0  // timing experiments only (scripts/variants.sh): wrong output
+#endif
+    if (PBX_LZ_SKIP_FILL) {
+    } else if (direct) {
         FillPre<LZ_PF> pf;
         fill_issue<C::NT, LZ_PF>(pf, dr, (uint32_t)sp.base, sp.wl + sp.sl, tid);
         if (PROF) stamp();  // diagnostics: the first loads issued
@@ -594,11 +664,17 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
     }
     stamp();
     // the thread's chunk words (and the word before it) from LDS
+    // (wl is a multiple of 16: two aligned 16-byte reads; the word before the chunk is the
+    // previous lane's last, one wave shift; lane 0 reads it)
     const uint32_t cs = tid * C::CH, wi = (sp.wl + cs) >> 2;
     uint32_t cw[9];
-    cw[0] = wi ? S.buf[wi - 1] : 0u;
-#pragma unroll
-    for (int j = 0; j < 8; j++) cw[j + 1] = S.buf[wi + j];
+    {
+        const uint4 q0 = *(const uint4*)&S.buf[wi], q1 = *(const uint4*)&S.buf[wi + 4];
+        cw[1] = q0.x; cw[2] = q0.y; cw[3] = q0.z; cw[4] = q0.w;
+        cw[5] = q1.x; cw[6] = q1.y; cw[7] = q1.z; cw[8] = q1.w;
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cw[8], 0x138, 0xF, 0xF, false);  // wave_shr:1
+        cw[0] = lane ? prev : (wi ? S.buf[wi - 1] : 0u);
+    }
     uint32_t cover, smask;
     ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
     stamp();
@@ -1335,6 +1411,14 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
         cover(mp[m1] & 0xFFFFu, (mp[m1] & 0xFFFFu) + (mp[m1] >> 16) + 3);
         m1++;
     }
+    // a wave without matches or partial chunks (most waves on noisy data): literals only
+    if (__builtin_amdgcn_ballot_w64(lo < m1 || covered != 0) == 0) {
+#pragma unroll
+        for (int i = 0; i < C::CH; i++) slot[i] = S.lcode[(cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu];
+        slot[C::CH] = 0;
+        slot[C::CH + 1] = 0;
+        return;
+    }
     // the first match starting in the chunk goes in with the literals, branch-free; any
     // further ones (several short matches in 32 bytes) are patched in after
     uint32_t i0 = 0xFFu, A = 0, B = 0, Cx = 0;
@@ -1508,14 +1592,8 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i++) nbits += slot[i] >> 27;
     }
-    // the CRC tables (needed after barrier 3): loaded now, stored before barrier 2
-    {
-        constexpr uint32_t NT4 = 256, NN4 = CRC_NIB_LEVELS * 32;
-        for (uint32_t k = tid; k < NT4 + NN4; k += C::NT) {
-            if (k < NT4) ((uint4*)&S.crc_t[0][0])[k] = ((const uint4*)&kCrcTables.t[0][0])[k];
-            else ((uint4*)&S.crcn[0][0][0])[k - NT4] = ((const uint4*)&kCrcNib.t[0][0][0])[k - NT4];
-        }
-    }
+    // the slicing tables (needed after barrier 3): loaded now, stored before barrier 2
+    if (tid < 256) ((uint4*)&S.crc_t[0][0])[tid] = ((const uint4*)&kCrcTables.t[0][0])[tid];
     if (PROF) {  // diagnostics: slots built (wave 0)
         __builtin_amdgcn_s_waitcnt(0);
         stamp();
@@ -1532,6 +1610,11 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         pre += (uint32_t)i < w ? x : 0u;
         bitsum += x;
     }
+    // the combine tables go where the match lists were (every wave is past build_slots)
+    constexpr uint32_t NX4 = CRCX_WORDS / 4;
+    static_assert(NX4 <= 2 * (uint32_t)C::NT, "two 16-byte table loads per thread");
+    const uint4 tx0 = ((const uint4*)kCrcLane.t)[tid];
+    const uint4 tx1 = ((const uint4*)kCrcLane.t)[tid + C::NT < NX4 ? tid + C::NT : tid];
     if (stored) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; the bytes
         const uint32_t cs = tid * C::CH, o = P + (first ? 5u : 0u);
 #pragma unroll
@@ -1565,26 +1648,27 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
             }
         }
     }
+    ((uint4*)S.crcx)[tid] = tx0;
+    if (tid + C::NT < NX4) ((uint4*)S.crcx)[tid + C::NT] = tx1;
     __syncthreads();
     stamp();
     // CRC-32 of out[P, P + o1) (the shared head byte as zero): raw CRC of the 32-byte chunks,
-    // combined per wave by shuffles with the constant operators x^(8*32*2^k), then every
-    // wave's by x^(8*2048*(NW-1-w)) (its distance to the end), XOR-ed by thread 0.  Waves
-    // whose chunks are all empty skip it.
+    // each moved to its wave's end by its own operator x^(8*32*(63-lane)) (two table
+    // multiplies), XOR-ed over the wave, moved to the segment end by x^(8*2048*(NW-1-w)) and
+    // XOR-ed over the waves by thread 0.  Waves whose chunks are all empty skip it.
     const uint32_t nv = (P + o1) >> 2;
     const bool wact = nv >= 8u * (uint32_t)(C::NT - 64 * w - 63);
     uint32_t c = 0;
     if (!PBX_ENC_SKIP_CRC && wact) {
         c = crc_chunk_aligned<C>(tid, S, nv, lb ? P : 0xFFFFFFFFu);
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const uint32_t r = __shfl_down(c, 1 << k, 64);
-            c = crc_mul_nib(S, k, c) ^ r;
-        }
+        const uint32_t dl = 63 - lane;
+        c = crc_mul_lane(S.crcx + CRCX_TA, dl & 7u, c);
+        c = crc_mul_lane(S.crcx + CRCX_TB, dl >> 3, c);
+        c = wave_xor(c);
         const uint32_t d = (uint32_t)C::NW - 1 - w;  // waves after this one
 #pragma unroll
         for (int k = 0; k < 3; k++)
-            if ((d >> k) & 1u) c = crc_mul_nib(S, 6 + k, c);
+            if ((d >> k) & 1u) c = crc_mul_tab(S.crcx + CRCX_TW + 128 * k, c);
     }
     if (lane == 0) S.red[w] = c;
     // owned bytes to their final place: unaligned head and tail bytes, aligned words between
