@@ -270,7 +270,7 @@ struct DirectRows {
     int64_t pitch;
     uint32_t rowlen, rb, fb, h, nc, ngrp;
     int32_t bpp;
-    bool swap, flip;
+    bool swap, flip, aligned;
     __device__ __forceinline__ void init(const TileDesc& d) {
         row0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
         pitch = d.pitch;
@@ -283,6 +283,7 @@ struct DirectRows {
         bpp = d.bpp;
         swap = (d.flags & TF_SWAP) != 0;
         flip = (d.flags & TF_FLIP) != 0;
+        aligned = (rb & 15u) == 0;  // rows of whole chunks: aligned stores (fill_stores)
     }
 };
 
@@ -294,39 +295,77 @@ struct DirectRows {
 template <uint32_t K>
 struct FillPre {
     uint4 v[K];
+    uint4 pv;  // aligned fill: lane 0's chunk before the first task's (prev group / row)
 };
 
 struct FillGeom {
-    uint32_t ra, ntask;
+    uint32_t ra, rz, ntask;
     __device__ __forceinline__ FillGeom(const DirectRows& dr, uint32_t B, uint32_t nb) {
         ra = B / dr.rowlen;
-        const uint32_t rz = (B + nb - 1) / dr.rowlen;
+        rz = (B + nb - 1) / dr.rowlen;
         ntask = (rz - ra + 1) * dr.ngrp;
     }
 };
 
+// A wave's K tasks are consecutive (k0 .. k0+K-1): the chunk before a task's first is the
+// previous task's last (a readlane), except for the first task, whose lane 0 loads it (pv).
 template <int NT, uint32_t K>
-__device__ __forceinline__ void fill_loads(uint4 (&v)[K], const DirectRows& dr, const FillGeom& g,
-                                           uint32_t k0, uint32_t lane) {
-    constexpr uint32_t NW = NT / 64;
+__device__ __forceinline__ void fill_loads(uint4 (&v)[K], uint4& pv, const DirectRows& dr,
+                                           const FillGeom& g, uint32_t k0, uint32_t lane) {
 #pragma unroll
     for (uint32_t j = 0; j < K; j++) {
-        const uint32_t k = k0 + j * NW < g.ntask ? k0 + j * NW : k0;
+        const uint32_t k = k0 + j < g.ntask ? k0 + j : k0;
         const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
         const uint32_t c0 = (k - i * dr.ngrp) * 64;
         const uint8_t* rp = dr.row0 + (int64_t)(g.ra + i) * dr.pitch + 16 * c0;
         v[j] = gload16(rp + 16 * (c0 + lane < dr.nc ? lane : 0u));
+        if (j == 0 && dr.aligned) {  // lane 0: the chunk before (previous group, or the row above's last)
+            pv = make_uint4(0, 0, 0, 0);
+            if (lane == 0 && (c0 > 0 || g.ra + i > 0))
+                pv = gload16(c0 > 0 ? rp - 16 : rp - dr.pitch + 16 * (dr.nc - 1));
+        }
     }
 }
 
+// Bytes [16 - s, 16) of p followed by bytes [0, 16 - s) of x (little-endian 16-byte words),
+// s uniform in 0..15.
+__device__ __forceinline__ uint4 funnel16(const uint4& p, const uint4& x, uint32_t s) {
+    const uint32_t z[8] = {p.x, p.y, p.z, p.w, x.x, x.y, x.z, x.w};
+    const uint32_t q = (16 - s) >> 2, r = (16 - s) & 3;
+    uint32_t o[4];
+    switch (__builtin_amdgcn_readfirstlane(q)) {
+    case 0:
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(z[k + 1], z[k], r);
+        break;
+    case 1:
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(z[k + 2], z[k + 1], r);
+        break;
+    case 2:
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(z[k + 3], z[k + 2], r);
+        break;
+    case 3:
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(z[k + 4], z[k + 3], r);
+        break;
+    default:  // s == 0
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = z[k + 4];
+        break;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int NT, uint32_t K>
-__device__ __forceinline__ void fill_stores(const uint4 (&v)[K], uint8_t* bb, const DirectRows& dr,
-                                            const FillGeom& g, uint32_t B, uint32_t nb, uint32_t k0,
-                                            uint32_t lane) {
-    constexpr uint32_t NW = NT / 64;
+__device__ __forceinline__ void fill_stores(const uint4 (&v)[K], const uint4& pv, uint8_t* bb,
+                                            const DirectRows& dr, const FillGeom& g, uint32_t B,
+                                            uint32_t nb, uint32_t k0, uint32_t lane) {
+    uint4 xlast = make_uint4(0, 0, 0, 0);  // the previous task's last chunk (uniform)
 #pragma unroll
     for (uint32_t j = 0; j < K; j++) {
-        const uint32_t k = k0 + j * NW;
+        const uint32_t k = k0 + j;
         if (k >= g.ntask) break;  // uniform
         const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
         const uint32_t c0 = (k - i * dr.ngrp) * 64;
@@ -334,6 +373,62 @@ __device__ __forceinline__ void fill_stores(const uint4 (&v)[K], uint8_t* bb, co
         uint4 x = v[j];
         if (dr.swap) x = swap16(x, dr.bpp);
         if (dr.flip) x = flip_msb(x, dr.bpp);
+        if (dr.aligned) {
+            // Rows of whole 16-byte chunks: every lane stores the ALIGNED 16 bytes ending
+            // where its chunk starts + 16 - s (s = q0 mod 16, uniform): the previous lane's
+            // last s bytes (one wave shift) and its own first 16 - s; lane 0 takes the bytes
+            // before the task's first chunk from the previous task (a readlane) or its extra
+            // load (the filter byte 0 in front of a PNG row).  The task's last s bytes are the
+            // next task's lane 0's word (or the word before it, when the filter byte makes
+            // the next row start on a boundary); the buffer's last row writes them itself.
+            // Bytes past nb are zero.
+            uint4 p;
+            p.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.x, 0x138, 0xF, 0xF, false);  // wave_shr:1
+            p.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.y, 0x138, 0xF, 0xF, false);
+            p.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.z, 0x138, 0xF, 0xF, false);
+            p.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.w, 0x138, 0xF, 0xF, false);
+            if (lane == 0) {
+                uint4 y = xlast;
+                if (j == 0) {
+                    y = pv;
+                    if (dr.swap) y = swap16(y, dr.bpp);
+                    if (dr.flip) y = flip_msb(y, dr.bpp);
+                }
+                if (dr.fb && c0 == 0)  // the row above's last 15 bytes, then the filter byte
+                    y = make_uint4((y.x >> 8) | (y.y << 24), (y.y >> 8) | (y.z << 24), (y.z >> 8) | (y.w << 24),
+                                   y.w >> 8);
+                p = y;
+            }
+            const uint32_t sft = (uint32_t)q0 & 15u;
+            const int32_t A = q0 - (int32_t)sft;
+            const uint32_t nct = dr.nc - c0 < 64 ? dr.nc - c0 : 64u;  // chunks of this task
+            auto put = [&](int32_t at, uint4 w) {
+                if (at < 0 || at >= (int32_t)nb) return;
+                if (at + 16 > (int32_t)nb) {  // zero the bytes past the buffer
+                    const uint32_t keep = (uint32_t)((int32_t)nb - at);
+                    uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++) {
+                        const int32_t kb = (int32_t)keep - 4 * (int32_t)q;
+                        const uint32_t nbits = kb <= 0 ? 0u : kb >= 4 ? 32u : 8u * (uint32_t)kb;
+                        ww[q] &= (uint32_t)((1ull << nbits) - 1ull);
+                    }
+                    w = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                }
+                *(uint4*)(bb + at) = w;
+            };
+            if (lane < nct) put(A + 16 * (int32_t)lane, funnel16(p, x, sft));
+            // a PNG row starting on a word boundary: the word before (the row above's last 15
+            // bytes and this row's filter byte) is this lane 0's too
+            if (lane == 0 && dr.fb && c0 == 0 && sft == 0) put(A - 16, p);
+            // the task's tail: the last chunk's last s bytes, when no task follows in the buffer
+            if (lane == nct - 1 && sft && g.ra + i == g.rz && c0 + nct == dr.nc)
+                put(A + 16 * (int32_t)nct, funnel16(x, make_uint4(0, 0, 0, 0), sft));
+            const int ll = (int)nct - 1;
+            xlast = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)x.x, ll), (uint32_t)__builtin_amdgcn_readlane((int)x.y, ll),
+                               (uint32_t)__builtin_amdgcn_readlane((int)x.z, ll), (uint32_t)__builtin_amdgcn_readlane((int)x.w, ll));
+            continue;
+        }
         const uint32_t c = c0 + lane;
         const int32_t dst = q0 + 16 * (int32_t)lane;  // LDS byte of the chunk's first byte
         const bool valid = c < dr.nc;
@@ -357,7 +452,7 @@ __device__ __forceinline__ void fill_issue(FillPre<K>& pf, const DirectRows& dr,
                                            uint32_t tid) {
     const FillGeom g(dr, B, nb);
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (w < g.ntask) fill_loads<NT, K>(pf.v, dr, g, w, tid & 63);
+    if (w * K < g.ntask) fill_loads<NT, K>(pf.v, pf.pv, dr, g, w * K, tid & 63);
 }
 
 template <int NT, uint32_t K>
@@ -368,11 +463,11 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
     const uint32_t lane = tid & 63;
     const FillGeom g(dr, B, nb);
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (w < g.ntask) fill_stores<NT, K>(pf.v, bb, dr, g, B, nb, w, lane);
-    for (uint32_t k0 = w + K * NW; k0 < g.ntask; k0 += K * NW) {  // batches past the prefetched one
-        uint4 v[K];
-        fill_loads<NT, K>(v, dr, g, k0, lane);
-        fill_stores<NT, K>(v, bb, dr, g, B, nb, k0, lane);
+    if (w * K < g.ntask) fill_stores<NT, K>(pf.v, pf.pv, bb, dr, g, B, nb, w * K, lane);
+    for (uint32_t k0 = (w + NW) * K; k0 < g.ntask; k0 += K * NW) {  // batches past the prefetched one
+        uint4 v[K], pv;
+        fill_loads<NT, K>(v, pv, dr, g, k0, lane);
+        fill_stores<NT, K>(v, pv, bb, dr, g, B, nb, k0, lane);
     }
     // zero tail: bytes [nb, round4(nb)) and words up to nz
     const uint32_t nb4 = (nb + 3) & ~3u;
