@@ -351,6 +351,60 @@ def wholeslide_line(svc, rank, world, barrier, steps=2, side=100000, channels=5,
     return line
 
 
+def adaptive_filter_line(svc, rank, world, barrier, side):
+    """PNG with the adaptive per-row filter (cfg.png_filter = ADAPTIVE: k_filter picks
+    None/Sub/Up/Avg/Paeth per row by minimum sum |residual|), on G_NOISE, G_FAKE and a
+    Poisson-like plane: tiles/s (device-resident, like the headline) and bytes per tile
+    against the filter-None path and zlib-6 of the filter-None stream (the reference's
+    ImageIO PNG), the last two on a sample of 8 tiles fetched through the raw path."""
+    import zlib
+    import numpy as np
+    out = {}
+    rng = np.random.default_rng(1234 + rank)
+    ps = 8192  # Poisson-like plane: lambda drifting 200..300 over the plane
+    yy, xx = np.mgrid[0:ps:64, 0:ps:64]
+    lam = 200.0 + 100.0 * (0.5 + 0.25 * np.sin(xx / 900.0) + 0.25 * np.cos(yy / 1300.0))
+    lam = np.repeat(np.repeat(lam, 64, 0), 64, 1)
+    pois = rng.poisson(lam).astype(np.uint16)
+    with pbx.PixelsService(device=torch.cuda.current_device(), png_filter=pbx.FILTER_ADAPTIVE) as sa:
+        for k, (name, gen, sz) in enumerate((("noise", "noise", side), ("fake", "fake", side),
+                                            ("poisson", None, ps))):
+            pid = 40 + k
+            held = []
+            for s_ in (sa, svc):
+                if gen:
+                    held.append((s_, s_.register_plane(pid, 0, 0, 0, pbx.UINT16, sz, sz, generator=gen,
+                                                       plane_no=rank)))
+                else:
+                    held.append((s_, s_.register_plane(pid, 0, 0, 0, pbx.UINT16, sz, sz, data=pois,
+                                                       big_endian=False)))
+            n = (sz // TILE) ** 2
+            ctxs = grid_ctxs(pid, "png", n=min(n, GRID * GRID))
+            dt, st, _ = run_steps(sa, ctxs, 3, 1, barrier)
+            sample = [pbx.TileCtx(pid, 0, 0, 0, (j * 7 % (sz // TILE)) * TILE,
+                                  (j * 5 % (sz // TILE)) * TILE, TILE, TILE) for j in range(8)]
+            raw = [b for _, b in svc.get_tiles(sample)]
+            png_ad = [b for _, b in sa.get_tiles([pbx.TileCtx(c.imageId, 0, 0, 0, c.region["x"], c.region["y"],
+                                                              TILE, TILE, format="png") for c in sample])]
+            png_no = [b for _, b in svc.get_tiles([pbx.TileCtx(c.imageId, 0, 0, 0, c.region["x"], c.region["y"],
+                                                               TILE, TILE, format="png") for c in sample])]
+            z6 = 0
+            for b in raw:  # filter-None scanlines (filter byte 0 + big-endian row), zlib level 6
+                rows = np.frombuffer(b, np.uint8).reshape(TILE, TILE * 2)
+                z6 += len(zlib.compress(np.concatenate([np.zeros((TILE, 1), np.uint8), rows], 1).tobytes(), 6))
+            out[name] = {
+                "tiles_per_s": round(len(ctxs) * 3 * world / dt, 1),
+                "k_filter_ms": round(mean(st, "ms_filter"), 3),
+                "deflate_chain_ms": round(mean(st, "ms_deflate") + mean(st, "ms_assemble"), 3),
+                "sample_bytes_per_tile": {"adaptive": round(sum(map(len, png_ad)) / 8, 1),
+                                          "filter_none": round(sum(map(len, png_no)) / 8, 1),
+                                          "zlib6_filter_none_idat": round(z6 / 8, 1)}}
+            for s_, h in held:
+                s_.release_plane(h)
+    svc.release_cached()
+    return out
+
+
 def extra(out, svc, rank, world, barrier, iid, side):
     """Secondary lines: the other BASELINE configs (parity-tested in tests/), each timed
     device-resident like the headline; and the PCIe-inclusive end-to-end rate."""
@@ -403,6 +457,8 @@ def extra(out, svc, rank, world, barrier, iid, side):
         "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
         "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1),
         "deflate_chain_ms": round(mean(sf, "ms_deflate") + mean(sf, "ms_assemble"), 3)}
+    # the adaptive PNG filter (option; the reference writes filter None)
+    out["png_adaptive_filter_512x512_u16"] = adaptive_filter_line(svc, rank, world, barrier, side)
     # configs[2]: 4096 x 1024^2 uint16 PNG from a 65536^2 plane (8 GiB)
     svc.register_plane(3, 0, 0, 0, pbx.UINT16, 65536, 65536, generator="noise", plane_no=rank)
     c3 = grid_ctxs(3, "png", tile=1024)
