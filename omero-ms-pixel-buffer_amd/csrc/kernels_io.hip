@@ -516,4 +516,195 @@ hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntile
 
 uint32_t filter_band_rows() { return FB_ROWS; }
 
+// ------------------------------------------- K1+K2: PNG filters on 4-byte words
+// PNG tiles with a Sub/Up/Avg/Paeth or adaptive filter and rows of whole dwords (w*bpp % 4
+// == 0, <= F2_MAX_RB bytes; 16-byte aligned source rows): one 256-thread workgroup per
+// band of F2_ROWS rows.
+//   A  the band's rows and the row above, big-endian, into LDS (16-byte loads; 16 zero bytes
+//      before every row: the left neighbours of its first samples)
+//   B  (adaptive) each row's filter: one wave per row, the five sums of |signed residual|
+//      over dwords, four bytes at once (SWAR byte arithmetic; v_sad_u8 on the biased bytes
+//      gives sum |residual| in one instruction; Paeth on packed 16-bit pairs), minimum first
+//   C  every filtered dword of the band into LDS rows laid out as k_rows' staging rows
+//   D  the stream words (filter byte + filtered row), 16-byte aligned, assembled from the
+//      filtered rows with funnel shifts exactly as k_rows does, the filter bytes OR-ed in.
+// Output identical to k_filter's (the same per-row choice; tests compare both to the oracle).
+constexpr uint32_t F2_ROWS = 16;
+constexpr uint32_t F2_NT = 256;
+constexpr uint32_t F2_MAX_RB = 2048;
+
+__device__ __forceinline__ uint32_t sub8(uint32_t a, uint32_t b) {  // bytewise a - b mod 256
+    return ((a | 0x80808080u) - (b & 0x7F7F7F7Fu)) ^ ((a ^ ~b) & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t avg8(uint32_t a, uint32_t b) {  // bytewise floor((a + b) / 2)
+    return (a & b) + (((a ^ b) >> 1) & 0x7F7F7F7Fu);
+}
+typedef short f2_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2_s16x2 f2_abs(f2_s16x2 x) {
+    const f2_s16x2 m = x >> 15;
+    return (x ^ m) - m;
+}
+// PNG Paeth predictor of two 16-bit lanes holding bytes (a = left, b = up, c = up-left)
+__device__ __forceinline__ uint32_t paeth_pair(uint32_t a, uint32_t b, uint32_t c) {
+    const f2_s16x2 A = __builtin_bit_cast(f2_s16x2, a), B = __builtin_bit_cast(f2_s16x2, b),
+                   Cc = __builtin_bit_cast(f2_s16x2, c);
+    const f2_s16x2 pa = f2_abs(B - Cc), pb = f2_abs(A - Cc), pc = f2_abs(A + B - Cc - Cc);
+    const f2_s16x2 m1 = (pa <= pb) & (pa <= pc), m2 = pb <= pc;  // -1 / 0 per lane
+    const f2_s16x2 r = (m1 & A) | (~m1 & ((m2 & B) | (~m2 & Cc)));
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t paeth4(uint32_t l, uint32_t u, uint32_t ul) {
+    const uint32_t lo = paeth_pair(l & 0x00FF00FFu, u & 0x00FF00FFu, ul & 0x00FF00FFu);
+    const uint32_t hi = paeth_pair((l >> 8) & 0x00FF00FFu, (u >> 8) & 0x00FF00FFu, (ul >> 8) & 0x00FF00FFu);
+    return lo | (hi << 8);
+}
+// the bytes bpp before each byte of word k: from words k and k-1 (k-2 for 8-byte samples)
+__device__ __forceinline__ uint32_t back_bytes(const uint32_t* row, int32_t k, uint32_t bpp) {
+    if (bpp >= 4) return row[k - (int32_t)(bpp >> 2)];
+    return __builtin_amdgcn_alignbyte(row[k], row[k - 1], 4 - bpp);
+}
+__device__ __forceinline__ uint32_t filt_word(uint32_t ft, uint32_t cur, uint32_t left, uint32_t up, uint32_t ul) {
+    switch (ft) {
+    case 0: return cur;
+    case 1: return sub8(cur, left);
+    case 2: return sub8(cur, up);
+    case 3: return sub8(cur, avg8(left, up));
+    default: return sub8(cur, paeth4(left, up, ul));
+    }
+}
+
+size_t filter2_lds_bytes(uint32_t max_rb) {
+    const uint32_t rbq = (max_rb + 15) & ~15u;
+    return (size_t)(F2_ROWS + 1) * (rbq + 32) + 16 + (size_t)F2_ROWS * (rbq + 16) + 64;
+}
+
+__global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                  uint32_t rbq_max, uint8_t* __restrict__ stream) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const TileDesc d = dt[ti];
+    const uint32_t r0 = (b - d.blk_first) * F2_ROWS;
+    const uint32_t nr = (uint32_t)d.h - r0 < F2_ROWS ? (uint32_t)d.h - r0 : F2_ROWS;
+    const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp, nw = rb >> 2;
+    const uint32_t nc = (rb + 15) >> 4, sst = rbq_max + 32;
+    uint8_t* SA = sm;                                         // staged rows, slot q at SA + q*sst
+    uint32_t* FR = (uint32_t*)(sm + (F2_ROWS + 1) * sst + 16);  // filtered rows (k_rows layout)
+    const uint32_t rw = 4 * nc + 4;
+    uint32_t* ftype = (uint32_t*)(sm + (F2_ROWS + 1) * sst + 16 + F2_ROWS * (rbq_max + 16));
+    const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
+    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
+    // A: rows r0-1 .. r0+nr-1 (zeros above the tile)
+    for (uint32_t i = tid; i < (nr + 1) * nc; i += F2_NT) {
+        const uint32_t q = i / nc, c = i - q * nc;
+        const int64_t row = (int64_t)r0 - 1 + q;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (row >= 0) {
+            v = gload16(src0 + row * d.pitch + 16 * c);
+            if (swap) v = swap16(v, (int)bpp);
+            if (flip) v = flip_msb(v, (int)bpp);
+        }
+        *(uint4*)(SA + q * sst + 16 + 16 * c) = v;
+    }
+    for (uint32_t q = tid; q < nr + 1; q += F2_NT) *(uint4*)(SA + q * sst) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    // B: the adaptive choice, one wave per row
+    if (d.filter == 5) {
+        for (uint32_t q = 1 + wv; q <= nr; q += F2_NT / 64) {
+            const uint32_t* L = (const uint32_t*)(SA + q * sst + 16);
+            const uint32_t* U = (const uint32_t*)(SA + (q - 1) * sst + 16);
+            uint32_t s[5] = {0, 0, 0, 0, 0};
+            constexpr uint32_t M = 0x80808080u;
+            for (uint32_t k = lane; k < nw; k += 64) {
+                const uint32_t cur = L[k], up = U[k];
+                const uint32_t left = back_bytes(L, (int32_t)k, bpp), ul = back_bytes(U, (int32_t)k, bpp);
+                s[0] = __builtin_amdgcn_sad_u8(cur ^ M, M, s[0]);
+                s[1] = __builtin_amdgcn_sad_u8(sub8(cur, left) ^ M, M, s[1]);
+                s[2] = __builtin_amdgcn_sad_u8(sub8(cur, up) ^ M, M, s[2]);
+                s[3] = __builtin_amdgcn_sad_u8(sub8(cur, avg8(left, up)) ^ M, M, s[3]);
+                s[4] = __builtin_amdgcn_sad_u8(sub8(cur, paeth4(left, up, ul)) ^ M, M, s[4]);
+            }
+#pragma unroll
+            for (int f = 0; f < 5; f++)
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) s[f] += __shfl_xor(s[f], off, 64);
+            if (lane == 0) {
+                uint32_t best = 0;
+                for (uint32_t f = 1; f < 5; f++) if (s[f] < s[best]) best = f;
+                ftype[q - 1] = best;
+            }
+        }
+        __syncthreads();
+    }
+    // C: filtered dwords of every row
+    for (uint32_t i = tid; i < nr * nw; i += F2_NT) {
+        const uint32_t q = i / nw, k = i - q * nw;
+        const uint32_t* L = (const uint32_t*)(SA + (q + 1) * sst + 16);
+        const uint32_t* U = (const uint32_t*)(SA + q * sst + 16);
+        const uint32_t ft = d.filter == 5 ? ftype[q] : (uint32_t)d.filter;
+        FR[4 + q * rw + k] = filt_word(ft, L[k], back_bytes(L, (int32_t)k, bpp), U[k], back_bytes(U, (int32_t)k, bpp));
+    }
+    __syncthreads();
+    // D: the band's stream words (k_rows' assembly, filter bytes OR-ed in)
+    const uint32_t rowlen = d.rowlen;
+    const uint32_t o0 = r0 * rowlen, nb = nr * rowlen, nwo = (nb + 15) >> 4;
+    const uint32_t magic = 0xFFFFFFFFu / rowlen;
+    uint8_t* out = stream + d.out_off + o0;
+    const uint32_t* rows = FR + 4;
+    for (uint32_t kk = tid; kk < nwo; kk += F2_NT) {
+        const uint32_t o = kk << 4;
+        uint32_t r = __umulhi(o, magic);
+        if ((r + 1) * rowlen <= o) r++;
+        const uint32_t c = o - r * rowlen;
+        const int32_t s = (int32_t)c - 1;  // data byte of row r at word byte 0
+        const uint32_t* rp = rows + r * rw;
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) w[i] = lds_word4(rp, s, i);
+        const int32_t k1 = (int32_t)rowlen - (int32_t)c;  // bytes of row r in this word
+        const int32_t end = (int32_t)(nb - o) < 16 ? (int32_t)(nb - o) : 16;
+        const bool nxt = k1 < end && r + 1 < nr;
+        if (s < 0 || k1 < 16 || o + 16 > nb) {
+            const uint32_t* rq = rows + (r + 1) * rw;
+            const int32_t s2 = s - (int32_t)rowlen;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t m1 = byte_mask(c == 0 ? 1 : 0, k1 < end ? k1 : end, i);
+                uint32_t v = w[i] & m1;
+                if (nxt) v |= lds_word4(rq, s2, i) & byte_mask(k1 + 1, end, i);
+                w[i] = v;
+            }
+        }
+        if (c == 0) w[0] |= d.filter == 5 ? ftype[r] : (uint32_t)d.filter;
+        if (nxt) w[k1 >> 2] |= (d.filter == 5 ? ftype[r + 1] : (uint32_t)d.filter) << (8 * (k1 & 3));
+        *(uint4*)(out + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+hipError_t launch_filter2(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nblocks,
+                          uint32_t max_rb, uint8_t* stream) {
+    if (!ntiles || !nblocks) return hipSuccess;
+    const size_t lds = filter2_lds_bytes(max_rb);
+    if (lds > 64 * 1024) {
+        constexpr int kMaxDev = 64;
+        static std::once_flag once[kMaxDev];
+        static hipError_t res[kMaxDev];
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+        std::call_once(once[dev], [&] {
+            res[dev] = hipFuncSetAttribute((const void*)k_filter2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        });
+        if (res[dev] != hipSuccess) return res[dev];
+    }
+    hipLaunchKernelGGL(k_filter2, dim3(nblocks), dim3(F2_NT), lds, st, d_tiles, ntiles,
+                       (max_rb + 15) & ~15u, stream);
+    return hipGetLastError();
+}
+
+uint32_t filter2_band_rows() { return F2_ROWS; }
+uint32_t filter2_max_rb() { return F2_MAX_RB; }
+
 }  // namespace pbx

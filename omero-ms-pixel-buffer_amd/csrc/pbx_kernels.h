@@ -31,6 +31,12 @@ hipError_t launch_tiff_tiled(hipStream_t st, const TiledHdr* d_th, uint32_t nth,
 hipError_t launch_filter(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                          uint32_t nblocks, uint8_t* stream);
 uint32_t filter_band_rows();
+// PNG tiles with a Sub/Up/Avg/Paeth/adaptive filter and rows of whole dwords (<= 2 KiB,
+// 16-byte aligned source): the same streams from dword-wide filter arithmetic (k_filter2).
+hipError_t launch_filter2(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nblocks,
+                          uint32_t max_rb, uint8_t* stream);
+uint32_t filter2_band_rows();
+uint32_t filter2_max_rb();
 
 // K1+K2 for filter-None PNG rows and deflate-TIFF rows from 16-byte-aligned source rows:
 // one workgroup per band of ROWS_BAND rows, staged in LDS, aligned 16-byte stream words.

@@ -183,8 +183,9 @@ struct pbx_batch {
     std::vector<TiledHdr> th;              // tiled-TIFF responses (their sub-tiles carry TF_TILED)
     std::vector<uint32_t> th_req;
     uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
-    // dt = [direct tiles | k_rows tiles | k_filter tiles]
+    // dt = [direct tiles | k_rows tiles | k_filter2 tiles | k_filter tiles | tiled-TIFF sub-tiles]
     uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
+    uint32_t nfilt2_tiles = 0, filt2_blocks = 0, filt2_max_rb = 0;  // k_filter2 group
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -1145,8 +1146,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     const int32_t tiff_tile = ctx->cfg.tiff_tile;
     // deflate sub-tiles of a tiled TIFF stay consecutive (one response = one run of the
     // deflate arena): they go to k_filter, after the other banded tiles
-    std::vector<TileDesc> dt_direct, dt_rows, dt_band, dt_tiled;
-    std::vector<uint32_t> req_direct, req_rows, req_band, req_tiled;
+    std::vector<TileDesc> dt_direct, dt_rows, dt_filt2, dt_band, dt_tiled;
+    std::vector<uint32_t> req_direct, req_rows, req_filt2, req_band, req_tiled;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane pl;
@@ -1253,10 +1254,16 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             const uint32_t rb = (uint32_t)w * bpp;
             const bool rows_ok = d.filter == 0 && d.rowlen >= 32 && rb <= ROWS_MAX_RB &&
                                  ((uint64_t)d.x * bpp % 16) == 0;
+            // filtered PNG rows of whole dwords: dword-wide filter arithmetic (k_filter2)
+            const bool filt2_ok = (d.flags & TF_PNGROWS) && d.filter != 0 && rb % 4 == 0 && rb >= 16 &&
+                                  rb <= filter2_max_rb() && ((uint64_t)d.x * bpp % 16) == 0;
             if (rows_ok && bpp <= 4 && !ctx->cfg.stage_rows) {
                 d.flags |= TF_DIRECT;
                 dt_direct.push_back(d);
                 req_direct.push_back((uint32_t)i);
+            } else if (filt2_ok) {
+                dt_filt2.push_back(d);
+                req_filt2.push_back((uint32_t)i);
             } else {
                 (rows_ok ? dt_rows : dt_band).push_back(d);
                 (rows_ok ? req_rows : req_band).push_back((uint32_t)i);
@@ -1267,10 +1274,13 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->nrows_tiles = (uint32_t)dt_rows.size();
     b->dt = std::move(dt_direct);
     b->dt.insert(b->dt.end(), dt_rows.begin(), dt_rows.end());
+    b->nfilt2_tiles = (uint32_t)dt_filt2.size();
+    b->dt.insert(b->dt.end(), dt_filt2.begin(), dt_filt2.end());
     b->dt.insert(b->dt.end(), dt_band.begin(), dt_band.end());
     b->dt.insert(b->dt.end(), dt_tiled.begin(), dt_tiled.end());
     b->dt_req = std::move(req_direct);
     b->dt_req.insert(b->dt_req.end(), req_rows.begin(), req_rows.end());
+    b->dt_req.insert(b->dt_req.end(), req_filt2.begin(), req_filt2.end());
     b->dt_req.insert(b->dt_req.end(), req_band.begin(), req_band.end());
     b->dt_req.insert(b->dt_req.end(), req_tiled.begin(), req_tiled.end());
     const uint32_t tiled0 = (uint32_t)(b->dt.size() - dt_tiled.size());
@@ -1293,6 +1303,10 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.blk_first = b->rows_blocks;
             b->rows_blocks += rows_blocks_for((uint32_t)d.h);
             b->rows_max_rb = std::max<uint32_t>(b->rows_max_rb, d.rowlen - ((d.flags & TF_PNGROWS) ? 1u : 0u));
+        } else if (k < b->ndirect_tiles + b->nrows_tiles + b->nfilt2_tiles) {
+            d.blk_first = b->filt2_blocks;
+            b->filt2_blocks += (uint32_t)((d.h + filter2_band_rows() - 1) / filter2_band_rows());
+            b->filt2_max_rb = std::max<uint32_t>(b->filt2_max_rb, d.rowlen - 1);
         } else {
             d.blk_first = b->filt_blocks;
             b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
@@ -1345,8 +1359,11 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     HIP_TRY(hipEventRecord(b->ev[2], st));
     const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;
     HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
-    HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles, ndt - b->ndirect_tiles - b->nrows_tiles,
-                          b->filt_blocks, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
+                           (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles + b->nfilt2_tiles,
+                          ndt - b->ndirect_tiles - b->nrows_tiles - b->nfilt2_tiles, b->filt_blocks,
+                          (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;

@@ -339,3 +339,29 @@ def test_tiff_deflate_segment_capacity(adaptive_service):
     assert blks[0].btype == 0
     assert body[160:] == z
     assert zlib.decompress(body[160:]) == data
+
+
+@pytest.mark.parametrize("filt", [pbx.FILTER_SUB, pbx.FILTER_UP, pbx.FILTER_AVG, pbx.FILTER_PAETH,
+                                  pbx.FILTER_ADAPTIVE])
+def test_png_filters_dword_path(oracle, filt):
+    """Filtered PNG rows of whole dwords from aligned source rows go through k_filter2 (SWAR
+    filter arithmetic); the inflated IDAT must equal the oracle's filtered scanlines (the
+    adaptive choice included) for every PNG type, down to 16-byte and up to 2 KiB rows."""
+    with pbx.PixelsService(png_filter=filt) as svc:
+        for pt in PNG_TYPES:
+            bpp = oracle.BPP[pt]
+            sx, sy = 2600 // bpp, 90
+            iid = next(_ids)
+            plane = oracle.gen_region(2, pt, 0, 0, sx, sy)
+            svc.register_plane(iid, 0, 0, 0, pt, sx, sy, data=plane, big_endian=True)
+            regions = [(0, 0, 512 // bpp, 40), (16 // bpp, 3, 64 // bpp, 37), (0, 0, 16 // bpp, 5),
+                       (32 // bpp, 1, 2048 // bpp, 17), (0, 7, 1024 // bpp, 1)]
+            res = svc.get_tiles([pbx.TileCtx(iid, 0, 0, 0, *r, format="png") for r in regions])
+            for (x, y, w, h), (st, body) in zip(regions, res):
+                assert st == pbx.OK
+                tile = oracle_tile(oracle, plane, pt, sx, x, y, w, h)
+                r, px, _ = oracle.png_decode(body)
+                assert r == 0 and px == flip_png(tile, pt), (pt, x, y, w, h)
+                stream = oracle.png_filter_stream(np.frombuffer(tile, np.uint8), pt, w, h, filt).tobytes()
+                r, idat = oracle.png_inflate_idat(body, len(stream))
+                assert idat == stream, (pt, x, y, w, h)
