@@ -318,7 +318,14 @@ __device__ __forceinline__ void fill_loads(uint4 (&v)[K], uint4& pv, const Direc
         const uint32_t i = dr.ngrp == 1 ? k : k / dr.ngrp;
         const uint32_t c0 = (k - i * dr.ngrp) * 64;
         const uint8_t* rp = dr.row0 + (int64_t)(g.ra + i) * dr.pitch + 16 * c0;
+#ifdef PBX_LZ_FAKE_LOAD  // timing experiment only (scripts/variants.sh): hashed bytes, no plane reads
+        {
+            const uint64_t h = splitmix64((uint64_t)(uintptr_t)(rp + 16 * lane));
+            v[j] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(h * 3), (uint32_t)(h >> 17));
+        }
+#else
         v[j] = gload16(rp + 16 * (c0 + lane < dr.nc ? lane : 0u));
+#endif
         if (j == 0 && dr.aligned) {  // lane 0: the chunk before (previous group, or the row above's last)
             pv = make_uint4(0, 0, 0, 0);
             if (lane == 0 && (c0 > 0 || g.ra + i > 0))
@@ -1478,8 +1485,10 @@ constexpr uint32_t SLOT_NONE = 288;
 // Same tokens as walk_tokens (deflate_seg.h) over the same match lists.  Literals first,
 // branch-free: covered positions read the empty slot; then the (few) matches starting in
 // the chunk overwrite their three slots.
+// Returns true (wave-uniform) when the wave's slots are literals only (no match, full
+// chunks): slots 32 and 33 are then empty and every slot holds <= 15 bits.
 template <class C, class SM>
-__device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const SegParams& sp,
+__device__ __forceinline__ bool build_slots(uint32_t tid, const SM& S, const SegParams& sp,
                                             const uint32_t (&cb)[C::CH / 4],
                                             uint32_t (&slot)[C::CH + 2]) {
     const uint32_t cs = tid * C::CH;
@@ -1512,7 +1521,7 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
         for (int i = 0; i < C::CH; i++) slot[i] = S.lcode[(cb[i >> 2] >> ((i & 3) * 8)) & 0xFFu];
         slot[C::CH] = 0;
         slot[C::CH + 1] = 0;
-        return;
+        return true;
     }
     // the first match starting in the chunk goes in with the literals, branch-free; any
     // further ones (several short matches in 32 bytes) are patched in after
@@ -1554,6 +1563,7 @@ __device__ __forceinline__ void build_slots(uint32_t tid, const SM& S, const Seg
             slot[j] = dj == 0 ? A : dj == 1 ? B : dj == 2 ? Cx : slot[j];
         }
     }
+    return false;
 }
 
 // One segment's part of its block: the header (first segment), its tokens, and the end of
@@ -1682,10 +1692,11 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     stamp();  // diagnostics: inputs in LDS
     uint32_t slot[C::CH + 2];
     uint32_t nbits = 0;
+    bool lit_only = false;
     if (!stored) {
-        build_slots<C>(tid, S, sp, cb, slot);
+        lit_only = build_slots<C>(tid, S, sp, cb, slot);
 #pragma unroll
-        for (int i = 0; i < C::CH + 2; i++) nbits += slot[i] >> 27;
+        for (int i = 0; i < C::CH + 2; i += 2) nbits += (slot[i] >> 27) + (slot[i + 1] >> 27);
     }
     // the slicing tables (needed after barrier 3): loaded now, stored before barrier 2
     if (tid < 256) ((uint4*)&S.crc_t[0][0])[tid] = ((const uint4*)&kCrcTables.t[0][0])[tid];
@@ -1729,8 +1740,16 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         }
         const uint32_t tb = SH + lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
         LdsRunWriter bw(S.out, tb + pre + inc - nbits);
+        if (lit_only) {  // literal codes (<= 15 bits) put in pairs: half the puts
 #pragma unroll
-        for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
+            for (int i = 0; i < C::CH; i += 2) {
+                const uint32_t n0 = slot[i] >> 27;
+                bw.put((slot[i] & 0x7FFFFFFu) | ((slot[i + 1] & 0x7FFFFFFu) << n0), n0 + (slot[i + 1] >> 27));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < C::CH + 2; i++) bw.put(slot[i] & 0x7FFFFFFu, slot[i] >> 27);
+        }
         bw.finish();
         if (lastb && tid == 0) {  // end of block; a non-final block ends byte-aligned
             const uint32_t eob = S.lcode[256];
