@@ -20,12 +20,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "dev_util.h"
 #include "pbx_common.h"
 #include "pbx_kernels.h"
 #include "zarr_dev.h"
 
 namespace pbx {
+
+constexpr uint32_t ZL_BYTES = ZR_LZ4 + ZWIN + 64;  // LZ4 / BloscLZ per wave: ring, window, trash
 
 // ------------------------------------------------------------------------------ LZ4
 __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st, uint32_t n,
@@ -36,10 +40,10 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
     if (si >= n) return;
     const ZStream t = st[si];
     const uint32_t ilen = rfl(t.csize);
-    const uint32_t wb = w * (ZR_LZ4 + ZWIN);
+    const uint32_t wb = w * ZL_BYTES;
     InWin win{src + t.src_off, wb + ZR_LZ4, 0, lane};
     win.load(0);
-    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZR_LZ4 + ZWIN};
 #ifdef PBX_ZARR_CLOCKS  // diagnostic build: shader clocks and real time of stream 0
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     uint32_t nseq = 0;
@@ -66,7 +70,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
                 if (ll0) {
                     const uint32_t bsel = 1 + lane, ws = bsel >> 2;
                     const uint32_t wv = ws == 0 ? h[0] : ws == 1 ? h[1] : ws == 2 ? h[2] : h[3];
-                    if (lane < ll0) o.ring(o.op + lane) = (uint8_t)(wv >> ((bsel & 3) * 8));
+                    o.put_if(lane < ll0, o.op + lane, (wv >> ((bsel & 3) * 8)));
                     o.op += ll0;  // flushed with the match below (the ring has room)
                 }
                 const uint32_t off = hb(1 + ll0) | hb(2 + ll0) << 8, len = ml0 + 4;
@@ -75,7 +79,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
                     const uint32_t rep = o.period_lane(off);
                     const uint32_t v = o.ring(o.op - off + rep);
                     win.peek16(ip, h);
-                    if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
+                    o.put_if(lane < len, o.op + lane, v);
                     o.op += len;
                     o.flush(o.op);
                 } else {
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
         for (uint32_t c = 0; c < ll; c += 64) {
             const uint32_t nb = ll - c < 64 ? ll - c : 64;
             const uint32_t v = win.lane_byte(ls + c);
-            if (lane < nb) o.ring(o.op + c + lane) = (uint8_t)v;
+            o.put_if(lane < nb, o.op + c + lane, v);
             o.flush(o.op + c + nb);
         }
         o.op += ll;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
             const uint32_t rep = o.period_lane(off);
             const uint32_t v = o.ring(o.op - off + rep);
             win.peek16(ip, h);
-            if (lane < len) o.ring(o.op + lane) = (uint8_t)v;
+            o.put_if(lane < len, o.op + lane, v);
             o.op += len;
             o.flush(o.op);
         } else {
@@ -162,10 +166,10 @@ __global__ __launch_bounds__(256) void k_zarr_blosclz(const ZStream* __restrict_
     if (si >= n) return;
     const ZStream t = st[si];
     const uint32_t ilen = rfl(t.csize);
-    const uint32_t wb = w * (ZR_LZ4 + ZWIN);
+    const uint32_t wb = w * ZL_BYTES;
     InWin win{src + t.src_off, wb + ZR_LZ4, 0, lane};
     win.load(0);
-    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZR_LZ4 + ZWIN};
     uint32_t ip = 0, bad = ilen == 0 ? 1u : 0u;
     uint32_t ctrl = bad ? 0u : win.byte(ip++) & 31u;
     while (!bad) {
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(256) void k_zarr_blosclz(const ZStream* __restrict_
             const uint32_t nl = ctrl + 1;  // <= 32 literals: one lane step
             if (nl > o.olen - o.op || ip + nl > ilen) { bad = 7; break; }
             const uint32_t v = win.lane_byte(ip);
-            if (lane < nl) o.ring(o.op + lane) = (uint8_t)v;
+            o.put_if(lane < nl, o.op + lane, v);
             o.op += nl;
             o.flush(o.op);
             ip += nl;
@@ -231,6 +235,11 @@ struct BitIn {
     uint64_t buf;
     uint32_t cnt, ipos, ilen;
     __device__ void refill() {
+        // the bit-stream state is wave-uniform: pin it to SGPRs (LLVM otherwise moves it to
+        // VGPRs through a phi and turns every branch on it into exec-mask code)
+        cnt = rfl(cnt);
+        ipos = rfl(ipos);
+        buf = (uint64_t)rfl((uint32_t)(buf >> 32)) << 32 | rfl((uint32_t)buf);
         if (cnt <= 32) {
             // past the stream's end (corrupt input) feed zeros instead of reading on: the
             // decoder stops at the output bound and the consumed-bytes check fails the stream
@@ -290,9 +299,10 @@ __device__ bool build_table(HTab& h, uint32_t lens /* LDS offset */, uint32_t n,
     return !over;
 }
 
-// Decode one symbol (the bit buffer holds >= 15 bits); returns -1 on an invalid code.
-__device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
-    const uint32_t rev = __builtin_bitreverse32((uint32_t)bi.buf & 0x7fffu) >> 17;  // 15 bits, MSB-first
+// Canonical decode of the code in the low bits of `bits` (>= 15 valid bits): the symbol, and
+// its length in nb; -1 on an invalid code.
+__device__ __forceinline__ int decode_bits(const HTab& h, uint32_t bits, uint32_t lane, uint32_t& nb) {
+    const uint32_t rev = __builtin_bitreverse32(bits & 0x7fffu) >> 17;  // 15 bits, MSB-first
     const uint32_t L = lane + 1;
     const uint32_t code = L <= 15 ? rev >> (15 - L) : 0;
     const bool ok = L <= 15 && (code - h.first) < h.count;
@@ -300,14 +310,22 @@ __device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
     if (!m) return -1;
     const uint32_t l = (uint32_t)__builtin_ctzll(m);
     const uint32_t idx = rdl(h.offs + code - h.first, l);
-    bi.bits(l + 1);
+    nb = l + 1;
     return (int)rfl(lds16(h.syms + 2 * idx));
+}
+// Decode one symbol (the bit buffer holds >= 15 bits); returns -1 on an invalid code.
+__device__ int decode_sym(const HTab& h, BitIn& bi, uint32_t lane) {
+    uint32_t nb = 0;
+    const int sym = decode_bits(h, (uint32_t)bi.buf, lane, nb);
+    if (sym >= 0) bi.bits(nb);
+    return sym;
 }
 
 // First-level table of a built code: lut[next 9 stream bits] = sym | len << 9 for codes of
 // <= 9 bits (every extension of the bit-reversed code), 0xFFFF (-> decode_sym) otherwise.
+template <uint32_t LB = ZLUT>
 __device__ void build_lut(const HTab& h, uint32_t lens, uint32_t lut, uint32_t lane) {
-    for (uint32_t e = lane; e < (1u << ZLUT); e += 64) lds16(lut + 2 * e) = 0xFFFF;
+    for (uint32_t e = lane; e < (1u << LB); e += 64) lds16(lut + 2 * e) = 0xFFFF;
     __builtin_amdgcn_wave_barrier();
     const uint32_t total = rdl(h.offs + h.count, 14);  // symbols with a code
     for (uint32_t g = 0; g < total; g += 64) {  // uniform trip count: the shuffles see all lanes
@@ -317,9 +335,9 @@ __device__ void build_lut(const HTab& h, uint32_t lens, uint32_t lut, uint32_t l
         const uint32_t src = len ? len - 1 : 0;
         const uint32_t first = (uint32_t)__shfl((int)h.first, (int)src, 64);
         const uint32_t offs = (uint32_t)__shfl((int)h.offs, (int)src, 64);
-        if (len == 0 || len > ZLUT) continue;
+        if (len == 0 || len > LB) continue;
         const uint32_t rev = __builtin_bitreverse32(first + (j - offs)) >> (32 - len);
-        for (uint32_t k = 0; k < (1u << (ZLUT - len)); k++)
+        for (uint32_t k = 0; k < (1u << (LB - len)); k++)
             lds16(lut + 2 * (rev | (k << len))) = (uint16_t)(sym | len << 9);
     }
     __builtin_amdgcn_wave_barrier();
@@ -351,7 +369,7 @@ constexpr uint32_t ZLENS = 352;
 constexpr uint32_t ZI_RING = 0, ZI_LSYMS = ZR_INF, ZI_DSYMS = ZI_LSYMS + 2 * 288,
                    ZI_LENS = ZI_DSYMS + 2 * 32, ZI_NEXT = ZI_LENS + ZLENS,
                    ZI_LLUT = ZI_NEXT + 64, ZI_DLUT = ZI_LLUT + 2 * (1u << ZLUT),
-                   ZI_BYTES = ZI_DLUT + 2 * (1u << ZLUT);
+                   ZI_TRASH = ZI_DLUT + 2 * (1u << ZLUT), ZI_BYTES = ZI_TRASH + 64;
 
 __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict__ st, uint32_t n,
                                                       const uint8_t* __restrict__ src,
@@ -364,7 +382,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
     const ZStream t = st[si];
     BitIn bi{{src + t.src_off, wb + ZI_BYTES, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
     bi.win.load(0);
-    OutRing<ZR_INF> o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<ZR_INF> o{wb + ZI_RING, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZI_TRASH};
     HTab lt{0, 0, 0, wb + ZI_LSYMS}, dt{0, 0, 0, wb + ZI_DSYMS};
     uint32_t bad = 0;
     bi.refill();
@@ -394,7 +412,7 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
             for (uint32_t k = 0; k < rest; k += 64) {
                 const uint32_t nb = rest - k < 64 ? rest - k : 64;
                 const uint32_t v = bi.win.lane_byte(q + k);
-                if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+                o.put_if(lane < nb, o.op + k + lane, v);
                 o.flush(o.op + k + nb);
             }
             o.op += rest;
@@ -504,6 +522,396 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
     if (!bad && o.op != o.olen) bad = 27;
     o.finish();
     if (lane == 0) err[si] = bad;
+}
+
+// ------------------------------------------------------------ inflate, two-wave pipeline
+// One zlib stream is one serial symbol chain, and a plane of 512^2 chunks gives only one
+// stream per SIMD: the single-wave decoder above is bound by the latency of that chain
+// (Huffman lookup -> bits consumed -> next lookup, plus the match copies).  Here each stream
+// gets TWO waves of one workgroup, a pipeline through an LDS token FIFO:
+//   producer  the bit stream: block headers and code tables as above, then the symbols.
+//             Per refill it gathers the literal/length and distance first-level table entries
+//             at EVERY bit offset of the 64-bit buffer in one LDS round trip (lane k: the
+//             entries for the bits from offset k), then walks literals and whole matches
+//             (length, its extra bits, distance code, its extra bits) by readlanes until the
+//             buffer runs short; codes of more than 9 bits take the table path.  Tokens go to
+//             a VGPR (lane n holds token n) and to the FIFO 64 at a time.
+//   consumer  the output: 64 tokens per round (one read per lane); a run of literals is
+//             written by as many lanes at once, a match is the ring copy of the single-wave
+//             decoder; the ring flushes to HBM as it fills.
+// Tokens: literal 0x01000000 | byte; match 0x40000000 | (len - 3) << 16 | (dist - 1);
+// stored run 0x80000000 | len, then the run's input offset; end 0xC0000000 | error code.
+constexpr uint32_t ZP_TOKQ = 256;                   // FIFO tokens per stream (power of two)
+constexpr uint32_t ZPLUT = 10;                      // producer's first-level tables: codes <= 10 bits
+constexpr uint32_t ZP_WIN = 0, ZP_LLUT = ZWIN, ZP_DLUT = ZP_LLUT + 2 * (1u << ZPLUT),
+                   ZP_LSYMS = ZP_DLUT + 2 * (1u << ZPLUT), ZP_DSYMS = ZP_LSYMS + 2 * 288,
+                   ZP_LENS = ZP_DSYMS + 2 * 32, ZP_NEXT = ZP_LENS + ZLENS, ZP_FIFO = ZP_NEXT + 64,
+                   ZP_RING = ZP_FIFO + 4 * ZP_TOKQ, ZP_CTRL = ZP_RING + ZR_INF,
+                   ZP_TRASH = ZP_CTRL + 16,         // 4 bytes per lane: masked-off lanes' stores
+                   ZP_FLAG = ZP_TRASH + 256 + 64,   // the consumer's token-start flags (+ trash)
+                   ZP_BYTES = ZP_FLAG + 128;        // per stream
+static_assert(ZP_BYTES <= 160 * 1024 / 4, "four streams (eight waves) per CU");
+constexpr uint32_t ZP_STREAMS = 1;                  // streams (x 2 waves) per workgroup
+enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8 };
+
+__device__ __forceinline__ uint32_t zp_lext(uint32_t ls) { return ls < 8 || ls == 28 ? 0u : (ls - 4) >> 2; }
+__device__ __forceinline__ uint32_t zp_lbase(uint32_t ls) {
+    return ls < 8 ? 3 + ls : ls == 28 ? 258u : ((4 + (ls & 3)) << ((ls >> 2) - 1)) + 3;
+}
+__device__ __forceinline__ uint32_t zp_dext(uint32_t ds) { return ds < 4 ? 0u : (ds >> 1) - 1; }
+__device__ __forceinline__ uint32_t zp_dbase(uint32_t ds) {
+    return ds < 4 ? ds + 1 : ((2 + (ds & 1)) << ((ds >> 1) - 1)) + 1;
+}
+// The FIFO control words.  Both waves' LDS operations complete in issue order, so a plain
+// (volatile, LDS-typed) store of `tail` after the token stores publishes them; no memory
+// fence (a workgroup fence would also wait for every outstanding HBM store of the consumer).
+typedef volatile __attribute__((address_space(3))) uint32_t lds_vu32_t;
+__device__ __forceinline__ uint32_t lds_load_volatile(uint32_t off) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t v = rfl(*(lds_vu32_t*)(zlds + off));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return v;
+}
+__device__ __forceinline__ void lds_store_volatile(uint32_t off, uint32_t v) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    *(lds_vu32_t*)(zlds + off) = v;  // every lane: the same word
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+struct TokOut {  // the producer's side of the FIFO
+    uint32_t tail, head, sb, lane;
+    __device__ bool room(uint32_t k) {  // false if the consumer aborted
+        while (tail + k - head > ZP_TOKQ) {
+            head = lds_load_volatile(sb + ZP_CTRL + ZPC_HEAD);
+            if (tail + k - head <= ZP_TOKQ) break;
+            if (lds_load_volatile(sb + ZP_CTRL + ZPC_ABORT)) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return true;
+    }
+    // the tokens of the lanes in m, in lane order (stores without a lane branch: a divergent
+    // branch anywhere in the symbol loop makes LLVM structurize it with exec masks)
+    __device__ bool put_lanes(uint64_t m, uint32_t tok) {
+        const uint32_t nt = (uint32_t)__popcll(m);
+        if (!nt) return true;
+        if (!room(nt)) return false;
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        lds32((m >> lane) & 1 ? sb + ZP_FIFO + 4 * ((tail + rank) & (ZP_TOKQ - 1)) : sb + ZP_TRASH + 4 * lane) = tok;
+        tail += nt;
+        lds_store_volatile(sb + ZP_CTRL + ZPC_TAIL, tail);
+        return true;
+    }
+    __device__ bool put(uint32_t tok) { return put_lanes(1ull, tok); }
+};
+
+#ifdef PBX_ZARR_DIAG  // diagnostic build only: per-stream clocks and token counts (printf, stream 0)
+#define ZDIAG(...) __VA_ARGS__
+#else
+#define ZDIAG(...)
+#endif
+// Per-lane decode kinds of the lane-parallel round
+enum : uint32_t { ZK_TOK = 0, ZK_EOB = 1, ZK_SLOW = 2, ZK_BAD = 3 };
+
+__device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src, uint32_t sb, uint32_t lane, uint32_t si) {
+    const uint32_t LENS = sb + ZP_LENS, NEXT = sb + ZP_NEXT, LLUT = sb + ZP_LLUT, DLUT = sb + ZP_DLUT;
+    constexpr uint32_t LM = (1u << ZPLUT) - 1;
+    BitIn bi{{src + t.src_off, sb + ZP_WIN, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
+    bi.win.load(0);
+    HTab lt{0, 0, 0, sb + ZP_LSYMS}, dt{0, 0, 0, sb + ZP_DSYMS};
+    TokOut to{0, 0, sb, lane};
+    uint32_t bad = 0, final = 0;
+    bool alive = true;
+    ZDIAG(const uint64_t c0 = __builtin_amdgcn_s_memtime(); uint64_t chdr = 0, cdata = 0; uint32_t nblocks = 0, nround = 0, nslow = 0, ntok = 0;)
+    bi.refill();
+    if (t.kind == ZS_ZLIB) {
+        const uint32_t cmf = bi.bits(8), flg = bi.bits(8);
+        if ((cmf & 15) != 8 || (cmf >> 4) > 7 || (flg & 0x20) || ((cmf << 8) | flg) % 31) bad = 10;
+    }
+    while (!bad && !final && alive) {
+        bi.refill();
+        final = bi.bits(1);
+        const uint32_t type = bi.bits(2);
+        if (type == 0) {  // stored: the consumer copies the bytes from the input
+            bi.bits(bi.cnt & 7);
+            bi.refill();
+            const uint32_t len = bi.bits(16), nlen = bi.bits(16);
+            if ((len ^ 0xffffu) != nlen) { bad = 11; break; }
+            const uint32_t q = bi.ipos - bi.cnt / 8;  // the next byte of the input (buffered ones rewound)
+            if (q + len > bi.ilen) { bad = 12; break; }
+            if (len) alive = to.put_lanes(3ull, lane ? q : (0x80000000u | len));
+            bi.ipos = q + len;
+            bi.buf = 0;
+            bi.cnt = 0;
+            continue;
+        }
+        if (type == 3) { bad = 13; break; }
+        ZDIAG(const uint64_t ch0 = __builtin_amdgcn_s_memtime(); nblocks++;)
+        if (type == 1) {
+            for (uint32_t s2 = lane; s2 < 320; s2 += 64)
+                zlds[LENS + s2] = s2 < 144 ? 8 : s2 < 256 ? 9 : s2 < 280 ? 7 : s2 < 288 ? 8 : 5;
+            __builtin_amdgcn_wave_barrier();
+            build_table(lt, LENS, 288, lane, NEXT);
+            build_table(dt, LENS + 288, 30, lane, NEXT);
+        } else {
+            bi.refill();
+            const uint32_t hlit = bi.bits(5) + 257, hdist = bi.bits(5) + 1, hclen = bi.bits(4) + 4;
+            if (hlit > 286 || hdist > 30) { bad = 14; break; }
+            for (uint32_t s2 = lane; s2 < 19; s2 += 64) zlds[LENS + s2] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t k = 0; k < hclen; k++) {
+                bi.refill();
+                const uint32_t v = bi.bits(3);
+                if (lane == 0) zlds[LENS + c_clord[k]] = (uint8_t)v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            HTab ct{0, 0, 0, sb + ZP_LSYMS};
+            if (!build_table(ct, LENS, 19, lane, NEXT)) { bad = 15; break; }
+            uint32_t k = 0, prev = 0;
+            while (k < hlit + hdist) {
+                bi.refill();
+                const int sym = decode_sym(ct, bi, lane);
+                if (sym < 0) { bad = 16; break; }
+                uint32_t rep = 1, val = (uint32_t)sym;
+                if (sym == 16) {
+                    if (k == 0) { bad = 17; break; }
+                    rep = 3 + bi.bits(2); val = prev;
+                } else if (sym == 17) { rep = 3 + bi.bits(3); val = 0; }
+                else if (sym == 18) { rep = 11 + bi.bits(7); val = 0; }
+                if (k + rep > hlit + hdist) { bad = 18; break; }
+                for (uint32_t r = lane; r < rep; r += 64) zlds[LENS + 19 + k + r] = (uint8_t)val;
+                __builtin_amdgcn_wave_barrier();
+                k += rep;
+                prev = val;
+            }
+            if (bad) break;
+            for (uint32_t s2 = lane; s2 < 320; s2 += 64) {
+                const uint8_t v = s2 < hlit + hdist ? zlds[LENS + 19 + s2] : 0;
+                __builtin_amdgcn_wave_barrier();
+                zlds[LENS + s2] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            {
+                const uint8_t dv = lane < hdist ? zlds[LENS + hlit + lane] : 0;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t s2 = hlit + lane; s2 < ZLENS; s2 += 64) zlds[LENS + s2] = 0;
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 32) zlds[LENS + 288 + lane] = dv;
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (!build_table(lt, LENS, 288, lane, NEXT)) { bad = 19; break; }
+            if (!build_table(dt, LENS + 288, 30, lane, NEXT)) { bad = 20; break; }
+        }
+        build_lut<ZPLUT>(lt, LENS, LLUT, lane);
+        build_lut<ZPLUT>(dt, LENS + 288, DLUT, lane);
+        ZDIAG(const uint64_t cd0 = __builtin_amdgcn_s_memtime(); chdr += cd0 - ch0;)
+        // block data, one round per 64 bit offsets: lane k decodes the whole token (literal, or
+        // length + extra + distance code + extra) that would start k bits into the window and
+        // its bit length; a scalar walk from offset 0 picks the real tokens (<= 48 bits each,
+        // so the 121 window bits cover a token starting at any offset < 64)
+        uint32_t bp = bi.ipos * 8 - bi.cnt;  // bit position in the stream
+        bool eob = false;
+        while (!eob && !bad && alive) {
+            ZDIAG(nround++;)
+            uint32_t d[4];
+            bi.win.peek16(bp >> 3, d);
+            const uint32_t sh = bp & 7;
+            uint64_t lo = (uint64_t)d[1] << 32 | d[0], hi = (uint64_t)d[3] << 32 | d[2];
+            lo = (lo >> sh) | (sh ? hi << (64 - sh) : 0ull);
+            hi >>= sh;
+            const uint64_t x = lane ? (lo >> lane) | (hi << (64 - lane)) : lo;  // window bits from offset `lane`
+            const uint32_t e = lds16(LLUT + 2 * ((uint32_t)x & LM));
+            const uint32_t l = (e >> 9) & 15, sym = e & 511, ls = sym - 257;
+            const uint32_t lsv = ls < 29 ? ls : 0u;  // in range for the arithmetic of every lane
+            const uint32_t le = zp_lext(lsv), p2 = l + le;
+            const uint32_t len = zp_lbase(lsv) + ((uint32_t)(x >> l) & ((1u << le) - 1));
+            const uint32_t de = lds16(DLUT + 2 * ((uint32_t)(x >> p2) & LM));
+            const uint32_t dl = (de >> 9) & 15, ds = de & 511, dsv = ds < 30 ? ds : 0u;
+            const uint32_t dx = zp_dext(dsv), p3 = p2 + dl;
+            const uint32_t dist = zp_dbase(dsv) + ((uint32_t)(x >> p3) & ((1u << dx) - 1));
+            // (selects, not branches: see TokOut)
+            const bool short_sym = sym <= 256;  // literal or end of block: no distance
+            const uint32_t kind = e == 0xFFFF ? ZK_SLOW
+                                : sym == 256  ? ZK_EOB
+                                : short_sym   ? ZK_TOK
+                                : ls >= 29    ? ZK_BAD
+                                : de == 0xFFFF ? ZK_SLOW
+                                : ds >= 30    ? ZK_BAD : ZK_TOK;
+            const uint32_t adv = short_sym ? l : p3 + dx;
+            const uint32_t tok = short_sym ? 0x01000000u | sym
+                               : kind == ZK_BAD ? (ls >= 29 ? 23u : 24u)
+                               : 0x40000000u | ((len - 3) << 16) | (dist - 1);
+            const uint32_t nxv = (lane + adv) | (kind << 8);
+            // the walk: real token starts, as a lane mask
+            uint64_t m = 0;
+            uint32_t p = 0, stop = ZK_TOK;
+            while (p < 64) {
+                const uint32_t v = rdl(nxv, p);
+                if (v >> 8 != ZK_TOK) { stop = v >> 8; break; }
+                m |= 1ull << p;
+                p = v & 255;
+            }
+            if (stop == ZK_EOB) { p = rdl(nxv, p) & 255; eob = true; }
+            else if (stop == ZK_BAD) bad = rdl(tok, p);
+            ZDIAG(ntok += (uint32_t)__popcll(m);)
+            if (!(alive = to.put_lanes(m, tok))) break;
+            bp += p;
+            if (stop == ZK_SLOW) {
+                // one token with a code longer than the first-level tables: canonical decode
+                // from the 64 window bits at the new position
+                ZDIAG(nslow++;)
+                const uint64_t y = (uint64_t)rdl((uint32_t)(x >> 32), p) << 32 | rdl((uint32_t)x, p);
+                uint32_t nb = 0, nd = 0;
+                const int s1 = decode_bits(lt, (uint32_t)y, lane, nb);
+                if (s1 < 0) { bad = 21; break; }
+                if (s1 < 256) { alive = to.put(0x01000000u | (uint32_t)s1); bp += nb; continue; }
+                if (s1 == 256) { eob = true; bp += nb; break; }
+                const uint32_t sl = (uint32_t)s1 - 257;
+                if (sl >= 29) { bad = 23; break; }
+                const uint32_t sle = zp_lext(sl);
+                const uint32_t slen = zp_lbase(sl) + ((uint32_t)(y >> nb) & ((1u << sle) - 1));
+                const uint32_t q2 = nb + sle;
+                const int s2 = decode_bits(dt, (uint32_t)(y >> q2), lane, nd);
+                if (s2 < 0 || s2 >= 30) { bad = 24; break; }
+                const uint32_t sdx = zp_dext((uint32_t)s2);
+                const uint32_t sdist = zp_dbase((uint32_t)s2) + ((uint32_t)(y >> (q2 + nd)) & ((1u << sdx) - 1));
+                alive = to.put(0x40000000u | ((slen - 3) << 16) | (sdist - 1));
+                bp += q2 + nd + sdx;
+            }
+        }
+        ZDIAG(cdata += __builtin_amdgcn_s_memtime() - cd0;)
+        // back to the bit reader at bp (block headers, stored blocks)
+        bi.ipos = bp >> 3;
+        bi.buf = 0;
+        bi.cnt = 0;
+        bi.refill();
+        bi.bits(bp & 7);
+        if (!bad && bi.consumed_bytes() > bi.ilen) bad = 26;
+    }
+    ZDIAG(if (si == 0 && lane == 0) printf("[zp producer] total %lu hdr %lu data %lu blocks %u rounds %u slow %u tokens %u\n",
+                                           (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)chdr,
+                                           (unsigned long)cdata, nblocks, nround, nslow, ntok);)
+    if (alive) to.put(0xC0000000u | bad);
+}
+
+__device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src, uint8_t* dst, uint32_t sb, uint32_t lane,
+                                            uint32_t* errp, uint32_t si) {
+    OutRing<ZR_INF> o{sb + ZP_RING, dst + t.dst_off, 0, 0, t.dlen, lane, sb + ZP_TRASH + 256};
+    const uint8_t* in = src + t.src_off;
+    const uint32_t FLAG = sb + ZP_FLAG;
+    uint32_t head = 0, code = 0;
+    bool done = false;
+    ZDIAG(const uint64_t c0 = __builtin_amdgcn_s_memtime(); uint64_t cwait = 0, cpar = 0; uint32_t nbatch = 0, nchunk = 0, njump = 0;)
+    while (!done) {
+        uint32_t tail;
+        ZDIAG(const uint64_t w0 = __builtin_amdgcn_s_memtime();)
+        while ((tail = lds_load_volatile(sb + ZP_CTRL + ZPC_TAIL)) == head) __builtin_amdgcn_s_sleep(1);
+        ZDIAG(const uint64_t w1 = __builtin_amdgcn_s_memtime(); cwait += w1 - w0; nbatch++;)
+        const uint32_t n = tail - head < 64 ? tail - head : 64u;
+        const uint32_t tq = lds32(sb + ZP_FIFO + 4 * ((head + lane) & (ZP_TOKQ - 1)));
+        const uint32_t tok = lane < n ? tq : 0xC0000000u;
+        const uint32_t typ = tok >> 30;
+        const uint64_t special = __ballot(typ >= 2);  // stored runs, the end token, lanes >= n
+        const uint32_t k = special ? (uint32_t)__builtin_ctzll(special) : 64u;
+        if (k) {
+            // tokens [0, k), literals and matches, all at once: output offsets by a prefix sum,
+            // then 64 output bytes per step, each lane finding its token (a flag per token
+            // start, ballot, mbcnt) and its byte (the literal, the ring below this step, or
+            // a lane of this step: pointer jumping over in-step sources)
+            const bool act = lane < k;
+            const uint32_t len = !act ? 0u : typ == 0 ? 1u : ((tok >> 16) & 0x3FFFu) + 3;
+            const uint32_t end = wave_incl_add(len, lane), start = end - len;
+            const uint32_t T = rdl(end, 63);
+            const uint32_t dist = (tok & 0xFFFFu) + 1;
+            const uint32_t op0 = o.op;
+            const bool far = act && typ == 1 && dist > op0 + start;  // before the stream start
+            if (__ballot(far) || T > o.olen - op0) {
+                code = __ballot(act && typ == 1) ? 25u : 22u;
+                done = true;
+            } else {
+                uint32_t base = 0;
+                for (uint32_t cb = 0; cb < T; cb += 64) {
+                    ZDIAG(nchunk++;)
+                    zlds[FLAG + lane] = 0;
+                    const uint32_t rs = start - cb;
+                    zlds[act && rs < 64 ? FLAG + rs : FLAG + 64 + lane] = 1;
+                    const uint32_t f = zlds[FLAG + lane];
+                    const uint64_t M = __ballot(f != 0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0));
+                    const uint32_t idx = base + below + f - 1;
+                    base += (uint32_t)__popcll(M);
+                    const uint32_t p = cb + lane;
+                    const uint32_t ttok = (uint32_t)__shfl((int)tok, (int)idx, 64);
+                    const bool valid = p < T, ismatch = (ttok >> 30) == 1;
+                    const uint32_t s = p - ((ttok & 0xFFFFu) + 1);  // source offset (from op0; may be < 0)
+                    const uint32_t rv = o.ring(op0 + s);
+                    uint32_t v = ismatch ? rv : (ttok & 255u);
+                    bool pend = valid && ismatch && (int32_t)s >= (int32_t)cb;
+                    uint32_t ptr = s - cb;
+                    while (__ballot(pend)) {
+                        ZDIAG(njump++;)
+                        const uint32_t nv = (uint32_t)__shfl((int)v, (int)ptr, 64);
+                        const uint32_t np = (uint32_t)__shfl((int)pend, (int)ptr, 64);
+                        const uint32_t nq = (uint32_t)__shfl((int)ptr, (int)ptr, 64);
+                        v = pend && !np ? nv : v;
+                        ptr = pend && np ? nq : ptr;
+                        pend = pend && np;
+                    }
+                    o.put_if(valid, op0 + p, v);
+                    o.flush(op0 + (T - cb < 64 ? T : cb + 64));
+                }
+                o.op = op0 + T;
+            }
+        }
+        ZDIAG(cpar += __builtin_amdgcn_s_memtime() - w1;)
+        uint32_t used = k;
+        if (!done && k < n) {
+            const uint32_t tk = rdl(tok, k);
+            if (tk >> 30 == 2) {  // a stored run: its input offset follows (in this batch unless k == 63)
+                if (k + 1 < n) {
+                    const uint32_t len = tk & 0xFFFFu, q = rdl(tok, k + 1);
+                    if (len > o.olen - o.op) { code = 12; done = true; }
+                    else {
+                        for (uint32_t kk = 0; kk < len; kk += 64) {
+                            const uint32_t nb = len - kk < 64 ? len - kk : 64;
+                            const uint32_t v = in[q + kk + lane];  // (the input has slack after every stream)
+                            o.put_if(lane < nb, o.op + kk + lane, v);
+                            o.flush(o.op + kk + nb);
+                        }
+                        o.op += len;
+                    }
+                    used = k + 2;
+                }
+            } else {
+                code = tk & 0xFFu;
+                done = true;
+                used = k + 1;
+            }
+        }
+        head += used;
+        lds_store_volatile(sb + ZP_CTRL + ZPC_HEAD, head);
+        if (done && code) lds_store_volatile(sb + ZP_CTRL + ZPC_ABORT, 1);
+    }
+    if (!code && o.op != o.olen) code = 27;
+    o.finish();
+    if (lane == 0) *errp = code;
+    ZDIAG(if (si == 0 && lane == 0) printf("[zp consumer] total %lu wait %lu parallel %lu batches %u chunks %u jumps %u\n",
+                                           (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)cwait,
+                                           (unsigned long)cpar, nbatch, nchunk, njump);)
+}
+
+__global__ __launch_bounds__(64 * 2 * ZP_STREAMS) void k_zarr_inflate2(const ZStream* __restrict__ st, uint32_t n,
+                                                                       const uint8_t* __restrict__ src,
+                                                                       uint8_t* __restrict__ dst,
+                                                                       uint32_t* __restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);
+    const uint32_t s = w >> 1, si = blockIdx.x * ZP_STREAMS + s;
+    const uint32_t sb = s * ZP_BYTES;
+    if (lane < 4) lds32(sb + ZP_CTRL + 4 * lane) = 0;
+    __syncthreads();
+    if (si >= n) return;
+    const ZStream t = st[si];
+    if (w & 1) zp_consumer(t, src, dst, sb, lane, err + si, si);
+    else zp_producer(t, src, sb, lane, si);
 }
 
 // ------------------------------------------------------------------------------ stored
@@ -699,10 +1107,23 @@ hipError_t launch_zarr_decode(hipStream_t st, const ZStream* d_streams, const ui
         if (!n) continue;
         const dim3 g((n + ZWAVES - 1) / ZWAVES), b(64 * ZWAVES);
         switch (k) {
-        case ZS_LZ4: hipLaunchKernelGGL(k_zarr_lz4, g, b, ZWAVES * (ZR_LZ4 + ZWIN), st, s, n, src, scratch, e); break;
-        case ZS_ZLIB: hipLaunchKernelGGL(k_zarr_inflate, g, b, ZWAVES * (ZI_BYTES + ZWIN), st, s, n, src, scratch, e); break;
+        case ZS_LZ4: hipLaunchKernelGGL(k_zarr_lz4, g, b, ZWAVES * ZL_BYTES, st, s, n, src, scratch, e); break;
+        case ZS_ZLIB:
+            if (getenv("PBX_INFLATE_1WAVE")) {  // the single-wave decoder (A/B)
+                static std::once_flag once[64];
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                std::call_once(once[dev & 63], [] {
+                    (void)hipFuncSetAttribute((const void*)k_zarr_inflate,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                });
+                hipLaunchKernelGGL(k_zarr_inflate, g, b, ZWAVES * (ZI_BYTES + ZWIN), st, s, n, src, scratch, e);
+            } else
+                hipLaunchKernelGGL(k_zarr_inflate2, dim3((n + ZP_STREAMS - 1) / ZP_STREAMS), dim3(128 * ZP_STREAMS),
+                                   ZP_STREAMS * ZP_BYTES, st, s, n, src, scratch, e);
+            break;
         case ZS_COPY: hipLaunchKernelGGL(k_zarr_copy, g, b, 0, st, s, n, src, scratch, e); break;
-        case ZS_BLOSCLZ: hipLaunchKernelGGL(k_zarr_blosclz, g, b, ZWAVES * (ZR_LZ4 + ZWIN), st, s, n, src, scratch, e); break;
+        case ZS_BLOSCLZ: hipLaunchKernelGGL(k_zarr_blosclz, g, b, ZWAVES * ZL_BYTES, st, s, n, src, scratch, e); break;
         default: {
             hipError_t r = launch_zarr_zstd(st, s, n, src, scratch, zstd_lit, e);
             if (r != hipSuccess) return r;

@@ -35,7 +35,8 @@ constexpr uint32_t ZD_NEXT = ZD_NORM + 512;      // u32 symbolNext [256]
 constexpr uint32_t ZD_SPREAD = ZD_NEXT + 1024;   // u8 spread symbols [512]
 constexpr uint32_t ZD_WGT = ZD_SPREAD + 512;     // u8 Huffman weights [256]
 constexpr uint32_t ZD_WT = ZD_WGT + 256;         // FSE table of the weights (<= 64 entries)
-constexpr uint32_t ZD_BYTES = ZD_WT + 64 * 4;
+constexpr uint32_t ZD_TRASH = ZD_WT + 64 * 4;    // the output ring's trash bytes (OutRing::put_if)
+constexpr uint32_t ZD_BYTES = ZD_TRASH + 64;
 
 __device__ __forceinline__ uint32_t& zd32(uint32_t off) { return *(uint32_t*)(zlds + off); }
 __device__ __forceinline__ uint16_t& zd16(uint32_t off) { return *(uint16_t*)(zlds + off); }
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
     const uint32_t wb = w * ZD_BYTES;
     ZIn in{InWin{src + t.src_off, wb + ZD_WIN, 0, lane}, rfl(t.csize)};
     in.win.load(0);
-    OutRing<4096> o{wb + ZD_RING, dst + t.dst_off, 0, 0, t.dlen, lane};
+    OutRing<4096> o{wb + ZD_RING, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZD_TRASH};
     uint8_t* lit = litbuf + (size_t)si * ZSTD_LITBUF;
     const uint32_t ilen = in.len;
     uint32_t bad = 0, q = 0;
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             for (uint32_t k = 0; k < bsize; k += 64) {
                 const uint32_t nb = bsize - k < 64 ? bsize - k : 64;
                 const uint32_t v = in.win.lane_byte(q + k);
-                if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+                o.put_if(lane < nb, o.op + k + lane, v);
                 o.flush(o.op + k + nb);
             }
             o.op += bsize;
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             const uint32_t v = in.byte(q++);
             for (uint32_t k = 0; k < bsize; k += 64) {
                 const uint32_t nb = bsize - k < 64 ? bsize - k : 64;
-                if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+                o.put_if(lane < nb, o.op + k + lane, v);
                 o.flush(o.op + k + nb);
             }
             o.op += bsize;
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             for (uint32_t k = 0; k < n2; k += 64) {
                 const uint32_t nb = n2 - k < 64 ? n2 - k : 64;
                 const uint32_t v = lane < nb ? *(const __attribute__((address_space(1))) uint8_t*)(lit + lp + k + lane) : 0u;
-                if (lane < nb) o.ring(o.op + k + lane) = (uint8_t)v;
+                o.put_if(lane < nb, o.op + k + lane, v);
                 o.flush(o.op + k + nb);
             }
             o.op += n2;

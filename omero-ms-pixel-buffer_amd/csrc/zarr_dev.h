@@ -7,7 +7,7 @@
 
 namespace pbx {
 
-constexpr uint32_t ZR_INF = 4096;            // LDS output ring per wave (inflate): 16 waves/CU
+constexpr uint32_t ZR_INF = 32768;           // inflate: the whole deflate window (no far match reads HBM)
 constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
 constexpr uint32_t ZWAVES = 4;              // waves per workgroup
 constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
@@ -76,13 +76,22 @@ struct InWin {
 
 // Output through the LDS ring (offset rb, 256-aligned); bytes [flushed, op) are in the ring
 // only.  Completed 256-byte runs go to HBM as one dword store per lane.
+// Partial-wave stores go through put_if: the lanes outside the predicate write a byte of their
+// own in a 64-byte trash area instead of branching round the store.  A divergent branch
+// anywhere inside a decoder's symbol loop makes LLVM structurize the whole loop with exec
+// masks, which moves the (wave-uniform) stream state into VGPRs and every test on it into
+// v_cmp + s_and_saveexec code: several times the instructions per symbol.
 template <uint32_t RING>
 struct OutRing {
     static constexpr uint32_t ZM = RING - 1, ZR = RING;
     uint32_t rb;
     uint8_t* out;
     uint32_t op, flushed, olen, lane;
+    uint32_t trash;  // LDS offset of 64 bytes
     __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
+    __device__ void put_if(bool pred, uint32_t pos, uint32_t v) const {
+        zlds[pred ? rb + (pos & ZM) : trash + lane] = (uint8_t)v;
+    }
     __device__ void flush(uint32_t upto) {
         uint32_t f = rfl(flushed);  // keep the ring state in SGPRs (scalar branches)
         upto = rfl(upto);
@@ -115,14 +124,14 @@ struct OutRing {
                 const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 const uint32_t v = *(const __attribute__((address_space(1))) uint8_t*)(out + p - off + rep);
-                if (lane < n) ring(p + lane) = (uint8_t)v;
+                put_if(lane < n, p + lane, v);
                 flush(p + n);
             }
         } else {
             for (uint32_t k = 0; k < len; k += 64) {
                 const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
                 const uint32_t v = ring(p - off + rep);
-                if (lane < n) ring(p + lane) = (uint8_t)v;
+                put_if(lane < n, p + lane, v);
                 flush(p + n);
             }
         }
@@ -130,7 +139,7 @@ struct OutRing {
         return true;
     }
     __device__ void put1(uint32_t v) {
-        if (lane == 0) ring(op) = (uint8_t)v;
+        ring(op) = (uint8_t)v;  // every lane: the same byte
         op = rfl(op) + 1;
         // `flushed` is a multiple of 256 and every other writer flushes as it goes, so a
         // single byte completes a run exactly when op reaches a multiple of 256
