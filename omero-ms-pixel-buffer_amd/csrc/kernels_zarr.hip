@@ -529,30 +529,32 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
 // stream per SIMD: the single-wave decoder above is bound by the latency of that chain
 // (Huffman lookup -> bits consumed -> next lookup, plus the match copies).  Here each stream
 // gets TWO waves of one workgroup, a pipeline through an LDS token FIFO:
-//   producer  the bit stream: block headers and code tables as above, then the symbols.
-//             Per refill it gathers the literal/length and distance first-level table entries
-//             at EVERY bit offset of the 64-bit buffer in one LDS round trip (lane k: the
-//             entries for the bits from offset k), then walks literals and whole matches
-//             (length, its extra bits, distance code, its extra bits) by readlanes until the
-//             buffer runs short; codes of more than 9 bits take the table path.  Tokens go to
-//             a VGPR (lane n holds token n) and to the FIFO 64 at a time.
-//   consumer  the output: 64 tokens per round (one read per lane); a run of literals is
-//             written by as many lanes at once, a match is the ring copy of the single-wave
-//             decoder; the ring flushes to HBM as it fills.
+//   producer  the bit stream: block headers and code tables serially, as above; a Huffman
+//             block's data by self-synchronizing macro-rounds (zp_huff_block): 64 segments of
+//             ~24 tokens each decoded at once, one per lane, from guessed starts, then stitched
+//             where the chains meet.  Whole tokens (literal, or length + distance with their
+//             extra bits) go to the FIFO at each lane's prefix-sum offset.
+//   consumer  the output: batches of >= 32 tokens; offsets by a prefix sum, then 64 output
+//             bytes per step, each lane finding its token and its byte (the literal, the ring,
+//             or pointer jumping over sources inside the step); the ring flushes to HBM.
 // Tokens: literal 0x01000000 | byte; match 0x40000000 | (len - 3) << 16 | (dist - 1);
 // stored run 0x80000000 | len, then the run's input offset; end 0xC0000000 | error code.
-constexpr uint32_t ZP_TOKQ = 256;                   // FIFO tokens per stream (power of two)
+constexpr uint32_t ZP_TOKQ = 2048;                  // FIFO tokens per stream (power of two)
 constexpr uint32_t ZPLUT = 10;                      // producer's first-level tables: codes <= 10 bits
-constexpr uint32_t ZP_WIN = 0, ZP_LLUT = ZWIN, ZP_DLUT = ZP_LLUT + 2 * (1u << ZPLUT),
+constexpr uint32_t ZP_WINB = 3072;                  // input window: a macro-round's 64 segments
+constexpr uint32_t ZP_SMAX = 256;                   // longest segment (bits): 8 * ZP_SMAX + 24 <= ZP_WINB
+constexpr uint32_t ZP_SEGTOK = 24;                  // tokens per segment aimed at
+constexpr uint32_t ZP_WIN = 0, ZP_LLUT = ZP_WINB, ZP_DLUT = ZP_LLUT + 2 * (1u << ZPLUT),
                    ZP_LSYMS = ZP_DLUT + 2 * (1u << ZPLUT), ZP_DSYMS = ZP_LSYMS + 2 * 288,
                    ZP_LENS = ZP_DSYMS + 2 * 32, ZP_NEXT = ZP_LENS + ZLENS, ZP_FIFO = ZP_NEXT + 64,
                    ZP_RING = ZP_FIFO + 4 * ZP_TOKQ, ZP_CTRL = ZP_RING + ZR_INF,
                    ZP_TRASH = ZP_CTRL + 16,         // 4 bytes per lane: masked-off lanes' stores
                    ZP_FLAG = ZP_TRASH + 256 + 64,   // the consumer's token-start flags (+ trash)
                    ZP_BYTES = ZP_FLAG + 128;        // per stream
-static_assert(ZP_BYTES <= 160 * 1024 / 4, "four streams (eight waves) per CU");
+static_assert(ZP_BYTES <= 160 * 1024 / 3, "three streams (six waves) per CU");
 constexpr uint32_t ZP_STREAMS = 1;                  // streams (x 2 waves) per workgroup
-enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8 };
+enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8, ZPC_DONE = 12 };
+constexpr uint32_t ZP_BATCH = 32;  // the consumer waits for this many tokens (or the end)
 
 __device__ __forceinline__ uint32_t zp_lext(uint32_t ls) { return ls < 8 || ls == 28 ? 0u : (ls - 4) >> 2; }
 __device__ __forceinline__ uint32_t zp_lbase(uint32_t ls) {
@@ -612,16 +614,230 @@ struct TokOut {  // the producer's side of the FIFO
 // Per-lane decode kinds of the lane-parallel round
 enum : uint32_t { ZK_TOK = 0, ZK_EOB = 1, ZK_SLOW = 2, ZK_BAD = 3 };
 
+// Per-lane decode of the whole token that starts at bit `pos` of the stream (the LDS window
+// [wbase, wbase + ZP_WINB) must hold its bytes): literal, end of block, or length + extra bits +
+// distance + extra bits.  Codes longer than the first-level tables take a per-lane canonical
+// search over the remaining lengths (uniform loop, only when some lane needs it).
+struct ZLane {
+    uint32_t kind, adv, tok;  // ZK_*, bits, FIFO token (or the error code of ZK_BAD)
+};
+__device__ __forceinline__ uint32_t canon_lane(const HTab& h, uint32_t bits, bool need) {
+    const uint32_t rev = __builtin_bitreverse32(bits & 0x7fffu) >> 17;
+    uint32_t res = 0xFFFF, idx = 0;
+    for (uint32_t L = ZPLUT + 1; L <= 15; L++) {
+        const uint32_t f = rdl(h.first, L - 1), c = rdl(h.count, L - 1), o = rdl(h.offs, L - 1);
+        const uint32_t code = rev >> (15 - L);
+        const bool hit = need && res == 0xFFFF && code - f < c;
+        idx = hit ? o + code - f : idx;
+        res = hit ? L << 9 : res;
+    }
+    const uint32_t sym = lds16(h.syms + 2 * idx);
+    return res == 0xFFFF ? res : res | sym;
+}
+__device__ __forceinline__ ZLane zp_decode_at(uint32_t pos, uint32_t win, uint32_t wbase, uint32_t LLUT,
+                                              uint32_t DLUT, const HTab& lt, const HTab& dt) {
+    constexpr uint32_t LM = (1u << ZPLUT) - 1;
+    const uint32_t bo = win + (pos >> 3) - wbase;
+    uint32_t w0, w1;
+    __builtin_memcpy(&w0, zlds + bo, 4);
+    __builtin_memcpy(&w1, zlds + bo + 4, 4);
+    const uint64_t x = ((uint64_t)w1 << 32 | w0) >> (pos & 7);  // >= 57 valid bits
+    uint32_t e = lds16(LLUT + 2 * ((uint32_t)x & LM));
+    if (__ballot(e == 0xFFFF)) e = e == 0xFFFF ? canon_lane(lt, (uint32_t)x, true) : e;
+    const uint32_t l = (e >> 9) & 15, sym = e & 511, ls = sym - 257;
+    const uint32_t lsv = ls < 29 ? ls : 0u;  // in range for the arithmetic of every lane
+    const uint32_t le = zp_lext(lsv), p2 = l + le;
+    const uint32_t len = zp_lbase(lsv) + ((uint32_t)(x >> l) & ((1u << le) - 1));
+    const uint32_t xd = (uint32_t)(x >> p2);
+    uint32_t de = lds16(DLUT + 2 * (xd & LM));
+    const bool need_d = sym > 256 && ls < 29 && de == 0xFFFF;
+    if (__ballot(need_d)) de = need_d ? canon_lane(dt, xd, true) : de;
+    const uint32_t dl = (de >> 9) & 15, ds = de & 511, dsv = ds < 30 ? ds : 0u;
+    const uint32_t dx = zp_dext(dsv), p3 = p2 + dl;
+    const uint32_t dist = zp_dbase(dsv) + ((uint32_t)(x >> p3) & ((1u << dx) - 1));
+    const bool short_sym = sym <= 256;
+    ZLane r;
+    r.kind = e == 0xFFFF ? ZK_BAD : sym == 256 ? ZK_EOB : short_sym ? ZK_TOK
+           : ls >= 29 ? ZK_BAD : de == 0xFFFF ? ZK_BAD : ds >= 30 ? ZK_BAD : ZK_TOK;
+    r.adv = short_sym ? l : p3 + dx;
+    r.tok = r.kind == ZK_BAD ? (e == 0xFFFF ? 21u : ls >= 29 ? 23u : 24u)
+          : short_sym ? 0x01000000u | sym : 0x40000000u | ((len - 3) << 16) | (dist - 1);
+    return r;
+}
+
+// Token starts met in a segment (<= ZP_SMAX bits): four words in VGPRs, indexed by selects (an
+// array indexed by a lane-varying bit would live in scratch memory).
+struct SegBits {
+    uint64_t a = 0, b = 0, c = 0, d = 0;
+    __device__ void set(uint32_t r) {
+        const uint64_t m = 1ull << (r & 63);
+        const uint32_t w = r >> 6;
+        a |= w == 0 ? m : 0ull; b |= w == 1 ? m : 0ull; c |= w == 2 ? m : 0ull; d |= w == 3 ? m : 0ull;
+    }
+    __device__ bool test(uint32_t r) const {  // (masks: a ?: chain becomes a scratch-memory table)
+        const uint32_t w = r >> 6;
+        const uint64_t x = (a & (0ull - (uint64_t)(w == 0))) | (b & (0ull - (uint64_t)(w == 1))) |
+                           (c & (0ull - (uint64_t)(w == 2))) | (d & (0ull - (uint64_t)(w == 3)));
+        return (x >> (r & 63)) & 1;
+    }
+    __device__ uint32_t count_below(uint32_t r) const {  // set bits < r (r < 256)
+        const uint32_t w = r >> 6;
+        const uint64_t m = (1ull << (r & 63)) - 1;
+        uint32_t n = (uint32_t)__popcll(w == 0 ? a & m : a);
+        n += w >= 1 ? (uint32_t)__popcll(w == 1 ? b & m : b) : 0u;
+        n += w >= 2 ? (uint32_t)__popcll(w == 2 ? c & m : c) : 0u;
+        n += w >= 3 ? (uint32_t)__popcll(d & m) : 0u;
+        return n;
+    }
+    // bits >= r of this, bits < r of o
+    __device__ void splice(const SegBits& o, uint32_t r) {
+        const uint32_t w = r >> 6;
+        const uint64_t m = (1ull << (r & 63)) - 1;
+        const uint64_t la = w > 0 ? ~0ull : m, lb = w > 1 ? ~0ull : w == 1 ? m : 0ull,
+                       lc = w > 2 ? ~0ull : w == 2 ? m : 0ull, ld = w == 3 ? m : 0ull;
+        a = (o.a & la) | (a & ~la);
+        b = (o.b & lb) | (b & ~lb);
+        c = (o.c & lc) | (c & ~lc);
+        d = (o.d & ld) | (d & ~ld);
+    }
+};
+
+// One Huffman block's data, self-synchronizing: a macro-round splits the next 64*S bits into
+// 64 segments and lane i decodes from the START of segment i, which is probably not a token
+// boundary (pass A), recording the token starts it meets in the segment.
+// Pass B re-decodes each lane from where its left neighbour's chain left the segments before
+// it, until that chain meets one of the recorded starts: from there the two chains are the
+// same token sequence (decoding is a function of the bit position), so the lane's pass-A
+// count and exit stand.  A chain that meets none decodes the whole segment, and its right
+// neighbour is checked again.  Pass C re-decodes every lane from its true entry and
+// writes its tokens to the FIFO at the lane's offset (a prefix sum of the counts).
+// Returns the bit position after the block (or of the round's end when it stopped early).
+__device__ __forceinline__ uint32_t zp_huff_block(uint32_t B, BitIn& bi, TokOut& to, uint32_t sb, uint32_t lane,
+                                                  const HTab& lt, const HTab& dt, uint32_t& bad, bool& alive,
+                                                  uint32_t& sbits ZDIAG(, uint32_t* dg)) {
+    const uint32_t WIN = sb + ZP_WIN, LLUT = sb + ZP_LLUT, DLUT = sb + ZP_DLUT;
+    bool loaded = false;  // the bit reader's window is 1 KiB: reload the whole window once
+    for (;;) {
+        // segment length: about 16 tokens per lane at the last round's bits per token
+        const uint32_t S = sbits;
+        const uint32_t q = B >> 3;
+        if (q > bi.ilen) { bad = 26; return B; }  // (corrupt input: the window would leave the slack)
+        if (!loaded || q < bi.win.base || q + 8 * S + 24 > bi.win.base + ZP_WINB) {
+            loaded = true;
+            uint4 v[ZP_WINB / 1024];
+#pragma unroll
+            for (uint32_t k = 0; k < ZP_WINB / 1024; k++) __builtin_memcpy(&v[k], bi.win.in + q + 1024 * k + 16 * lane, 16);
+#pragma unroll
+            for (uint32_t k = 0; k < ZP_WINB / 1024; k++) *(uint4*)(zlds + WIN + 1024 * k + 16 * lane) = v[k];
+            bi.win.base = q;
+        }
+        const uint32_t wb = bi.win.base;
+        const uint32_t b0 = B + lane * S, e0 = b0 + S;
+        ZDIAG(dg[0]++;)
+        // pass A
+        uint32_t pos = b0, cs = 0, fl = ZK_TOK, ec = 0;
+        SegBits vis;
+        bool act = true;
+        while (__ballot(act)) {
+            ZDIAG(dg[1]++;)
+            const ZLane d = zp_decode_at(act ? pos : B, WIN, wb, LLUT, DLUT, lt, dt);
+            if (act) vis.set(pos - b0);
+            const bool stop = d.kind != ZK_TOK;
+            fl = act && stop ? d.kind : fl;
+            ec = act && d.kind == ZK_BAD ? d.tok : ec;
+            cs += act && !stop ? 1u : 0u;
+            pos += act && d.kind != ZK_BAD ? d.adv : 0u;
+            act = act && !stop && pos < e0;
+        }
+        // pass B
+        uint32_t xs = pos, chk = b0;
+        for (;;) {
+            const uint32_t pe = (uint32_t)__shfl_up((int)xs, 1, 64), pf = (uint32_t)__shfl_up((int)fl, 1, 64);
+            const uint32_t e = lane ? pe : B;
+            const bool todo = lane && pf == ZK_TOK && e != chk;
+            if (!__ballot(todo)) break;
+            ZDIAG(dg[2]++;)
+            uint32_t p = e, c = 0;
+            bool walk = todo;  // from the entry until the old chain is met (or the segment ends)
+            SegBits vn;
+            while (__ballot(walk)) {
+                ZDIAG(dg[3]++;)
+                const uint32_t rel = p - b0;
+                if (walk && vis.test(rel)) {  // the chains meet at p
+                    cs = c + (cs - vis.count_below(rel));
+                    vis.splice(vn, rel);
+                    walk = false;
+                }
+                const ZLane d = zp_decode_at(walk ? p : B, WIN, wb, LLUT, DLUT, lt, dt);
+                if (walk) {
+                    vn.set(rel);
+                    const bool stop = d.kind != ZK_TOK;
+                    c += stop ? 0u : 1u;
+                    p += d.kind != ZK_BAD ? d.adv : 0u;
+                    if (stop || p >= e0) {  // the new chain is this lane's chain
+                        xs = p;
+                        cs = c;
+                        fl = d.kind;
+                        ec = d.kind == ZK_BAD ? d.tok : ec;
+                        vis = vn;
+                        walk = false;
+                    }
+                }
+            }
+            chk = todo ? e : chk;
+        }
+        // pass C: the lanes up to the first chain that ends the block (EOB or an error)
+        const uint64_t ends = __ballot(fl != ZK_TOK);
+        const uint32_t first = ends ? (uint32_t)__builtin_ctzll(ends) : 63u;
+        const uint32_t cnt = lane <= first ? cs : 0u;
+        const uint32_t incl = wave_incl_add(cnt, lane), off = incl - cnt;
+        // as many lanes as the FIFO takes now (lane 0 always: <= S tokens <= the FIFO)
+        to.head = lds_load_volatile(sb + ZP_CTRL + ZPC_HEAD);
+        if (!(alive = to.room(rdl(cnt, 0)))) return B;
+        const uint32_t room = ZP_TOKQ - (to.tail - to.head);
+        const uint64_t fits = __ballot(lane <= first && incl <= room);
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(fits);  // lanes 0..last (fits is a prefix)
+        const uint32_t n = lane <= last ? cnt : 0u;
+        const uint32_t total = rdl(incl, last);
+        ZDIAG(dg[4] += total;)
+        {
+            const uint32_t pe = (uint32_t)__shfl_up((int)xs, 1, 64);
+            uint32_t p = lane ? pe : B, j = 0;
+            while (__ballot(j < n)) {
+                ZDIAG(dg[5]++;)
+                const ZLane d = zp_decode_at(j < n ? p : B, WIN, wb, LLUT, DLUT, lt, dt);
+                lds32(j < n ? sb + ZP_FIFO + 4 * ((to.tail + off + j) & (ZP_TOKQ - 1)) : sb + ZP_TRASH + 4 * lane) = d.tok;
+                p += j < n ? d.adv : 0u;
+                j++;
+            }
+        }
+        to.tail += total;
+        lds_store_volatile(sb + ZP_CTRL + ZPC_TAIL, to.tail);
+        const uint32_t nB = rdl(xs, last);
+        // next segment length from this round's bits per token
+        if (total) {
+            const uint32_t bpt = ((nB - B) * ZP_SEGTOK + total - 1) / total;
+            sbits = bpt < 64 ? 64u : bpt > ZP_SMAX ? ZP_SMAX : (bpt + 7) & ~7u;
+        }
+        if (last == first && (ends >> first) & 1) {  // this round reached the end of the block
+            const uint32_t f = rdl(fl, first);
+            if (f == ZK_BAD) bad = rdl(ec, first);
+            return nB;
+        }
+        B = nB;
+    }
+}
+
 __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src, uint32_t sb, uint32_t lane, uint32_t si) {
     const uint32_t LENS = sb + ZP_LENS, NEXT = sb + ZP_NEXT, LLUT = sb + ZP_LLUT, DLUT = sb + ZP_DLUT;
-    constexpr uint32_t LM = (1u << ZPLUT) - 1;
     BitIn bi{{src + t.src_off, sb + ZP_WIN, 0, lane}, 0ull, 0, 0, rfl(t.csize)};
     bi.win.load(0);
     HTab lt{0, 0, 0, sb + ZP_LSYMS}, dt{0, 0, 0, sb + ZP_DSYMS};
     TokOut to{0, 0, sb, lane};
     uint32_t bad = 0, final = 0;
     bool alive = true;
-    ZDIAG(const uint64_t c0 = __builtin_amdgcn_s_memtime(); uint64_t chdr = 0, cdata = 0; uint32_t nblocks = 0, nround = 0, nslow = 0, ntok = 0;)
+    uint32_t sbits = 128;  // segment length of the next macro-round
+    ZDIAG(const uint64_t c0 = __builtin_amdgcn_s_memtime(); uint64_t chdr = 0, cdata = 0; uint32_t nblocks = 0; uint32_t dg[6] = {0, 0, 0, 0, 0, 0};)
     bi.refill();
     if (t.kind == ZS_ZLIB) {
         const uint32_t cmf = bi.bits(8), flg = bi.bits(8);
@@ -704,80 +920,8 @@ __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src
         build_lut<ZPLUT>(lt, LENS, LLUT, lane);
         build_lut<ZPLUT>(dt, LENS + 288, DLUT, lane);
         ZDIAG(const uint64_t cd0 = __builtin_amdgcn_s_memtime(); chdr += cd0 - ch0;)
-        // block data, one round per 64 bit offsets: lane k decodes the whole token (literal, or
-        // length + extra + distance code + extra) that would start k bits into the window and
-        // its bit length; a scalar walk from offset 0 picks the real tokens (<= 48 bits each,
-        // so the 121 window bits cover a token starting at any offset < 64)
-        uint32_t bp = bi.ipos * 8 - bi.cnt;  // bit position in the stream
-        bool eob = false;
-        while (!eob && !bad && alive) {
-            ZDIAG(nround++;)
-            uint32_t d[4];
-            bi.win.peek16(bp >> 3, d);
-            const uint32_t sh = bp & 7;
-            uint64_t lo = (uint64_t)d[1] << 32 | d[0], hi = (uint64_t)d[3] << 32 | d[2];
-            lo = (lo >> sh) | (sh ? hi << (64 - sh) : 0ull);
-            hi >>= sh;
-            const uint64_t x = lane ? (lo >> lane) | (hi << (64 - lane)) : lo;  // window bits from offset `lane`
-            const uint32_t e = lds16(LLUT + 2 * ((uint32_t)x & LM));
-            const uint32_t l = (e >> 9) & 15, sym = e & 511, ls = sym - 257;
-            const uint32_t lsv = ls < 29 ? ls : 0u;  // in range for the arithmetic of every lane
-            const uint32_t le = zp_lext(lsv), p2 = l + le;
-            const uint32_t len = zp_lbase(lsv) + ((uint32_t)(x >> l) & ((1u << le) - 1));
-            const uint32_t de = lds16(DLUT + 2 * ((uint32_t)(x >> p2) & LM));
-            const uint32_t dl = (de >> 9) & 15, ds = de & 511, dsv = ds < 30 ? ds : 0u;
-            const uint32_t dx = zp_dext(dsv), p3 = p2 + dl;
-            const uint32_t dist = zp_dbase(dsv) + ((uint32_t)(x >> p3) & ((1u << dx) - 1));
-            // (selects, not branches: see TokOut)
-            const bool short_sym = sym <= 256;  // literal or end of block: no distance
-            const uint32_t kind = e == 0xFFFF ? ZK_SLOW
-                                : sym == 256  ? ZK_EOB
-                                : short_sym   ? ZK_TOK
-                                : ls >= 29    ? ZK_BAD
-                                : de == 0xFFFF ? ZK_SLOW
-                                : ds >= 30    ? ZK_BAD : ZK_TOK;
-            const uint32_t adv = short_sym ? l : p3 + dx;
-            const uint32_t tok = short_sym ? 0x01000000u | sym
-                               : kind == ZK_BAD ? (ls >= 29 ? 23u : 24u)
-                               : 0x40000000u | ((len - 3) << 16) | (dist - 1);
-            const uint32_t nxv = (lane + adv) | (kind << 8);
-            // the walk: real token starts, as a lane mask
-            uint64_t m = 0;
-            uint32_t p = 0, stop = ZK_TOK;
-            while (p < 64) {
-                const uint32_t v = rdl(nxv, p);
-                if (v >> 8 != ZK_TOK) { stop = v >> 8; break; }
-                m |= 1ull << p;
-                p = v & 255;
-            }
-            if (stop == ZK_EOB) { p = rdl(nxv, p) & 255; eob = true; }
-            else if (stop == ZK_BAD) bad = rdl(tok, p);
-            ZDIAG(ntok += (uint32_t)__popcll(m);)
-            if (!(alive = to.put_lanes(m, tok))) break;
-            bp += p;
-            if (stop == ZK_SLOW) {
-                // one token with a code longer than the first-level tables: canonical decode
-                // from the 64 window bits at the new position
-                ZDIAG(nslow++;)
-                const uint64_t y = (uint64_t)rdl((uint32_t)(x >> 32), p) << 32 | rdl((uint32_t)x, p);
-                uint32_t nb = 0, nd = 0;
-                const int s1 = decode_bits(lt, (uint32_t)y, lane, nb);
-                if (s1 < 0) { bad = 21; break; }
-                if (s1 < 256) { alive = to.put(0x01000000u | (uint32_t)s1); bp += nb; continue; }
-                if (s1 == 256) { eob = true; bp += nb; break; }
-                const uint32_t sl = (uint32_t)s1 - 257;
-                if (sl >= 29) { bad = 23; break; }
-                const uint32_t sle = zp_lext(sl);
-                const uint32_t slen = zp_lbase(sl) + ((uint32_t)(y >> nb) & ((1u << sle) - 1));
-                const uint32_t q2 = nb + sle;
-                const int s2 = decode_bits(dt, (uint32_t)(y >> q2), lane, nd);
-                if (s2 < 0 || s2 >= 30) { bad = 24; break; }
-                const uint32_t sdx = zp_dext((uint32_t)s2);
-                const uint32_t sdist = zp_dbase((uint32_t)s2) + ((uint32_t)(y >> (q2 + nd)) & ((1u << sdx) - 1));
-                alive = to.put(0x40000000u | ((slen - 3) << 16) | (sdist - 1));
-                bp += q2 + nd + sdx;
-            }
-        }
+        // block data: self-synchronizing macro-rounds
+        const uint32_t bp = zp_huff_block(bi.ipos * 8 - bi.cnt, bi, to, sb, lane, lt, dt, bad, alive, sbits ZDIAG(, dg));
         ZDIAG(cdata += __builtin_amdgcn_s_memtime() - cd0;)
         // back to the bit reader at bp (block headers, stored blocks)
         bi.ipos = bp >> 3;
@@ -787,10 +931,11 @@ __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src
         bi.bits(bp & 7);
         if (!bad && bi.consumed_bytes() > bi.ilen) bad = 26;
     }
-    ZDIAG(if (si == 0 && lane == 0) printf("[zp producer] total %lu hdr %lu data %lu blocks %u rounds %u slow %u tokens %u\n",
+    ZDIAG(if (si == 0 && lane == 0) printf("[zp producer] total %lu hdr %lu data %lu blocks %u rounds %u stepsA %u syncs %u stepsB %u tokens %u stepsC %u\n",
                                            (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)chdr,
-                                           (unsigned long)cdata, nblocks, nround, nslow, ntok);)
+                                           (unsigned long)cdata, nblocks, dg[0], dg[1], dg[2], dg[3], dg[4], dg[5]);)
     if (alive) to.put(0xC0000000u | bad);
+    lds_store_volatile(sb + ZP_CTRL + ZPC_DONE, 1);
 }
 
 __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src, uint8_t* dst, uint32_t sb, uint32_t lane,
@@ -804,7 +949,11 @@ __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src
     while (!done) {
         uint32_t tail;
         ZDIAG(const uint64_t w0 = __builtin_amdgcn_s_memtime();)
-        while ((tail = lds_load_volatile(sb + ZP_CTRL + ZPC_TAIL)) == head) __builtin_amdgcn_s_sleep(1);
+        // a batch of >= ZP_BATCH tokens: the output steps are 64 bytes whatever the batch
+        while ((tail = lds_load_volatile(sb + ZP_CTRL + ZPC_TAIL)) - head < ZP_BATCH &&
+               !lds_load_volatile(sb + ZP_CTRL + ZPC_DONE))
+            __builtin_amdgcn_s_sleep(2);
+        if (tail == head) tail = lds_load_volatile(sb + ZP_CTRL + ZPC_TAIL);  // DONE seen: the end token is in
         ZDIAG(const uint64_t w1 = __builtin_amdgcn_s_memtime(); cwait += w1 - w0; nbatch++;)
         const uint32_t n = tail - head < 64 ? tail - head : 64u;
         const uint32_t tq = lds32(sb + ZP_FIFO + 4 * ((head + lane) & (ZP_TOKQ - 1)));
