@@ -419,6 +419,42 @@ def test_gpu_inflate_sync_flush_and_tiny_stored_blocks(service, oracle, level, p
     service.release_plane(pid)
 
 
+def _strategy_plane(kind, h, w):
+    """Planes whose deflate streams stress different paths of the self-synchronizing decoder:
+    long runs (258-byte matches at distance 1-2), short codes (many tokens per segment: the
+    FIFO-room truncation of a macro-round), smooth data, and noise."""
+    rng = np.random.default_rng(23)
+    if kind == "zeros":
+        return np.zeros((h, w), ">u2")
+    if kind == "steps":
+        return (np.arange(h * w, dtype=np.uint32) // 1000 % 7).astype(">u2").reshape(h, w)
+    if kind == "gradient":
+        return (np.add.outer(np.arange(h), np.arange(w)) * 13).astype(">u2")
+    if kind == "sparse":
+        p = np.zeros((h, w), ">u2")
+        p.flat[rng.integers(0, h * w, h * w // 50)] = rng.integers(0, 65535, h * w // 50)
+        return p
+    return rng.integers(0, 4096, (h, w)).astype(">u2")
+
+
+@gpu
+@pytest.mark.parametrize("strategy", [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE,
+                                      zlib.Z_FIXED], ids=["default", "filtered", "huffman-only", "rle", "fixed"])
+@pytest.mark.parametrize("kind", ["zeros", "steps", "gradient", "sparse", "noise12"])
+@pytest.mark.parametrize("level", [1, 9])
+def test_gpu_inflate_strategies(service, oracle, strategy, kind, level):
+    """zlib streams of every deflate strategy (fixed and dynamic codes, literal-only, run-length
+    only) over compressible and noisy planes decode exactly like zlib's inflate."""
+    import pbx
+    h, w = 300, 520
+    plane = _strategy_plane(kind, h, w)
+    co = zlib.compressobj(level, zlib.DEFLATED, 15, 9, strategy)
+    enc = co.compress(plane.tobytes()) + co.flush()
+    pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, w, h, w, h, "zlib", [enc])
+    assert np.array_equal(plane_be(service, pid, ">u2", h, w), plane)
+    service.release_plane(pid)
+
+
 @gpu
 @pytest.mark.parametrize("cname", ["blosclz", "zstd", "lz4", "zlib"])
 @pytest.mark.parametrize("shuffle", [0, 1, 2], ids=["noshuffle", "shuffle", "bitshuffle"])
