@@ -22,6 +22,7 @@ namespace pbx {
 
 constexpr uint32_t ZSTD_WAVES = 2;           // waves (frames) per workgroup
 constexpr uint32_t ZSTD_LITBUF = 128 * 1024; // Block_Maximum_Size: a block's literals
+constexpr uint32_t ZSTD_LITSTRIDE = ZSTD_LITBUF + 64;  // + the masked-off lanes' trash bytes
 
 // Per-wave LDS (byte offsets from the wave's base)
 constexpr uint32_t ZD_RING = 0;                  // 4 KiB output ring
@@ -46,13 +47,13 @@ __device__ __forceinline__ int16_t& zdi16(uint32_t off) { return *(int16_t*)(zld
 __constant__ uint32_t c_ll_base[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22,
                                        24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192,
                                        16384, 32768, 65536};
-__constant__ uint8_t c_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+__constant__ uint32_t c_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
                                       2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 __constant__ uint32_t c_ml_base[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20,
                                        21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 37,
                                        39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051,
                                        4099, 8195, 16387, 32771, 65539};
-__constant__ uint8_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+__constant__ uint32_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                       0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9,
                                       10, 11, 12, 13, 14, 15, 16};
 // predefined distributions (3.1.1.3.2.2)
@@ -73,6 +74,7 @@ struct ZIn {
     __device__ uint32_t byte(uint32_t q) { return win.byte(q); }
     // 8 bytes from q (little-endian), window placed to end just after them (backward reads)
     __device__ uint64_t le64_back(uint32_t q) {
+        win.base = rfl(win.base);
         if (q < win.base || q + 8 > win.base + ZWIN) win.load(q + 8 > ZWIN ? q + 8 - ZWIN : 0u);
         uint32_t a, b;
         __builtin_memcpy(&a, zlds + win.wo + q - win.base, 4);
@@ -92,27 +94,41 @@ struct ZIn {
 // Backward bitstream over frame bytes [lo, hi): the last byte's highest set bit is the end
 // marker; reads take the highest remaining bits first; bits below the start read as zeros
 // (pos < 0 afterwards = over-read).
+// The bits are cached: cont holds stream bits [cb, cb + 64) (cb a multiple of 8), refilled
+// from the LDS window when a read leaves it (about once per 32 bits instead of per read).
 struct BitBack {
     uint32_t lo;
     int32_t pos;  // bits left, counted from lo * 8
+    int32_t cb;   // first bit of cont
+    uint64_t cont;
     __device__ bool init(ZIn& in, uint32_t lo_, uint32_t hi_) {
         lo = lo_;
+        cb = 0x7FFFFFFF;  // nothing cached
+        cont = 0;
         if (hi_ <= lo_) return false;
         const uint32_t last = in.byte(hi_ - 1);
         if (!last) return false;
         pos = (int32_t)((hi_ - lo_ - 1) * 8 + hibit(last));
         return true;
     }
+    // the state is wave-uniform: pin it to SGPRs at the top of a decode loop (LLVM otherwise
+    // carries it in VGPRs through the loop's phis)
+    __device__ void pin() {
+        pos = (int32_t)rfl((uint32_t)pos);
+        cb = (int32_t)rfl((uint32_t)cb);
+        cont = (uint64_t)rfl((uint32_t)(cont >> 32)) << 32 | rfl((uint32_t)cont);
+    }
     __device__ uint32_t peek(ZIn& in, uint32_t n) {  // n <= 32
         if (n == 0) return 0;
         const int32_t q = pos - (int32_t)n;
-        uint64_t v;
-        if (q >= 0) {
-            v = in.le64_back(lo + ((uint32_t)q >> 3)) >> (q & 7);
-        } else {
-            const uint32_t z = (uint32_t)(-q);  // zero bits below the start
-            v = z >= 32 ? 0ull : in.le64_back(lo) << z;
+        if (q < cb || pos > cb + 64) {  // refill: the 8 bytes ending at pos's byte
+            const int32_t e = (pos + 7) >> 3;
+            const int32_t sb = e >= 8 ? e - 8 : 0;
+            cont = in.le64_back(lo + (uint32_t)sb);
+            cb = 8 * sb;
         }
+        // q >= cb, or q < 0 with cb == 0: the bits below the start read as zeros
+        const uint64_t v = q >= cb ? cont >> (q - cb) : cont << (cb - q);
         return (uint32_t)v & (n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
     }
     __device__ uint32_t read(ZIn& in, uint32_t n) {
@@ -359,17 +375,17 @@ __device__ uint32_t read_huf_tree(ZIn& in, uint32_t wb, uint32_t q, uint32_t qen
 // Decode `n` Huffman literals of one stream [lo, hi) into lit[0..n): 64 at a time, lane k
 // holding the k-th of each group, stored by one byte store per lane.
 __device__ bool huf_stream(ZIn& in, uint32_t wb, uint32_t hlog, uint32_t lo, uint32_t hi, uint8_t* lit,
-                           uint32_t n, uint32_t lane) {
+                           uint32_t n, uint8_t* trash, uint32_t lane) {
     BitBack br;
     if (!br.init(in, lo, hi)) return false;
     uint32_t acc = 0;
     for (uint32_t i = 0; i < n; i++) {
-        const uint32_t e = zd16(wb + ZD_HUF + 2 * br.peek(in, hlog));
+        br.pin();
+        const uint32_t e = rfl(zd16(wb + ZD_HUF + 2 * br.peek(in, hlog)));
         br.pos -= (int32_t)(e >> 8);
         acc = (lane == (i & 63)) ? (e & 0xFF) : acc;
-        if ((i & 63) == 63 || i + 1 == n) {
-            if (lane <= (i & 63)) lit[(i & ~63u) + lane] = (uint8_t)acc;
-        }
+        if ((i & 63) == 63 || i + 1 == n)  // (no lane branch: masked-off lanes write the trash bytes)
+            *(lane <= (i & 63) ? lit + (i & ~63u) + lane : trash + lane) = (uint8_t)acc;
     }
     return br.pos == 0;
 }
@@ -387,9 +403,18 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
     ZIn in{InWin{src + t.src_off, wb + ZD_WIN, 0, lane}, rfl(t.csize)};
     in.win.load(0);
     OutRing<4096> o{wb + ZD_RING, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZD_TRASH};
-    uint8_t* lit = litbuf + (size_t)si * ZSTD_LITBUF;
+    uint8_t* lit = litbuf + (size_t)si * ZSTD_LITSTRIDE;
     const uint32_t ilen = in.len;
     uint32_t bad = 0, q = 0;
+#ifdef PBX_ZARR_DIAG  // diagnostic build only: stream 0's clocks (printf)
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+    uint64_t clit = 0, cseq = 0, ctab = 0;
+    uint32_t nlits = 0, nseqs = 0, nblk = 0, nfar = 0, nlitrun = 0;
+    uint64_t cread = 0, ccopy = 0, cmatch = 0;
+#define ZSD(...) __VA_ARGS__
+#else
+#define ZSD(...)
+#endif
     // ---- frame header
     if (ilen < 6) bad = 1;
     const uint32_t magic = bad ? 0u : (uint32_t)in.le64_fwd(0);
@@ -444,6 +469,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             continue;
         }
         // ---- compressed block [q, bend)
+        ZSD(const uint64_t b0 = __builtin_amdgcn_s_memtime(); nblk++;)
         const uint32_t bend = q + bsize;
         if (bend > ilen || bsize > ZSTD_LITBUF) { bad = 10; break; }
         const uint64_t lh = in.le64_fwd(q);
@@ -488,7 +514,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
                 break;
             }
             if (!four) {
-                if (!huf_stream(in, wb, hlog, lq, lend, lit, nlit, lane)) { bad = 17; break; }
+                if (!huf_stream(in, wb, hlog, lq, lend, lit, nlit, lit + ZSTD_LITBUF, lane)) { bad = 17; break; }
             } else {
                 if (lq + 6 > lend) { bad = 18; break; }
                 const uint64_t jt = in.le64_fwd(lq);
@@ -498,10 +524,10 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
                 if (d2 > lend) { bad = 19; break; }
                 const uint32_t per = (nlit + 3) / 4;
                 if (3 * per > nlit) { bad = 20; break; }
-                if (!huf_stream(in, wb, hlog, a, b2, lit, per, lane) ||
-                    !huf_stream(in, wb, hlog, b2, c2, lit + per, per, lane) ||
-                    !huf_stream(in, wb, hlog, c2, d2, lit + 2 * per, per, lane) ||
-                    !huf_stream(in, wb, hlog, d2, lend, lit + 3 * per, nlit - 3 * per, lane)) {
+                if (!huf_stream(in, wb, hlog, a, b2, lit, per, lit + ZSTD_LITBUF, lane) ||
+                    !huf_stream(in, wb, hlog, b2, c2, lit + per, per, lit + ZSTD_LITBUF, lane) ||
+                    !huf_stream(in, wb, hlog, c2, d2, lit + 2 * per, per, lit + ZSTD_LITBUF, lane) ||
+                    !huf_stream(in, wb, hlog, d2, lend, lit + 3 * per, nlit - 3 * per, lit + ZSTD_LITBUF, lane)) {
                     bad = 21;
                     break;
                 }
@@ -510,6 +536,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         }
         // the literals just stored are read back by this wave below
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        ZSD(const uint64_t b1 = __builtin_amdgcn_s_memtime(); clit += b1 - b0; nlits += nlit;)
         // ---- sequences section
         if (q >= bend) { bad = 22; break; }
         uint32_t nseq = in.byte(q++);
@@ -524,11 +551,26 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             }
         }
         uint32_t lp = 0;  // literals consumed
+        // the literals through a register window: literals [lwb, lwb + 256) one dword per lane
+        // in lcur, the next 256 in lnxt (loaded a window ahead: no HBM wait per sequence)
+        auto lit_word = [&](uint32_t i) -> uint32_t {
+            const uint32_t at = i + 4 * lane < ZSTD_LITBUF - 4 ? i + 4 * lane : ZSTD_LITBUF - 4;
+            return *(const __attribute__((address_space(1))) uint32_t*)(lit + at);
+        };
+        uint32_t lwb = 0, lcur = lit_word(0), lnxt = lit_word(256);
         auto copy_lits = [&](uint32_t n2) -> bool {
             if (lp + n2 > nlit || n2 > o.olen - o.op) return false;
             for (uint32_t k = 0; k < n2; k += 64) {
+                while (lp + k >= lwb + 256) {
+                    lcur = lnxt;
+                    lwb += 256;
+                    lnxt = lit_word(lwb + 256);
+                }
                 const uint32_t nb = n2 - k < 64 ? n2 - k : 64;
-                const uint32_t v = lane < nb ? *(const __attribute__((address_space(1))) uint8_t*)(lit + lp + k + lane) : 0u;
+                const uint32_t wi = lp + k + lane - lwb;  // < 320
+                const uint32_t a = (uint32_t)__shfl((int)lcur, (int)((wi >> 2) & 63), 64);
+                const uint32_t b = (uint32_t)__shfl((int)lnxt, (int)((wi >> 2) & 63), 64);
+                const uint32_t v = ((wi < 256 ? a : b) >> ((wi & 3) * 8)) & 0xFFu;
                 o.put_if(lane < nb, o.op + k + lane, v);
                 o.flush(o.op + k + nb);
             }
@@ -553,17 +595,26 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         u = seq_table(in, wb, wb + ZD_ML, (modes >> 2) & 3, q, bend, c_ml_def, 53, 6, 52, 9, ml_log, have_ml, lane);
         if (u < 0) { bad = 29; break; }
         q += (uint32_t)u;
+        ZSD(const uint64_t b2 = __builtin_amdgcn_s_memtime(); ctab += b2 - b1; nseqs += nseq;)
         BitBack br;
         if (!br.init(in, q, bend)) { bad = 30; break; }
         uint32_t lls = br.read(in, ll_log), ofs = br.read(in, of_log), mls = br.read(in, ml_log);
         for (uint32_t i = 0; i < nseq; i++) {
-            const uint32_t le = zd32(wb + ZD_LL + 4 * lls), oe = zd32(wb + ZD_OF + 4 * ofs),
-                           me = zd32(wb + ZD_ML + 4 * mls);
+            ZSD(const uint64_t s0 = __builtin_amdgcn_s_memtime();)
+            // the sequence state is wave-uniform: keep it in SGPRs (see BitBack::pin)
+            br.pin();
+            lls = rfl(lls); ofs = rfl(ofs); mls = rfl(mls);
+            rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
+            lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed);
+            const uint32_t le = rfl(zd32(wb + ZD_LL + 4 * lls)), oe = rfl(zd32(wb + ZD_OF + 4 * ofs)),
+                           me = rfl(zd32(wb + ZD_ML + 4 * mls));
             const uint32_t llc = le & 0xFF, ofc = oe & 0xFF, mlc = me & 0xFF;
             if (llc > 35 || mlc > 52 || ofc > 31) { bad = 31; break; }
+            // the four code tables up front (scalar loads, one wait)
+            const uint32_t mlb = c_ml_base[mlc], mlx = c_ml_bits[mlc], llb = c_ll_base[llc], llx = c_ll_bits[llc];
             const uint32_t ofv = (1u << ofc) + br.read(in, ofc);
-            const uint32_t ml = c_ml_base[mlc] + br.read(in, c_ml_bits[mlc]);
-            const uint32_t ll = c_ll_base[llc] + br.read(in, c_ll_bits[llc]);
+            const uint32_t ml = mlb + br.read(in, mlx);
+            const uint32_t ll = llb + br.read(in, llx);
             uint32_t off;
             if (ofv > 3) {
                 off = ofv - 3;
@@ -588,21 +639,29 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
                 mls = (me >> 16) + br.read(in, (me >> 8) & 0xFF);
                 ofs = (oe >> 16) + br.read(in, (oe >> 8) & 0xFF);
             }
+            ZSD(cread += __builtin_amdgcn_s_memtime() - s0;)
+            ZSD(const uint64_t s1 = __builtin_amdgcn_s_memtime(); nfar += off > 4096; nlitrun += ll > 0;)
             if (!copy_lits(ll)) { bad = 32; break; }
+            ZSD(const uint64_t s2 = __builtin_amdgcn_s_memtime(); ccopy += s2 - s1;)
             if (!o.match(off, ml)) { bad = 33; break; }
+            ZSD(cmatch += __builtin_amdgcn_s_memtime() - s2;)
         }
         if (bad) break;
         if (br.pos != 0) { bad = 34; break; }
         if (!copy_lits(nlit - lp)) { bad = 35; break; }
+        ZSD(cseq += __builtin_amdgcn_s_memtime() - b2;)
         q = bend;
     }
+    ZSD(if (si == 0 && lane == 0) printf("[zstd] total %lu literals %lu tables %lu sequences %lu (read %lu copy %lu match %lu) blocks %u nlit %u nseq %u far %u litruns %u dlen %u\n",
+        (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)clit, (unsigned long)ctab,
+        (unsigned long)cseq, (unsigned long)cread, (unsigned long)ccopy, (unsigned long)cmatch, nblk, nlits, nseqs, nfar, nlitrun, t.dlen);)
     if (!bad && checksum) q += 4;
     if (!bad && (o.op != o.olen || q > ilen)) bad = 36;
     o.finish();
     if (lane == 0) err[si] = bad;
 }
 
-size_t zstd_scratch_bytes(uint32_t nstreams) { return (size_t)nstreams * ZSTD_LITBUF; }
+size_t zstd_scratch_bytes(uint32_t nstreams) { return (size_t)nstreams * ZSTD_LITSTRIDE; }
 
 hipError_t launch_zarr_zstd(hipStream_t st, const ZStream* d_streams, uint32_t n, const uint8_t* src,
                             uint8_t* scratch, uint8_t* litbuf, uint32_t* err) {
