@@ -597,3 +597,65 @@ def test_gpu_ngff_pyramid_one_call(service, tmp_path, b2r):
     for lvl in reg.values():
         for pid in lvl.values():
             service.release_plane(pid)
+
+
+def _corruptions(enc: bytes, seed: int, hdr: int):
+    """Deterministic damage to one compressed stream: byte flips after the header, a
+    truncation, or a garbage tail."""
+    rng = np.random.default_rng(seed)
+    b = bytearray(enc)
+    kind = seed % 4
+    if kind == 0:
+        for _ in range(int(rng.integers(1, 5))):
+            b[int(rng.integers(hdr, len(b)))] ^= int(rng.integers(1, 256))
+    elif kind == 1:
+        b = b[:int(rng.integers(hdr, len(b)))]
+    elif kind == 2:
+        k = int(rng.integers(hdr, len(b)))
+        b[k:] = rng.integers(0, 256, len(b) - k, dtype=np.uint8).tobytes()
+    else:
+        k = int(rng.integers(hdr, len(b) - 8))
+        b[k:k + 8] = b"\xff" * 8
+    return bytes(b)
+
+
+@gpu
+@pytest.mark.parametrize("codec", ["zlib1", "zlib9-fixed", "zlib6-rle", "blosc-zstd", "blosc-lz4", "blosc-blosclz"])
+def test_gpu_corrupt_streams_fuzz(service, codec):
+    """Damaged streams of every decoder (flipped bytes, truncation, garbage tails) either fail the
+    call with 400 or decode; a stream the CPU codec accepts decodes to the same bytes.  (No
+    fault, no hang: every decoder's loops are bounded by the stream and output lengths.)"""
+    import pbx
+    h, w = 96, 128
+    plane = _zarr.noise_plane(h, w, ">u2", seed=41) & 0x0FFF
+    raw = plane.tobytes()
+    if codec.startswith("zlib"):
+        level = int(codec[4])
+        strat = zlib.Z_FIXED if codec.endswith("fixed") else zlib.Z_RLE if codec.endswith("rle") else 0
+        co = zlib.compressobj(level, zlib.DEFLATED, 15, 9, strat)
+        enc, comp, hdr = co.compress(raw) + co.flush(), "zlib", 2
+        ref = lambda b: zlib.decompress(b)
+    else:
+        if _zarr.cblosc() is None:
+            pytest.skip("c-blosc not in this image")
+        enc, comp, hdr = _zarr.cblosc_encode(raw, 2, codec.split("-")[1], 5, 1), "blosc", 16
+        ref = lambda b: _zarr.cblosc_decode(b, len(raw))
+    ok = failed = 0
+    for seed in range(24):
+        bad = _corruptions(enc, seed, hdr)
+        try:
+            want = ref(bad)
+        except Exception:
+            want = None
+        try:
+            pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, w, h, w, h, comp, [bad])
+        except pbx.PbxError as e:
+            assert e.status == 400
+            failed += 1
+            continue
+        got = plane_be(service, pid, ">u2", h, w).tobytes()
+        service.release_plane(pid)
+        if want is not None and len(want) == len(raw):
+            assert got == want, seed
+        ok += 1
+    assert failed > 0
