@@ -824,7 +824,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
 // ==================================================================== k_huff
 // Ascending sort of the KEYN keys (padded to 512 with KEY_NONE) by one wave: 8 per lane (lane*8 + r), partners at distance
 // j >= 8 by shuffle, j < 8 inside the lane's registers.
-__device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
+__device__ __forceinline__ void sort512_wave(uint32_t* keys, uint32_t lane) {
     uint32_t v[8];
 #pragma unroll
     for (int r = 0; r < 8; r++) v[r] = lane * 8 + r < KEYN ? keys[lane * 8 + r] : KEY_NONE;
@@ -866,7 +866,7 @@ __device__ void sort512_wave(uint32_t* keys, uint32_t lane) {
 // steps of the serial merge and give exactly its records (twoqueue_serial in deflate_seg.h,
 // which the emulator runs): step s = li0 | qi0 << 10 | cnt << 20.
 template <class SM>
-__device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
+__device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
     const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
     const uint32_t* sk = S.hs.skey + base;
@@ -957,7 +957,7 @@ __device__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
 // Parents from the merge records (ph_parents without the pointer-jumping depths, which the
 // device does not use): leafpar of every leaf, aA of every internal node.
 template <class SM>
-__device__ void parents_wave(SM& S, uint32_t tid) {
+__device__ __forceinline__ void parents_wave(SM& S, uint32_t tid) {
     for (uint32_t i = tid; i < 320; i += 64) {
         uint32_t T, s;
         tree_slot(i, T, s);
@@ -975,7 +975,7 @@ __device__ void parents_wave(SM& S, uint32_t tid) {
 // round, so the rounds taken in reverse order each resolve in one parallel step (instead
 // of pointer jumping).  Result in dB, as ph_jump leaves it.
 template <class SM>
-__device__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
+__device__ __forceinline__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t nr = __builtin_amdgcn_readfirstlane(S.nrounds[T]);
     if (nr == 0) return;
     uint16_t* dd = S.hs.dB[T];
@@ -994,7 +994,7 @@ __device__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
 // leaf j of a tree gets the length L with end(L+1) <= j < end(L), end(L) = leaves of
 // length >= L.  Sums and maxima by wave reductions instead of same-address LDS atomics.
 template <class SM>
-__device__ void assign_wave(SM& S, uint32_t lane) {
+__device__ __forceinline__ void assign_wave(SM& S, uint32_t lane) {
     uint32_t e0[16], e1[16];
 #pragma unroll
     for (int L = 1; L < 16; L++) {
@@ -1048,7 +1048,7 @@ __device__ void assign_wave(SM& S, uint32_t lane) {
 // stable (freq, symbol) order, serial two-queue merge on lane-held arrays, depths, zlib's
 // overflow repair at 7 bits, longest codes to the least frequent, canonical codes.
 template <class SM>
-__device__ void clen_wave(SM& S, uint32_t lane) {
+__device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
     const bool sy = lane < 19;
     uint32_t f = sy ? S.hw.clfreq[lane] : 0u;
     {   // at least two used symbols: the first unused ones get frequency 1

@@ -548,12 +548,12 @@ constexpr uint32_t ZP_WIN = 0, ZP_LLUT = ZP_WINB, ZP_DLUT = ZP_LLUT + 2 * (1u <<
                    ZP_LSYMS = ZP_DLUT + 2 * (1u << ZPLUT), ZP_DSYMS = ZP_LSYMS + 2 * 288,
                    ZP_LENS = ZP_DSYMS + 2 * 32, ZP_NEXT = ZP_LENS + ZLENS, ZP_FIFO = ZP_NEXT + 64,
                    ZP_RING = ZP_FIFO + 4 * ZP_TOKQ, ZP_CTRL = ZP_RING + ZR_INF,
-                   ZP_TRASH = ZP_CTRL + 16,         // 4 bytes per lane: masked-off lanes' stores
+                   ZP_TRASH = ZP_CTRL + 32,         // 4 bytes per lane: masked-off lanes' stores
                    ZP_FLAG = ZP_TRASH + 256 + 64,   // the consumer's token-start flags (+ trash)
                    ZP_BYTES = ZP_FLAG + 128;        // per stream
 static_assert(ZP_BYTES <= 160 * 1024 / 3, "three streams (six waves) per CU");
 constexpr uint32_t ZP_STREAMS = 1;                  // streams (x 2 waves) per workgroup
-enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8, ZPC_DONE = 12 };
+enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8, ZPC_DONE = 12, ZPC_ADLER = 16 };
 constexpr uint32_t ZP_BATCH = 32;  // the consumer waits for this many tokens (or the end)
 
 __device__ __forceinline__ uint32_t zp_lext(uint32_t ls) { return ls < 8 || ls == 28 ? 0u : (ls - 4) >> 2; }
@@ -931,6 +931,12 @@ __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src
         bi.bits(bp & 7);
         if (!bad && bi.consumed_bytes() > bi.ilen) bad = 26;
     }
+    if (!bad) {  // RFC 1950 trailer: Adler-32 of the output, big-endian, at the next byte
+        const uint32_t q = (bi.ipos * 8 - bi.cnt + 7) >> 3;
+        if (q + 4 > bi.ilen) bad = 28;
+        else lds_store_volatile(sb + ZP_CTRL + ZPC_ADLER, bi.win.byte(q) << 24 | bi.win.byte(q + 1) << 16 |
+                                                              bi.win.byte(q + 2) << 8 | bi.win.byte(q + 3));
+    }
     ZDIAG(if (si == 0 && lane == 0) printf("[zp producer] total %lu hdr %lu data %lu blocks %u rounds %u stepsA %u syncs %u stepsB %u tokens %u stepsC %u\n",
                                            (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)chdr,
                                            (unsigned long)cdata, nblocks, dg[0], dg[1], dg[2], dg[3], dg[4], dg[5]);)
@@ -940,7 +946,7 @@ __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src
 
 __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src, uint8_t* dst, uint32_t sb, uint32_t lane,
                                             uint32_t* errp, uint32_t si) {
-    OutRing<ZR_INF> o{sb + ZP_RING, dst + t.dst_off, 0, 0, t.dlen, lane, sb + ZP_TRASH + 256};
+    OutRing<ZR_INF, true> o{sb + ZP_RING, dst + t.dst_off, 0, 0, t.dlen, lane, sb + ZP_TRASH + 256};
     const uint8_t* in = src + t.src_off;
     const uint32_t FLAG = sb + ZP_FLAG;
     uint32_t head = 0, code = 0;
@@ -1042,6 +1048,9 @@ __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src
     }
     if (!code && o.op != o.olen) code = 27;
     o.finish();
+    // the zlib trailer (stored by the producer before its end token): java.util.zip's
+    // Inflater fails such a stream too
+    if (!code && o.adler32() != lds_load_volatile(sb + ZP_CTRL + ZPC_ADLER)) code = 29;
     if (lane == 0) *errp = code;
     ZDIAG(if (si == 0 && lane == 0) printf("[zp consumer] total %lu wait %lu parallel %lu batches %u chunks %u jumps %u\n",
                                            (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)cwait,
@@ -1055,7 +1064,7 @@ __global__ __launch_bounds__(64 * 2 * ZP_STREAMS) void k_zarr_inflate2(const ZSt
     const uint32_t lane = threadIdx.x & 63, w = rfl(threadIdx.x >> 6);
     const uint32_t s = w >> 1, si = blockIdx.x * ZP_STREAMS + s;
     const uint32_t sb = s * ZP_BYTES;
-    if (lane < 4) lds32(sb + ZP_CTRL + 4 * lane) = 0;
+    if (lane < 8) lds32(sb + ZP_CTRL + 4 * lane) = 0;
     __syncthreads();
     if (si >= n) return;
     const ZStream t = st[si];

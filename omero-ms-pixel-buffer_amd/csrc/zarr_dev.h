@@ -81,13 +81,17 @@ struct InWin {
 // anywhere inside a decoder's symbol loop makes LLVM structurize the whole loop with exec
 // masks, which moves the (wave-uniform) stream state into VGPRs and every test on it into
 // v_cmp + s_and_saveexec code: several times the instructions per symbol.
-template <uint32_t RING>
+// With ADLER, every byte written to HBM also goes into the lane's Adler-32 partial sums
+// (sum of bytes, sum of position * byte; adler32() reduces them over the wave).
+template <uint32_t RING, bool ADLER = false>
 struct OutRing {
     static constexpr uint32_t ZM = RING - 1, ZR = RING;
     uint32_t rb;
     uint8_t* out;
     uint32_t op, flushed, olen, lane;
     uint32_t trash;  // LDS offset of 64 bytes
+    uint32_t asb = 0;  // (ADLER) this lane's bytes: sum
+    uint64_t asi = 0;  //          sum of position * byte
     __device__ uint8_t& ring(uint32_t pos) const { return zlds[rb + (pos & ZM)]; }
     __device__ void put_if(bool pred, uint32_t pos, uint32_t v) const {
         zlds[pred ? rb + (pos & ZM) : trash + lane] = (uint8_t)v;
@@ -98,14 +102,37 @@ struct OutRing {
         while (upto - f >= 256u) {
             const uint32_t v = *(const uint32_t*)(zlds + rb + ((f + 4 * lane) & ZM));
             __builtin_memcpy(out + f + 4 * lane, &v, 4);
+            if (ADLER) {
+                const uint32_t s = __builtin_amdgcn_udot4(v, 0x01010101u, 0u, false);
+                asb += s;
+                asi += (uint64_t)(f + 4 * lane) * s + __builtin_amdgcn_udot4(v, 0x03020100u, 0u, false);
+            }
             f += 256;
         }
         flushed = f;
     }
     __device__ void finish() {
-        for (uint32_t k = flushed; k < op; k += 64)
-            if (k + lane < op) out[k + lane] = ring(k + lane);
+        for (uint32_t k = flushed; k < op; k += 64) {
+            const uint32_t b = k + lane < op ? ring(k + lane) : 0u;
+            if (k + lane < op) out[k + lane] = (uint8_t)b;
+            if (ADLER) {
+                asb += b;
+                asi += (uint64_t)(k + lane) * b;
+            }
+        }
         flushed = op;
+    }
+    // (ADLER, after finish) Adler-32 of out[0, op): A = 1 + sum b, B = n + sum (n - i) b_i
+    __device__ uint32_t adler32() const {
+        uint64_t sb = asb, si = asi;
+        for (int o = 32; o > 0; o >>= 1) {
+            sb += (uint64_t)__shfl_xor((long long)sb, o, 64);
+            si += (uint64_t)__shfl_xor((long long)si, o, 64);
+        }
+        constexpr uint64_t M = 65521;
+        const uint64_t n = op % M, a = (1 + sb) % M;
+        const uint64_t b = (n + n * (sb % M) + M - si % M) % M;
+        return (uint32_t)(b << 16 | a);
     }
     // out[op .. op+len) = out[op-off .. op-off+len) (overlapping: period off)
     // lane % off for off < 64 without an integer division: lane / off is exact to within 1/63

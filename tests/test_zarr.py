@@ -659,3 +659,21 @@ def test_gpu_corrupt_streams_fuzz(service, codec):
             assert got == want, seed
         ok += 1
     assert failed > 0
+
+
+@gpu
+def test_gpu_zlib_adler_mismatch_is_400(service):
+    """A zlib stream whose deflate data is intact but whose Adler-32 trailer is wrong fails like
+    java.util.zip.Inflater ('incorrect data check'); the intact stream decodes."""
+    import pbx
+    plane = _zarr.noise_plane(64, 96, ">u2", seed=8)
+    enc = bytearray(zlib.compress(plane.tobytes(), 6))
+    pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 96, 64, 96, 64, "zlib", [bytes(enc)])
+    assert np.array_equal(plane_be(service, pid, ">u2", 64, 96), plane)
+    service.release_plane(pid)
+    enc[-1] ^= 1
+    with pytest.raises(zlib.error):
+        zlib.decompress(bytes(enc))
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 96, 64, 96, 64, "zlib", [bytes(enc)])
+    assert ei.value.status == 400
