@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dev_util.h"
 #include "pbx_kernels.h"
 #include "zarr_dev.h"
 
@@ -37,7 +38,8 @@ constexpr uint32_t ZD_SPREAD = ZD_NEXT + 1024;   // u8 spread symbols [512]
 constexpr uint32_t ZD_WGT = ZD_SPREAD + 512;     // u8 Huffman weights [256]
 constexpr uint32_t ZD_WT = ZD_WGT + 256;         // FSE table of the weights (<= 64 entries)
 constexpr uint32_t ZD_TRASH = ZD_WT + 64 * 4;    // the output ring's trash bytes (OutRing::put_if)
-constexpr uint32_t ZD_BYTES = ZD_TRASH + 64;
+constexpr uint32_t ZD_FLAG = ZD_TRASH + 64;       // sequence-start flags of a batch step (+ trash)
+constexpr uint32_t ZD_BYTES = ZD_FLAG + 128;
 
 __device__ __forceinline__ uint32_t& zd32(uint32_t off) { return *(uint32_t*)(zlds + off); }
 __device__ __forceinline__ uint16_t& zd16(uint32_t off) { return *(uint16_t*)(zlds + off); }
@@ -599,13 +601,85 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         BitBack br;
         if (!br.init(in, q, bend)) { bad = 30; break; }
         uint32_t lls = br.read(in, ll_log), ofs = br.read(in, of_log), mls = br.read(in, ml_log);
+        // Sequences are decoded into a batch (lane j: sequence j's literal length, match length
+        // and offset) and a batch of up to 64 is executed byte-parallel: output offsets by prefix
+        // sums, then 64 output bytes per step, each lane finding its sequence (start flags,
+        // ballot, mbcnt) and its byte: a literal (register window), a ring byte, an HBM byte
+        // (offsets beyond the ring) or, for a source inside the step, by pointer jumping.
+        uint32_t bll = 0, bml = 0, boff = 0, bn = 0;
+        auto exec_batch = [&]() -> bool {
+            const bool act = lane < bn;
+            const uint32_t sl = act ? bll + bml : 0u, sll = act ? bll : 0u;
+            const uint32_t end = wave_incl_add(sl, lane), st0 = end - sl;
+            const uint32_t lend = wave_incl_add(sll, lane), lst = lend - sll;
+            const uint32_t T = rdl(end, 63), TL = rdl(lend, 63);
+            const uint32_t op0 = o.op;
+            if (lp + TL > nlit || T > o.olen - op0) return false;
+            if (__ballot(act && (boff == 0 || boff > op0 + st0 + bll))) return false;  // before the frame start
+            const uint32_t FLAG = wb + ZD_FLAG;
+            uint32_t base = 0, lcnt = 0;
+            for (uint32_t cb = 0; cb < T; cb += 64) {
+                zlds[FLAG + lane] = 0;
+                const uint32_t rs = st0 - cb;
+                zlds[act && rs < 64 ? FLAG + rs : FLAG + 64 + lane] = 1;
+                const uint32_t f = zlds[FLAG + lane];
+                const uint64_t M = __ballot(f != 0);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0));
+                const uint32_t idx = base + below + f - 1;
+                base += (uint32_t)__popcll(M);
+                const uint32_t p = cb + lane;
+                const bool valid = p < T;
+                const uint32_t s_st = (uint32_t)__shfl((int)st0, (int)idx, 64), s_ll = (uint32_t)__shfl((int)bll, (int)idx, 64);
+                const uint32_t s_off = (uint32_t)__shfl((int)boff, (int)idx, 64), s_lst = (uint32_t)__shfl((int)lst, (int)idx, 64);
+                const uint32_t r = p - s_st;
+                const bool islit = r < s_ll;
+                // literals: the step's are consecutive, from literal lp + lcnt
+                while (lp + lcnt >= lwb + 256) {
+                    lcur = lnxt;
+                    lwb += 256;
+                    lnxt = lit_word(lwb + 256);
+                }
+                const uint32_t wi = lp + s_lst + r - lwb;  // < 320 on literal lanes
+                const uint32_t la = (uint32_t)__shfl((int)lcur, (int)((wi >> 2) & 63), 64);
+                const uint32_t lb2 = (uint32_t)__shfl((int)lnxt, (int)((wi >> 2) & 63), 64);
+                const uint32_t lv = ((wi < 256 ? la : lb2) >> ((wi & 3) * 8)) & 0xFFu;
+                lcnt += (uint32_t)__popcll(__ballot(valid && islit));
+                // match bytes
+                const uint32_t src = p - s_off;  // from op0 (may be < 0: an earlier batch)
+                const bool mt = valid && !islit;
+                const bool far = mt && s_off > 4096 - 64;  // below the ring: in HBM (flushed)
+                uint32_t v = o.ring(op0 + src);
+                if (__ballot(far)) {
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's flushes
+                    const uint32_t hv = *(const __attribute__((address_space(1))) uint8_t*)(o.out + (far ? op0 + src : 0u));
+                    v = far ? hv : v;
+                }
+                v = islit ? lv : v;
+                bool pend = mt && (int32_t)src >= (int32_t)cb;
+                uint32_t ptr = src - cb;
+                while (__ballot(pend)) {
+                    const uint32_t nv = (uint32_t)__shfl((int)v, (int)ptr, 64);
+                    const uint32_t np = (uint32_t)__shfl((int)pend, (int)ptr, 64);
+                    const uint32_t nq = (uint32_t)__shfl((int)ptr, (int)ptr, 64);
+                    v = pend && !np ? nv : v;
+                    ptr = pend && np ? nq : ptr;
+                    pend = pend && np;
+                }
+                o.put_if(valid, op0 + p, v);
+                o.flush(op0 + (T - cb < 64 ? T : cb + 64));
+            }
+            o.op = op0 + T;
+            lp += TL;
+            bn = 0;
+            return true;
+        };
         for (uint32_t i = 0; i < nseq; i++) {
             ZSD(const uint64_t s0 = __builtin_amdgcn_s_memtime();)
             // the sequence state is wave-uniform: keep it in SGPRs (see BitBack::pin)
             br.pin();
             lls = rfl(lls); ofs = rfl(ofs); mls = rfl(mls);
             rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
-            lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed);
+            lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed); bn = rfl(bn);
             const uint32_t le = rfl(zd32(wb + ZD_LL + 4 * lls)), oe = rfl(zd32(wb + ZD_OF + 4 * ofs)),
                            me = rfl(zd32(wb + ZD_ML + 4 * mls));
             const uint32_t llc = le & 0xFF, ofc = oe & 0xFF, mlc = me & 0xFF;
@@ -641,10 +715,15 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             }
             ZSD(cread += __builtin_amdgcn_s_memtime() - s0;)
             ZSD(const uint64_t s1 = __builtin_amdgcn_s_memtime(); nfar += off > 4096; nlitrun += ll > 0;)
-            if (!copy_lits(ll)) { bad = 32; break; }
-            ZSD(const uint64_t s2 = __builtin_amdgcn_s_memtime(); ccopy += s2 - s1;)
-            if (!o.match(off, ml)) { bad = 33; break; }
-            ZSD(cmatch += __builtin_amdgcn_s_memtime() - s2;)
+            bll = lane == bn ? ll : bll;
+            bml = lane == bn ? ml : bml;
+            boff = lane == bn ? off : boff;
+            bn++;
+            if (bn == 64 || i + 1 == nseq) {
+                bn = rfl(bn);
+                if (!exec_batch()) { bad = 33; break; }
+            }
+            ZSD(cmatch += __builtin_amdgcn_s_memtime() - s1;)
         }
         if (bad) break;
         if (br.pos != 0) { bad = 34; break; }
