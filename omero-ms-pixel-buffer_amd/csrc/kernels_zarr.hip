@@ -540,6 +540,9 @@ __global__ __launch_bounds__(256) void k_zarr_inflate(const ZStream* __restrict_
 // Tokens: literal 0x01000000 | byte; match 0x40000000 | (len - 3) << 16 | (dist - 1);
 // stored run 0x80000000 | len, then the run's input offset; end 0xC0000000 | error code.
 constexpr uint32_t ZP_TOKQ = 2048;                  // FIFO tokens per stream (power of two)
+// The consumer's output ring: half the deflate window.  Farther sources (1.2% of zlib-1's
+// matches on noise) are read back from HBM; the LDS saved is the fourth stream per CU.
+constexpr uint32_t ZP_RINGB = 16384;
 constexpr uint32_t ZPLUT = 10;                      // producer's first-level tables: codes <= 10 bits
 constexpr uint32_t ZP_WINB = 3072;                  // input window: a macro-round's 64 segments
 constexpr uint32_t ZP_SMAX = 256;                   // longest segment (bits): 8 * ZP_SMAX + 24 <= ZP_WINB
@@ -547,11 +550,11 @@ constexpr uint32_t ZP_SEGTOK = 24;                  // tokens per segment aimed 
 constexpr uint32_t ZP_WIN = 0, ZP_LLUT = ZP_WINB, ZP_DLUT = ZP_LLUT + 2 * (1u << ZPLUT),
                    ZP_LSYMS = ZP_DLUT + 2 * (1u << ZPLUT), ZP_DSYMS = ZP_LSYMS + 2 * 288,
                    ZP_LENS = ZP_DSYMS + 2 * 32, ZP_NEXT = ZP_LENS + ZLENS, ZP_FIFO = ZP_NEXT + 64,
-                   ZP_RING = ZP_FIFO + 4 * ZP_TOKQ, ZP_CTRL = ZP_RING + ZR_INF,
+                   ZP_RING = ZP_FIFO + 4 * ZP_TOKQ, ZP_CTRL = ZP_RING + ZP_RINGB,
                    ZP_TRASH = ZP_CTRL + 32,         // 4 bytes per lane: masked-off lanes' stores
                    ZP_FLAG = ZP_TRASH + 256 + 64,   // the consumer's token-start flags (+ trash)
                    ZP_BYTES = ZP_FLAG + 128;        // per stream
-static_assert(ZP_BYTES <= 160 * 1024 / 3, "three streams (six waves) per CU");
+static_assert(ZP_BYTES <= 160 * 1024 / 4, "four streams (eight waves) per CU");
 constexpr uint32_t ZP_STREAMS = 1;                  // streams (x 2 waves) per workgroup
 enum : uint32_t { ZPC_TAIL = 0, ZPC_HEAD = 4, ZPC_ABORT = 8, ZPC_DONE = 12, ZPC_ADLER = 16 };
 constexpr uint32_t ZP_BATCH = 32;  // the consumer waits for this many tokens (or the end)
@@ -946,7 +949,7 @@ __device__ __forceinline__ void zp_producer(const ZStream& t, const uint8_t* src
 
 __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src, uint8_t* dst, uint32_t sb, uint32_t lane,
                                             uint32_t* errp, uint32_t si) {
-    OutRing<ZR_INF, true> o{sb + ZP_RING, dst + t.dst_off, 0, 0, t.dlen, lane, sb + ZP_TRASH + 256};
+    OutRing<ZP_RINGB, true> o{sb + ZP_RING, dst + t.dst_off, 0, 0, t.dlen, lane, sb + ZP_TRASH + 256};
     const uint8_t* in = src + t.src_off;
     const uint32_t FLAG = sb + ZP_FLAG;
     uint32_t head = 0, code = 0;
@@ -997,8 +1000,17 @@ __device__ __forceinline__ void zp_consumer(const ZStream& t, const uint8_t* src
                     const uint32_t p = cb + lane;
                     const uint32_t ttok = (uint32_t)__shfl((int)tok, (int)idx, 64);
                     const bool valid = p < T, ismatch = (ttok >> 30) == 1;
-                    const uint32_t s = p - ((ttok & 0xFFFFu) + 1);  // source offset (from op0; may be < 0)
-                    const uint32_t rv = o.ring(op0 + s);
+                    const uint32_t dist = (ttok & 0xFFFFu) + 1;
+                    const uint32_t s = p - dist;  // source offset (from op0; may be < 0)
+                    uint32_t rv = o.ring(op0 + s);
+                    // a source more than a ring back lies below `flushed` (< 256 bytes stay
+                    // unflushed after a step): wait for this wave's stores, read it from HBM
+                    const bool far = valid && ismatch && dist > ZP_RINGB - 64;
+                    if (__ballot(far)) {
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                        const uint32_t hv = *(const __attribute__((address_space(1))) uint8_t*)(o.out + (far ? op0 + s : 0u));
+                        rv = far ? hv : rv;
+                    }
                     uint32_t v = ismatch ? rv : (ttok & 255u);
                     bool pend = valid && ismatch && (int32_t)s >= (int32_t)cb;
                     uint32_t ptr = s - cb;
