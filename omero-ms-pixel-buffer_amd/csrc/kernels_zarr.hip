@@ -29,9 +29,17 @@
 
 namespace pbx {
 
-constexpr uint32_t ZL_BYTES = ZR_LZ4 + ZWIN + 64;  // LZ4 / BloscLZ per wave: ring, window, trash
+constexpr uint32_t ZL_BYTES = ZR_LZ4 + ZWIN + 64 + 128 + 1024;  // LZ4 / BloscLZ per wave: ring, window, trash, flags, batch
 
 // ------------------------------------------------------------------------------ LZ4
+// Most LZ4 sequences of image data are short (a few literals, a 4..18-byte match): one wave
+// walking them one by one spends ~900 cycles on each, two LDS round trips in a chain.  Here
+// they are parsed 64 input offsets at a time: lane k reads the sequence that would start k
+// bytes on (token, literal count, offset: one round of LDS reads), a scalar walk from offset 0
+// picks the real ones (a readlane and an add each), and their fields go to an LDS batch of up
+// to 64 sequences executed by seq_batch (byte-parallel output steps).  Sequences with
+// length-extension bytes (long literal runs or matches) and the final literals take the
+// per-sequence path after the pending batch.
 __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st, uint32_t n,
                                                   const uint8_t* __restrict__ src,
                                                   uint8_t* __restrict__ dst, uint32_t* __restrict__ err) {
@@ -44,112 +52,146 @@ __global__ __launch_bounds__(256) void k_zarr_lz4(const ZStream* __restrict__ st
     InWin win{src + t.src_off, wb + ZR_LZ4, 0, lane};
     win.load(0);
     OutRing<ZR_LZ4> o{wb, dst + t.dst_off, 0, 0, t.dlen, lane, wb + ZR_LZ4 + ZWIN};
-#ifdef PBX_ZARR_CLOCKS  // diagnostic build: shader clocks and real time of stream 0
-    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t nseq = 0;
+    const uint32_t FLAG = wb + ZR_LZ4 + ZWIN + 64, BATCH = FLAG + 128;  // batch: ll, ml, off, src x 64
+    uint32_t ip = 0, bad = 0, bn = 0;
+#ifdef PBX_ZARR_CLOCKS  // diagnostic build: stream 0's clocks
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+    uint64_t cexec = 0, cgen = 0;
+    uint32_t nbat = 0, nseq = 0, ngen = 0, nround = 0;
+#define ZLC(...) __VA_ARGS__
+#else
+#define ZLC(...)
 #endif
-    uint32_t ip = 0, bad = 0;
-    // the sequence header (token, length bytes, offset) usually lies in these 16 bytes; the
-    // next one is fetched while a short match's ring read is in flight (one LDS round trip
-    // per sequence)
-    uint32_t h[4];
-    win.peek16(0, h);
+    auto flush_batch = [&]() -> bool {
+        bn = rfl(bn);
+        if (!bn) return true;
+        ZLC(const uint64_t x0 = __builtin_amdgcn_s_memtime(); nbat++;)
+        const uint32_t bll = lds32(BATCH + 4 * lane), bml = lds32(BATCH + 256 + 4 * lane);
+        const uint32_t boff = lds32(BATCH + 512 + 4 * lane), bsrc = lds32(BATCH + 768 + 4 * lane);
+        const uint32_t wo = win.wo, wbase = win.base;
+        const bool ok = seq_batch(o, FLAG, lane, bn, bll, bml, boff, bsrc,
+                                  [&](uint32_t pos, uint32_t, bool) -> uint32_t {
+            const uint32_t at = pos - wbase;  // literals of the batch lie in the LDS window
+            return zlds[wo + (at < ZWIN ? at : 0u)];
+        });
+        bn = 0;
+        ZLC(cexec += __builtin_amdgcn_s_memtime() - x0;)
+        return ok;
+    };
     for (;;) {
+        ip = rfl(ip); bn = rfl(bn); o.op = rfl(o.op); o.flushed = rfl(o.flushed);
         if (ip >= ilen) { bad = 1; break; }
-        auto hb = [&](uint32_t k) -> uint32_t {  // byte ip + k (k uniform)
-            if (k >= 16) return win.byte(ip + k);
-            const uint32_t d = k < 4 ? h[0] : k < 8 ? h[1] : k < 12 ? h[2] : h[3];
-            return (d >> ((k & 3) * 8)) & 0xffu;
-        };
-        const uint32_t tok = h[0] & 0xffu;
-        {
-            // common sequence: no length-extension bytes, <= 13 literals, so the literals and
-            // the offset all lie in the 16 header bytes already in SGPRs
-            const uint32_t ll0 = tok >> 4, ml0 = tok & 15;
-            if (ll0 <= 13 && ml0 < 15 && ilen - ip >= 3 + ll0 && ll0 <= o.olen - o.op) {
-                if (ll0) {
-                    const uint32_t bsel = 1 + lane, ws = bsel >> 2;
-                    const uint32_t wv = ws == 0 ? h[0] : ws == 1 ? h[1] : ws == 2 ? h[2] : h[3];
-                    o.put_if(lane < ll0, o.op + lane, (wv >> ((bsel & 3) * 8)));
-                    o.op += ll0;  // flushed with the match below (the ring has room)
-                }
-                const uint32_t off = hb(1 + ll0) | hb(2 + ll0) << 8, len = ml0 + 4;
-                ip += 3 + ll0;
-                if (off != 0 && off <= ZR_LZ4 && off <= o.op && len <= o.olen - o.op) {
-                    const uint32_t rep = o.period_lane(off);
-                    const uint32_t v = o.ring(o.op - off + rep);
-                    win.peek16(ip, h);
-                    o.put_if(lane < len, o.op + lane, v);
-                    o.op += len;
-                    o.flush(o.op);
-                } else {
-                    o.flush(o.op);
-                    if (!o.match(off, len)) { bad = 6; break; }
-                    win.peek16(ip, h);
-                }
-                continue;
-            }
+        // the LDS window covers the 64 candidate starts and their headers and literals
+        // (<= 17 bytes each); the batch's literals lie behind ip in it
+        if (ip + 64 + 20 > win.base + ZWIN) {
+            if (!flush_batch()) { bad = 6; break; }
+            win.load(ip);
         }
-        uint32_t k = 1, ll = tok >> 4;
-        if (ll == 15) {
+        // lane k: the sequence starting at ip + k, if it is a short one
+        const uint32_t q = ip + lane, qa = q - win.base;
+        const uint32_t h = ld_u32_unaligned(zlds + win.wo + (qa < ZWIN - 4 ? qa : ZWIN - 4));
+        const uint32_t tok = h & 0xFFu, ll = tok >> 4, ml0 = tok & 15;
+        const uint32_t oa = qa + 1 + ll;
+        const uint32_t off = ld_u32_unaligned(zlds + win.wo + (oa < ZWIN - 4 ? oa : ZWIN - 4)) & 0xFFFFu;
+        const bool ok = ll < 15 && ml0 < 15 && q + 3 + ll <= ilen && q + 1 + ll != ilen;
+        const uint32_t nx = (lane + 3 + ll) | (ok ? 0u : 0x100u);
+        // the walk: real sequence starts (at most 64 - bn of them)
+        uint64_t M = 0;
+        uint32_t p = 0, cnt = 0;
+        const uint32_t cap = 64 - bn;
+        while (p < 64 && cnt < cap) {
+            const uint32_t v = rdl(nx, p);
+            if (v & 0x100u) break;
+            M |= 1ull << p;
+            cnt++;
+            p = v;
+        }
+        ZLC(nround++; nseq += cnt;)
+        if (cnt) {
+            const uint32_t rank = bn + __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0));
+            const bool in = (M >> lane) & 1;
+            const uint32_t slot = in ? BATCH + 4 * rank : FLAG + 64;  // (masked-off lanes: trash)
+            lds32(slot) = ll;
+            lds32(slot + (in ? 256u : 0u)) = ml0 + 4;
+            lds32(slot + (in ? 512u : 0u)) = off;
+            lds32(slot + (in ? 768u : 0u)) = q + 1;
+            bn += cnt;
+            ip += p;
+            if (bn == 64 && !flush_batch()) { bad = 6; break; }
+            continue;
+        }
+        // a sequence with length-extension bytes (or the final literals): parsed serially; it
+        // joins the batch when it is short enough and its literals lie in the LDS window, else
+        // (a long literal run or match, or the end) the batch is executed and it is copied here
+        ZLC(const uint64_t g0 = __builtin_amdgcn_s_memtime(); ngen++;)
+        auto sbyte = [&](uint32_t qq) -> uint32_t {  // (the batch's literals must stay in the window)
+            if (qq - win.base > ZWIN - 1 && !flush_batch()) bad = 6;
+            return win.byte(qq);
+        };
+        const uint32_t t0 = sbyte(ip);
+        if (bad) break;
+        uint32_t k = 1, lln = t0 >> 4;
+        if (lln == 15) {
             uint32_t b;
             do {
                 if (ip + k >= ilen) { bad = 2; break; }
-                b = hb(k++);
-                ll += b;
+                b = sbyte(ip + k++);
+                lln += b;
             } while (b == 255);
             if (bad) break;
         }
         const uint32_t ls = ip + k;
-        if (ll > ilen - ls || ll > o.olen - o.op) { bad = 3; break; }
-        for (uint32_t c = 0; c < ll; c += 64) {
-            const uint32_t nb = ll - c < 64 ? ll - c : 64;
+        if (lln > ilen - ls || lln > o.olen - o.op) { bad = 3; break; }
+        const bool final = ls + lln == ilen;
+        uint32_t ml = t0 & 15, off2 = 0;
+        if (!final) {
+            if (ilen - (ls + lln) < 2) { bad = 4; break; }
+            k += lln;  // offset at ip + k
+            off2 = sbyte(ip + k) | sbyte(ip + k + 1) << 8;
+            k += 2;
+            if (ml == 15) {
+                uint32_t b;
+                do {
+                    if (ip + k >= ilen) { bad = 5; break; }
+                    b = sbyte(ip + k++);
+                    ml += b;
+                } while (b == 255);
+                if (bad) break;
+            }
+            if (bad) break;
+            // (long matches copy faster on the per-sequence path: 64 bytes a step without the
+            // batch's bookkeeping, 1 KiB per HBM round trip when far)
+            if (ml + 4 <= 256 && lln <= 256 && ls >= win.base && ls + lln + 24 <= win.base + ZWIN) {
+                const uint32_t slot = lane == 0 ? BATCH + 4 * rfl(bn) : FLAG + 64;
+                lds32(slot) = lln;
+                lds32(slot + (lane == 0 ? 256u : 0u)) = ml + 4;
+                lds32(slot + (lane == 0 ? 512u : 0u)) = off2;
+                lds32(slot + (lane == 0 ? 768u : 0u)) = ls;
+                bn++;
+                ip += k;
+                ZLC(cgen += __builtin_amdgcn_s_memtime() - g0;)
+                if (bn == 64 && !flush_batch()) { bad = 6; break; }
+                continue;
+            }
+        }
+        if (!flush_batch()) { bad = 6; break; }
+        for (uint32_t c = 0; c < lln; c += 64) {
+            const uint32_t nb = lln - c < 64 ? lln - c : 64;
             const uint32_t v = win.lane_byte(ls + c);
             o.put_if(lane < nb, o.op + c + lane, v);
             o.flush(o.op + c + nb);
         }
-        o.op += ll;
-        if (ls + ll == ilen) { ip = ilen; break; }
-        if (ilen - (ls + ll) < 2) { bad = 4; break; }
-        uint32_t ml = tok & 15;
-        k += ll;  // offset at ip + k
-        const uint32_t off = hb(k) | hb(k + 1) << 8;
-        k += 2;
-        if (ml == 15) {
-            uint32_t b;
-            do {
-                if (ip + k >= ilen) { bad = 5; break; }
-                b = hb(k++);
-                ml += b;
-            } while (b == 255);
-            if (bad) break;
-        }
+        o.op += lln;
+        if (final) { ip = ilen; break; }
         ip += k;
-#ifdef PBX_ZARR_CLOCKS
-        nseq++;
-#endif
-        const uint32_t len = ml + 4;
-        if (len <= 64 && off <= ZR_LZ4 && off != 0 && off <= o.op && len <= o.olen - o.op) {
-            const uint32_t rep = o.period_lane(off);
-            const uint32_t v = o.ring(o.op - off + rep);
-            win.peek16(ip, h);
-            o.put_if(lane < len, o.op + lane, v);
-            o.op += len;
-            o.flush(o.op);
-        } else {
-            if (!o.match(off, len)) { bad = 6; break; }
-            win.peek16(ip, h);
-        }
+        if (!o.match(off2, ml + 4)) { bad = 6; break; }
+        ZLC(cgen += __builtin_amdgcn_s_memtime() - g0;)
+        if (ip < ilen && (ip < win.base || ip + 84 > win.base + ZWIN)) win.load(ip);
     }
     if (!bad && o.op != o.olen) bad = 7;
     o.finish();
-#ifdef PBX_ZARR_CLOCKS
-    if (lane == 0 && (si == 0 || si == 1)) {
-        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        printf("lz4 stream %u: %u sequences, %u bytes, %llu shader clocks, %llu realtime ticks\n", si, nseq,
-               o.op, (unsigned long long)(t1 - t0), (unsigned long long)(r1 - r0));
-    }
-#endif
+    ZLC(if (lane == 0 && si < 2) printf("lz4 stream %u: total %lu exec %lu (%u batches, %u sequences, %u rounds) per-sequence path %lu (%u)\n", si,
+        (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)cexec, nbat, nseq, nround, (unsigned long)cgen, ngen);)
     if (lane == 0) err[si] = bad;
 }
 
@@ -223,12 +265,6 @@ struct HTab {
     uint32_t first, count, offs;
     uint32_t syms;  // LDS byte offset of the sorted symbol list (uint16)
 };
-__device__ __forceinline__ uint16_t& lds16(uint32_t byte_off) {
-    return *(uint16_t*)(zlds + byte_off);
-}
-__device__ __forceinline__ uint32_t& lds32(uint32_t byte_off) {
-    return *(uint32_t*)(zlds + byte_off);
-}
 
 struct BitIn {
     InWin win;

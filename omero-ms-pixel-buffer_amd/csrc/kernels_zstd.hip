@@ -608,70 +608,27 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         // (offsets beyond the ring) or, for a source inside the step, by pointer jumping.
         uint32_t bll = 0, bml = 0, boff = 0, bn = 0;
         auto exec_batch = [&]() -> bool {
-            const bool act = lane < bn;
-            const uint32_t sl = act ? bll + bml : 0u, sll = act ? bll : 0u;
-            const uint32_t end = wave_incl_add(sl, lane), st0 = end - sl;
-            const uint32_t lend = wave_incl_add(sll, lane), lst = lend - sll;
-            const uint32_t T = rdl(end, 63), TL = rdl(lend, 63);
-            const uint32_t op0 = o.op;
-            if (lp + TL > nlit || T > o.olen - op0) return false;
-            if (__ballot(act && (boff == 0 || boff > op0 + st0 + bll))) return false;  // before the frame start
-            const uint32_t FLAG = wb + ZD_FLAG;
-            uint32_t base = 0, lcnt = 0;
-            for (uint32_t cb = 0; cb < T; cb += 64) {
-                zlds[FLAG + lane] = 0;
-                const uint32_t rs = st0 - cb;
-                zlds[act && rs < 64 ? FLAG + rs : FLAG + 64 + lane] = 1;
-                const uint32_t f = zlds[FLAG + lane];
-                const uint64_t M = __ballot(f != 0);
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0));
-                const uint32_t idx = base + below + f - 1;
-                base += (uint32_t)__popcll(M);
-                const uint32_t p = cb + lane;
-                const bool valid = p < T;
-                const uint32_t s_st = (uint32_t)__shfl((int)st0, (int)idx, 64), s_ll = (uint32_t)__shfl((int)bll, (int)idx, 64);
-                const uint32_t s_off = (uint32_t)__shfl((int)boff, (int)idx, 64), s_lst = (uint32_t)__shfl((int)lst, (int)idx, 64);
-                const uint32_t r = p - s_st;
-                const bool islit = r < s_ll;
-                // literals: the step's are consecutive, from literal lp + lcnt
-                while (lp + lcnt >= lwb + 256) {
-                    lcur = lnxt;
-                    lwb += 256;
-                    lnxt = lit_word(lwb + 256);
-                }
-                const uint32_t wi = lp + s_lst + r - lwb;  // < 320 on literal lanes
-                const uint32_t la = (uint32_t)__shfl((int)lcur, (int)((wi >> 2) & 63), 64);
-                const uint32_t lb2 = (uint32_t)__shfl((int)lnxt, (int)((wi >> 2) & 63), 64);
-                const uint32_t lv = ((wi < 256 ? la : lb2) >> ((wi & 3) * 8)) & 0xFFu;
-                lcnt += (uint32_t)__popcll(__ballot(valid && islit));
-                // match bytes
-                const uint32_t src = p - s_off;  // from op0 (may be < 0: an earlier batch)
-                const bool mt = valid && !islit;
-                const bool far = mt && s_off > 4096 - 64;  // below the ring: in HBM (flushed)
-                uint32_t v = o.ring(op0 + src);
-                if (__ballot(far)) {
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's flushes
-                    const uint32_t hv = *(const __attribute__((address_space(1))) uint8_t*)(o.out + (far ? op0 + src : 0u));
-                    v = far ? hv : v;
-                }
-                v = islit ? lv : v;
-                bool pend = mt && (int32_t)src >= (int32_t)cb;
-                uint32_t ptr = src - cb;
-                while (__ballot(pend)) {
-                    const uint32_t nv = (uint32_t)__shfl((int)v, (int)ptr, 64);
-                    const uint32_t np = (uint32_t)__shfl((int)pend, (int)ptr, 64);
-                    const uint32_t nq = (uint32_t)__shfl((int)ptr, (int)ptr, 64);
-                    v = pend && !np ? nv : v;
-                    ptr = pend && np ? nq : ptr;
-                    pend = pend && np;
-                }
-                o.put_if(valid, op0 + p, v);
-                o.flush(op0 + (T - cb < 64 ? T : cb + 64));
-            }
-            o.op = op0 + T;
+            const uint32_t sll = lane < bn ? bll : 0u;
+            const uint32_t lend = wave_incl_add(sll, lane), lst = lend - sll;  // literal index of each sequence
+            const uint32_t TL = rdl(lend, 63);
+            if (lp + TL > nlit) return false;
+            const bool ok = seq_batch(o, wb + ZD_FLAG, lane, bn, bll, bml, boff, lst,
+                                      [&](uint32_t li, uint32_t lfirst, bool any) -> uint32_t {
+                // literal lp + li from the register window (the step's are consecutive)
+                if (any)
+                    while (lp + lfirst >= lwb + 256) {
+                        lcur = lnxt;
+                        lwb += 256;
+                        lnxt = lit_word(lwb + 256);
+                    }
+                const uint32_t wi = lp + li - lwb;  // < 320 on literal lanes
+                const uint32_t a = (uint32_t)__shfl((int)lcur, (int)((wi >> 2) & 63), 64);
+                const uint32_t b2 = (uint32_t)__shfl((int)lnxt, (int)((wi >> 2) & 63), 64);
+                return ((wi < 256 ? a : b2) >> ((wi & 3) * 8)) & 0xFFu;
+            });
             lp += TL;
             bn = 0;
-            return true;
+            return ok;
         };
         for (uint32_t i = 0; i < nseq; i++) {
             ZSD(const uint64_t s0 = __builtin_amdgcn_s_memtime();)

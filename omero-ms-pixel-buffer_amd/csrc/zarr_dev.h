@@ -5,10 +5,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dev_util.h"
+
 namespace pbx {
 
 constexpr uint32_t ZR_INF = 32768;           // inflate: the whole deflate window (no far match reads HBM)
-constexpr uint32_t ZR_LZ4 = 4096;            // LZ4: smaller ring, more waves per CU
+constexpr uint32_t ZR_LZ4 = 4096;            // LZ4 / BloscLZ ring: more waves per CU
 constexpr uint32_t ZWAVES = 4;              // waves per workgroup
 constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes of <= 9 bits
 
@@ -16,6 +18,12 @@ constexpr uint32_t ZLUT = 9;                // inflate first-level lookup: codes
 // become a FLAT pointer; a selected one, a stack slot).  Per wave: ring, then (inflate) tables.
 extern __shared__ uint8_t zlds[];
 
+__device__ __forceinline__ uint16_t& lds16(uint32_t byte_off) {
+    return *(uint16_t*)(zlds + byte_off);
+}
+__device__ __forceinline__ uint32_t& lds32(uint32_t byte_off) {
+    return *(uint32_t*)(zlds + byte_off);
+}
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
@@ -146,12 +154,22 @@ struct OutRing {
         if (off == 0 || off > op || len > olen - op) return false;
         const uint32_t rep = period_lane(off);
         if (off > ZR) {
-            // a far source lies below `flushed`: wait for this wave's stores, read HBM
-            for (uint32_t k = 0; k < len; k += 64) {
-                const uint32_t p = op + k, n = len - k < 64 ? len - k : 64;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                const uint32_t v = *(const __attribute__((address_space(1))) uint8_t*)(out + p - off + rep);
-                put_if(lane < n, p + lane, v);
+            // A far source lies well below `flushed`: read it back from HBM, 1 KiB per round
+            // trip (16 bytes a lane; off > ZR >= 4096 > 1024, so a chunk never overlaps its
+            // source).  Its bytes end before p - 3072 while the last 8 flush stores (one per
+            // 256 bytes) cover bytes >= p - 2303: vmcnt(8) (in-order completion on gfx9)
+            // waits for the stores of the source and not for the latest ones.
+            static_assert(ZR >= 4096, "far chunks of 1 KiB behind the last 8 flushes");
+            for (uint32_t k = 0; k < len; k += 1024) {
+                const uint32_t p = op + k, n = len - k < 1024 ? len - k : 1024;
+                __builtin_amdgcn_s_waitcnt(0xF78);  // vmcnt(8), expcnt / lgkmcnt unconstrained
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const v4u q = *(const __attribute__((address_space(1))) v4u*)(out + p - off + 16 * lane);
+#pragma unroll
+                for (uint32_t b = 0; b < 16; b++) {
+                    const uint32_t wv = b < 4 ? q.x : b < 8 ? q.y : b < 12 ? q.z : q.w;
+                    put_if(16 * lane + b < n, p + 16 * lane + b, wv >> ((b & 3) * 8));
+                }
                 flush(p + n);
             }
         } else {
@@ -174,5 +192,88 @@ struct OutRing {
     }
 };
 
+
+// Byte-parallel execution of a batch of up to 64 LZ77 sequences (LZ4, zstd): lane j holds
+// sequence j = bll literals (source positions bsrc, bsrc + 1, ...) then bml bytes copied from
+// boff back; no sequence is empty.  Output offsets by a prefix sum, then 64 output bytes per
+// step: each lane finds its sequence (start flags in LDS at `flag`, ballot, mbcnt) and its
+// byte: a literal (lit(position, step's first literal position, any literal in the step),
+// called by every lane), a ring byte, an HBM byte (offsets beyond the ring, one round trip
+// for the step), or a byte of the same step (pointer jumping).  False if a match reaches
+// before the stream start or the output overflows.
+template <uint32_t RING, bool ADL, class LitF>
+__device__ bool seq_batch(OutRing<RING, ADL>& o, uint32_t flag, uint32_t lane, uint32_t bn, uint32_t bll,
+                          uint32_t bml, uint32_t boff, uint32_t bsrc, LitF&& lit) {
+    const bool act = lane < bn;
+    const uint32_t sl = act ? bll + bml : 0u;
+    const uint32_t end = wave_incl_add(sl, lane), st0 = end - sl;
+    const uint32_t T = rdl(end, 63);
+    const uint32_t op0 = rfl(o.op);
+    if (T > o.olen - op0) return false;
+    if (__ballot(act && bml != 0 && (boff == 0 || boff > op0 + st0 + bll))) return false;
+    uint32_t base = 0;
+    for (uint32_t cb = 0; cb < T; cb += 64) {
+        zlds[flag + lane] = 0;
+        const uint32_t rs = st0 - cb;
+        zlds[act && rs < 64 ? flag + rs : flag + 64 + lane] = 1;
+        const uint32_t f = zlds[flag + lane];
+        const uint64_t M = __ballot(f != 0);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0));
+        const uint32_t idx = base + below + f - 1;
+        base += (uint32_t)__popcll(M);
+        const uint32_t p = cb + lane;
+        const bool valid = p < T;
+        const uint32_t s_st = (uint32_t)__shfl((int)st0, (int)idx, 64), s_ll = (uint32_t)__shfl((int)bll, (int)idx, 64);
+        const uint32_t s_off = (uint32_t)__shfl((int)boff, (int)idx, 64), s_src = (uint32_t)__shfl((int)bsrc, (int)idx, 64);
+        const uint32_t r = p - s_st;
+        const bool islit = valid && r < s_ll;
+        const uint64_t L = __ballot(islit);
+        const uint32_t lpos = s_src + r;
+        const uint32_t lfirst = L ? rdl(lpos, (uint32_t)__builtin_ctzll(L)) : 0u;
+        const uint32_t lv = lit(lpos, lfirst, L != 0);
+        const bool mt = valid && !islit;
+        // a match byte's source; for a period s_off < 64 the copy of it in the first period
+        // (before the match), so that runs do not chain through the step byte by byte
+        const uint32_t rm = r - s_ll;
+        uint32_t rep = rm;
+        if (__ballot(mt && s_off < 64)) {
+            const uint32_t d = s_off ? s_off : 1u;
+            const uint32_t qq = (uint32_t)((float)rm * __builtin_amdgcn_rcpf((float)d));
+            int32_t rr = (int32_t)(rm - qq * d);
+            rr = rr < 0 ? rr + (int32_t)d : rr;
+            rr = rr < 0 ? rr + (int32_t)d : rr;
+            rr = rr >= (int32_t)d ? rr - (int32_t)d : rr;
+            rr = rr >= (int32_t)d ? rr - (int32_t)d : rr;
+            rep = s_off < 64 ? (uint32_t)rr : rm;
+        }
+        const uint32_t src = s_st + s_ll + rep - s_off;  // from op0 (may be < 0: an earlier batch)
+        // below the ring: in HBM, under `flushed` (< 256 bytes stay unflushed after a step).
+        // The source ends before p - (RING - 64) <= cb - 3968 while the last 8 flush stores
+        // cover bytes >= cb - 2303: vmcnt(8) (in-order completion) waits for its stores only.
+        static_assert(RING >= 4096, "far sources behind the last 8 flushes");
+        const bool far = mt && s_off > RING - 64;
+        uint32_t v = o.ring(op0 + src);
+        if (__ballot(far)) {
+            __builtin_amdgcn_s_waitcnt(0xF78);  // vmcnt(8), expcnt / lgkmcnt unconstrained
+            const uint32_t hv = *(const __attribute__((address_space(1))) uint8_t*)(o.out + (far ? op0 + src : 0u));
+            v = far ? hv : v;
+        }
+        v = islit ? lv : v;
+        bool pend = mt && (int32_t)src >= (int32_t)cb;
+        uint32_t ptr = src - cb;
+        while (__ballot(pend)) {
+            const uint32_t nv = (uint32_t)__shfl((int)v, (int)ptr, 64);
+            const uint32_t np = (uint32_t)__shfl((int)pend, (int)ptr, 64);
+            const uint32_t nq = (uint32_t)__shfl((int)ptr, (int)ptr, 64);
+            v = pend && !np ? nv : v;
+            ptr = pend && np ? nq : ptr;
+            pend = pend && np;
+        }
+        o.put_if(valid, op0 + p, v);
+        o.flush(op0 + (T - cb < 64 ? T : cb + 64));
+    }
+    o.op = op0 + T;
+    return true;
+}
 
 }  // namespace pbx
