@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 4
+#define PBX_ABI_VERSION 5
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -253,6 +253,16 @@ int pbx_release_cached(pbx_ctx* ctx);
 
 /* Synchronise the context's device (bench/test hook). */
 int pbx_device_synchronize(pbx_ctx* ctx);
+
+/* Pipelined batches (pbx_batch_launch, pbx_submit) with deflate work alternate over
+ * `streams` kernel streams (1..4; default 3, or $PBX_KSTREAMS), each starting behind the
+ * previous batch's stage `stagger` (1 = after its k_lz77 (default), 2 k_huff, 3 the
+ * offsets scan, 4 k_encode; 0 = no wait), so one batch's latency-bound phases overlap
+ * the next batch's kernels.  streams = 1: every batch in launch order on one stream
+ * (per-kernel timings then have no overlap).  Synchronous calls (pbx_get_tile(s)) and
+ * batches without deflate work always use the one stream.  No reference counterpart
+ * (the reference runs one request per worker thread). */
+int pbx_set_kernel_streams(pbx_ctx* ctx, int32_t streams, int32_t stagger);
 
 /* sizeof of the ABI structs, for bindings to check their layouts: pbx_config,
  * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats (in that order). */

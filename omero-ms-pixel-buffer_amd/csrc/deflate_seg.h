@@ -463,8 +463,12 @@ PBX_HD void ph_leafdepth(uint32_t tid, SM& S) {
     for (uint32_t i = tid; i < 320; i += C::HT) {
         uint32_t T, j;
         tree_slot(i, T, j);
-        if (j >= tree_n(S.misc, T)) continue;
+        const uint32_t n = tree_n(S.misc, T);
+        if (j >= n) continue;
         auto& H = S.hs;
+        // zlib's overflow count (trees.c gen_bitlen) is over every node deeper than 15,
+        // internal ones included: counting leaves only under-repairs deep trees
+        if (j + 1 < n && H.dB[T][j] > 15) Ops::add(&S.hover[T], 1u);
         uint32_t d = H.dB[T][H.leafpar[T][j]] + 1;
         if (d > 15) { d = 15; Ops::add(&S.hover[T], 1u); }
         Ops::add(&S.hblc[T][d], 1u);
@@ -551,7 +555,8 @@ PBX_HD void huff_lengths_small(const uint32_t* wsorted, const uint32_t* sorted, 
     w[root] = 0;
     for (uint32_t i = root; i-- > 0;) w[i] = w[parent[i]] + 1;
     for (uint32_t b = 0; b < 16; b++) hw.blc[b] = 0;
-    int overflow = 0;
+    int overflow = 0;  // every node deeper than maxbits, internal ones included (zlib)
+    for (uint32_t i = n; i < root; i++) overflow += w[i] > maxbits ? 1 : 0;
     for (uint32_t i = 0; i < n; i++) {
         uint32_t d = w[i];
         if (d > maxbits) { d = maxbits; overflow++; }

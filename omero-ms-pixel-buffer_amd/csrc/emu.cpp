@@ -207,6 +207,8 @@ extern "C" {
 int pbxemu_seg_bytes(void) { return C::SEG; }
 int pbxemu_win_bytes(void) { return C::WIN; }
 int pbxemu_threads(void) { return C::NT; }
+int pbxemu_blk_segs(void) { return (int)BLK_SEGS; }
+int pbxemu_split_max(void) { return (int)SPLIT_MAX; }
 
 // Deflate `len` bytes into a zlib stream exactly as the batch pipeline does for one tile
 // (segments of seg_len_for(len) bytes, window, per-segment blocks, combined Adler-32).

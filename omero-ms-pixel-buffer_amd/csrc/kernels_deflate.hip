@@ -1100,7 +1100,8 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
     }
     // bit-length counts (lane L holds blc[L]) and overflow repair
     const bool leaf = lane < ncl;
-    const uint32_t over = (uint32_t)__builtin_popcountll(__ballot(leaf && dv > 7));
+    // zlib counts every node deeper than 7, internal ones (lanes ncl..2ncl-3) included
+    const uint32_t over = (uint32_t)__builtin_popcountll(__ballot(lane + 2 < 2 * ncl && dv > 7));
     const uint32_t dcl = dv > 7 ? 7u : dv;
     uint32_t blc = 0;
     for (uint32_t L = 1; L <= 7; L++) {
@@ -1933,7 +1934,7 @@ hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* 
     return hipGetLastError();
 }
 
-hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev) {
+hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev, hipEvent_t* ev2) {
     if (!a.ntiles || !a.nseg) return hipSuccess;
     const bool prof = a.stamps != nullptr;
     hipLaunchKernelGGL(k_seg_map, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
@@ -1946,6 +1947,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
         hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
     if (ev) (void)hipEventRecord(ev[0], st);
+    if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof)
         hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
@@ -1953,10 +1955,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
     if (ev) (void)hipEventRecord(ev[1], st);
+    if (ev2) (void)hipEventRecord(ev2[1], st);
     hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
                        a.blk, a.sizes);
     hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
     if (ev) (void)hipEventRecord(ev[2], st);
+    if (ev2) (void)hipEventRecord(ev2[2], st);
     if (prof)
         hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
@@ -1964,6 +1968,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
         hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
     if (ev) (void)hipEventRecord(ev[3], st);
+    if (ev2) (void)hipEventRecord(ev2[3], st);
     hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
                        a.blk, a.offs, a.out);
     return hipGetLastError();

@@ -19,11 +19,13 @@ namespace pbx {
 #define PBX_SEG 16384
 #endif
 #ifndef PBX_BLK
-#define PBX_BLK 3
+#define PBX_BLK 4
 #endif
 using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
 constexpr uint32_t BLK_SEGS = PBX_BLK;
-static_assert(BLK_SEGS >= 1 && BLK_SEGS * PBX_SEG <= 65535, "a stored block holds <= 65535 bytes");
+// The planner's longest segment: SEG, or less so that BLK_SEGS segments fit one stored block.
+constexpr uint32_t SPLIT_MAX = BLK_SEGS * PBX_SEG <= 65535 ? PBX_SEG : (65535 / BLK_SEGS) & ~15u;
+static_assert(BLK_SEGS >= 1 && BLK_SEGS * SPLIT_MAX <= 65535, "a stored block holds <= 65535 bytes");
 
 // Huffman blocks of a tile of nseg segments.
 PBX_HD uint32_t tile_blocks(uint32_t nseg) { return (nseg + BLK_SEGS - 1) / BLK_SEGS; }
@@ -38,7 +40,7 @@ constexpr uint32_t CODE_WORDS = 320 + DeflateMainCfg::HDRW;  // codes + block he
 // rounded up to 16 bytes (segment starts stay 16-byte aligned for vector loads); the
 // count is then recomputed so that the last segment is never empty.
 inline void deflate_split(uint64_t len, uint32_t& nseg, uint32_t& seg_len) {
-    const uint64_t S = (uint64_t)DeflateMainCfg::SEG;
+    const uint64_t S = (uint64_t)SPLIT_MAX;
     if (len == 0) { nseg = 1; seg_len = 16; return; }
     const uint64_t n0 = (len + S - 1) / S;
     uint64_t l = ((len + n0 - 1) / n0 + 15) & ~15ull;

@@ -67,7 +67,9 @@ struct DeflateLaunch {
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.  If ev is given,
 // ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.
-hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr);
+// ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode.
+hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr,
+                          hipEvent_t* ev2 = nullptr);
 size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
 // k_huff alone (test hook): blk[].seg0 / .nseg and info[].sl / .last must be set.
 hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* info,

@@ -150,7 +150,20 @@ struct pbx_ctx {
     int device = 0;
     int cus = 256;                      // compute units (persistent kernel grids)
     pbx_config cfg{};
-    hipStream_t stream = nullptr;       // kernels (batches run in launch order)
+    hipStream_t stream = nullptr;       // kernels (planes, Zarr; batches on kstream[])
+    // Batch kernel streams: batch k runs on kstream[k % nks], so one batch's latency-bound
+    // phases (k_huff, the small compaction kernels, kernel tails) overlap the next batch's
+    // kernels.  kstream[0] is `stream`.  PBX_KSTREAMS (1..4, default 3).
+    hipStream_t kstream[4] = {};
+    std::atomic<int> nks{1};
+    std::atomic<uint32_t> kturn{0};
+    // Stagger (PBX_KSTAGGER, 1..4): a batch's first kernel waits for the previous batch's
+    // stage event (after k_lz77, k_huff, k_scan_offsets, k_encode); 0 = no wait.  Default 1:
+    // a batch's k_lz77 starts when the previous batch's k_lz77 has ended, so it overlaps
+    // that batch's k_huff and k_encode rather than competing with its k_lz77.
+    std::atomic<int> stagger{1};
+    hipEvent_t stage_ev[4][4] = {};     // [stream][stage]
+    std::atomic<int> last_ks{-1};       // stream of the last overlapped deflate batch
     hipStream_t copy_stream = nullptr;  // D2H of finished batches, overlapping later kernels
     std::mutex reg_mu;   // plane registry
     std::mutex run_mu;   // plan + launch of one batch at a time on the stream
@@ -165,6 +178,17 @@ struct pbx_ctx {
 };
 
 namespace {
+
+// Waits for every batch kernel stream (before a plane or a pooled block is freed).
+hipError_t sync_kernel_streams(pbx_ctx* ctx) {
+    hipError_t r = hipSuccess;
+    for (int k = 0; k < 4; k++) {
+        if (k && !ctx->kstream[k]) continue;
+        const hipError_t e = hipStreamSynchronize(k ? ctx->kstream[k] : ctx->stream);
+        if (r == hipSuccess) r = e;
+    }
+    return r;
+}
 
 // Host-side result storage shared by the results of one batch fetch.
 struct HostBlock {
@@ -314,6 +338,8 @@ void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
 
 }  // namespace
 
+static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap);
+
 // One synchronous batch: plan + launch under run_mu (launches stay in order on the
 // kernel stream), then the fetch outside it, so that concurrent callers overlap one
 // batch's D2H with the next batch's kernels.  A device failure fails every request of the
@@ -325,7 +351,7 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
         std::lock_guard<std::mutex> run(ctx->run_mu);
         st = pbx_batch_plan(ctx, reqs, n, &b);
         if (st) return st;
-        st = pbx_batch_launch(ctx, b);
+        st = batch_launch(ctx, b, false);
     }
     ctx->n_batches++;
     ctx->n_requests += n;
@@ -435,7 +461,7 @@ struct Coalescer {
             {
                 std::lock_guard<std::mutex> run(ctx->run_mu);
                 f.rc = pbx_batch_plan(ctx, reqs.data(), reqs.size(), &f.b);
-                if (f.rc == PBX_OK) f.rc = pbx_batch_launch(ctx, f.b);
+                if (f.rc == PBX_OK) f.rc = batch_launch(ctx, f.b, false);
                 if (f.rc != PBX_OK) f.err = g_err;
             }
             ctx->n_batches++;
@@ -587,6 +613,15 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (const char* ks = getenv("PBX_KSTREAMS")) ctx->nks = std::min(4, std::max(1, atoi(ks)));
+    else ctx->nks = 3;
+    ctx->kstream[0] = ctx->stream;
+    for (int k = 1; k < 4 && e == hipSuccess; k++)
+        e = hipStreamCreateWithFlags(&ctx->kstream[k], hipStreamNonBlocking);
+    if (const char* sg = getenv("PBX_KSTAGGER")) ctx->stagger = std::min(4, std::max(0, atoi(sg)));
+    for (int k = 0; k < 4 && e == hipSuccess; k++)
+        for (int j = 0; j < 4 && e == hipSuccess; j++)
+            e = hipEventCreateWithFlags(&ctx->stage_ev[k][j], hipEventDisableTiming);
     if (e != hipSuccess) {
         delete ctx;
         return fail(PBX_E_INTERNAL, "init: %s", hipGetErrorString(e));
@@ -601,11 +636,15 @@ void pbx_shutdown(pbx_ctx* ctx) {
     delete ctx->coal;  // drains queued requests, joins its threads
     ctx->coal = nullptr;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    (void)sync_kernel_streams(ctx);
     (void)hipStreamSynchronize(ctx->copy_stream);
     for (auto& kv : ctx->planes) (void)hipFree(kv.second.dev);
     ctx->dpool.release_all();
     ctx->hpool.release_all();
+    for (int k = 1; k < 4; k++)
+        if (ctx->kstream[k]) (void)hipStreamDestroy(ctx->kstream[k]);
+    for (auto& r : ctx->stage_ev)
+        for (auto& x : r) if (x) (void)hipEventDestroy(x);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->copy_stream);
     delete ctx;
@@ -615,10 +654,21 @@ int pbx_release_cached(pbx_ctx* ctx) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     std::lock_guard<std::mutex> run(ctx->run_mu);
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(sync_kernel_streams(ctx));
     HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
     ctx->dpool.trim();
     ctx->hpool.trim();
+    return PBX_OK;
+}
+
+int pbx_set_kernel_streams(pbx_ctx* ctx, int32_t streams, int32_t stagger) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    if (streams < 1 || streams > 4 || stagger < 0 || stagger > 4)
+        return fail(PBX_E_BADARG, "kernel streams %d / stagger %d out of range", streams, stagger);
+    std::lock_guard<std::mutex> run(ctx->run_mu);
+    ctx->nks = streams;
+    ctx->stagger = stagger;
+    ctx->last_ks = -1;
     return PBX_OK;
 }
 
@@ -1107,7 +1157,7 @@ int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
         if (--im->second.planes == 0) ctx->images.erase(im);
     }
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    (void)sync_kernel_streams(ctx);
     HIP_TRY(hipFree(p.dev));
     return PBX_OK;
 }
@@ -1316,7 +1366,12 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     return PBX_OK;
 }
 
-int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
+int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) { return batch_launch(ctx, b, true); }
+
+// overlap: the caller pipelines batches (pbx_batch_launch, pbx_submit), so a batch with
+// deflate work goes to the next of the kernel streams, staggered behind the previous one;
+// otherwise (synchronous calls, the coalescer, raw/TIFF-only batches) it runs on `stream`.
+static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     hipError_t err = hipSuccess;
@@ -1346,7 +1401,13 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     if (!b->ev[0])
         for (auto& e : b->ev) HIP_TRY(hipEventCreate(&e));
-    hipStream_t st = ctx->stream;
+    const int nks = ctx->nks.load();
+    const bool multi = overlap && nks > 1 && b->nseg > 0;
+    const int ks = multi ? (int)(ctx->kturn++ % (uint32_t)nks) : 0;
+    hipStream_t st = ctx->kstream[ks];
+    const int prev = ctx->last_ks.load(), stagger = ctx->stagger.load();
+    if (multi && stagger && prev >= 0 && prev != ks)
+        HIP_TRY(hipStreamWaitEvent(st, ctx->stage_ev[prev][stagger - 1], 0));
     HIP_TRY(hipEventRecord(b->ev[0], st));
     if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
     if (ndt)
@@ -1388,7 +1449,8 @@ int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     a.cus = (uint32_t)ctx->cus;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
-        HIP_TRY(launch_deflate(st, a, b->ev + 4));
+        HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr));
+        ctx->last_ks = multi ? ks : -1;
     } else {
         for (int k = 4; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
     }
@@ -1594,7 +1656,7 @@ int pbx_submit(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* o
         std::lock_guard<std::mutex> run(ctx->run_mu);
         st = pbx_batch_plan(ctx, reqs, n, &b);
         if (st) return st;
-        st = pbx_batch_launch(ctx, b);
+        st = batch_launch(ctx, b, true);
     }
     ctx->n_batches++;
     ctx->n_requests += n;

@@ -105,6 +105,7 @@ EXPORTS = [
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
     "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
     "pbx_plane_register_zarr", "pbx_planes_register_zarr", "pbx_release_cached",
+    "pbx_set_kernel_streams",
 ]
 
 _lib = None
@@ -131,6 +132,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_shutdown.argtypes = [vp]
     L.pbx_shutdown.restype = None
     L.pbx_device_synchronize.argtypes = [vp]
+    L.pbx_set_kernel_streams.argtypes = [vp, i32, i32]
     L.pbx_release_cached.argtypes = [vp]
     L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
     L.pbx_plane_release.argtypes = [vp, u64]
@@ -591,6 +593,10 @@ class PixelsService:
 
     def synchronize(self) -> None:
         _check(lib().pbx_device_synchronize(self._h))
+
+    def set_kernel_streams(self, streams: int, stagger: int = 1) -> None:
+        """Kernel streams for pipelined batches (pbx_set_kernel_streams); 1 = serial."""
+        _check(lib().pbx_set_kernel_streams(self._h, streams, stagger))
 
     def release_cached(self) -> None:
         """Free cached batch buffers (device and pinned) no live batch uses."""

@@ -97,13 +97,16 @@ def test_lz77_records_cover_the_segment(kind):
 
 
 def skewed_block_stream(seed=7):
-    """Three 16 KiB segments (one Huffman block): bytes 0..127 in the first two, 128..255 in
-    the third, no repeats.  The block's code favours the first two, so the third's share of
-    a Huffman-coded block would exceed 16 KiB: the block must be stored."""
+    """One Huffman block of full segments: bytes 0..127 in all but the last, 128..255 in
+    the last, no repeats.  The block's code favours the first ones, so the last one's share
+    of a Huffman-coded block would exceed its 16 KiB output buffer: the block must be
+    stored."""
     import numpy as np
+    L = _emu.lib()
+    nblk, seg = L.pbxemu_blk_segs(), L.pbxemu_split_max()
     rng = np.random.default_rng(seed)
-    a = rng.integers(0, 128, 2 * 16384, dtype=np.uint8)
-    b = rng.integers(128, 256, 16384, dtype=np.uint8)
+    a = rng.integers(0, 128, (nblk - 1) * seg, dtype=np.uint8)
+    b = rng.integers(128, 256, seg, dtype=np.uint8)
     return np.concatenate([a, b]).tobytes()
 
 

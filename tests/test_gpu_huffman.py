@@ -13,8 +13,13 @@ import pbx
 pytestmark = pytest.mark.gpu
 
 
-def test_gpu_huffman_matches_emulator(service):
-    hs = _hists.cases(seed=0) + _hists.cases(seed=1)
+@pytest.mark.parametrize("which", ["hists", "random"])
+def test_gpu_huffman_matches_emulator(service, which):
+    """`random`: uneven histograms whose code-length codes need zlib's 7-bit overflow
+    repair several levels deep (test_emu_huffman.random_hists)."""
+    from test_emu_huffman import random_hists
+    hs = (_hists.cases(seed=0) + _hists.cases(seed=1) if which == "hists"
+          else random_hists(0, 200) + random_hists(2, 200))
     n = len(hs)
     hist = np.ascontiguousarray(np.stack(hs), dtype=np.uint32)
     sl_last = np.zeros((n, 2), np.uint32)

@@ -325,17 +325,19 @@ def test_mixed_batch(service, oracle):
 
 
 def test_tiff_deflate_segment_capacity(adaptive_service):
-    """A Huffman block (3 segments) whose code would give one segment more than 16 KiB of
-    bits is stored (k_huff's seg_shares_fit): the GPU stream equals the CPU emulation byte
-    for byte and decodes exactly."""
+    """A Huffman block (BLK_SEGS segments) whose code would give one segment more than
+    16 KiB of bits is stored (k_huff's seg_shares_fit): the GPU stream equals the CPU
+    emulation byte for byte and decodes exactly."""
     from test_emu_deflate import skewed_block_stream
     data = skewed_block_stream()
+    w = next(w for w in (256, 1023, 1024, 2048) if len(data) % w == 0)
+    h = len(data) // w
     iid = next(_ids)
-    plane = np.frombuffer(data, np.uint8).reshape(192, 256)
-    adaptive_service.register_plane(iid, 0, 0, 0, pbx.UINT8, 256, 192, data=plane, big_endian=True)
-    (st, body), = adaptive_service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 0, 0, 256, 192, format="tif")])
+    plane = np.frombuffer(data, np.uint8).reshape(h, w)
+    adaptive_service.register_plane(iid, 0, 0, 0, pbx.UINT8, w, h, data=plane, big_endian=True)
+    (st, body), = adaptive_service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="tif")])
     assert st == pbx.OK
-    z, blks = _emu.deflate(data, 256)
+    z, blks = _emu.deflate(data, w)
     assert blks[0].btype == 0
     assert body[160:] == z
     assert zlib.decompress(body[160:]) == data
