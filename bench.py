@@ -39,6 +39,7 @@ METRIC = "tiles/sec (512x512 uint16 PNG) + achieved HBM GB/s at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TILE, GRID = 512, 64
 KSTREAMS, KSTAGGER = int(os.environ.get("PBX_KSTREAMS", "3")), 1  # the library's defaults
+PIPE_DEPTH = int(os.environ.get("PBX_BENCH_DEPTH", "2"))  # batches in flight
 
 
 def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
@@ -49,30 +50,34 @@ def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
 def run_steps(svc, ctxs, steps, warmup, barrier):
     """Warmup, then `steps` timed steps; returns (seconds, per-step stats, mean host ms).
 
-    Steps are pipelined two deep, as a server feeds its GPU: the host plans and launches
-    batch k+1 (request validation, descriptors, upload) while batch k runs, then waits for
-    batch k (its own completion event).  The request array is built once."""
+    Steps are pipelined PIPE_DEPTH deep, as a server feeds its GPU: the host plans and
+    launches batch k+1 (request validation, descriptors, upload) while earlier batches run,
+    then waits for the oldest one (its own completion event).  The request array is built
+    once."""
     reqs = pbx.make_reqs(ctxs)
 
     def one_pass(n, record):
-        prev = None
+        q = []
         host = 0.0
         out = []
+
+        def retire():
+            b = q.pop(0)
+            b.sync()
+            if record:
+                out.append(b.stats())
+            b.close()
+
         for _ in range(n):
             t0 = time.perf_counter()
             b = pbx.Batch(svc, reqs=reqs)
             b.launch()
             host += time.perf_counter() - t0
-            if prev is not None:
-                prev.sync()
-                if record:
-                    out.append(prev.stats())
-                prev.close()
-            prev = b
-        prev.sync()
-        if record:
-            out.append(prev.stats())
-        prev.close()
+            q.append(b)
+            if len(q) >= PIPE_DEPTH:
+                retire()
+        while q:
+            retire()
         return out, host
 
     if warmup:

@@ -715,9 +715,11 @@ PBX_HD void ph_rle_bits(uint32_t tid, SM& S) {
     }
 }
 
-// Output bytes of a segment with the given block type and block bits (EOB included).
-PBX_HD uint32_t block_nbytes(uint32_t btype, uint64_t bits, uint32_t sl, uint32_t last) {
-    if (btype == 0) return 5 + sl;
+// Output bytes of a block of nsg segments (sl bytes in all) with the given block type and
+// block bits (EOB included).  Stored, every segment is its own stored block (5-byte
+// header): a block of many segments may hold more than a stored block's 65535 bytes.
+PBX_HD uint32_t block_nbytes(uint32_t btype, uint64_t bits, uint32_t sl, uint32_t last, uint32_t nsg) {
+    if (btype == 0) return 5 * nsg + sl;
     return last ? (uint32_t)((bits + 7) / 8) : (uint32_t)((bits + 3 + 7) / 8 + 4);
 }
 
@@ -744,12 +746,12 @@ PBX_HD bool seg_shares_fit(const uint32_t* dk, uint32_t nsg, uint32_t hdr, uint3
 // chosen block, M_DATABITS = its data bits (EOB included) and M_NBYTES = the segment's
 // exact output bytes.
 template <class C, class SM>
-PBX_HD void ph_choose(uint32_t tid, SM& S, uint32_t sl, uint32_t last) {
+PBX_HD void ph_choose(uint32_t tid, SM& S, uint32_t sl, uint32_t last, uint32_t nsg) {
     if (tid != 0) return;
     const uint64_t hdr = 3 + 5 + 5 + 4 + 3ull * S.misc[M_HCLEN] + S.misc[M_HDRBITS];
     const uint64_t dyn_bits = hdr + S.misc[M_DYNBITS], fix_bits = 3ull + S.misc[M_FIXBITS];
-    const uint32_t dyn = block_nbytes(2, dyn_bits, sl, last), fix = block_nbytes(1, fix_bits, sl, last);
-    const uint32_t sto = block_nbytes(0, 0, sl, last);
+    const uint32_t dyn = block_nbytes(2, dyn_bits, sl, last, nsg), fix = block_nbytes(1, fix_bits, sl, last, nsg);
+    const uint32_t sto = block_nbytes(0, 0, sl, last, nsg);
     uint32_t btype = 2, best = dyn;
     if (fix <= best) { btype = 1; best = fix; }
     if (sto <= best) { btype = 0; best = sto; }

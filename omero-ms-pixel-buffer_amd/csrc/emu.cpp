@@ -56,7 +56,7 @@ uint32_t scan_excl_add(uint32_t* a, int n) {
 }
 
 // k_huff (one wave of HT threads): needs lfreq / dfreq.
-void run_huff(Smem& S, uint32_t sl, uint32_t last) {
+void run_huff(Smem& S, uint32_t sl, uint32_t last, uint32_t nsg) {
     for (int t = 0; t < C::HT; t++) ph_huff_init<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_keys<C, EmuOps>(t, S);
     std::sort(S.hs.skey, S.hs.skey + KEYN);
@@ -81,7 +81,7 @@ void run_huff(Smem& S, uint32_t sl, uint32_t last) {
     for (int t = 0; t < C::HT; t++) ph_clen<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_rle_bits<C>(t, S);
     S.misc[M_HDRBITS] = scan_excl_add(S.rboff, RLEN);
-    for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sl, last);
+    for (int t = 0; t < C::HT; t++) ph_choose<C>(t, S, sl, last, nsg);
     for (int t = 0; t < C::HT; t++) ph_codes<C>(t, S);
     for (int t = 0; t < C::HT; t++) ph_header<C, EmuOps>(t, S, last);
 }
@@ -145,7 +145,7 @@ int run_block(std::vector<std::unique_ptr<Smem>>& LZ, Smem& H, const Src& src, c
         for (uint32_t k = 0; k < nsg; k++) v += LZ[k]->dfreq[i];
         H.dfreq[i] = v;
     }
-    run_huff(H, sl, last);
+    run_huff(H, sl, last, nsg);
     if (H.misc[M_BTYPE] != 0) {  // k_huff's per-segment capacity rule (seg_shares_fit)
         uint32_t dk[BLK_SEGS];
         for (uint32_t k = 0; k < nsg; k++) {
@@ -157,20 +157,23 @@ int run_block(std::vector<std::unique_ptr<Smem>>& LZ, Smem& H, const Src& src, c
             H.misc[M_BTYPE] = 0;
             H.misc[M_HDRBITS] = 0;
             H.misc[M_DATABITS] = 0;
-            H.misc[M_NBYTES] = block_nbytes(0, 0, sl, last);
+            H.misc[M_NBYTES] = block_nbytes(0, 0, sl, last, nsg);
         }
     }
     for (uint32_t k = 0; k < 256; k++) H.crc_t[0][k] = crc_table_entry(k);
     const uint32_t bt = H.misc[M_BTYPE], nbytes = H.misc[M_NBYTES];
     if (nbytes > cap) return -1;
     std::vector<uint32_t> words((nbytes + 8) / 4 + 2, 0);
-    if (bt == 0) {
+    if (bt == 0) {  // every segment its own stored block
         uint8_t* o = (uint8_t*)words.data();
-        o[0] = last ? 1 : 0;
-        o[1] = (uint8_t)sl; o[2] = (uint8_t)(sl >> 8); o[3] = (uint8_t)~sl; o[4] = (uint8_t)(~sl >> 8);
-        uint32_t p = 5;
-        for (uint32_t k = 0; k < nsg; k++)
-            for (uint32_t j = 0; j < sps[k].sl; j++) o[p++] = (uint8_t)lds_byte(*LZ[k], sps[k].wl + j);
+        uint32_t p = 0;
+        for (uint32_t k = 0; k < nsg; k++) {
+            const uint32_t n = sps[k].sl;
+            o[p] = (last && k + 1 == nsg) ? 1 : 0;
+            o[p + 1] = (uint8_t)n; o[p + 2] = (uint8_t)(n >> 8); o[p + 3] = (uint8_t)~n; o[p + 4] = (uint8_t)(~n >> 8);
+            p += 5;
+            for (uint32_t j = 0; j < n; j++) o[p++] = (uint8_t)lds_byte(*LZ[k], sps[k].wl + j);
+        }
     } else {
         const uint32_t hdr = H.misc[M_HDRBITS];
         for (uint32_t w = 0; w < (hdr + 31) / 32; w++) words[w] = H.hdrw[w];
@@ -241,8 +244,9 @@ int pbxemu_deflate(const uint8_t* stream, uint64_t len, uint32_t rowlen, uint8_t
     out[o++] = 0x78;
     out[o++] = 0x9C;
     uint32_t s1 = 0, s2 = 0;
-    for (uint32_t k0 = 0, bi = 0; k0 < nseg; k0 += BLK_SEGS, bi++) {
-        const uint32_t nsg = nseg - k0 < BLK_SEGS ? nseg - k0 : BLK_SEGS;
+    const uint32_t nb = tile_blocks(nseg);
+    for (uint32_t bi = 0; bi < nb; bi++) {
+        const uint32_t k0 = block_seg0(bi, nseg, nb), nsg = block_seg0(bi + 1, nseg, nb) - k0;
         SegParams sps[BLK_SEGS];
         for (uint32_t q = 0; q < nsg; q++) {
             SegParams& sp = sps[q];
@@ -320,7 +324,7 @@ int pbxemu_huffman(const uint32_t* hist, uint32_t sl, uint32_t last, uint32_t* c
     memset(S.get(), 0xCD, sizeof(Smem));
     for (int i = 0; i < 288; i++) S->lfreq[i] = i == 256 ? 1u : hist[i];  // one end of block
     for (int i = 0; i < 32; i++) S->dfreq[i] = hist[288 + i];
-    run_huff(*S, sl, last);
+    run_huff(*S, sl, last, 1);
     for (int i = 0; i < 288; i++) codes[i] = S->lcode[i];
     for (int i = 0; i < 32; i++) codes[288 + i] = S->dcode[i];
     for (int i = 0; i < C::HDRW; i++) codes[320 + i] = S->hdrw[i];

@@ -79,6 +79,7 @@ struct HuffSmem {
     uint32_t lbm[16 * 9], dbm[16];
     uint32_t misc[M_NMISC];
     uint32_t nrounds[2];
+    uint32_t dk[BLK_SEGS];  // token bits of every segment of the block under its code
     union {
         HuffScratchDev hs;
         struct {  // from ph_rle_init on
@@ -1168,28 +1169,28 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         nst++;
     };
     stamp();
-    // the segments' histograms, kept in registers for their bit counts at the end
-    uint32_t hreg[BLK_SEGS][5];
+    // the segments' histograms summed (read again, L2-hot, for their bit counts at the end)
+    uint32_t hs[5] = {0, 0, 0, 0, 0};
+    for (uint32_t k0 = 0; k0 < nsg; k0 += 4) {  // four segments' loads in flight
+        uint32_t hr[4][5];
 #pragma unroll
-    for (uint32_t k = 0; k < BLK_SEGS; k++)
+        for (uint32_t k = 0; k < 4; k++)
 #pragma unroll
-        for (int j = 0; j < 5; j++)
-            hreg[k][j] = k < nsg ? hist[(size_t)(seg0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+            for (int j = 0; j < 5; j++)
+                hr[k][j] = k0 + k < nsg ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+#pragma unroll
+            for (int j = 0; j < 5; j++) hs[j] += hr[k][j];
+    }
 #pragma unroll
     for (int j = 0; j < 5; j++) {
         const uint32_t i = tid + 64 * j;
-        uint32_t v = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < BLK_SEGS; k++) v += hreg[k][j];
-        if (i == 256) v = 1;  // one end of block (every segment's histogram counted one)
+        const uint32_t v = i == 256 ? 1u : hs[j];  // one end of block (every segment counted one)
         if (i < 288) S.lfreq[i] = v; else S.dfreq[i - 288] = v;
     }
-    uint32_t sl = 0, sls[BLK_SEGS];
-#pragma unroll
-    for (uint32_t k = 0; k < BLK_SEGS; k++) {
-        sls[k] = k < nsg ? info[seg0 + k].sl : 0u;
-        sl += sls[k];
-    }
+    uint32_t sl = 0;
+    for (uint32_t k = 0; k < nsg; k++) sl += info[seg0 + k].sl;
     const uint32_t last = info[seg0 + nsg - 1].last;
     ph_huff_init<C>(tid, S);
     __syncthreads();
@@ -1243,7 +1244,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         if (tid == 0) S.misc[M_HDRBITS] = hb;
     }
     __syncthreads();
-    ph_choose<C>(tid, S, sl, last);
+    ph_choose<C>(tid, S, sl, last, nsg);
     __syncthreads();
     stamp();
     ph_codes<C>(tid, S);
@@ -1255,36 +1256,39 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         cg[i] = i < 288 ? S.lcode[i] : i < 320 ? S.dcode[i - 288] : S.hdrw[i - 320];
     // every segment's bit range in the block: [header] tokens of segment 0, 1, ... [EOB]
     // [empty stored block unless the tile ends here]; a stored block is byte-aligned
-    // the segments' token bits under the block's code (wave-uniform)
-    uint32_t dk[BLK_SEGS];
+    // the segments' token bits under the block's code (wave-uniform), into LDS: the
+    // per-symbol cost (code length + extra bits) of this lane's 5 symbols, then one dot
+    // product per segment with its histogram
+    uint32_t cost[5];
 #pragma unroll
-    for (uint32_t k = 0; k < BLK_SEGS; k++) {
+    for (int j = 0; j < 5; j++) {
+        const uint32_t i = tid + 64 * j;
+        const bool skip = i == 256 || (i >= 286 && i < 288) || i >= 318;
+        const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i < 320 ? i - 288 : 0]) >> 16;
+        const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i < 318 ? i - 288 : 0);
+        cost[j] = skip ? 0u : L + eb;
+    }
+    for (uint32_t k = 0; k < nsg; k++) {
         uint32_t d = 0;
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const uint32_t i = tid + 64 * j, f = hreg[k][j];
-            if (i == 256 || (i >= 286 && i < 288) || i >= 318 || !f) continue;
-            const uint32_t L = (i < 288 ? S.lcode[i] : S.dcode[i - 288]) >> 16;
-            const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i - 288);
-            d += f * (L + eb);
-        }
+        for (int j = 0; j < 5; j++) d += cost[j] * hist[(size_t)(seg0 + k) * HIST_WORDS + tid + 64 * j];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-        dk[k] = d;
+        if (tid == 0) S.dk[k] = d;
     }
+    __syncthreads();
     // a segment's share of a Huffman-coded block must fit k_encode's output buffer
     // (deflate_seg.h seg_share_fits); else the block is stored
     uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
     uint32_t dbits = S.misc[M_DATABITS];
-    if (bt != 0 && !seg_shares_fit<C>(dk, nsg, hdr, S.lcode[256] >> 16, last, nbytes)) {
+    if (bt != 0 && !seg_shares_fit<C>(S.dk, nsg, hdr, S.lcode[256] >> 16, last, nbytes)) {
         bt = 0; hdr = 0; dbits = 0;
-        nbytes = block_nbytes(0, 0, sl, last);
+        nbytes = block_nbytes(0, 0, sl, last, nsg);
     }
-    uint32_t run = bt == 0 ? 40u : hdr;
-#pragma unroll
-    for (uint32_t k = 0; k < BLK_SEGS; k++) {
-        if (k >= nsg) break;
-        const uint32_t d = bt == 0 ? 8 * sls[k] : dk[k];
+    // stored: every segment is its own stored block (5-byte header + its bytes)
+    uint32_t run = bt == 0 ? 0u : hdr;
+    for (uint32_t k = 0; k < nsg; k++) {
+        const uint32_t d = bt == 0 ? 8 * (5 + info[seg0 + k].sl) : S.dk[k];
         if (tid == 0) {
             SegInfo& g = info[seg0 + k];
             g.btype = bt;
@@ -1318,17 +1322,18 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
     if (i >= ndt) return;
     const uint32_t f = dt[i].seg_first, n = dt[i].seg_count, hb = dt[i].hblk_first;
     const uint32_t zoff = container_zoff(dt[i]);
-    for (uint32_t k = 0; k < n; k++) {
-        seg_tile[f + k] = i;
-        const uint32_t j = k / BLK_SEGS, r = k % BLK_SEGS;
-        info[f + k].blk = hb + j;
-        info[f + k].tile = i;
-        info[f + k].zoff = zoff;
-        info[f + k].flags = (r == 0 ? SF_FIRST : 0u) | (r + 1 == BLK_SEGS || k + 1 == n ? SF_LAST : 0u) |
-                            ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
-        if (r == 0) {
-            blk[hb + j].seg0 = f + k;
-            blk[hb + j].nseg = n - k < BLK_SEGS ? n - k : BLK_SEGS;
+    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(dt[i]));
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t s0 = block_seg0(j, n, nb), s1 = block_seg0(j + 1, n, nb);
+        blk[hb + j].seg0 = f + s0;
+        blk[hb + j].nseg = s1 - s0;
+        for (uint32_t k = s0; k < s1; k++) {
+            seg_tile[f + k] = i;
+            info[f + k].blk = hb + j;
+            info[f + k].tile = i;
+            info[f + k].zoff = zoff;
+            info[f + k].flags = (k == s0 ? SF_FIRST : 0u) | (k + 1 == s1 ? SF_LAST : 0u) |
+                                ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
         }
     }
 }
@@ -1345,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ 
     if (i >= ndt) return;
     const TileDesc& d = dt[i];
     uint32_t off = 0;
-    const uint32_t nb = tile_blocks(d.seg_count);
+    const uint32_t nb = tile_blocks(d.seg_count, PBX_TILE_BLK_CAP(d));
     for (uint32_t k = 0; k < nb; k++) {
         BlkInfo& g = blk[d.hblk_first + k];
         g.off = off;
@@ -1722,14 +1727,14 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     static_assert(NX4 <= 2 * (uint32_t)C::NT, "two 16-byte table loads per thread");
     const uint4 tx0 = ((const uint4*)kCrcLane.t)[tid];
     const uint4 tx1 = ((const uint4*)kCrcLane.t)[tid + C::NT < NX4 ? tid + C::NT : tid];
-    if (stored) {  // stored block: (first segment) BFINAL/BTYPE byte, LEN, NLEN; the bytes
-        const uint32_t cs = tid * C::CH, o = P + (first ? 5u : 0u);
+    if (stored) {  // the segment's own stored block: BFINAL/BTYPE byte, LEN, NLEN, the bytes
+        const uint32_t cs = tid * C::CH, o = P + 5u;
 #pragma unroll
         for (uint32_t i = 0; i < (uint32_t)C::CH; i++)
             if (cs + i < sp.sl) *out_byte_ptr(S, o + cs + i) = (uint8_t)(cb[i >> 2] >> ((i & 3) * 8));
-        if (first && tid == 0) {
-            const uint32_t len = bi.nbytes - 5;  // LEN: every byte of the block's segments
-            *out_byte_ptr(S, P) = (uint8_t)(bi.fin ? 1 : 0);
+        if (tid == 0) {
+            const uint32_t len = sp.sl;
+            *out_byte_ptr(S, P) = (uint8_t)(final_seg ? 1 : 0);
             *out_byte_ptr(S, P + 1) = (uint8_t)len; *out_byte_ptr(S, P + 2) = (uint8_t)(len >> 8);
             *out_byte_ptr(S, P + 3) = (uint8_t)~len; *out_byte_ptr(S, P + 4) = (uint8_t)(~len >> 8);
         }
@@ -1851,7 +1856,7 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
         const SegInfo& g = info[d.seg_first + k];
         adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.sl);
     }
-    const uint32_t nb = tile_blocks(d.seg_count);
+    const uint32_t nb = tile_blocks(d.seg_count, PBX_TILE_BLK_CAP(d));
     for (uint32_t k = 0; k < nb; k++) payload += blk[d.hblk_first + k].nbytes;
     const uint32_t adler = adler_final(s1, s2, d.stream_len);
     const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;

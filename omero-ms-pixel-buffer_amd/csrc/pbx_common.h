@@ -71,6 +71,9 @@ struct alignas(16) TileDesc {
                             // sub-tile of a response only)
 };
 
+// Segments per Huffman block at most for a deflate tile (pbx_config.h BLK_SEGS*).
+#define PBX_TILE_BLK_CAP(d) ((d).filter != 0 ? BLK_SEGS_FILTERED : BLK_SEGS)
+
 // Per-segment deflate result.
 struct SegOut {
     uint32_t nbytes;        // compressed bytes in the slot

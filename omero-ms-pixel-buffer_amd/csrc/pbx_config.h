@@ -19,17 +19,27 @@ namespace pbx {
 #define PBX_SEG 16384
 #endif
 #ifndef PBX_BLK
-#define PBX_BLK 4
+#define PBX_BLK 16
 #endif
 using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
-constexpr uint32_t BLK_SEGS = PBX_BLK;
-// The planner's longest segment: SEG, or less so that BLK_SEGS segments fit one stored block.
-constexpr uint32_t SPLIT_MAX = BLK_SEGS * PBX_SEG <= 65535 ? PBX_SEG : (65535 / BLK_SEGS) & ~15u;
-static_assert(BLK_SEGS >= 1 && BLK_SEGS * SPLIT_MAX <= 65535, "a stored block holds <= 65535 bytes");
+constexpr uint32_t BLK_SEGS = PBX_BLK;  // segments per Huffman block at most (filter None, TIFF)
+// With a PNG row filter the byte statistics change from row to row, and smaller blocks
+// whose codes follow them compress better (adaptive filter on noise: 3 segments 382 KB,
+// 16 segments 392 KB per 512x512 uint16 tile).
+constexpr uint32_t BLK_SEGS_FILTERED = 3;
+// The planner's longest segment.  A stored Huffman block is one stored block per segment
+// (block_nbytes), so only a segment must fit a stored block's 65535 bytes.
+constexpr uint32_t SPLIT_MAX = PBX_SEG;
+static_assert(BLK_SEGS >= 1 && BLK_SEGS <= 64 && SPLIT_MAX <= 65535, "a stored block holds <= 65535 bytes");
 
 // Huffman blocks of a tile of nseg segments.
-PBX_HD uint32_t tile_blocks(uint32_t nseg) { return (nseg + BLK_SEGS - 1) / BLK_SEGS; }
-
+PBX_HD uint32_t tile_blocks(uint32_t nseg, uint32_t cap = BLK_SEGS) { return (nseg + cap - 1) / cap; }
+// Block j of a tile's nb blocks holds its segments [block_seg0(j, nseg, nb),
+// block_seg0(j + 1, nseg, nb)): an even split (33 segments of a 512x512 uint16 PNG in
+// three blocks of 11).
+PBX_HD uint32_t block_seg0(uint32_t j, uint32_t nseg, uint32_t nb) {
+    return (uint32_t)((uint64_t)j * nseg / nb);
+}
 // Per-segment HBM records between the deflate kernels (32-bit words).
 constexpr uint32_t HIST_WORDS = 320;  // literal/length + distance histogram
 constexpr uint32_t MREC_WORDS =       // per-wave match counts, positions|lengths, distances

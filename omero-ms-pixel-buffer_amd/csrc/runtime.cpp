@@ -1342,7 +1342,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         d.seg_first = b->nseg;
         b->nseg += d.seg_count;
         d.hblk_first = b->nblk;
-        b->nblk += tile_blocks(d.seg_count);
+        b->nblk += tile_blocks(d.seg_count, PBX_TILE_BLK_CAP(d));
         b->stream_bytes += d.stream_len;
         b->png_cap += ((uint64_t)TIFF_DATA_OFFSET + d.tiff_hdr + 128 + d.stream_len + 16ull * d.seg_count + 255) &
                       ~255ull;
