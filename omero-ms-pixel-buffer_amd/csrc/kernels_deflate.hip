@@ -721,7 +721,8 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
                                                 const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
-                                                uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps) {
+                                                uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps,
+                                                uint32_t uniform_nseg) {
     __shared__ LzSmem<C> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
@@ -731,7 +732,8 @@ __global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ 
         nst++;
     };
     stamp();
-    const TileDesc d = load_desc(dt + seg_tile[seg]);
+    // (tiles of equal segment counts: the tile by a division, one dependent load less)
+    const TileDesc d = load_desc(dt + (uniform_nseg ? seg / uniform_nseg : seg_tile[seg]));
     const SegParams sp = seg_params(d, seg - d.seg_first);
     const bool direct = (d.flags & TF_DIRECT) != 0;
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
@@ -1947,10 +1949,10 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     const uint32_t lz_grid = a.nseg;
     if (prof)
         hipLaunchKernelGGL((k_lz77<DC, true>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg);
     else
         hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps);
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg);
     if (ev) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof)

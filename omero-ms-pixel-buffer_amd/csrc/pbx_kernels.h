@@ -64,9 +64,9 @@ struct DeflateLaunch {
     uint64_t* stamps;       // [nseg * 32] phase clocks (diagnostics) or nullptr
     uint32_t* seg_tile;     // [nseg] tile of every segment (k_seg_map)
     uint32_t cus = 256;     // compute units of the device (persistent grids)
+    uint32_t uniform_nseg = 0;  // every tile has this many segments (tile = seg / it), or 0
 };
-// k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.  If ev is given,
-// ev[0..3] are recorded after k_lz77, k_huff, the offsets scan and k_encode.
+// k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.
 // ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode.
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr,
                           hipEvent_t* ev2 = nullptr);

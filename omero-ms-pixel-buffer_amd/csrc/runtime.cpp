@@ -1447,6 +1447,9 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     a.blk = (BlkInfo*)b->d_blk;
     a.nblk = b->nblk;
     a.cus = (uint32_t)ctx->cus;
+    a.uniform_nseg = ndt ? b->dt[0].seg_count : 0u;
+    for (uint32_t k = 1; k < ndt && a.uniform_nseg; k++)
+        if (b->dt[k].seg_count != a.uniform_nseg) a.uniform_nseg = 0;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr));
