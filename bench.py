@@ -419,7 +419,8 @@ def extra(out, svc, rank, world, barrier, iid, side):
     rate, gbs = e2e_rate(svc, grid_ctxs(iid, "png"))
     out["e2e_with_d2h"] = {"tiles_per_s": round(rate, 1), "d2h_gbps": round(gbs, 1)}
     # the served path: concurrent single-tile callers through the coalescer
-    out["served_get_tile_512x512_u16_png"] = serve_lines(svc, iid)
+    # (one node's ranks together: 512 callers per rank only on a single GPU)
+    out["served_get_tile_512x512_u16_png"] = serve_lines(svc, iid, (32, 128, 512) if world == 1 else (32, 128))
     # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
     raw = grid_ctxs(iid, None)
     dtr, sr, _ = run_steps(svc, raw, 5, 2, barrier)
