@@ -297,3 +297,34 @@ def test_resolution_pyramid(service, oracle, pt, source):
         assert r == 0 and px == bytes(flip)
     else:
         assert s2 == pbx.E_NOTFOUND  # APNGWriter rejects 32/64-bit types
+
+
+@pytest.mark.parametrize("streams,stagger", [(3, 1), (2, 0), (4, 2), (3, 4)])
+def test_kernel_streams_overlap_same_bytes(service, streams, stagger):
+    """Pipelined batches overlapped on several kernel streams (pbx_set_kernel_streams), each
+    staggered behind the previous batch's stage, return exactly the bytes the same batches
+    give one at a time on one stream (PNG and deflate-free batches interleaved)."""
+    iid = next(_ids)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT16, 4096, 4096, generator="noise", seed=5)
+
+    def run(ns, sg):
+        service.set_kernel_streams(ns, sg)
+        out = []
+        try:
+            batches = []
+            for k in range(6):
+                ctxs = [pbx.TileCtx(iid, 0, 0, 0, 512 * ((i + k) % 8), 512 * ((i // 8 + k) % 8), 512, 512,
+                                    format=None if k == 3 else "png") for i in range(64)]
+                b = pbx.Batch(service, ctxs)
+                b.launch()
+                batches.append(b)
+            for b in batches:
+                out.append(b.fetch())
+                b.close()
+        finally:
+            service.set_kernel_streams(3, 1)
+        return out
+
+    want = run(1, 0)
+    got = run(streams, stagger)
+    assert got == want
