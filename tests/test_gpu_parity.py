@@ -367,3 +367,30 @@ def test_png_filters_dword_path(oracle, filt):
                 stream = oracle.png_filter_stream(np.frombuffer(tile, np.uint8), pt, w, h, filt).tobytes()
                 r, idat = oracle.png_inflate_idat(body, len(stream))
                 assert idat == stream, (pt, x, y, w, h)
+
+
+def test_incompressible_tiles_stored_per_segment(service, adaptive_service, oracle):
+    """Random bytes: every Huffman block (up to 16 segments) is stored, one stored block per
+    segment (a block may then hold more than one stored block's 65535 bytes).  PNG and
+    deflate-TIFF tiles of 1024^2 uint8 decode exactly and equal the CPU emulation byte for
+    byte."""
+    rng = np.random.default_rng(77)
+    plane = rng.integers(0, 256, (1100, 1100), dtype=np.uint8)
+    iid = next(_ids)
+    for s_ in (service, adaptive_service):
+        s_.register_plane(iid, 0, 0, 0, pbx.UINT8, 1100, 1100, data=plane, big_endian=True)
+    (st, png), = service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 7, 9, 1024, 1024, format="png")])
+    (st2, tif), = adaptive_service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, 7, 9, 1024, 1024, format="tif")])
+    assert st == pbx.OK and st2 == pbx.OK
+    tile = plane[9:9 + 1024, 7:7 + 1024]
+    r, px, _ = oracle.png_decode(png)
+    assert r == 0 and px == tile.tobytes()
+    stream = np.concatenate([np.zeros((1024, 1), np.uint8), tile], 1).tobytes()
+    z, blks = _emu.deflate(stream, 1025)
+    assert all(b.btype == 0 for b in blks) and len(blks) > 1
+    assert png[99:99 + len(z)] == z
+    assert zlib.decompress(z) == stream
+    r, px, meta = oracle.tiff_decode(tif, 1024 * 1024)
+    assert r == 0 and meta["compression"] == 8 and px == tile.tobytes()
+    z2, _ = _emu.deflate(tile.tobytes(), 1024)
+    assert tif[160:160 + len(z2)] == z2
