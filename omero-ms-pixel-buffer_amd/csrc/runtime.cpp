@@ -1366,7 +1366,11 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     return PBX_OK;
 }
 
-int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) { return batch_launch(ctx, b, true); }
+int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
+    if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
+    std::lock_guard<std::mutex> run(ctx->run_mu);  // launches (and the stream turn) in order
+    return batch_launch(ctx, b, true);
+}
 
 // overlap: the caller pipelines batches (pbx_batch_launch, pbx_submit), so a batch with
 // deflate work goes to the next of the kernel streams, staggered behind the previous one;
