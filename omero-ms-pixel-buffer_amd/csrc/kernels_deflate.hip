@@ -81,6 +81,7 @@ struct HuffSmem {
     uint32_t misc[M_NMISC];
     uint32_t nrounds[2];
     uint32_t dk[BLK_SEGS];  // token bits of every segment of the block under its code
+    uint32_t sls[BLK_SEGS];  // stream bytes of every segment
     union {
         HuffScratchDev hs;
         struct {  // from ph_rle_init on
@@ -203,6 +204,15 @@ __device__ __forceinline__ uint32_t crc_mul_tab(const uint32_t* t, uint32_t b) {
 #pragma unroll
     for (int j = 0; j < 8; j++) r ^= t[j * 16 + ((b >> (4 * j)) & 0xFu)];
     return r;
+}
+// Sum of x over the wave (row scans by DPP shifts, then the four row totals), uniform.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 // XOR of x over the wave (row scans by DPP shifts, then the four row totals), uniform.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
@@ -1154,6 +1164,8 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
     if (lane == 0) S.misc[M_HCLEN] = hclen < 4 ? 4u : hclen;
 }
 
+constexpr uint32_t HUFF_LDSEG = 4;  // k_huff: segments whose histogram loads are in flight together
+
 // One Huffman block = the BLK_SEGS (or fewer, at a tile's end) consecutive segments of
 // one tile whose histograms it sums; one wave per block.
 template <class C, bool PROF>
@@ -1174,15 +1186,15 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     stamp();
     // the segments' histograms summed (read again, L2-hot, for their bit counts at the end)
     uint32_t hs[5] = {0, 0, 0, 0, 0};
-    for (uint32_t k0 = 0; k0 < nsg; k0 += 4) {  // four segments' loads in flight
-        uint32_t hr[4][5];
+    for (uint32_t k0 = 0; k0 < nsg; k0 += HUFF_LDSEG) {  // HUFF_LDSEG segments' loads in flight
+        uint32_t hr[HUFF_LDSEG][5];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++)
+        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++)
                 hr[k][j] = k0 + k < nsg ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++)
+        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++) hs[j] += hr[k][j];
     }
@@ -1192,8 +1204,10 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         const uint32_t v = i == 256 ? 1u : hs[j];  // one end of block (every segment counted one)
         if (i < 288) S.lfreq[i] = v; else S.dfreq[i - 288] = v;
     }
-    uint32_t sl = 0;
-    for (uint32_t k = 0; k < nsg; k++) sl += info[seg0 + k].sl;
+    // the segments' lengths: lane k loads segment k's (one round trip), kept in LDS
+    const uint32_t my_sl = tid < nsg ? info[seg0 + tid].sl : 0u;
+    if (tid < nsg) S.sls[tid] = my_sl;
+    const uint32_t sl = wave_sum(my_sl);
     const uint32_t last = info[seg0 + nsg - 1].last;
     ph_huff_init<C>(tid, S);
     __syncthreads();
@@ -1271,13 +1285,21 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i < 318 ? i - 288 : 0);
         cost[j] = skip ? 0u : L + eb;
     }
-    for (uint32_t k = 0; k < nsg; k++) {
-        uint32_t d = 0;
+    for (uint32_t k0 = 0; k0 < nsg; k0 += HUFF_LDSEG) {
+        uint32_t hr[HUFF_LDSEG][5];
 #pragma unroll
-        for (int j = 0; j < 5; j++) d += cost[j] * hist[(size_t)(seg0 + k) * HIST_WORDS + tid + 64 * j];
+        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-        if (tid == 0) S.dk[k] = d;
+            for (int j = 0; j < 5; j++)
+                hr[k][j] = k0 + k < nsg ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < HUFF_LDSEG; k++) {
+            uint32_t d = 0;
+#pragma unroll
+            for (int j = 0; j < 5; j++) d += cost[j] * hr[k][j];
+            d = wave_sum(d);
+            if (tid == 0 && k0 + k < nsg) S.dk[k0 + k] = d;
+        }
     }
     __syncthreads();
     // a segment's share of a Huffman-coded block must fit k_encode's output buffer
@@ -1291,7 +1313,7 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     // stored: every segment is its own stored block (5-byte header + its bytes)
     uint32_t run = bt == 0 ? 0u : hdr;
     for (uint32_t k = 0; k < nsg; k++) {
-        const uint32_t d = bt == 0 ? 8 * (5 + info[seg0 + k].sl) : S.dk[k];
+        const uint32_t d = bt == 0 ? 8 * (5 + S.sls[k]) : S.dk[k];
         if (tid == 0) {
             SegInfo& g = info[seg0 + k];
             g.btype = bt;
