@@ -412,16 +412,25 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
     return out
 
 
+def progress(rank, msg):
+    """A line on stderr per bench section (rank 0): long runs show they are alive."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def extra(out, svc, rank, world, barrier, iid, side):
     """Secondary lines: the other BASELINE configs (parity-tested in tests/), each timed
     device-resident like the headline; and the PCIe-inclusive end-to-end rate."""
     # PCIe-inclusive end-to-end (D2H of every PNG into pinned host memory)
+    progress(rank, "e2e with D2H")
     rate, gbs = e2e_rate(svc, grid_ctxs(iid, "png"))
     out["e2e_with_d2h"] = {"tiles_per_s": round(rate, 1), "d2h_gbps": round(gbs, 1)}
     # the served path: concurrent single-tile callers through the coalescer
+    progress(rank, "served path")
     # (one node's ranks together: 512 callers per rank only on a single GPU)
     out["served_get_tile_512x512_u16_png"] = serve_lines(svc, iid, (32, 128, 512) if world == 1 else (32, 128))
     # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
+    progress(rank, "raw")
     raw = grid_ctxs(iid, None)
     dtr, sr, _ = run_steps(svc, raw, 5, 2, barrier)
     ms_ext = mean(sr, "ms_extract")
@@ -432,6 +441,7 @@ def extra(out, svc, rank, world, barrier, iid, side):
         "k_extract_frac": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
     # A/B: the same headline batch with the filter-None rows staged in a stream buffer by
     # k_rows first (cfg.stage_rows), instead of assembled from the plane inside k_lz77
+    progress(rank, "staged rows")
     # (serial: one kernel stream, so the kernel times are the kernels' own; compare with
     # the headline's kernel_streams.serial_pass_tiles_per_s)
     with pbx.PixelsService(device=torch.cuda.current_device(), stage_rows=True) as ss:
@@ -445,6 +455,7 @@ def extra(out, svc, rank, world, barrier, iid, side):
             "k_lz77_ms": round(mean(sst, "ms_lz77"), 3)}
     # Row f3: on-GPU resolution pyramid of the headline plane (6 levels of 2x2 box means);
     # algorithmic bytes = every level read once + every lower level written once
+    progress(rank, "pyramid")
     pid = svc.register_plane(5, 0, 0, 0, pbx.UINT16, side, side, generator="noise", plane_no=rank)
     _, pms = svc.build_pyramid(pid, 6, timing=True)
     pb, wl = 0, side
@@ -459,8 +470,10 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # G_NOISE plane stored as 512^2 chunks (1,024 chunks); blosc-lz4 (shuffle, the NGFF
     # writers' default) and zlib-1.  Timed: the decode kernels and the placement kernel
     # (HIP events); the chunk upload is PCIe and reported apart.
+    progress(rank, "zarr")
     out["zarr_decode_16384sq_u16_512chunks"] = zarr_lines(svc, rank, world)
     # G_FAKE (FakeReader-like gradient) PNG, compressible data
+    progress(rank, "fake")
     svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
     fk = grid_ctxs(2, "png")
     dtf, sf, _ = run_steps(svc, fk, 3, 2, barrier)
@@ -468,8 +481,10 @@ def extra(out, svc, rank, world, barrier, iid, side):
         "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
         "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1)}
     # the adaptive PNG filter (option; the reference writes filter None)
+    progress(rank, "adaptive filter")
     out["png_adaptive_filter_512x512_u16"] = adaptive_filter_line(svc, rank, world, barrier, side)
     # configs[2]: 4096 x 1024^2 uint16 PNG from a 65536^2 plane (8 GiB)
+    progress(rank, "configs[2]")
     svc.register_plane(3, 0, 0, 0, pbx.UINT16, 65536, 65536, generator="noise", plane_no=rank)
     c3 = grid_ctxs(3, "png", tile=1024)
     dt3, s3, _ = run_steps(svc, c3, 2, 2, barrier)
@@ -479,6 +494,7 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # configs[3]: whole slide 100000^2 x 5 channels uint16, 512^2 tiles (edge 160 px) -> TIFF.
     # Every rank holds the 5 channels and serves its contiguous band of tile rows of each
     # (SURVEY.md §8(e)); over all ranks the bands cover the whole slide (192,080 tiles).
+    progress(rank, "configs[3]")
     out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
     svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
     with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
@@ -487,6 +503,7 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # configs[4]: mixed stream (uint8/int32/float32 planes 16384^2, w,h in 256..2048,
     # png/tif/raw), 16384 requests as 8 batches of 2048
     import random
+    progress(rank, "configs[4]")
     rnd = random.Random(rank)
     for k, pt in enumerate((pbx.UINT8, pbx.INT32, pbx.FLOAT)):
         svc.register_plane(10 + k, 0, 0, 0, pt, 16384, 16384, generator="noise", plane_no=rank)
@@ -605,10 +622,13 @@ def main():
         return dry_run(args, world, rank)
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
-    torch.cuda.set_device(local)
+    # PBX_BENCH_ONE_GPU=1: every rank on GPU 0 (a rehearsal of the N-rank path on a one-GPU
+    # box; per-rank numbers then share one device)
+    dev = 0 if os.environ.get("PBX_BENCH_ONE_GPU") else local
+    torch.cuda.set_device(dev)
     barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
 
-    svc = pbx.PixelsService(device=local)
+    svc = pbx.PixelsService(device=dev)
     side = GRID * TILE
     iid = 1
     svc.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0,
@@ -689,6 +709,7 @@ def main():
         extra(out, svc, rank, world, barrier, iid, side)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress(rank, "cpu baseline")
         out["cpu_baseline"] = cpu_baseline(threads=args.cpu_threads)
         out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
