@@ -495,11 +495,15 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # Every rank holds the 5 channels and serves its contiguous band of tile rows of each
     # (SURVEY.md §8(e)); over all ranks the bands cover the whole slide (192,080 tiles).
     progress(rank, "configs[3]")
-    out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
-    svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
-    with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
-        out["c4_wholeslide_tif_deflate_100k_u16_5ch"] = wholeslide_line(sd, rank, world, barrier,
-                                                                        steps=1)
+    if os.environ.get("PBX_BENCH_ONE_GPU") and world > 1:
+        # N ranks' 100 GB slides do not fit one GPU: the rehearsal skips configs[3]
+        out["c4_wholeslide_tif_100k_u16_5ch"] = {"skipped": "PBX_BENCH_ONE_GPU rehearsal"}
+    else:
+        out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
+        svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
+        with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
+            out["c4_wholeslide_tif_deflate_100k_u16_5ch"] = wholeslide_line(sd, rank, world, barrier,
+                                                                            steps=1)
     # configs[4]: mixed stream (uint8/int32/float32 planes 16384^2, w,h in 256..2048,
     # png/tif/raw), 16384 requests as 8 batches of 2048
     import random
