@@ -114,7 +114,7 @@ struct EncSmem {
     uint32_t red[C::NW];
 };
 static_assert(CRCX_WORDS * 4 <= DC::NW * DC::MAXMW * 6, "the CRC combine tables fit the match lists' room");
-static_assert(sizeof(EncSmem<DC>) <= 40 * 1024, "four encode workgroups per CU (160 KiB LDS)");
+static_assert(sizeof(EncSmem<DC>) * 512 <= 40 * 1024 * DC::NT, "32 encode waves per CU (160 KiB LDS)");
 
 // Slicing-by-4 CRC-32 tables, built at compile time into device memory (copied to LDS).
 struct CrcTables {
