@@ -328,3 +328,13 @@ def test_kernel_streams_overlap_same_bytes(service, streams, stagger):
     want = run(1, 0)
     got = run(streams, stagger)
     assert got == want
+
+
+def test_kernel_streams_bad_arguments(service):
+    """pbx_set_kernel_streams: 1..4 streams, stagger 0..4; anything else is a 400 and keeps
+    the setting."""
+    for ns, sg in [(0, 1), (5, 1), (3, -1), (3, 5)]:
+        with pytest.raises(pbx.PbxError) as e:
+            service.set_kernel_streams(ns, sg)
+        assert e.value.status == pbx.E_BADARG
+    service.set_kernel_streams(3, 1)
