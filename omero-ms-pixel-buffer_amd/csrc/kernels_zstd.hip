@@ -138,6 +138,21 @@ struct BitBack {
         pos -= (int32_t)n;
         return v;
     }
+    // n <= 56 bits at once (a refill leaves >= 57 cached bits below pos): the first field
+    // read is the value's top bits
+    __device__ uint64_t read64(ZIn& in, uint32_t n) {
+        if (n == 0) return 0;
+        const int32_t q = pos - (int32_t)n;
+        if (q < cb || pos > cb + 64) {
+            const int32_t e = (pos + 7) >> 3;
+            const int32_t sb = e >= 8 ? e - 8 : 0;
+            cont = in.le64_back(lo + (uint32_t)sb);
+            cb = 8 * sb;
+        }
+        const uint64_t v = q >= cb ? cont >> (q - cb) : cont << (cb - q);
+        pos = q;
+        return v & ((1ull << n) - 1ull);
+    }
 };
 
 // FSE table description (RFC 8878 4.1.1) at frame byte q: normalized counts into ZD_NORM;
@@ -643,9 +658,27 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             if (llc > 35 || mlc > 52 || ofc > 31) { bad = 31; break; }
             // the four code tables up front (scalar loads, one wait)
             const uint32_t mlb = c_ml_base[mlc], mlx = c_ml_bits[mlc], llb = c_ll_base[llc], llx = c_ll_bits[llc];
-            const uint32_t ofv = (1u << ofc) + br.read(in, ofc);
-            const uint32_t ml = mlb + br.read(in, mlx);
-            const uint32_t ll = llb + br.read(in, llx);
+            // every bit this sequence reads (offset, match and literal length extra bits, then
+            // the three state updates) in one read when they fit 56 bits: the fields are
+            // shifts of one value instead of six dependent reads
+            const uint32_t nbl = (le >> 8) & 0xFF, nbm = (me >> 8) & 0xFF, nbo = (oe >> 8) & 0xFF;
+            const uint32_t nup = i + 1 < nseq ? nbl + nbm + nbo : 0u;
+            const uint32_t T = ofc + mlx + llx + nup;
+            uint32_t ofx, mlv, llv;
+            uint64_t all = 0;
+            if (T <= 56) {
+                all = br.read64(in, T);
+                ofx = (uint32_t)(all >> (T - ofc)) & ((1u << ofc) - 1u);
+                mlv = (uint32_t)(all >> (T - ofc - mlx)) & ((1u << mlx) - 1u);
+                llv = (uint32_t)(all >> (T - ofc - mlx - llx)) & ((1u << llx) - 1u);
+            } else {
+                ofx = br.read(in, ofc);
+                mlv = br.read(in, mlx);
+                llv = br.read(in, llx);
+            }
+            const uint32_t ofv = (1u << ofc) + ofx;
+            const uint32_t ml = mlb + mlv;
+            const uint32_t ll = llb + llv;
             uint32_t off;
             if (ofv > 3) {
                 off = ofv - 3;
@@ -666,9 +699,15 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
                 }
             }
             if (i + 1 < nseq) {  // state updates: literal lengths, match lengths, offsets
-                lls = (le >> 16) + br.read(in, (le >> 8) & 0xFF);
-                mls = (me >> 16) + br.read(in, (me >> 8) & 0xFF);
-                ofs = (oe >> 16) + br.read(in, (oe >> 8) & 0xFF);
+                if (T <= 56) {
+                    lls = (le >> 16) + ((uint32_t)(all >> (nbm + nbo)) & ((1u << nbl) - 1u));
+                    mls = (me >> 16) + ((uint32_t)(all >> nbo) & ((1u << nbm) - 1u));
+                    ofs = (oe >> 16) + ((uint32_t)all & ((1u << nbo) - 1u));
+                } else {
+                    lls = (le >> 16) + br.read(in, nbl);
+                    mls = (me >> 16) + br.read(in, nbm);
+                    ofs = (oe >> 16) + br.read(in, nbo);
+                }
             }
             ZSD(cread += __builtin_amdgcn_s_memtime() - s0;)
             ZSD(const uint64_t s1 = __builtin_amdgcn_s_memtime(); nfar += off > 4096; nlitrun += ll > 0;)
