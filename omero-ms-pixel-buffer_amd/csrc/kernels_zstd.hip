@@ -423,6 +423,10 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
     uint8_t* lit = litbuf + (size_t)si * ZSTD_LITSTRIDE;
     const uint32_t ilen = in.len;
     uint32_t bad = 0, q = 0;
+    // the length codes' baselines and extra bits, lane-held (a readlane per sequence instead
+    // of a scalar-cache round trip)
+    const uint32_t v_llb = c_ll_base[lane < 36 ? lane : 35], v_llx = c_ll_bits[lane < 36 ? lane : 35];
+    const uint32_t v_mlb = c_ml_base[lane < 53 ? lane : 52], v_mlx = c_ml_bits[lane < 53 ? lane : 52];
 #ifdef PBX_ZARR_DIAG  // diagnostic build only: stream 0's clocks (printf)
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     uint64_t clit = 0, cseq = 0, ctab = 0;
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             const uint32_t llc = le & 0xFF, ofc = oe & 0xFF, mlc = me & 0xFF;
             if (llc > 35 || mlc > 52 || ofc > 31) { bad = 31; break; }
             // the four code tables up front (scalar loads, one wait)
-            const uint32_t mlb = c_ml_base[mlc], mlx = c_ml_bits[mlc], llb = c_ll_base[llc], llx = c_ll_bits[llc];
+            const uint32_t mlb = rdl(v_mlb, mlc), mlx = rdl(v_mlx, mlc), llb = rdl(v_llb, llc), llx = rdl(v_llx, llc);
             // every bit this sequence reads (offset, match and literal length extra bits, then
             // the three state updates) in one read when they fit 56 bits: the fields are
             // shifts of one value instead of six dependent reads
