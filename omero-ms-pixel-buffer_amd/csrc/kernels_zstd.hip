@@ -116,6 +116,7 @@ struct BitBack {
     // the state is wave-uniform: pin it to SGPRs at the top of a decode loop (LLVM otherwise
     // carries it in VGPRs through the loop's phis)
     __device__ void pin() {
+        lo = rfl(lo);
         pos = (int32_t)rfl((uint32_t)pos);
         cb = (int32_t)rfl((uint32_t)cb);
         cont = (uint64_t)rfl((uint32_t)(cont >> 32)) << 32 | rfl((uint32_t)cont);
@@ -653,6 +654,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             ZSD(const uint64_t s0 = __builtin_amdgcn_s_memtime();)
             // the sequence state is wave-uniform: keep it in SGPRs (see BitBack::pin)
             br.pin();
+            in.win.base = rfl(in.win.base);
             lls = rfl(lls); ofs = rfl(ofs); mls = rfl(mls);
             rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
             lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed); bn = rfl(bn);
