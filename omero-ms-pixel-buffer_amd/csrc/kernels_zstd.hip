@@ -621,6 +621,10 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         BitBack br;
         if (!br.init(in, q, bend)) { bad = 30; break; }
         uint32_t lls = br.read(in, ll_log), ofs = br.read(in, of_log), mls = br.read(in, ml_log);
+        // the next sequence's three table entries are read as soon as its states are known
+        // (the LDS latency overlaps the batch bookkeeping); uniform values, taken at the top
+        uint32_t pe_l = zd32(wb + ZD_LL + 4 * lls), pe_o = zd32(wb + ZD_OF + 4 * ofs),
+                 pe_m = zd32(wb + ZD_ML + 4 * mls);
         // Sequences are decoded into a batch (lane j: sequence j's literal length, match length
         // and offset) and a batch of up to 64 is executed byte-parallel: output offsets by prefix
         // sums, then 64 output bytes per step, each lane finding its sequence (start flags,
@@ -658,8 +662,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             lls = rfl(lls); ofs = rfl(ofs); mls = rfl(mls);
             rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
             lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed); bn = rfl(bn);
-            const uint32_t le = rfl(zd32(wb + ZD_LL + 4 * lls)), oe = rfl(zd32(wb + ZD_OF + 4 * ofs)),
-                           me = rfl(zd32(wb + ZD_ML + 4 * mls));
+            const uint32_t le = rfl(pe_l), oe = rfl(pe_o), me = rfl(pe_m);
             const uint32_t llc = le & 0xFF, ofc = oe & 0xFF, mlc = me & 0xFF;
             if (llc > 35 || mlc > 52 || ofc > 31) { bad = 31; break; }
             // the four code tables up front (scalar loads, one wait)
@@ -714,6 +717,9 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
                     mls = (me >> 16) + br.read(in, nbm);
                     ofs = (oe >> 16) + br.read(in, nbo);
                 }
+                pe_l = zd32(wb + ZD_LL + 4 * lls);
+                pe_o = zd32(wb + ZD_OF + 4 * ofs);
+                pe_m = zd32(wb + ZD_ML + 4 * mls);
             }
             ZSD(cread += __builtin_amdgcn_s_memtime() - s0;)
             ZSD(const uint64_t s1 = __builtin_amdgcn_s_memtime(); nfar += off > 4096; nlitrun += ll > 0;)
