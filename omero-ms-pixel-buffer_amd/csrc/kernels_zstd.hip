@@ -58,6 +58,13 @@ __constant__ uint32_t c_ml_base[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 
 __constant__ uint32_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                       0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9,
                                       10, 11, 12, 13, 14, 15, 16};
+// A decoding-table entry's payload (its low 13 bits): the symbol for offsets; for literal
+// and match lengths the code's extra-bit count x (5 bits) and baseline: 1 << x (+ 3 for
+// match lengths) when bit 5 is set, else bits 6..12 (every other baseline is < 128).  The
+// sequence loop then needs no second lookup per length code.
+__device__ __forceinline__ uint32_t len_payload(uint32_t base, uint32_t bits, uint32_t add) {
+    return base == (1u << bits) + add ? bits | 32u : bits | (base << 6);
+}
 // predefined distributions (3.1.1.3.2.2)
 __constant__ int16_t c_ll_def[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2,
                                      2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
@@ -213,9 +220,16 @@ __device__ uint32_t read_ncount(ZIn& in, uint32_t wb, uint32_t q, uint32_t qend,
     return used;
 }
 
+// The payload of symbol s of table kind (0 literal lengths, 1 offsets, 2 match lengths).
+__device__ __forceinline__ uint32_t tab_payload(uint32_t kind, uint32_t s) {
+    if (kind == 0) return len_payload(c_ll_base[s < 36 ? s : 35], c_ll_bits[s < 36 ? s : 35], 0);
+    if (kind == 2) return len_payload(c_ml_base[s < 53 ? s : 52], c_ml_bits[s < 53 ? s : 52], 3);
+    return s;
+}
+
 // FSE decoding table (RFC 8878 4.1.1, zstd FSE_buildDTable) from the counts in ZD_NORM:
-// entries u32 sym | nbBits << 8 | baseline << 16 at LDS byte `tab`.
-__device__ void build_fse(uint32_t wb, uint32_t tab, uint32_t log, uint32_t nsym, uint32_t lane) {
+// entries u32 payload(sym) | nbBits << 13 | baseline << 17 at LDS byte `tab`.
+__device__ void build_fse(uint32_t wb, uint32_t tab, uint32_t log, uint32_t nsym, uint32_t lane, uint32_t kind) {
     const uint32_t size = 1u << log, mask = size - 1;
     uint32_t high = size - 1;
     // "less than 1" symbols at the top; symbolNext = count (1 for those)
@@ -253,7 +267,7 @@ __device__ void build_fse(uint32_t wb, uint32_t tab, uint32_t log, uint32_t nsym
         if (u < size) {
             const uint32_t nb = log - hibit(ns);
             const uint32_t base = (ns << nb) - size;
-            zd32(tab + 4 * u) = s | (nb << 8) | (base << 16);
+            zd32(tab + 4 * u) = tab_payload(kind, s) | (nb << 13) | (base << 17);
             atomicAdd(&zd32(wb + ZD_NEXT + 4 * s), 1u);  // this group's occurrences
         }
         __builtin_amdgcn_wave_barrier();
@@ -264,15 +278,15 @@ __device__ void build_fse(uint32_t wb, uint32_t tab, uint32_t log, uint32_t nsym
 // A sequence table for a Symbol_Compression_Mode: 0 predefined, 1 RLE, 2 FSE-compressed,
 // 3 repeat (the table and log are left as they are).  Returns the bytes of the section used,
 // or -1 on error.
-__device__ int32_t seq_table(ZIn& in, uint32_t wb, uint32_t tab, uint32_t mode, uint32_t q, uint32_t qend,
-                             const int16_t* def, uint32_t def_n, uint32_t def_log, uint32_t max_sym,
-                             uint32_t max_log, uint32_t& log, bool& have, uint32_t lane) {
+__device__ int32_t seq_table(ZIn& in, uint32_t wb, uint32_t tab, uint32_t kind, uint32_t mode, uint32_t q,
+                             uint32_t qend, const int16_t* def, uint32_t def_n, uint32_t def_log,
+                             uint32_t max_sym, uint32_t max_log, uint32_t& log, bool& have, uint32_t lane) {
     if (mode == 0) {
         for (uint32_t s = lane; s < 256; s += 64)
             zdi16(wb + ZD_NORM + 2 * s) = s < def_n ? def[s] : (int16_t)0;
         __builtin_amdgcn_wave_barrier();
         log = def_log;
-        build_fse(wb, tab, log, def_n, lane);
+        build_fse(wb, tab, log, def_n, lane, kind);
         have = true;
         return 0;
     }
@@ -280,7 +294,7 @@ __device__ int32_t seq_table(ZIn& in, uint32_t wb, uint32_t tab, uint32_t mode, 
         if (q >= qend) return -1;
         const uint32_t s = in.byte(q);
         if (s > max_sym) return -1;
-        if (lane == 0) zd32(tab) = s;  // nbBits 0, baseline 0
+        if (lane == 0) zd32(tab) = tab_payload(kind, s);  // nbBits 0, baseline 0
         __builtin_amdgcn_wave_barrier();
         log = 0;
         have = true;
@@ -291,7 +305,7 @@ __device__ int32_t seq_table(ZIn& in, uint32_t wb, uint32_t tab, uint32_t mode, 
         const uint32_t used = read_ncount(in, wb, q, qend, max_sym, max_log, l, n, lane);
         if (!used) return -1;
         log = l;
-        build_fse(wb, tab, log, n, lane);
+        build_fse(wb, tab, log, n, lane, kind);
         have = true;
         return (int32_t)used;
     }
@@ -320,7 +334,7 @@ __device__ uint32_t read_huf_tree(ZIn& in, uint32_t wb, uint32_t q, uint32_t qen
         uint32_t wlog, wn;
         const uint32_t nc = read_ncount(in, wb, q + 1, q + used, 255, 6, wlog, wn, lane);
         if (!nc) return 0;
-        build_fse(wb, wb + ZD_WT, wlog, wn, lane);
+        build_fse(wb, wb + ZD_WT, wlog, wn, lane, 1);
         BitBack br;
         if (!br.init(in, q + 1 + nc, q + used)) return 0;
         uint32_t s1 = br.read(in, wlog), s2 = br.read(in, wlog);
@@ -329,7 +343,7 @@ __device__ uint32_t read_huf_tree(ZIn& in, uint32_t wb, uint32_t q, uint32_t qen
             if (nw >= 255) return 0;
             if (lane == 0) zlds[wb + ZD_WGT + nw] = (uint8_t)(e & 0xFF);
             nw++;
-            s1 = (e >> 16) + br.read(in, (e >> 8) & 0xFF);
+            s1 = (e >> 17) + br.read(in, (e >> 13) & 15);
             if (br.pos < 0) {
                 e = zd32(wb + ZD_WT + 4 * s2);
                 if (nw >= 255) return 0;
@@ -341,7 +355,7 @@ __device__ uint32_t read_huf_tree(ZIn& in, uint32_t wb, uint32_t q, uint32_t qen
             if (nw >= 255) return 0;
             if (lane == 0) zlds[wb + ZD_WGT + nw] = (uint8_t)(e & 0xFF);
             nw++;
-            s2 = (e >> 16) + br.read(in, (e >> 8) & 0xFF);
+            s2 = (e >> 17) + br.read(in, (e >> 13) & 15);
             if (br.pos < 0) {
                 e = zd32(wb + ZD_WT + 4 * s1);
                 if (nw >= 255) return 0;
@@ -424,10 +438,6 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
     uint8_t* lit = litbuf + (size_t)si * ZSTD_LITSTRIDE;
     const uint32_t ilen = in.len;
     uint32_t bad = 0, q = 0;
-    // the length codes' baselines and extra bits, lane-held (a readlane per sequence instead
-    // of a scalar-cache round trip)
-    const uint32_t v_llb = c_ll_base[lane < 36 ? lane : 35], v_llx = c_ll_bits[lane < 36 ? lane : 35];
-    const uint32_t v_mlb = c_ml_base[lane < 53 ? lane : 52], v_mlx = c_ml_bits[lane < 53 ? lane : 52];
 #ifdef PBX_ZARR_DIAG  // diagnostic build only: stream 0's clocks (printf)
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     uint64_t clit = 0, cseq = 0, ctab = 0;
@@ -608,13 +618,13 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         if (q >= bend) { bad = 25; break; }
         const uint32_t modes = in.byte(q++);
         if (modes & 3) { bad = 26; break; }
-        int32_t u = seq_table(in, wb, wb + ZD_LL, modes >> 6, q, bend, c_ll_def, 36, 6, 35, 9, ll_log, have_ll, lane);
+        int32_t u = seq_table(in, wb, wb + ZD_LL, 0, modes >> 6, q, bend, c_ll_def, 36, 6, 35, 9, ll_log, have_ll, lane);
         if (u < 0) { bad = 27; break; }
         q += (uint32_t)u;
-        u = seq_table(in, wb, wb + ZD_OF, (modes >> 4) & 3, q, bend, c_of_def, 29, 5, 31, 8, of_log, have_of, lane);
+        u = seq_table(in, wb, wb + ZD_OF, 1, (modes >> 4) & 3, q, bend, c_of_def, 29, 5, 31, 8, of_log, have_of, lane);
         if (u < 0) { bad = 28; break; }
         q += (uint32_t)u;
-        u = seq_table(in, wb, wb + ZD_ML, (modes >> 2) & 3, q, bend, c_ml_def, 53, 6, 52, 9, ml_log, have_ml, lane);
+        u = seq_table(in, wb, wb + ZD_ML, 2, (modes >> 2) & 3, q, bend, c_ml_def, 53, 6, 52, 9, ml_log, have_ml, lane);
         if (u < 0) { bad = 29; break; }
         q += (uint32_t)u;
         ZSD(const uint64_t b2 = __builtin_amdgcn_s_memtime(); ctab += b2 - b1; nseqs += nseq;)
@@ -663,14 +673,17 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
             lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed); bn = rfl(bn);
             const uint32_t le = rfl(pe_l), oe = rfl(pe_o), me = rfl(pe_m);
-            const uint32_t llc = le & 0xFF, ofc = oe & 0xFF, mlc = me & 0xFF;
-            if (llc > 35 || mlc > 52 || ofc > 31) { bad = 31; break; }
+            // (the tables hold only symbols read_ncount / the RLE mode checked against the
+            // alphabets: offset codes <= 31, every length code valid)
+            const uint32_t ofc = oe & 0x1F;
             // the four code tables up front (scalar loads, one wait)
-            const uint32_t mlb = rdl(v_mlb, mlc), mlx = rdl(v_mlx, mlc), llb = rdl(v_llb, llc), llx = rdl(v_llx, llc);
+            const uint32_t llx = le & 31, mlx = me & 31;
+            const uint32_t llb = (le & 32) ? 1u << llx : (le >> 6) & 127;
+            const uint32_t mlb = (me & 32) ? (1u << mlx) + 3 : (me >> 6) & 127;
             // every bit this sequence reads (offset, match and literal length extra bits, then
             // the three state updates) in one read when they fit 56 bits: the fields are
             // shifts of one value instead of six dependent reads
-            const uint32_t nbl = (le >> 8) & 0xFF, nbm = (me >> 8) & 0xFF, nbo = (oe >> 8) & 0xFF;
+            const uint32_t nbl = (le >> 13) & 15, nbm = (me >> 13) & 15, nbo = (oe >> 13) & 15;
             const uint32_t nup = i + 1 < nseq ? nbl + nbm + nbo : 0u;
             const uint32_t T = ofc + mlx + llx + nup;
             uint32_t ofx, mlv, llv;
@@ -709,13 +722,13 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             }
             if (i + 1 < nseq) {  // state updates: literal lengths, match lengths, offsets
                 if (T <= 56) {
-                    lls = (le >> 16) + ((uint32_t)(all >> (nbm + nbo)) & ((1u << nbl) - 1u));
-                    mls = (me >> 16) + ((uint32_t)(all >> nbo) & ((1u << nbm) - 1u));
-                    ofs = (oe >> 16) + ((uint32_t)all & ((1u << nbo) - 1u));
+                    lls = (le >> 17) + ((uint32_t)(all >> (nbm + nbo)) & ((1u << nbl) - 1u));
+                    mls = (me >> 17) + ((uint32_t)(all >> nbo) & ((1u << nbm) - 1u));
+                    ofs = (oe >> 17) + ((uint32_t)all & ((1u << nbo) - 1u));
                 } else {
-                    lls = (le >> 16) + br.read(in, nbl);
-                    mls = (me >> 16) + br.read(in, nbm);
-                    ofs = (oe >> 16) + br.read(in, nbo);
+                    lls = (le >> 17) + br.read(in, nbl);
+                    mls = (me >> 17) + br.read(in, nbm);
+                    ofs = (oe >> 17) + br.read(in, nbo);
                 }
                 pe_l = zd32(wb + ZD_LL + 4 * lls);
                 pe_o = zd32(wb + ZD_OF + 4 * ofs);
