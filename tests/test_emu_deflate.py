@@ -115,3 +115,25 @@ def test_segment_share_over_capacity_is_stored():
     z, blks = _emu.deflate(data, 256)
     assert zlib.decompress(z) == data
     assert blks[0].btype == 0  # stored: a coded block would overflow the third segment
+
+
+@pytest.mark.parametrize("n", [1, 16383, 16384 * 16, 16384 * 16 + 1, 524800, 1024 * 2049, 3_000_017])
+def test_blocks_split_segments_evenly(n):
+    """A tile's segments go to ceil(nseg / BLK) Huffman blocks of nearly equal size (at most
+    BLK segments each, sizes differing by at most one segment): the 33 segments of a 512x512
+    uint16 PNG make three blocks of 11."""
+    L = _emu.lib()
+    blk, seg = L.pbxemu_blk_segs(), L.pbxemu_split_max()
+    data = bytes((i * 7 + (i >> 9)) & 0xFF for i in range(n))
+    z, blks = _emu.deflate(data, 1025)
+    assert zlib.decompress(z) == data
+    nseg = L.pbxemu_nsegs(n)
+    assert len(blks) == -(-nseg // blk)
+    assert sum(b.len for b in blks) == n
+    n0 = -(-n // seg)
+    seg_len = min(seg, (-(-n // n0) + 15) // 16 * 16)  # deflate_split: equal but the last
+    counts = [-(-b.len // seg_len) for b in blks]
+    assert sum(counts) == nseg
+    assert max(counts) <= blk and max(counts) - min(counts) <= 1
+    if n == 524800:
+        assert counts == [11, 11, 11]
