@@ -239,12 +239,12 @@ def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
         "decoded_gbps": round(side * side * 2 / ((md + mp) * 1e-3) / 1e9, 1)}
     # the same chunks for 4 planes (4 x 512 MiB) in ONE pbx_planes_register_zarr call: 4x the
     # streams in flight hide the per-stream decode latency
-    for name, comp in (("blosc_lz4", "blosc"), ("zlib1", "zlib")):
+    multi = [("blosc_lz4", "blosc", {}), ("zlib1", "zlib", {"level": 1})]
+    if _zarr.cblosc() is not None:
+        multi.append(("blosc_zstd5", "blosc", {"cname": "zstd", "clevel": 5, "shuffle": 1}))
+    for name, comp, kw in multi:
         with ThreadPoolExecutor(16) as ex:
-            if comp == "blosc":
-                chunks = list(ex.map(lambda c: _zarr.blosc_encode(c.tobytes(), 2), grid))
-            else:
-                chunks = list(ex.map(lambda c: _zarr.zlib_encode(c.tobytes(), 1), grid))
+            chunks = list(ex.map(lambda c: enc(c, comp, kw), grid))
         specs = [dict(image_id=22, z=k, c=0, t=0, pixel_type=pbx.UINT16, size_x=side, size_y=side,
                       chunk_x=chunk, chunk_y=chunk, codec=comp, chunks=chunks) for k in range(4)]
         dec, plc = [], []
