@@ -666,12 +666,9 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
         };
         for (uint32_t i = 0; i < nseq; i++) {
             ZSD(const uint64_t s0 = __builtin_amdgcn_s_memtime();)
-            // the sequence state is wave-uniform: keep it in SGPRs (see BitBack::pin)
-            br.pin();
-            in.win.base = rfl(in.win.base);
-            lls = rfl(lls); ofs = rfl(ofs); mls = rfl(mls);
-            rep1 = rfl(rep1); rep2 = rfl(rep2); rep3 = rfl(rep3);
-            lp = rfl(lp); lwb = rfl(lwb); o.op = rfl(o.op); o.flushed = rfl(o.flushed); bn = rfl(bn);
+            // (The sequence state is wave-uniform but left where LLVM puts it, much of it in
+            // VGPRs: pinning it all to SGPRs put the loop on the CU's one scalar unit, which
+            // eight frames per CU saturate; 45.6 -> 54.7 GB/s without the pins.)
             const uint32_t le = rfl(pe_l), oe = rfl(pe_o), me = rfl(pe_m);
             // (the tables hold only symbols read_ncount / the RLE mode checked against the
             // alphabets: offset codes <= 31, every length code valid)
