@@ -412,7 +412,6 @@ __device__ bool huf_stream(ZIn& in, uint32_t wb, uint32_t hlog, uint32_t lo, uin
     if (!br.init(in, lo, hi)) return false;
     uint32_t acc = 0;
     for (uint32_t i = 0; i < n; i++) {
-        br.pin();
         const uint32_t e = rfl(zd16(wb + ZD_HUF + 2 * br.peek(in, hlog)));
         br.pos -= (int32_t)(e >> 8);
         acc = (lane == (i & 63)) ? (e & 0xFF) : acc;
