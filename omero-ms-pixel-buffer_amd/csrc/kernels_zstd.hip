@@ -668,7 +668,7 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
             // (The sequence state is wave-uniform but left where LLVM puts it, much of it in
             // VGPRs: pinning it all to SGPRs put the loop on the CU's one scalar unit, which
             // eight frames per CU saturate; 45.6 -> 54.7 GB/s without the pins.)
-            const uint32_t le = rfl(pe_l), oe = rfl(pe_o), me = rfl(pe_m);
+            const uint32_t le = pe_l, oe = pe_o, me = pe_m;  // (every lane the same)
             // (the tables hold only symbols read_ncount / the RLE mode checked against the
             // alphabets: offset codes <= 31, every length code valid)
             const uint32_t ofc = oe & 0x1F;
