@@ -88,7 +88,7 @@ struct ZIn {
         uint32_t a, b;
         __builtin_memcpy(&a, zlds + win.wo + q - win.base, 4);
         __builtin_memcpy(&b, zlds + win.wo + q - win.base + 4, 4);
-        return ((uint64_t)rfl(b) << 32) | rfl(a);
+        return ((uint64_t)b << 32) | a;  // (every lane the same: no readfirstlane, see §10)
     }
     // 8 bytes from q (little-endian), window placed to start at q (forward reads)
     __device__ uint64_t le64_fwd(uint32_t q) {
