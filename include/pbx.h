@@ -28,17 +28,31 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 5
+#define PBX_ABI_VERSION 6
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
- * IllegalArgumentException -> 400 (:137-140); any other exception -> 500 (:141-146). */
+ * IllegalArgumentException -> 400 (:137-140); any other exception -> 500 (:141-146).
+ *
+ * PBX_E_NOT_RESIDENT is never sent to a client.  It means "this context does not hold the
+ * plane the request needs": the image is unknown here, its (z, c, t, level) plane was never
+ * loaded or was evicted, or the region lies outside the row band this context owns.  The
+ * reference would open the plane on demand (getPixels + getPixelBuffer,
+ * TileRequestHandler.java:84-86,201-241); the binding does the same — look the image up,
+ * load the plane with pbx_image_declare / pbx_plane_create / pbx_plane_write_rows /
+ * pbx_plane_commit and retry.  A context answers 404 only for what the
+ * reference itself answers 404. */
 enum pbx_status {
     PBX_OK = 0,
     PBX_E_BADARG = 400,
     PBX_E_NOTFOUND = 404,
+    PBX_E_EXISTS = 409,      /* registration: the (image, z, c, t, level) key is taken (loaded
+                                or being loaded by another caller) */
+    PBX_E_NOT_RESIDENT = 460,/* tile status: load the plane, then retry (see above) */
     PBX_E_INTERNAL = 500,
-    PBX_E_PENDING = 504      /* pbx_wait: the batch is still running (not a tile status) */
+    PBX_E_PENDING = 504,     /* pbx_wait: the batch is still running (not a tile status) */
+    PBX_E_NO_SPACE = 507     /* registration: the plane does not fit the HBM residency budget
+                                even after evicting every idle plane */
 };
 
 /* OMERO pixel types (ome.xml.model.enums.PixelType; TileRequestHandler.java:100-101,164-165). */
@@ -112,7 +126,74 @@ typedef struct pbx_plane_desc {
 } pbx_plane_desc;
 
 int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* desc, uint64_t* plane_id);
+/* Frees the plane.  Batches planned before the call keep reading it: the HBM is returned
+ * when the last of them is destroyed (pbx_batch_destroy), never under a running kernel. */
 int pbx_plane_release(pbx_ctx* ctx, uint64_t plane_id);
+
+/* ---- Plane residency: planes opened on demand, in row bands, under an HBM budget ----
+ *
+ * The reference opens an image's PixelBuffer per request (getPixels :220-241, then
+ * getPixelBuffer :201-211 and getTileDirect :107-109).  Here the bytes of a plane are loaded
+ * into HBM once and then serve every tile of it; a request for a plane this context does not
+ * hold answers PBX_E_NOT_RESIDENT and the binding loads it.
+ *
+ * pbx_image_declare records the Pixels row getPixels returns (:84; pixelsType, sizeX/Y/Z/C/T)
+ * and the PixelBuffer's getResolutionLevels().  With it a request for a z/c/t outside the
+ * image, or a resolution outside its levels, is the reference's 404 without loading anything;
+ * without it (planes registered directly) the image is described by its registered planes. */
+typedef struct pbx_image_desc {
+    int64_t image_id;
+    int32_t pixel_type;          /* enum pbx_pixel_type (Pixels.pixelsType) */
+    int32_t size_x, size_y;      /* full resolution (Pixels.sizeX / sizeY) */
+    int32_t size_z, size_c, size_t_;
+    int32_t levels;              /* PixelBuffer.getResolutionLevels(); >= 1 */
+    int32_t reserved;
+} pbx_image_desc;
+/* Idempotent; 400 if it contradicts an earlier declaration or a registered plane. */
+int pbx_image_declare(pbx_ctx* ctx, const pbx_image_desc* desc);
+/* Releases every plane of the image and forgets its record (requests then answer
+ * NOT_RESIDENT).  404 if the image is unknown. */
+int pbx_image_release(pbx_ctx* ctx, int64_t image_id);
+
+/* Allocates a plane — or only its rows [band_y0, band_y0 + band_rows) when band_rows > 0 (a
+ * rank's tile-row band of a whole slide) — under the key desc->(image_id, z,
+ * c, t, resolution).  desc->size_x / size_y are the plane's (the level's) full size; requests
+ * for rows outside the band answer PBX_E_NOT_RESIDENT (another context owns them).
+ * desc->source: PBX_SRC_HOST -> the plane is empty and not served until pbx_plane_commit;
+ * its rows arrive by pbx_plane_write_rows in desc->byte_order.  Generators -> the band is
+ * generated on the GPU and the plane is ready at once.  409 if the key is loaded or being
+ * loaded; 507 if it does not fit the residency budget (pbx_set_residency_budget). */
+int pbx_plane_create(pbx_ctx* ctx, const pbx_plane_desc* desc, int32_t band_y0, int32_t band_rows,
+                     uint64_t* plane_id);
+/* Rows [y0, y0 + rows) of a created plane (inside its band): `rows` rows of size_x samples,
+ * packed (size_x * bpp bytes each), as PixelBuffer.getTileDirect(z, c, t, 0, y0, sizeX, rows)
+ * returns them.  Copied through pooled pinned staging to HBM; the caller's buffer is free
+ * again when the call returns.  Any number of calls, in any order, of any band size. */
+int pbx_plane_write_rows(pbx_ctx* ctx, uint64_t plane_id, int32_t y0, int32_t rows, const void* data,
+                         uint64_t bytes);
+/* Publishes a created plane: from now on its tiles are served.  400 if a row of the band was
+ * never written. */
+int pbx_plane_commit(pbx_ctx* ctx, uint64_t plane_id);
+/* The plane registered under a key (STORED level): its id and state (0 loading, 1 ready,
+ * 2 evicted) and resident band; 404 if the key is not registered.  Lets a binding that got
+ * NOT_RESIDENT tell "load it" from "another caller is loading it". */
+int pbx_plane_lookup(pbx_ctx* ctx, int64_t image_id, int32_t z, int32_t c, int32_t t, int32_t level,
+                     uint64_t* plane_id, int32_t* state, int32_t* band_y0, int32_t* band_rows);
+
+/* HBM residency budget for planes (bytes; 0 = none, the default, or $PBX_HBM_BUDGET_MB).  A
+ * registration that would exceed it first evicts idle planes, least recently used first (a
+ * plane is idle when no planned batch reads it).  With or without a budget, a plane
+ * allocation that fails for lack of device memory evicts idle planes and retries.  An evicted
+ * plane's requests answer PBX_E_NOT_RESIDENT until it is registered again. */
+int pbx_set_residency_budget(pbx_ctx* ctx, uint64_t bytes);
+typedef struct pbx_residency_stats {
+    uint64_t budget;             /* 0 = none */
+    uint64_t resident_bytes;     /* HBM held by planes (incl. released ones still read) */
+    uint64_t planes;             /* registered planes resident in HBM */
+    uint64_t evicted_planes;     /* registered keys whose plane was evicted */
+    uint64_t evictions, evicted_bytes;  /* totals since pbx_init */
+} pbx_residency_stats;
+int pbx_residency_stats_get(pbx_ctx* ctx, pbx_residency_stats* out);
 /* Resolution pyramid on the GPU (the lower levels
  * PixelBuffer.setResolutionLevel selects, TileRequestHandler.java:89-91): registers `levels`
  * planes of the same (image, z, c, t) at resolutions r+1 .. r+levels (r = the plane's), each
@@ -265,7 +346,8 @@ int pbx_device_synchronize(pbx_ctx* ctx);
 int pbx_set_kernel_streams(pbx_ctx* ctx, int32_t streams, int32_t stagger);
 
 /* sizeof of the ABI structs, for bindings to check their layouts: pbx_config,
- * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats (in that order). */
+ * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats, pbx_image_desc,
+ * pbx_residency_stats (in that order).  Returns the number of structs (7). */
 int pbx_abi_sizes(uint64_t* sizes, int n);
 
 /* Request sharding across GPUs (one process per GPU, no collectives): the rank that

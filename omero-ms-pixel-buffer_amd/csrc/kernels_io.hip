@@ -19,16 +19,17 @@
 namespace pbx {
 
 // ------------------------------------------------------------------- synthetic planes
+// Rows [y0, y0 + rows) of the plane (a row band, or the whole plane), row y0 at `out`.
 __global__ __launch_bounds__(256) void k_gen_plane(uint8_t* __restrict__ out, int64_t pitch,
-                                                   int32_t sx, int32_t sy, int32_t pt, int32_t bpp,
-                                                   int32_t kind, uint64_t seed, int32_t plane_no,
-                                                   int32_t z, int32_t c, int32_t t) {
-    const uint64_t total = (uint64_t)sx * (uint64_t)sy;
+                                                   int32_t sx, int32_t y0, int32_t rows, int32_t pt,
+                                                   int32_t bpp, int32_t kind, uint64_t seed,
+                                                   int32_t plane_no, int32_t z, int32_t c, int32_t t) {
+    const uint64_t total = (uint64_t)sx * (uint64_t)rows;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
-        const uint64_t y = idx / (uint64_t)sx, x = idx - y * (uint64_t)sx;
-        const uint64_t v = gen_sample(kind, seed, plane_no, z, c, t, pt, (int64_t)x, (int64_t)y);
-        uint8_t* p = out + (int64_t)y * pitch + (int64_t)x * bpp;
+        const uint64_t r = idx / (uint64_t)sx, x = idx - r * (uint64_t)sx;
+        const uint64_t v = gen_sample(kind, seed, plane_no, z, c, t, pt, (int64_t)x, (int64_t)y0 + (int64_t)r);
+        uint8_t* p = out + (int64_t)r * pitch + (int64_t)x * bpp;
         switch (bpp) {
         case 1: *p = (uint8_t)v; break;
         case 2: *(uint16_t*)p = (uint16_t)v; break;
@@ -376,15 +377,15 @@ hipError_t launch_tiff_tiled(hipStream_t st, const TiledHdr* d_th, uint32_t nth,
     return hipGetLastError();
 }
 
-hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t sy,
-                            int32_t pt, int32_t kind, uint64_t seed, int32_t plane_no, int32_t z,
-                            int32_t c, int32_t t) {
+hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t y0,
+                            int32_t rows, int32_t pt, int32_t kind, uint64_t seed, int32_t plane_no,
+                            int32_t z, int32_t c, int32_t t) {
     static const int bpps[PT_N] = {1, 1, 2, 2, 4, 4, 4, 8};
-    const uint64_t total = (uint64_t)sx * (uint64_t)sy;
+    const uint64_t total = (uint64_t)sx * (uint64_t)rows;
     uint64_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gen_plane, dim3((uint32_t)blocks), dim3(256), 0, st, out, pitch, sx, sy, pt,
+    hipLaunchKernelGGL(k_gen_plane, dim3((uint32_t)blocks), dim3(256), 0, st, out, pitch, sx, y0, rows, pt,
                        bpps[pt], kind, seed, plane_no, z, c, t);
     return hipGetLastError();
 }

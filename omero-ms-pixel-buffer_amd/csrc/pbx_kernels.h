@@ -9,9 +9,10 @@
 namespace pbx {
 
 // Synthetic plane (G_FAKE / G_NOISE) written little-endian into a pitched HBM plane.
-hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t sy,
-                            int32_t pixel_type, int32_t kind, uint64_t seed, int32_t plane_no,
-                            int32_t z, int32_t c, int32_t t);
+// rows [y0, y0 + rows) of a synthetic plane, row y0 at `out`
+hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t sx, int32_t y0,
+                            int32_t rows, int32_t pixel_type, int32_t kind, uint64_t seed,
+                            int32_t plane_no, int32_t z, int32_t c, int32_t t);
 
 // K1: raw / uncompressed-TIFF tiles (getTileDirect + big-endian; TIFF header in front).
 // Resolution pyramid level: dst (dx x dy) = 2x2 box mean of src (sx x sy), edge samples

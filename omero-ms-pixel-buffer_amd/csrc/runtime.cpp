@@ -57,22 +57,48 @@ const int kBpp[PBX_NPIXEL_TYPES] = {1, 1, 2, 2, 4, 4, 4, 8};
 int bpp_of(int32_t pt) { return (pt >= 0 && pt < PBX_NPIXEL_TYPES) ? kBpp[pt] : 0; }
 int log2i(int v) { int l = 0; while ((1 << l) < v) l++; return l; }
 
+// A registered plane (the bytes getPixelBuffer + getTileDirect read, TileRequestHandler.java:
+// 86,107-109) or the row band of one that this context owns.  Records live in
+// pbx_ctx::planes and are heap-allocated so that batches can pin them.
+enum PlaneState : int {
+    PS_FILLING = 0,  // created (pbx_plane_create), rows arriving, not served yet
+    PS_READY = 1,    // served
+    PS_EVICTED = 2   // key still registered, HBM returned (NOT_RESIDENT until re-registered)
+};
+
 struct Plane {
     uint64_t id = 0;
     int64_t image_id = 0;
     int32_t z = 0, c = 0, t = 0, res = 0, pixel_type = 0, size_x = 0, size_y = 0;
     bool little_endian = false;
-    uint8_t* dev = nullptr;
+    uint8_t* dev = nullptr;      // allocation: rows [band_y0, band_y0 + band_rows) + 256 B slack
     int64_t pitch = 0;
     size_t bytes = 0;
+    int32_t band_y0 = 0, band_rows = 0;  // resident rows (band_rows == size_y: the whole plane)
+    // registry state, under reg_mu
+    int state = PS_FILLING;
+    bool indexed = false;        // reachable from ctx->index (false once released)
+    int64_t pins = 0;            // planned batches / running kernels that read the plane
+    uint64_t last_use = 0;       // LRU tick of the last request served from it
+    std::vector<uint8_t> rows_done;  // PS_FILLING host planes: which band rows were written
+    uint64_t rows_left = 0;
+    // the kernels address rows by their index in the whole plane
+    uint8_t* base() const { return dev - (int64_t)band_y0 * pitch; }
+    bool whole() const { return band_y0 == 0 && band_rows == size_y; }
 };
 
 struct Image {
     int32_t pixel_type = 0, size_x = 0, size_y = 0;
-    int32_t planes = 0;
-    std::map<int32_t, int32_t> level_planes;  // stored pyramid level -> registered planes
-    // PixelBuffer.getResolutionLevels(): the number of stored levels (0 .. max)
-    int32_t levels() const { return level_planes.empty() ? 0 : level_planes.rbegin()->first + 1; }
+    int32_t planes = 0;                       // registry keys (any state)
+    std::map<int32_t, int32_t> level_planes;  // stored pyramid level -> registry keys
+    // pbx_image_declare: the Pixels row and PixelBuffer.getResolutionLevels()
+    bool declared = false;
+    int32_t size_z = 0, size_c = 0, size_t_ = 0, nlevels = 0;
+    // PixelBuffer.getResolutionLevels(): declared, else the number of stored levels (0 .. max)
+    int32_t levels() const {
+        if (declared) return nlevels;
+        return level_planes.empty() ? 0 : level_planes.rbegin()->first + 1;
+    }
 };
 
 // Grow-only caching allocator for device and pinned host blocks (power-of-two classes).
@@ -165,15 +191,21 @@ struct pbx_ctx {
     hipEvent_t stage_ev[4][4] = {};     // [stream][stage]
     std::atomic<int> last_ks{-1};       // stream of the last overlapped deflate batch
     hipStream_t copy_stream = nullptr;  // D2H of finished batches, overlapping later kernels
+    hipStream_t upload_stream = nullptr;  // H2D of plane rows (pbx_plane_write_rows / register)
     std::mutex reg_mu;   // plane registry
     std::mutex run_mu;   // plan + launch of one batch at a time on the stream
     std::mutex copy_mu;  // one fetch at a time on the copy stream
+    std::mutex upload_mu;  // one staged upload at a time on upload_stream
     Coalescer* coal = nullptr;
     std::atomic<uint64_t> n_batches{0}, n_requests{0};
-    std::unordered_map<uint64_t, Plane> planes;
+    // registry (reg_mu): id -> record (every key's record, evicted ones included, plus
+    // released records until their last pin goes), key -> id, image records
+    std::unordered_map<uint64_t, Plane*> planes;
     std::map<std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>, uint64_t> index;
     std::unordered_map<int64_t, Image> images;
     uint64_t next_id = 1;
+    // residency (reg_mu)
+    uint64_t budget = 0, resident_bytes = 0, use_tick = 0, evictions = 0, evicted_bytes = 0;
     Pool dpool, hpool;
 };
 
@@ -221,7 +253,11 @@ struct pbx_batch {
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
     bool launched = false;
+    bool attempted = false;  // batch_launch began enqueuing work (it may have failed midway)
     std::vector<uint64_t> h_offs;
+    // planes this batch reads (pinned by pbx_batch_plan, unpinned by pbx_batch_destroy), with
+    // the number of pins taken on each
+    std::vector<std::pair<Plane*, int64_t>> pins;
 };
 
 namespace {
@@ -234,21 +270,67 @@ int ensure_device(pbx_ctx* ctx) {
 using PlaneKey = std::tuple<int64_t, int32_t, int32_t, int32_t, int32_t>;
 PlaneKey key_of(const Plane& p) { return std::make_tuple(p.image_id, p.z, p.c, p.t, p.res); }
 
-// Checks, under reg_mu, that a plane may join the registry: its key is free and it agrees
-// with the image record (the Pixels row: pixel type; full-resolution size).
+// Checks, under reg_mu, that a plane may join the registry: its key is free (or holds an
+// evicted plane, which the new one replaces) and it agrees with the image record (the
+// Pixels row: pixel type; full-resolution size; declared z/c/t extents and levels).
 int registry_check(pbx_ctx* ctx, const Plane& p) {
-    if (ctx->index.count(key_of(p))) return fail(PBX_E_BADARG, "plane already registered");
+    auto it = ctx->index.find(key_of(p));
+    if (it != ctx->index.end() && ctx->planes.at(it->second)->state != PS_EVICTED)
+        return fail(PBX_E_EXISTS, "plane already registered");
     auto im = ctx->images.find(p.image_id);
     if (im == ctx->images.end()) return PBX_OK;
-    if (im->second.pixel_type != p.pixel_type) return fail(PBX_E_BADARG, "pixel type differs from the image's");
-    if (p.res == 0 && im->second.level_planes.count(0) &&
-        (im->second.size_x != p.size_x || im->second.size_y != p.size_y))
+    const Image& I = im->second;
+    if ((I.planes || I.declared) && I.pixel_type != p.pixel_type)
+        return fail(PBX_E_BADARG, "pixel type differs from the image's");
+    if (p.res == 0 && (I.level_planes.count(0) || I.declared) &&
+        (I.size_x != p.size_x || I.size_y != p.size_y))
         return fail(PBX_E_BADARG, "plane size differs from the image's");
+    if (I.declared && (p.z < 0 || p.z >= I.size_z || p.c < 0 || p.c >= I.size_c || p.t < 0 ||
+                       p.t >= I.size_t_ || p.res >= I.nlevels))
+        return fail(PBX_E_BADARG, "plane (z=%d c=%d t=%d level=%d) outside the declared image", p.z, p.c, p.t,
+                    p.res);
     return PBX_OK;
 }
 
-// Inserts planes into the registry, all or none, re-checking every key under reg_mu at
-// insertion time (a concurrent registration of the same key loses with 400 instead of
+// Drops an evicted record the key of `p` still points at (under reg_mu; it holds no HBM and
+// no pins: only READY planes are pinned).  Returns true if the key was such an entry.
+bool drop_evicted(pbx_ctx* ctx, const Plane& p) {
+    auto it = ctx->index.find(key_of(p));
+    if (it == ctx->index.end()) return false;
+    auto pit = ctx->planes.find(it->second);
+    Plane* old = pit->second;
+    if (old->state != PS_EVICTED) return false;
+    ctx->planes.erase(pit);
+    ctx->index.erase(it);
+    delete old;
+    return true;
+}
+
+// Adds one record under reg_mu (its checks done): a new id, the index entry and the image
+// record.  A key that held an evicted plane was already counted by its image.
+Plane* registry_add(pbx_ctx* ctx, const Plane& p) {
+    const bool replaced = drop_evicted(ctx, p);
+    Plane* q = new Plane(p);
+    q->id = ctx->next_id++;
+    q->indexed = true;
+    q->last_use = ++ctx->use_tick;
+    ctx->planes[q->id] = q;
+    ctx->index[key_of(*q)] = q->id;
+    Image& im = ctx->images[q->image_id];
+    if (!im.declared && (q->res == 0 || im.planes == 0)) {  // the Pixels row: full-resolution sizes
+        im.pixel_type = q->pixel_type;
+        im.size_x = q->size_x;
+        im.size_y = q->size_y;
+    }
+    if (!replaced) {
+        im.planes++;
+        im.level_planes[q->res]++;
+    }
+    return q;
+}
+
+// Inserts finished planes into the registry, all or none, re-checking every key under reg_mu
+// at insertion time (a concurrent registration of the same key loses with 409 instead of
 // both succeeding).  On failure the caller still owns (and frees) the planes' memory.
 int registry_insert(pbx_ctx* ctx, std::vector<Plane>& ps, uint64_t* ids) {
     std::lock_guard<std::mutex> g(ctx->reg_mu);
@@ -258,31 +340,137 @@ int registry_insert(pbx_ctx* ctx, std::vector<Plane>& ps, uint64_t* ids) {
             if (key_of(ps[j]) == key_of(ps[k])) return fail(PBX_E_BADARG, "the same plane twice in one call");
     }
     for (size_t k = 0; k < ps.size(); k++) {
-        Plane& p = ps[k];
-        p.id = ctx->next_id++;
-        ctx->planes[p.id] = p;
-        ctx->index[key_of(p)] = p.id;
-        Image& im = ctx->images[p.image_id];
-        if (p.res == 0 || im.planes == 0) {  // the Pixels row: full-resolution sizes
-            im.pixel_type = p.pixel_type;
-            im.size_x = p.size_x;
-            im.size_y = p.size_y;
-        }
-        im.planes++;
-        im.level_planes[p.res]++;
-        if (ids) ids[k] = p.id;
+        ps[k].state = PS_READY;
+        Plane* q = registry_add(ctx, ps[k]);
+        ps[k].id = q->id;
+        if (ids) ids[k] = q->id;
     }
     return PBX_OK;
 }
 
+// Removes a record's key from the registry (release), under reg_mu.  The record itself goes
+// when nothing pins it: its HBM (if any) is appended to `to_free` and the record deleted.
+void registry_remove(pbx_ctx* ctx, Plane* p, std::vector<std::pair<void*, size_t>>& to_free) {
+    ctx->planes.erase(p->id);
+    ctx->index.erase(key_of(*p));
+    p->indexed = false;
+    auto im = ctx->images.find(p->image_id);
+    if (im != ctx->images.end()) {
+        if (--im->second.level_planes[p->res] == 0) im->second.level_planes.erase(p->res);
+        if (--im->second.planes == 0 && !im->second.declared) ctx->images.erase(im);
+    }
+    if (p->pins == 0) {
+        if (p->dev) to_free.emplace_back(p->dev, p->bytes);
+        delete p;
+    }
+}
+
+// Drops `n` pins of a record (under reg_mu); a released record whose last pin goes is freed.
+void unpin_locked(pbx_ctx* ctx, Plane* p, int64_t n, std::vector<std::pair<void*, size_t>>& to_free) {
+    (void)ctx;
+    p->pins -= n;
+    if (p->pins == 0 && !p->indexed) {
+        if (p->dev) to_free.emplace_back(p->dev, p->bytes);
+        delete p;
+    }
+}
+
+// Returns plane HBM (outside reg_mu: hipFree may wait for the device).  Nothing reads it:
+// its record had no pins, and it was unreachable from the index or evicted.
+void free_planes(pbx_ctx* ctx, const std::vector<std::pair<void*, size_t>>& to_free) {
+    if (to_free.empty()) return;
+    (void)hipSetDevice(ctx->device);
+    uint64_t bytes = 0;
+    for (auto& f : to_free) {
+        (void)hipFree(f.first);
+        bytes += f.second;
+    }
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    ctx->resident_bytes -= bytes;
+}
+
+// Evicts the least recently used idle plane (READY, registered, no pins), under reg_mu.
+// Its key stays registered (PS_EVICTED: requests answer NOT_RESIDENT).  Its HBM goes to
+// `to_free` for a plain hipFree (no longer counted as resident).  False if none.
+bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_free) {
+    Plane* v = nullptr;
+    for (auto& kv : ctx->planes) {
+        Plane* p = kv.second;
+        if (p->state == PS_READY && p->indexed && p->pins == 0 && p->dev && (!v || p->last_use < v->last_use))
+            v = p;
+    }
+    if (!v) return false;
+    to_free.emplace_back(v->dev, v->bytes);
+    ctx->resident_bytes -= v->bytes;
+    ctx->evictions++;
+    ctx->evicted_bytes += v->bytes;
+    v->dev = nullptr;
+    v->state = PS_EVICTED;
+    return true;
+}
+
+// HBM for a plane, within the residency budget: evicts idle planes (LRU) to make room, and
+// again whenever hipMalloc runs out of device memory.  The bytes count as resident from here
+// on; plane_free returns them.
+int plane_alloc(pbx_ctx* ctx, size_t bytes, uint8_t** out) {
+    *out = nullptr;
+    std::vector<std::pair<void*, size_t>> victims;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        if (ctx->budget) {
+            uint64_t idle = 0;
+            for (auto& kv : ctx->planes) {
+                const Plane* p = kv.second;
+                if (p->state == PS_READY && p->indexed && p->pins == 0 && p->dev) idle += p->bytes;
+            }
+            if (ctx->resident_bytes + bytes > ctx->budget + idle)
+                return fail(PBX_E_NO_SPACE, "plane of %zu bytes does not fit the residency budget (%llu of %llu "
+                            "bytes held, %llu idle)", bytes, (unsigned long long)ctx->resident_bytes,
+                            (unsigned long long)ctx->budget, (unsigned long long)idle);
+            while (ctx->resident_bytes + bytes > ctx->budget)
+                if (!evict_one_locked(ctx, victims)) break;
+        }
+        ctx->resident_bytes += bytes;
+    }
+    for (auto& v : victims) (void)hipFree(v.first);
+    for (;;) {
+        const hipError_t e = hipMalloc((void**)out, bytes);
+        if (e == hipSuccess) return PBX_OK;
+        (void)hipGetLastError();
+        std::vector<std::pair<void*, size_t>> one;
+        {
+            std::lock_guard<std::mutex> g(ctx->reg_mu);
+            if (e != hipErrorOutOfMemory || !evict_one_locked(ctx, one)) {
+                ctx->resident_bytes -= bytes;
+                *out = nullptr;
+                return fail(e == hipErrorOutOfMemory ? PBX_E_NO_SPACE : PBX_E_INTERNAL,
+                            "plane of %zu bytes: hipMalloc: %s (no idle plane left to evict)", bytes,
+                            hipGetErrorString(e));
+            }
+        }
+        (void)hipFree(one[0].first);
+    }
+}
+
+void plane_free(pbx_ctx* ctx, void* dev, size_t bytes) {
+    if (!dev) return;
+    free_planes(ctx, {{dev, bytes}});
+}
+
 // Mirrors TileRequestHandler.getTile (TileRequestHandler.java:80-139) up to the dispatch:
-// returns PBX_OK and the plane, or the status the reference ends with.
-int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane& plane) {
+// returns PBX_OK and the plane (pinned: the caller unpins it), the status the reference ends
+// with, or PBX_E_NOT_RESIDENT where the reference would open a plane this context does not
+// hold (getPixels + getPixelBuffer, :84-86).
+int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*& plane) {
     w = r.w;
     h = r.h;
+    plane = nullptr;
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     auto im = ctx->images.find(r.image_id);
-    if (im == ctx->images.end()) return fail(PBX_E_NOTFOUND, "Cannot find Image:%lld", (long long)r.image_id);
+    // :84 getPixels — the image's Pixels row is not known here; the binding looks it up
+    // (null -> 404 there) and loads the plane
+    if (im == ctx->images.end())
+        return fail(PBX_E_NOT_RESIDENT, "Image:%lld not resident", (long long)r.image_id);
     // :89-91 — pixelBuffer.setResolutionLevel(resolution) when given.  OMERO numbers levels
     // the other way round from storage: resolution getResolutionLevels()-1 is the full
     // resolution and 0 the smallest (omero-zarr-pixel-buffer's ZarrPixelBuffer maps it to
@@ -304,24 +492,56 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane&
     const int64_t tile_size = (int64_t)w * (int64_t)h * bpp;
     if (w < 0 || h < 0 || tile_size > 2147483647LL || tile_size <= 0)
         return fail(PBX_E_NOTFOUND, "invalid tile size %dx%d", w, h);
-    auto it = ctx->index.find(std::make_tuple(r.image_id, r.z, r.c, r.t, level));
-    if (it == ctx->index.end())
-        return fail(PBX_E_NOTFOUND, "no plane z=%d c=%d t=%d level=%d", r.z, r.c, r.t, level);
-    plane = ctx->planes[it->second];
-    // getTileDirect outside the plane throws (upstream PixelBuffer) -> 404
-    if (r.x < 0 || r.y < 0 || (int64_t)r.x + w > plane.size_x || (int64_t)r.y + h > plane.size_y)
-        return fail(PBX_E_NOTFOUND, "region outside plane");
+    // The format is decided after getTileDirect upstream, but both of its failures end in
+    // null -> 404 whatever the plane holds, so they are checked before loading anything.
     switch (r.format) {
     case PBX_FMT_RAW:
     case PBX_FMT_TIF:
-        return PBX_OK;
+        break;
     case PBX_FMT_PNG:
         // APNGWriter accepts int8/uint8/int16/uint16 only ("Unsupported image type")
         if (bpp > 2) return fail(PBX_E_NOTFOUND, "png: unsupported pixel type");
-        return PBX_OK;
+        break;
     default:
         return fail(PBX_E_NOTFOUND, "Unknown output format");  // :125-126
     }
+    const Image& I = im->second;
+    auto it = ctx->index.find(std::make_tuple(r.image_id, r.z, r.c, r.t, level));
+    if (it == ctx->index.end()) {
+        // getTileDirect of a z/c/t outside the declared image throws -> 404; otherwise the
+        // plane exists upstream and is not loaded here
+        if (I.declared && (r.z < 0 || r.z >= I.size_z || r.c < 0 || r.c >= I.size_c || r.t < 0 ||
+                           r.t >= I.size_t_))
+            return fail(PBX_E_NOTFOUND, "no plane z=%d c=%d t=%d", r.z, r.c, r.t);
+        return fail(PBX_E_NOT_RESIDENT, "plane z=%d c=%d t=%d level=%d not resident", r.z, r.c, r.t, level);
+    }
+    Plane* p = ctx->planes.at(it->second);
+    if (p->state != PS_READY)
+        return fail(PBX_E_NOT_RESIDENT, "plane z=%d c=%d t=%d level=%d %s", r.z, r.c, r.t, level,
+                    p->state == PS_EVICTED ? "evicted" : "still loading");
+    // getTileDirect outside the plane throws (upstream PixelBuffer) -> 404
+    if (r.x < 0 || r.y < 0 || (int64_t)r.x + w > p->size_x || (int64_t)r.y + h > p->size_y)
+        return fail(PBX_E_NOTFOUND, "region outside plane");
+    // a row band: rows outside it belong to another context
+    if (r.y < p->band_y0 || (int64_t)r.y + h > (int64_t)p->band_y0 + p->band_rows)
+        return fail(PBX_E_NOT_RESIDENT, "rows %d..%lld outside the resident band %d..%d", r.y,
+                    (long long)r.y + h, p->band_y0, p->band_y0 + p->band_rows);
+    p->pins++;
+    p->last_use = ++ctx->use_tick;
+    plane = p;
+    return PBX_OK;
+}
+
+// Drops every pin a batch holds (its kernels have finished or never ran).
+void batch_unpin(pbx_ctx* ctx, pbx_batch* b) {
+    if (b->pins.empty()) return;
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        for (auto& pc : b->pins) unpin_locked(ctx, pc.first, pc.second, to_free);
+    }
+    b->pins.clear();
+    free_planes(ctx, to_free);
 }
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
@@ -613,6 +833,8 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking);
+    if (const char* hb = getenv("PBX_HBM_BUDGET_MB")) ctx->budget = (uint64_t)strtoull(hb, nullptr, 10) << 20;
     if (const char* ks = getenv("PBX_KSTREAMS")) ctx->nks = std::min(4, std::max(1, atoi(ks)));
     else ctx->nks = 3;
     ctx->kstream[0] = ctx->stream;
@@ -638,7 +860,12 @@ void pbx_shutdown(pbx_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)sync_kernel_streams(ctx);
     (void)hipStreamSynchronize(ctx->copy_stream);
-    for (auto& kv : ctx->planes) (void)hipFree(kv.second.dev);
+    (void)hipStreamSynchronize(ctx->upload_stream);
+    for (auto& kv : ctx->planes) {  // records of released planes still pinned by undestroyed
+        (void)hipFree(kv.second->dev);  // batches are leaked with those batches
+        delete kv.second;
+    }
+    ctx->planes.clear();
     ctx->dpool.release_all();
     ctx->hpool.release_all();
     for (int k = 1; k < 4; k++)
@@ -647,6 +874,7 @@ void pbx_shutdown(pbx_ctx* ctx) {
         for (auto& x : r) if (x) (void)hipEventDestroy(x);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
     delete ctx;
 }
 
@@ -679,81 +907,432 @@ int pbx_device_synchronize(pbx_ctx* ctx) {
     return PBX_OK;
 }
 
-int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id) {
-    if (!ctx || !d || !plane_id) return fail(PBX_E_BADARG, "null argument");
+// ------------------------------------------------------------- staged host -> HBM upload
+}  // extern "C"
+namespace {
+
+// Copies `rows` packed host rows of `row` bytes (pageable caller memory) to HBM rows `pitch`
+// apart, through pinned staging blocks of the context's pinned pool: each piece (whole rows,
+// or a part of one row longer than a piece) is copied into a pinned block by several host
+// threads (one thread's memcpy is the bottleneck otherwise) and DMA'd asynchronously on `st`
+// while the next piece is being staged.  Returns once every piece is staged and its DMA has
+// completed; the pinned blocks go back to the pool.
+int upload_rows(pbx_ctx* ctx, uint8_t* dev, int64_t pitch, const uint8_t* host, uint64_t row, uint64_t rows,
+                hipStream_t st) {
+    constexpr uint64_t PIECE = 32ull << 20;
+    constexpr int NBUF = 3;
+    const uint64_t total = row * rows;
+    if (!total) return PBX_OK;
+    if (total < (4ull << 20)) {  // small: one pageable copy
+        if ((uint64_t)pitch == row || rows == 1)
+            HIP_TRY(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, st));
+        else
+            HIP_TRY(hipMemcpy2DAsync(dev, pitch, host, row, row, rows, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return PBX_OK;
+    }
+    // pieces: k whole rows (row <= PIECE), or [off, off + n) of one row (row > PIECE)
+    const bool whole_rows = row <= PIECE;
+    const uint64_t k_rows = whole_rows ? std::max<uint64_t>(1, PIECE / row) : 1;
+    const uint64_t per_row = whole_rows ? 1 : (row + PIECE - 1) / PIECE;
+    const uint64_t npieces = whole_rows ? (rows + k_rows - 1) / k_rows : rows * per_row;
+    void* blk[NBUF] = {};
+    hipEvent_t ev[NBUF] = {};
+    bool used[NBUF] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < NBUF && e == hipSuccess; i++) {
+        blk[i] = ctx->hpool.get(PIECE, &e);
+        if (blk[i]) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    }
+    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    for (uint64_t p = 0; p < npieces && e == hipSuccess; p++) {
+        uint64_t r0, k, off, n;
+        if (whole_rows) {
+            r0 = p * k_rows;
+            k = std::min(k_rows, rows - r0);
+            off = 0;
+            n = row;
+        } else {
+            r0 = p / per_row;
+            k = 1;
+            off = (p % per_row) * PIECE;
+            n = std::min(PIECE, row - off);
+        }
+        const int b = (int)(p % NBUF);
+        if (used[b]) e = hipEventSynchronize(ev[b]);  // the block's previous DMA is done
+        if (e != hipSuccess) break;
+        uint8_t* dst = (uint8_t*)blk[b];
+        const uint8_t* src = host + r0 * row + off;
+        const uint64_t bytes = k * n;  // contiguous on the host in both cases
+        const uint64_t per = (bytes + nth - 1) / nth;
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nth && t * per < bytes; t++)
+            th.emplace_back([=] { memcpy(dst + t * per, src + t * per, std::min(per, bytes - t * per)); });
+        memcpy(dst, src, std::min(per, bytes));
+        for (auto& x : th) x.join();
+        uint8_t* d = dev + (int64_t)r0 * pitch + off;
+        if (k == 1 || (uint64_t)pitch == n)
+            e = hipMemcpyAsync(d, dst, bytes, hipMemcpyHostToDevice, st);
+        else
+            e = hipMemcpy2DAsync(d, pitch, dst, n, n, k, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(ev[b], st);
+        used[b] = true;
+    }
+    for (int i = 0; i < NBUF; i++) {
+        if (used[i]) (void)hipEventSynchronize(ev[i]);
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+        if (blk[i]) ctx->hpool.put(blk[i]);
+    }
+    if (e != hipSuccess) return fail(PBX_E_INTERNAL, "staged upload: %s", hipGetErrorString(e));
+    return PBX_OK;
+}
+
+// Contiguous bytes (Zarr chunk data) to HBM, as one "row".
+int upload_staged(pbx_ctx* ctx, uint8_t* dev, const uint8_t* host, uint64_t bytes, hipStream_t st) {
+    return upload_rows(ctx, dev, (int64_t)bytes, host, bytes, 1, st);
+}
+
+// Pins the record of `id` if it is in one of `states` (bit mask of 1 << PlaneState); the
+// caller unpins it with unpin_id.  Returns the record or sets the status.
+Plane* pin_id(pbx_ctx* ctx, uint64_t id, unsigned states, int* rc) {
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->planes.find(id);
+    if (it == ctx->planes.end()) {
+        *rc = fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+        return nullptr;
+    }
+    Plane* p = it->second;
+    if (!((1u << p->state) & states)) {
+        static const char* names[3] = {"still loading", "ready", "evicted"};
+        *rc = fail(p->state == PS_READY ? PBX_E_EXISTS : p->state == PS_EVICTED ? PBX_E_NOT_RESIDENT : PBX_E_BADARG,
+                   "plane %llu is %s", (unsigned long long)id, names[p->state]);
+        return nullptr;
+    }
+    p->pins++;
+    *rc = PBX_OK;
+    return p;
+}
+
+void unpin_one(pbx_ctx* ctx, Plane* p) {
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        unpin_locked(ctx, p, 1, to_free);
+    }
+    free_planes(ctx, to_free);
+}
+
+// pbx_plane_create: reserve the key (409 if taken), allocate the band within the budget,
+// generate it for generator sources.  The new record is returned pinned.
+int plane_create(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t y0, int32_t nrows, Plane** out) {
+    *out = nullptr;
+    if (!d) return fail(PBX_E_BADARG, "null argument");
     const int bpp = bpp_of(d->pixel_type);
     if (!bpp) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
     if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
     if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
+    if (d->source != PBX_SRC_HOST && d->source != PBX_SRC_GEN_FAKE && d->source != PBX_SRC_GEN_NOISE)
+        return fail(PBX_E_BADARG, "bad source %d", d->source);
+    if (nrows == 0) {
+        if (y0 != 0) return fail(PBX_E_BADARG, "band_rows 0 (whole plane) needs band_y0 0");
+        nrows = d->size_y;
+    }
+    if (y0 < 0 || nrows < 0 || (int64_t)y0 + nrows > d->size_y)
+        return fail(PBX_E_BADARG, "band %d+%d outside the plane's %d rows", y0, nrows, d->size_y);
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     Plane p;
     p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
     p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
+    p.band_y0 = y0;
+    p.band_rows = nrows;
     const int64_t row = (int64_t)d->size_x * bpp;
     p.pitch = (row + 255) & ~(int64_t)255;
-    p.bytes = (size_t)p.pitch * d->size_y + 256;
+    p.bytes = (size_t)p.pitch * nrows + 256;
+    p.little_endian = d->source == PBX_SRC_HOST ? (d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1) : bpp > 1;
+    p.state = PS_FILLING;
+    Plane* q;
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         if (int rc = registry_check(ctx, p)) return rc;
+        q = registry_add(ctx, p);  // the key is ours: concurrent creators get 409
+        q->pins = 1;
     }
-    HIP_TRY(hipMalloc((void**)&p.dev, p.bytes));
-    if (d->source == PBX_SRC_HOST) {
-        if (!d->host_data || d->host_bytes < (uint64_t)row * d->size_y) {
-            (void)hipFree(p.dev);
-            return fail(PBX_E_BADARG, "host_data too small");
+    auto abandon = [&](int rc) {
+        const std::string msg = g_err;
+        std::vector<std::pair<void*, size_t>> to_free;
+        {
+            std::lock_guard<std::mutex> g(ctx->reg_mu);
+            if (q->indexed) registry_remove(ctx, q, to_free);  // still pinned: not freed yet
+            unpin_locked(ctx, q, 1, to_free);
         }
-        p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
-        HIP_TRY(hipMemcpy2DAsync(p.dev, p.pitch, d->host_data, row, row, d->size_y,
-                                 hipMemcpyHostToDevice, ctx->stream));
-    } else if (d->source == PBX_SRC_GEN_FAKE || d->source == PBX_SRC_GEN_NOISE) {
-        p.little_endian = bpp > 1;
-        HIP_TRY(launch_gen_plane(ctx->stream, p.dev, p.pitch, d->size_x, d->size_y, d->pixel_type,
-                                 d->source == PBX_SRC_GEN_FAKE ? GEN_FAKE : GEN_NOISE, d->seed,
-                                 d->plane_no, d->z, d->c, d->t));
-    } else {
-        (void)hipFree(p.dev);
-        return fail(PBX_E_BADARG, "bad source %d", d->source);
-    }
-    hipError_t e = hipMemsetAsync(p.dev + (size_t)p.pitch * d->size_y, 0, 256, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) {
-        (void)hipFree(p.dev);
-        return fail(PBX_E_INTERNAL, "plane upload: %s", hipGetErrorString(e));
-    }
-    std::vector<Plane> one{p};
-    if (int rc = registry_insert(ctx, one, plane_id)) {  // lost a race for the same key
-        (void)hipFree(p.dev);
+        free_planes(ctx, to_free);
+        g_err = msg;
         return rc;
+    };
+    uint8_t* dev = nullptr;
+    if (int rc = plane_alloc(ctx, p.bytes, &dev)) return abandon(rc);
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        q->dev = dev;
+        if (d->source == PBX_SRC_HOST) {
+            q->rows_done.assign((size_t)nrows, 0);
+            q->rows_left = (uint64_t)nrows;
+        }
     }
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> u(ctx->upload_mu);
+        e = hipMemsetAsync(dev + (size_t)p.pitch * nrows, 0, 256, ctx->upload_stream);  // over-read slack
+        if (e == hipSuccess && d->source != PBX_SRC_HOST)
+            e = launch_gen_plane(ctx->upload_stream, dev, p.pitch, d->size_x, y0, nrows, d->pixel_type,
+                                 d->source == PBX_SRC_GEN_FAKE ? GEN_FAKE : GEN_NOISE, d->seed, d->plane_no,
+                                 d->z, d->c, d->t);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->upload_stream);
+    }
+    if (e != hipSuccess) return abandon(fail(PBX_E_INTERNAL, "plane create: %s", hipGetErrorString(e)));
+    if (d->source != PBX_SRC_HOST) {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        q->state = PS_READY;
+    }
+    *out = q;
+    return PBX_OK;
+}
+
+// The rows of a FILLING record that the caller has pinned.
+int plane_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
+    const int bpp = bpp_of(q->pixel_type);
+    const uint64_t row = (uint64_t)q->size_x * bpp;
+    if (rows < 0 || y0 < q->band_y0 || (int64_t)y0 + rows > (int64_t)q->band_y0 + q->band_rows)
+        return fail(PBX_E_BADARG, "rows %d+%d outside the plane's band %d+%d", y0, rows, q->band_y0, q->band_rows);
+    if (!rows) return PBX_OK;
+    if (!data || bytes < row * (uint64_t)rows)
+        return fail(PBX_E_BADARG, "%llu bytes for %d rows of %llu", (unsigned long long)bytes, rows,
+                    (unsigned long long)row);
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    {
+        std::lock_guard<std::mutex> u(ctx->upload_mu);
+        if (int rc = upload_rows(ctx, q->dev + (int64_t)(y0 - q->band_y0) * q->pitch, q->pitch,
+                                 (const uint8_t*)data, row, (uint64_t)rows, ctx->upload_stream))
+            return rc;
+    }
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    for (int32_t r = y0 - q->band_y0; r < y0 - q->band_y0 + rows; r++)
+        if (!q->rows_done[(size_t)r]) {
+            q->rows_done[(size_t)r] = 1;
+            q->rows_left--;
+        }
+    return PBX_OK;
+}
+
+int plane_commit(pbx_ctx* ctx, Plane* q) {
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    if (q->state != PS_FILLING) return fail(PBX_E_BADARG, "plane %llu is not being loaded", (unsigned long long)q->id);
+    if (q->rows_left)
+        return fail(PBX_E_BADARG, "plane %llu: %llu rows of its band were never written", (unsigned long long)q->id,
+                    (unsigned long long)q->rows_left);
+    q->rows_done.clear();
+    q->rows_done.shrink_to_fit();
+    q->state = PS_READY;
+    q->last_use = ++ctx->use_tick;
+    return PBX_OK;
+}
+
+}  // namespace
+extern "C" {
+
+int pbx_plane_create(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t band_y0, int32_t band_rows, uint64_t* plane_id) {
+    if (!ctx || !d || !plane_id) return fail(PBX_E_BADARG, "null argument");
+    Plane* q = nullptr;
+    if (int rc = plane_create(ctx, d, band_y0, band_rows, &q)) return rc;
+    *plane_id = q->id;
+    unpin_one(ctx, q);
+    return PBX_OK;
+}
+
+int pbx_plane_write_rows(pbx_ctx* ctx, uint64_t id, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    int rc;
+    Plane* q = pin_id(ctx, id, 1u << PS_FILLING, &rc);
+    if (!q) return rc;
+    rc = plane_write(ctx, q, y0, rows, data, bytes);
+    const std::string msg = g_err;
+    unpin_one(ctx, q);
+    g_err = msg;
+    return rc;
+}
+
+int pbx_plane_commit(pbx_ctx* ctx, uint64_t id) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    int rc;
+    Plane* q = pin_id(ctx, id, 1u << PS_FILLING, &rc);
+    if (!q) return rc;
+    rc = plane_commit(ctx, q);
+    const std::string msg = g_err;
+    unpin_one(ctx, q);
+    g_err = msg;
+    return rc;
+}
+
+int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id) {
+    if (!ctx || !d || !plane_id) return fail(PBX_E_BADARG, "null argument");
+    const int bpp = bpp_of(d->pixel_type);
+    if (d->source == PBX_SRC_HOST && bpp && d->size_x > 0 && d->size_y > 0 &&
+        (!d->host_data || d->host_bytes < (uint64_t)d->size_x * bpp * (uint64_t)d->size_y))
+        return fail(PBX_E_BADARG, "host_data too small");
+    Plane* q = nullptr;
+    if (int rc = plane_create(ctx, d, 0, 0, &q)) return rc;
+    int rc = PBX_OK;
+    if (d->source == PBX_SRC_HOST) {
+        rc = plane_write(ctx, q, 0, d->size_y, d->host_data, d->host_bytes);
+        if (rc == PBX_OK) rc = plane_commit(ctx, q);
+    }
+    const std::string msg = g_err;
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        if (rc != PBX_OK && q->indexed) registry_remove(ctx, q, to_free);  // all or nothing
+        if (rc == PBX_OK) *plane_id = q->id;
+        unpin_locked(ctx, q, 1, to_free);
+    }
+    free_planes(ctx, to_free);
+    g_err = msg;
+    return rc;
+}
+
+int pbx_plane_lookup(pbx_ctx* ctx, int64_t image_id, int32_t z, int32_t c, int32_t t, int32_t level,
+                     uint64_t* plane_id, int32_t* state, int32_t* band_y0, int32_t* band_rows) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->index.find(std::make_tuple(image_id, z, c, t, level));
+    if (it == ctx->index.end()) return fail(PBX_E_NOTFOUND, "no plane registered under that key");
+    const Plane* p = ctx->planes.at(it->second);
+    if (plane_id) *plane_id = p->id;
+    if (state) *state = p->state;
+    if (band_y0) *band_y0 = p->band_y0;
+    if (band_rows) *band_rows = p->band_rows;
+    return PBX_OK;
+}
+
+int pbx_image_declare(pbx_ctx* ctx, const pbx_image_desc* d) {
+    if (!ctx || !d) return fail(PBX_E_BADARG, "null argument");
+    if (!bpp_of(d->pixel_type)) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
+    if (d->size_x <= 0 || d->size_y <= 0 || d->size_z <= 0 || d->size_c <= 0 || d->size_t_ <= 0 || d->levels <= 0 ||
+        d->levels > 64)
+        return fail(PBX_E_BADARG, "bad image extents");
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->images.find(d->image_id);
+    if (it != ctx->images.end()) {
+        const Image& I = it->second;
+        if (I.declared) {
+            if (I.pixel_type != d->pixel_type || I.size_x != d->size_x || I.size_y != d->size_y || I.size_z != d->size_z ||
+                I.size_c != d->size_c || I.size_t_ != d->size_t_ || I.nlevels != d->levels)
+                return fail(PBX_E_BADARG, "Image:%lld declared differently before", (long long)d->image_id);
+            return PBX_OK;
+        }
+        if (I.planes && I.pixel_type != d->pixel_type)
+            return fail(PBX_E_BADARG, "pixel type differs from the registered planes'");
+        if (I.level_planes.count(0) && (I.size_x != d->size_x || I.size_y != d->size_y))
+            return fail(PBX_E_BADARG, "size differs from the registered full-resolution planes'");
+        if (I.levels() > d->levels) return fail(PBX_E_BADARG, "a plane is registered at level %d", I.levels() - 1);
+        for (auto& kv : ctx->index) {
+            if (std::get<0>(kv.first) != d->image_id) continue;
+            const int32_t z = std::get<1>(kv.first), c = std::get<2>(kv.first), t = std::get<3>(kv.first);
+            if (z < 0 || z >= d->size_z || c < 0 || c >= d->size_c || t < 0 || t >= d->size_t_)
+                return fail(PBX_E_BADARG, "a plane is registered at z=%d c=%d t=%d", z, c, t);
+        }
+    }
+    Image& I = ctx->images[d->image_id];
+    I.declared = true;
+    I.pixel_type = d->pixel_type;
+    I.size_x = d->size_x;
+    I.size_y = d->size_y;
+    I.size_z = d->size_z;
+    I.size_c = d->size_c;
+    I.size_t_ = d->size_t_;
+    I.nlevels = d->levels;
+    return PBX_OK;
+}
+
+int pbx_image_release(pbx_ctx* ctx, int64_t image_id) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto im = ctx->images.find(image_id);
+        if (im == ctx->images.end()) return fail(PBX_E_NOTFOUND, "Image:%lld unknown", (long long)image_id);
+        std::vector<Plane*> ps;
+        for (auto& kv : ctx->index)
+            if (std::get<0>(kv.first) == image_id) ps.push_back(ctx->planes.at(kv.second));
+        for (Plane* p : ps) registry_remove(ctx, p, to_free);
+        ctx->images.erase(image_id);
+    }
+    free_planes(ctx, to_free);
+    return PBX_OK;
+}
+
+int pbx_set_residency_budget(pbx_ctx* ctx, uint64_t bytes) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::vector<std::pair<void*, size_t>> victims;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        ctx->budget = bytes;
+        while (bytes && ctx->resident_bytes > bytes)  // shrink now, as far as idle planes allow
+            if (!evict_one_locked(ctx, victims)) break;
+    }
+    if (!victims.empty()) {
+        (void)hipSetDevice(ctx->device);
+        for (auto& v : victims) (void)hipFree(v.first);
+    }
+    return PBX_OK;
+}
+
+int pbx_residency_stats_get(pbx_ctx* ctx, pbx_residency_stats* s) {
+    if (!ctx || !s) return fail(PBX_E_BADARG, "null argument");
+    memset(s, 0, sizeof *s);
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    s->budget = ctx->budget;
+    s->resident_bytes = ctx->resident_bytes;
+    for (auto& kv : ctx->planes) {
+        if (!kv.second->indexed) continue;
+        if (kv.second->state == PS_EVICTED) s->evicted_planes++;
+        else if (kv.second->dev) s->planes++;
+    }
+    s->evictions = ctx->evictions;
+    s->evicted_bytes = ctx->evicted_bytes;
     return PBX_OK;
 }
 
 int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t* ids, double* kernel_ms) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     if (levels < 1 || levels > 30) return fail(PBX_E_BADARG, "bad level count %d", levels);
-    // run_mu from the source lookup through the last kernel: pbx_plane_release takes it
-    // before freeing a plane, so the source cannot be freed under the downsampling kernels.
-    std::lock_guard<std::mutex> run(ctx->run_mu);
-    Plane src;
-    {
-        std::lock_guard<std::mutex> g(ctx->reg_mu);
-        auto it = ctx->planes.find(id);
-        if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
-        src = it->second;
-        for (int32_t k = 1; k <= levels; k++)
-            if (ctx->index.count(std::make_tuple(src.image_id, src.z, src.c, src.t, src.res + k)))
-                return fail(PBX_E_BADARG, "resolution %d already registered", src.res + k);
-    }
-    if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    const int bpp = bpp_of(src.pixel_type);
+    // the source stays pinned from the lookup through the last kernel: a concurrent
+    // pbx_plane_release cannot free it under the downsampling kernels
+    int rc;
+    Plane* sp = pin_id(ctx, id, 1u << PS_READY, &rc);
+    if (!sp) return rc;
+    const Plane src = *sp;
     std::vector<Plane> made;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     auto undo = [&](int code) {
-        for (Plane& q : made) (void)hipFree(q.dev);
+        const std::string msg = g_err;
+        for (Plane& q : made) plane_free(ctx, q.dev, q.bytes);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        unpin_one(ctx, sp);
+        g_err = msg;
         return code;
     };
+    if (!src.whole()) return undo(fail(PBX_E_BADARG, "plane %llu is a row band: no pyramid", (unsigned long long)id));
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        for (int32_t k = 1; k <= levels; k++) {
+            auto it = ctx->index.find(std::make_tuple(src.image_id, src.z, src.c, src.t, src.res + k));
+            if (it != ctx->index.end() && ctx->planes.at(it->second)->state != PS_EVICTED)
+                return undo(fail(PBX_E_EXISTS, "resolution %d already registered", src.res + k));
+        }
+    }
+    if (ensure_device(ctx)) return undo(PBX_E_INTERNAL);
+    const int bpp = bpp_of(src.pixel_type);
     hipError_t e = hipSuccess;
     if (kernel_ms) {
         e = hipEventCreate(&ev0);
@@ -762,14 +1341,16 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
     }
     Plane prev = src;
     for (int32_t k = 1; k <= levels; k++) {
-        Plane p = prev;
+        Plane p;
+        p.image_id = src.image_id; p.z = src.z; p.c = src.c; p.t = src.t;
+        p.pixel_type = src.pixel_type;
+        p.little_endian = src.little_endian;
         p.size_x = (prev.size_x + 1) / 2;
         p.size_y = (prev.size_y + 1) / 2;
+        p.band_rows = p.size_y;
         p.pitch = ((int64_t)p.size_x * bpp + 255) & ~(int64_t)255;
         p.bytes = (size_t)p.pitch * p.size_y + 256;
-        p.dev = nullptr;
-        e = hipMalloc((void**)&p.dev, p.bytes);
-        if (e != hipSuccess) return undo(fail(PBX_E_INTERNAL, "hipMalloc: %s", hipGetErrorString(e)));
+        if (int rc2 = plane_alloc(ctx, p.bytes, &p.dev)) return undo(rc2);
         p.res = src.res + k;
         made.push_back(p);
         prev = p;
@@ -791,61 +1372,10 @@ int pbx_plane_build_pyramid(pbx_ctx* ctx, uint64_t id, int32_t levels, uint64_t*
         (void)hipEventElapsedTime(&ms, ev0, ev1);
         *kernel_ms = ms;
     }
-    if (int rc = registry_insert(ctx, made, ids)) return undo(rc);  // keys re-checked here
+    if (int rc2 = registry_insert(ctx, made, ids)) return undo(rc2);  // keys re-checked here
     made.clear();
-    return undo(PBX_OK);  // events only
+    return undo(PBX_OK);  // events and the source pin only
 }
-
-// ------------------------------------------------------------- staged host -> HBM upload
-namespace {
-
-// Copies host bytes (pageable caller memory) to HBM through pinned staging blocks of the
-// context's pinned pool: each piece is copied into a pinned block by several host threads
-// (one thread's memcpy is the bottleneck otherwise) and DMA'd asynchronously on `st` while
-// the next piece is being staged.  Returns once every piece is staged and its DMA queued; the
-// pinned blocks go back to the pool after their copies completed.
-int upload_staged(pbx_ctx* ctx, uint8_t* dev, const uint8_t* host, uint64_t bytes, hipStream_t st) {
-    constexpr uint64_t PIECE = 32ull << 20;
-    constexpr int NBUF = 3;
-    if (bytes < (4ull << 20)) {  // small: one pageable copy
-        HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, st));
-        return PBX_OK;
-    }
-    void* blk[NBUF] = {};
-    hipEvent_t ev[NBUF] = {};
-    bool used[NBUF] = {};
-    hipError_t e = hipSuccess;
-    for (int i = 0; i < NBUF && e == hipSuccess; i++) {
-        blk[i] = ctx->hpool.get(PIECE, &e);
-        if (blk[i]) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-    }
-    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    for (uint64_t off = 0, p = 0; off < bytes && e == hipSuccess; off += PIECE, p++) {
-        const int b = (int)(p % NBUF);
-        const uint64_t n = std::min(PIECE, bytes - off);
-        if (used[b]) e = hipEventSynchronize(ev[b]);  // the block's previous DMA is done
-        if (e != hipSuccess) break;
-        uint8_t* dst = (uint8_t*)blk[b];
-        const uint64_t per = (n + nth - 1) / nth;
-        std::vector<std::thread> th;
-        for (unsigned t = 1; t < nth && t * per < n; t++)
-            th.emplace_back([=] { memcpy(dst + t * per, host + off + t * per, std::min(per, n - t * per)); });
-        memcpy(dst, host + off, std::min(per, n));
-        for (auto& x : th) x.join();
-        e = hipMemcpyAsync(dev + off, dst, n, hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipEventRecord(ev[b], st);
-        used[b] = true;
-    }
-    for (int i = 0; i < NBUF; i++) {
-        if (used[i]) (void)hipEventSynchronize(ev[i]);
-        if (ev[i]) (void)hipEventDestroy(ev[i]);
-        if (blk[i]) ctx->hpool.put(blk[i]);
-    }
-    if (e != hipSuccess) return fail(PBX_E_INTERNAL, "staged upload: %s", hipGetErrorString(e));
-    return PBX_OK;
-}
-
-}  // namespace
 
 // ------------------------------------------------------------------ NGFF / Zarr planes
 namespace {
@@ -990,15 +1520,12 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
                     return fail(PBX_E_BADARG, "planes of image %lld disagree on type or size",
                                 (long long)ds[a].image_id);
         std::lock_guard<std::mutex> g(ctx->reg_mu);
-        for (uint64_t k = 0; k < n; k++) {
-            const pbx_plane_desc* d = &ds[k];
-            if (ctx->index.count(keys[k])) return fail(PBX_E_BADARG, "plane already registered");
-            auto im = ctx->images.find(d->image_id);
-            if (im != ctx->images.end() && im->second.pixel_type != d->pixel_type)
-                return fail(PBX_E_BADARG, "pixel type differs from the image's");
-            if (d->resolution == 0 && im != ctx->images.end() &&
-                (im->second.size_x != d->size_x || im->second.size_y != d->size_y))
-                return fail(PBX_E_BADARG, "plane size differs from the image's");
+        for (uint64_t k = 0; k < n; k++) {  // early: a taken key fails before any decoding
+            Plane p;
+            p.image_id = ds[k].image_id; p.z = ds[k].z; p.c = ds[k].c; p.t = ds[k].t;
+            p.res = ds[k].resolution; p.pixel_type = ds[k].pixel_type;
+            p.size_x = ds[k].size_x; p.size_y = ds[k].size_y;
+            if (int rc = registry_check(ctx, p)) return rc;
         }
     }
     // host plan: metadata of every chunk of every plane, one upload buffer, one scratch
@@ -1026,6 +1553,7 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
         p.little_endian = d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1;
         p.pitch = ((int64_t)d->size_x * bpp + 255) & ~(int64_t)255;
         p.bytes = (size_t)p.pitch * d->size_y + 256;
+        p.band_rows = d->size_y;
         uint64_t fill = 0;  // fill bytes in the stored byte order
         for (int j = 0; j < bpp; j++) {
             const uint64_t byte = (zs[k].fill_bits >> (8 * j)) & 0xff;
@@ -1050,19 +1578,27 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     // launch scratch (input, decoded chunks, tables) comes from the context's device pool and
     // goes back to it: only the planes themselves are new allocations
     auto cleanup = [&](bool planes_too) {
+        // queued copies, memsets or decoders may still write these blocks on an error path;
+        // the pool hands them to other streams' batches as soon as they are back
+        (void)hipStreamSynchronize(ctx->stream);
         for (void* q : {(void*)d_in, (void*)d_scr, (void*)d_lit, (void*)d_st, (void*)d_ch, (void*)d_pl, (void*)d_err})
             if (q) ctx->dpool.put(q);
         for (auto& x : ev) if (x) (void)hipEventDestroy(x);
         if (planes_too)
-            for (Plane& p : ps) if (p.dev) (void)hipFree(p.dev);
+            for (Plane& p : ps) plane_free(ctx, p.dev, p.bytes);
     };
     hipError_t e = hipSuccess;
     auto dget = [&](auto*& ptr, size_t bytes) {
         if (e != hipSuccess) return;
         ptr = (std::remove_reference_t<decltype(ptr)>)ctx->dpool.get(std::max<size_t>(bytes, 256), &e);
     };
-    for (uint64_t k = 0; k < n && e == hipSuccess; k++) {
-        e = hipMalloc((void**)&ps[k].dev, ps[k].bytes);
+    for (uint64_t k = 0; k < n; k++) {
+        if (int rc = plane_alloc(ctx, ps[k].bytes, &ps[k].dev)) {
+            const std::string msg = g_err;
+            cleanup(true);
+            g_err = msg;
+            return rc;
+        }
         zp[k].dev = ps[k].dev;
     }
     dget(d_in, in_bytes + 4096);  // decoder window over-read slack
@@ -1131,7 +1667,9 @@ int pbx_planes_register_zarr(pbx_ctx* ctx, uint64_t n, const pbx_plane_desc* ds,
     }
     cleanup(false);
     if (int rc = registry_insert(ctx, ps, plane_ids)) {  // keys re-checked at insertion
-        for (Plane& p : ps) (void)hipFree(p.dev);
+        const std::string msg = g_err;
+        for (Plane& p : ps) plane_free(ctx, p.dev, p.bytes);
+        g_err = msg;
         return rc;
     }
     return PBX_OK;
@@ -1144,43 +1682,41 @@ int pbx_plane_register_zarr(pbx_ctx* ctx, const pbx_plane_desc* d, const pbx_zar
 
 int pbx_plane_release(pbx_ctx* ctx, uint64_t id) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
-    std::lock_guard<std::mutex> run(ctx->run_mu);
-    std::lock_guard<std::mutex> g(ctx->reg_mu);
-    auto it = ctx->planes.find(id);
-    if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
-    Plane p = it->second;
-    ctx->planes.erase(it);
-    ctx->index.erase(std::make_tuple(p.image_id, p.z, p.c, p.t, p.res));
-    auto im = ctx->images.find(p.image_id);
-    if (im != ctx->images.end()) {
-        if (--im->second.level_planes[p.res] == 0) im->second.level_planes.erase(p.res);
-        if (--im->second.planes == 0) ctx->images.erase(im);
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        auto it = ctx->planes.find(id);
+        if (it == ctx->planes.end() || !it->second->indexed)
+            return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+        // batches planned before this call hold pins: the HBM goes with their last one
+        registry_remove(ctx, it->second, to_free);
     }
-    (void)hipSetDevice(ctx->device);
-    (void)sync_kernel_streams(ctx);
-    HIP_TRY(hipFree(p.dev));
+    free_planes(ctx, to_free);
     return PBX_OK;
 }
 
 int pbx_plane_read_be(pbx_ctx* ctx, uint64_t id, void* out, uint64_t bytes) {
     if (!ctx || !out) return fail(PBX_E_BADARG, "null argument");
-    Plane p;
-    {
-        std::lock_guard<std::mutex> g(ctx->reg_mu);
-        auto it = ctx->planes.find(id);
-        if (it == ctx->planes.end()) return fail(PBX_E_NOTFOUND, "no plane");
-        p = it->second;
-    }
-    const int bpp = bpp_of(p.pixel_type);
-    const int64_t row = (int64_t)p.size_x * bpp;
-    if (bytes < (uint64_t)row * p.size_y) return fail(PBX_E_BADARG, "buffer too small");
-    if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    HIP_TRY(hipMemcpy2D(out, row, p.dev, p.pitch, row, p.size_y, hipMemcpyDeviceToHost));
-    if (p.little_endian) {
-        uint8_t* b = (uint8_t*)out;
-        for (int64_t i = 0; i < row * p.size_y; i += bpp) std::reverse(b + i, b + i + bpp);
-    }
-    return PBX_OK;
+    int rc;
+    Plane* p = pin_id(ctx, id, 1u << PS_READY, &rc);
+    if (!p) return rc;
+    rc = [&]() -> int {
+        const int bpp = bpp_of(p->pixel_type);
+        const int64_t row = (int64_t)p->size_x * bpp;
+        const int64_t rows = p->band_rows;  // a band plane: its rows only
+        if (bytes < (uint64_t)row * rows) return fail(PBX_E_BADARG, "buffer too small");
+        if (ensure_device(ctx)) return PBX_E_INTERNAL;
+        HIP_TRY(hipMemcpy2D(out, row, p->dev, p->pitch, row, rows, hipMemcpyDeviceToHost));
+        if (p->little_endian) {
+            uint8_t* b = (uint8_t*)out;
+            for (int64_t i = 0; i < row * rows; i += bpp) std::reverse(b + i, b + i + bpp);
+        }
+        return PBX_OK;
+    }();
+    const std::string msg = g_err;
+    unpin_one(ctx, p);
+    g_err = msg;
+    return rc;
 }
 
 int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch** out) {
@@ -1200,17 +1736,20 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     std::vector<uint32_t> req_direct, req_rows, req_filt2, req_band, req_tiled;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
-        Plane pl;
+        Plane* pp = nullptr;
         int32_t w = 0, h = 0;
-        const int st = validate(ctx, r, w, h, pl);
+        const int st = validate(ctx, r, w, h, pp);
         b->status[i] = st;
         b->w[i] = w;
         b->h[i] = h;
         if (st != PBX_OK) continue;
+        if (!b->pins.empty() && b->pins.back().first == pp) b->pins.back().second++;
+        else b->pins.emplace_back(pp, 1);
+        const Plane& pl = *pp;  // pinned until pbx_batch_destroy; its geometry never changes
         const int bpp = bpp_of(pl.pixel_type);
         TileDesc d;
         memset(&d, 0, sizeof d);
-        d.plane = pl.dev;
+        d.plane = pl.base();
         d.pitch = pl.pitch;
         d.x = r.x; d.y = r.y; d.w = w; d.h = h;
         d.bpp = bpp; d.lbpp = log2i(bpp);
@@ -1412,6 +1951,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     const int prev = ctx->last_ks.load(), stagger = ctx->stagger.load();
     if (multi && stagger && prev >= 0 && prev != ks)
         HIP_TRY(hipStreamWaitEvent(st, ctx->stage_ev[prev][stagger - 1], 0));
+    b->attempted = true;
     HIP_TRY(hipEventRecord(b->ev[0], st));
     if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
     if (ndt)
@@ -1622,6 +2162,8 @@ void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return;
     (void)hipSetDevice(ctx->device);
     if (b->launched) (void)hipEventSynchronize(b->ev[8]);
+    else if (b->attempted) (void)sync_kernel_streams(ctx);  // a launch that failed midway
+    batch_unpin(ctx, b);
     free_batch_device(ctx, b);
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1716,11 +2258,12 @@ int pbx_wait(pbx_ctx* ctx, pbx_ticket* t, int64_t timeout_us) {
 }
 
 int pbx_abi_sizes(uint64_t* sizes, int n) {
-    const uint64_t v[5] = {sizeof(pbx_config), sizeof(pbx_plane_desc), sizeof(pbx_tile_req),
-                           sizeof(pbx_result), sizeof(pbx_batch_stats)};
+    const uint64_t v[7] = {sizeof(pbx_config), sizeof(pbx_plane_desc), sizeof(pbx_tile_req),
+                           sizeof(pbx_result), sizeof(pbx_batch_stats), sizeof(pbx_image_desc),
+                           sizeof(pbx_residency_stats)};
     if (!sizes || n < 0) return fail(PBX_E_BADARG, "null argument");
-    for (int i = 0; i < n && i < 5; i++) sizes[i] = v[i];
-    return 5;
+    for (int i = 0; i < n && i < 7; i++) sizes[i] = v[i];
+    return 7;
 }
 
 int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last, uint32_t nseg,

@@ -10,7 +10,8 @@ same names, argument meanings and error behaviour:
 * ``TileCtx.from_params`` raises ``ValueError`` for unparsable numbers (Java
   ``NumberFormatException`` -> HTTP 400, PixelBufferMicroserviceVerticle.java:344-348);
 * ``TileRequestHandler.get_tile`` returns ``None`` for every failure the reference maps
-  to ``null`` (unknown image, bad region, unsupported type/format: 404);
+  to ``null`` (unknown image, bad region, unsupported type/format: 404), and opens planes
+  the GPU does not hold yet from a ``PixelSource`` (getPixels + getPixelBuffer);
 * ``handle_get_tile`` reproduces the event-bus consumer: status, body and the
   ``filename`` header.
 
@@ -28,8 +29,12 @@ from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PBX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpbx.so")
 
-# enum pbx_status — the HTTP status the reference ends with
+# enum pbx_status — the HTTP status the reference ends with; E_NOT_RESIDENT (never sent to a
+# client) = the context does not hold the plane: load it and retry (TileRequestHandler below)
 OK, E_BADARG, E_NOTFOUND, E_INTERNAL, E_PENDING = 0, 400, 404, 500, 504
+E_EXISTS, E_NOT_RESIDENT, E_NO_SPACE = 409, 460, 507
+# plane states (pbx_plane_lookup)
+PS_FILLING, PS_READY, PS_EVICTED = 0, 1, 2
 # enum pbx_pixel_type (OMERO PixelType names)
 PIXEL_TYPES = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "float", "double"]
 INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT, DOUBLE = range(8)
@@ -57,6 +62,18 @@ class PbxPlaneDesc(ctypes.Structure):
                 ("source", ctypes.c_int32), ("host_data", ctypes.c_void_p),
                 ("host_bytes", ctypes.c_uint64), ("seed", ctypes.c_uint64),
                 ("plane_no", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class PbxImageDesc(ctypes.Structure):
+    _fields_ = [("image_id", ctypes.c_int64), ("pixel_type", ctypes.c_int32),
+                ("size_x", ctypes.c_int32), ("size_y", ctypes.c_int32), ("size_z", ctypes.c_int32),
+                ("size_c", ctypes.c_int32), ("size_t_", ctypes.c_int32), ("levels", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class PbxResidencyStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("budget", "resident_bytes", "planes", "evicted_planes", "evictions", "evicted_bytes")]
 
 
 class PbxZarrChunks(ctypes.Structure):
@@ -105,7 +122,9 @@ EXPORTS = [
     "pbx_abi_sizes", "pbx_shard_of", "pbx_test_huffman", "pbx_ctx_stats_get",
     "pbx_test_batch_lz77", "pbx_submit", "pbx_wait", "pbx_plane_build_pyramid",
     "pbx_plane_register_zarr", "pbx_planes_register_zarr", "pbx_release_cached",
-    "pbx_set_kernel_streams",
+    "pbx_set_kernel_streams", "pbx_image_declare", "pbx_image_release", "pbx_plane_create",
+    "pbx_plane_write_rows", "pbx_plane_commit", "pbx_plane_lookup", "pbx_set_residency_budget",
+    "pbx_residency_stats_get",
 ]
 
 _lib = None
@@ -136,6 +155,15 @@ def lib() -> ctypes.CDLL:
     L.pbx_release_cached.argtypes = [vp]
     L.pbx_plane_register.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), ctypes.POINTER(u64)]
     L.pbx_plane_release.argtypes = [vp, u64]
+    L.pbx_image_declare.argtypes = [vp, ctypes.POINTER(PbxImageDesc)]
+    L.pbx_image_release.argtypes = [vp, ctypes.c_int64]
+    L.pbx_plane_create.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), i32, i32, ctypes.POINTER(u64)]
+    L.pbx_plane_write_rows.argtypes = [vp, u64, i32, i32, vp, u64]
+    L.pbx_plane_commit.argtypes = [vp, u64]
+    L.pbx_plane_lookup.argtypes = [vp, ctypes.c_int64, i32, i32, i32, i32, ctypes.POINTER(u64),
+                                   ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.pbx_set_residency_budget.argtypes = [vp, u64]
+    L.pbx_residency_stats_get.argtypes = [vp, ctypes.POINTER(PbxResidencyStats)]
     L.pbx_plane_read_be.argtypes = [vp, u64, vp, u64]
     L.pbx_plane_build_pyramid.argtypes = [vp, u64, i32, ctypes.POINTER(u64),
                                           ctypes.POINTER(ctypes.c_double)]
@@ -410,6 +438,9 @@ class PixelsService:
         h = ctypes.c_void_p()
         _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        import threading
+        self._load_lock = threading.Lock()  # load_plane: one loader per plane key
+        self._loading: Dict[tuple, "threading.Lock"] = {}
 
     def close(self) -> None:
         if self._h:
@@ -575,6 +606,118 @@ class PixelsService:
 
     def release_plane(self, plane_id: int) -> None:
         _check(lib().pbx_plane_release(self._h, plane_id))
+
+    # ---------------------------------------------------------------- plane residency
+    def declare_image(self, pixels: "Pixels") -> None:
+        """pbx_image_declare: the Pixels row (getPixels, TileRequestHandler.java:220-241) and
+        the PixelBuffer's resolution level count, so that z/c/t/resolution outside the image
+        answer the reference's 404 without loading anything."""
+        d = PbxImageDesc(pixels.image_id, pixels.pixel_type, pixels.size_x, pixels.size_y,
+                         pixels.size_z, pixels.size_c, pixels.size_t, pixels.levels, 0)
+        _check(lib().pbx_image_declare(self._h, ctypes.byref(d)))
+
+    def release_image(self, image_id: int) -> None:
+        _check(lib().pbx_image_release(self._h, image_id))
+
+    def create_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int, size_x: int,
+                     size_y: int, level: int = 0, band: Optional[Tuple[int, int]] = None,
+                     big_endian: bool = True, generator: Optional[str] = None, seed: int = 0,
+                     plane_no: int = 0) -> int:
+        """pbx_plane_create: allocate a plane, or only the row band (y0, rows) of it.  Host
+        planes are filled with write_rows() and published by commit_plane(); generator
+        planes are generated on the GPU and ready at once."""
+        d = PbxPlaneDesc()
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, level
+        d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
+        d.byte_order = BIG_ENDIAN if big_endian else LITTLE_ENDIAN
+        if generator is not None:
+            d.source = {"fake": SRC_GEN_FAKE, "noise": SRC_GEN_NOISE}[generator]
+            d.seed, d.plane_no = seed, plane_no
+        y0, rows = band if band is not None else (0, 0)
+        pid = ctypes.c_uint64()
+        _check(lib().pbx_plane_create(self._h, ctypes.byref(d), y0, rows, ctypes.byref(pid)))
+        return pid.value
+
+    def write_rows(self, plane_id: int, y0: int, data) -> None:
+        """pbx_plane_write_rows: packed rows (bytes or an array of rows x size_x samples, in
+        the byte order given to create_plane) starting at plane row y0."""
+        import numpy as np
+        a = np.ascontiguousarray(data) if not isinstance(data, (bytes, bytearray, memoryview)) else \
+            np.frombuffer(data, np.uint8)
+        buf = a.view(np.uint8).reshape(-1)
+        rows = a.shape[0] if a.ndim >= 2 else None
+        if rows is None:
+            raise ValueError("write_rows: pass a 2-D array of rows (or use write_rows_bytes)")
+        _check(lib().pbx_plane_write_rows(self._h, plane_id, y0, rows, buf.ctypes.data, buf.nbytes))
+
+    def write_rows_bytes(self, plane_id: int, y0: int, rows: int, data: bytes) -> None:
+        buf = ctypes.create_string_buffer(bytes(data), len(data)) if not isinstance(data, bytes) else data
+        _check(lib().pbx_plane_write_rows(self._h, plane_id, y0, rows, buf, len(data)))
+
+    def commit_plane(self, plane_id: int) -> None:
+        _check(lib().pbx_plane_commit(self._h, plane_id))
+
+    def lookup_plane(self, image_id: int, z: int, c: int, t: int, level: int = 0):
+        """(plane id, state, band_y0, band_rows) of the plane registered under a key, or None."""
+        pid, st, y0, n = ctypes.c_uint64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        r = lib().pbx_plane_lookup(self._h, image_id, z, c, t, level, ctypes.byref(pid),
+                                   ctypes.byref(st), ctypes.byref(y0), ctypes.byref(n))
+        if r == E_NOTFOUND:
+            return None
+        _check(r)
+        return pid.value, st.value, y0.value, n.value
+
+    def set_residency_budget(self, nbytes: int) -> None:
+        """pbx_set_residency_budget: HBM for planes (0 = none); idle planes are evicted LRU."""
+        _check(lib().pbx_set_residency_budget(self._h, nbytes))
+
+    def residency_stats(self) -> Dict[str, int]:
+        s = PbxResidencyStats()
+        _check(lib().pbx_residency_stats_get(self._h, ctypes.byref(s)))
+        return {n: getattr(s, n) for n, _ in PbxResidencyStats._fields_}
+
+    def load_plane(self, source: "PixelSource", pixels: "Pixels", z: int, c: int, t: int,
+                   level: int = 0, band: Optional[Tuple[int, int]] = None,
+                   band_bytes: int = 64 << 20, timeout_s: float = 60.0) -> int:
+        """Open a plane this context does not hold, as getPixelBuffer + getTileDirect would
+        (TileRequestHandler.java:86,107-109,201-211): declare the image, create the plane (or
+        only `band` = (y0, rows) of it), stream its rows from `source` in bands of about
+        `band_bytes`, commit.  If another caller is loading the same key, wait for it."""
+        import threading
+        import time
+        self.declare_image(pixels)
+        key = (pixels.image_id, z, c, t, level)
+        with self._load_lock:
+            lk = self._loading.setdefault(key, threading.Lock())
+        with lk:
+            found = self.lookup_plane(*key)
+            if found is not None and found[1] == PS_READY:
+                return found[0]
+            sx, sy = source.level_size(pixels, level)
+            y0, rows = band if band is not None else (0, sy)
+            try:
+                pid = self.create_plane(pixels.image_id, z, c, t, pixels.pixel_type, sx, sy, level,
+                                        band=(y0, rows), big_endian=True)
+            except PbxError as e:
+                if e.status != E_EXISTS:
+                    raise
+                deadline = time.monotonic() + timeout_s  # another context user loads it
+                while time.monotonic() < deadline:
+                    found = self.lookup_plane(*key)
+                    if found is None or found[1] != PS_FILLING:
+                        return found[0] if found is not None else 0
+                    time.sleep(0.001)
+                raise
+            step = max(1, band_bytes // max(1, sx * BYTES_PER_PIXEL[pixels.pixel_type]))
+            try:
+                for r in range(y0, y0 + rows, step):
+                    n = min(step, y0 + rows - r)
+                    self.write_rows_bytes(pid, r, n, source.read_rows(pixels, z, c, t, level, r, n))
+                self.commit_plane(pid)
+            except BaseException:
+                self.release_plane(pid)
+                raise
+            return pid
 
     def build_pyramid(self, plane_id: int, levels: int, timing: bool = False):
         """Stored levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
@@ -754,23 +897,82 @@ class Batch:
             pass
 
 
+# ----------------------------------------------------------------- plane sources
+
+class Pixels:
+    """The Pixels row getPixels returns (TileRequestHandler.java:220-241: pixelsType, sizeX..T)
+    plus the PixelBuffer's getResolutionLevels()."""
+
+    def __init__(self, image_id: int, pixel_type: int, size_x: int, size_y: int, size_z: int = 1,
+                 size_c: int = 1, size_t: int = 1, levels: int = 1):
+        self.image_id, self.pixel_type = image_id, pixel_type
+        self.size_x, self.size_y = size_x, size_y
+        self.size_z, self.size_c, self.size_t, self.levels = size_z, size_c, size_t, levels
+
+
+class PixelSource:
+    """Where a plane comes from when this context does not hold it: the reference's
+    getPixels (TileRequestHandler.java:220-241) and getPixelBuffer(pixels) (:201-211) +
+    PixelBuffer.getTileDirect (:107-109).  Subclass per storage (ROMIO files, Zarr, ...)."""
+
+    def get_pixels(self, image_id: int) -> Optional[Pixels]:
+        """The image's Pixels, or None if it does not exist (-> 404, :130-132)."""
+        raise NotImplementedError
+
+    def level_size(self, pixels: Pixels, level: int) -> Tuple[int, int]:
+        """(size_x, size_y) of STORED level `level` (0 = full resolution)."""
+        if level == 0:
+            return pixels.size_x, pixels.size_y
+        raise NotImplementedError
+
+    def read_rows(self, pixels: Pixels, z: int, c: int, t: int, level: int, y0: int,
+                  rows: int) -> bytes:
+        """getTileDirect(z, c, t, 0, y0, sizeX, rows) at that level: packed big-endian rows."""
+        raise NotImplementedError
+
+
 # ----------------------------------------------------------------- TileRequestHandler
 
 class TileRequestHandler:
-    """TileRequestHandler.java:53-243 — ``get_tile()`` returns bytes, or None (-> 404)."""
+    """TileRequestHandler.java:53-243 — ``get_tile()`` returns bytes, or None (-> 404).
 
-    def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx):
+    With a ``source`` (PixelSource), a plane the context does not hold (status
+    E_NOT_RESIDENT) is opened as the reference opens it per request — getPixels (:84; None ->
+    404), getPixelBuffer + getTileDirect (:86,107-109) — loaded into HBM once, and the request
+    retried.  ``band`` = (y0, rows) loads only that row band (a rank's share of a whole slide);
+    requests outside it stay E_NOT_RESIDENT and are answered None here (another rank serves
+    them).  Without a source the context is a closed registry: not resident -> None (404)."""
+
+    def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx,
+                 source: Optional[PixelSource] = None, band: Optional[Tuple[int, int]] = None):
         self.pixels_service = pixels_service
         self.tile_ctx = tile_ctx
+        self.source = source
+        self.band = band
 
     def get_tile(self, client=None) -> Optional[bytes]:
         status, body = self.pixels_service.get_tile(self.tile_ctx)
+        if status == E_NOT_RESIDENT and self.source is not None:
+            pixels = self.source.get_pixels(self.tile_ctx.imageId)
+            if pixels is None:
+                return None  # :130-132 "Cannot find Image"
+            level = 0
+            r = self.tile_ctx.resolution
+            if r is not None:
+                level = pixels.levels - 1 - r  # OMERO numbering -> stored level (include/pbx.h)
+            if 0 <= level < pixels.levels and 0 <= self.tile_ctx.z < pixels.size_z and \
+                    0 <= self.tile_ctx.c < pixels.size_c and 0 <= self.tile_ctx.t < pixels.size_t:
+                self.pixels_service.load_plane(self.source, pixels, self.tile_ctx.z,
+                                               self.tile_ctx.c, self.tile_ctx.t, level, self.band)
+            else:
+                self.pixels_service.declare_image(pixels)  # the retry answers the 404
+            status, body = self.pixels_service.get_tile(self.tile_ctx)
         return body if status == OK else None
 
     getTile = get_tile
 
 
-def handle_get_tile(service: PixelsService, body: str):
+def handle_get_tile(service: PixelsService, body: str, source: Optional[PixelSource] = None):
     """PixelBufferVerticle.getTile (PixelBufferVerticle.java:90-147) over the JSON body.
 
     Returns (status, payload bytes or message, headers).  400 for an undecodable TileCtx,
@@ -781,7 +983,7 @@ def handle_get_tile(service: PixelsService, body: str):
     except Exception:
         return 400, b"Illegal tile context", {}
     try:
-        tile = TileRequestHandler(service, ctx).get_tile()
+        tile = TileRequestHandler(service, ctx, source).get_tile()
     except PbxError as e:
         return (400 if e.status == E_BADARG else 500), b"Exception while retrieving tile", {}
     if tile is None:

@@ -171,8 +171,10 @@ def test_tiff_all_types(service, oracle, pt):
 def test_error_statuses(service, oracle):
     iid, _ = host_plane(service, oracle, pbx.UINT16, 50, 40)
     cases = [
-        (pbx.TileCtx(iid + 999999, 0, 0, 0), pbx.E_NOTFOUND),                 # unknown image
-        (pbx.TileCtx(iid, 1, 0, 0, 0, 0, 4, 4), pbx.E_NOTFOUND),              # no such z
+        # an image / plane this context does not hold: the binding looks it up and loads it
+        # (getPixels + getPixelBuffer); without a PixelSource the handler answers 404 below
+        (pbx.TileCtx(iid + 999999, 0, 0, 0), pbx.E_NOT_RESIDENT),             # unknown image
+        (pbx.TileCtx(iid, 1, 0, 0, 0, 0, 4, 4), pbx.E_NOT_RESIDENT),          # z not loaded
         (pbx.TileCtx(iid, 0, 0, 0, 48, 0, 4, 4), pbx.E_NOTFOUND),             # out of bounds
         (pbx.TileCtx(iid, 0, 0, 0, -1, 0, 4, 4), pbx.E_NOTFOUND),
         (pbx.TileCtx(iid, 0, 0, 0, 10, 0, 0, 4), pbx.E_NOTFOUND),             # w default + x
@@ -187,6 +189,9 @@ def test_error_statuses(service, oracle):
     # the event-bus consumer mapping (PixelBufferVerticle.java:90-147)
     st, body, hdr = pbx.handle_get_tile(service, "{not json")
     assert st == 400
+    for c, _ in cases[:2]:  # closed registry (no PixelSource): not resident -> null -> 404
+        st, body, hdr = pbx.handle_get_tile(service, c.to_json())
+        assert st == 404 and body == f"Cannot find Image:{c.imageId}".encode()
     ok = pbx.TileCtx(iid, 0, 0, 0, 1, 2, 0, 3)
     st, body, hdr = pbx.handle_get_tile(service, ok.to_json())
     assert st == 404  # w defaults to 50 with x=1 -> outside the plane

@@ -26,11 +26,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_struct_sizes_match_bindings():
-    sizes = (ctypes.c_uint64 * 5)()
-    assert pbx.lib().pbx_abi_sizes(sizes, 5) == 5
+    sizes = (ctypes.c_uint64 * 7)()
+    assert pbx.lib().pbx_abi_sizes(sizes, 7) == 7
     assert list(sizes) == [ctypes.sizeof(t) for t in (pbx.PbxConfig, pbx.PbxPlaneDesc,
                                                       pbx.PbxTileReq, pbx.PbxResult,
-                                                      pbx.PbxBatchStats)]
+                                                      pbx.PbxBatchStats, pbx.PbxImageDesc,
+                                                      pbx.PbxResidencyStats)]
 
 
 def test_jni_shim_matches_abi():
@@ -49,7 +50,7 @@ def test_jni_shim_matches_abi():
 
 def test_enums_and_names():
     L = pbx.lib()
-    assert L.pbx_abi_version() == 5
+    assert L.pbx_abi_version() == 6
     assert L.pbx_format_from_string(None) == pbx.FMT_RAW
     assert L.pbx_format_from_string(b"png") == pbx.FMT_PNG
     assert L.pbx_format_from_string(b"tif") == pbx.FMT_TIF
