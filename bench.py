@@ -96,6 +96,28 @@ def mean(stats, field):
     return sum(getattr(s, field) for s in stats) / len(stats)
 
 
+def secondary_steps(svc, ctxs, steps, warmup, barrier):
+    """run_steps for a secondary line: at least PIPE_DEPTH warmup batches, so that every
+    batch the timed pass keeps in flight finds its device and pinned pool blocks already
+    allocated (a fresh service with one warmup batch allocated the second in-flight batch's
+    ~4 GB of blocks inside the timed region: BENCH_r02's adaptive line read 53k tiles/s for
+    8 ms of kernels per 4096 tiles)."""
+    return run_steps(svc, ctxs, steps, max(warmup, PIPE_DEPTH), barrier)
+
+
+def wall_vs_kernels(dt, steps, stats, world=1):
+    """Wall time per step next to the batch's own kernel time (HIP events, first to last
+    kernel of one batch); a line whose wall time exceeds 1.5x its kernels is flagged: it is
+    then measuring something other than the kernels it names."""
+    wall = 1e3 * dt / steps
+    kern = mean(stats, "ms_total")
+    out = {"wall_ms_per_step": round(wall, 3), "kernel_ms_per_step": round(kern, 3),
+           "wall_over_kernels": round(wall / kern, 3) if kern else None}
+    if kern and wall > 1.5 * kern:
+        out["flag"] = "wall time > 1.5x the batch's kernel time: not a kernel measurement"
+    return out
+
+
 def e2e_rate(svc, ctxs, batches=6):
     """End-to-end incl. D2H into pinned host memory (PCIe-inclusive; never the headline):
     batches pipelined two deep, batch k's D2H (copy stream) overlapping batch k+1's
@@ -325,15 +347,30 @@ def run_stream(svc, req_chunks, barrier, warmup=1, steps=1):
     return (time.perf_counter() - t0) / steps, stats
 
 
-def wholeslide_line(svc, rank, world, barrier, steps=2, side=100000, channels=5, tile=512,
+C4_SIDE, C4_CHANNELS = 100000, 5
+
+
+def c4_band(world, rank, side=C4_SIDE, tile=TILE):
+    """configs[3] ownership: rank r owns the contiguous tile-row band
+    [lo, hi) of every channel, i.e. plane rows [y0, y1)."""
+    n = (side + tile - 1) // tile
+    lo, hi = pbx.band_rows(n, world, rank)
+    return lo, hi, tile * lo, min(side, tile * hi)
+
+
+def wholeslide_line(svc, rank, world, barrier, steps=2, side=C4_SIDE, channels=C4_CHANNELS, tile=512,
                     band_batch_rows=49):
     """configs[3]: this rank's tile-row band of all 5 channels of a 100000^2 uint16 slide as
     TIFF (uncompressed = the reference's TiffWriter default, or Compression=8 when the
-    service deflates TIFF), in batches of `band_batch_rows` tile rows (bounded arenas)."""
+    service deflates TIFF), in batches of `band_batch_rows` tile rows (bounded arenas).  Each
+    rank holds ONLY its band of each channel in HBM (pbx_plane_create with band_y0/band_rows:
+    ~100 GB / N per rank); tiles of other bands would answer NOT_RESIDENT here."""
     n = (side + tile - 1) // tile
-    pids = [svc.register_plane(4, 0, c, 0, pbx.UINT16, side, side, generator="noise",
-                               plane_no=c) for c in range(channels)]
-    lo, hi = pbx.band_rows(n, world, rank)
+    lo, hi, y0, y1 = c4_band(world, rank, side, tile)
+    before = svc.residency_stats()["resident_bytes"]
+    pids = [svc.create_plane(4, 0, c, 0, pbx.UINT16, side, side, band=(y0, y1 - y0), generator="noise",
+                             plane_no=c) for c in range(channels)]
+    held = svc.residency_stats()["resident_bytes"] - before
     chunks, ntiles = [], 0
     for c in range(channels):
         for r0 in range(lo, hi, band_batch_rows):
@@ -346,15 +383,47 @@ def wholeslide_line(svc, rank, world, barrier, steps=2, side=100000, channels=5,
     in_bytes = sum(s.in_bytes for s in stats)
     out_bytes = sum(s.out_bytes for s in stats)
     line = {"tiles_this_rank": ntiles, "tiles_all_ranks": n * n * channels,
+            "tile_rows_this_rank": [lo, hi], "plane_rows_this_rank": [y0, y1],
+            "hbm_plane_bytes_this_rank": held,
             "tiles_per_s": round(ntiles * world / dt, 1), "ms_per_pass": round(dt * 1e3, 2),
             "pixel_bytes": in_bytes, "response_bytes": out_bytes,
             "d2h_bytes_saved_vs_uncompressed": int(in_bytes + ntiles * 160 - out_bytes)}
     ext = sum(s.ms_extract for s in stats)
     if out_bytes >= in_bytes:  # uncompressed: the HBM-bound k_extract does all the work
         line["k_extract_gbps"] = round(2 * in_bytes / (ext * 1e-3) / 1e9, 1)
+    # a tile of another rank's band is not resident here (world > 1)
+    if world > 1:
+        other = (hi % n) * tile if hi < n else 0
+        (st, _), = svc.get_tiles([pbx.TileCtx(4, 0, 0, 0, 0, other, tile, tile, format="tif")])
+        line["foreign_band_status"] = st
     for pid in pids:
         svc.release_plane(pid)
     return line
+
+
+C5_SEED, C5_REQUESTS, C5_SIDE = 5, 16384, 16384
+
+
+def c5_stream():
+    """configs[4]: ONE common mixed request stream (the same in every rank: seeded RNG
+    independent of the rank): uint8/int32/float32 planes of 16384^2, w, h in 256..2048,
+    png/tif/raw."""
+    import random
+    rnd = random.Random(C5_SEED)
+    reqs = []
+    for _ in range(C5_REQUESTS):
+        k = rnd.randrange(3)
+        w, h = 256 * rnd.randint(1, 8), 256 * rnd.randint(1, 8)
+        reqs.append(pbx.TileCtx(10 + k, 0, 0, 0, rnd.randrange(C5_SIDE - w + 1),
+                                rnd.randrange(C5_SIDE - h + 1), w, h,
+                                format=rnd.choice([None, "png", "tif"])))
+    return reqs
+
+
+def c5_shard(reqs, rank, world):
+    """The requests rank `rank` serves: pbx_shard_of(req) == rank (hash of image, z, c, t and
+    the 512-px tile cell), no collective."""
+    return [i for i, c in enumerate(reqs) if world == 1 or pbx.shard_of(c, world) == rank]
 
 
 def adaptive_filter_line(svc, rank, world, barrier, side):
@@ -387,7 +456,7 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                                                        big_endian=False)))
             n = (sz // TILE) ** 2
             ctxs = grid_ctxs(pid, "png", n=min(n, GRID * GRID))
-            dt, st, _ = run_steps(sa, ctxs, 3, 1, barrier)
+            dt, st, _ = secondary_steps(sa, ctxs, 3, 1, barrier)
             sample = [pbx.TileCtx(pid, 0, 0, 0, (j * 7 % (sz // TILE)) * TILE,
                                   (j * 5 % (sz // TILE)) * TILE, TILE, TILE) for j in range(8)]
             raw = [b for _, b in svc.get_tiles(sample)]
@@ -401,6 +470,7 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 z6 += len(zlib.compress(np.concatenate([np.zeros((TILE, 1), np.uint8), rows], 1).tobytes(), 6))
             out[name] = {
                 "tiles_per_s": round(len(ctxs) * 3 * world / dt, 1),
+                **wall_vs_kernels(dt, 3, st),
                 "k_filter_ms": round(mean(st, "ms_filter"), 3),
                 "deflate_chain_ms": round(mean(st, "ms_deflate") + mean(st, "ms_assemble"), 3),
                 "sample_bytes_per_tile": {"adaptive": round(sum(map(len, png_ad)) / 8, 1),
@@ -432,10 +502,10 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
     progress(rank, "raw")
     raw = grid_ctxs(iid, None)
-    dtr, sr, _ = run_steps(svc, raw, 5, 2, barrier)
+    dtr, sr, _ = secondary_steps(svc, raw, 5, 2, barrier)
     ms_ext = mean(sr, "ms_extract")
     out["raw_4096x512x512_u16"] = {
-        "tiles_per_s": round(len(raw) * 5 * world / dtr, 1),
+        "tiles_per_s": round(len(raw) * 5 * world / dtr, 1), **wall_vs_kernels(dtr, 5, sr),
         "k_extract_ms": round(ms_ext, 3),
         "k_extract_gbps": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9, 1),
         "k_extract_frac": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
@@ -448,9 +518,10 @@ def extra(out, svc, rank, world, barrier, iid, side):
         ss.set_kernel_streams(1, 0)
         ss.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0,
                           plane_no=rank)
-        dts, sst, _ = run_steps(ss, grid_ctxs(iid, "png"), 5, 2, barrier)
+        dts, sst, _ = secondary_steps(ss, grid_ctxs(iid, "png"), 5, 2, barrier)
         out["png_staged_rows_4096x512x512_u16"] = {
             "tiles_per_s": round(len(grid_ctxs(iid, "png")) * 5 * world / dts, 1),
+            **wall_vs_kernels(dts, 5, sst),
             "k_rows_ms": round(mean(sst, "ms_filter"), 3),
             "k_lz77_ms": round(mean(sst, "ms_lz77"), 3)}
     # Row f3: on-GPU resolution pyramid of the headline plane (6 levels of 2x2 box means);
@@ -476,9 +547,9 @@ def extra(out, svc, rank, world, barrier, iid, side):
     progress(rank, "fake")
     svc.register_plane(2, 0, 0, 0, pbx.UINT16, side, side, generator="fake", plane_no=rank)
     fk = grid_ctxs(2, "png")
-    dtf, sf, _ = run_steps(svc, fk, 3, 2, barrier)
+    dtf, sf, _ = secondary_steps(svc, fk, 3, 2, barrier)
     out["png_fake_4096x512x512_u16"] = {
-        "tiles_per_s": round(len(fk) * 3 * world / dtf, 1),
+        "tiles_per_s": round(len(fk) * 3 * world / dtf, 1), **wall_vs_kernels(dtf, 3, sf),
         "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1)}
     # the adaptive PNG filter (option; the reference writes filter None)
     progress(rank, "adaptive filter")
@@ -487,38 +558,29 @@ def extra(out, svc, rank, world, barrier, iid, side):
     progress(rank, "configs[2]")
     svc.register_plane(3, 0, 0, 0, pbx.UINT16, 65536, 65536, generator="noise", plane_no=rank)
     c3 = grid_ctxs(3, "png", tile=1024)
-    dt3, s3, _ = run_steps(svc, c3, 2, 2, barrier)
+    dt3, s3, _ = secondary_steps(svc, c3, 2, 2, barrier)
     out["c3_png_4096x1024x1024_u16"] = {
-        "tiles_per_s": round(len(c3) * 2 * world / dt3, 1),
+        "tiles_per_s": round(len(c3) * 2 * world / dt3, 1), **wall_vs_kernels(dt3, 2, s3),
         "compressed_bytes_per_tile": round(s3[-1].deflate_out_bytes / len(c3), 1)}
     # configs[3]: whole slide 100000^2 x 5 channels uint16, 512^2 tiles (edge 160 px) -> TIFF.
-    # Every rank holds the 5 channels and serves its contiguous band of tile rows of each
+    # Every rank holds and serves its contiguous band of tile rows of the 5 channels
     # (SURVEY.md §8(e)); over all ranks the bands cover the whole slide (192,080 tiles).
     progress(rank, "configs[3]")
-    if os.environ.get("PBX_BENCH_ONE_GPU") and world > 1:
-        # N ranks' 100 GB slides do not fit one GPU: the rehearsal skips configs[3]
-        out["c4_wholeslide_tif_100k_u16_5ch"] = {"skipped": "PBX_BENCH_ONE_GPU rehearsal"}
-    else:
-        out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
-        svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
-        with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
-            out["c4_wholeslide_tif_deflate_100k_u16_5ch"] = wholeslide_line(sd, rank, world, barrier,
-                                                                            steps=1)
-    # configs[4]: mixed stream (uint8/int32/float32 planes 16384^2, w,h in 256..2048,
-    # png/tif/raw), 16384 requests as 8 batches of 2048
-    import random
+    # Each rank holds only its band (the one-GPU rehearsal's ranks share ~100 GB).
+    out["c4_wholeslide_tif_100k_u16_5ch"] = wholeslide_line(svc, rank, world, barrier)
+    svc.release_cached()  # the deflate-TIFF service below needs the HBM the caches hold
+    with pbx.PixelsService(device=torch.cuda.current_device(), tiff_deflate=True) as sd:
+        out["c4_wholeslide_tif_deflate_100k_u16_5ch"] = wholeslide_line(sd, rank, world, barrier,
+                                                                        steps=1)
+    # configs[4]: one common mixed stream of 16,384 requests (uint8/int32/float32 planes
+    # 16384^2, w,h in 256..2048, png/tif/raw); each rank serves its pbx_shard_of share, in
+    # batches of 2048
     progress(rank, "configs[4]")
-    rnd = random.Random(rank)
     for k, pt in enumerate((pbx.UINT8, pbx.INT32, pbx.FLOAT)):
-        svc.register_plane(10 + k, 0, 0, 0, pt, 16384, 16384, generator="noise", plane_no=rank)
-    reqs5 = []
-    for _ in range(16384):
-        k = rnd.randrange(3)
-        w, h = 256 * rnd.randint(1, 8), 256 * rnd.randint(1, 8)
-        reqs5.append(pbx.TileCtx(10 + k, 0, 0, 0, rnd.randrange(16384 - w + 1),
-                                 rnd.randrange(16384 - h + 1), w, h,
-                                 format=rnd.choice([None, "png", "tif"])))
-    chunks = [pbx.make_reqs(reqs5[j:j + 2048]) for j in range(0, len(reqs5), 2048)]
+        svc.register_plane(10 + k, 0, 0, 0, pt, C5_SIDE, C5_SIDE, generator="noise")
+    reqs5 = c5_stream()
+    mine = [reqs5[i] for i in c5_shard(reqs5, rank, world)]
+    chunks = [pbx.make_reqs(mine[j:j + 2048]) for j in range(0, len(mine), 2048)]
 
     def stream_pass():
         ok = err = 0
@@ -545,8 +607,16 @@ def extra(out, svc, rank, world, barrier, iid, side):
     torch.cuda.synchronize()
     barrier()
     dt5 = time.perf_counter() - t0
-    out["c5_mixed_16384_requests"] = {"tiles_per_s": round(ok * world / dt5, 1),
-                                      "ok": ok, "errors_404": err}
+    tot = torch.tensor([ok, err, dt5], dtype=torch.float64)
+    if world > 1:  # whole-stream totals over the ranks; time = the slowest rank's
+        t_max = torch.tensor([dt5], dtype=torch.float64)
+        dist.all_reduce(tot)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dt5 = float(t_max[0])
+    out["c5_mixed_16384_requests"] = {"tiles_per_s": round(float(tot[0]) / dt5, 1),
+                                      "ok": int(tot[0]), "errors_404": int(tot[1]),
+                                      "requests_this_rank": len(mine),
+                                      "stream": f"one common stream (seed {C5_SEED}), sharded by pbx_shard_of"}
 
 
 def launch_ranks(n, argv):
@@ -594,10 +664,28 @@ def dry_run(args, world, rank):
     if world > 1:
         dist.barrier()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # the data partitioning each rank would serve (host only: pbx_shard_of and the band
+    # split are pure functions of the request / grid): C5's common stream by request hash,
+    # C4's tile-row bands; rank 0 checks that the ranks' shares partition the whole
+    reqs = c5_stream()
+    shard = c5_shard(reqs, rank, world)
+    band = c4_band(world, rank)
+    parts = [(shard, band)]
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, (shard, band))
     if rank == 0:
+        idx = [i for sh, _ in parts for i in sh]
+        bands = [b for _, b in parts]
+        n_rows = (C4_SIDE + TILE - 1) // TILE
         print(json.dumps({"metric": METRIC, "value": None, "unit": "tiles/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "ranks_met": int(met[0]), "max_step_s": float(t[0])}), flush=True)
+                          "ranks_met": int(met[0]), "max_step_s": float(t[0]),
+                          "c5_requests_per_rank": [len(sh) for sh, _ in parts],
+                          "c5_shards_partition_stream": sorted(idx) == list(range(len(reqs))),
+                          "c4_tile_row_bands": [[b[0], b[1]] for b in bands],
+                          "c4_bands_partition_slide": bands[0][0] == 0 and bands[-1][1] == n_rows and
+                          all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

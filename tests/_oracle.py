@@ -213,3 +213,37 @@ def bench(kind, pt, fmt, pw, ph, w, h, tiles, threads):
     nb = ctypes.c_uint64()
     sec = lib().pbxo_bench(kind, pt, fmt, pw, ph, w, h, tiles, threads, ctypes.byref(nb))
     return sec, nb.value
+
+
+def check_png_grid_pixels(bodies, pt, tile_w, tile_h, grid_x, y_row0, kind=2, seed=0, threads=8):
+    """Pixel check of EVERY tile of a grid of filter-None PNG responses (PNG of 8/16-bit
+    unsigned samples), tile i at (tile_w * (i % grid_x), y_row0 + tile_h * (i // grid_x)):
+    each IDAT is inflated by zlib and its scanlines, filter bytes stripped, must equal the
+    oracle generator's big-endian tile.  One oracle band per grid row (threads in parallel).
+    Returns the indices of the tiles that differ."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    bpp = BPP[pt]
+    rows = (len(bodies) + grid_x - 1) // grid_x
+
+    def row(r):
+        band = gen_region(kind, pt, 0, y_row0 + r * tile_h, tile_w * grid_x, tile_h, seed=seed)
+        band = band.reshape(tile_h, tile_w * grid_x * bpp)
+        bad = []
+        for i in range(r * grid_x, min(len(bodies), (r + 1) * grid_x)):
+            b = bodies[i]
+            x = i % grid_x
+            try:
+                n = int.from_bytes(b[91:95], "big")
+                scan = np.frombuffer(zlib.decompress(b[99:99 + n]), np.uint8)
+                scan = scan.reshape(tile_h, 1 + tile_w * bpp)
+                ok = not scan[:, 0].any() and np.array_equal(
+                    scan[:, 1:], band[:, x * tile_w * bpp:(x + 1) * tile_w * bpp])
+            except Exception:
+                ok = False
+            if not ok:
+                bad.append(i)
+        return bad
+
+    with ThreadPoolExecutor(threads) as ex:
+        return [i for part in ex.map(row, range(rows)) for i in part]

@@ -59,6 +59,12 @@ def test_bench_launches_ranks(world):
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == world and rec["ranks_met"] == world and rec["steps"] == 3
+    # the bench's multi-rank data split: C5's one common stream sharded by pbx_shard_of, and
+    # C4's tile-row bands, each partitioning the whole over the ranks
+    assert rec["c5_shards_partition_stream"] is True
+    assert sum(rec["c5_requests_per_rank"]) == 16384
+    assert all(n > 16384 / world * 0.8 for n in rec["c5_requests_per_rank"])
+    assert rec["c4_bands_partition_slide"] is True and len(rec["c4_tile_row_bands"]) == world
 
 
 @pytest.mark.parametrize("world", [2])

@@ -22,7 +22,7 @@ import pbx
 
 pytestmark = pytest.mark.gpu
 
-_ids = itertools.count(90000)
+_ids = itertools.count(90000, 10)
 NOISE = 2
 
 

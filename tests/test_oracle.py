@@ -112,3 +112,15 @@ def test_filename_and_content_type(oracle):
     assert oracle.content_type("png") == "image/png"
     assert oracle.content_type("tif") == "image/tiff"
     assert oracle.content_type(None) == oracle.content_type("jpg") == "application/octet-stream"
+
+
+def test_grid_pixel_checker_catches_a_wrong_tile(oracle):
+    """check_png_grid_pixels (used on every tile of the full-size GPU grids) accepts the
+    oracle's own PNGs and names a tile whose pixels belong elsewhere in the grid."""
+    bodies = []
+    for i in range(6):
+        t = oracle.gen_region(2, oracle.UINT16, (i % 3) * 64, (i // 3) * 32, 64, 32)
+        bodies.append(bytes(oracle.png_encode(t, oracle.UINT16, 64, 32)[1]))
+    assert oracle.check_png_grid_pixels(bodies, oracle.UINT16, 64, 32, 3, 0) == []
+    bodies[4] = bodies[1]
+    assert oracle.check_png_grid_pixels(bodies, oracle.UINT16, 64, 32, 3, 0) == [4]
