@@ -7,16 +7,25 @@
  *   getTile            TileRequestHandler.getTile body, :98-128 (getTileDirect :107-109 +
  *                      writeImage :123, with the w/h defaulting of :92-97)
  *   init / shutdown    PixelBufferMicroserviceVerticle.start :114-233 / stop :298-308
- *   registerPlane      the PixelBuffer a deployment reads planes from (ROMIO / Zarr),
- *                      once per (image, z, c, t, level) instead of once per tile
+ *   declareImage       the Pixels row getPixels returns (:84, :220-241)
+ *   createPlane / writeRows / commitPlane
+ *                      getPixelBuffer (:86, :201-211) + getTileDirect reads, done once per
+ *                      (image, z, c, t, level) — or per row band — instead of once per tile
  *   registerZarr       ZarrPixelsService chunk reads (PixelBufferVerticle.java:29,56)
  */
 package com.glencoesoftware.omero.ms.pixelbuffer;
+
+import java.nio.ByteBuffer;
 
 final class PbxNative {
     static { System.loadLibrary("pbx_jni"); }   // libpbx_jni.so, linked against libpbx.so
 
     private PbxNative() {}
+
+    /** pbx_status values getTile reports in statusOut[2]. */
+    static final int OK = 0, BADARG = 400, NOTFOUND = 404, NOT_RESIDENT = 460, INTERNAL = 500;
+    /** planeState values. */
+    static final int PLANE_ABSENT = -1, PLANE_LOADING = 0, PLANE_READY = 1, PLANE_EVICTED = 2;
 
     /** pbx_init.  device -1 = $PBX_DEVICE / $LOCAL_RANK / 0; tiffTile 0 = one strip. */
     static native long init(int device, int pngFilter, boolean tiffDeflate, int tiffTile);
@@ -24,13 +33,53 @@ final class PbxNative {
     static native void shutdown(long ctx);
 
     /**
-     * pbx_plane_register of one plane's samples as PixelBuffer returns them (big-endian
-     * unless littleEndian).  level = STORED level, 0 = full resolution.  Returns the plane
-     * id; throws IllegalArgumentException (400) / RuntimeException (500).
+     * pbx_image_declare: the Pixels row (pixelsType value, sizeX..T) and the PixelBuffer's
+     * getResolutionLevels().  Idempotent; throws IllegalArgumentException if it contradicts
+     * an earlier declaration.
+     */
+    static native void declareImage(long ctx, long imageId, String pixelsType, int sizeX, int sizeY,
+                                    int sizeZ, int sizeC, int sizeT, int levels);
+
+    static native void releaseImage(long ctx, long imageId);
+
+    /**
+     * pbx_plane_create: an empty plane of STORED level `level` (0 = full resolution), or only
+     * its rows [bandY0, bandY0 + bandRows) (bandRows 0 = whole plane), whose rows arrive by
+     * writeRows in the given byte order.  Returns the plane id, or 0 when another caller
+     * holds the key (it is loading the plane: wait until planeState is no longer LOADING).
+     * Throws 507 (RuntimeException) when the plane does not fit the HBM residency budget.
+     */
+    static native long createPlane(long ctx, long imageId, int z, int c, int t, int level,
+                                   String pixelsType, int sizeX, int sizeY, boolean littleEndian,
+                                   int bandY0, int bandRows);
+
+    /**
+     * pbx_plane_write_rows: `rows` packed rows of rowBytes (= sizeX * bytesPerPixel) from
+     * data[off ..], e.g. one PixelBuffer.getTileDirect(z, c, t, 0, y0, sizeX, rows, data).
+     * Copied out in pieces (no JNI critical section), so a band of any size may be passed.
+     */
+    static native void writeRows(long ctx, long planeId, int y0, int rows, int rowBytes, byte[] data,
+                                 int off);
+
+    /** The same from a direct ByteBuffer (its capacity bounds what is read). */
+    static native void writeRowsDirect(long ctx, long planeId, int y0, int rows, ByteBuffer data);
+
+    /** pbx_plane_commit: the plane is served from now on (every row must be written). */
+    static native void commitPlane(long ctx, long planeId);
+
+    /** pbx_plane_lookup: PLANE_ABSENT / LOADING / READY / EVICTED for a key. */
+    static native int planeState(long ctx, long imageId, int z, int c, int t, int level);
+
+    /** pbx_set_residency_budget: HBM bytes for planes (0 = none); idle planes evicted LRU. */
+    static native void setResidencyBudget(long ctx, long bytes);
+
+    /**
+     * A whole plane (< 2 GiB) in one call: createPlane + writeRows + commitPlane.  Planes
+     * larger than a Java array are loaded in row bands with those three calls.
      */
     static native long registerPlane(long ctx, long imageId, int z, int c, int t, int level,
-                                     String pixelsType /* Pixels.getPixelsType() value */,
-                                     int sizeX, int sizeY, boolean littleEndian, byte[] plane);
+                                     String pixelsType, int sizeX, int sizeY, boolean littleEndian,
+                                     byte[] plane);
 
     /** pbx_plane_build_pyramid: `levels` 2x2-mean levels below the plane; returns their ids. */
     static native long[] buildPyramid(long ctx, long planeId, int levels);
@@ -39,8 +88,8 @@ final class PbxNative {
 
     /**
      * pbx_plane_register_zarr: the concatenated chunk files of one plane (C order over the
-     * chunk grid, offsets has gx*gy + 1 entries, an empty range = missing chunk).
-     * codec 0 null, 1 blosc, 2 zlib (.zarray "compressor").
+     * chunk grid, offsets has gx*gy + 1 non-decreasing entries within chunks, an empty range
+     * = missing chunk).  codec 0 null, 1 blosc, 2 zlib (.zarray "compressor").
      */
     static native long registerZarr(long ctx, long imageId, int z, int c, int t, int level,
                                     String pixelsType, int sizeX, int sizeY, boolean littleEndian,
@@ -48,14 +97,16 @@ final class PbxNative {
                                     long[] offsets, long fillBits);
 
     /**
-     * pbx_get_tile: the response body, or null exactly where TileRequestHandler.getTile
-     * returns null (-> 404).  resolution: TileCtx.resolution in OMERO's numbering, null
-     * -> pass RESOLUTION_NONE; a given negative value must be passed as < -1 (it throws in
-     * setResolutionLevel upstream -> null).  regionOut receives the post-defaulting w, h.
-     * A device failure throws RuntimeException (-> 500, PixelBufferVerticle.java:141-146).
+     * pbx_get_tile: the response body, or null.  statusOut (length 3) receives the
+     * post-defaulting w, h (the filename header's) and the status: OK; NOTFOUND / BADARG
+     * where TileRequestHandler.getTile returns null (-> 404); NOT_RESIDENT when this context
+     * does not hold the plane (load it, then call again).  resolution: TileCtx.resolution in
+     * OMERO's numbering, null -> RESOLUTION_NONE, a given negative value -> below -1
+     * (resolutionArg).  A device failure throws RuntimeException (-> 500,
+     * PixelBufferVerticle.java:141-146).
      */
     static native byte[] getTile(long ctx, long imageId, int z, int c, int t, int resolution,
-                                 int x, int y, int w, int h, String format, int[] regionOut);
+                                 int x, int y, int w, int h, String format, int[] statusOut);
 
     static final int RESOLUTION_NONE = -1;
 

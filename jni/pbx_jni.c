@@ -5,8 +5,14 @@
  *
  * Error mapping follows the reference: PBX_E_NOTFOUND / PBX_E_BADARG statuses of a tile are
  * the nulls TileRequestHandler.getTile returns (-> 404, PixelBufferVerticle.java:132-136);
- * PBX_E_INTERNAL is an exception (-> 500, :141-146).  Registration errors throw
- * IllegalArgumentException (400) or RuntimeException (500). */
+ * PBX_E_INTERNAL is an exception (-> 500, :141-146).  PBX_E_NOT_RESIDENT is reported through
+ * getTile's status slot so that the handler can load the plane (getPixels + getPixelBuffer)
+ * and retry.  Registration errors throw IllegalArgumentException (400) or
+ * RuntimeException (500).
+ *
+ * No JNI critical section is ever held across library calls: Java arrays are copied out in
+ * bounded pieces (GetByteArrayRegion) into native buffers, or read in place from direct
+ * ByteBuffers, so the GPU work never stalls the JVM's garbage collector. */
 #include <jni.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -15,12 +21,17 @@
 #include "pbx.h"
 
 #define PBX_CTX(h) ((pbx_ctx*)(intptr_t)(h))
+#define PIECE_BYTES (16u << 20) /* Java -> native copy granule of writeRows */
+
+static void throw_class(JNIEnv* env, const char* cls, const char* msg) {
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
 
 static void throw_status(JNIEnv* env, int st) {
-    const char* cls = st == PBX_E_BADARG || st == PBX_E_NOTFOUND ? "java/lang/IllegalArgumentException"
-                                                                 : "java/lang/RuntimeException";
-    jclass c = (*env)->FindClass(env, cls);
-    if (c) (*env)->ThrowNew(env, c, pbx_last_error());
+    throw_class(env, st == PBX_E_BADARG || st == PBX_E_NOTFOUND || st == PBX_E_EXISTS
+                         ? "java/lang/IllegalArgumentException" : "java/lang/RuntimeException",
+                pbx_last_error());
 }
 
 static int pixel_type(JNIEnv* env, jstring s) {
@@ -64,21 +75,157 @@ static void fill_desc(pbx_plane_desc* d, jlong image, jint z, jint c, jint t, ji
     d->source = PBX_SRC_HOST;
 }
 
-JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_registerPlane(
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_declareImage(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image, jstring ptype, jint sx, jint sy, jint sz, jint sc,
+        jint st_, jint levels) {
+    (void)cls;
+    pbx_image_desc d;
+    memset(&d, 0, sizeof d);
+    d.image_id = image;
+    d.pixel_type = pixel_type(env, ptype);
+    d.size_x = sx; d.size_y = sy; d.size_z = sz; d.size_c = sc; d.size_t_ = st_;
+    d.levels = levels;
+    int st = pbx_image_declare(PBX_CTX(ctx), &d);
+    if (st != PBX_OK) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_releaseImage(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image) {
+    (void)cls;
+    int st = pbx_image_release(PBX_CTX(ctx), image);
+    if (st != PBX_OK && st != PBX_E_NOTFOUND) throw_status(env, st);
+}
+
+/* 0 when another caller holds the key (409: it is loading or has loaded the plane). */
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_createPlane(
         JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint level,
-        jstring ptype, jint sx, jint sy, jboolean le, jbyteArray plane) {
+        jstring ptype, jint sx, jint sy, jboolean le, jint band_y0, jint band_rows) {
     (void)cls;
     pbx_plane_desc d;
     fill_desc(&d, image, z, c, t, level, pixel_type(env, ptype), sx, sy, le);
-    const jsize n = (*env)->GetArrayLength(env, plane);
-    jbyte* data = (*env)->GetPrimitiveArrayCritical(env, plane, NULL);
-    d.host_data = data;
-    d.host_bytes = (uint64_t)n;
     uint64_t id = 0;
-    int st = pbx_plane_register(PBX_CTX(ctx), &d, &id);
-    (*env)->ReleasePrimitiveArrayCritical(env, plane, data, JNI_ABORT);
-    if (st != PBX_OK) throw_status(env, st);
+    int st = pbx_plane_create(PBX_CTX(ctx), &d, band_y0, band_rows, &id);
+    if (st == PBX_E_EXISTS) return 0;
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return 0;
+    }
     return (jlong)id;
+}
+
+/* Rows [y0, y0 + rows) from data[off .. off + rows * rowBytes): copied out of the Java array
+ * in whole-row pieces of at most PIECE_BYTES (no critical section), each handed to
+ * pbx_plane_write_rows (pinned staging, DMA). */
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_writeRows(
+        JNIEnv* env, jclass cls, jlong ctx, jlong plane, jint y0, jint rows, jint row_bytes, jbyteArray data,
+        jint off) {
+    (void)cls;
+    if (!data || rows < 0 || row_bytes <= 0 || off < 0) {
+        throw_class(env, "java/lang/IllegalArgumentException", "writeRows: bad arguments");
+        return;
+    }
+    const jsize n = (*env)->GetArrayLength(env, data);
+    if ((int64_t)off + (int64_t)rows * row_bytes > (int64_t)n) {
+        throw_class(env, "java/lang/IllegalArgumentException", "writeRows: array shorter than rows * rowBytes");
+        return;
+    }
+    if (!rows) return;
+    int32_t per = (int32_t)(PIECE_BYTES / (uint32_t)row_bytes);
+    if (per < 1) per = 1;
+    if (per > rows) per = rows;
+    jbyte* buf = malloc((size_t)per * (size_t)row_bytes);
+    if (!buf) {
+        throw_class(env, "java/lang/OutOfMemoryError", "writeRows: native staging buffer");
+        return;
+    }
+    for (int32_t r = 0; r < rows; r += per) {
+        const int32_t k = rows - r < per ? rows - r : per;
+        (*env)->GetByteArrayRegion(env, data, off + r * row_bytes, k * row_bytes, buf);
+        if ((*env)->ExceptionCheck(env)) break;
+        int st = pbx_plane_write_rows(PBX_CTX(ctx), (uint64_t)plane, y0 + r, k, buf, (uint64_t)k * row_bytes);
+        if (st != PBX_OK) {
+            throw_status(env, st);
+            break;
+        }
+    }
+    free(buf);
+}
+
+/* The same from a direct ByteBuffer (no copy on the Java side). */
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_writeRowsDirect(
+        JNIEnv* env, jclass cls, jlong ctx, jlong plane, jint y0, jint rows, jobject buffer) {
+    (void)cls;
+    void* p = buffer ? (*env)->GetDirectBufferAddress(env, buffer) : NULL;
+    const jlong cap = buffer ? (*env)->GetDirectBufferCapacity(env, buffer) : -1;
+    if (!p || cap < 0) {
+        throw_class(env, "java/lang/IllegalArgumentException", "writeRowsDirect: not a direct buffer");
+        return;
+    }
+    int st = pbx_plane_write_rows(PBX_CTX(ctx), (uint64_t)plane, y0, rows, p, (uint64_t)cap);
+    if (st != PBX_OK) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_commitPlane(
+        JNIEnv* env, jclass cls, jlong ctx, jlong plane) {
+    (void)cls;
+    int st = pbx_plane_commit(PBX_CTX(ctx), (uint64_t)plane);
+    if (st != PBX_OK) throw_status(env, st);
+}
+
+/* State of the plane under a key: 0 loading, 1 ready, 2 evicted; -1 not registered. */
+JNIEXPORT jint JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_planeState(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint level) {
+    (void)cls;
+    int32_t state = -1;
+    int st = pbx_plane_lookup(PBX_CTX(ctx), image, z, c, t, level, NULL, &state, NULL, NULL);
+    if (st == PBX_E_NOTFOUND) return -1;
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return -1;
+    }
+    return state;
+}
+
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_setResidencyBudget(
+        JNIEnv* env, jclass cls, jlong ctx, jlong bytes) {
+    (void)cls;
+    int st = pbx_set_residency_budget(PBX_CTX(ctx), bytes < 0 ? 0 : (uint64_t)bytes);
+    if (st != PBX_OK) throw_status(env, st);
+}
+
+/* A whole plane in one call, through the same create / writeRows / commit path (a plane
+ * larger than a Java array is loaded with createPlane + writeRows bands instead). */
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_registerPlane(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint level,
+        jstring ptype, jint sx, jint sy, jboolean le, jbyteArray plane) {
+    const int pt = pixel_type(env, ptype);
+    const int bpp = pbx_bytes_per_pixel(pt);
+    if (!plane || bpp <= 0 || sx <= 0 || sy <= 0) {
+        throw_class(env, "java/lang/IllegalArgumentException", "registerPlane: bad arguments");
+        return 0;
+    }
+    const int64_t row = (int64_t)sx * bpp;
+    if (row > 0x7fffffff || row * sy > (int64_t)(*env)->GetArrayLength(env, plane)) {
+        throw_class(env, "java/lang/IllegalArgumentException", "registerPlane: array shorter than the plane");
+        return 0;
+    }
+    pbx_plane_desc d;
+    fill_desc(&d, image, z, c, t, level, pt, sx, sy, le);
+    uint64_t id = 0;
+    int st = pbx_plane_create(PBX_CTX(ctx), &d, 0, 0, &id);
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return 0;
+    }
+    Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_writeRows(env, cls, ctx, (jlong)id, 0, sy,
+                                                                      (jint)row, plane, 0);
+    if (!(*env)->ExceptionCheck(env)) {
+        st = pbx_plane_commit(PBX_CTX(ctx), id);
+        if (st == PBX_OK) return (jlong)id;
+        throw_status(env, st);
+    }
+    (void)pbx_plane_release(PBX_CTX(ctx), id);  /* all or nothing */
+    return 0;
 }
 
 JNIEXPORT jlongArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_buildPyramid(
@@ -114,10 +261,36 @@ JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_
         jstring ptype, jint sx, jint sy, jboolean le, jint chunk_x, jint chunk_y, jint codec,
         jbyteArray chunks, jlongArray offsets, jlong fill_bits) {
     (void)cls;
+    if (!chunks || !offsets || sx <= 0 || sy <= 0 || chunk_x <= 0 || chunk_y <= 0) {
+        throw_class(env, "java/lang/IllegalArgumentException", "registerZarr: bad arguments");
+        return 0;
+    }
+    /* the C-ABI reads offsets[0 .. gx*gy] and data[0 .. offsets[gx*gy]): check both against
+     * the Java arrays before handing them over */
+    const int64_t gx = ((int64_t)sx + chunk_x - 1) / chunk_x, gy = ((int64_t)sy + chunk_y - 1) / chunk_y;
+    const jsize n_off = (*env)->GetArrayLength(env, offsets), n_data = (*env)->GetArrayLength(env, chunks);
+    if ((int64_t)n_off < gx * gy + 1) {
+        throw_class(env, "java/lang/IllegalArgumentException", "registerZarr: offsets needs gx*gy + 1 entries");
+        return 0;
+    }
+    jlong* offs = (*env)->GetLongArrayElements(env, offsets, NULL);
+    if (!offs) return 0;  /* OutOfMemoryError pending */
+    for (int64_t i = 0; i < gx * gy; i++)
+        if (offs[i] < 0 || offs[i + 1] < offs[i] || offs[i + 1] > (jlong)n_data) {
+            (*env)->ReleaseLongArrayElements(env, offsets, offs, JNI_ABORT);
+            throw_class(env, "java/lang/IllegalArgumentException",
+                        "registerZarr: offsets must be non-decreasing and within chunks");
+            return 0;
+        }
+    /* a copy (or a pinned view the VM chooses), never a critical section: the call below
+     * uploads and decodes on the GPU */
+    jbyte* data = (*env)->GetByteArrayElements(env, chunks, NULL);
+    if (!data) {
+        (*env)->ReleaseLongArrayElements(env, offsets, offs, JNI_ABORT);
+        return 0;
+    }
     pbx_plane_desc d;
     fill_desc(&d, image, z, c, t, level, pixel_type(env, ptype), sx, sy, le);
-    jlong* offs = (*env)->GetLongArrayElements(env, offsets, NULL);   /* gx*gy + 1 entries */
-    jbyte* data = (*env)->GetPrimitiveArrayCritical(env, chunks, NULL);
     pbx_zarr_chunks zc;
     memset(&zc, 0, sizeof zc);
     zc.chunk_x = chunk_x; zc.chunk_y = chunk_y; zc.codec = codec;
@@ -126,39 +299,49 @@ JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_
     zc.fill_bits = (uint64_t)fill_bits;
     uint64_t id = 0;
     int st = pbx_plane_register_zarr(PBX_CTX(ctx), &d, &zc, &id, NULL);
-    (*env)->ReleasePrimitiveArrayCritical(env, chunks, data, JNI_ABORT);
+    (*env)->ReleaseByteArrayElements(env, chunks, data, JNI_ABORT);
     (*env)->ReleaseLongArrayElements(env, offsets, offs, JNI_ABORT);
     if (st != PBX_OK) throw_status(env, st);   /* 400: corrupt / unsupported chunk */
     return (jlong)id;
 }
 
+/* statusOut (length >= 3): [0] w, [1] h after the :92-97 defaulting, [2] the pbx status. */
 JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_getTile(
         JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint res,
-        jint x, jint y, jint w, jint h, jstring jfmt, jintArray region_out) {
+        jint x, jint y, jint w, jint h, jstring jfmt, jintArray status_out) {
     (void)cls;
     pbx_tile_req req;
     memset(&req, 0, sizeof req);
     req.image_id = image; req.z = z; req.c = c; req.t = t; req.resolution = res;
     req.x = x; req.y = y; req.w = w; req.h = h;
     const char* fmt = jfmt ? (*env)->GetStringUTFChars(env, jfmt, NULL) : NULL;
+    if (jfmt && !fmt) return NULL;  /* OutOfMemoryError pending */
     req.format = pbx_format_from_string(fmt);
     if (fmt) (*env)->ReleaseStringUTFChars(env, jfmt, fmt);
     pbx_result r;
+    memset(&r, 0, sizeof r);   /* pbx_get_tile may return before it writes the result */
+    r.status = PBX_E_INTERNAL;
     int st = pbx_get_tile(PBX_CTX(ctx), &req, &r);
-    if (region_out) {
-        jint wh[2] = {r.w, r.h};   /* the :92-97 defaulting the filename header relies on */
-        (*env)->SetIntArrayRegion(env, region_out, 0, 2, wh);
-    }
-    if (st == PBX_E_INTERNAL) {
-        pbx_results_release(PBX_CTX(ctx), &r, 1);
-        throw_status(env, st);
-        return NULL;
+    /* a call-level failure (null ctx, shutdown, failed plan) leaves the result unfilled */
+    const int status = r.owner || r.status == st ? r.status : st;
+    if (status_out && (*env)->GetArrayLength(env, status_out) >= 3) {
+        jint v[3] = {r.w, r.h, status};
+        (*env)->SetIntArrayRegion(env, status_out, 0, 3, v);
     }
     jbyteArray out = NULL;
-    if (r.status == PBX_OK) {                      /* else every null the reference returns */
+    if (status == PBX_OK) {
+        if (r.len > 0x7fffffffu) {  /* a Java array cannot hold it */
+            if (r.owner) pbx_results_release(PBX_CTX(ctx), &r, 1);
+            throw_class(env, "java/lang/IllegalArgumentException", "tile response larger than 2^31-1 bytes");
+            return NULL;
+        }
         out = (*env)->NewByteArray(env, (jsize)r.len);   /* exact length, :188-193 */
-        if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)r.len, (const jbyte*)r.data);
+        if (out && r.len) (*env)->SetByteArrayRegion(env, out, 0, (jsize)r.len, (const jbyte*)r.data);
     }
-    pbx_results_release(PBX_CTX(ctx), &r, 1);
-    return out;
+    if (r.owner) pbx_results_release(PBX_CTX(ctx), &r, 1);
+    if (status == PBX_E_INTERNAL) {
+        throw_status(env, status);   /* -> 500 */
+        return NULL;
+    }
+    return out;   /* null for every status the reference answers null, and NOT_RESIDENT */
 }
