@@ -706,6 +706,263 @@ hipError_t launch_filter2(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
 }
 
 uint32_t filter2_band_rows() { return F2_ROWS; }
+
+// ------------------------------------------- K1+K2: streaming PNG filter rows
+// PNG tiles with a Sub/Up/Avg/Paeth or adaptive filter, rows of whole 16-byte chunks
+// (w * bpp % 16 == 0, <= 2 KiB; 16-byte aligned source rows).  No LDS and no barriers: one
+// WAVE per run of F3_RUN consecutive rows of one tile holds a whole row in registers (lane l
+// = 16-byte chunks l, 64 + l), keeps the row above in registers, and prefetches the next row
+// while it filters the current one.  A sample's left neighbour is the previous lane's chunk
+// (one DPP wave shift; lane 0: the previous 64-chunk group, or zero before the row).  The
+// adaptive choice (minimum sum of |signed residual|, first filter on ties: the oracle's rule)
+// needs the whole row: five per-lane sums reduced over the wave by DPP.  Stream words are
+// stored 16-byte aligned: lane l writes the aligned word ending where its chunk's first 16 - s
+// bytes end (s = the row's start offset mod 16), i.e. the previous chunk's last s bytes and its
+// own first 16 - s (k_rows' layout); lane 0 of a row writes the word that holds the previous
+// row's tail and the filter byte.  That word needs the previous row's filtered tail, so a run
+// also filters the row before it (without storing it): 1/F3_RUN extra reads, no cross-wave
+// hand-off.
+constexpr uint32_t F3_RUN = 32;
+constexpr uint32_t F3_NT = 256;
+
+__device__ __forceinline__ uint32_t f3_wave_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// The previous lane's chunk (wave shift right by one lane); lane 0 gets `first`.
+__device__ __forceinline__ uint4 f3_prev_lane(const uint4& x, const uint4& first) {
+    return make_uint4((uint32_t)__builtin_amdgcn_update_dpp((int)first.x, (int)x.x, 0x138, 0xF, 0xF, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)first.y, (int)x.y, 0x138, 0xF, 0xF, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)first.z, (int)x.z, 0x138, 0xF, 0xF, false),
+                      (uint32_t)__builtin_amdgcn_update_dpp((int)first.w, (int)x.w, 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint4 f3_readlane(const uint4& x, uint32_t l) {
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)x.x, l), (uint32_t)__builtin_amdgcn_readlane((int)x.y, l),
+                      (uint32_t)__builtin_amdgcn_readlane((int)x.z, l), (uint32_t)__builtin_amdgcn_readlane((int)x.w, l));
+}
+// The four words of the bytes bpp before each byte of chunk x (p = the chunk before it).
+__device__ __forceinline__ void f3_left(const uint4& x, const uint4& p, uint32_t bpp, uint32_t (&l)[4]) {
+    if (bpp == 8) {
+        l[0] = p.z; l[1] = p.w; l[2] = x.x; l[3] = x.y;
+    } else if (bpp == 4) {
+        l[0] = p.w; l[1] = x.x; l[2] = x.y; l[3] = x.z;
+    } else {
+        const uint32_t sh = 4 - bpp;
+        l[0] = __builtin_amdgcn_alignbyte(x.x, p.w, sh);
+        l[1] = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
+        l[2] = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
+        l[3] = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
+    }
+}
+
+// v[g] for a uniform g < G, by masks (no dynamic register index: that would be scratch)
+template <uint32_t G>
+__device__ __forceinline__ uint4 f3_pick(const uint4 (&v)[G], uint32_t g) {
+    uint4 r = v[0];
+#pragma unroll
+    for (uint32_t k = 1; k < G; k++) {
+        const uint32_t m = 0u - (uint32_t)(g == k);
+        r = make_uint4((r.x & ~m) | (v[k].x & m), (r.y & ~m) | (v[k].y & m), (r.z & ~m) | (v[k].z & m),
+                       (r.w & ~m) | (v[k].w & m));
+    }
+    return r;
+}
+
+template <uint32_t G, bool ADAPTIVE>
+__global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                  uint32_t nwaves, uint8_t* __restrict__ stream) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x) * (F3_NT / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wi >= nwaves) return;  // a whole wave: no barrier in this kernel
+    const uint32_t ti = upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; });
+    const TileDesc d = dt[ti];
+    const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
+    const uint32_t h = (uint32_t)d.h;
+    const uint32_t r0 = (wi - d.blk_first) * F3_RUN, r1 = r0 + F3_RUN < h ? r0 + F3_RUN : h;
+    const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
+    const uint32_t fixed = (uint32_t)d.filter;  // 1..4 (ADAPTIVE: 5)
+    const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
+    uint8_t* out = stream + d.out_off;
+    const uint4 Z = make_uint4(0, 0, 0, 0);
+    auto load_row = [&](uint32_t r, uint4 (&v)[G]) {
+        const uint8_t* rp = src0 + (int64_t)r * d.pitch;
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t c = 64 * g + lane;
+            v[g] = gload16(rp + 16 * (c < nc ? c : 0u));
+        }
+    };
+    auto conv = [&](uint4 (&v)[G]) {  // big-endian samples (and the sign flip), zero past the row
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            uint4 q = v[g];
+            if (swap) q = swap16(q, (int)bpp);
+            if (flip) q = flip_msb(q, (int)bpp);
+            v[g] = 64 * g + lane < nc ? q : Z;
+        }
+    };
+    const uint32_t rs = r0 ? r0 - 1 : 0;  // first row filtered (the one before the run: not stored)
+    // rows in registers: up (r - 1), cur (r), and the loads of rows r + 1, r + 2 in flight
+    uint4 up[G], cur[G], n1[G], n2[G];
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) up[g] = n1[g] = n2[g] = Z;
+    if (rs) load_row(rs - 1, up);
+    load_row(rs, cur);
+    if (rs + 1 < r1) load_row(rs + 1, n1);
+    if (rs + 2 < r1) load_row(rs + 2, n2);
+    if (rs) conv(up);
+    uint4 tail = Z;  // the previous row's last filtered chunk (uniform)
+    const uint32_t cl = nc - 1, gl = cl >> 6, ll = cl & 63;
+    for (uint32_t r = rs; r < r1; r++) {
+        uint4 n3[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) n3[g] = Z;
+        if (r + 3 < r1) load_row(r + 3, n3);  // three rows ahead in flight
+        conv(cur);
+        uint4 lft[G], ul[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            lft[g] = f3_prev_lane(cur[g], g ? f3_readlane(cur[g - 1], 63) : Z);
+            ul[g] = f3_prev_lane(up[g], g ? f3_readlane(up[g - 1], 63) : Z);
+        }
+        uint4 f[G];
+        uint32_t ft = fixed;
+        if (ADAPTIVE) {
+            // every candidate ([0] Sub, [1] Up, [2] Avg, [3] Paeth) and its sum of |residual|
+            uint32_t fw[G][4][4];
+            uint32_t sm[5] = {0, 0, 0, 0, 0};
+            constexpr uint32_t M = 0x80808080u;
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                uint32_t l[4], lu[4];
+                f3_left(cur[g], lft[g], bpp, l);
+                f3_left(up[g], ul[g], bpp, lu);
+                const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
+                const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    fw[g][0][j] = sub8(x[j], l[j]);
+                    fw[g][1][j] = sub8(x[j], u[j]);
+                    fw[g][2][j] = sub8(x[j], avg8(l[j], u[j]));
+                    fw[g][3][j] = sub8(x[j], paeth4(l[j], u[j], lu[j]));
+                }
+                if (64 * g + lane < nc) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        sm[0] = __builtin_amdgcn_sad_u8(x[j] ^ M, M, sm[0]);
+#pragma unroll
+                        for (uint32_t k = 0; k < 4; k++) sm[k + 1] = __builtin_amdgcn_sad_u8(fw[g][k][j] ^ M, M, sm[k + 1]);
+                    }
+                }
+            }
+            uint32_t best = 0, bs = f3_wave_sum(sm[0]);
+#pragma unroll
+            for (uint32_t k = 1; k < 5; k++) {
+                const uint32_t v = f3_wave_sum(sm[k]);
+                if (v < bs) { bs = v; best = k; }
+            }
+            ft = best;
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
+                const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+                const uint32_t m0 = ~(m1 | m2 | m3 | m4);
+                uint32_t o[4];
+                const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    o[j] = (x[j] & m0) | (fw[g][0][j] & m1) | (fw[g][1][j] & m2) | (fw[g][2][j] & m3) |
+                           (fw[g][3][j] & m4);
+                f[g] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+        } else {
+            // one filter for every row: only it (ft is uniform: a scalar branch)
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                uint32_t l[4], lu[4], o[4];
+                const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
+                const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
+                if (ft == 2) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], u[j]);
+                } else {
+                    f3_left(cur[g], lft[g], bpp, l);
+                    if (ft == 1) {
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], l[j]);
+                    } else if (ft == 3) {
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], avg8(l[j], u[j]));
+                    } else {
+                        f3_left(up[g], ul[g], bpp, lu);
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], paeth4(l[j], u[j], lu[j]));
+                    }
+                }
+                f[g] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+        }
+        if (r >= r0) {
+            // stream words of row r: data chunk c at q = r * rowlen + 1 + 16 c, s = q mod 16
+            const uint32_t q0 = r * rowlen + 1, s = q0 & 15u, A = q0 - s;
+            // lane 0's word before its chunk: the previous row's last s - 1 bytes and the filter byte
+            const uint4 y = make_uint4((tail.x >> 8) | (tail.y << 24), (tail.y >> 8) | (tail.z << 24),
+                                       (tail.z >> 8) | (tail.w << 24), (tail.w >> 8) | (ft << 24));
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t c = 64 * g + lane;
+                const uint4 pf = f3_prev_lane(f[g], g ? f3_readlane(f[g - 1], 63) : y);
+                uint4 wv = f[g];
+                if (s) {
+                    uint32_t ww[4];
+                    funnel16(pf, f[g], 16 - s, ww);
+                    wv = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                }
+                if (c < nc) gstore16(out + A + 16 * c, wv);
+            }
+            if (s == 0 && lane == 0) gstore16(out + A - 16, y);  // (r > 0: s == 1 at r == 0)
+            if (r + 1 == h && s) {  // the tile's last row: its tail word (zeros after the stream)
+                const uint4 fl = f3_pick(f, gl);
+                if (lane == ll) {
+                    uint32_t ww[4];
+                    funnel16(fl, Z, 16 - s, ww);
+                    gstore16(out + A + 16 * nc, make_uint4(ww[0], ww[1], ww[2], ww[3]));
+                }
+            }
+        }
+        tail = f3_readlane(f3_pick(f, gl), ll);
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            up[g] = cur[g];
+            cur[g] = n1[g];
+            n1[g] = n2[g];
+            n2[g] = n3[g];
+        }
+    }
+}
+
+hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
+                          uint32_t max_rb, bool adaptive, uint8_t* stream) {
+    if (!ntiles || !nwaves) return hipSuccess;
+    const uint32_t blocks = (nwaves + F3_NT / 64 - 1) / (F3_NT / 64);
+    const dim3 g(blocks), b(F3_NT);
+    if (max_rb <= 1024) {
+        if (adaptive) hipLaunchKernelGGL((k_filter3<1, true>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
+        else hipLaunchKernelGGL((k_filter3<1, false>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
+    } else {
+        if (adaptive) hipLaunchKernelGGL((k_filter3<2, true>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
+        else hipLaunchKernelGGL((k_filter3<2, false>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
+    }
+    return hipGetLastError();
+}
+
+uint32_t filter3_run_rows() { return F3_RUN; }
+uint32_t filter3_max_rb() { return 2048; }
 uint32_t filter2_max_rb() { return F2_MAX_RB; }
 
 }  // namespace pbx

@@ -75,6 +75,73 @@ __constant__ int16_t c_of_def[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1
 
 __device__ __forceinline__ uint32_t hibit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
+// ---- XXH64 (seed 0) of a decoded frame: the optional Content_Checksum (RFC 8878 3.1.1; low
+// 32 bits of XXH64 of the frame's content), which libzstd verifies.  The four stripe
+// accumulators are inherently serial over the 32-byte stripes, so lanes 0..3 run them; the wave
+// loads 1 KiB (32 stripes) at a time, one 16-byte word per lane, and lane k takes 8-byte word k
+// of each stripe from the lane holding it (ds_bpermute).
+constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull, XP2 = 0xC2B2AE3D27D4EB4Full, XP3 = 0x165667B19E3779F9ull,
+                   XP4 = 0x85EBCA77C2B2AE63ull, XP5 = 0x27D4EB2F165667C5ull;
+__device__ __forceinline__ uint64_t xrotl(uint64_t x, uint32_t r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) { return xrotl(acc + in * XP2, 31) * XP1; }
+__device__ __forceinline__ uint64_t xmerge(uint64_t h, uint64_t v) { return (h ^ xround(0, v)) * XP1 + XP4; }
+__device__ __forceinline__ uint64_t gld64(const uint8_t* p) {  // 8 bytes, any alignment
+    const uint32_t* q = (const uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t sh = ((uint32_t)(uintptr_t)p & 3u) * 8;
+    const uint32_t a = q[0], b = q[1], c = q[2];
+    const uint32_t lo = sh ? (a >> sh) | (b << (32 - sh)) : a, hi = sh ? (b >> sh) | (c << (32 - sh)) : b;
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ uint64_t xxh64_wave(const uint8_t* p, uint32_t len, uint32_t lane) {
+    const uint32_t nst = len / 32, k = lane & 3;
+    uint64_t v = k == 0 ? XP1 + XP2 : k == 1 ? XP2 : k == 2 ? 0ull : 0ull - XP1;
+    for (uint32_t b = 0; b < nst; b += 32) {
+        const uint32_t at = 32 * b + 16 * lane;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (at + 16 <= 32 * nst) {
+            const uint64_t lo = gld64(p + at), hi = gld64(p + at + 8);
+            x = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        }
+        const uint32_t ns = nst - b < 32 ? nst - b : 32;
+        for (uint32_t j = 0; j < ns; j++) {
+            const int src = (int)(2 * j + (k >> 1));
+            const uint32_t a0 = (uint32_t)__shfl((int)x.x, src, 64), a1 = (uint32_t)__shfl((int)x.y, src, 64);
+            const uint32_t a2 = (uint32_t)__shfl((int)x.z, src, 64), a3 = (uint32_t)__shfl((int)x.w, src, 64);
+            const uint64_t in = (k & 1) ? ((uint64_t)a3 << 32) | a2 : ((uint64_t)a1 << 32) | a0;
+            v = xround(v, in);
+        }
+    }
+    auto rl = [](uint64_t x, int l) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    };
+    uint64_t h;
+    if (nst) {
+        const uint64_t v1 = rl(v, 0), v2 = rl(v, 1), v3 = rl(v, 2), v4 = rl(v, 3);
+        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = XP5;
+    }
+    h += len;
+    uint32_t i = 32 * nst;
+    for (; i + 8 <= len; i += 8) h = xrotl(h ^ xround(0, gld64(p + i)), 27) * XP1 + XP4;
+    if (i + 4 <= len) {
+        h = xrotl(h ^ ((uint64_t)(uint32_t)gld64(p + i) * XP1), 23) * XP2 + XP3;
+        i += 4;
+    }
+    for (; i < len; i++) h = xrotl(h ^ ((uint64_t)p[i] * XP5), 11) * XP1;
+    h ^= h >> 33;
+    h *= XP2;
+    h ^= h >> 29;
+    h *= XP3;
+    h ^= h >> 32;
+    return h;
+}
+
 // Input bytes of the frame through the LDS window, read forward or backward: the window is
 // reloaded so that it covers [q, q + n) with room in the direction of travel.
 struct ZIn {
@@ -751,9 +818,20 @@ __global__ __launch_bounds__(64 * ZSTD_WAVES) void k_zarr_zstd(const ZStream* __
     ZSD(if (si == 0 && lane == 0) printf("[zstd] total %lu literals %lu tables %lu sequences %lu (read %lu copy %lu match %lu) blocks %u nlit %u nseq %u far %u litruns %u dlen %u\n",
         (unsigned long)(__builtin_amdgcn_s_memtime() - c0), (unsigned long)clit, (unsigned long)ctab,
         (unsigned long)cseq, (unsigned long)cread, (unsigned long)ccopy, (unsigned long)cmatch, nblk, nlits, nseqs, nfar, nlitrun, t.dlen);)
-    if (!bad && checksum) q += 4;
+    uint32_t want = 0;
+    if (!bad && checksum) {
+        if (q + 4 > ilen) bad = 36;
+        else want = (uint32_t)in.le64_fwd(q);
+        q += 4;
+    }
     if (!bad && (o.op != o.olen || q > ilen)) bad = 36;
     o.finish();
+    if (!bad && checksum) {
+        // the content checksum over the output this wave stored: its stores complete and the
+        // vector L1 invalidated (agent-scope fence), then read back
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        if ((uint32_t)xxh64_wave(dst + t.dst_off, t.dlen, lane) != want) bad = 37;
+    }
     if (lane == 0) err[si] = bad;
 }
 

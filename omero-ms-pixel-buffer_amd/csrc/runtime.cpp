@@ -239,9 +239,11 @@ struct pbx_batch {
     std::vector<TiledHdr> th;              // tiled-TIFF responses (their sub-tiles carry TF_TILED)
     std::vector<uint32_t> th_req;
     uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
-    // dt = [direct tiles | k_rows tiles | k_filter2 tiles | k_filter tiles | tiled-TIFF sub-tiles]
+    // dt = [direct tiles | k_rows tiles | k_filter2 tiles | k_filter3 tiles | k_filter tiles |
+    //       tiled-TIFF sub-tiles]
     uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
     uint32_t nfilt2_tiles = 0, filt2_blocks = 0, filt2_max_rb = 0;  // k_filter2 group
+    uint32_t nfilt3_tiles = 0, filt3_waves = 0, filt3_max_rb = 0;   // k_filter3 group
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -1732,8 +1734,9 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     const int32_t tiff_tile = ctx->cfg.tiff_tile;
     // deflate sub-tiles of a tiled TIFF stay consecutive (one response = one run of the
     // deflate arena): they go to k_filter, after the other banded tiles
-    std::vector<TileDesc> dt_direct, dt_rows, dt_filt2, dt_band, dt_tiled;
-    std::vector<uint32_t> req_direct, req_rows, req_filt2, req_band, req_tiled;
+    std::vector<TileDesc> dt_direct, dt_rows, dt_filt2, dt_filt3, dt_band, dt_tiled;
+    std::vector<uint32_t> req_direct, req_rows, req_filt2, req_filt3, req_band, req_tiled;
+    static const bool use_f3 = !getenv("PBX_FILTER3") || atoi(getenv("PBX_FILTER3")) != 0;
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane* pp = nullptr;
@@ -1765,8 +1768,13 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             const uint32_t ntx = ((uint32_t)w + T - 1) / T, nty = ((uint32_t)h + T - 1) / T;
             const uint64_t nsub = (uint64_t)ntx * nty, sub = (uint64_t)T * T * bpp;
             const uint64_t D = tiff_tiled_data_offset(nsub);
-            if (D + nsub * sub > 0xFFFFFFFFull) {  // classic TIFF: 32-bit offsets
-                b->status[i] = fail(PBX_E_BADARG, "tiled TIFF response over 4 GiB");
+            // The response must fit a Java byte[] (the reference's int tileSize rule, :100-103:
+            // past 2^31-1 bytes getTile returns null -> 404); zero-padding the edge sub-tiles
+            // can push it past the unpadded tile's size, and a deflated sub-tile is at most its
+            // stored form (5 bytes per 16 KiB block) plus the zlib framing.
+            const uint64_t sub_max = deflate ? sub + 5 * ((sub + 16383) / 16384) + 64 : sub;
+            if (D + nsub * sub_max > 2147483647ull) {
+                b->status[i] = fail(PBX_E_NOTFOUND, "tiled TIFF response over 2^31-1 bytes");
                 b->in_bytes -= tile_bytes;
                 continue;
             }
@@ -1846,10 +1854,15 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             // filtered PNG rows of whole dwords: dword-wide filter arithmetic (k_filter2)
             const bool filt2_ok = (d.flags & TF_PNGROWS) && d.filter != 0 && rb % 4 == 0 && rb >= 16 &&
                                   rb <= filter2_max_rb() && ((uint64_t)d.x * bpp % 16) == 0;
+            // filtered PNG rows of whole 16-byte chunks: the streaming one-wave-per-run k_filter3
+            const bool filt3_ok = use_f3 && filt2_ok && rb % 16 == 0 && rb <= filter3_max_rb();
             if (rows_ok && bpp <= 4 && !ctx->cfg.stage_rows) {
                 d.flags |= TF_DIRECT;
                 dt_direct.push_back(d);
                 req_direct.push_back((uint32_t)i);
+            } else if (filt3_ok) {
+                dt_filt3.push_back(d);
+                req_filt3.push_back((uint32_t)i);
             } else if (filt2_ok) {
                 dt_filt2.push_back(d);
                 req_filt2.push_back((uint32_t)i);
@@ -1865,11 +1878,14 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     b->dt.insert(b->dt.end(), dt_rows.begin(), dt_rows.end());
     b->nfilt2_tiles = (uint32_t)dt_filt2.size();
     b->dt.insert(b->dt.end(), dt_filt2.begin(), dt_filt2.end());
+    b->nfilt3_tiles = (uint32_t)dt_filt3.size();
+    b->dt.insert(b->dt.end(), dt_filt3.begin(), dt_filt3.end());
     b->dt.insert(b->dt.end(), dt_band.begin(), dt_band.end());
     b->dt.insert(b->dt.end(), dt_tiled.begin(), dt_tiled.end());
     b->dt_req = std::move(req_direct);
     b->dt_req.insert(b->dt_req.end(), req_rows.begin(), req_rows.end());
     b->dt_req.insert(b->dt_req.end(), req_filt2.begin(), req_filt2.end());
+    b->dt_req.insert(b->dt_req.end(), req_filt3.begin(), req_filt3.end());
     b->dt_req.insert(b->dt_req.end(), req_band.begin(), req_band.end());
     b->dt_req.insert(b->dt_req.end(), req_tiled.begin(), req_tiled.end());
     const uint32_t tiled0 = (uint32_t)(b->dt.size() - dt_tiled.size());
@@ -1896,6 +1912,10 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.blk_first = b->filt2_blocks;
             b->filt2_blocks += (uint32_t)((d.h + filter2_band_rows() - 1) / filter2_band_rows());
             b->filt2_max_rb = std::max<uint32_t>(b->filt2_max_rb, d.rowlen - 1);
+        } else if (k < b->ndirect_tiles + b->nrows_tiles + b->nfilt2_tiles + b->nfilt3_tiles) {
+            d.blk_first = b->filt3_waves;  // first wave (run of rows) of the tile
+            b->filt3_waves += (uint32_t)((d.h + filter3_run_rows() - 1) / filter3_run_rows());
+            b->filt3_max_rb = std::max<uint32_t>(b->filt3_max_rb, d.rowlen - 1);
         } else {
             d.blk_first = b->filt_blocks;
             b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
@@ -1966,9 +1986,11 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
                            (uint8_t*)b->d_stream));
-    HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles + b->nfilt2_tiles,
-                          ndt - b->ndirect_tiles - b->nrows_tiles - b->nfilt2_tiles, b->filt_blocks,
-                          (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter3(st, d_rows + b->nrows_tiles + b->nfilt2_tiles, b->nfilt3_tiles, b->filt3_waves,
+                           b->filt3_max_rb, ctx->cfg.png_filter == PBX_FILTER_ADAPTIVE, (uint8_t*)b->d_stream));
+    HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles + b->nfilt2_tiles + b->nfilt3_tiles,
+                          ndt - b->ndirect_tiles - b->nrows_tiles - b->nfilt2_tiles - b->nfilt3_tiles,
+                          b->filt_blocks, (uint8_t*)b->d_stream));
     HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;

@@ -33,6 +33,43 @@ def lz4_block(data: bytes, accel: int = 1) -> bytes:
     return out.raw[:n]
 
 
+_zstd = None
+
+
+def _libzstd():
+    global _zstd
+    if _zstd is None:
+        L = ctypes.CDLL("libzstd.so.1")
+        L.ZSTD_createCCtx.restype = ctypes.c_void_p
+        L.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+        L.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.ZSTD_compressBound.restype = ctypes.c_size_t
+        L.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+        L.ZSTD_compress2.restype = ctypes.c_size_t
+        L.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                     ctypes.c_size_t]
+        L.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        _zstd = L
+    return _zstd
+
+
+def zstd_frame(data: bytes, level: int = 5, checksum: bool = False) -> bytes:
+    """One zstd frame from the system libzstd (ZSTD_c_compressionLevel = 100,
+    ZSTD_c_checksumFlag = 201: the optional XXH64 content checksum)."""
+    L = _libzstd()
+    cc = L.ZSTD_createCCtx()
+    try:
+        L.ZSTD_CCtx_setParameter(cc, 100, level)
+        L.ZSTD_CCtx_setParameter(cc, 201, 1 if checksum else 0)
+        cap = L.ZSTD_compressBound(len(data))
+        out = ctypes.create_string_buffer(cap)
+        n = L.ZSTD_compress2(cc, out, cap, data, len(data))
+        assert not L.ZSTD_isError(n)
+        return out.raw[:n]
+    finally:
+        L.ZSTD_freeCCtx(cc)
+
+
 def blosc_blocksize(nbytes: int, typesize: int, clevel: int, codec: str) -> int:
     """c-blosc 1.21 compute_blocksize() for the automatic block size."""
     L1 = 32 * 1024
@@ -61,14 +98,15 @@ def shuffle_block(block: bytes, ts: int) -> bytes:
 
 
 def blosc_encode(raw: bytes, typesize: int, clevel: int = 5, shuffle: bool = True,
-                 codec: str = "lz4", blocksize: int = 0, split: bool = True) -> bytes:
+                 codec: str = "lz4", blocksize: int = 0, split: bool = True,
+                 zstd_checksum: bool = False) -> bytes:
     nbytes = len(raw)
     ts = max(1, typesize)
     bs = blocksize or blosc_blocksize(nbytes, ts, clevel, codec)
     bs = max(1, min(bs, nbytes))
     nblocks = -(-nbytes // bs)
     leftover = nbytes % bs
-    compcode = {"lz4": 1, "lz4hc": 1, "zlib": 3}[codec]
+    compcode = {"lz4": 1, "lz4hc": 1, "zlib": 3, "zstd": 4}[codec]
     flags = (0x1 if shuffle else 0) | (compcode << 5) | (0 if split else 0x10)
     body = bytearray()
     starts = []
@@ -84,7 +122,10 @@ def blosc_encode(raw: bytes, typesize: int, clevel: int = 5, shuffle: bool = Tru
         starts.append(hdr + len(body))
         for s in range(nsp):
             part = block[s * neb:(s + 1) * neb]
-            c = lz4_block(part, max(1, 10 - clevel)) if codec != "zlib" else zlib.compress(part, clevel)
+            if codec == "zstd":  # (zstd_checksum: frames carrying XXH64 content checksums)
+                c = zstd_frame(part, clevel, zstd_checksum)
+            else:
+                c = lz4_block(part, max(1, 10 - clevel)) if codec != "zlib" else zlib.compress(part, clevel)
             if len(c) >= neb:
                 c = part
             body += len(c).to_bytes(4, "little") + c

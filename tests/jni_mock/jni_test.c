@@ -1,0 +1,281 @@
+/* jni_test.c — TEST-ONLY driver of jni/pbx_jni.c against the minimal JNI environment
+ * (jni.h here) and the scripted fake libpbx (fake_pbx.c): argument checks, error mapping,
+ * the getTile status slot, piecewise row copies.  Built and run by tests/test_jni_shim.py. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fake_pbx.h"
+#include "jni.h"
+
+#define J(name) Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_##name
+
+/* the shim's entry points (its own file has no header) */
+jlong J(createPlane)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jstring, jint, jint, jboolean, jint, jint);
+void J(writeRows)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jbyteArray, jint);
+void J(writeRowsDirect)(JNIEnv*, jclass, jlong, jlong, jint, jint, jobject);
+void J(commitPlane)(JNIEnv*, jclass, jlong, jlong);
+jint J(planeState)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint);
+jlong J(registerPlane)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jstring, jint, jint, jboolean, jbyteArray);
+jlong J(registerZarr)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jstring, jint, jint, jboolean, jint, jint,
+                      jint, jbyteArray, jlongArray, jlong);
+jbyteArray J(getTile)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jint, jint, jint, jint, jstring, jintArray);
+void J(declareImage)(JNIEnv*, jclass, jlong, jlong, jstring, jint, jint, jint, jint, jint, jint);
+
+/* ---- the mock VM: arrays, strings, direct buffers, one pending exception */
+struct mock_obj {
+    int kind;  /* 0 string, 1 byte[], 2 long[], 3 int[], 4 direct buffer, 5 class */
+    size_t len;
+    void* data;
+    const char* name;
+};
+static char pending[256];
+static int failures;
+
+#define CHECK(c)                                                        \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            failures++;                                                 \
+        }                                                               \
+    } while (0)
+
+static jclass m_FindClass(JNIEnv* e, const char* n) {
+    (void)e;
+    static struct mock_obj c[8];
+    static int k;
+    struct mock_obj* o = &c[k++ % 8];
+    o->kind = 5;
+    o->name = n;
+    return o;
+}
+static jint m_ThrowNew(JNIEnv* e, jclass c, const char* msg) {
+    (void)e;
+    snprintf(pending, sizeof pending, "%s: %s", c->name, msg);
+    return 0;
+}
+static jboolean m_ExceptionCheck(JNIEnv* e) { (void)e; return pending[0] != 0; }
+static const char* m_GetStringUTFChars(JNIEnv* e, jstring s, jboolean* c) { (void)e; (void)c; return (const char*)s->data; }
+static void m_ReleaseStringUTFChars(JNIEnv* e, jstring s, const char* p) { (void)e; (void)s; (void)p; }
+static jsize m_GetArrayLength(JNIEnv* e, jarray a) { (void)e; return (jsize)a->len; }
+static void m_GetByteArrayRegion(JNIEnv* e, jbyteArray a, jsize s, jsize n, jbyte* buf) {
+    (void)e;
+    if (s < 0 || n < 0 || (size_t)s + (size_t)n > a->len) {
+        snprintf(pending, sizeof pending, "java/lang/ArrayIndexOutOfBoundsException");
+        return;
+    }
+    memcpy(buf, (char*)a->data + s, (size_t)n);
+}
+static void m_SetByteArrayRegion(JNIEnv* e, jbyteArray a, jsize s, jsize n, const jbyte* buf) {
+    (void)e;
+    memcpy((char*)a->data + s, buf, (size_t)n);
+}
+static struct mock_obj made[16];
+static int nmade;
+static jbyteArray m_NewByteArray(JNIEnv* e, jsize n) {
+    (void)e;
+    struct mock_obj* o = &made[nmade++ % 16];
+    o->kind = 1;
+    o->len = (size_t)n;
+    o->data = calloc((size_t)n + 1, 1);
+    return o;
+}
+static jbyte* m_GetByteArrayElements(JNIEnv* e, jbyteArray a, jboolean* c) { (void)e; (void)c; return a->data; }
+static void m_ReleaseByteArrayElements(JNIEnv* e, jbyteArray a, jbyte* p, jint m) { (void)e; (void)a; (void)p; (void)m; }
+static jlong* m_GetLongArrayElements(JNIEnv* e, jlongArray a, jboolean* c) { (void)e; (void)c; return a->data; }
+static void m_ReleaseLongArrayElements(JNIEnv* e, jlongArray a, jlong* p, jint m) { (void)e; (void)a; (void)p; (void)m; }
+static jlongArray m_NewLongArray(JNIEnv* e, jsize n) {
+    (void)e;
+    struct mock_obj* o = &made[nmade++ % 16];
+    o->kind = 2;
+    o->len = (size_t)n;
+    o->data = calloc((size_t)n + 1, 8);
+    return o;
+}
+static void m_SetLongArrayRegion(JNIEnv* e, jlongArray a, jsize s, jsize n, const jlong* b) {
+    (void)e;
+    memcpy((jlong*)a->data + s, b, 8 * (size_t)n);
+}
+static void m_SetIntArrayRegion(JNIEnv* e, jintArray a, jsize s, jsize n, const jint* b) {
+    (void)e;
+    memcpy((jint*)a->data + s, b, 4 * (size_t)n);
+}
+static void* m_GetDirectBufferAddress(JNIEnv* e, jobject b) { (void)e; return b && b->kind == 4 ? b->data : NULL; }
+static jlong m_GetDirectBufferCapacity(JNIEnv* e, jobject b) { (void)e; return b && b->kind == 4 ? (jlong)b->len : -1; }
+
+static const struct JNINativeInterface_ table = {
+    m_FindClass, m_ThrowNew, m_ExceptionCheck, m_GetStringUTFChars, m_ReleaseStringUTFChars,
+    m_GetArrayLength, m_GetByteArrayRegion, m_SetByteArrayRegion, m_NewByteArray,
+    m_GetByteArrayElements, m_ReleaseByteArrayElements, m_GetLongArrayElements,
+    m_ReleaseLongArrayElements, m_NewLongArray, m_SetLongArrayRegion, m_SetIntArrayRegion,
+    m_GetDirectBufferAddress, m_GetDirectBufferCapacity};
+static JNIEnv envp = &table;
+static JNIEnv* env = &envp;
+
+static struct mock_obj str(const char* s) { struct mock_obj o = {0, strlen(s), (void*)s, NULL}; return o; }
+static struct mock_obj arr(int kind, size_t len, size_t esz) {
+    struct mock_obj o = {kind, len, calloc(len + 1, esz), NULL};
+    return o;
+}
+static void reset(void) {
+    memset(&fake, 0, sizeof fake);
+    pending[0] = 0;
+}
+static int threw(const char* cls) { return strncmp(pending, cls, strlen(cls)) == 0; }
+
+int main(void) {
+    struct mock_obj u16 = str("uint16"), png = str("png");
+    /* ---- getTile: a call-level failure (null ctx / shutdown) never releases a garbage owner */
+    {
+        reset();
+        fake.tile_rc = PBX_E_BADARG;
+        struct mock_obj so = arr(3, 3, 4);
+        jbyteArray r = J(getTile)(env, NULL, 0, 1, 0, 0, 0, -1, 0, 0, 64, 64, &png, &so);
+        CHECK(r == NULL && !pending[0]);
+        CHECK(((jint*)so.data)[2] == PBX_E_BADARG);
+        CHECK(fake.releases_results == 0);
+        reset();
+        fake.tile_rc = PBX_E_INTERNAL;
+        r = J(getTile)(env, NULL, 1, 1, 0, 0, 0, -1, 0, 0, 64, 64, &png, &so);
+        CHECK(r == NULL && threw("java/lang/RuntimeException"));
+        CHECK(fake.releases_results == 0 && ((jint*)so.data)[2] == PBX_E_INTERNAL);
+    }
+    /* ---- getTile OK: exact-length body, the post-defaulting region, one release */
+    {
+        reset();
+        static const uint8_t body[5] = {1, 2, 3, 4, 5};
+        fake.tile_fill = 1;
+        fake.tile_status = 0;
+        fake.body = body;
+        fake.body_len = 5;
+        struct mock_obj so = arr(3, 3, 4);
+        jbyteArray r = J(getTile)(env, NULL, 1, 9, 1, 2, 3, 4, 10, 20, 0, 0, &png, &so);
+        CHECK(r && r->len == 5 && memcmp(r->data, body, 5) == 0 && !pending[0]);
+        CHECK(((jint*)so.data)[0] == 512 && ((jint*)so.data)[1] == 256 && ((jint*)so.data)[2] == 0);
+        CHECK(fake.releases_results == 1 && fake.bad_release == 0);
+        CHECK(fake.last_req.image_id == 9 && fake.last_req.resolution == 4 && fake.last_req.format == PBX_FMT_PNG);
+        /* a response a Java array cannot hold: IllegalArgumentException, still released */
+        reset();
+        fake.tile_fill = 1;
+        fake.body = body;
+        fake.body_len = 0x80000000ull;
+        r = J(getTile)(env, NULL, 1, 9, 0, 0, 0, -1, 0, 0, 0, 0, NULL, &so);
+        CHECK(r == NULL && threw("java/lang/IllegalArgumentException") && fake.releases_results == 1);
+    }
+    /* ---- getTile statuses: 404 -> null, NOT_RESIDENT -> null with the status for the handler */
+    {
+        struct mock_obj so = arr(3, 3, 4);
+        int sts[2] = {PBX_E_NOTFOUND, PBX_E_NOT_RESIDENT};
+        for (int k = 0; k < 2; k++) {
+            reset();
+            fake.tile_fill = 1;
+            fake.tile_status = sts[k];
+            jbyteArray r = J(getTile)(env, NULL, 1, 9, 0, 0, 0, -1, 0, 0, 8, 8, NULL, &so);
+            CHECK(r == NULL && !pending[0] && ((jint*)so.data)[2] == sts[k] && fake.releases_results == 0);
+        }
+    }
+    /* ---- writeRows: whole-row pieces of at most 16 MiB, every row once, bounds checked */
+    {
+        reset();
+        const jint row = 65536 * 2, rows = 300;  /* 37.5 MiB */
+        struct mock_obj a = arr(1, (size_t)row * rows + 7, 1);
+        for (size_t i = 0; i < a.len; i++) ((uint8_t*)a.data)[i] = (uint8_t)(i / row);
+        J(writeRows)(env, NULL, 1, 77, 1000, rows, row, &a, 7 - 7);
+        CHECK(!pending[0]);
+        int32_t y = 1000;
+        uint64_t tot = 0;
+        for (int i = 0; i < fake.nwrites; i++) {
+            CHECK(fake.w_y0[i] == y && fake.w_bytes[i] == (uint64_t)fake.w_rows[i] * row);
+            CHECK(fake.w_bytes[i] <= (16u << 20));
+            CHECK(fake.w_first[i] == (uint8_t)(y - 1000));
+            y += fake.w_rows[i];
+            tot += fake.w_bytes[i];
+        }
+        CHECK(fake.nwrites == 3 && y == 1000 + rows && tot == (uint64_t)row * rows);
+        reset();
+        J(writeRows)(env, NULL, 1, 77, 0, rows + 1, row, &a, 0);  /* array too short */
+        CHECK(threw("java/lang/IllegalArgumentException") && fake.nwrites == 0);
+        reset();
+        fake.write_fail_at = 2;
+        J(writeRows)(env, NULL, 1, 77, 0, rows, row, &a, 0);  /* a library failure stops the copy */
+        CHECK(threw("java/lang/RuntimeException") && fake.nwrites == 2);
+        reset();
+        struct mock_obj db = {4, 4096, calloc(4096, 1), NULL};
+        J(writeRowsDirect)(env, NULL, 1, 77, 5, 2, &db);
+        CHECK(!pending[0] && fake.nwrites == 1 && fake.w_bytes[0] == 4096);
+        struct mock_obj notdirect = arr(1, 16, 1);
+        reset();
+        J(writeRowsDirect)(env, NULL, 1, 77, 5, 2, &notdirect);
+        CHECK(threw("java/lang/IllegalArgumentException"));
+    }
+    /* ---- createPlane: 409 (another loader) is 0, not an exception; 507 throws */
+    {
+        reset();
+        CHECK(J(createPlane)(env, NULL, 1, 9, 0, 1, 0, 0, &u16, 100, 200, 0, 64, 32) == 77 && !pending[0]);
+        CHECK(fake.create_y0 == 64 && fake.create_rows == 32 && fake.last_desc.pixel_type == PBX_UINT16 &&
+              fake.last_desc.byte_order == PBX_BIG_ENDIAN && fake.last_desc.source == PBX_SRC_HOST);
+        reset();
+        fake.create_rc = PBX_E_EXISTS;
+        CHECK(J(createPlane)(env, NULL, 1, 9, 0, 1, 0, 0, &u16, 100, 200, 0, 0, 0) == 0 && !pending[0]);
+        reset();
+        fake.create_rc = PBX_E_NO_SPACE;
+        CHECK(J(createPlane)(env, NULL, 1, 9, 0, 1, 0, 0, &u16, 100, 200, 0, 0, 0) == 0 &&
+              threw("java/lang/RuntimeException"));
+    }
+    /* ---- planeState, declareImage */
+    {
+        reset();
+        fake.lookup_rc = PBX_E_NOTFOUND;
+        CHECK(J(planeState)(env, NULL, 1, 9, 0, 0, 0, 0) == -1 && !pending[0]);
+        reset();
+        fake.lookup_state = 2;
+        CHECK(J(planeState)(env, NULL, 1, 9, 0, 0, 0, 0) == 2);
+        reset();
+        J(declareImage)(env, NULL, 1, 9, &u16, 10, 20, 3, 4, 5, 2);
+        CHECK(!pending[0] && fake.last_image.size_z == 3 && fake.last_image.size_c == 4 &&
+              fake.last_image.size_t_ == 5 && fake.last_image.levels == 2 && fake.last_image.pixel_type == 3);
+    }
+    /* ---- registerPlane: create + rows + commit; a failed copy releases the plane */
+    {
+        reset();
+        struct mock_obj a = arr(1, 100 * 2 * 10, 1);
+        CHECK(J(registerPlane)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 100, 10, 0, &a) == 77);
+        CHECK(!pending[0] && fake.creates == 1 && fake.nwrites == 1 && fake.commits == 1 && fake.releases == 0);
+        reset();
+        struct mock_obj small = arr(1, 100 * 2 * 10 - 1, 1);
+        CHECK(J(registerPlane)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 100, 10, 0, &small) == 0);
+        CHECK(threw("java/lang/IllegalArgumentException") && fake.creates == 0);
+        reset();
+        fake.write_fail_at = 1;
+        CHECK(J(registerPlane)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 100, 10, 0, &a) == 0);
+        CHECK(threw("java/lang/RuntimeException") && fake.commits == 0 && fake.releases == 1);
+    }
+    /* ---- registerZarr: offsets checked against both Java arrays before the call */
+    {
+        struct mock_obj chunks = arr(1, 1000, 1);
+        struct mock_obj offs = arr(2, 5, 8);  /* 2 x 2 chunks of 64 -> needs 5 entries */
+        jlong* o = offs.data;
+        o[0] = 0; o[1] = 100; o[2] = 100; o[3] = 600; o[4] = 1000;
+        reset();
+        CHECK(J(registerZarr)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 128, 128, 0, 64, 64, 1, &chunks, &offs, 0) == 55);
+        CHECK(!pending[0] && fake.zarr_calls == 1);
+        struct mock_obj shortoffs = arr(2, 4, 8);
+        reset();
+        CHECK(J(registerZarr)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 128, 128, 0, 64, 64, 1, &chunks, &shortoffs, 0) == 0);
+        CHECK(threw("java/lang/IllegalArgumentException") && fake.zarr_calls == 0);
+        o[4] = 1001;  /* past the chunk bytes */
+        reset();
+        CHECK(J(registerZarr)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 128, 128, 0, 64, 64, 1, &chunks, &offs, 0) == 0);
+        CHECK(threw("java/lang/IllegalArgumentException") && fake.zarr_calls == 0);
+        o[4] = 1000; o[2] = 50;  /* decreasing */
+        reset();
+        CHECK(J(registerZarr)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 128, 128, 0, 64, 64, 1, &chunks, &offs, 0) == 0);
+        CHECK(threw("java/lang/IllegalArgumentException") && fake.zarr_calls == 0);
+    }
+    if (failures) {
+        fprintf(stderr, "%d failures\n", failures);
+        return 1;
+    }
+    printf("jni shim ok\n");
+    return 0;
+}

@@ -677,3 +677,48 @@ def test_gpu_zlib_adler_mismatch_is_400(service):
     with pytest.raises(pbx.PbxError) as ei:
         service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 96, 64, 96, 64, "zlib", [bytes(enc)])
     assert ei.value.status == 400
+
+
+def _zstd_checksummed_chunk(seed=12):
+    """A 96 x 128 uint16 chunk as a blosc frame whose zstd streams carry the optional XXH64
+    content checksum (c-blosc writes none; libzstd, the reference path's codec, verifies it),
+    and the same chunk with the last checksum byte flipped."""
+    plane = _zarr.noise_plane(96, 128, ">u2", seed=seed) & 0x0FFF
+    enc = _zarr.blosc_encode(plane.tobytes(), 2, 5, True, "zstd", split=False, zstd_checksum=True)
+    assert enc[2] & 0x2 == 0  # compressed, not memcpyed: the last bytes are the checksum
+    bad = bytearray(enc)
+    bad[-1] ^= 0x40
+    return plane, enc, bytes(bad)
+
+
+def test_oracle_zstd_content_checksum(oracle):
+    """The oracle (libzstd) decodes checksummed zstd splits and rejects a wrong checksum."""
+    import ctypes
+    plane, enc, bad = _zstd_checksummed_chunk()
+    out = ctypes.create_string_buffer(plane.nbytes)
+    offs = (ctypes.c_uint64 * 2)(0, len(enc))
+    assert oracle.lib().pbxo_zarr_plane(1, 2, 128, 96, 128, 96, enc, offs, b"\0\0", out) == 0
+    assert out.raw == plane.tobytes()
+    offs = (ctypes.c_uint64 * 2)(0, len(bad))
+    assert oracle.lib().pbxo_zarr_plane(1, 2, 128, 96, 128, 96, bad, offs, b"\0\0", out) != 0
+
+
+@gpu
+def test_gpu_zstd_content_checksum(service):
+    """zstd frames with Content_Checksum_flag: the GPU verifies XXH64 of what it decoded
+    (as libzstd does): the intact chunk decodes exactly, a wrong checksum fails with 400."""
+    import pbx
+    plane, enc, bad = _zstd_checksummed_chunk()
+    pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 128, 96, 128, 96, "blosc", [enc])
+    assert np.array_equal(plane_be(service, pid, ">u2", 96, 128), plane)
+    service.release_plane(pid)
+    with pytest.raises(pbx.PbxError) as ei:
+        service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 128, 96, 128, 96, "blosc", [bad])
+    assert ei.value.status == 400
+    # larger frames (many 32-byte stripes, a tail) through the same check
+    big = _zarr.noise_plane(512, 512, ">u2", seed=3)
+    chunks = [_zarr.blosc_encode(c.tobytes(), 2, 3, True, "zstd", zstd_checksum=True)
+              for c in _zarr.chunk_grid(big, 256, 256)]
+    pid = service.register_zarr_plane(next(_ids), 0, 0, 0, pbx.UINT16, 512, 512, 256, 256, "blosc", chunks)
+    assert np.array_equal(plane_be(service, pid, ">u2", 512, 512), big)
+    service.release_plane(pid)
