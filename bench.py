@@ -160,6 +160,24 @@ def load_traffic(kernel):
     return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(files[-1], ROOT)
 
 
+def load_issue(kernels=("k_encode", "k_lz77")):
+    """The issue roofline of the deflate kernels from the latest committed PMC passes
+    (profiles/*pmc*/issue.json, scripts/pmc_summary.py: VALU busy = 2 cycles per wave64 VALU
+    instruction per SIMD-cycle, SALU busy = 1 per CU-cycle, wave-time split), same workload."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "issue.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    out = {k: t["kernels"][k] for k in kernels if k in t.get("kernels", {})}
+    if not out:
+        return None
+    out["source"] = os.path.relpath(files[-1], ROOT)
+    out["rule"] = t.get("rule")
+    return out
+
+
 def cpu_baseline(seconds=10.0, threads=16):
     """The C oracle (zlib-6 filter-None PNG, same region extraction) on host threads."""
     import _oracle as O
@@ -786,7 +804,8 @@ def main():
                      "alg_bytes_per_launch": int(dom_bytes),
                      "note": "deflate kernels are VALU-issue/latency-bound integer work, not "
                              "HBM-bound; the HBM-bound extraction kernel (k_extract) is in "
-                             "raw_4096x512x512_u16"},
+                             "raw_4096x512x512_u16; their issue roofline is in `issue`",
+                     "issue": load_issue()},
         "kernels": kernels,
         "deflate_chain_ms": round(chain_ms, 3),
         "hbm_gbps_step": round((st.in_bytes + st.deflate_out_bytes) * world * args.steps / dt / 1e9, 1),

@@ -251,7 +251,10 @@ struct pbx_batch {
          *d_info = nullptr, *d_hist = nullptr, *d_mrec = nullptr, *d_codes = nullptr,
          *d_sizes = nullptr, *d_offs = nullptr, *d_png = nullptr, *d_stamps = nullptr,
          *d_segmap = nullptr, *d_blk = nullptr, *d_th = nullptr;
-    void* h_desc = nullptr;  // pinned staging for descriptors
+    void* h_desc = nullptr;  // pinned staging for descriptors (+ the tile offsets read back)
+    uint64_t* h_offs_pin = nullptr;  // in h_desc: the deflate tiles' output offsets, D2H'd by the
+    bool offs_ready = false;         // kernel stream at the end of a launch that will be fetched
+    hipEvent_t ev_copy = nullptr;    // the fetch's D2H on the copy stream
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
     bool launched = false;
@@ -560,7 +563,7 @@ void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
 
 }  // namespace
 
-static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap);
+static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_follows);
 
 // One synchronous batch: plan + launch under run_mu (launches stay in order on the
 // kernel stream), then the fetch outside it, so that concurrent callers overlap one
@@ -573,7 +576,7 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
         std::lock_guard<std::mutex> run(ctx->run_mu);
         st = pbx_batch_plan(ctx, reqs, n, &b);
         if (st) return st;
-        st = batch_launch(ctx, b, false);
+        st = batch_launch(ctx, b, false, true);
     }
     ctx->n_batches++;
     ctx->n_requests += n;
@@ -602,8 +605,9 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
 // (PixelBufferMicroserviceVerticle.java:117-118,224-233; PixelBufferVerticle.java:109-110).
 // Callers block as before; a launcher thread turns every request queued while the GPU is
 // busy into ONE batch (no fixed time window: an idle GPU takes a lone request at once),
-// with at most DEPTH batches in flight, and a completer thread fetches finished batches
-// (D2H on the copy stream) and wakes their callers.
+// with at most DEPTH batches in flight, and completer threads ($PBX_COMPLETERS, default 2)
+// fetch finished batches (D2H on the copy stream, the copies of two batches queued back to
+// back) and wake their callers.
 struct Coalescer {
     static constexpr size_t MAX_BATCH = 1 << 16;
     struct Pending {
@@ -634,12 +638,15 @@ struct Coalescer {
     std::deque<Flight> flights;
     int inflight = 0;
     bool stop = false;
-    std::thread launcher, completer;
+    std::thread launcher;
+    std::vector<std::thread> completers;
 
     explicit Coalescer(pbx_ctx* c) : ctx(c) {
         if (const char* d = getenv("PBX_COALESCE_DEPTH")) depth = std::min(8, std::max(1, atoi(d)));
+        int nc = 2;
+        if (const char* c = getenv("PBX_COMPLETERS")) nc = std::min(8, std::max(1, atoi(c)));
         launcher = std::thread([this] { launch_loop(); });
-        completer = std::thread([this] { complete_loop(); });
+        for (int k = 0; k < nc; k++) completers.emplace_back([this] { complete_loop(); });
     }
     ~Coalescer() {
         {
@@ -649,7 +656,7 @@ struct Coalescer {
         cv_launch.notify_all();
         cv_complete.notify_all();
         launcher.join();
-        completer.join();
+        for (auto& t : completers) t.join();
     }
     int submit(const pbx_tile_req& r, pbx_result* out) {
         Pending p;
@@ -683,7 +690,7 @@ struct Coalescer {
             {
                 std::lock_guard<std::mutex> run(ctx->run_mu);
                 f.rc = pbx_batch_plan(ctx, reqs.data(), reqs.size(), &f.b);
-                if (f.rc == PBX_OK) f.rc = batch_launch(ctx, f.b, false);
+                if (f.rc == PBX_OK) f.rc = batch_launch(ctx, f.b, false, true);
                 if (f.rc != PBX_OK) f.err = g_err;
             }
             ctx->n_batches++;
@@ -741,6 +748,7 @@ struct Coalescer {
                 inflight--;
             }
             cv_launch.notify_one();
+            cv_complete.notify_all();  // (shutdown: the other completers see inflight == 0)
         }
     }
 };
@@ -1928,13 +1936,16 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
 int pbx_batch_launch(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     std::lock_guard<std::mutex> run(ctx->run_mu);  // launches (and the stream turn) in order
-    return batch_launch(ctx, b, true);
+    return batch_launch(ctx, b, true, false);
 }
 
 // overlap: the caller pipelines batches (pbx_batch_launch, pbx_submit), so a batch with
 // deflate work goes to the next of the kernel streams, staggered behind the previous one;
 // otherwise (synchronous calls, the coalescer, raw/TIFF-only batches) it runs on `stream`.
-static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
+// fetch_follows: the results go to the host (pbx_batch_fetch): the tile offsets are read back
+// by the kernel stream itself at the end of the launch, so the fetch needs no round trip for
+// them before its data copy (the served path's per-batch latency).
+static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_follows) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     hipError_t err = hipSuccess;
@@ -1946,9 +1957,11 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     const uint32_t nft = (uint32_t)b->ft.size(), ndt = (uint32_t)b->dt.size(), nth = (uint32_t)b->th.size();
     const size_t ft_bytes = nft * sizeof(TileDesc), dt_bytes = ndt * sizeof(TileDesc),
                  th_bytes = nth * sizeof(TiledHdr);
+    const size_t offs_at = (ft_bytes + dt_bytes + th_bytes + 15) & ~(size_t)15;
     if (!b->h_desc) {
-        b->h_desc = ctx->hpool.get(ft_bytes + dt_bytes + th_bytes + 256, &err);
+        b->h_desc = ctx->hpool.get(offs_at + (ndt + 1) * sizeof(uint64_t) + 256, &err);
         if (!b->h_desc) return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
+        b->h_offs_pin = (uint64_t*)((uint8_t*)b->h_desc + offs_at);
         if (nft) memcpy(b->h_desc, b->ft.data(), ft_bytes);
         if (ndt) memcpy((uint8_t*)b->h_desc + ft_bytes, b->dt.data(), dt_bytes);
         if (nth) memcpy((uint8_t*)b->h_desc + ft_bytes + dt_bytes, b->th.data(), th_bytes);
@@ -2025,6 +2038,10 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap) {
     }
     HIP_TRY(launch_tiff_tiled(st, (const TiledHdr*)b->d_th, nth, (uint8_t*)b->d_fixed, (const uint64_t*)b->d_offs,
                               (uint8_t*)b->d_png));
+    if (fetch_follows && ndt) {
+        HIP_TRY(hipMemcpyAsync(b->h_offs_pin, b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        b->offs_ready = true;
+    }
     HIP_TRY(hipEventRecord(b->ev[8], st));
     b->launched = true;
     return PBX_OK;
@@ -2116,10 +2133,12 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     // Wait for this batch only (later batches may already run on the kernel stream) and
     // copy on the copy stream, so the D2H overlaps the next batch's kernels.
     HIP_TRY(hipEventSynchronize(b->ev[8]));
-    std::lock_guard<std::mutex> cg(ctx->copy_mu);
     const uint32_t ndt = (uint32_t)b->dt.size();
     b->h_offs.assign(ndt + 1, 0);
-    if (ndt) {
+    if (ndt && b->offs_ready) {
+        memcpy(b->h_offs.data(), b->h_offs_pin, (ndt + 1) * sizeof(uint64_t));  // read back at launch
+    } else if (ndt) {
+        std::lock_guard<std::mutex> cg(ctx->copy_mu);
         HIP_TRY(hipMemcpyAsync(b->h_offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t),
                                hipMemcpyDeviceToHost, ctx->copy_stream));
         HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
@@ -2134,12 +2153,27 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
         return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
     }
     uint8_t* h = (uint8_t*)hb->pinned;
-    if (b->fixed_bytes)
-        HIP_TRY(hipMemcpyAsync(h, b->d_fixed, b->fixed_bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
-    if (png_total)
-        HIP_TRY(hipMemcpyAsync(h + b->fixed_bytes, b->d_png, png_total, hipMemcpyDeviceToHost,
-                               ctx->copy_stream));
-    HIP_TRY(hipStreamSynchronize(ctx->copy_stream));
+    auto fail_hb = [&](hipError_t e) {
+        ctx->hpool.put(hb->pinned);
+        delete hb;
+        return fail(PBX_E_INTERNAL, "fetch: %s", hipGetErrorString(e));
+    };
+    if (!b->ev_copy) {
+        const hipError_t e = hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming);
+        if (e != hipSuccess) return fail_hb(e);
+    }
+    {   // the copies are queued back to back on the copy stream (several completers may have
+        // theirs in flight: the link never waits for a host round trip); the wait is outside
+        std::lock_guard<std::mutex> cg(ctx->copy_mu);
+        hipError_t e = hipSuccess;
+        if (b->fixed_bytes)
+            e = hipMemcpyAsync(h, b->d_fixed, b->fixed_bytes, hipMemcpyDeviceToHost, ctx->copy_stream);
+        if (e == hipSuccess && png_total)
+            e = hipMemcpyAsync(h + b->fixed_bytes, b->d_png, png_total, hipMemcpyDeviceToHost, ctx->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(b->ev_copy, ctx->copy_stream);
+        if (e != hipSuccess) return fail_hb(e);
+    }
+    if (const hipError_t e = hipEventSynchronize(b->ev_copy)) return fail_hb(e);
     int refs = 0;
     for (size_t k = 0; k < b->ft.size(); k++) {
         const TileDesc& d = b->ft[k];
@@ -2185,10 +2219,12 @@ void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
     (void)hipSetDevice(ctx->device);
     if (b->launched) (void)hipEventSynchronize(b->ev[8]);
     else if (b->attempted) (void)sync_kernel_streams(ctx);  // a launch that failed midway
+    if (b->ev_copy) (void)hipEventSynchronize(b->ev_copy);
     batch_unpin(ctx, b);
     free_batch_device(ctx, b);
     for (auto& e : b->ev)
         if (e) (void)hipEventDestroy(e);
+    if (b->ev_copy) (void)hipEventDestroy(b->ev_copy);
     delete b;
 }
 
@@ -2227,7 +2263,7 @@ int pbx_submit(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* o
         std::lock_guard<std::mutex> run(ctx->run_mu);
         st = pbx_batch_plan(ctx, reqs, n, &b);
         if (st) return st;
-        st = batch_launch(ctx, b, true);
+        st = batch_launch(ctx, b, true, true);
     }
     ctx->n_batches++;
     ctx->n_requests += n;

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc0 -o run --output-format csv -- python3 scripts/prof_workload.py noise 3 > gpurun_out/pmc0.log 2>&1 || { echo pass0 FAIL; tail -20 gpurun_out/pmc0.log; exit 1; }
 PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT -d gpurun_out/pmc1 -o run --output-format csv -- python3 scripts/prof_workload.py noise 2 > gpurun_out/pmc1.log 2>&1 || { echo pass1 FAIL; tail -20 gpurun_out/pmc1.log; exit 1; }
-PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d gpurun_out/pmc2 -o run --output-format csv -- python3 scripts/prof_workload.py noise 2 > gpurun_out/pmc2.log 2>&1 || { echo pass2 FAIL; tail -20 gpurun_out/pmc2.log; exit 1; }
+PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc2 -o run --output-format csv -- python3 scripts/prof_workload.py noise 2 > gpurun_out/pmc2.log 2>&1 || { echo pass2 FAIL; tail -20 gpurun_out/pmc2.log; exit 1; }
 PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc3 -o run --output-format csv -- python3 scripts/prof_workload.py noise 2 > gpurun_out/pmc3.log 2>&1 || { echo pass3 FAIL; tail -20 gpurun_out/pmc3.log; exit 1; }
 PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc4 -o run --output-format csv -- python3 scripts/prof_workload.py noise 2 > gpurun_out/pmc4.log 2>&1 || { echo pass4 FAIL; tail -20 gpurun_out/pmc4.log; exit 1; }
 echo all passes ok
