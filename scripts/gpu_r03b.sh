@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo tests ok || { echo tests FAIL; tail -60 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo tests ok || { echo tests FAIL; tail -60 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
 timeout -k 10 200 python -u scripts/filter_bench.py > $O/filter3.txt 2>&1 && cat $O/filter3.txt || { echo filter FAIL; tail -20 $O/filter3.txt; exit 1; }
 for nc in 1 2; do

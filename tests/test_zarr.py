@@ -683,7 +683,7 @@ def _zstd_checksummed_chunk(seed=12):
     """A 96 x 128 uint16 chunk as a blosc frame whose zstd streams carry the optional XXH64
     content checksum (c-blosc writes none; libzstd, the reference path's codec, verifies it),
     and the same chunk with the last checksum byte flipped."""
-    plane = _zarr.noise_plane(96, 128, ">u2", seed=seed) & 0x0FFF
+    plane = (_zarr.noise_plane(96, 128, ">u2", seed=seed) & 0x0FFF).astype(">u2")  # (& gives native order)
     enc = _zarr.blosc_encode(plane.tobytes(), 2, 5, True, "zstd", split=False, zstd_checksum=True)
     assert enc[2] & 0x2 == 0  # compressed, not memcpyed: the last bytes are the checksum
     bad = bytearray(enc)
