@@ -12,3 +12,4 @@ timeout -k 10 200 python -u scripts/filter_bench.py > $O/filter3.txt 2>&1 && cat
 for nc in 1 2; do
 PBX_COMPLETERS=$nc timeout -k 10 300 python -u scripts/serve_sweep.py 3,4 > $O/serve_c$nc.json 2> $O/serve_c$nc.err && echo "completers $nc" && cat $O/serve_c$nc.json || { echo serve FAIL; tail -20 $O/serve_c$nc.err; exit 1; }
 done
+VARIANT_GENS=noise timeout -k 10 400 bash scripts/variants.sh > $O/variants.txt 2>&1 && cat $O/variants.txt || { echo variants FAIL; tail -20 $O/variants.txt; exit 1; }
