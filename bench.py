@@ -490,6 +490,8 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 "tiles_per_s": round(len(ctxs) * 3 * world / dt, 1),
                 **wall_vs_kernels(dt, 3, st),
                 "k_filter_ms": round(mean(st, "ms_filter"), 3),
+                "k_filter_frac": round((st[-1].in_bytes + st[-1].stream_bytes) / (mean(st, "ms_filter") * 1e-3)
+                                       / 1e9 / HBM_PEAK_GBPS, 4),
                 "deflate_chain_ms": round(mean(st, "ms_deflate") + mean(st, "ms_assemble"), 3),
                 "sample_bytes_per_tile": {"adaptive": round(sum(map(len, png_ad)) / 8, 1),
                                           "filter_none": round(sum(map(len, png_no)) / 8, 1),
@@ -497,6 +499,28 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
             for s_, h in held:
                 s_.release_plane(h)
     svc.release_cached()
+    return out
+
+
+def fixed_filter_line(rank, world, barrier, side):
+    """PNG with one fixed filter for every row (cfg.png_filter = Sub / Up / Avg / Paeth:
+    k_filter3), the headline's 4096 G_NOISE tiles, one kernel stream (k_filter_ms is the
+    kernel's own HIP-event time).  Algorithmic bytes = the tiles read + the filtered stream
+    written; gbps / frac against the 8 TB/s HBM peak."""
+    out = {}
+    for f, name in ((1, "sub"), (2, "up"), (3, "avg"), (4, "paeth")):
+        with pbx.PixelsService(device=torch.cuda.current_device(), png_filter=f) as sf:
+            sf.set_kernel_streams(1, 0)
+            sf.register_plane(45, 0, 0, 0, pbx.UINT16, side, side, generator="noise", plane_no=rank)
+            ctxs = grid_ctxs(45, "png")
+            dt, st, _ = secondary_steps(sf, ctxs, 3, 1, barrier)
+            ms = mean(st, "ms_filter")
+            alg = st[-1].in_bytes + st[-1].stream_bytes
+            out[name] = {"tiles_per_s": round(len(ctxs) * 3 * world / dt, 1), **wall_vs_kernels(dt, 3, st),
+                         "k_filter_ms": round(ms, 3), "k_filter_alg_bytes": alg,
+                         "k_filter_gbps": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "k_filter_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "compressed_bytes_per_tile": round(st[-1].deflate_out_bytes / len(ctxs), 1)}
     return out
 
 
@@ -572,6 +596,8 @@ def extra(out, svc, rank, world, barrier, iid, side):
     # the adaptive PNG filter (option; the reference writes filter None)
     progress(rank, "adaptive filter")
     out["png_adaptive_filter_512x512_u16"] = adaptive_filter_line(svc, rank, world, barrier, side)
+    progress(rank, "fixed filters")
+    out["png_fixed_filter_4096x512x512_u16"] = fixed_filter_line(rank, world, barrier, side)
     # configs[2]: 4096 x 1024^2 uint16 PNG from a 65536^2 plane (8 GiB)
     progress(rank, "configs[2]")
     svc.register_plane(3, 0, 0, 0, pbx.UINT16, 65536, 65536, generator="noise", plane_no=rank)

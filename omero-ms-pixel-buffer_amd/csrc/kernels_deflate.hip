@@ -727,8 +727,16 @@ __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, c
 // parsed -- needed more registers than 8 waves per SIMD allow and spilled; the fill is
 // issue-bound rather than latency-bound anyway: the same cycles with every plane read a cache
 // hit, profiles/r01_s4_phase_direct_sametile.log.)
+#ifndef PBX_LZ_MINB  // experiments only: the min-blocks launch bound of k_lz77 (0 = none)
+#define PBX_LZ_MINB 8
+#endif
+#if PBX_LZ_MINB
+#define PBX_LZ_BOUNDS __launch_bounds__(C::NT, PBX_LZ_MINB)
+#else
+#define PBX_LZ_BOUNDS __launch_bounds__(C::NT)
+#endif
 template <class C, bool PROF>
-__global__ __launch_bounds__(C::NT, 8) void k_lz77(const TileDesc* __restrict__ dt,
+__global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,

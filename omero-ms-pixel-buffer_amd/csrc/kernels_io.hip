@@ -545,14 +545,19 @@ __device__ __forceinline__ f2_s16x2 f2_abs(f2_s16x2 x) {
     const f2_s16x2 m = x >> 15;
     return (x ^ m) - m;
 }
-// PNG Paeth predictor of two 16-bit lanes holding bytes (a = left, b = up, c = up-left)
+// PNG Paeth predictor of two 16-bit lanes holding bytes (a = left, b = up, c = up-left), all
+// packed arithmetic: pa = |b - c|, pb = |a - c|, pc = |a + b - 2c| (<= 510), and the choice
+// (a if pa <= min(pb, pc), else b if pb <= pc, else c) from the signs of two differences.
 __device__ __forceinline__ uint32_t paeth_pair(uint32_t a, uint32_t b, uint32_t c) {
     const f2_s16x2 A = __builtin_bit_cast(f2_s16x2, a), B = __builtin_bit_cast(f2_s16x2, b),
-                   Cc = __builtin_bit_cast(f2_s16x2, c);
-    const f2_s16x2 pa = f2_abs(B - Cc), pb = f2_abs(A - Cc), pc = f2_abs(A + B - Cc - Cc);
-    const f2_s16x2 m1 = (pa <= pb) & (pa <= pc), m2 = pb <= pc;  // -1 / 0 per lane
-    const f2_s16x2 r = (m1 & A) | (~m1 & ((m2 & B) | (~m2 & Cc)));
-    return __builtin_bit_cast(uint32_t, r);
+                   C = __builtin_bit_cast(f2_s16x2, c);
+    const f2_s16x2 d1 = B - C, d2 = A - C, d3 = d1 + d2;
+    const f2_s16x2 pa = __builtin_elementwise_max(d1, -d1), pb = __builtin_elementwise_max(d2, -d2),
+                   pc = __builtin_elementwise_max(d3, -d3);
+    const uint32_t na = __builtin_bit_cast(uint32_t, (f2_s16x2)((__builtin_elementwise_min(pb, pc) - pa) >> 15));
+    const uint32_t nb = __builtin_bit_cast(uint32_t, (f2_s16x2)((pc - pb) >> 15));  // -1: pb > pc
+    const uint32_t t = (nb & c) | (~nb & b);
+    return (na & t) | (~na & a);  // na = -1: pa > min(pb, pc)
 }
 __device__ __forceinline__ uint32_t paeth4(uint32_t l, uint32_t u, uint32_t ul) {
     const uint32_t lo = paeth_pair(l & 0x00FF00FFu, u & 0x00FF00FFu, ul & 0x00FF00FFu);
@@ -722,16 +727,43 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // row's tail and the filter byte.  That word needs the previous row's filtered tail, so a run
 // also filters the row before it (without storing it): 1/F3_RUN extra reads, no cross-wave
 // hand-off.
-constexpr uint32_t F3_RUN = 32;
+#ifndef PBX_F3_RUN
+#define PBX_F3_RUN 32
+#endif
+#ifndef PBX_F3_NTS
+#define PBX_F3_NTS 0
+#endif
+constexpr uint32_t F3_RUN = PBX_F3_RUN;
+// stream stores: nontemporal (the stream is re-read only by the next kernel, from HBM anyway)
+__device__ __forceinline__ void f3_store(uint8_t* p, const uint4& v) {
+    if (PBX_F3_NTS) {
+        pbx_v4u x;
+        x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+        __builtin_nontemporal_store(x, (__attribute__((address_space(1))) pbx_v4u*)p);
+    } else {
+        gstore16(p, v);
+    }
+}
 constexpr uint32_t F3_NT = 256;
+// row buffers per wave (up, cur and NB - 2 loads in flight), by the registers the variant has
+#ifndef PBX_F3_NB
+#define PBX_F3_NB 0
+#endif
+template <uint32_t G, bool ADAPTIVE>
+constexpr uint32_t F3_NB() {
+    return PBX_F3_NB ? PBX_F3_NB : G == 1 ? (ADAPTIVE ? 5 : 6) : 4;
+}
 
+// Sum over the wave: row prefix sums (row_shr, zero shifted in), then row_bcast:15 / :31 carry
+// the row totals up to lane 63.  bound_ctrl lets each step fold into one v_add_u32_dpp.
 __device__ __forceinline__ uint32_t f3_wave_sum(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
-           (uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 // The previous lane's chunk (wave shift right by one lane); lane 0 gets `first`.
 __device__ __forceinline__ uint4 f3_prev_lane(const uint4& x, const uint4& first) {
@@ -739,6 +771,13 @@ __device__ __forceinline__ uint4 f3_prev_lane(const uint4& x, const uint4& first
                       (uint32_t)__builtin_amdgcn_update_dpp((int)first.y, (int)x.y, 0x138, 0xF, 0xF, false),
                       (uint32_t)__builtin_amdgcn_update_dpp((int)first.z, (int)x.z, 0x138, 0xF, 0xF, false),
                       (uint32_t)__builtin_amdgcn_update_dpp((int)first.w, (int)x.w, 0x138, 0xF, 0xF, false));
+}
+// The same with zero into lane 0 (bound_ctrl: no old value to set up)
+__device__ __forceinline__ uint4 f3_prev_lane0(const uint4& x) {
+    return make_uint4((uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.x, 0x138, 0xF, 0xF, true),
+                      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.y, 0x138, 0xF, 0xF, true),
+                      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.z, 0x138, 0xF, 0xF, true),
+                      (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.w, 0x138, 0xF, 0xF, true));
 }
 __device__ __forceinline__ uint4 f3_readlane(const uint4& x, uint32_t l) {
     return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)x.x, l), (uint32_t)__builtin_amdgcn_readlane((int)x.y, l),
@@ -779,11 +818,13 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
     const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x) * (F3_NT / 64) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wi >= nwaves) return;  // a whole wave: no barrier in this kernel
-    const uint32_t ti = upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
     const TileDesc d = dt[ti];
     const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
     const uint32_t h = (uint32_t)d.h;
-    const uint32_t r0 = (wi - d.blk_first) * F3_RUN, r1 = r0 + F3_RUN < h ? r0 + F3_RUN : h;
+    // uniform row bounds: the row loop and its prefetch stay scalar branches
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane((wi - d.blk_first) * F3_RUN);
+    const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + F3_RUN < h ? r0 + F3_RUN : h);
     const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
     const uint32_t fixed = (uint32_t)d.filter;  // 1..4 (ADAPTIVE: 5)
     const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
@@ -807,28 +848,17 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
         }
     };
     const uint32_t rs = r0 ? r0 - 1 : 0;  // first row filtered (the one before the run: not stored)
-    // rows in registers: up (r - 1), cur (r), and the loads of rows r + 1, r + 2 in flight
-    uint4 up[G], cur[G], n1[G], n2[G];
-#pragma unroll
-    for (uint32_t g = 0; g < G; g++) up[g] = n1[g] = n2[g] = Z;
-    if (rs) load_row(rs - 1, up);
-    load_row(rs, cur);
-    if (rs + 1 < r1) load_row(rs + 1, n1);
-    if (rs + 2 < r1) load_row(rs + 2, n2);
-    if (rs) conv(up);
+    const uint32_t rl = r1 - 1;
     uint4 tail = Z;  // the previous row's last filtered chunk (uniform)
     const uint32_t cl = nc - 1, gl = cl >> 6, ll = cl & 63;
-    for (uint32_t r = rs; r < r1; r++) {
-        uint4 n3[G];
-#pragma unroll
-        for (uint32_t g = 0; g < G; g++) n3[g] = Z;
-        if (r + 3 < r1) load_row(r + 3, n3);  // three rows ahead in flight
+    // filter row r (cur, converted here) against up (already converted) and store it
+    auto step = [&](const uint4 (&up)[G], uint4 (&cur)[G], uint32_t r) {
         conv(cur);
         uint4 lft[G], ul[G];
 #pragma unroll
         for (uint32_t g = 0; g < G; g++) {
-            lft[g] = f3_prev_lane(cur[g], g ? f3_readlane(cur[g - 1], 63) : Z);
-            ul[g] = f3_prev_lane(up[g], g ? f3_readlane(up[g - 1], 63) : Z);
+            lft[g] = g ? f3_prev_lane(cur[g], f3_readlane(cur[g - 1], 63)) : f3_prev_lane0(cur[g]);
+            ul[g] = g ? f3_prev_lane(up[g], f3_readlane(up[g - 1], 63)) : f3_prev_lane0(up[g]);
         }
         uint4 f[G];
         uint32_t ft = fixed;
@@ -923,27 +953,47 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
                     funnel16(pf, f[g], 16 - s, ww);
                     wv = make_uint4(ww[0], ww[1], ww[2], ww[3]);
                 }
-                if (c < nc) gstore16(out + A + 16 * c, wv);
+                if (c < nc) f3_store(out + A + 16 * c, wv);
             }
-            if (s == 0 && lane == 0) gstore16(out + A - 16, y);  // (r > 0: s == 1 at r == 0)
+            if (s == 0 && lane == 0) f3_store(out + A - 16, y);  // (r > 0: s == 1 at r == 0)
             if (r + 1 == h && s) {  // the tile's last row: its tail word (zeros after the stream)
                 const uint4 fl = f3_pick(f, gl);
                 if (lane == ll) {
                     uint32_t ww[4];
                     funnel16(fl, Z, 16 - s, ww);
-                    gstore16(out + A + 16 * nc, make_uint4(ww[0], ww[1], ww[2], ww[3]));
+                    f3_store(out + A + 16 * nc, make_uint4(ww[0], ww[1], ww[2], ww[3]));
                 }
             }
         }
         tail = f3_readlane(f3_pick(f, gl), ll);
+    };
+    // A ring of NB row buffers, rotated by NAME (the loop is unrolled NB times): B[k] = up,
+    // B[k + 1] = cur, the other NB - 2 = loads in flight.  Moving registers that a load is still
+    // filling would make the compiler wait for every load (vmcnt(0)) each row; loads are
+    // unconditional (clamped to the run's last row) so the counters stay exact.
+    constexpr uint32_t NB = F3_NB<G, ADAPTIVE>();
+    uint4 B[NB][G];
+    load_row(rs ? rs - 1 : 0, B[0]);
 #pragma unroll
-        for (uint32_t g = 0; g < G; g++) {
-            up[g] = cur[g];
-            cur[g] = n1[g];
-            n1[g] = n2[g];
-            n2[g] = n3[g];
+    for (uint32_t k = 1; k < NB; k++) load_row(rs + k - 1 < rl ? rs + k - 1 : rl, B[k]);
+    conv(B[0]);
+    if (!rs) {
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) B[0][g] = Z;
+    }
+    const uint32_t nrow = r1 - rs, nfull = nrow - nrow % NB;
+    uint32_t r = rs;
+    for (; r < rs + nfull; r += NB) {
+#pragma unroll
+        for (uint32_t k = 0; k < NB; k++) {
+            step(B[k], B[(k + 1) % NB], r + k);
+            const uint32_t rn = r + k + NB - 1;
+            load_row(rn < rl ? rn : rl, B[k]);
         }
     }
+#pragma unroll
+    for (uint32_t k = 0; k + 1 < NB; k++)  // the last nrow % NB rows: already loaded
+        if (r + k < r1) step(B[k], B[(k + 1) % NB], r + k);
 }
 
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
