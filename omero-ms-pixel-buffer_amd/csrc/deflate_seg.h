@@ -55,6 +55,7 @@ struct DeflateCfg {
     static constexpr int NW = NT / 64;    // waves
     static constexpr int SUB = SEG / NW;  // positions parsed by one wave
     static constexpr int MAXMW = 256;     // matches kept per wave (then literals only)
+    static constexpr int MINCOV = 32;     // a wave keeps its matches only if they cover >= MINCOV bytes
     static constexpr int CAP = PBX_CAP;   // match length found by the masks before the wave extends it
     static constexpr int CRCC = 32;       // CRC chunk bytes per thread (thread 0: the rest too)
     static constexpr int LOG2_CRCC = 5;
@@ -220,7 +221,7 @@ template <class C, class SM>
 PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
     const uint32_t ss = w * C::SUB;
     const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
-    uint32_t nm = 0, p = ss;
+    uint32_t nm = 0, p = ss, cov = 0;
     while (p < se) {
         uint32_t L, D, L1, D1;
         best_match<C>(S, sp, p, se, L, D);
@@ -232,10 +233,14 @@ PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
             S.mpos[w * C::MAXMW + nm] = p | ((L - 3) << 16);
             S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
             nm++;
+            cov += L;
         }
         p += L;
     }
-    S.w_nm[w] = nm;
+    // Matches covering fewer than MINCOV of the sub-segment's bytes (noise: a few 3-byte
+    // runs, < 0.1% smaller) are dropped: the wave is then coded as literals only, which the
+    // encoder does at half the cost (k_encode's literal-only path).
+    S.w_nm[w] = cov < (uint32_t)C::MINCOV ? 0u : nm;
 }
 
 // Emit this thread's chunk of tokens in stream order: matches starting in the chunk

@@ -494,6 +494,109 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
     for (uint32_t k = nb4 / 4 + tid; k < nz / 4; k += NT) buf[k] = 0;
 }
 
+// The common geometry, without per-task bookkeeping: rows of whole 16-byte chunks, at most
+// 64 chunks (one wave per row), the sample conversion fixed at compile time (SB: bytes per
+// swapped sample, 0 = none; FL: the PNG sign flip).  Wave w fills rows w, w + NW, ... of the
+// buffer, FR rows' loads in flight together; every lane also loads the row above's last
+// chunk (one address for the whole wave), so rows need nothing from each other.  Row r's
+// lane l stores the aligned word ending where its chunk's first 16 - s bytes end (s = the
+// row's start mod 16), lane 0's word holding the row above's tail and the filter byte (the
+// layout fill_stores writes); the buffer's last row writes its own tail.  Only rows that
+// cross the buffer's ends clip per lane.
+template <int NT, uint32_t SB, bool FL>
+__device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb, uint32_t nz,
+                          uint32_t tid, uint32_t ra, uint32_t rz) {
+    constexpr uint32_t NW = NT / 64, FR = 2;
+    uint8_t* bb = (uint8_t*)buf;
+    const uint32_t lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t nc = dr.nc, fb = dr.fb, rowlen = dr.rowlen, nrows = rz - ra + 1;
+    const uint32_t flipm = dr.bpp == 1 ? 0x80808080u : 0x00800080u;
+    const uint4 Z = make_uint4(0, 0, 0, 0);
+    auto conv = [&](uint4 v) {
+        if (SB) v = swap16(v, (int)SB);
+        if (FL) { v.x ^= flipm; v.y ^= flipm; v.z ^= flipm; v.w ^= flipm; }
+        return v;
+    };
+    // one 16-byte word at buffer byte `at` (aligned): skipped outside [0, nb), zero past nb
+    auto put = [&](int32_t at, uint4 v) {
+        if (at < 0 || at >= (int32_t)nb) return;
+        if (at + 16 > (int32_t)nb) {
+            const uint32_t keep = (uint32_t)((int32_t)nb - at);
+            uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const int32_t kb = (int32_t)keep - 4 * (int32_t)q;
+                const uint32_t nbits = kb <= 0 ? 0u : kb >= 4 ? 32u : 8u * (uint32_t)kb;
+                ww[q] &= (uint32_t)((1ull << nbits) - 1ull);
+            }
+            v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+        }
+        *(uint4*)(bb + at) = v;
+    };
+    for (uint32_t i0 = w; i0 < nrows; i0 += NW * FR) {
+        uint4 x[FR], pl[FR];
+#pragma unroll
+        for (uint32_t j = 0; j < FR; j++) {  // unconditional loads (clamped row): exact counters
+            const uint32_t i = i0 + NW * j;
+            const uint32_t r = ra + (i < nrows ? i : i0);
+            const uint8_t* rp = dr.row0 + (int64_t)r * dr.pitch;
+            x[j] = gload16(rp + 16 * (lane < nc ? lane : 0u));
+            pl[j] = gload16(r ? rp - dr.pitch + 16 * (nc - 1) : rp);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < FR; j++) {
+            const uint32_t i = i0 + NW * j;
+            if (i >= nrows) break;  // uniform
+            const uint32_t r = ra + i;
+            const uint4 xc = conv(x[j]);
+            uint4 y = r ? conv(pl[j]) : Z;  // the row above's last chunk
+            if (fb)  // its last 15 bytes, then the filter byte (0)
+                y = make_uint4((y.x >> 8) | (y.y << 24), (y.y >> 8) | (y.z << 24), (y.z >> 8) | (y.w << 24), y.w >> 8);
+            uint4 pv;  // the previous lane's chunk; lane 0: y
+            pv.x = (uint32_t)__builtin_amdgcn_update_dpp((int)y.x, (int)xc.x, 0x138, 0xF, 0xF, false);  // wave_shr:1
+            pv.y = (uint32_t)__builtin_amdgcn_update_dpp((int)y.y, (int)xc.y, 0x138, 0xF, 0xF, false);
+            pv.z = (uint32_t)__builtin_amdgcn_update_dpp((int)y.z, (int)xc.z, 0x138, 0xF, 0xF, false);
+            pv.w = (uint32_t)__builtin_amdgcn_update_dpp((int)y.w, (int)xc.w, 0x138, 0xF, 0xF, false);
+            const int32_t q0 = (int32_t)(r * rowlen + fb) - (int32_t)B;
+            const uint32_t sft = (uint32_t)q0 & 15u;
+            const int32_t A = q0 - (int32_t)sft;
+            const uint4 wv = funnel16(pv, xc, sft);
+            const bool last = r == rz && sft;  // the buffer's last row writes its own tail
+            if (A >= 16 && A + 16 * (int32_t)(nc + 1) <= (int32_t)nb) {  // uniform: no clipping
+                if (lane < nc) *(uint4*)(bb + A + 16 * (int32_t)lane) = wv;
+                if (lane == 0 && fb && sft == 0) *(uint4*)(bb + A - 16) = pv;
+                if (lane == nc - 1 && last) *(uint4*)(bb + A + 16 * (int32_t)nc) = funnel16(xc, Z, sft);
+            } else {
+                if (lane < nc) put(A + 16 * (int32_t)lane, wv);
+                if (lane == 0 && fb && sft == 0) put(A - 16, pv);
+                if (lane == nc - 1 && last) put(A + 16 * (int32_t)nc, funnel16(xc, Z, sft));
+            }
+        }
+    }
+    // zero tail: bytes [nb, round4(nb)) and words up to nz
+    const uint32_t nb4 = (nb + 3) & ~3u;
+    if (tid < nb4 - nb) bb[nb + tid] = 0;
+    for (uint32_t k = nb4 / 4 + tid; k < nz / 4; k += NT) buf[k] = 0;
+}
+
+// fill_fast for the tile's sample conversion; false when the geometry is not its case
+template <int NT>
+__device__ __forceinline__ bool fill_fast_any(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
+                                              uint32_t nz, uint32_t tid) {
+    if (!dr.aligned || dr.ngrp != 1 || dr.bpp > 4) return false;
+    const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
+    const uint32_t sb = dr.swap ? (uint32_t)dr.bpp : 0u;
+    const uint32_t mode = (sb == 1 ? 0u : sb) * 2 + (dr.flip ? 1u : 0u);
+    switch (mode) {
+    case 0: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    case 1: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    case 4: fill_fast<NT, 2, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    case 5: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    case 8: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    default: return false;
+    }
+}
+
 // ==================================================================== k_lz77
 // Zero bytes of x as 4 bits (bit j: byte j of x is zero).
 __device__ __forceinline__ uint32_t zero_nibble(uint32_t x) {
@@ -594,7 +697,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     }
     const uint64_t B = __ballot(M != 0);
     const uint32_t lsub = se - ss;
-    uint32_t nm = 0, o = 0;
+    uint32_t nm = 0, o = 0, cov = 0;
     while (o < lsub) {
         // the first position >= o where a match pays
         const uint32_t t0 = o >> 5;
@@ -646,15 +749,9 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             L = __builtin_amdgcn_readfirstlane(l < maxlen ? l : maxlen);
         }
         if (nm < (uint32_t)C::MAXMW) {
-            if (lane == 0) {
-                S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
-                uint32_t sy, e, v;
-                len_code(L, sy, e, v);
-                atomicAdd(&S.h8[sy * LZ_HCOPIES], 1u);
-                dist_code(D, sy, e, v);
-                atomicAdd(&S.dfreq[sy], 1u);
-            }
+            if (lane == 0) S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
             nm++;
+            cov += L;
             // positions [p, p + L) of this lane's chunk are covered
             const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + L - p0;
             if (p + L > p0 && p < p0 + 32) {
@@ -663,6 +760,22 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             }
         }
         o = k + L;
+    }
+    // ph_parse_emu's rule: matches covering < MINCOV bytes are dropped (literals only)
+    if (cov < (uint32_t)C::MINCOV) {
+        nm = 0;
+        cover = 0;
+    }
+    // the kept matches' length and distance symbols, one match per lane (this wave's own
+    // records: LDS operations of one wave complete in order)
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t m = lane; m < nm; m += 64) {
+        const uint32_t r = S.mrl[w * C::MAXMW + m], c = r >> 19;
+        uint32_t sy, e, v;
+        len_code(((r >> 11) & 255u) + 3, sy, e, v);
+        atomicAdd(&S.h8[sy * LZ_HCOPIES + (lane & (LZ_HCOPIES - 1))], 1u);
+        dist_code(c == 0 ? 1u : c == 1 ? 2u : sp.rowlen, sy, e, v);
+        atomicAdd(&S.dfreq[sy], 1u);
     }
     if (lane == 0) S.w_nm[w] = nm;
 }
@@ -758,10 +871,16 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
     dr.init(d);
     const uint32_t nz = lz_fill_bytes<C>(sp) & ~15u;
+#ifndef PBX_LZ_FAST_FILL
+#define PBX_LZ_FAST_FILL 1  // fill_fast for the common geometry (0: the general fill only)
+#endif
 #ifndef PBX_LZ_SKIP_FILL
 #define PBX_LZ_SKIP_FILL 0  // timing experiments only (scripts/variants.sh): wrong output
 #endif
     if (PBX_LZ_SKIP_FILL) {
+    } else if (direct && PBX_LZ_FAST_FILL &&
+               fill_fast_any<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid)) {
+        if (PROF) stamp();
     } else if (direct) {
         FillPre<LZ_PF> pf;
         fill_issue<C::NT, LZ_PF>(pf, dr, (uint32_t)sp.base, sp.wl + sp.sl, tid);
@@ -799,13 +918,26 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cw[8], 0x138, 0xF, 0xF, false);  // wave_shr:1
         cw[0] = lane ? prev : (wi ? S.buf[wi - 1] : 0u);
     }
-    uint32_t cover, smask;
-    ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
+    uint32_t cover = 0, smask = 0xFFFFFFFFu;
+#ifndef PBX_LZ_SKIP_PARSE
+#define PBX_LZ_SKIP_PARSE 0  // timing experiments only: no matches (valid output, lower ratio)
+#endif
+    if (PBX_LZ_SKIP_PARSE) {
+        if (lane == 0) S.w_nm[w] = 0;
+        const uint32_t p0 = tid * C::CH;
+        const uint32_t nval = sp.sl > p0 ? sp.sl - p0 : 0u;
+        smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
+    } else {
+        ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
+    }
     stamp();
     // literal histogram of the chunk (positions no recorded match covers), 8 interleaved
     // copies against same-address LDS atomics, branch-free: a covered position adds into the
     // lane's own sink word.  Adler-32 partial sums from the same words.
-    {
+#ifndef PBX_LZ_SKIP_HIST
+#define PBX_LZ_SKIP_HIST 0  // timing experiments only: wrong output
+#endif
+    if (!PBX_LZ_SKIP_HIST) {
         const uint32_t lit = ~cover & smask, cp = lane & (LZ_HCOPIES - 1);
         const uint32_t sink = (uint32_t)(&S.hdummy[lane] - S.h8);
 #pragma unroll
@@ -839,7 +971,10 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     if (lane == 0) { S.red[3 * w] = s1 % ADLER_BASE; S.red[3 * w + 1] = s2 % ADLER_BASE; S.red[3 * w + 2] = n; }
     __syncthreads();
     stamp();
-    lz_write_out<C>(S, seg, sp, d.out_off + sp.base + sp.wl, info, hist, mrec, tid);
+#ifndef PBX_LZ_SKIP_OUT
+#define PBX_LZ_SKIP_OUT 0  // timing experiments only: wrong output
+#endif
+    if (!PBX_LZ_SKIP_OUT) lz_write_out<C>(S, seg, sp, d.out_off + sp.base + sp.wl, info, hist, mrec, tid);
     stamp();
 }
 

@@ -10,4 +10,5 @@ timeout -k 10 200 python -u scripts/phase_profile.py noise 4096 > $O/phase_noise
 if [ "$2" = "pmc" ]; then
 bash scripts/pmc_run.sh > $O/pmc_run.log 2>&1 && echo pmc ok || { echo pmc FAIL; tail -20 $O/pmc_run.log; exit 1; }
 mkdir -p $O/pmc && cp -r gpurun_out/pmc[0-9] $O/pmc/ && python3 scripts/pmc_summary.py gpurun_out $O/traffic.json > $O/pmc_summary.txt && tail -80 $O/pmc_summary.txt
+if [ -d gpurun_out/pmcf ]; then python3 scripts/pmc_summary.py gpurun_out/pmcf $O/traffic_filter.json > $O/pmc_filter_summary.txt && cat $O/pmc_filter_summary.txt; fi
 fi

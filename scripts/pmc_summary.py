@@ -17,6 +17,8 @@ for f in sorted(glob.glob(os.path.join(base, "pmc[1-9]", "*counter_collection.cs
     per = defaultdict(lambda: defaultdict(float))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if "k_filter3" in k:  # fixed vs adaptive variants apart
+            k = "pbx::k_filter3_adaptive" if "true" in k else "pbx::k_filter3_fixed"
         k = k.split("<")[0]
         per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         per[(k, r["Dispatch_Id"])]["_dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -87,7 +89,8 @@ if traffic_out:
                                                      "write_bytes": int(w * 1024)}
     with open(traffic_out, "w") as fo:
         json.dump(t, fo, indent=1)
-    with open(os.path.join(os.path.dirname(traffic_out) or ".", "issue.json"), "w") as fo:
+    issue_name = os.path.basename(traffic_out).replace("traffic", "issue")
+    with open(os.path.join(os.path.dirname(traffic_out) or ".", issue_name), "w") as fo:
         json.dump({"rule": "valu_busy = 2 x SQ_INSTS_VALU / (1024 SIMDs x cycles); salu_busy = "
                            "SQ_INSTS_SALU / (256 CUs x cycles); cycles = duration x GRBM_GUI_ACTIVE/8/duration",
                    "kernels": issue}, fo, indent=1)
