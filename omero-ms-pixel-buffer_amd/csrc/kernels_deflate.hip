@@ -17,6 +17,7 @@
 // kernels gives each its own occupancy: k_lz77 and k_encode hold ~46-50 KB of LDS
 // (4 workgroups per CU), k_huff 8.9 KB per wave, so the serial Huffman merge of many
 // segments overlaps on every CU.
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include "deflate_seg.h"
@@ -226,6 +227,20 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 
 __device__ __forceinline__ uint32_t crc_x8n_small(uint32_t n) {  // n < 2^16
     return crc_multmodp(kCrcPow.lo[n & 0xFFu], kCrcPow.hi[(n >> 8) & 0xFFu]);
+}
+// Per byte count n < CRC_TAB_N (any segment's compressed bytes): x^(8n) mod P (the crc32_combine
+// operator) and the standard CRC-32 of n bytes whose zero-init CRC is 0 (crc_from_raw's
+// constant term), filled once per device by k_crc_tables.  k_encode's last step is then two
+// loads instead of two 32-step carry-less products on one lane.
+constexpr uint32_t CRC_TAB_N = 32768;
+__device__ uint32_t g_crc_x8n[CRC_TAB_N];
+__device__ uint32_t g_crc_fin[CRC_TAB_N];
+__global__ __launch_bounds__(256) void k_crc_tables() {
+    const uint32_t n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= CRC_TAB_N) return;
+    const uint32_t op = crc_x8n_small(n);
+    g_crc_x8n[n] = op;
+    g_crc_fin[n] = crc_from_raw(0u, op);
 }
 
 // Segment geometry from the tile descriptor.
@@ -496,17 +511,19 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
 
 // The common geometry, without per-task bookkeeping: rows of whole 16-byte chunks, at most
 // 64 chunks (one wave per row), the sample conversion fixed at compile time (SB: bytes per
-// swapped sample, 0 = none; FL: the PNG sign flip).  Wave w fills rows w, w + NW, ... of the
-// buffer, FR rows' loads in flight together; every lane also loads the row above's last
-// chunk (one address for the whole wave), so rows need nothing from each other.  Row r's
+// swapped sample, 0 = none; FL: the PNG sign flip).  Wave w fills blocks of FR consecutive
+// rows of the buffer, their loads in flight together.  Row r's
 // lane l stores the aligned word ending where its chunk's first 16 - s bytes end (s = the
 // row's start mod 16), lane 0's word holding the row above's tail and the filter byte (the
 // layout fill_stores writes); the buffer's last row writes its own tail.  Only rows that
 // cross the buffer's ends clip per lane.
+#ifndef PBX_FF_FR
+#define PBX_FF_FR 2  // fill_fast: consecutive rows per wave block
+#endif
 template <int NT, uint32_t SB, bool FL>
 __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb, uint32_t nz,
                           uint32_t tid, uint32_t ra, uint32_t rz) {
-    constexpr uint32_t NW = NT / 64, FR = 2;
+    constexpr uint32_t NW = NT / 64, FR = PBX_FF_FR;
     uint8_t* bb = (uint8_t*)buf;
     const uint32_t lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nc = dr.nc, fb = dr.fb, rowlen = dr.rowlen, nrows = rz - ra + 1;
@@ -533,30 +550,32 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
         }
         *(uint4*)(bb + at) = v;
     };
-    for (uint32_t i0 = w; i0 < nrows; i0 += NW * FR) {
-        uint4 x[FR], pl[FR];
+    // wave w: blocks of FR consecutive rows, w, w + NW, ...; the chunk before a block's first
+    // row is one extra load, before its other rows the previous row's last chunk (a readlane)
+    for (uint32_t i0 = w * FR; i0 < nrows; i0 += NW * FR) {
+        uint4 x[FR];
 #pragma unroll
         for (uint32_t j = 0; j < FR; j++) {  // unconditional loads (clamped row): exact counters
-            const uint32_t i = i0 + NW * j;
-            const uint32_t r = ra + (i < nrows ? i : i0);
-            const uint8_t* rp = dr.row0 + (int64_t)r * dr.pitch;
-            x[j] = gload16(rp + 16 * (lane < nc ? lane : 0u));
-            pl[j] = gload16(r ? rp - dr.pitch + 16 * (nc - 1) : rp);
+            const uint32_t r = ra + (i0 + j < nrows ? i0 + j : i0);
+            x[j] = gload16(dr.row0 + (int64_t)r * dr.pitch + 16 * (lane < nc ? lane : 0u));
         }
+        const uint32_t r0 = ra + i0;
+        const uint8_t* rp0 = dr.row0 + (int64_t)r0 * dr.pitch;
+        uint4 y = gload16(r0 ? rp0 - dr.pitch + 16 * (nc - 1) : rp0);  // the row above's last chunk
+        y = r0 ? conv(y) : Z;
 #pragma unroll
         for (uint32_t j = 0; j < FR; j++) {
-            const uint32_t i = i0 + NW * j;
-            if (i >= nrows) break;  // uniform
-            const uint32_t r = ra + i;
+            if (i0 + j >= nrows) break;  // uniform
+            const uint32_t r = r0 + j;
             const uint4 xc = conv(x[j]);
-            uint4 y = r ? conv(pl[j]) : Z;  // the row above's last chunk
-            if (fb)  // its last 15 bytes, then the filter byte (0)
-                y = make_uint4((y.x >> 8) | (y.y << 24), (y.y >> 8) | (y.z << 24), (y.z >> 8) | (y.w << 24), y.w >> 8);
-            uint4 pv;  // the previous lane's chunk; lane 0: y
-            pv.x = (uint32_t)__builtin_amdgcn_update_dpp((int)y.x, (int)xc.x, 0x138, 0xF, 0xF, false);  // wave_shr:1
-            pv.y = (uint32_t)__builtin_amdgcn_update_dpp((int)y.y, (int)xc.y, 0x138, 0xF, 0xF, false);
-            pv.z = (uint32_t)__builtin_amdgcn_update_dpp((int)y.z, (int)xc.z, 0x138, 0xF, 0xF, false);
-            pv.w = (uint32_t)__builtin_amdgcn_update_dpp((int)y.w, (int)xc.w, 0x138, 0xF, 0xF, false);
+            uint4 yf = y;
+            if (fb)  // the row above's last 15 bytes, then the filter byte (0)
+                yf = make_uint4((y.x >> 8) | (y.y << 24), (y.y >> 8) | (y.z << 24), (y.z >> 8) | (y.w << 24), y.w >> 8);
+            uint4 pv;  // the previous lane's chunk; lane 0: yf
+            pv.x = (uint32_t)__builtin_amdgcn_update_dpp((int)yf.x, (int)xc.x, 0x138, 0xF, 0xF, false);  // wave_shr:1
+            pv.y = (uint32_t)__builtin_amdgcn_update_dpp((int)yf.y, (int)xc.y, 0x138, 0xF, 0xF, false);
+            pv.z = (uint32_t)__builtin_amdgcn_update_dpp((int)yf.z, (int)xc.z, 0x138, 0xF, 0xF, false);
+            pv.w = (uint32_t)__builtin_amdgcn_update_dpp((int)yf.w, (int)xc.w, 0x138, 0xF, 0xF, false);
             const int32_t q0 = (int32_t)(r * rowlen + fb) - (int32_t)B;
             const uint32_t sft = (uint32_t)q0 & 15u;
             const int32_t A = q0 - (int32_t)sft;
@@ -571,6 +590,8 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
                 if (lane == 0 && fb && sft == 0) put(A - 16, pv);
                 if (lane == nc - 1 && last) put(A + 16 * (int32_t)nc, funnel16(xc, Z, sft));
             }
+            y = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)xc.x, nc - 1), (uint32_t)__builtin_amdgcn_readlane((int)xc.y, nc - 1),
+                           (uint32_t)__builtin_amdgcn_readlane((int)xc.z, nc - 1), (uint32_t)__builtin_amdgcn_readlane((int)xc.w, nc - 1));
         }
     }
     // zero tail: bytes [nb, round4(nb)) and words up to nz
@@ -802,13 +823,30 @@ template <class C>
 __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, const SegParams& sp, uint64_t src,
                                              SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
                                              uint32_t* __restrict__ mrec, uint32_t tid) {
-    if (tid == 0) {
-        uint32_t a1 = S.red[0], a2 = S.red[1];
-        for (int k = 1; k < C::NW; k++) adler_combine(a1, a2, S.red[3 * k], S.red[3 * k + 1], S.red[3 * k + 2]);
-        SegInfo& g = info[seg];
-        g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
-        g.adler_s1 = a1; g.adler_s2 = a2;
-        g.src_lo = (uint32_t)src; g.src_hi = (uint32_t)(src >> 32);
+    if (tid < 64) {
+        // the segment's Adler-32 sums from the waves' (s1_k, s2_k, n_k): s1 = sum s1_k,
+        // s2 = sum (s2_k + s1_k * bytes after wave k) (adler_combine folded), lane k < NW
+        // one term, reduced over the wave
+        uint32_t t1 = 0, t2 = 0;
+        if (tid < (uint32_t)C::NW) {
+            uint32_t after = 0;
+#pragma unroll
+            for (int j = 1; j < C::NW; j++) after += (uint32_t)j > tid ? S.red[3 * j + 2] : 0u;
+            t1 = S.red[3 * tid];
+            t2 = (uint32_t)(((uint64_t)t1 * after + S.red[3 * tid + 1]) % ADLER_BASE);
+        }
+#pragma unroll
+        for (int off = 1; off < C::NW; off <<= 1) {
+            t1 += __shfl_xor(t1, off, 64);
+            t2 += __shfl_xor(t2, off, 64);
+        }
+        const uint32_t a1 = t1 % ADLER_BASE, a2 = t2 % ADLER_BASE;
+        if (tid == 0) {
+            SegInfo& g = info[seg];
+            g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
+            g.adler_s1 = a1; g.adler_s2 = a2;
+            g.src_lo = (uint32_t)src; g.src_hi = (uint32_t)(src >> 32);
+        }
     }
     uint32_t* hg = hist + (size_t)seg * HIST_WORDS;
     for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
@@ -1644,6 +1682,9 @@ __device__ __forceinline__ uint32_t crc_chunk_aligned(uint32_t tid, const SM& S,
 #ifndef PBX_ENC_SKIP_CRC
 #define PBX_ENC_SKIP_CRC 0
 #endif
+#ifndef PBX_ENC_LIT_BF
+#define PBX_ENC_LIT_BF 0  // literal-only waves: branch-free word puts
+#endif
 #ifndef PBX_ENC_SKIP_STORE
 #define PBX_ENC_SKIP_STORE 0
 #endif
@@ -1914,7 +1955,21 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         }
         const uint32_t tb = SH + lb + (first ? gi.hdr_bits : 0u);  // first token bit in out[]
         LdsRunWriter bw(S.out, tb + pre + inc - nbits);
-        if (lit_only) {  // literal codes (<= 15 bits) put in pairs: half the puts
+        if (lit_only && PBX_ENC_LIT_BF) {
+            // literal codes in pairs (<= 30 bits: at most one word completes per pair), no
+            // branch: a pair that completes no word ORs zero into the current one
+#pragma unroll
+            for (int i = 0; i < C::CH; i += 2) {
+                const uint32_t n0 = slot[i] >> 27;
+                bw.acc |= (uint64_t)((slot[i] & 0x7FFFFFFu) | ((slot[i + 1] & 0x7FFFFFFu) << n0)) << bw.nacc;
+                bw.nacc += n0 + (slot[i + 1] >> 27);
+                const uint32_t full = bw.nacc >= 32 ? 1u : 0u;
+                atomicOr(&S.out[bw.word], full ? (uint32_t)bw.acc : 0u);
+                bw.acc = full ? bw.acc >> 32 : bw.acc;
+                bw.word += full;
+                bw.nacc -= 32 * full;
+            }
+        } else if (lit_only) {  // literal codes (<= 15 bits) put in pairs: half the puts
 #pragma unroll
             for (int i = 0; i < C::CH; i += 2) {
                 const uint32_t n0 = slot[i] >> 27;
@@ -1978,10 +2033,15 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         uint32_t part = 0;
         if (lb) part |= out_byte_at(S, P) | SP_HEAD;
         if (has_tail) part |= (out_byte_at(S, P + (le >> 3)) << 8) | SP_TAIL;
-        const uint32_t op = crc_x8n_small(nbytes);
         SegInfo& g = info[seg];
-        g.crc = crc_from_raw(raw, op);
-        g.crc_op = op;
+        if (nbytes < CRC_TAB_N) {
+            g.crc = raw ^ g_crc_fin[nbytes];
+            g.crc_op = g_crc_x8n[nbytes];
+        } else {
+            const uint32_t op = crc_x8n_small(nbytes);
+            g.crc = crc_from_raw(raw, op);
+            g.crc_op = op;
+        }
         g.part = part;
         g.bitsum = bitsum;
     }
@@ -2107,8 +2167,31 @@ hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* 
     return hipGetLastError();
 }
 
+// k_crc_tables once per device, finished before any deflate launch can use the tables
+static hipError_t crc_tables_ready() {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static hipError_t res[kMaxDev];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [&] {
+        hipStream_t s = nullptr;
+        res[dev] = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (res[dev] != hipSuccess) return;
+        hipLaunchKernelGGL(k_crc_tables, dim3(CRC_TAB_N / 256), dim3(256), 0, s);
+        res[dev] = hipGetLastError();
+        const hipError_t e2 = hipStreamSynchronize(s);
+        if (res[dev] == hipSuccess) res[dev] = e2;
+        (void)hipStreamDestroy(s);
+    });
+    return res[dev];
+}
+
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev, hipEvent_t* ev2) {
     if (!a.ntiles || !a.nseg) return hipSuccess;
+    if (const hipError_t e = crc_tables_ready(); e != hipSuccess) return e;
     const bool prof = a.stamps != nullptr;
     hipLaunchKernelGGL(k_seg_map, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
                        a.seg_tile, a.info, a.blk);
