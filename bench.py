@@ -324,8 +324,8 @@ def serve_lines(svc, iid, threads=(32, 128, 512)):
     res = {}
     for t in threads:
         s = ServeStats()
-        total = max(8192, 16 * t)
-        rc = L.pbx_serve_bench(svc.handle, reqs, len(ctxs), t, total, 2 * t, ctypes.byref(s))
+        total = max(8192, 32 * t)
+        rc = L.pbx_serve_bench(svc.handle, reqs, len(ctxs), t, total, max(2048, 4 * t), ctypes.byref(s))
         if rc != 0:
             raise RuntimeError(f"pbx_serve_bench: {rc}")
         res[f"threads_{t}"] = {

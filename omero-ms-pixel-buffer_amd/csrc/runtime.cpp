@@ -631,7 +631,11 @@ struct Coalescer {
     // the k-th concurrent batch only once `launch_min[k]` requests wait, so that few callers
     // get few, larger batches and many callers get a deeper pipeline (measured:
     // scripts/serve_sweep.py).
-    int depth = 3;
+    int depth = 4;
+    // Requests per batch at most ($PBX_MAX_BATCH): with many callers, batches of <= 64 keep
+    // the kernel / D2H pipeline fine-grained, so no caller waits behind one large batch's
+    // copy (512 callers: p99 4.6 ms at 64, 15-46 ms uncapped; profiles/r03_sv).
+    size_t max_batch = 64;
     size_t launch_min[8] = {1, 4, 32, 64, 128, 256, 512, 1024};
     bool may_launch() const { return !queue.empty() && inflight < depth && queue.size() >= launch_min[inflight]; }
     std::deque<Pending*> queue;
@@ -643,6 +647,7 @@ struct Coalescer {
 
     explicit Coalescer(pbx_ctx* c) : ctx(c) {
         if (const char* d = getenv("PBX_COALESCE_DEPTH")) depth = std::min(8, std::max(1, atoi(d)));
+        if (const char* m = getenv("PBX_MAX_BATCH")) max_batch = std::min<size_t>(MAX_BATCH, std::max(1, atoi(m)));
         int nc = 2;
         if (const char* c = getenv("PBX_COMPLETERS")) nc = std::min(8, std::max(1, atoi(c)));
         launcher = std::thread([this] { launch_loop(); });
@@ -678,7 +683,7 @@ struct Coalescer {
                 std::unique_lock<std::mutex> g(mu);
                 cv_launch.wait(g, [&] { return (stop && queue.empty()) || may_launch(); });
                 if (queue.empty()) break;  // stopping, nothing left
-                while (!queue.empty() && take.size() < MAX_BATCH) {
+                while (!queue.empty() && take.size() < max_batch) {
                     take.push_back(queue.front());
                     queue.pop_front();
                 }
