@@ -520,9 +520,11 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
 #ifndef PBX_FF_FR
 #define PBX_FF_FR 2  // fill_fast: consecutive rows per wave block
 #endif
+// gseg (optional): the segment's bytes (buffer bytes [wl, nb)) are also stored there, from
+// the same registers (k_encode's input), instead of re-read from LDS after the fill.
 template <int NT, uint32_t SB, bool FL>
 __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb, uint32_t nz,
-                          uint32_t tid, uint32_t ra, uint32_t rz) {
+                          uint32_t tid, uint32_t ra, uint32_t rz, uint8_t* gseg, uint32_t wl) {
     constexpr uint32_t NW = NT / 64, FR = PBX_FF_FR;
     uint8_t* bb = (uint8_t*)buf;
     const uint32_t lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -549,6 +551,12 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
             v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
         }
         *(uint4*)(bb + at) = v;
+        if (gseg && at >= (int32_t)wl) gstore16(gseg + (at - (int32_t)wl), v);
+    };
+    // interior word: no clipping in LDS, the global copy for segment bytes only
+    auto put_in = [&](int32_t at, uint4 v) {
+        *(uint4*)(bb + at) = v;
+        if (gseg && at >= (int32_t)wl) gstore16(gseg + (at - (int32_t)wl), v);
     };
     // wave w: blocks of FR consecutive rows, w, w + NW, ...; the chunk before a block's first
     // row is one extra load, before its other rows the previous row's last chunk (a readlane)
@@ -582,9 +590,9 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
             const uint4 wv = funnel16(pv, xc, sft);
             const bool last = r == rz && sft;  // the buffer's last row writes its own tail
             if (A >= 16 && A + 16 * (int32_t)(nc + 1) <= (int32_t)nb) {  // uniform: no clipping
-                if (lane < nc) *(uint4*)(bb + A + 16 * (int32_t)lane) = wv;
-                if (lane == 0 && fb && sft == 0) *(uint4*)(bb + A - 16) = pv;
-                if (lane == nc - 1 && last) *(uint4*)(bb + A + 16 * (int32_t)nc) = funnel16(xc, Z, sft);
+                if (lane < nc) put_in(A + 16 * (int32_t)lane, wv);
+                if (lane == 0 && fb && sft == 0) put_in(A - 16, pv);
+                if (lane == nc - 1 && last) put_in(A + 16 * (int32_t)nc, funnel16(xc, Z, sft));
             } else {
                 if (lane < nc) put(A + 16 * (int32_t)lane, wv);
                 if (lane == 0 && fb && sft == 0) put(A - 16, pv);
@@ -603,17 +611,17 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
 // fill_fast for the tile's sample conversion; false when the geometry is not its case
 template <int NT>
 __device__ __forceinline__ bool fill_fast_any(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
-                                              uint32_t nz, uint32_t tid) {
+                                              uint32_t nz, uint32_t tid, uint8_t* gseg, uint32_t wl) {
     if (!dr.aligned || dr.ngrp != 1 || dr.bpp > 4) return false;
     const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
     const uint32_t sb = dr.swap ? (uint32_t)dr.bpp : 0u;
     const uint32_t mode = (sb == 1 ? 0u : sb) * 2 + (dr.flip ? 1u : 0u);
     switch (mode) {
-    case 0: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
-    case 1: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz); return true;
-    case 4: fill_fast<NT, 2, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
-    case 5: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz); return true;
-    case 8: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz); return true;
+    case 0: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
+    case 1: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
+    case 4: fill_fast<NT, 2, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
+    case 5: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
+    case 8: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
     default: return false;
     }
 }
@@ -909,15 +917,21 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
     dr.init(d);
     const uint32_t nz = lz_fill_bytes<C>(sp) & ~15u;
+#ifndef PBX_LZ_SKIP_STORE
+#define PBX_LZ_SKIP_STORE 0  // timing experiments only (scripts/variants.sh): wrong output
+#endif
 #ifndef PBX_LZ_FAST_FILL
 #define PBX_LZ_FAST_FILL 1  // fill_fast for the common geometry (0: the general fill only)
 #endif
 #ifndef PBX_LZ_SKIP_FILL
 #define PBX_LZ_SKIP_FILL 0  // timing experiments only (scripts/variants.sh): wrong output
 #endif
+    bool stored = false;  // the segment's stream bytes already written (fill_fast)
     if (PBX_LZ_SKIP_FILL) {
     } else if (direct && PBX_LZ_FAST_FILL &&
-               fill_fast_any<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid)) {
+               fill_fast_any<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid,
+                                    PBX_LZ_SKIP_STORE ? nullptr : stream + d.out_off + sp.base + sp.wl, sp.wl)) {
+        stored = true;
         if (PROF) stamp();
     } else if (direct) {
         FillPre<LZ_PF> pf;
@@ -935,10 +949,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         stamp();
     }
     __syncthreads();
-#ifndef PBX_LZ_SKIP_STORE
-#define PBX_LZ_SKIP_STORE 0  // timing experiments only (scripts/variants.sh): wrong output
-#endif
-    if (direct && !PBX_LZ_SKIP_STORE) {  // the segment's stream bytes for k_encode (16-byte words; slack after every tile)
+    if (direct && !stored && !PBX_LZ_SKIP_STORE) {  // the segment's stream bytes for k_encode (16-byte words; slack after every tile)
         uint8_t* o = stream + d.out_off + sp.base + sp.wl;
         for (uint32_t k = tid; k < (sp.sl + 15) / 16; k += C::NT)
             *(uint4*)(o + 16 * k) = *(const uint4*)(S.buf + sp.wl / 4 + 4 * k);
