@@ -988,11 +988,21 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
 #endif
     if (!PBX_LZ_SKIP_HIST) {
         const uint32_t lit = ~cover & smask, cp = lane & (LZ_HCOPIES - 1);
-        const uint32_t sink = (uint32_t)(&S.hdummy[lane] - S.h8);
+        if (__builtin_amdgcn_ballot_w64(lit != 0xFFFFFFFFu) == 0) {
+            // every position of the wave a literal (no kept match, whole chunks: most waves on
+            // noisy data): the bin address only, no per-position select
 #pragma unroll
-        for (int j = 0; j < 32; j++) {
-            const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
-            atomicAdd(&S.h8[((lit >> j) & 1u) ? bt * LZ_HCOPIES + cp : sink], 1u);
+            for (int j = 0; j < 32; j++) {
+                const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+                atomicAdd(&S.h8[bt * LZ_HCOPIES + cp], 1u);
+            }
+        } else {
+            const uint32_t sink = (uint32_t)(&S.hdummy[lane] - S.h8);
+#pragma unroll
+            for (int j = 0; j < 32; j++) {
+                const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+                atomicAdd(&S.h8[((lit >> j) & 1u) ? bt * LZ_HCOPIES + cp : sink], 1u);
+            }
         }
     }
     if (tid == 0) atomicAdd(&S.h8[256 * LZ_HCOPIES], 1u);  // end of block
