@@ -36,7 +36,10 @@ constexpr uint32_t STAMP_STRIDE = 32;  // diagnostics: k_lz77 0.., k_huff 8.., k
 // (8 bits), candidate index (2 bits: distance 1, 2 or one row), unpacked into the mrec form
 // (pos | (len - 3) << 16, dist - 1) when written to HBM.  4 KB less than two arrays: the room
 // for 8 histogram copies at 4 workgroups per CU.
-constexpr uint32_t LZ_HCOPIES = 8;
+#ifndef PBX_LZ_HCOPIES
+#define PBX_LZ_HCOPIES 8  // experiments: histogram copies (a power of two, >= 8)
+#endif
+constexpr uint32_t LZ_HCOPIES = PBX_LZ_HCOPIES;
 template <class C>
 struct LzSmem {
     static_assert(C::SUB == 2048, "11-bit sub-segment positions in the packed match records");
@@ -660,6 +663,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0;
+    uint64_t cvb = 0;  // bytes inside some paying run (the walk's coverage bound, below)
 #pragma unroll
     for (int c = 0; c < NCAND; c++) {
         const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
@@ -722,7 +726,25 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             if (ml[c] >= 4) r &= x >> 3;
             if (ml[c] >= 6) r &= (x >> 4) & (x >> 5);
             M |= (uint32_t)r;
+            const uint64_t r32 = (uint32_t)r;  // [j, j + ml) for every paying start j of the lane
+            uint64_t D = r32 | (r32 << 1) | (r32 << 2);
+            if (ml[c] >= 4) D |= r32 << 3;
+            if (ml[c] >= 6) D |= (r32 << 4) | (r32 << 5);
+            cvb |= D;
         }
+    }
+#ifndef PBX_LZ_COVBOUND
+#define PBX_LZ_COVBOUND 1  // skip the walk when its matches cannot reach MINCOV (0: always walk)
+#endif
+    // Every match the walk records lies inside a run of >= ml equal bytes of its candidate,
+    // i.e. inside the union of [j, j + ml) over that candidate's paying starts j; a match
+    // extended past CAP lies in a run of >= CAP >= MINCOV bytes.  So the walk's coverage is at
+    // most the wave's count of such bytes (per lane, bytes past the lane's chunk counted too:
+    // an overestimate), and below MINCOV the walk would drop all its matches (noise: most
+    // waves hold a few 3-4 byte runs): the same result without the walk.
+    if (PBX_LZ_COVBOUND && wave_sum((uint32_t)__builtin_popcountll(cvb)) < (uint32_t)C::MINCOV) {
+        if (lane == 0) S.w_nm[w] = 0;
+        return;
     }
     const uint64_t B = __ballot(M != 0);
     const uint32_t lsub = se - ss;
@@ -860,9 +882,13 @@ __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, c
     for (uint32_t i = tid; i < HIST_WORDS; i += C::NT) {
         uint32_t v;
         if (i < 288) {
-            const uint4 a = *(const uint4*)&S.h8[i * LZ_HCOPIES];
-            const uint4 b = *(const uint4*)&S.h8[i * LZ_HCOPIES + 4];
-            v = (a.x + a.y) + (a.z + a.w) + (b.x + b.y) + (b.z + b.w);
+            v = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < LZ_HCOPIES; k += 8) {
+                const uint4 a = *(const uint4*)&S.h8[i * LZ_HCOPIES + k];
+                const uint4 b = *(const uint4*)&S.h8[i * LZ_HCOPIES + k + 4];
+                v += (a.x + a.y) + (a.z + a.w) + (b.x + b.y) + (b.z + b.w);
+            }
         } else {
             v = S.dfreq[i - 288];
         }
@@ -2038,13 +2064,54 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     // owned bytes to their final place: unaligned head and tail bytes, aligned words between
     const uint32_t nbytes = o1 - o0;
     uint8_t* dst = out + tile_off + gi.zoff + ZLIB_HDR_BYTES + bi.off + byte0 + o0;
-    uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
-    if (head > nbytes) head = nbytes;
-    const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
     const uint32_t b0 = P + o0;
-    if (tid < head) dst[tid] = (uint8_t)out_byte_at(S, b0 + tid);
-    for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, b0 + head + 4 * k);
-    for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_at(S, b0 + j);
+#ifndef PBX_ENC_STORE16
+#define PBX_ENC_STORE16 1  // 16-byte output stores (0: dword stores, the round-2 form)
+#endif
+    if (PBX_ENC_STORE16) {
+        // aligned 16-byte units: two aligned LDS reads, a uniform word selection and byte
+        // shift (the units' LDS offset mod 16 is the same for every thread)
+        uint32_t head = (uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u);
+        if (head > nbytes) head = nbytes;
+        const uint32_t n16 = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 4;
+        if (tid < head) dst[tid] = (uint8_t)out_byte_at(S, b0 + tid);
+        const uint32_t j0 = b0 + head, w0 = (j0 >> 2) & ~3u, sb = j0 & 3u;
+        const uint32_t wq = __builtin_amdgcn_readfirstlane((j0 >> 2) & 3u);
+        for (uint32_t k = tid; k < n16; k += C::NT) {
+            const uint4 a = *(const uint4*)&S.out[w0 + 4 * k], b = *(const uint4*)&S.out[w0 + 4 * k + 4];
+            const uint32_t z[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint32_t q[5];
+            switch (wq) {
+            case 0:
+#pragma unroll
+                for (int i = 0; i < 5; i++) q[i] = z[i];
+                break;
+            case 1:
+#pragma unroll
+                for (int i = 0; i < 5; i++) q[i] = z[i + 1];
+                break;
+            case 2:
+#pragma unroll
+                for (int i = 0; i < 5; i++) q[i] = z[i + 2];
+                break;
+            default:
+#pragma unroll
+                for (int i = 0; i < 5; i++) q[i] = z[i + 3];
+                break;
+            }
+            *(uint4*)(dst + head + 16 * k) =
+                make_uint4(__builtin_amdgcn_alignbyte(q[1], q[0], sb), __builtin_amdgcn_alignbyte(q[2], q[1], sb),
+                           __builtin_amdgcn_alignbyte(q[3], q[2], sb), __builtin_amdgcn_alignbyte(q[4], q[3], sb));
+        }
+        for (uint32_t j = head + 16 * n16 + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_at(S, b0 + j);
+    } else {
+        uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
+        if (head > nbytes) head = nbytes;
+        const uint32_t nwords = PBX_ENC_SKIP_STORE ? 0u : (nbytes - head) >> 2;
+        if (tid < head) dst[tid] = (uint8_t)out_byte_at(S, b0 + tid);
+        for (uint32_t k = tid; k < nwords; k += C::NT) *(uint32_t*)(dst + head + 4 * k) = out_word(S, b0 + head + 4 * k);
+        for (uint32_t j = head + 4 * nwords + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_at(S, b0 + j);
+    }
     __syncthreads();
     if (tid == 0) {
         uint32_t raw = 0;
