@@ -212,6 +212,8 @@ int pbxemu_win_bytes(void) { return C::WIN; }
 int pbxemu_threads(void) { return C::NT; }
 int pbxemu_blk_segs(void) { return (int)BLK_SEGS; }
 int pbxemu_split_max(void) { return (int)SPLIT_MAX; }
+// The device's division by a precomputed reciprocal (pbx_common.h div_rcp), for the tests.
+uint32_t pbxemu_div_rcp(uint32_t n, uint32_t d) { return div_rcp(n, d, recip32(d)); }
 
 // Deflate `len` bytes into a zlib stream exactly as the batch pipeline does for one tile
 // (segments of seg_len_for(len) bytes, window, per-segment blocks, combined Adler-32).

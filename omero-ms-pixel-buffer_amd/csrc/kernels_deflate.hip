@@ -301,11 +301,13 @@ struct DirectRows {
     uint32_t rowlen, rb, fb, h, nc, ngrp;
     int32_t bpp;
     bool swap, flip, aligned;
+    uint32_t rcp;  // recip32(rowlen): stream offset -> row without a division
     __device__ __forceinline__ void init(const TileDesc& d) {
         row0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * d.bpp;
         pitch = d.pitch;
         fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
         rowlen = d.rowlen;
+        rcp = d.rowlen_rcp;
         rb = rowlen - fb;
         h = (uint32_t)d.h;
         nc = (rb + 15) >> 4;
@@ -331,8 +333,8 @@ struct FillPre {
 struct FillGeom {
     uint32_t ra, rz, ntask;
     __device__ __forceinline__ FillGeom(const DirectRows& dr, uint32_t B, uint32_t nb) {
-        ra = B / dr.rowlen;
-        rz = (B + nb - 1) / dr.rowlen;
+        ra = div_rcp(B, dr.rowlen, dr.rcp);
+        rz = div_rcp(B + nb - 1, dr.rowlen, dr.rcp);
         ntask = (rz - ra + 1) * dr.ngrp;
     }
 };
@@ -523,12 +525,15 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
 #ifndef PBX_FF_FR
 #define PBX_FF_FR 2  // fill_fast: consecutive rows per wave block
 #endif
+#ifndef PBX_FF_FR4
+#define PBX_FF_FR4 3  // 16-bit samples without the sign flip (the headline): three rows, one load round for 18 rows
+#endif
 // gseg (optional): the segment's bytes (buffer bytes [wl, nb)) are also stored there, from
 // the same registers (k_encode's input), instead of re-read from LDS after the fill.
-template <int NT, uint32_t SB, bool FL>
+template <int NT, uint32_t SB, bool FL, uint32_t FR = PBX_FF_FR>
 __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb, uint32_t nz,
                           uint32_t tid, uint32_t ra, uint32_t rz, uint8_t* gseg, uint32_t wl) {
-    constexpr uint32_t NW = NT / 64, FR = PBX_FF_FR;
+    constexpr uint32_t NW = NT / 64;
     uint8_t* bb = (uint8_t*)buf;
     const uint32_t lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nc = dr.nc, fb = dr.fb, rowlen = dr.rowlen, nrows = rz - ra + 1;
@@ -616,13 +621,13 @@ template <int NT>
 __device__ __forceinline__ bool fill_fast_any(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
                                               uint32_t nz, uint32_t tid, uint8_t* gseg, uint32_t wl) {
     if (!dr.aligned || dr.ngrp != 1 || dr.bpp > 4) return false;
-    const uint32_t ra = B / dr.rowlen, rz = (B + nb - 1) / dr.rowlen;
+    const uint32_t ra = div_rcp(B, dr.rowlen, dr.rcp), rz = div_rcp(B + nb - 1, dr.rowlen, dr.rcp);
     const uint32_t sb = dr.swap ? (uint32_t)dr.bpp : 0u;
     const uint32_t mode = (sb == 1 ? 0u : sb) * 2 + (dr.flip ? 1u : 0u);
     switch (mode) {
     case 0: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
     case 1: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    case 4: fill_fast<NT, 2, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
+    case 4: fill_fast<NT, 2, false, PBX_FF_FR4>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
     case 5: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
     case 8: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
     default: return false;
@@ -926,7 +931,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
                                                 uint32_t nseg, uint8_t* __restrict__ stream,
                                                 SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
                                                 uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps,
-                                                uint32_t uniform_nseg) {
+                                                uint32_t uniform_nseg, uint32_t uniform_rcp) {
     __shared__ LzSmem<C> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
@@ -937,7 +942,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     };
     stamp();
     // (tiles of equal segment counts: the tile by a division, one dependent load less)
-    const TileDesc d = load_desc(dt + (uniform_nseg ? seg / uniform_nseg : seg_tile[seg]));
+    const TileDesc d = load_desc(dt + (uniform_nseg ? div_rcp(seg, uniform_nseg, uniform_rcp) : seg_tile[seg]));
     const SegParams sp = seg_params(d, seg - d.seg_first);
     const bool direct = (d.flags & TF_DIRECT) != 0;
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
@@ -2286,10 +2291,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     const uint32_t lz_grid = a.nseg;
     if (prof)
         hipLaunchKernelGGL((k_lz77<DC, true>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg);
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg,
+                           a.uniform_rcp);
     else
         hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg);
+                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg,
+                           a.uniform_rcp);
     if (ev) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof)

@@ -47,6 +47,18 @@ constexpr uint32_t TIFF_NTAGS = 11;
 constexpr uint32_t TIFF_DATA_OFFSET = 160;
 
 // Per-tile descriptor (device side).  64-byte aligned POD, filled by the host planner.
+// Division by a divisor known ahead (a tile's row length, a batch's segments per tile)
+// without the ~20-instruction integer division sequence: recip32(d) = floor((2^32-1) / d) + 1
+// makes umulhi(n, recip) floor(n / d) or one more (the error n * r / (d 2^32) < 1 for every
+// 32-bit n), and the sign of n - q d (|n - q d| < d < 2^31) corrects it, all in 32-bit scalar
+// arithmetic.  d <= 1: recip 0 (n / 1 = n).
+PBX_HD uint32_t recip32(uint32_t d) { return d > 1 ? (uint32_t)(0xFFFFFFFFull / d) + 1u : 0u; }
+PBX_HD uint32_t div_rcp(uint32_t n, uint32_t d, uint32_t rcp) {
+    if (!rcp) return d ? n : 0u;
+    const uint32_t q = (uint32_t)(((uint64_t)n * rcp) >> 32);
+    return (int32_t)(n - q * d) < 0 ? q - 1u : q;
+}
+
 struct alignas(16) TileDesc {
     const uint8_t* plane;   // plane base in HBM
     int64_t pitch;          // bytes per plane row
@@ -61,7 +73,7 @@ struct alignas(16) TileDesc {
     uint32_t seg_first;     // deflate tiles: first segment index in the batch
     uint32_t seg_count;
     uint32_t seg_len;       // nominal segment length (the last may be shorter)
-    uint32_t rowfilt_off;   // (unused)
+    uint32_t rowlen_rcp;    // deflate tiles: recip32(rowlen), divisions by rowlen on the device
     uint32_t blk_first;     // first workgroup of this tile (extract / filter bands)
     uint32_t rows_per_blk;  // extract: rows handled by one workgroup
     uint32_t hblk_first;    // deflate tiles: first Huffman block index in the batch
@@ -332,7 +344,7 @@ struct TileStream {
     PBX_HD void init(const TileDesc& d, const uint8_t* rowfilt_base) {
         plane = d.plane; pitch = d.pitch; x = d.x; y = d.y; bpp = d.bpp; lbpp = d.lbpp;
         rowlen = d.rowlen; flags = d.flags; filter = d.filter;
-        rowfilt = rowfilt_base ? rowfilt_base + d.rowfilt_off : nullptr;
+        rowfilt = rowfilt_base;
         vrb = d.vw ? d.vw * (uint32_t)d.bpp : 0xFFFFFFFFu;
         vh = d.vw ? d.vh : 0xFFFFFFFFu;
     }

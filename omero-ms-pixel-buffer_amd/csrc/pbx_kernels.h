@@ -72,6 +72,7 @@ struct DeflateLaunch {
     uint32_t* seg_tile;     // [nseg] tile of every segment (k_seg_map)
     uint32_t cus = 256;     // compute units of the device (persistent grids)
     uint32_t uniform_nseg = 0;  // every tile has this many segments (tile = seg / it), or 0
+    uint32_t uniform_rcp = 0;   // recip32(uniform_nseg)
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.
 // ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode.

@@ -1907,6 +1907,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     for (size_t k = 0; k < b->dt.size(); k++) {
         TileDesc& d = b->dt[k];
         deflate_split(d.stream_len, d.seg_count, d.seg_len);
+        d.rowlen_rcp = recip32(d.rowlen);
         d.seg_first = b->nseg;
         b->nseg += d.seg_count;
         d.hblk_first = b->nblk;
@@ -2034,6 +2035,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     a.uniform_nseg = ndt ? b->dt[0].seg_count : 0u;
     for (uint32_t k = 1; k < ndt && a.uniform_nseg; k++)
         if (b->dt[k].seg_count != a.uniform_nseg) a.uniform_nseg = 0;
+    a.uniform_rcp = recip32(a.uniform_nseg);
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr));

@@ -137,3 +137,21 @@ def test_blocks_split_segments_evenly(n):
     assert max(counts) <= blk and max(counts) - min(counts) <= 1
     if n == 524800:
         assert counts == [11, 11, 11]
+
+
+def test_div_rcp_exact():
+    """div_rcp (the kernels' division by a host-computed reciprocal: segment -> tile, stream
+    offset -> plane row) equals integer division for divisors up to 2^31 and any 32-bit n."""
+    import ctypes
+    L = _emu.lib()
+    L.pbxemu_div_rcp.restype = ctypes.c_uint32
+    L.pbxemu_div_rcp.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    rng = np.random.default_rng(11)
+    ds = [1, 2, 3, 7, 16, 33, 1025, 1040, 2049, 4097, 65535, 65536, 99991, 2**24 + 1, 2**31 - 1, 2**31]
+    ds += [int(x) for x in rng.integers(2, 2**31, 200)]
+    for d in ds:
+        ns = [0, 1, d - 1, d, d + 1, 2 * d - 1, 2**32 - 1, 2**32 - 2, 2**31]
+        ns += [int(x) for x in rng.integers(0, 2**32, 200)] + [int(x) for x in rng.integers(0, 2**20, 50)]
+        for n in ns:
+            n &= 0xFFFFFFFF
+            assert L.pbxemu_div_rcp(n, d) == n // d, (n, d)
