@@ -45,6 +45,18 @@ __device__ __forceinline__ uint32_t upper_index(uint32_t n, uint32_t v, F key) {
     return lo;
 }
 
+// Inclusive prefix sum over the wave by DPP alone (no ds_bpermute round trips): row scans by
+// row_shr (zero shifted in), then row_bcast:15 / :31 carry the row totals into the rows above.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t lane) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {

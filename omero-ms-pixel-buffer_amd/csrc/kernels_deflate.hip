@@ -721,8 +721,8 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             const uint32_t vm = a0 >= d ? 0xFFFFFFFFu : (d - a0 >= 32 ? 0u : 0xFFFFFFFFu << (d - a0));
             e &= vm & smask;
         }
-        uint32_t nx = __shfl_down(e, 1, 64);
-        nx = lane == 63 ? 0u : nx;
+        // the next lane's E (wave_shl:1; lane 63: none, matches stay in the sub-segment)
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x130, 0xF, 0xF, false);
         exlo[c] = e;
         exhi[c] = nx;
         if (d) {
@@ -870,12 +870,7 @@ __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, c
             t1 = S.red[3 * tid];
             t2 = (uint32_t)(((uint64_t)t1 * after + S.red[3 * tid + 1]) % ADLER_BASE);
         }
-#pragma unroll
-        for (int off = 1; off < C::NW; off <<= 1) {
-            t1 += __shfl_xor(t1, off, 64);
-            t2 += __shfl_xor(t2, off, 64);
-        }
-        const uint32_t a1 = t1 % ADLER_BASE, a2 = t2 % ADLER_BASE;
+        const uint32_t a1 = wave_sum(t1) % ADLER_BASE, a2 = wave_sum(t2) % ADLER_BASE;  // lanes >= NW hold 0
         if (tid == 0) {
             SegInfo& g = info[seg];
             g.sl = sp.sl; g.last = sp.last; g.wl = sp.wl; g.rowlen = sp.rowlen;
@@ -1050,15 +1045,15 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         }
         s2 -= (cs + (uint32_t)C::CH - ce) * s1;
     }
-    // Adler-32 partials: wave tree on raw sums (one wave covers <= 2048 bytes: s1 < 2^20,
-    // s2 < 2^30, no modular reduction needed), reduced once per wave
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t r1 = __shfl_down(s1, off, 64), r2 = __shfl_down(s2, off, 64);
-        const uint32_t rn = __shfl_down(n, off, 64);
-        if ((lane & (2 * off - 1)) == 0 && lane + off < 64) { s2 += rn * s1 + r2; s1 += r1; n += rn; }
+    // Adler-32 partials of the wave on raw sums (one wave covers <= 2048 bytes: s1 < 2^20,
+    // s2 < 2^31, no modular reduction needed): s1 = sum s1_l, s2 = sum (s2_l + s1_l * bytes
+    // of the lanes after l), by DPP scans and sums (no ds_bpermute round trips)
+    {
+        const uint32_t ninc = wave_incl_scan_dpp(n);
+        const uint32_t ntot = (uint32_t)__builtin_amdgcn_readlane((int)ninc, 63);
+        const uint32_t w1 = wave_incl_scan_dpp(s1), w2 = wave_incl_scan_dpp(s2 + s1 * (ntot - ninc));
+        if (lane == 63) { S.red[3 * w] = w1 % ADLER_BASE; S.red[3 * w + 1] = w2 % ADLER_BASE; S.red[3 * w + 2] = ntot; }
     }
-    if (lane == 0) { S.red[3 * w] = s1 % ADLER_BASE; S.red[3 * w + 1] = s2 % ADLER_BASE; S.red[3 * w + 2] = n; }
     __syncthreads();
     stamp();
 #ifndef PBX_LZ_SKIP_OUT
@@ -1972,7 +1967,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         stamp();
     }
     // exclusive scan of the token bits over the workgroup (one barrier)
-    const uint32_t inc = wave_incl_add(nbits, lane);
+    const uint32_t inc = wave_incl_scan_dpp(nbits);
     if (lane == 63) S.wtot[w] = inc;
     __syncthreads();
     stamp();
