@@ -101,6 +101,10 @@ struct HuffSmem {
 // m = 0..7 chunks) and x^(8*256*m) (TB, 8-chunk steps), then the wave-distance operators
 // x^(8*2048*2^k) (TW, k = 0..2), each as nibble tables (crc_lane_tables below).
 constexpr uint32_t CRCX_TA = 0, CRCX_TB = 1024, CRCX_TW = 2048, CRCX_WORDS = 2048 + 3 * 128;
+#ifndef PBX_CRC_SLICES
+#define PBX_CRC_SLICES 4  // k_encode's CRC: slicing-by-4 (8: slicing-by-8, measured slower: r03_p7)
+#endif
+static_assert(PBX_CRC_SLICES == 4 || PBX_CRC_SLICES == 8, "slicing by 4 or 8");
 template <class C>
 struct EncSmem {
     union {
@@ -113,16 +117,16 @@ struct EncSmem {
     uint32_t w_nm[C::NW];
     uint32_t lcode[289], dcode[32];  // slot form; lcode[288] = no token
     alignas(16) uint32_t out[(C::OUTW + 3) & ~3];
-    alignas(16) uint32_t crc_t[4][256];
+    alignas(16) uint32_t crc_t[PBX_CRC_SLICES][256];
     uint32_t wtot[16];
     uint32_t red[C::NW];
 };
 static_assert(CRCX_WORDS * 4 <= DC::NW * DC::MAXMW * 6, "the CRC combine tables fit the match lists' room");
 static_assert(sizeof(EncSmem<DC>) * 512 <= 40 * 1024 * DC::NT, "32 encode waves per CU (160 KiB LDS)");
 
-// Slicing-by-4 CRC-32 tables, built at compile time into device memory (copied to LDS).
+// Slicing-by-4 (or 8) CRC-32 tables, built at compile time into device memory (copied to LDS).
 struct CrcTables {
-    uint32_t t[4][256];
+    uint32_t t[PBX_CRC_SLICES][256];
 };
 constexpr uint32_t crc_entry_c(uint32_t n) {
     uint32_t c = n;
@@ -132,7 +136,7 @@ constexpr uint32_t crc_entry_c(uint32_t n) {
 constexpr CrcTables make_crc_tables() {
     CrcTables T{};
     for (uint32_t i = 0; i < 256; i++) T.t[0][i] = crc_entry_c(i);
-    for (int k = 1; k < 4; k++)
+    for (int k = 1; k < PBX_CRC_SLICES; k++)
         for (uint32_t i = 0; i < 256; i++) T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xFF];
     return T;
 }
@@ -793,7 +797,26 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         const uint32_t p = ss + k;
         const uint32_t rem = se - p;
         const uint32_t maxlen = rem < 258 ? rem : 258;
-        if (L >= (uint32_t)C::CAP && L < maxlen) {
+#ifndef PBX_LZ_MASKEXT
+#define PBX_LZ_MASKEXT 1  // extend capped matches from the lanes' equality masks (0: LDS compare)
+#endif
+        if (PBX_LZ_MASKEXT && C::CAP == 32 && L >= (uint32_t)C::CAP && L < maxlen) {
+            // the run of the chosen candidate's equality bits from position k over the wave's
+            // masks: the rest of lane t, the whole lanes after it (a ballot of all-ones masks),
+            // and the first bits of the next lane; masked bits (past se) end it, so capped at
+            // maxlen it is the length the byte compare below finds
+            static_assert(NCAND == 3, "three candidate masks");
+            const uint32_t es = Dc == 0 ? exlo[0] : Dc == 1 ? exlo[1] : exlo[2];
+            const uint64_t full = __ballot(es == 0xFFFFFFFFu);
+            uint32_t run = 32 - i;  // a capped length of CAP = 32: the rest of lane t is equal
+            if (t < 63) {
+                const uint32_t nf = (uint32_t)__builtin_ctzll(~(full >> (t + 1)));  // whole lanes after t
+                const uint32_t t2 = t + 1 + nf;  // the first lane that is not (all its bits < 32)
+                run += 32 * nf;
+                if (t2 < 64) run += (uint32_t)__builtin_ctz(~(uint32_t)__builtin_amdgcn_readlane(es, t2));
+            }
+            L = __builtin_amdgcn_readfirstlane(run < maxlen ? run : maxlen);
+        } else if (L >= (uint32_t)C::CAP && L < maxlen) {
             // one wave-wide compare of 4 bytes per lane extends the match past the cap
             const uint32_t a = sp.wl + p, off = L + 4 * lane;
             const uint32_t x = off < maxlen ? (lds_ld4(S, a - D + off) ^ lds_ld4(S, a + off)) : 0u;
@@ -895,7 +918,9 @@ __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, c
         hg[i] = v;
     }
     uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
-    if (tid < (uint32_t)C::NW) mg[tid] = S.w_nm[tid];
+    const uint32_t nmw = S.w_nm[tid & (uint32_t)(C::NW - 1)];
+    if (tid < (uint32_t)C::NW) mg[tid] = nmw;
+    if (__builtin_amdgcn_ballot_w64(nmw != 0) == 0) return;  // no wave kept a match (noise)
     for (uint32_t i = tid; i < (uint32_t)(C::NW * C::MAXMW); i += C::NT) {
         if (i % C::MAXMW < S.w_nm[i / C::MAXMW]) {
             const uint32_t r = S.mrl[i], c = r >> 19;
@@ -1685,6 +1710,15 @@ struct LdsBitWriter {
 };
 
 // Slicing-by-4 CRC step over one little-endian word.
+// Slicing-by-8 CRC step over two little-endian words: the second word's four lookups do not
+// depend on the running CRC, so a chain of 8 bytes is one round of dependent LDS reads, not two.
+template <class SM>
+__device__ __forceinline__ uint32_t crc_word2(const SM& S, uint32_t c, uint32_t v0, uint32_t v1) {
+    static_assert(sizeof(S.crc_t) / sizeof(S.crc_t[0]) == 8, "slicing-by-8 tables");
+    c ^= v0;
+    return (S.crc_t[7][c & 0xFF] ^ S.crc_t[6][(c >> 8) & 0xFF] ^ S.crc_t[5][(c >> 16) & 0xFF] ^ S.crc_t[4][c >> 24]) ^
+           (S.crc_t[3][v1 & 0xFF] ^ S.crc_t[2][(v1 >> 8) & 0xFF] ^ S.crc_t[1][(v1 >> 16) & 0xFF] ^ S.crc_t[0][v1 >> 24]);
+}
 template <class SM>
 __device__ __forceinline__ uint32_t crc_word(const SM& S, uint32_t c, uint32_t v) {
     c ^= v;
@@ -1705,10 +1739,15 @@ __device__ __forceinline__ uint32_t crc_chunk_aligned(uint32_t tid, const SM& S,
         const uint4 q = *(const uint4*)&S.out[k];
         uint32_t v[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
+        for (uint32_t j = 0; j < 4; j++)
             if (k + j == (zb >> 2)) v[j] &= ~(0xFFu << (8 * (zb & 3)));
-            c = crc_word(S, c, v[j]);
-        }
+#if PBX_CRC_SLICES == 8
+        c = crc_word2(S, c, v[0], v[1]);
+        c = crc_word2(S, c, v[2], v[3]);
+#else
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) c = crc_word(S, c, v[j]);
+#endif
     };
     if (tid == 0) {
         for (int32_t k = 0; k < hi; k += 4) step((uint32_t)k);  // its chunk and everything before
@@ -1923,7 +1962,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     // the block header (first segment of a Huffman block): word tid, OR-ed in at bit SH + 32 tid
     const bool hdr = first && !stored;
     const uint32_t hraw = cg[320 + (tid < (uint32_t)C::HDRW ? tid : (uint32_t)C::HDRW - 1)];
-    {
+    if (__builtin_amdgcn_readfirstlane(nmw) != 0) {  // uniform: most waves on noise keep no match
         static_assert(C::MAXMW == 256, "four match slots per lane");
         const uint32_t* gp = mg + C::NW + w * C::MAXMW;
         const uint32_t* gd = mg + C::NW + C::NW * C::MAXMW + w * C::MAXMW;
@@ -1961,7 +2000,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         for (int i = 0; i < C::CH + 2; i += 2) nbits += (slot[i] >> 27) + (slot[i + 1] >> 27);
     }
     // the slicing tables (needed after barrier 3): loaded now, stored before barrier 2
-    if (tid < 256) ((uint4*)&S.crc_t[0][0])[tid] = ((const uint4*)&kCrcTables.t[0][0])[tid];
+    if (tid < 64 * PBX_CRC_SLICES) ((uint4*)&S.crc_t[0][0])[tid] = ((const uint4*)&kCrcTables.t[0][0])[tid];
     if (PROF) {  // diagnostics: slots built (wave 0)
         __builtin_amdgcn_s_waitcnt(0);
         stamp();

@@ -28,15 +28,25 @@ def _streams():
     wide[1::2] = wide[0::2]
     out.append(("wide16", pbx.UINT16, wide))
     out.append(("narrow8", pbx.UINT8, rng.integers(0, 2, (400, 3)).astype(np.uint8)))
+    # the headline geometry (rows of whole 16-byte chunks: k_lz77's fast fill, three-row
+    # blocks for 16-bit samples): 12-bit noise, and rows repeated in runs (matches extended
+    # past the cap from the lanes' equality masks)
+    out.append(("noise512", pbx.UINT16, rng.integers(0, 4096, (80, 512)).astype(">u2")))
+    rep = np.repeat(rng.integers(0, 65536, (10, 512)), 8, axis=0).astype(">u2")
+    rep[5::13] = rng.integers(0, 65536, (len(rep[5::13]), 512))
+    out.append(("rowrep512", pbx.UINT16, rep))
     return out
 
 
-@pytest.mark.parametrize("case", range(7))
+@pytest.mark.parametrize("case", range(9))
 def test_gpu_lz77_matches_emulator(service, case):
     name, pt, a = _streams()[case]
     h, w = a.shape
     iid = 9100 + case
-    service.register_plane(iid, 0, 0, 0, pt, w, h, data=a, big_endian=True)
+    if name.endswith("512"):  # little-endian plane: the byte-swapping fill (the headline's)
+        service.register_plane(iid, 0, 0, 0, pt, w, h, data=a.astype("<u2"), big_endian=False)
+    else:
+        service.register_plane(iid, 0, 0, 0, pt, w, h, data=a, big_endian=True)
     b = pbx.Batch(service, [pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="png")])
     b.launch()
     b.sync()
