@@ -646,6 +646,26 @@ __device__ __forceinline__ uint32_t zero_nibble(uint32_t x) {
     return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
 }
 
+#ifndef PBX_LZ_DOT4PACK
+#define PBX_LZ_DOT4PACK 1  // equality bits packed by v_dot4 (0: shifts and ORs per word)
+#endif
+// Zero bytes of the eight words x[j] as 32 bits (bit 4j + k: byte k of x[j] is zero).  Each
+// word's zero-byte flags sit at bit 7 of its bytes (0 or 128 as a byte); one v_dot4_u32_u8
+// against the weights 1, 2, 4, 8 (or 16 .. 128 for the second word of a pair) sums them into
+// 128 x the pair's eight bits: two dot products, a shift and an OR per pair of words instead
+// of four shifts and three ORs per word.
+__device__ __forceinline__ uint32_t pack_zero_bytes8(const uint32_t (&x)[8]) {
+    uint32_t e = 0;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const uint32_t za = ~(((x[2 * p] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x[2 * p]) & 0x80808080u;
+        const uint32_t zb = ~(((x[2 * p + 1] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x[2 * p + 1]) & 0x80808080u;
+        const uint32_t b = dot4_u8(za, 0x08040201u, dot4_u8(zb, 0x80402010u, 0u)) >> 7;
+        e |= b << (8 * p);
+    }
+    return e;
+}
+
 // Parse of wave w's sub-segment (scalar twin: ph_parse_emu in deflate_seg.h).  Lane l holds
 // positions p0 = ss + 32 l .. p0 + 31 (its thread chunk).  Per candidate distance d the lane
 // builds E_d, bit i = (byte p0+i == byte p0+i-d), masked to valid positions (< se, d not
@@ -682,8 +702,15 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         if (d) {
             if (c < 2) {  // d = 1, 2: the lane's own words shifted by d bytes
                 const uint32_t sh = 32 - 8 * d;
+                if (PBX_LZ_DOT4PACK) {
+                    uint32_t xw[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh)) << (4 * j);
+                    for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh);
+                    e = pack_zero_bytes8(xw);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh)) << (4 * j);
+                }
             } else {  // one row up: unaligned words at a0 - d
                 const int32_t b = (int32_t)a0 - (int32_t)d;
                 const int32_t r = b >> 2;
@@ -719,8 +746,15 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                     for (int j = 0; j < 9; j++) rw[j] = q12[j + 3];
                     break;
                 }
+                if (PBX_LZ_DOT4PACK) {
+                    uint32_t xw[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
+                    for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh);
+                    e = pack_zero_bytes8(xw);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
+                }
             }
             const uint32_t vm = a0 >= d ? 0xFFFFFFFFu : (d - a0 >= 32 ? 0u : 0xFFFFFFFFu << (d - a0));
             e &= vm & smask;
