@@ -692,7 +692,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0;
-    uint64_t cvb = 0;  // bytes inside some paying run (the walk's coverage bound, below)
+    uint32_t cvb_lo = 0, cvb_hi = 0;  // bytes inside some paying run (the walk's coverage bound, below)
 #pragma unroll
     for (int c = 0; c < NCAND; c++) {
         const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
@@ -764,16 +764,18 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         exlo[c] = e;
         exhi[c] = nx;
         if (d) {
-            const uint64_t x = ((uint64_t)nx << 32) | e;
-            uint64_t r = x & (x >> 1) & (x >> 2);
-            if (ml[c] >= 4) r &= x >> 3;
-            if (ml[c] >= 6) r &= (x >> 4) & (x >> 5);
-            M |= (uint32_t)r;
-            const uint64_t r32 = (uint32_t)r;  // [j, j + ml) for every paying start j of the lane
-            uint64_t D = r32 | (r32 << 1) | (r32 << 2);
-            if (ml[c] >= 4) D |= r32 << 3;
-            if (ml[c] >= 6) D |= (r32 << 4) | (r32 << 5);
-            cvb |= D;
+            // (E | next lane's E << 32) >> k, low word: one funnel shift (v_alignbit) each
+            uint32_t r = e & __builtin_amdgcn_alignbit(nx, e, 1) & __builtin_amdgcn_alignbit(nx, e, 2);
+            if (ml[c] >= 4) r &= __builtin_amdgcn_alignbit(nx, e, 3);
+            if (ml[c] >= 6) r &= __builtin_amdgcn_alignbit(nx, e, 4) & __builtin_amdgcn_alignbit(nx, e, 5);
+            M |= r;
+            // [j, j + ml) for every paying start j of the lane: bits inside the lane (lo) and
+            // the ones past its end (hi)
+            uint32_t dlo = r | (r << 1) | (r << 2), dhi = (r >> 31) | (r >> 30);
+            if (ml[c] >= 4) { dlo |= r << 3; dhi |= r >> 29; }
+            if (ml[c] >= 6) { dlo |= (r << 4) | (r << 5); dhi |= (r >> 28) | (r >> 27); }
+            cvb_lo |= dlo;
+            cvb_hi |= dhi;
         }
     }
 #ifndef PBX_LZ_COVBOUND
@@ -785,7 +787,8 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     // most the wave's count of such bytes (per lane, bytes past the lane's chunk counted too:
     // an overestimate), and below MINCOV the walk would drop all its matches (noise: most
     // waves hold a few 3-4 byte runs): the same result without the walk.
-    if (PBX_LZ_COVBOUND && wave_sum((uint32_t)__builtin_popcountll(cvb)) < (uint32_t)C::MINCOV) {
+    if (PBX_LZ_COVBOUND &&
+        wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) < (uint32_t)C::MINCOV) {
         if (lane == 0) S.w_nm[w] = 0;
         return;
     }
