@@ -57,14 +57,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(v, off, 64);
-        if (lane >= (uint32_t)off) v += t;
-    }
-    return v;
-}
+// (every lane active at the call, as DPP reads its source lanes' registers)
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t /*lane*/) { return wave_incl_scan_dpp(v); }
 
 // Exclusive prefix sum of arr[0..NT) in place (one element per thread); returns the total.
 template <int NT>
@@ -94,7 +88,7 @@ __device__ uint32_t wave_scan_excl_add(uint32_t* arr, uint32_t lane) {
 #pragma unroll
     for (int k = 0; k < K; k++) { v[k] = arr[lane * K + k]; s += v[k]; }
     const uint32_t inc = wave_incl_add(s, lane);
-    const uint32_t tot = __shfl(inc, 63, 64);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     uint32_t run = inc - s;
 #pragma unroll
     for (int k = 0; k < K; k++) { arr[lane * K + k] = run; run += v[k]; }

@@ -1126,8 +1126,37 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
 }
 
 // ==================================================================== k_huff
+// x of lane (lane ^ M) without an LDS round trip: DPP quad permutes (1, 2), two row shifts
+// and a select (4), a row rotate (8), gfx950's permlane swaps and a select (16, 32).
+template <uint32_t M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    } else if constexpr (M == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x104, 0xF, 0xF, false);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+        return (lane & 4u) ? dn : up;
+    } else if constexpr (M == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (M == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16u) ? p[0] : p[1];
+    } else {
+        static_assert(M == 32, "lane distances 1 .. 32");
+        const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32u) ? p[0] : p[1];
+    }
+}
+template <uint32_t M>
+__device__ __forceinline__ void lane_xor8(const uint32_t (&v)[8], uint32_t (&o)[8], uint32_t lane) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) o[r] = lane_xor<M>(v[r], lane);
+}
+
 // Ascending sort of the KEYN keys (padded to 512 with KEY_NONE) by one wave: 8 per lane (lane*8 + r), partners at distance
-// j >= 8 by shuffle, j < 8 inside the lane's registers.
+// j >= 8 by lane exchanges (lane_xor, no LDS), j < 8 inside the lane's registers.
 __device__ __forceinline__ void sort512_wave(uint32_t* keys, uint32_t lane) {
     uint32_t v[8];
 #pragma unroll
@@ -1137,9 +1166,18 @@ __device__ __forceinline__ void sort512_wave(uint32_t* keys, uint32_t lane) {
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             if (j >= 8) {
+                uint32_t ox[8];
+                switch (j >> 3) {
+                case 1: lane_xor8<1>(v, ox, lane); break;
+                case 2: lane_xor8<2>(v, ox, lane); break;
+                case 4: lane_xor8<4>(v, ox, lane); break;
+                case 8: lane_xor8<8>(v, ox, lane); break;
+                case 16: lane_xor8<16>(v, ox, lane); break;
+                default: lane_xor8<32>(v, ox, lane); break;
+                }
 #pragma unroll
                 for (int r = 0; r < 8; r++) {
-                    const uint32_t o = __shfl_xor(v[r], (int)(j >> 3), 64);
+                    const uint32_t o = ox[r];
                     const uint32_t e = lane * 8 + r;
                     const bool up = (e & k) == 0, lower = (e & j) == 0;
                     v[r] = (lower == up) ? (v[r] < o ? v[r] : o) : (v[r] < o ? o : v[r]);
@@ -1334,14 +1372,20 @@ __device__ __forceinline__ void assign_wave(SM& S, uint32_t lane) {
             hdist = sym + 1 > hdist ? sym + 1 : hdist;
         }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        dyn += __shfl_xor(dyn, off, 64);
-        fix += __shfl_xor(fix, off, 64);
-        const uint32_t h1 = __shfl_xor(hlit, off, 64), h2 = __shfl_xor(hdist, off, 64);
+    auto xstep = [&](auto m) {  // one butterfly level of the sums and maxima (lane_xor, no LDS)
+        constexpr uint32_t M = decltype(m)::value;
+        dyn += lane_xor<M>(dyn, lane);
+        fix += lane_xor<M>(fix, lane);
+        const uint32_t h1 = lane_xor<M>(hlit, lane), h2 = lane_xor<M>(hdist, lane);
         hlit = h1 > hlit ? h1 : hlit;
         hdist = h2 > hdist ? h2 : hdist;
-    }
+    };
+    xstep(std::integral_constant<uint32_t, 32>{});
+    xstep(std::integral_constant<uint32_t, 16>{});
+    xstep(std::integral_constant<uint32_t, 8>{});
+    xstep(std::integral_constant<uint32_t, 4>{});
+    xstep(std::integral_constant<uint32_t, 2>{});
+    xstep(std::integral_constant<uint32_t, 1>{});
     if (lane == 0) {
         S.misc[M_DYNBITS] = dyn; S.misc[M_FIXBITS] = fix;
         S.misc[M_HLIT] = hlit; S.misc[M_HDIST] = hdist;
