@@ -620,23 +620,52 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
     for (uint32_t k = nb4 / 4 + tid; k < nz / 4; k += NT) buf[k] = 0;
 }
 
+// fill_fast's sample conversion for a tile's geometry, + 1 (0: not its case -- rows not whole
+// 16-byte chunks, more than 64 chunks a row, 8-byte samples, a flip with a swap of 4 bytes).
+__device__ __forceinline__ uint32_t fast_fill_mode(const DirectRows& dr) {
+    if (!dr.aligned || dr.ngrp != 1 || dr.bpp > 4) return 0u;
+    const uint32_t sb = dr.swap ? (uint32_t)dr.bpp : 0u;
+    const uint32_t mode = (sb == 1 ? 0u : sb) * 2 + (dr.flip ? 1u : 0u);
+    return (mode == 0 || mode == 1 || mode == 4 || mode == 5 || mode == 8) ? mode + 1 : 0u;
+}
+
+// fill_fast for a mode of fast_fill_mode (!= 0)
+template <int NT>
+__device__ __forceinline__ void fill_fast_mode(uint32_t mode, uint32_t* buf, const DirectRows& dr, uint32_t B,
+                                               uint32_t nb, uint32_t nz, uint32_t tid, uint32_t ra, uint32_t rz,
+                                               uint8_t* gseg, uint32_t wl) {
+    switch (mode) {
+    case 1: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); break;
+    case 2: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); break;
+    case 5: fill_fast<NT, 2, false, PBX_FF_FR4>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); break;
+    case 6: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); break;
+    default: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); break;
+    }
+}
+
 // fill_fast for the tile's sample conversion; false when the geometry is not its case
 template <int NT>
 __device__ __forceinline__ bool fill_fast_any(uint32_t* buf, const DirectRows& dr, uint32_t B, uint32_t nb,
                                               uint32_t nz, uint32_t tid, uint8_t* gseg, uint32_t wl) {
-    if (!dr.aligned || dr.ngrp != 1 || dr.bpp > 4) return false;
+    const uint32_t mode = fast_fill_mode(dr);
+    if (!mode) return false;
     const uint32_t ra = div_rcp(B, dr.rowlen, dr.rcp), rz = div_rcp(B + nb - 1, dr.rowlen, dr.rcp);
-    const uint32_t sb = dr.swap ? (uint32_t)dr.bpp : 0u;
-    const uint32_t mode = (sb == 1 ? 0u : sb) * 2 + (dr.flip ? 1u : 0u);
-    switch (mode) {
-    case 0: fill_fast<NT, 0, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    case 1: fill_fast<NT, 0, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    case 4: fill_fast<NT, 2, false, PBX_FF_FR4>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    case 5: fill_fast<NT, 2, true>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    case 8: fill_fast<NT, 4, false>(buf, dr, B, nb, nz, tid, ra, rz, gseg, wl); return true;
-    default: return false;
-    }
+    fill_fast_mode<NT>(mode, buf, dr, B, nb, nz, tid, ra, rz, gseg, wl);
+    return true;
 }
+
+#ifndef PBX_LZ_FAST_FILL
+#define PBX_LZ_FAST_FILL 1  // fill_fast for the common geometry (0: the general fill only)
+#endif
+// 1: for direct tiles of fill_fast's geometry k_encode rebuilds the segment's bytes from the
+// plane (each wave its 2 KiB, through its part of the LDS output buffer) and k_lz77 writes no
+// stream bytes for them -- the stream's HBM round trip (every byte written, read back) gone.
+// Correct (every -m gpu test green) but slower: k_lz77 1.48 -> 1.36 ms, k_encode 1.57 ->
+// 1.92 ms, the conversion's VALU in the issue-bound encoder (profiles/r03_p17/).  0 (default):
+// k_lz77 stores the bytes from its fill registers and k_encode reads them back.
+#ifndef PBX_ENC_FROM_PLANE
+#define PBX_ENC_FROM_PLANE 0
+#endif
 
 // ==================================================================== k_lz77
 // Zero bytes of x as 4 bits (bit j: byte j of x is zero).
@@ -1008,9 +1037,6 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
 #ifndef PBX_LZ_SKIP_STORE
 #define PBX_LZ_SKIP_STORE 0  // timing experiments only (scripts/variants.sh): wrong output
 #endif
-#ifndef PBX_LZ_FAST_FILL
-#define PBX_LZ_FAST_FILL 1  // fill_fast for the common geometry (0: the general fill only)
-#endif
 #ifndef PBX_LZ_SKIP_FILL
 #define PBX_LZ_SKIP_FILL 0  // timing experiments only (scripts/variants.sh): wrong output
 #endif
@@ -1018,8 +1044,10 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     if (PBX_LZ_SKIP_FILL) {
     } else if (direct && PBX_LZ_FAST_FILL &&
                fill_fast_any<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid,
-                                    PBX_LZ_SKIP_STORE ? nullptr : stream + d.out_off + sp.base + sp.wl, sp.wl)) {
-        stored = true;
+                                    PBX_LZ_SKIP_STORE || PBX_ENC_FROM_PLANE ? nullptr
+                                                                            : stream + d.out_off + sp.base + sp.wl,
+                                    sp.wl)) {
+        stored = true;  // (or not needed: k_encode reads the plane)
         if (PROF) stamp();
     } else if (direct) {
         FillPre<LZ_PF> pf;
@@ -1970,8 +1998,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
                                                   const uint32_t* __restrict__ codes,
                                                   const uint64_t* __restrict__ offs,
                                                   uint8_t* __restrict__ out,
-                                                  uint64_t* __restrict__ stamps) {
+                                                  uint64_t* __restrict__ stamps,
+                                                  uint32_t uniform_nseg, uint32_t uniform_rcp) {
     static_assert(C::CH == 32 && C::CRCC == 32, "two 16-byte loads per thread chunk");
+    static_assert(C::SUB == 64 * C::CH && C::NW * C::SUB <= 4 * C::OUTW, "a wave's bytes staged in its part of out[]");
     __shared__ EncSmem<C> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2001,6 +2031,11 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         __builtin_memcpy((uint4*)&gi + 3, &g3, 16);
         __builtin_memcpy((uint4*)&gi + 4, &g4, 16);
     }
+    // the tile (its plane rows, PBX_ENC_FROM_PLANE): in round 1 too when every tile has the
+    // same number of segments
+    const TileDesc d = PBX_ENC_FROM_PLANE
+                           ? load_desc(dt + (uniform_nseg ? div_rcp(seg, uniform_nseg, uniform_rcp) : gi.tile))
+                           : TileDesc{};
     const uint32_t ti = gi.tile;
     SegParams sp;  // the encoder holds the segment only (no window)
     sp.base = 0;
@@ -2023,7 +2058,34 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     // round 2: the thread's chunk bytes (zero past the segment: loads past it read the
     // segment start instead, no branch), the wave's matches, the block's codes and header
     uint32_t cb[C::CH / 4];
-    {
+    DirectRows dr;
+    dr.init(d);
+    const uint32_t fmode = PBX_ENC_FROM_PLANE && PBX_LZ_FAST_FILL && (d.flags & TF_DIRECT) ? fast_fill_mode(dr) : 0u;
+    if (fmode) {
+        // k_lz77 stored no bytes: the wave converts its 2 KiB of the segment from the plane
+        // rows into its part of out[] (fill_fast as one 64-thread group, zero past the
+        // segment), each lane reads its 32 bytes back and zeroes them.  Wave-local: the LDS
+        // operations of one wave complete in order.
+        uint32_t* wbuf = S.out + w * (C::SUB / 4);
+        const uint32_t wb = w * C::SUB;
+        if (wb < sp.sl) {
+            const uint32_t nbw = sp.sl - wb < (uint32_t)C::SUB ? sp.sl - wb : (uint32_t)C::SUB;
+            const uint32_t B = (uint32_t)(seg_off - d.out_off) + wb;  // tile stream offset
+            const uint32_t ra = div_rcp(B, dr.rowlen, dr.rcp), rz = div_rcp(B + nbw - 1, dr.rowlen, dr.rcp);
+            fill_fast_mode<64>(fmode, wbuf, dr, B, nbw, C::SUB, lane, ra, rz, nullptr, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint4 q0 = *(const uint4*)&wbuf[8 * lane], q1 = *(const uint4*)&wbuf[8 * lane + 4];
+            cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
+            cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < C::CH / 4; k++) cb[k] = 0;
+        }
+        *(uint4*)&wbuf[8 * lane] = make_uint4(0, 0, 0, 0);
+        *(uint4*)&wbuf[8 * lane + 4] = make_uint4(0, 0, 0, 0);
+    } else {
         const uint32_t cs = tid * C::CH;
         const uint4 q0 = *(const uint4*)(stream + seg_off + (cs < sp.sl ? cs : 0u));
         const uint4 q1 = *(const uint4*)(stream + seg_off + (cs + 16 < sp.sl ? cs + 16 : 0u));
@@ -2066,9 +2128,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     if (lane == 0) S.w_nm[w] = nmw;
     if (tid < 288) S.lcode[tid] = slot_from_code(craw); else if (tid < 320) S.dcode[tid - 288] = slot_from_code(craw);
     if (tid == 0) S.lcode[SLOT_NONE] = 0;
-    {   // zero the output words
+    {   // zero the output words (with the bytes from the plane: past the waves' staging parts)
         uint4* o4 = (uint4*)S.out;
-        for (uint32_t k = tid; k < (uint32_t)(sizeof(S.out) / 16); k += C::NT) o4[k] = make_uint4(0, 0, 0, 0);
+        const uint32_t k0 = fmode ? (uint32_t)(C::NW * C::SUB / 16) : 0u;
+        for (uint32_t k = k0 + tid; k < (uint32_t)(sizeof(S.out) / 16); k += C::NT) o4[k] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     stamp();  // diagnostics: inputs in LDS
@@ -2429,10 +2492,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     if (ev2) (void)hipEventRecord(ev2[2], st);
     if (prof)
         hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
+                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
+                           a.uniform_nseg, a.uniform_rcp);
     else
         hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps);
+                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
+                           a.uniform_nseg, a.uniform_rcp);
     if (ev) (void)hipEventRecord(ev[3], st);
     if (ev2) (void)hipEventRecord(ev2[3], st);
     hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
