@@ -27,6 +27,17 @@ __device__ __forceinline__ void gstore16(void* p, const uint4& v) {
     *(__attribute__((address_space(1))) pbx_v4u*)p = x;
 }
 
+// Streaming forms (nontemporal: data read or written once, not kept in the caches).
+__device__ __forceinline__ uint4 gload16_nt(const void* p) {
+    const pbx_v4u v = __builtin_nontemporal_load((const __attribute__((address_space(1))) pbx_v4u*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16_nt(void* p, const uint4& v) {
+    pbx_v4u x;
+    x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    __builtin_nontemporal_store(x, (__attribute__((address_space(1))) pbx_v4u*)p);
+}
+
 // Bijective XCD-aware remap: consecutive logical ids land on the same XCD (shared L2),
 // since workgroups are dealt round-robin over the 8 XCDs.  Speed only, never correctness.
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {

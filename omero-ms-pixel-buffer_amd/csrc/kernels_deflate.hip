@@ -532,6 +532,9 @@ __device__ __forceinline__ void fill_finish(const FillPre<K>& pf, uint32_t* buf,
 #ifndef PBX_FF_FR4
 #define PBX_FF_FR4 3  // 16-bit samples without the sign flip (the headline): three rows, one load round for 18 rows
 #endif
+#ifndef PBX_NT_STREAM
+#define PBX_NT_STREAM 0  // nontemporal accesses: 1 k_lz77's stream stores, 2 k_encode's stream loads, 4 its output stores
+#endif
 // gseg (optional): the segment's bytes (buffer bytes [wl, nb)) are also stored there, from
 // the same registers (k_encode's input), instead of re-read from LDS after the fill.
 template <int NT, uint32_t SB, bool FL, uint32_t FR = PBX_FF_FR>
@@ -563,12 +566,16 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
             v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
         }
         *(uint4*)(bb + at) = v;
-        if (gseg && at >= (int32_t)wl) gstore16(gseg + (at - (int32_t)wl), v);
+        if (gseg && at >= (int32_t)wl) {
+            if (PBX_NT_STREAM & 1) gstore16_nt(gseg + (at - (int32_t)wl), v); else gstore16(gseg + (at - (int32_t)wl), v);
+        }
     };
     // interior word: no clipping in LDS, the global copy for segment bytes only
     auto put_in = [&](int32_t at, uint4 v) {
         *(uint4*)(bb + at) = v;
-        if (gseg && at >= (int32_t)wl) gstore16(gseg + (at - (int32_t)wl), v);
+        if (gseg && at >= (int32_t)wl) {
+            if (PBX_NT_STREAM & 1) gstore16_nt(gseg + (at - (int32_t)wl), v); else gstore16(gseg + (at - (int32_t)wl), v);
+        }
     };
     // wave w: blocks of FR consecutive rows, w, w + NW, ...; the chunk before a block's first
     // row is one extra load, before its other rows the previous row's last chunk (a readlane)
@@ -2087,8 +2094,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         *(uint4*)&wbuf[8 * lane + 4] = make_uint4(0, 0, 0, 0);
     } else {
         const uint32_t cs = tid * C::CH;
-        const uint4 q0 = *(const uint4*)(stream + seg_off + (cs < sp.sl ? cs : 0u));
-        const uint4 q1 = *(const uint4*)(stream + seg_off + (cs + 16 < sp.sl ? cs + 16 : 0u));
+        const uint8_t* p0 = stream + seg_off + (cs < sp.sl ? cs : 0u);
+        const uint8_t* p1 = stream + seg_off + (cs + 16 < sp.sl ? cs + 16 : 0u);
+        const uint4 q0 = (PBX_NT_STREAM & 2) ? gload16_nt(p0) : *(const uint4*)p0;
+        const uint4 q1 = (PBX_NT_STREAM & 2) ? gload16_nt(p1) : *(const uint4*)p1;
         cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
         cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
 #pragma unroll
@@ -2282,9 +2291,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
                 for (int i = 0; i < 5; i++) q[i] = z[i + 3];
                 break;
             }
-            *(uint4*)(dst + head + 16 * k) =
+            const uint4 ov =
                 make_uint4(__builtin_amdgcn_alignbyte(q[1], q[0], sb), __builtin_amdgcn_alignbyte(q[2], q[1], sb),
                            __builtin_amdgcn_alignbyte(q[3], q[2], sb), __builtin_amdgcn_alignbyte(q[4], q[3], sb));
+            if (PBX_NT_STREAM & 4) gstore16_nt(dst + head + 16 * k, ov); else *(uint4*)(dst + head + 16 * k) = ov;
         }
         for (uint32_t j = head + 16 * n16 + tid; j < nbytes; j += C::NT) dst[j] = (uint8_t)out_byte_at(S, b0 + j);
     } else {
