@@ -1533,7 +1533,10 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
     if (lane == 0) S.misc[M_HCLEN] = hclen < 4 ? 4u : hclen;
 }
 
-constexpr uint32_t HUFF_LDSEG = 4;  // k_huff: segments whose histogram loads are in flight together
+#ifndef PBX_HUFF_LDSEG
+#define PBX_HUFF_LDSEG 12  // 4: 0.215 ms, 8: 0.213, 12: 0.208 (profiles/r03_p19/; VGPRs 51 -> 73, occupancy still set by LDS)
+#endif
+constexpr uint32_t HUFF_LDSEG = PBX_HUFF_LDSEG;  // k_huff: segments whose histogram loads are in flight together
 
 // One Huffman block = the BLK_SEGS (or fewer, at a tile's end) consecutive segments of
 // one tile whose histograms it sums; one wave per block.
