@@ -344,7 +344,7 @@ struct HuffWork {  // the 19-symbol code-length code (one thread)
     uint32_t cllen[19], clcode[19], clfreq[19], clsort[19];
 };
 
-// Node indices, depths and internal weights (<= SEG + 2) fit 16 bits.  (The RLE counts,
+// Node indices and depths fit 16 bits (internal weights, up to a block's symbol count, do not).  (The RLE counts,
 // rcnt[RLEN], are a member of the phases' state struct itself.)
 struct HuffScratch {
     uint32_t skey[KEYN];

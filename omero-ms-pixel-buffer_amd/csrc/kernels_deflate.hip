@@ -72,7 +72,14 @@ struct HuffScratchDev {
     uint32_t skey[KEYN];
     Split2<uint32_t, 288, 32> rec;      // step s: li0 | qi0 << 10 | cnt << 20
     Split2<uint16_t, 288, 32> leafpar;  // (merge rounds: the merged prefix)
-    Split2<uint16_t, 288, 32> aA, dB;
+    union {
+        struct {
+            Split2<uint16_t, 288, 32> aA, dB;
+        };
+        // merge rounds: the internal nodes' weights, 32-bit (a block of up to BLK_SEGS
+        // segments counts far more than 65535 symbols); aA and dB are written after them
+        Split2<uint32_t, 288, 32> iw;
+    };
     Split2<uint16_t, 290, 34> rst;      // first internal node of every merge round (+ the end)
 };
 
@@ -1247,7 +1254,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
     const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
     const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
     const uint32_t* sk = S.hs.skey + base;
-    uint16_t* iq = S.hs.dB[T];        // internal weights (dB is free until the depth rounds)
+    uint32_t* iq = S.hs.iw[T];        // internal weights (aA, dB are free until the parents)
     uint16_t* M = S.hs.leafpar.v;     // merged prefix: leaf index | 0x8000, or internal index
     uint32_t* rq = S.hs.rec[T];
     uint16_t* rs = S.hs.rst[T];
@@ -1256,7 +1263,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
         return;
     }
     if (lane == 0) {
-        iq[0] = (uint16_t)(key_weight(sk[0]) + key_weight(sk[1]));
+        iq[0] = key_weight(sk[0]) + key_weight(sk[1]);
         rq[0] = 2u << 20;
         rs[0] = 0;
     }
@@ -1277,7 +1284,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
         const uint32_t b = ni - qi, P = a + b;
         if (P == 1) {  // the lone internal node qi pairs with the next leaf
             if (lane == 0) {
-                iq[ni] = (uint16_t)(iq[qi] + key_weight(sk[li]));
+                iq[ni] = iq[qi] + key_weight(sk[li]);
                 rq[ni] = li | (qi << 10) | (1u << 20);
             }
             li++; qi++; ni++;
@@ -1314,7 +1321,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
             const uint32_t w1 = (x1 & 0x8000u) ? key_weight(sk[x1 & 0x7FFFu]) : iq[x1];
             const uint32_t lb = leaves_before(2 * k, x0);
             const uint32_t cnt = (x0 >> 15) + (x1 >> 15);
-            iq[ni + k] = (uint16_t)(w0 + w1);
+            iq[ni + k] = w0 + w1;
             rq[ni + k] = (li + lb) | ((qi + 2 * k - lb) << 10) | (cnt << 20);
         }
         uint32_t lb = a;
