@@ -4,7 +4,7 @@
 //
 //   k_lz77        512 threads / segment: window + segment in LDS, first-occurrence hash,
 //                 wave-serial greedy/lazy parse, symbol histogram, Adler-32 partials
-//   k_huff        ONE WAVE / Huffman block of up to 16 segments (many per CU): code
+//   k_huff        ONE WAVE / Huffman block of up to 64 segments (many per CU): code
 //                 lengths and canonical codes, code-length RLE, the block header bits, the
 //                 exact output size, every segment's bit range
 //   k_seg_sizes   per tile: segment byte offsets and container size -> k_scan_offsets

@@ -19,13 +19,15 @@ namespace pbx {
 #define PBX_SEG 16384
 #endif
 #ifndef PBX_BLK
-#define PBX_BLK 16
+#define PBX_BLK 64
 #endif
 using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
 constexpr uint32_t BLK_SEGS = PBX_BLK;  // segments per Huffman block at most (filter None, TIFF)
 // With a PNG row filter the byte statistics change from row to row, and smaller blocks
 // whose codes follow them compress better (adaptive filter on noise: 3 segments 382 KB,
-// 16 segments 392 KB per 512x512 uint16 tile).
+// 16 segments 392 KB per 512x512 uint16 tile).  Without a filter one code per tile of up to
+// 64 segments: the same bytes as blocks of 11 on noise (+0.005%), +0.3% on G_FAKE, and a
+// third of the k_huff waves (0.208 -> 0.125 ms per 4096 tiles, profiles/r03_p22-23).
 constexpr uint32_t BLK_SEGS_FILTERED = 3;
 // The planner's longest segment.  A stored Huffman block is one stored block per segment
 // (block_nbytes), so only a segment must fit a stored block's 65535 bytes.
@@ -36,7 +38,7 @@ static_assert(BLK_SEGS >= 1 && BLK_SEGS <= 64 && SPLIT_MAX <= 65535, "a stored b
 PBX_HD uint32_t tile_blocks(uint32_t nseg, uint32_t cap = BLK_SEGS) { return (nseg + cap - 1) / cap; }
 // Block j of a tile's nb blocks holds its segments [block_seg0(j, nseg, nb),
 // block_seg0(j + 1, nseg, nb)): an even split (33 segments of a 512x512 uint16 PNG in
-// three blocks of 11).
+// one block of 33 at the default cap; three blocks of 11 at a cap of 16).
 PBX_HD uint32_t block_seg0(uint32_t j, uint32_t nseg, uint32_t nb) {
     return (uint32_t)((uint64_t)j * nseg / nb);
 }

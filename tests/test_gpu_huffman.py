@@ -22,7 +22,7 @@ def _block_len(h):
 def test_gpu_huffman_matches_emulator(service, which):
     """`random`: uneven histograms whose code-length codes need zlib's 7-bit overflow
     repair several levels deep (test_emu_huffman.random_hists).  `block`: the histograms
-    of whole blocks (11 segments, as in the headline's 512x512 uint16 tiles): symbol counts
+    of whole blocks (11 segments; the headline's 512x512 uint16 tiles make one of 33): symbol counts
     far above 65535, so the merge's internal weights need 32 bits."""
     from test_emu_huffman import random_hists
     if which == "hists":

@@ -368,7 +368,7 @@ def test_png_filters_dword_path(oracle, filt):
 
 
 def test_incompressible_tiles_stored_per_segment(service, adaptive_service, oracle):
-    """Random bytes: every Huffman block (up to 16 segments) is stored, one stored block per
+    """Random bytes: every Huffman block (up to BLK_SEGS segments) is stored, one stored block per
     segment (a block may then hold more than one stored block's 65535 bytes).  PNG and
     deflate-TIFF tiles of 1024^2 uint8 decode exactly and equal the CPU emulation byte for
     byte."""
