@@ -2371,7 +2371,8 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
     const bool tiff = (d.flags & TF_TIFF) != 0;
     const uint32_t zoff = container_zoff(d);
     uint32_t s1 = 0, s2 = 0, payload = 0;
-    for (uint32_t k = 0; k < d.seg_count; k++) {
+#pragma unroll 4
+    for (uint32_t k = 0; k < d.seg_count; k++) {  // (unrolled: four segments' loads in flight)
         const SegInfo& g = info[d.seg_first + k];
         adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.sl);
     }

@@ -276,9 +276,11 @@ constexpr uint32_t ADLER_BASE = 65521u;
 
 // Combine raw partial sums (s1 = sum b, s2 = sum (n-i) b) of L (left) and R (right, lenR bytes).
 PBX_HD void adler_combine(uint32_t& s1L, uint32_t& s2L, uint32_t s1R, uint32_t s2R, uint64_t lenR) {
-    uint64_t s2 = (uint64_t)s2L + (uint64_t)(lenR % ADLER_BASE) * s1L + s2R;
-    s1L = (uint32_t)(((uint64_t)s1L + s1R) % ADLER_BASE);
-    s2L = (uint32_t)(s2 % ADLER_BASE);
+    // (all sums < ADLER_BASE: s2L + lr * s1L + s2R < 2^32, so 32-bit arithmetic suffices)
+    const uint32_t lr = lenR < ADLER_BASE ? (uint32_t)lenR : (uint32_t)(lenR % ADLER_BASE);
+    const uint32_t s2 = s2L + lr * s1L + s2R, s1 = s1L + s1R;
+    s1L = s1 >= ADLER_BASE ? s1 - ADLER_BASE : s1;
+    s2L = s2 % ADLER_BASE;
 }
 
 // Final adler32 value for a stream of total length n with raw sums s1, s2.
