@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 6
+#define PBX_ABI_VERSION 7
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -180,6 +180,30 @@ int pbx_plane_commit(pbx_ctx* ctx, uint64_t plane_id);
 int pbx_plane_lookup(pbx_ctx* ctx, int64_t image_id, int32_t z, int32_t c, int32_t t, int32_t level,
                      uint64_t* plane_id, int32_t* state, int32_t* band_y0, int32_t* band_rows);
 
+/* Sparse planes: region-proportional residency.  The reference reads only the requested region
+ * per request (new byte[w*h*bpp] then getTileDirect(z, c, t, x, y, w, h), TileRequestHandler.java:
+ * 102-109); a whole-slide plane is far larger than one request.  A sparse plane is registered
+ * under its key at once (READY) but holds its rows as bands of `band_rows` rows (band k = rows
+ * [k*band_rows, (k+1)*band_rows)), each loaded on demand, pinned by the batches that read it and
+ * evicted on its own, least recently used first, under the residency budget.  A request whose
+ * rows cover a band that is not resident answers PBX_E_NOT_RESIDENT; the binding loads the
+ * covering bands (rows y .. y+h-1, by pbx_band_write) and retries.  A region straddling bands is
+ * served bit-exact (its rows are gathered into a per-batch bridge buffer on the GPU).
+ * own_y0 / own_rows (0/0 = the whole plane): the rows this context may hold; own_y0 a multiple of
+ * band_rows; rows outside answer PBX_E_NOT_RESIDENT (another context owns them).  Generator
+ * sources generate each band on the GPU when it is written with data == NULL. */
+int pbx_plane_create_sparse(pbx_ctx* ctx, const pbx_plane_desc* desc, int32_t band_rows, int32_t own_y0,
+                            int32_t own_rows, uint64_t* plane_id);
+/* Rows [y0, y0 + rows) of ONE band (packed, desc->byte_order), as getTileDirect(z, c, t, 0, y0,
+ * sizeX, rows) returns them; the first write of an absent band allocates it (507 if it cannot be
+ * made to fit), the write that completes it makes it resident.  409 if the band is resident (or
+ * another caller is allocating it).  data == NULL: generate the rows (generator planes). */
+int pbx_band_write(pbx_ctx* ctx, uint64_t plane_id, int32_t y0, int32_t rows, const void* data,
+                   uint64_t bytes);
+/* band_rows and the number of bands of a sparse plane; states (may be NULL, nbands entries):
+ * 0 absent (never loaded, or evicted), 1 loading, 2 resident.  400 for a plane that is not sparse. */
+int pbx_plane_band_info(pbx_ctx* ctx, uint64_t plane_id, int32_t* band_rows, int32_t* nbands, uint8_t* states);
+
 /* HBM residency budget for planes (bytes; 0 = none, the default, or $PBX_HBM_BUDGET_MB).  A
  * registration that would exceed it first evicts idle planes, least recently used first (a
  * plane is idle when no planned batch reads it).  With or without a budget, a plane
@@ -188,10 +212,12 @@ int pbx_plane_lookup(pbx_ctx* ctx, int64_t image_id, int32_t z, int32_t c, int32
 int pbx_set_residency_budget(pbx_ctx* ctx, uint64_t bytes);
 typedef struct pbx_residency_stats {
     uint64_t budget;             /* 0 = none */
-    uint64_t resident_bytes;     /* HBM held by planes (incl. released ones still read) */
-    uint64_t planes;             /* registered planes resident in HBM */
+    uint64_t resident_bytes;     /* HBM held by planes and bands (incl. released ones still read) */
+    uint64_t planes;             /* registered (non-sparse) planes resident in HBM */
     uint64_t evicted_planes;     /* registered keys whose plane was evicted */
-    uint64_t evictions, evicted_bytes;  /* totals since pbx_init */
+    uint64_t evictions, evicted_bytes;  /* totals since pbx_init (planes and bands) */
+    uint64_t bands;              /* resident bands of sparse planes */
+    uint64_t band_evictions;     /* bands evicted since pbx_init */
 } pbx_residency_stats;
 int pbx_residency_stats_get(pbx_ctx* ctx, pbx_residency_stats* out);
 /* Resolution pyramid on the GPU (the lower levels
@@ -275,6 +301,7 @@ typedef struct pbx_result {
 int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out);
 /* Synchronous batch: n independent getTile calls executed as one set of GPU launches. */
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out);
+/* Results go back to the context that produced them (ctx may be NULL). */
 void pbx_results_release(pbx_ctx* ctx, pbx_result* results, uint64_t n);
 
 /* Batched async: pbx_submit plans and launches n independent getTile
@@ -349,6 +376,36 @@ int pbx_set_kernel_streams(pbx_ctx* ctx, int32_t streams, int32_t stagger);
  * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats, pbx_image_desc,
  * pbx_residency_stats (in that order).  Returns the number of structs (7). */
 int pbx_abi_sizes(uint64_t* sizes, int n);
+
+/* ---- A node: N device contexts in ONE process ----
+ * The reference deploys its worker verticles in one JVM (PixelBufferMicroserviceVerticle.java:
+ * 117-118,224-233: worker_pool_size threads calling TileRequestHandler.getTile).  A node-wide
+ * drop-in therefore holds one context per GPU in that process and routes each request to the
+ * context that holds its plane, or its row band (a whole slide split into tile-row bands over
+ * the GPUs); where several hold it (planes replicated on every GPU) the
+ * pbx_shard_of owner among them serves it.  devices: n HIP ordinals (NULL = 0 .. n-1; one
+ * device may appear several times); shard_tile: the tile cell of the shard hash (0 = 512). */
+typedef struct pbx_node pbx_node;
+int pbx_node_init(const pbx_config* cfg, int32_t n, const int32_t* devices, int32_t shard_tile,
+                  pbx_node** out);
+void pbx_node_shutdown(pbx_node* node);
+int32_t pbx_node_size(pbx_node* node);
+/* Context k of the node (register planes / bands there; NULL if out of range). */
+pbx_ctx* pbx_node_context(pbx_node* node, int32_t k);
+/* The context that serves `req`: *index = a context that holds the plane (the status it would
+ * answer is returned: PBX_OK, or the reference's 404 ...), else PBX_E_NOT_RESIDENT with *index =
+ * the pbx_shard_of owner, the context the binding should load the plane into. */
+int pbx_node_route(pbx_node* node, const pbx_tile_req* req, int32_t* index);
+/* pbx_get_tile on the routed context (served_by may be NULL); results are released with
+ * pbx_results_release (any context of the node, or NULL). */
+int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, int32_t* served_by);
+
+/* Fault injection (test hook): the `ahead`-th batch launched by this context from
+ * now on (1 = the next) completes with a device failure: each of its requests answers 500
+ * (PBX_E_INTERNAL, PixelBufferVerticle.java:141-146) unless it already had its own 4xx; the
+ * context keeps serving.  0 disables.  $PBX_FAIL_BATCH=k does the same for the k-th launch
+ * since pbx_init. */
+int pbx_test_fail_batch(pbx_ctx* ctx, uint64_t ahead);
 
 /* Request sharding across GPUs (one process per GPU, no collectives): the rank that
  * owns a request, by hash of (image, z, c, t, tile column, tile row) for tile_w x tile_h

@@ -66,6 +66,24 @@ enum PlaneState : int {
     PS_EVICTED = 2   // key still registered, HBM returned (NOT_RESIDENT until re-registered)
 };
 
+// One row band of a sparse plane (pbx_plane_create_sparse): rows [k*B, (k+1)*B) of the plane
+// (clipped to the plane and to the context's owned rows), loaded on demand, pinned by the
+// batches that read it and evicted on its own (region-proportional residency: a request
+// loads only the bands its rows cover, as getTileDirect reads only the requested region,
+// TileRequestHandler.java:102-109).
+enum BandState : int { BS_ABSENT = 0, BS_LOADING = 1, BS_READY = 2 };
+
+struct Band {
+    uint8_t* dev = nullptr;      // the band's rows at the plane's pitch + 256 B slack
+    size_t bytes = 0;
+    int state = BS_ABSENT;
+    int64_t pins = 0;            // planned batches that read it
+    uint64_t last_use = 0;
+    uint32_t rows_left = 0;      // BS_LOADING: rows not written yet
+    int32_t writers = 0;         // pbx_band_write calls in flight
+    std::vector<uint8_t> rows_done;
+};
+
 struct Plane {
     uint64_t id = 0;
     int64_t image_id = 0;
@@ -75,6 +93,13 @@ struct Plane {
     int64_t pitch = 0;
     size_t bytes = 0;
     int32_t band_y0 = 0, band_rows = 0;  // resident rows (band_rows == size_y: the whole plane)
+    // sparse planes: held as bands of sparse_rows rows (bands[k]), `dev` unused; band_y0 /
+    // band_rows are then the rows this context may hold (another context owns the rest)
+    int32_t sparse_rows = 0;
+    std::vector<Band> bands;
+    int32_t gen_source = 0;      // sparse generator planes: bands are generated on demand
+    uint64_t gen_seed = 0;
+    int32_t gen_plane_no = 0;
     // registry state, under reg_mu
     int state = PS_FILLING;
     bool indexed = false;        // reachable from ctx->index (false once released)
@@ -82,9 +107,22 @@ struct Plane {
     uint64_t last_use = 0;       // LRU tick of the last request served from it
     std::vector<uint8_t> rows_done;  // PS_FILLING host planes: which band rows were written
     uint64_t rows_left = 0;
+    int32_t writers = 0;         // pbx_plane_write_rows calls in flight (commit waits for none)
     // the kernels address rows by their index in the whole plane
     uint8_t* base() const { return dev - (int64_t)band_y0 * pitch; }
-    bool whole() const { return band_y0 == 0 && band_rows == size_y; }
+    bool whole() const { return !sparse_rows && band_y0 == 0 && band_rows == size_y; }
+    // sparse: rows of band k, [y0, y1)
+    int32_t band_lo(int32_t k) const { return std::max(k * sparse_rows, band_y0); }
+    int32_t band_hi(int32_t k) const {
+        return (int32_t)std::min<int64_t>({(int64_t)(k + 1) * sparse_rows, size_y, (int64_t)band_y0 + band_rows});
+    }
+    uint8_t* band_base(int32_t k) const { return bands[(size_t)k].dev - (int64_t)band_lo(k) * pitch; }
+    // every HBM block the record holds
+    void memory(std::vector<std::pair<void*, size_t>>& out) const {
+        if (dev) out.emplace_back(dev, bytes);
+        for (const Band& b : bands)
+            if (b.dev) out.emplace_back(b.dev, b.bytes);
+    }
 };
 
 struct Image {
@@ -172,6 +210,63 @@ struct Pool {
 
 struct Coalescer;
 
+// Returns plane HBM with hipFree on a thread of its own: hipFree waits for the whole device,
+// so it must never run on a completer (pbx_batch_destroy of a batch holding the last pin of
+// a released plane) or on the launch path, where it would stall every in-flight batch.
+struct Reaper {
+    std::mutex mu;
+    std::condition_variable cv, cv_idle;
+    std::deque<void*> q;
+    int busy = 0;
+    bool stop = false;
+    std::thread th;
+    int device = 0;
+
+    void start(int dev) {
+        device = dev;
+        th = std::thread([this] { loop(); });
+    }
+    void loop() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> g(mu);
+        for (;;) {
+            cv.wait(g, [&] { return stop || !q.empty(); });
+            if (q.empty()) break;  // stopping, nothing left
+            std::vector<void*> take(q.begin(), q.end());
+            q.clear();
+            busy++;
+            g.unlock();
+            for (void* p : take) (void)hipFree(p);
+            g.lock();
+            busy--;
+            cv_idle.notify_all();
+        }
+    }
+    void put(void* p) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            q.push_back(p);
+        }
+        cv.notify_one();
+    }
+    // Waits until every handed-over block is back with the device (an allocation that ran out
+    // of memory retries only after that).
+    void drain() {
+        std::unique_lock<std::mutex> g(mu);
+        cv_idle.wait(g, [&] { return q.empty() && busy == 0; });
+    }
+    void finish() {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+};
+
 struct pbx_ctx {
     int device = 0;
     int cus = 256;                      // compute units (persistent kernel grids)
@@ -205,8 +300,13 @@ struct pbx_ctx {
     std::unordered_map<int64_t, Image> images;
     uint64_t next_id = 1;
     // residency (reg_mu)
-    uint64_t budget = 0, resident_bytes = 0, use_tick = 0, evictions = 0, evicted_bytes = 0;
+    uint64_t budget = 0, resident_bytes = 0, use_tick = 0, evictions = 0, evicted_bytes = 0, band_evictions = 0;
     Pool dpool, hpool;
+    Reaper reaper;  // hipFree of plane HBM, off the serving threads
+    // fault injection (tests): the batch launched with ordinal fail_at (1-based,
+    // counted over every batch launch of this context; $PBX_FAIL_BATCH or
+    // pbx_test_fail_batch) completes with a device failure (500 for its requests)
+    std::atomic<uint64_t> launch_seq{0}, fail_at{0};
 };
 
 namespace {
@@ -259,10 +359,24 @@ struct pbx_batch {
     hipEvent_t ev[9] = {};
     bool launched = false;
     bool attempted = false;  // batch_launch began enqueuing work (it may have failed midway)
+    uint64_t ordinal = 0;    // launch ordinal in the context (fault injection)
+    bool inject_fail = false;  // completes with an injected device failure (pbx_test_fail_batch)
     std::vector<uint64_t> h_offs;
     // planes this batch reads (pinned by pbx_batch_plan, unpinned by pbx_batch_destroy), with
-    // the number of pins taken on each
+    // the number of pins taken on each; the bands of sparse planes it reads, one pin each
     std::vector<std::pair<Plane*, int64_t>> pins;
+    std::vector<std::pair<Plane*, int32_t>> band_pins;
+    // regions of sparse planes that straddle bands: copied (D2D) into one bridge buffer at
+    // launch, before the kernels; their descriptors address the bridge (TF_BRIDGE)
+    struct Bridge {
+        Plane* p;
+        int32_t x, y, w, h, k0, k1;
+        int64_t xo, bp;      // column offset (x*bpp mod 256, alignment kept) and row pitch
+        uint64_t off;        // offset in the bridge buffer
+    };
+    std::vector<Bridge> bridges;
+    uint64_t bridge_bytes = 0;
+    void* d_bridge = nullptr;
 };
 
 namespace {
@@ -365,7 +479,7 @@ void registry_remove(pbx_ctx* ctx, Plane* p, std::vector<std::pair<void*, size_t
         if (--im->second.planes == 0 && !im->second.declared) ctx->images.erase(im);
     }
     if (p->pins == 0) {
-        if (p->dev) to_free.emplace_back(p->dev, p->bytes);
+        p->memory(to_free);
         delete p;
     }
 }
@@ -375,19 +489,19 @@ void unpin_locked(pbx_ctx* ctx, Plane* p, int64_t n, std::vector<std::pair<void*
     (void)ctx;
     p->pins -= n;
     if (p->pins == 0 && !p->indexed) {
-        if (p->dev) to_free.emplace_back(p->dev, p->bytes);
+        p->memory(to_free);
         delete p;
     }
 }
 
-// Returns plane HBM (outside reg_mu: hipFree may wait for the device).  Nothing reads it:
-// its record had no pins, and it was unreachable from the index or evicted.
+// Returns plane HBM (outside reg_mu): the blocks go to the reaper thread, which hipFrees them
+// (hipFree waits for the whole device).  Nothing reads them: their record had no pins, and it
+// was unreachable from the index or evicted.  They stop counting as resident at once.
 void free_planes(pbx_ctx* ctx, const std::vector<std::pair<void*, size_t>>& to_free) {
     if (to_free.empty()) return;
-    (void)hipSetDevice(ctx->device);
     uint64_t bytes = 0;
     for (auto& f : to_free) {
-        (void)hipFree(f.first);
+        ctx->reaper.put(f.first);
         bytes += f.second;
     }
     std::lock_guard<std::mutex> g(ctx->reg_mu);
@@ -397,21 +511,59 @@ void free_planes(pbx_ctx* ctx, const std::vector<std::pair<void*, size_t>>& to_f
 // Evicts the least recently used idle plane (READY, registered, no pins), under reg_mu.
 // Its key stays registered (PS_EVICTED: requests answer NOT_RESIDENT).  Its HBM goes to
 // `to_free` for a plain hipFree (no longer counted as resident).  False if none.
+// Bands of sparse planes compete in the same LRU: a READY band no batch pins is evicted on its
+// own (state back to BS_ABSENT; the plane stays registered and READY).
 bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_free) {
     Plane* v = nullptr;
+    Band* vb = nullptr;
+    uint64_t best = UINT64_MAX;
     for (auto& kv : ctx->planes) {
         Plane* p = kv.second;
-        if (p->state == PS_READY && p->indexed && p->pins == 0 && p->dev && (!v || p->last_use < v->last_use))
+        if (!p->indexed || p->state != PS_READY) continue;
+        if (p->sparse_rows) {
+            for (Band& b : p->bands)
+                if (b.state == BS_READY && b.pins == 0 && b.dev && b.last_use < best) {
+                    best = b.last_use;
+                    v = p;
+                    vb = &b;
+                }
+        } else if (p->pins == 0 && p->dev && p->last_use < best) {
+            best = p->last_use;
             v = p;
+            vb = nullptr;
+        }
     }
     if (!v) return false;
-    to_free.emplace_back(v->dev, v->bytes);
-    ctx->resident_bytes -= v->bytes;
+    uint8_t** dev = vb ? &vb->dev : &v->dev;
+    const size_t bytes = vb ? vb->bytes : v->bytes;
+    to_free.emplace_back(*dev, bytes);
+    ctx->resident_bytes -= bytes;
     ctx->evictions++;
-    ctx->evicted_bytes += v->bytes;
-    v->dev = nullptr;
-    v->state = PS_EVICTED;
+    ctx->evicted_bytes += bytes;
+    *dev = nullptr;
+    if (vb) {
+        vb->state = BS_ABSENT;
+        ctx->band_evictions++;
+    } else {
+        v->state = PS_EVICTED;
+    }
     return true;
+}
+
+// Bytes an eviction could return now (idle planes and idle bands), under reg_mu.
+uint64_t idle_bytes_locked(pbx_ctx* ctx) {
+    uint64_t idle = 0;
+    for (auto& kv : ctx->planes) {
+        const Plane* p = kv.second;
+        if (!p->indexed || p->state != PS_READY) continue;
+        if (p->sparse_rows) {
+            for (const Band& b : p->bands)
+                if (b.state == BS_READY && b.pins == 0 && b.dev) idle += b.bytes;
+        } else if (p->pins == 0 && p->dev) {
+            idle += p->bytes;
+        }
+    }
+    return idle;
 }
 
 // HBM for a plane, within the residency budget: evicts idle planes (LRU) to make room, and
@@ -423,11 +575,7 @@ int plane_alloc(pbx_ctx* ctx, size_t bytes, uint8_t** out) {
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         if (ctx->budget) {
-            uint64_t idle = 0;
-            for (auto& kv : ctx->planes) {
-                const Plane* p = kv.second;
-                if (p->state == PS_READY && p->indexed && p->pins == 0 && p->dev) idle += p->bytes;
-            }
+            const uint64_t idle = idle_bytes_locked(ctx);
             if (ctx->resident_bytes + bytes > ctx->budget + idle)
                 return fail(PBX_E_NO_SPACE, "plane of %zu bytes does not fit the residency budget (%llu of %llu "
                             "bytes held, %llu idle)", bytes, (unsigned long long)ctx->resident_bytes,
@@ -437,11 +585,17 @@ int plane_alloc(pbx_ctx* ctx, size_t bytes, uint8_t** out) {
         }
         ctx->resident_bytes += bytes;
     }
-    for (auto& v : victims) (void)hipFree(v.first);
+    for (auto& v : victims) ctx->reaper.put(v.first);
+    bool drained = false;
     for (;;) {
         const hipError_t e = hipMalloc((void**)out, bytes);
         if (e == hipSuccess) return PBX_OK;
         (void)hipGetLastError();
+        if (e == hipErrorOutOfMemory && !drained) {  // blocks on their way back first
+            ctx->reaper.drain();
+            drained = true;
+            continue;
+        }
         std::vector<std::pair<void*, size_t>> one;
         {
             std::lock_guard<std::mutex> g(ctx->reg_mu);
@@ -453,7 +607,8 @@ int plane_alloc(pbx_ctx* ctx, size_t bytes, uint8_t** out) {
                             hipGetErrorString(e));
             }
         }
-        (void)hipFree(one[0].first);
+        ctx->reaper.put(one[0].first);
+        ctx->reaper.drain();
     }
 }
 
@@ -466,16 +621,26 @@ void plane_free(pbx_ctx* ctx, void* dev, size_t bytes) {
 // returns PBX_OK and the plane (pinned: the caller unpins it), the status the reference ends
 // with, or PBX_E_NOT_RESIDENT where the reference would open a plane this context does not
 // hold (getPixels + getPixelBuffer, :84-86).
-int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*& plane) {
+// pin = false: a probe (node routing) that takes no pin and leaves the LRU stamps alone.
+// kr (sparse planes): the first and last band the region covers, each pinned with the plane.
+int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*& plane, bool pin = true,
+             int32_t* kr = nullptr) {
     w = r.w;
     h = r.h;
     plane = nullptr;
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     auto im = ctx->images.find(r.image_id);
     // :84 getPixels — the image's Pixels row is not known here; the binding looks it up
-    // (null -> 404 there) and loads the plane
-    if (im == ctx->images.end())
+    // (null -> 404 there) and loads the plane.  What ends in null whatever the image holds is
+    // answered first, so that nothing is loaded for it: an unknown format (:125-126) and a
+    // region no pixel type makes a valid byte[] (negative, or w*h alone past 2^31-1, :100-103).
+    if (im == ctx->images.end()) {
+        if (r.format != PBX_FMT_RAW && r.format != PBX_FMT_PNG && r.format != PBX_FMT_TIF)
+            return fail(PBX_E_NOTFOUND, "Unknown output format");
+        if (r.w < 0 || r.h < 0 || (int64_t)r.w * (int64_t)r.h > 2147483647LL)
+            return fail(PBX_E_NOTFOUND, "invalid tile size %dx%d", r.w, r.h);
         return fail(PBX_E_NOT_RESIDENT, "Image:%lld not resident", (long long)r.image_id);
+    }
     // :89-91 — pixelBuffer.setResolutionLevel(resolution) when given.  OMERO numbers levels
     // the other way round from storage: resolution getResolutionLevels()-1 is the full
     // resolution and 0 the smallest (omero-zarr-pixel-buffer's ZarrPixelBuffer maps it to
@@ -531,6 +696,27 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*
     if (r.y < p->band_y0 || (int64_t)r.y + h > (int64_t)p->band_y0 + p->band_rows)
         return fail(PBX_E_NOT_RESIDENT, "rows %d..%lld outside the resident band %d..%d", r.y,
                     (long long)r.y + h, p->band_y0, p->band_y0 + p->band_rows);
+    if (p->sparse_rows) {  // every band the rows cover must be resident
+        const int32_t k0 = r.y / p->sparse_rows, k1 = (int32_t)(((int64_t)r.y + h - 1) / p->sparse_rows);
+        for (int32_t k = k0; k <= k1; k++)
+            if (p->bands[(size_t)k].state != BS_READY)
+                return fail(PBX_E_NOT_RESIDENT, "rows %d..%lld: band %d (rows %d..%d) of plane z=%d c=%d t=%d level=%d "
+                            "not resident", r.y, (long long)r.y + h, k, p->band_lo(k), p->band_hi(k), r.z, r.c, r.t,
+                            level);
+        if (kr) {
+            kr[0] = k0;
+            kr[1] = k1;
+        }
+        if (!pin) return PBX_OK;
+        const uint64_t tick = ++ctx->use_tick;
+        for (int32_t k = k0; k <= k1; k++) {
+            p->bands[(size_t)k].pins++;
+            p->bands[(size_t)k].last_use = tick;
+        }
+    } else if (kr) {
+        kr[0] = kr[1] = -1;
+    }
+    if (!pin) return PBX_OK;
     p->pins++;
     p->last_use = ++ctx->use_tick;
     plane = p;
@@ -543,8 +729,10 @@ void batch_unpin(pbx_ctx* ctx, pbx_batch* b) {
     std::vector<std::pair<void*, size_t>> to_free;
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
+        for (auto& bp : b->band_pins) bp.first->bands[(size_t)bp.second].pins--;  // before the plane pins
         for (auto& pc : b->pins) unpin_locked(ctx, pc.first, pc.second, to_free);
     }
+    b->band_pins.clear();
     b->pins.clear();
     free_planes(ctx, to_free);
 }
@@ -552,7 +740,7 @@ void batch_unpin(pbx_ctx* ctx, pbx_batch* b) {
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
     void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
                      &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps,
-                     &b->d_segmap, &b->d_blk, &b->d_th};
+                     &b->d_segmap, &b->d_blk, &b->d_th, &b->d_bridge};
     for (void** p : bufs) {
         ctx->dpool.put(*p);
         *p = nullptr;
@@ -863,6 +1051,8 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
         delete ctx;
         return fail(PBX_E_INTERNAL, "init: %s", hipGetErrorString(e));
     }
+    if (const char* fb = getenv("PBX_FAIL_BATCH")) ctx->fail_at = strtoull(fb, nullptr, 10);
+    ctx->reaper.start(dev);
     if (cfg.coalesce) ctx->coal = new Coalescer(ctx);
     *out = ctx;
     return PBX_OK;
@@ -876,6 +1066,7 @@ void pbx_shutdown(pbx_ctx* ctx) {
     (void)sync_kernel_streams(ctx);
     (void)hipStreamSynchronize(ctx->copy_stream);
     (void)hipStreamSynchronize(ctx->upload_stream);
+    ctx->reaper.finish();  // frees what it still holds
     for (auto& kv : ctx->planes) {  // records of released planes still pinned by undestroyed
         (void)hipFree(kv.second->dev);  // batches are leaked with those batches
         delete kv.second;
@@ -1124,13 +1315,22 @@ int plane_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* da
         return fail(PBX_E_BADARG, "%llu bytes for %d rows of %llu", (unsigned long long)bytes, rows,
                     (unsigned long long)row);
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    {   // a writer in flight: pbx_plane_commit refuses to publish the plane until it is done
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        if (q->state != PS_FILLING) return fail(PBX_E_BADARG, "plane %llu is not being loaded", (unsigned long long)q->id);
+        q->writers++;
+    }
+    int rc;
     {
         std::lock_guard<std::mutex> u(ctx->upload_mu);
-        if (int rc = upload_rows(ctx, q->dev + (int64_t)(y0 - q->band_y0) * q->pitch, q->pitch,
-                                 (const uint8_t*)data, row, (uint64_t)rows, ctx->upload_stream))
-            return rc;
+        rc = upload_rows(ctx, q->dev + (int64_t)(y0 - q->band_y0) * q->pitch, q->pitch, (const uint8_t*)data, row,
+                         (uint64_t)rows, ctx->upload_stream);
     }
     std::lock_guard<std::mutex> g(ctx->reg_mu);
+    q->writers--;
+    if (rc) return rc;
+    if (q->state != PS_FILLING)  // cannot happen while we were a writer; kept as the invariant
+        return fail(PBX_E_INTERNAL, "plane %llu was published during a write", (unsigned long long)q->id);
     for (int32_t r = y0 - q->band_y0; r < y0 - q->band_y0 + rows; r++)
         if (!q->rows_done[(size_t)r]) {
             q->rows_done[(size_t)r] = 1;
@@ -1142,6 +1342,9 @@ int plane_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* da
 int plane_commit(pbx_ctx* ctx, Plane* q) {
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     if (q->state != PS_FILLING) return fail(PBX_E_BADARG, "plane %llu is not being loaded", (unsigned long long)q->id);
+    if (q->writers)  // rows may still be in flight on upload_stream: never publish them half-written
+        return fail(PBX_E_EXISTS, "plane %llu: %d pbx_plane_write_rows calls still running", (unsigned long long)q->id,
+                    q->writers);
     if (q->rows_left)
         return fail(PBX_E_BADARG, "plane %llu: %llu rows of its band were never written", (unsigned long long)q->id,
                     (unsigned long long)q->rows_left);
@@ -1212,6 +1415,166 @@ int pbx_plane_register(pbx_ctx* ctx, const pbx_plane_desc* d, uint64_t* plane_id
     free_planes(ctx, to_free);
     g_err = msg;
     return rc;
+}
+
+// ------------------------------------------------------------------ sparse (banded) planes
+
+int pbx_plane_create_sparse(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t band_rows, int32_t own_y0,
+                            int32_t own_rows, uint64_t* plane_id) {
+    if (!ctx || !d || !plane_id) return fail(PBX_E_BADARG, "null argument");
+    const int bpp = bpp_of(d->pixel_type);
+    if (!bpp) return fail(PBX_E_BADARG, "bad pixel type %d", d->pixel_type);
+    if (d->size_x <= 0 || d->size_y <= 0) return fail(PBX_E_BADARG, "bad plane size");
+    if (d->resolution < 0) return fail(PBX_E_BADARG, "bad resolution");
+    if (d->source != PBX_SRC_HOST && d->source != PBX_SRC_GEN_FAKE && d->source != PBX_SRC_GEN_NOISE)
+        return fail(PBX_E_BADARG, "bad source %d", d->source);
+    if (band_rows <= 0) return fail(PBX_E_BADARG, "band_rows %d", band_rows);
+    if (own_rows == 0) {
+        if (own_y0 != 0) return fail(PBX_E_BADARG, "own_rows 0 (the whole plane) needs own_y0 0");
+        own_rows = d->size_y;
+    }
+    if (own_y0 < 0 || own_rows < 0 || (int64_t)own_y0 + own_rows > d->size_y || own_y0 % band_rows)
+        return fail(PBX_E_BADARG, "owned rows %d+%d: outside the plane or not at a band start", own_y0, own_rows);
+    Plane p;
+    p.image_id = d->image_id; p.z = d->z; p.c = d->c; p.t = d->t; p.res = d->resolution;
+    p.pixel_type = d->pixel_type; p.size_x = d->size_x; p.size_y = d->size_y;
+    p.band_y0 = own_y0;
+    p.band_rows = own_rows;
+    p.sparse_rows = band_rows;
+    p.pitch = ((int64_t)d->size_x * bpp + 255) & ~(int64_t)255;
+    p.little_endian = d->source == PBX_SRC_HOST ? (d->byte_order == PBX_LITTLE_ENDIAN && bpp > 1) : bpp > 1;
+    p.gen_source = d->source;
+    p.gen_seed = d->seed;
+    p.gen_plane_no = d->plane_no;
+    p.bands.resize((size_t)((d->size_y + (int64_t)band_rows - 1) / band_rows));
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    if (int rc = registry_check(ctx, p)) return rc;
+    p.state = PS_READY;  // served at once: requests answer NOT_RESIDENT per missing band
+    Plane* q = registry_add(ctx, p);
+    *plane_id = q->id;
+    return PBX_OK;
+}
+
+namespace {
+
+// Rows [y0, y0 + rows) of one band of a sparse plane: the first write of an absent band
+// allocates it (within the budget, evicting idle planes / bands), the last one publishes it.
+// data == NULL on a generator plane generates the rows on the GPU instead.
+int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
+    if (!q->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)q->id);
+    if (rows <= 0 || y0 < q->band_y0 || (int64_t)y0 + rows > (int64_t)q->band_y0 + q->band_rows)
+        return fail(PBX_E_BADARG, "rows %d+%d outside the rows %d+%d this context may hold", y0, rows, q->band_y0,
+                    q->band_rows);
+    const int32_t k = y0 / q->sparse_rows;
+    const int32_t lo = q->band_lo(k), hi = q->band_hi(k);
+    if (y0 + rows > hi) return fail(PBX_E_BADARG, "rows %d+%d cross the end of band %d (rows %d..%d)", y0, rows, k, lo, hi);
+    const int bpp = bpp_of(q->pixel_type);
+    const uint64_t row = (uint64_t)q->size_x * bpp;
+    const bool gen = data == nullptr;
+    if (gen && q->gen_source == PBX_SRC_HOST) return fail(PBX_E_BADARG, "null data");
+    if (!gen && bytes < row * (uint64_t)rows)
+        return fail(PBX_E_BADARG, "%llu bytes for %d rows of %llu", (unsigned long long)bytes, rows, (unsigned long long)row);
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    Band& b = q->bands[(size_t)k];
+    bool alloc = false;
+    size_t nbytes = 0;
+    {
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        if (b.state == BS_READY) return fail(PBX_E_EXISTS, "band %d is resident", k);
+        if (b.state == BS_ABSENT) {
+            b.state = BS_LOADING;
+            b.rows_done.assign((size_t)(hi - lo), 0);
+            b.rows_left = (uint32_t)(hi - lo);
+            alloc = true;
+        } else if (!b.dev) {
+            return fail(PBX_E_EXISTS, "band %d is being allocated by another caller", k);
+        }
+        nbytes = (size_t)q->pitch * (size_t)(hi - lo) + 256;
+        b.writers++;
+    }
+    auto undo = [&](int rc) {
+        const std::string msg = g_err;
+        std::vector<std::pair<void*, size_t>> to_free;
+        {
+            std::lock_guard<std::mutex> g(ctx->reg_mu);
+            b.writers--;
+            if (alloc) {  // the band goes back to absent; what it allocated is returned
+                if (b.dev) to_free.emplace_back(b.dev, b.bytes);
+                b.dev = nullptr;
+                b.state = BS_ABSENT;
+                b.rows_done.clear();
+            }
+        }
+        free_planes(ctx, to_free);
+        g_err = msg;
+        return rc;
+    };
+    if (alloc) {
+        uint8_t* dev = nullptr;
+        if (int rc = plane_alloc(ctx, nbytes, &dev)) return undo(rc);
+        std::lock_guard<std::mutex> g(ctx->reg_mu);
+        b.dev = dev;
+        b.bytes = nbytes;
+    }
+    hipError_t e = hipSuccess;
+    int rc = PBX_OK;
+    {
+        std::lock_guard<std::mutex> u(ctx->upload_mu);
+        if (alloc) e = hipMemsetAsync(b.dev + (size_t)q->pitch * (size_t)(hi - lo), 0, 256, ctx->upload_stream);
+        uint8_t* dst = b.dev + (int64_t)(y0 - lo) * q->pitch;
+        if (e == hipSuccess && gen) {
+            e = launch_gen_plane(ctx->upload_stream, dst, q->pitch, q->size_x, y0, rows, q->pixel_type,
+                                 q->gen_source == PBX_SRC_GEN_FAKE ? GEN_FAKE : GEN_NOISE, q->gen_seed,
+                                 q->gen_plane_no, q->z, q->c, q->t);
+            if (e == hipSuccess) e = hipStreamSynchronize(ctx->upload_stream);
+        } else if (e == hipSuccess) {
+            rc = upload_rows(ctx, dst, q->pitch, (const uint8_t*)data, row, (uint64_t)rows, ctx->upload_stream);
+        }
+    }
+    if (e != hipSuccess) rc = fail(PBX_E_INTERNAL, "band write: %s", hipGetErrorString(e));
+    if (rc) return undo(rc);
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    b.writers--;
+    for (int32_t r = y0 - lo; r < y0 - lo + rows; r++)
+        if (!b.rows_done[(size_t)r]) {
+            b.rows_done[(size_t)r] = 1;
+            b.rows_left--;
+        }
+    if (b.rows_left == 0 && b.writers == 0 && b.state == BS_LOADING) {  // the last write publishes it
+        b.rows_done.clear();
+        b.rows_done.shrink_to_fit();
+        b.state = BS_READY;
+        b.last_use = ++ctx->use_tick;
+    }
+    return PBX_OK;
+}
+
+}  // namespace
+
+int pbx_band_write(pbx_ctx* ctx, uint64_t id, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    int rc;
+    Plane* q = pin_id(ctx, id, 1u << PS_READY, &rc);
+    if (!q) return rc == PBX_E_EXISTS ? fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)id) : rc;
+    rc = band_write(ctx, q, y0, rows, data, bytes);
+    const std::string msg = g_err;
+    unpin_one(ctx, q);
+    g_err = msg;
+    return rc;
+}
+
+int pbx_plane_band_info(pbx_ctx* ctx, uint64_t id, int32_t* band_rows, int32_t* nbands, uint8_t* states) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->planes.find(id);
+    if (it == ctx->planes.end() || !it->second->indexed) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+    const Plane* p = it->second;
+    if (!p->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)id);
+    if (band_rows) *band_rows = p->sparse_rows;
+    if (nbands) *nbands = (int32_t)p->bands.size();
+    if (states)
+        for (size_t k = 0; k < p->bands.size(); k++) states[k] = (uint8_t)p->bands[k].state;
+    return PBX_OK;
 }
 
 int pbx_plane_lookup(pbx_ctx* ctx, int64_t image_id, int32_t z, int32_t c, int32_t t, int32_t level,
@@ -1294,10 +1657,7 @@ int pbx_set_residency_budget(pbx_ctx* ctx, uint64_t bytes) {
         while (bytes && ctx->resident_bytes > bytes)  // shrink now, as far as idle planes allow
             if (!evict_one_locked(ctx, victims)) break;
     }
-    if (!victims.empty()) {
-        (void)hipSetDevice(ctx->device);
-        for (auto& v : victims) (void)hipFree(v.first);
-    }
+    for (auto& v : victims) ctx->reaper.put(v.first);
     return PBX_OK;
 }
 
@@ -1308,12 +1668,15 @@ int pbx_residency_stats_get(pbx_ctx* ctx, pbx_residency_stats* s) {
     s->budget = ctx->budget;
     s->resident_bytes = ctx->resident_bytes;
     for (auto& kv : ctx->planes) {
-        if (!kv.second->indexed) continue;
-        if (kv.second->state == PS_EVICTED) s->evicted_planes++;
-        else if (kv.second->dev) s->planes++;
+        const Plane* p = kv.second;
+        if (!p->indexed) continue;
+        if (p->state == PS_EVICTED) s->evicted_planes++;
+        else if (p->dev) s->planes++;
+        for (const Band& b : p->bands) s->bands += b.state == BS_READY;
     }
     s->evictions = ctx->evictions;
     s->evicted_bytes = ctx->evicted_bytes;
+    s->band_evictions = ctx->band_evictions;
     return PBX_OK;
 }
 
@@ -1716,6 +2079,7 @@ int pbx_plane_read_be(pbx_ctx* ctx, uint64_t id, void* out, uint64_t bytes) {
     Plane* p = pin_id(ctx, id, 1u << PS_READY, &rc);
     if (!p) return rc;
     rc = [&]() -> int {
+        if (p->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is a sparse plane", (unsigned long long)id);
         const int bpp = bpp_of(p->pixel_type);
         const int64_t row = (int64_t)p->size_x * bpp;
         const int64_t rows = p->band_rows;  // a band plane: its rows only
@@ -1753,8 +2117,8 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
     for (uint64_t i = 0; i < n; i++) {
         const pbx_tile_req& r = reqs[i];
         Plane* pp = nullptr;
-        int32_t w = 0, h = 0;
-        const int st = validate(ctx, r, w, h, pp);
+        int32_t w = 0, h = 0, kr[2] = {-1, -1};
+        const int st = validate(ctx, r, w, h, pp, true, kr);
         b->status[i] = st;
         b->w[i] = w;
         b->h[i] = h;
@@ -1771,6 +2135,24 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         d.bpp = bpp; d.lbpp = log2i(bpp);
         d.pixel_type = pl.pixel_type;
         d.flags = pl.little_endian ? TF_SWAP : 0u;
+        if (pl.sparse_rows) {  // its bands are pinned (validate); the kernels read one band, or the bridge
+            for (int32_t k = kr[0]; k <= kr[1]; k++) b->band_pins.emplace_back(pp, k);
+            if (kr[0] == kr[1]) {
+                d.plane = pl.band_base(kr[0]);
+            } else {
+                pbx_batch::Bridge g;
+                g.p = pp;
+                g.x = r.x; g.y = r.y; g.w = w; g.h = h; g.k0 = kr[0]; g.k1 = kr[1];
+                g.xo = ((int64_t)r.x * bpp) & 255;  // same alignment as in the plane rows
+                g.bp = (g.xo + (int64_t)w * bpp + 16 + 255) & ~(int64_t)255;  // + vector over-read
+                g.off = b->bridge_bytes;
+                b->bridge_bytes += (uint64_t)g.bp * (uint64_t)h + 256;
+                b->bridges.push_back(g);
+                d.plane = (const uint8_t*)(uintptr_t)((int64_t)g.off + g.xo - (int64_t)r.y * g.bp - (int64_t)r.x * bpp);
+                d.pitch = g.bp;
+                d.flags |= TF_BRIDGE;
+            }
+        }
         const uint64_t tile_bytes = (uint64_t)w * h * bpp;
         b->in_bytes += tile_bytes;
         const bool deflate = r.format == PBX_FMT_PNG || (r.format == PBX_FMT_TIF && tiff_deflate);
@@ -1964,6 +2346,8 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     const size_t ft_bytes = nft * sizeof(TileDesc), dt_bytes = ndt * sizeof(TileDesc),
                  th_bytes = nth * sizeof(TiledHdr);
     const size_t offs_at = (ft_bytes + dt_bytes + th_bytes + 15) & ~(size_t)15;
+    if (b->bridge_bytes && !dget(b->d_bridge, b->bridge_bytes))
+        return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     if (!b->h_desc) {
         b->h_desc = ctx->hpool.get(offs_at + (ndt + 1) * sizeof(uint64_t) + 256, &err);
         if (!b->h_desc) return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
@@ -1971,6 +2355,14 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
         if (nft) memcpy(b->h_desc, b->ft.data(), ft_bytes);
         if (ndt) memcpy((uint8_t*)b->h_desc + ft_bytes, b->dt.data(), dt_bytes);
         if (nth) memcpy((uint8_t*)b->h_desc + ft_bytes + dt_bytes, b->th.data(), th_bytes);
+        if (b->bridge_bytes) {  // bridged regions: their plane base is relative to the bridge buffer
+            TileDesc* td = (TileDesc*)b->h_desc;
+            for (uint32_t k = 0; k < nft + ndt; k++)
+                if (td[k].flags & TF_BRIDGE) {
+                    td[k].plane = (const uint8_t*)b->d_bridge + (intptr_t)td[k].plane;
+                    td[k].flags &= ~(uint32_t)TF_BRIDGE;
+                }
+        }
     }
     const size_t ns = b->nseg;
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
@@ -1991,6 +2383,8 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     if (multi && stagger && prev >= 0 && prev != ks)
         HIP_TRY(hipStreamWaitEvent(st, ctx->stage_ev[prev][stagger - 1], 0));
     b->attempted = true;
+    b->ordinal = ++ctx->launch_seq;
+    b->inject_fail = b->ordinal == ctx->fail_at.load();
     HIP_TRY(hipEventRecord(b->ev[0], st));
     if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
     if (ndt)
@@ -1998,6 +2392,18 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     if (nth)
         HIP_TRY(hipMemcpyAsync(b->d_th, (uint8_t*)b->h_desc + ft_bytes + dt_bytes, th_bytes,
                                hipMemcpyHostToDevice, st));
+    // regions straddling bands of sparse planes: their rows, band by band, into the bridge
+    for (const pbx_batch::Bridge& g : b->bridges) {
+        const Plane& p = *g.p;  // pinned, and so are its bands k0..k1
+        const int64_t cb = (int64_t)g.w * bpp_of(p.pixel_type), xb = (int64_t)g.x * bpp_of(p.pixel_type);
+        for (int32_t k = g.k0; k <= g.k1; k++) {
+            const int32_t r0 = std::max(g.y, p.band_lo(k)), r1 = std::min(g.y + g.h, p.band_hi(k));
+            if (r1 <= r0) continue;
+            HIP_TRY(hipMemcpy2DAsync((uint8_t*)b->d_bridge + g.off + (int64_t)(r0 - g.y) * g.bp + g.xo, (size_t)g.bp,
+                                     p.band_base(k) + (int64_t)r0 * p.pitch + xb, (size_t)p.pitch, (size_t)cb,
+                                     (size_t)(r1 - r0), hipMemcpyDeviceToDevice, st));
+        }
+    }
     HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
     HIP_TRY(hipEventRecord(b->ev[2], st));
@@ -2058,6 +2464,8 @@ int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     if (b->launched) HIP_TRY(hipEventSynchronize(b->ev[8]));
+    if (b->inject_fail)
+        return fail(PBX_E_INTERNAL, "injected device failure in batch %llu", (unsigned long long)b->ordinal);
     if (b->d_stamps && b->nseg) {  // PBX_PHASE_PROFILE diagnostic: mean cycles per phase
         std::vector<uint64_t> st((size_t)b->nseg * 32);
         HIP_TRY(hipMemcpy(st.data(), b->d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
@@ -2140,6 +2548,10 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     // Wait for this batch only (later batches may already run on the kernel stream) and
     // copy on the copy stream, so the D2H overlaps the next batch's kernels.
     HIP_TRY(hipEventSynchronize(b->ev[8]));
+    // a device failure shows when the batch's completion is collected (hipErrorLaunchFailure
+    // at the event); the injected one takes the same way (PixelBufferVerticle.java:141-146: 500)
+    if (b->inject_fail)
+        return fail(PBX_E_INTERNAL, "injected device failure in batch %llu", (unsigned long long)b->ordinal);
     const uint32_t ndt = (uint32_t)b->dt.size();
     b->h_offs.assign(ndt + 1, 0);
     if (ndt && b->offs_ready) {
@@ -2243,7 +2655,8 @@ void pbx_results_release(pbx_ctx* ctx, pbx_result* res, uint64_t n) {
         res[i].data = nullptr;
         if (!hb) continue;
         if (hb->refs.fetch_sub(1) == 1) {
-            (ctx ? ctx : hb->ctx)->hpool.put(hb->pinned);
+            (void)ctx;  // the block goes back to the pool of the context that filled it
+            hb->ctx->hpool.put(hb->pinned);
             delete hb;
         }
     }
@@ -2407,6 +2820,98 @@ int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
     const int st = ctx->coal ? ctx->coal->submit(*req, out) : run_batch(ctx, req, 1, out);
     if (st) return st;
     return out->status;
+}
+
+int pbx_test_fail_batch(pbx_ctx* ctx, uint64_t ahead) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::lock_guard<std::mutex> run(ctx->run_mu);  // launches are ordered under run_mu
+    ctx->fail_at = ahead ? ctx->launch_seq.load() + ahead : 0;
+    return PBX_OK;
+}
+
+// ------------------------------------------------------------------ node: N contexts
+}  // extern "C"
+
+// Several device contexts in one process: the reference runs all its worker verticles in one
+// JVM (PixelBufferMicroserviceVerticle.java:117-118,224-233), so a node-wide drop-in routes
+// each getTile to the context that holds its plane (or row band), or, when several do (planes
+// replicated on every GPU), to the pbx_shard_of owner among them.
+struct pbx_node {
+    std::vector<pbx_ctx*> ctxs;
+    int32_t tile = 512;
+};
+
+extern "C" {
+
+int pbx_node_init(const pbx_config* cfg, int32_t n, const int32_t* devices, int32_t shard_tile, pbx_node** out) {
+    if (!out) return fail(PBX_E_BADARG, "null out");
+    *out = nullptr;
+    if (n < 1 || n > 64) return fail(PBX_E_BADARG, "node of %d contexts", n);
+    if (shard_tile < 0) return fail(PBX_E_BADARG, "bad shard tile %d", shard_tile);
+    pbx_config base;
+    if (cfg) base = *cfg; else pbx_config_default(&base);
+    pbx_node* node = new pbx_node();
+    node->tile = shard_tile ? shard_tile : 512;
+    for (int32_t k = 0; k < n; k++) {
+        pbx_config c = base;
+        c.device = devices ? devices[k] : k;  // the same device may appear several times
+        pbx_ctx* ctx = nullptr;
+        if (int rc = pbx_init(&c, &ctx)) {
+            const std::string msg = g_err;
+            pbx_node_shutdown(node);
+            g_err = msg;
+            return rc;
+        }
+        node->ctxs.push_back(ctx);
+    }
+    *out = node;
+    return PBX_OK;
+}
+
+void pbx_node_shutdown(pbx_node* node) {
+    if (!node) return;
+    for (pbx_ctx* c : node->ctxs) pbx_shutdown(c);
+    delete node;
+}
+
+int32_t pbx_node_size(pbx_node* node) { return node ? (int32_t)node->ctxs.size() : 0; }
+
+pbx_ctx* pbx_node_context(pbx_node* node, int32_t k) {
+    if (!node || k < 0 || k >= (int32_t)node->ctxs.size()) return nullptr;
+    return node->ctxs[(size_t)k];
+}
+
+int pbx_node_route(pbx_node* node, const pbx_tile_req* req, int32_t* index) {
+    if (!node || !req || !index) return fail(PBX_E_BADARG, "null argument");
+    const int32_t n = (int32_t)node->ctxs.size();
+    const int32_t owner = n == 1 ? 0 : pbx_shard_of(req, node->tile, node->tile, n);
+    if (owner < 0) return PBX_E_BADARG;
+    for (int32_t k = 0; k < n; k++) {  // the owner first, then the others in ring order
+        const int32_t c = (owner + k) % n;
+        int32_t w = 0, h = 0;
+        Plane* p = nullptr;
+        const int st = validate(node->ctxs[(size_t)c], *req, w, h, p, false);
+        if (st != PBX_E_NOT_RESIDENT) {
+            *index = c;
+            return st;
+        }
+    }
+    *index = owner;  // nobody holds it: the binding loads it into the owner and retries
+    return fail(PBX_E_NOT_RESIDENT, "no context of the node holds the plane (owner %d)", owner);
+}
+
+int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, int32_t* served_by) {
+    if (!node || !req || !out) return fail(PBX_E_BADARG, "null argument");
+    int st = PBX_E_NOT_RESIDENT;
+    for (int attempt = 0; attempt < 2; attempt++) {  // a plane evicted between route and get
+        int32_t k = 0;
+        const int r = pbx_node_route(node, req, &k);
+        if (r == PBX_E_BADARG) return r;
+        if (served_by) *served_by = k;
+        st = pbx_get_tile(node->ctxs[(size_t)k], req, out);
+        if (st != PBX_E_NOT_RESIDENT || r == PBX_E_NOT_RESIDENT) break;
+    }
+    return st;
 }
 
 int pbx_ctx_stats_get(pbx_ctx* ctx, uint64_t* batches, uint64_t* requests) {

@@ -33,8 +33,9 @@ LIB_PATH = os.environ.get("PBX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), 
 # client) = the context does not hold the plane: load it and retry (TileRequestHandler below)
 OK, E_BADARG, E_NOTFOUND, E_INTERNAL, E_PENDING = 0, 400, 404, 500, 504
 E_EXISTS, E_NOT_RESIDENT, E_NO_SPACE = 409, 460, 507
-# plane states (pbx_plane_lookup)
+# plane states (pbx_plane_lookup); band states of sparse planes (pbx_plane_band_info)
 PS_FILLING, PS_READY, PS_EVICTED = 0, 1, 2
+BS_ABSENT, BS_LOADING, BS_READY = 0, 1, 2
 # enum pbx_pixel_type (OMERO PixelType names)
 PIXEL_TYPES = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "float", "double"]
 INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT, DOUBLE = range(8)
@@ -73,7 +74,8 @@ class PbxImageDesc(ctypes.Structure):
 
 class PbxResidencyStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
-                ("budget", "resident_bytes", "planes", "evicted_planes", "evictions", "evicted_bytes")]
+                ("budget", "resident_bytes", "planes", "evicted_planes", "evictions", "evicted_bytes",
+                 "bands", "band_evictions")]
 
 
 class PbxZarrChunks(ctypes.Structure):
@@ -124,7 +126,9 @@ EXPORTS = [
     "pbx_plane_register_zarr", "pbx_planes_register_zarr", "pbx_release_cached",
     "pbx_set_kernel_streams", "pbx_image_declare", "pbx_image_release", "pbx_plane_create",
     "pbx_plane_write_rows", "pbx_plane_commit", "pbx_plane_lookup", "pbx_set_residency_budget",
-    "pbx_residency_stats_get",
+    "pbx_residency_stats_get", "pbx_test_fail_batch", "pbx_node_init", "pbx_node_shutdown",
+    "pbx_node_size", "pbx_node_context", "pbx_node_route", "pbx_node_get_tile",
+    "pbx_plane_create_sparse", "pbx_band_write", "pbx_plane_band_info",
 ]
 
 _lib = None
@@ -195,6 +199,19 @@ def lib() -> ctypes.CDLL:
     L.pbx_shard_of.argtypes = [ctypes.POINTER(PbxTileReq), i32, i32, i32]
     L.pbx_test_huffman.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 2 + [ctypes.c_uint32] + \
         [ctypes.c_void_p] * 2
+    L.pbx_test_fail_batch.argtypes = [vp, u64]
+    L.pbx_plane_create_sparse.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), i32, i32, i32, ctypes.POINTER(u64)]
+    L.pbx_band_write.argtypes = [vp, u64, i32, i32, vp, u64]
+    L.pbx_plane_band_info.argtypes = [vp, u64, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
+    L.pbx_node_init.argtypes = [ctypes.POINTER(PbxConfig), i32, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
+    L.pbx_node_shutdown.argtypes = [vp]
+    L.pbx_node_shutdown.restype = None
+    L.pbx_node_size.argtypes = [vp]
+    L.pbx_node_context.argtypes = [vp, i32]
+    L.pbx_node_context.restype = vp
+    L.pbx_node_route.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(i32)]
+    L.pbx_node_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult),
+                                    ctypes.POINTER(i32)]
     _lib = L
     return L
 
@@ -415,6 +432,21 @@ def ngff_multiscales(image_dir: str):
     return ms[0], image_dir
 
 
+def make_config(device: Optional[int] = None, png_filter: int = FILTER_NONE,
+                tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False,
+                tiff_tile: Optional[int] = None) -> PbxConfig:
+    cfg = PbxConfig()
+    _check(lib().pbx_config_default(ctypes.byref(cfg)))
+    cfg.device = -1 if device is None else device
+    cfg.png_filter = png_filter
+    cfg.tiff_deflate = 1 if tiff_deflate else 0
+    cfg.coalesce = 1 if coalesce else 0
+    cfg.stage_rows = 1 if stage_rows else 0
+    if tiff_tile is not None:  # else $PBX_TIFF_TILE or 0 (one strip, the reference's)
+        cfg.tiff_tile = int(tiff_tile)
+    return cfg
+
+
 class PixelsService:
     """Plane registry on one MI355X (the PixelsService / getPixels stand-in).
 
@@ -424,28 +456,28 @@ class PixelsService:
 
     def __init__(self, device: Optional[int] = None, png_filter: int = FILTER_NONE,
                  tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False,
-                 tiff_tile: Optional[int] = None):
+                 tiff_tile: Optional[int] = None, sparse_band_rows: int = 0, _handle=None):
+        """sparse_band_rows > 0: planes the handler opens on demand are sparse planes of bands
+        of that many rows (region-proportional residency); 0: whole planes (or the handler's
+        row band)."""
+        import threading
+        self.sparse_band_rows = int(sparse_band_rows)
+        self._load_lock = threading.Lock()  # one loader per plane key / band
+        self._loading: Dict[tuple, list] = {}  # key -> [lock, users]; removed with its last user
+        self._owned = _handle is None
+        if _handle is not None:  # a context owned by a PixelsNode
+            self._h = ctypes.c_void_p(_handle)
+            return
         L = lib()
-        cfg = PbxConfig()
-        _check(L.pbx_config_default(ctypes.byref(cfg)))
-        cfg.device = -1 if device is None else device
-        cfg.png_filter = png_filter
-        cfg.tiff_deflate = 1 if tiff_deflate else 0
-        cfg.coalesce = 1 if coalesce else 0
-        cfg.stage_rows = 1 if stage_rows else 0
-        if tiff_tile is not None:  # else $PBX_TIFF_TILE or 0 (one strip, the reference's)
-            cfg.tiff_tile = int(tiff_tile)
+        cfg = make_config(device, png_filter, tiff_deflate, coalesce, stage_rows, tiff_tile)
         h = ctypes.c_void_p()
         _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
-        import threading
-        self._load_lock = threading.Lock()  # load_plane: one loader per plane key
-        self._loading: Dict[tuple, "threading.Lock"] = {}
 
     def close(self) -> None:
-        if self._h:
+        if self._h and self._owned:
             lib().pbx_shutdown(self._h)
-            self._h = None
+        self._h = None
 
     def __enter__(self):
         return self
@@ -676,6 +708,70 @@ class PixelsService:
         _check(lib().pbx_residency_stats_get(self._h, ctypes.byref(s)))
         return {n: getattr(s, n) for n, _ in PbxResidencyStats._fields_}
 
+    # ------------------------------------------------------------- sparse (banded) planes
+    def create_sparse_plane(self, image_id: int, z: int, c: int, t: int, pixel_type: int, size_x: int,
+                            size_y: int, band_rows: int, level: int = 0,
+                            own: Optional[Tuple[int, int]] = None, big_endian: bool = True,
+                            generator: Optional[str] = None, seed: int = 0, plane_no: int = 0) -> int:
+        """pbx_plane_create_sparse: a plane held as bands of `band_rows` rows, each loaded on
+        demand (band_write) and evicted on its own; `own` = (y0, rows) limits the rows this
+        context may hold (another context owns the rest)."""
+        d = PbxPlaneDesc()
+        d.image_id, d.z, d.c, d.t, d.resolution = image_id, z, c, t, level
+        d.pixel_type, d.size_x, d.size_y = pixel_type, size_x, size_y
+        d.byte_order = BIG_ENDIAN if big_endian else LITTLE_ENDIAN
+        if generator is not None:
+            d.source = {"fake": SRC_GEN_FAKE, "noise": SRC_GEN_NOISE}[generator]
+            d.seed, d.plane_no = seed, plane_no
+        y0, rows = own if own is not None else (0, 0)
+        pid = ctypes.c_uint64()
+        _check(lib().pbx_plane_create_sparse(self._h, ctypes.byref(d), band_rows, y0, rows, ctypes.byref(pid)))
+        return pid.value
+
+    def band_write(self, plane_id: int, y0: int, rows: int, data: Optional[bytes]) -> None:
+        """pbx_band_write: rows [y0, y0 + rows) of one band (packed, the plane's byte order);
+        data None generates them (generator planes)."""
+        if data is None:
+            _check(lib().pbx_band_write(self._h, plane_id, y0, rows, None, 0))
+        else:
+            _check(lib().pbx_band_write(self._h, plane_id, y0, rows, data, len(data)))
+
+    def band_info(self, plane_id: int) -> Tuple[int, List[int]]:
+        """(band_rows, [state of band k]) of a sparse plane (BS_ABSENT / BS_LOADING / BS_READY)."""
+        br, nb = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().pbx_plane_band_info(self._h, plane_id, ctypes.byref(br), ctypes.byref(nb), None))
+        st = (ctypes.c_uint8 * max(nb.value, 1))()
+        _check(lib().pbx_plane_band_info(self._h, plane_id, ctypes.byref(br), ctypes.byref(nb), st))
+        return br.value, list(st)[:nb.value]
+
+    def test_fail_batch(self, ahead: int) -> None:
+        """Fault injection: the `ahead`-th batch launched from now on fails (500s); 0 = off."""
+        _check(lib().pbx_test_fail_batch(self._h, ahead))
+
+    # ------------------------------------------------------------- opening planes on demand
+    def _exclusive(self, key):
+        """Context manager: one loader per key (plane, or (plane, band)); the lock entry goes
+        with its last user."""
+        import contextlib
+        import threading
+
+        @contextlib.contextmanager
+        def cm():
+            with self._load_lock:
+                ent = self._loading.get(key)
+                if ent is None:
+                    ent = self._loading[key] = [threading.Lock(), 0]
+                ent[1] += 1
+            try:
+                with ent[0]:
+                    yield
+            finally:
+                with self._load_lock:
+                    ent[1] -= 1
+                    if ent[1] == 0:
+                        del self._loading[key]
+        return cm()
+
     def load_plane(self, source: "PixelSource", pixels: "Pixels", z: int, c: int, t: int,
                    level: int = 0, band: Optional[Tuple[int, int]] = None,
                    band_bytes: int = 64 << 20, timeout_s: float = 60.0) -> int:
@@ -683,13 +779,10 @@ class PixelsService:
         (TileRequestHandler.java:86,107-109,201-211): declare the image, create the plane (or
         only `band` = (y0, rows) of it), stream its rows from `source` in bands of about
         `band_bytes`, commit.  If another caller is loading the same key, wait for it."""
-        import threading
         import time
         self.declare_image(pixels)
         key = (pixels.image_id, z, c, t, level)
-        with self._load_lock:
-            lk = self._loading.setdefault(key, threading.Lock())
-        with lk:
+        with self._exclusive(key):
             found = self.lookup_plane(*key)
             if found is not None and found[1] == PS_READY:
                 return found[0]
@@ -718,6 +811,55 @@ class PixelsService:
                 self.release_plane(pid)
                 raise
             return pid
+
+    def load_bands(self, source: "PixelSource", pixels: "Pixels", z: int, c: int, t: int, level: int,
+                   y: int, h: int, own: Optional[Tuple[int, int]] = None,
+                   timeout_s: float = 60.0) -> int:
+        """Region-proportional loading (TileRequestHandler.java:102-109 reads only the region):
+        the sparse plane of the key (created if absent, bands of self.sparse_band_rows rows) gets
+        the bands that rows [y, y + h) cover, each read from `source` once; bands another
+        caller is loading are waited for.  Returns the plane id."""
+        import time
+        self.declare_image(pixels)
+        key = (pixels.image_id, z, c, t, level)
+        sx, sy = source.level_size(pixels, level)
+        with self._exclusive(key):
+            found = self.lookup_plane(*key)
+            if found is None or found[1] == PS_EVICTED:
+                try:
+                    pid = self.create_sparse_plane(pixels.image_id, z, c, t, pixels.pixel_type, sx, sy,
+                                                   self.sparse_band_rows, level, own=own)
+                except PbxError as e:
+                    if e.status != E_EXISTS:
+                        raise
+                    pid = self.lookup_plane(*key)[0]
+            else:
+                pid = found[0]
+        B, states = self.band_info(pid)
+        lo, hi = (own[0], own[0] + own[1]) if own is not None else (0, sy)
+        y0, y1 = max(y, lo), min(y + h, hi, sy)
+        for k in range(y0 // B, (y1 + B - 1) // B) if y1 > y0 else ():
+            if states[k] == BS_READY:
+                continue
+            with self._exclusive(key + (k,)):
+                deadline = time.monotonic() + timeout_s
+                while True:
+                    st = self.band_info(pid)[1][k]
+                    if st == BS_READY:
+                        break
+                    if st == BS_ABSENT:
+                        r0, r1 = max(k * B, lo), min((k + 1) * B, hi, sy)
+                        try:
+                            self.band_write(pid, r0, r1 - r0,
+                                            source.read_rows(pixels, z, c, t, level, r0, r1 - r0))
+                            break
+                        except PbxError as e:
+                            if e.status != E_EXISTS:  # another binding loads it: wait
+                                raise
+                    if time.monotonic() > deadline:
+                        raise PbxError(E_INTERNAL, "band %d of plane %d: timed out loading" % (k, pid))
+                    time.sleep(0.001)
+        return pid
 
     def build_pyramid(self, plane_id: int, levels: int, timing: bool = False):
         """Stored levels r+1 .. r+levels of a plane, built on the GPU (2x2 box means);
@@ -789,6 +931,67 @@ class PixelsService:
     # Batched async: submit returns at once, Ticket.wait() collects (pbx_submit / pbx_wait).
     def submit(self, ctxs: Sequence[TileCtx]) -> "Ticket":
         return Ticket(self, ctxs)
+
+
+class PixelsNode:
+    """N device contexts in ONE process (pbx_node_*): the reference runs all its worker
+    verticles in one JVM (PixelBufferMicroserviceVerticle.java:117-118,224-233), so a node-wide
+    drop-in holds one context per GPU and routes every getTile to the context holding its plane
+    or row band, or (planes replicated on every GPU) to the pbx_shard_of owner among them.
+    ``services[k]`` is context k as a PixelsService (register planes / bands there).  The same
+    device may be listed several times (tests run two contexts on one GPU)."""
+
+    def __init__(self, n: int, devices: Optional[Sequence[int]] = None, shard_tile: int = 512, **config):
+        L = lib()
+        cfg = make_config(**config)
+        devs = (ctypes.c_int32 * n)(*devices) if devices is not None else None
+        h = ctypes.c_void_p()
+        _check(L.pbx_node_init(ctypes.byref(cfg), n, devs, shard_tile, ctypes.byref(h)))
+        self._h = h
+        self.services = [PixelsService(_handle=L.pbx_node_context(h, k)) for k in range(n)]
+
+    def route(self, ctx: TileCtx) -> Tuple[int, int]:
+        """(status the serving context would answer, its index); E_NOT_RESIDENT -> the index is
+        the shard owner, where the binding should load the plane."""
+        req = ctx.to_req()
+        k = ctypes.c_int32()
+        st = lib().pbx_node_route(self._h, ctypes.byref(req), ctypes.byref(k))
+        if st == E_BADARG:
+            _check(st)
+        return st, k.value
+
+    def get_tile(self, ctx: TileCtx) -> Tuple[int, Optional[bytes], int]:
+        """(status, body, index of the context that served it)."""
+        req = ctx.to_req()
+        res = PbxResult()
+        k = ctypes.c_int32(-1)
+        lib().pbx_node_get_tile(self._h, ctypes.byref(req), ctypes.byref(res), ctypes.byref(k))
+        try:
+            body = ctypes.string_at(res.data, res.len) if res.status == OK and res.len else (
+                b"" if res.status == OK else None)
+            ctx.region["width"], ctx.region["height"] = res.w, res.h
+        finally:
+            lib().pbx_results_release(None, ctypes.byref(res), 1)
+        return res.status, body, k.value
+
+    def close(self) -> None:
+        if self._h:
+            for s_ in self.services:
+                s_._h = None
+            lib().pbx_node_shutdown(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Ticket:
@@ -938,10 +1141,17 @@ class TileRequestHandler:
 
     With a ``source`` (PixelSource), a plane the context does not hold (status
     E_NOT_RESIDENT) is opened as the reference opens it per request — getPixels (:84; None ->
-    404), getPixelBuffer + getTileDirect (:86,107-109) — loaded into HBM once, and the request
-    retried.  ``band`` = (y0, rows) loads only that row band (a rank's share of a whole slide);
-    requests outside it stay E_NOT_RESIDENT and are answered None here (another rank serves
-    them).  Without a source the context is a closed registry: not resident -> None (404)."""
+    404), getPixelBuffer + getTileDirect (:86,107-109) — loaded into HBM, and the request
+    retried.  The service's policy decides what is loaded: the whole plane, or (with
+    ``sparse_band_rows``) only the bands the request's rows cover (region-proportional, as
+    getTileDirect reads only the region).  ``band`` = (y0, rows) limits what this context
+    holds (a rank's share of a whole slide); requests outside it are answered None here
+    (another rank serves them).  Between a load and the retry another loader may evict what
+    was loaded (a residency budget smaller than the working set): the load is retried, and a
+    tile that still cannot be held is a 500, never the reference's 404.  Without a source the
+    context is a closed registry: not resident -> None (404)."""
+
+    LOAD_ATTEMPTS = 4
 
     def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx,
                  source: Optional[PixelSource] = None, band: Optional[Tuple[int, int]] = None):
@@ -950,24 +1160,43 @@ class TileRequestHandler:
         self.source = source
         self.band = band
 
-    def get_tile(self, client=None) -> Optional[bytes]:
-        status, body = self.pixels_service.get_tile(self.tile_ctx)
-        if status == E_NOT_RESIDENT and self.source is not None:
-            pixels = self.source.get_pixels(self.tile_ctx.imageId)
-            if pixels is None:
-                return None  # :130-132 "Cannot find Image"
-            level = 0
-            r = self.tile_ctx.resolution
-            if r is not None:
-                level = pixels.levels - 1 - r  # OMERO numbering -> stored level (include/pbx.h)
-            if 0 <= level < pixels.levels and 0 <= self.tile_ctx.z < pixels.size_z and \
-                    0 <= self.tile_ctx.c < pixels.size_c and 0 <= self.tile_ctx.t < pixels.size_t:
-                self.pixels_service.load_plane(self.source, pixels, self.tile_ctx.z,
-                                               self.tile_ctx.c, self.tile_ctx.t, level, self.band)
-            else:
-                self.pixels_service.declare_image(pixels)  # the retry answers the 404
-            status, body = self.pixels_service.get_tile(self.tile_ctx)
+    @staticmethod
+    def _answer(status: int, body: Optional[bytes]) -> Optional[bytes]:
+        """The tile, None for every status the reference answers null (-> 404), and an
+        exception (-> 500, PixelBufferVerticle.java:141-146) for a device failure."""
+        if status == E_INTERNAL:
+            raise PbxError(E_INTERNAL, "tile batch failed on the device: " +
+                           lib().pbx_last_error().decode(errors="replace"))
         return body if status == OK else None
+
+    def get_tile(self, client=None) -> Optional[bytes]:
+        svc, tc = self.pixels_service, self.tile_ctx
+        status, body = svc.get_tile(tc)
+        if status != E_NOT_RESIDENT or self.source is None:
+            return self._answer(status, body)
+        pixels = self.source.get_pixels(tc.imageId)
+        if pixels is None:
+            return None  # :130-132 "Cannot find Image"
+        level = 0
+        if tc.resolution is not None:
+            level = pixels.levels - 1 - tc.resolution  # OMERO numbering -> stored level (include/pbx.h)
+        if not (0 <= level < pixels.levels and 0 <= tc.z < pixels.size_z and
+                0 <= tc.c < pixels.size_c and 0 <= tc.t < pixels.size_t):
+            svc.declare_image(pixels)  # the retry answers the reference's 404
+            return self._answer(*svc.get_tile(tc))
+        y, h = tc.y, (tc.h or pixels.size_y)  # :92-97 defaulting from the full-resolution size
+        if self.band is not None and not (self.band[0] <= y and y + h <= self.band[0] + self.band[1]):
+            return None  # rows of another context's band
+        for _ in range(self.LOAD_ATTEMPTS):
+            if svc.sparse_band_rows:
+                svc.load_bands(self.source, pixels, tc.z, tc.c, tc.t, level, y, h, own=self.band)
+            else:
+                svc.load_plane(self.source, pixels, tc.z, tc.c, tc.t, level, self.band)
+            status, body = svc.get_tile(tc)
+            if status != E_NOT_RESIDENT:
+                return self._answer(status, body)
+        raise PbxError(E_INTERNAL, "Image:%d z=%d c=%d t=%d: the plane could not be held resident "
+                       "(residency budget smaller than the working set)" % (tc.imageId, tc.z, tc.c, tc.t))
 
     getTile = get_tile
 

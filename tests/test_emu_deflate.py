@@ -135,8 +135,15 @@ def test_blocks_split_segments_evenly(n):
     counts = [-(-b.len // seg_len) for b in blks]
     assert sum(counts) == nseg
     assert max(counts) <= blk and max(counts) - min(counts) <= 1
-    if n == 524800:
-        assert counts == ([33] if blk >= 33 else [11, 11, 11] if blk == 16 else counts)
+    # the exact even split of block_seg0 (pbx_config.h): block j holds [j*nseg/nb, (j+1)*nseg/nb)
+    nb = -(-nseg // blk)
+    assert counts == [(j + 1) * nseg // nb - j * nseg // nb for j in range(nb)]
+    if n == 524800:  # the headline tile: 33 segments
+        assert nseg == 33
+        if blk >= 33:
+            assert counts == [33]
+        elif blk == 16:
+            assert counts == [11, 11, 11]
 
 
 def test_div_rcp_exact():

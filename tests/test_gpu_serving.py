@@ -1,0 +1,264 @@
+"""Serving-path parity on the GPU:
+
+* configs[0] at its own workload: 512x512 uint8 PNG tiles of a 4096^2 Bio-Formats-fake
+  (G_FAKE) plane, the reference's CPU case (TileRequestHandler.java:119-124,176-199);
+* the reference's 404s are answered before anything is loaded (:84, :100-103, :125-132);
+* a device failure fails its batch with 500 and nothing else (PixelBufferVerticle.java:
+  131-146; SURVEY.md §5 fault injection), through the coalescer and the batch paths;
+* N device contexts in one process (the reference's one JVM, PixelBufferMicroserviceVerticle.
+  java:117-118,224-233): requests routed by band ownership and pbx_shard_of.
+
+Every body is checked against the CPU oracle (oracle/pbx_oracle.c).
+"""
+import itertools
+import threading
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import pbx
+import _emu
+
+pytestmark = pytest.mark.gpu
+
+_ids = itertools.count(700000, 10)
+FAKE, NOISE = 1, 2
+
+
+# ------------------------------------------------------------------- configs[0]
+
+C1_TILES = [(0, 0), (512, 0), (1536, 2048), (3584, 3584)]
+
+
+def test_c1_png_512x512_u8_fake(service, oracle):
+    """BASELINE configs[0]: 512x512 uint8 PNG tiles from a 4096^2 G_FAKE plane.  Each decodes
+    to the oracle's pixels, its inflated IDAT is the oracle's filter-None scanlines, and its
+    zlib stream is the CPU emulation of the deflate workgroups byte for byte; the single-tile
+    path (pbx_get_tile through the coalescer, as one Vert.x worker calls it) returns the same
+    bytes as the batch path on every repetition."""
+    iid = next(_ids)
+    pt, side = pbx.UINT8, 4096
+    service.register_plane(iid, 0, 0, 0, pt, side, side, generator="fake")
+    ctxs = [pbx.TileCtx(iid, 0, 0, 0, x, y, 512, 512, format="png") for x, y in C1_TILES]
+    res = service.get_tiles(ctxs)
+    z6 = []
+    for (x, y), (st, body) in zip(C1_TILES, res):
+        assert st == pbx.OK
+        tile = oracle.gen_region(FAKE, pt, x, y, 512, 512)
+        r, px, meta = oracle.png_decode(body)
+        assert r == 0 and px == tile.tobytes(), (x, y)
+        assert (meta["w"], meta["h"], meta["depth"], meta["color_type"]) == (512, 512, 8, 0)
+        stream = oracle.png_filter_stream(tile, pt, 512, 512, 0).tobytes()
+        r, idat = oracle.png_inflate_idat(body, len(stream))
+        assert r == 0 and idat == stream
+        z, _ = _emu.deflate(stream, 513)
+        assert body[99:99 + len(z)] == z
+        z6.append(len(zlib.compress(stream, 6)))
+    # compressed size against the reference's zlib-6 (ImageIO) stream, recorded for DESIGN §2
+    mine = [int.from_bytes(b[91:95], "big") for _, b in res]
+    assert all(m <= 2 * max(z, 1024) for m, z in zip(mine, z6)), (mine, z6)
+    # the served single-tile path: identical bytes, every time
+    first = res[0][1]
+    for _ in range(20):
+        st, body = service.get_tile(pbx.TileCtx(iid, 0, 0, 0, 0, 0, 512, 512, format="png"))
+        assert st == pbx.OK and body == first
+    # and through the event-bus consumer: 200, the filename and Content-Type headers
+    st, body, hdr = pbx.handle_get_tile(service, pbx.TileCtx(iid, 0, 0, 0, 0, 0, 512, 512,
+                                                               format="png").to_json())
+    assert st == 200 and body == first and hdr["Content-Type"] == "image/png"
+    assert hdr["filename"] == "image%d_z0_c0_t0_x0_y0_w512_h512.png" % iid
+
+
+# ------------------------------------------------------- 404 before NOT_RESIDENT
+
+class CountingSource(pbx.PixelSource):
+    def __init__(self, oracle, images):
+        self.oracle, self.images = oracle, dict(images)
+        self.lookups = self.reads = 0
+        self.lock = threading.Lock()
+
+    def get_pixels(self, image_id):
+        with self.lock:
+            self.lookups += 1
+        return self.images.get(image_id)
+
+    def read_rows(self, pixels, z, c, t, level, y0, rows):
+        with self.lock:
+            self.reads += 1
+        return self.oracle.gen_region(NOISE, pixels.pixel_type, 0, y0, pixels.size_x, rows, seed=11,
+                                      z=z, c=c, t=t).tobytes()
+
+
+def test_cold_image_404s_load_nothing(service, oracle):
+    """format=jpg, or a region no pixel type makes a Java byte[], on an image this context has
+    never seen: the reference's 404 at once (TileRequestHandler.java:100-103,125-126), with no
+    getPixels and no PixelSource read; a good request on the same cold image loads it."""
+    iid = next(_ids)
+    src = CountingSource(oracle, {iid: pbx.Pixels(iid, pbx.UINT16, 3000, 2000)})
+    for tc in (pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64, format="jpg"),
+               pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64, format="PNG"),
+               pbx.TileCtx(iid, 0, 0, 0, 0, 0, 50000, 50000),
+               pbx.TileCtx(iid, 0, 0, 0, 0, 0, -5, 64)):
+        assert pbx.TileRequestHandler(service, tc, src).get_tile() is None
+        st, _, _ = pbx.handle_get_tile(service, tc.to_json(), src)
+        assert st == 404
+    assert (src.lookups, src.reads) == (0, 0)
+    tc = pbx.TileCtx(iid, 0, 0, 0, 100, 50, 64, 64)
+    assert pbx.TileRequestHandler(service, tc, src).get_tile() == \
+        oracle.gen_region(NOISE, pbx.UINT16, 100, 50, 64, 64, seed=11).tobytes()
+    assert src.reads >= 1
+    service.release_image(iid)
+
+
+def test_eviction_between_load_and_retry_is_never_404(oracle):
+    """a budget that holds ONE plane and concurrent requests to two planes: a plane
+    evicted between its load and the retry is loaded again; every tile is served exactly, none
+    answers 404."""
+    pt, side = pbx.UINT16, 1024
+    pbytes = (side * 2 + 255) // 256 * 256 * side + 256
+    iid = next(_ids)
+    src = CountingSource(oracle, {iid: pbx.Pixels(iid, pt, side, side, size_c=2)})
+    with pbx.PixelsService() as svc:
+        svc.set_residency_budget(int(1.5 * pbytes))
+        ctxs = [pbx.TileCtx(iid, 0, k % 2, 0, 64 * (k % 7), 32 * (k % 5), 256, 256) for k in range(96)]
+        errors = []
+
+        def one(tc):
+            try:
+                body = pbx.TileRequestHandler(svc, tc, src).get_tile()
+            except pbx.PbxError as e:  # a plane that cannot be held is a 500, never a 404
+                assert e.status in (pbx.E_INTERNAL, pbx.E_NO_SPACE)  # both -> 500 (handle_get_tile)
+                return "500"
+            want = oracle.gen_region(NOISE, pt, tc.x, tc.y, 256, 256, seed=11, c=tc.c).tobytes()
+            if body != want:
+                errors.append((tc.c, tc.x, tc.y))
+            return "ok"
+
+        with ThreadPoolExecutor(16) as ex:
+            outcomes = list(ex.map(one, ctxs))
+        assert not errors, errors[:4]
+        assert outcomes.count("ok") >= len(ctxs) - 8  # at most a few give up after 4 loads
+        assert svc.residency_stats()["evictions"] >= 1
+
+
+# ------------------------------------------------------------- fault injection
+
+def test_failed_batch_is_500_for_its_requests_only(oracle):
+    """PBX fault injection: the 3rd batch the coalescer launches fails on the device.  With 32
+    concurrent callers, exactly that batch's requests answer 500 (a request that is the
+    reference's 404 keeps its 404), every other response is exact, and the context serves
+    normally afterwards (PixelBufferVerticle.java:131-146)."""
+    iid = next(_ids)
+    pt, side = pbx.UINT16, 4096
+    with pbx.PixelsService() as svc:
+        svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=11)
+        rng = np.random.default_rng(4)
+        reqs = []
+        for k in range(512):
+            if k % 17 == 5:
+                reqs.append(pbx.TileCtx(iid, 0, 0, 0, side - 10, 0, 64, 64, format="png"))  # 404
+            else:
+                x, y = (int(v) for v in rng.integers(0, side - 256, 2))
+                reqs.append(pbx.TileCtx(iid, 0, 0, 0, x, y, 256, 256, format=["png", None, "tif"][k % 3]))
+        b0, _ = svc.ctx_stats()
+        svc.test_fail_batch(3)
+        out = [None] * len(reqs)
+        barrier = threading.Barrier(32)
+
+        def worker(w):
+            barrier.wait()
+            for j in range(w, len(reqs), 32):
+                out[j] = svc.get_tile(reqs[j])
+
+        with ThreadPoolExecutor(32) as ex:
+            list(ex.map(worker, range(32)))
+        failed = [j for j, (st, _) in enumerate(out) if st == pbx.E_INTERNAL]
+        assert 1 <= len(failed) <= 64, len(failed)  # one coalesced batch (<= 64 requests)
+        for j, (st, body) in enumerate(out):
+            tc = reqs[j]
+            if tc.x == side - 10:
+                assert st == 404 and body is None
+                continue
+            if j in failed:
+                assert body is None
+                continue
+            assert st == pbx.OK, (j, st)
+            want = oracle.gen_region(NOISE, pt, tc.x, tc.y, 256, 256, seed=11)
+            if tc.format is None:
+                assert body == want.tobytes()
+            elif tc.format == "png":
+                r, px, _ = oracle.png_decode(body)
+                assert r == 0 and px == want.tobytes()
+            else:
+                assert body == oracle.tiff_encode(want, pt, 256, 256)[1]
+        b1, _ = svc.ctx_stats()
+        assert b1 - b0 >= 3
+        # the context keeps serving, on every path; and the event-bus consumer maps 500
+        st, body = svc.get_tile(reqs[0])
+        assert st == pbx.OK
+        svc.test_fail_batch(1)
+        st, _, _ = pbx.handle_get_tile(svc, reqs[0].to_json())
+        assert st == 500
+        svc.test_fail_batch(1)  # pbx_get_tiles (one synchronous batch)
+        res = svc.get_tiles(reqs[:8])
+        assert all(s == (404 if r.x == side - 10 else 500) for r, (s, _) in zip(reqs[:8], res))
+        svc.test_fail_batch(2)  # pbx_submit / pbx_wait: the second of two tickets fails
+        t1, t2 = svc.submit(reqs[:8]), svc.submit(reqs[8:16])
+        assert all(s == (404 if r.x == side - 10 else 0) for r, (s, _) in zip(reqs[:8], t1.wait()))
+        assert all(s == (404 if r.x == side - 10 else 500) for r, (s, _) in zip(reqs[8:16], t2.wait()))
+        assert [s for s, _ in svc.get_tiles(reqs[16:24])] == [404 if r.x == side - 10 else 0 for r in reqs[16:24]]
+
+
+# ---------------------------------------------------------------- node routing
+
+def test_node_two_contexts_one_device(oracle):
+    """Two contexts in one process on device 0 (SURVEY §4.5 "fake device count"): a slide split
+    into two row bands (context 0 holds rows [0, 2048), context 1 rows [2048, 4096)) and a plane
+    replicated in both.  32 concurrent callers through pbx_node_get_tile: band requests land on
+    their owner, replicated ones on their pbx_shard_of owner, and every body is exact."""
+    pt, side = pbx.UINT16, 4096
+    slide, rep = next(_ids), next(_ids)
+    with pbx.PixelsNode(2, devices=[0, 0]) as node:
+        for k, s_ in enumerate(node.services):
+            s_.create_plane(slide, 0, 0, 0, pt, side, side, band=(2048 * k, 2048), generator="noise",
+                            seed=11)
+            s_.register_plane(rep, 0, 0, 0, pt, side, side, generator="noise", seed=11)
+        rng = np.random.default_rng(8)
+        reqs = []
+        for k in range(640):
+            img = slide if k % 2 else rep
+            x = int(rng.integers(0, side // 512)) * 512
+            y = int(rng.integers(0, side // 512)) * 512
+            reqs.append(pbx.TileCtx(img, 0, 0, 0, x, y, 512, 512, format=["png", None][k % 4 == 1]))
+        # a region straddling the two bands: no context holds it
+        st, owner = node.route(pbx.TileCtx(slide, 0, 0, 0, 0, 2000, 512, 512))
+        assert st == pbx.E_NOT_RESIDENT and owner == pbx.shard_of(pbx.TileCtx(slide, 0, 0, 0, 0, 2000, 512, 512), 2)
+        out = [None] * len(reqs)
+        barrier = threading.Barrier(32)
+
+        def worker(w):
+            barrier.wait()
+            for j in range(w, len(reqs), 32):
+                out[j] = node.get_tile(reqs[j])
+
+        with ThreadPoolExecutor(32) as ex:
+            list(ex.map(worker, range(32)))
+        served = [0, 0]
+        for tc, (st, body, k) in zip(reqs, out):
+            assert st == pbx.OK
+            if tc.imageId == slide:
+                assert k == (0 if tc.y < 2048 else 1)
+            else:
+                assert k == pbx.shard_of(tc, 2)
+            served[k] += 1
+            want = oracle.gen_region(NOISE, pt, tc.x, tc.y, 512, 512, seed=11).tobytes()
+            if tc.format is None:
+                assert body == want
+            else:
+                r, px, _ = oracle.png_decode(body)
+                assert r == 0 and px == want
+        assert min(served) > 100
+        stats = [s_.ctx_stats()[1] for s_ in node.services]
+        assert sum(stats) == len(reqs) and min(stats) > 100
