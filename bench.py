@@ -178,19 +178,89 @@ def load_issue(kernels=("k_encode", "k_lz77")):
     return out
 
 
+def cpu_model():
+    """The host CPU model string (quote the CPU with the baseline)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _timed_oracle(run, seconds, threads):
+    """Calibrate on a short run, then time ~`seconds` of work: (items, seconds, bytes)."""
+    n0 = 2 * threads
+    sec, _ = run(n0)
+    n = max(threads, int(n0 / sec * seconds))
+    sec, nbytes = run(n)
+    return n, sec, nbytes
+
+
 def cpu_baseline(seconds=10.0, threads=16):
-    """The C oracle (zlib-6 filter-None PNG, same region extraction) on host threads."""
+    """The C oracle (zlib-6 filter-None PNG, same region extraction) on host threads: the
+    headline's 512x512 uint16 G_NOISE tiles on `threads` threads (the reported value), and on
+    one thread, and G_FAKE tiles; the CPU model is stated."""
     import _oracle as O
     O.lib()
     pw = ph = 4096
-    sec, _ = O.bench(O.GEN_NOISE, O.UINT16, O.FMT_PNG, pw, ph, TILE, TILE, 2 * threads, threads)
-    rate = 2 * threads / sec
-    n = max(threads, int(rate * seconds))
-    sec, nbytes = O.bench(O.GEN_NOISE, O.UINT16, O.FMT_PNG, pw, ph, TILE, TILE, n, threads)
+
+    def grid(kind, th):
+        return lambda n: O.bench(kind, O.UINT16, O.FMT_PNG, pw, ph, TILE, TILE, n, th)
+
+    n, sec, nbytes = _timed_oracle(grid(O.GEN_NOISE, threads), seconds, threads)
+    n1, sec1, _ = _timed_oracle(grid(O.GEN_NOISE, 1), seconds / 2, 1)
+    nf, secf, nbf = _timed_oracle(grid(O.GEN_FAKE, threads), seconds / 4, threads)
     return {"value": round(n / sec, 2), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "single_thread": {"value": round(n1 / sec1, 2), "unit": "tiles/s", "cores": 1,
+                              "sample": f"{n1} G_NOISE tiles, {sec1:.1f} s"},
+            "g_fake": {"value": round(nf / secf, 2), "unit": "tiles/s", "cores": threads,
+                       "sample": f"{nf} 512x512 uint16 G_FAKE tiles -> PNG, {secf:.1f} s; "
+                                 f"avg {nbf / nf:.0f} B/tile"},
             "sample": f"{n} tiles 512x512 uint16 G_NOISE -> PNG (filter None, zlib level 6) "
                       f"from a 4096x4096 plane, oracle/pbx_oracle.c on {threads} threads, "
                       f"{sec:.1f} s; avg {nbytes / n:.0f} B/tile"}
+
+
+def c1_line(svc, rank, world, barrier, threads=16, reps=2000):
+    """BASELINE configs[0] at its own workload: ONE 512x512 uint8 PNG request, tile (0, 0) of a
+    4096^2 Bio-Formats-fake (G_FAKE) plane, repeated (TileRequestHandler.java:119-124,
+    176-199).  GPU: (a) one caller in a loop through pbx_get_tile (the coalescer, D2H and the
+    JNI-style body copy included; native loop), p50/p99 latency; (b) the request repeated 1024x
+    in one device-resident batch, as the coalescer forms it under load.  CPU: the oracle for
+    the same request on 1 thread and on `threads` threads, with the CPU model."""
+    iid = 6
+    side = 4096
+    svc.register_plane(iid, 0, 0, 0, pbx.UINT8, side, side, generator="fake", plane_no=0)
+    tc = pbx.TileCtx(iid, 0, 0, 0, 0, 0, TILE, TILE, format="png")
+    one = serve_one(svc, [tc], 1, reps, 200)
+    ctxs = [tc] * 1024
+    dt, st, _ = secondary_steps(svc, ctxs, 5, 2, barrier)
+    line = {"request": "tile (0,0,512,512) uint8 png of a 4096^2 G_FAKE plane",
+            "single_caller_get_tile": one,
+            "batched_1024_repeats": {"tiles_per_s": round(len(ctxs) * 5 * world / dt, 1),
+                                     **wall_vs_kernels(dt, 5, st),
+                                     "bytes_per_tile": round(st[-1].deflate_out_bytes / len(ctxs), 1)}}
+    if rank == 0 and world == 1:
+        import _oracle as O
+        O.lib()
+        cpu = {}
+        for th in (1, threads):
+            n, sec, nbytes = _timed_oracle(
+                lambda k: O.bench_at(O.GEN_FAKE, O.UINT8, O.FMT_PNG, side, side, 0, 0, TILE, TILE, k, th),
+                3.0, th)
+            cpu[f"threads_{th}"] = {"tiles_per_s": round(n / sec, 1), "cores": th,
+                                    "latency_ms": round(1e3 * sec * th / n, 3),
+                                    "bytes_per_tile": round(nbytes / n, 1), "sample": f"{n} requests, {sec:.1f} s"}
+        cpu["kind"] = "port"
+        cpu["cpu_model"] = cpu_model()
+        line["cpu_oracle"] = cpu
+        line["gpu_over_cpu_1_thread_latency"] = round(cpu["threads_1"]["latency_ms"] / one["p50_ms"], 2)
+    svc.release_plane(svc.lookup_plane(iid, 0, 0, 0)[0])
+    return line
 
 
 def zarr_lines(svc, rank, world, side=16384, chunk=512, reps=3):
@@ -310,31 +380,32 @@ class ServeStats(ctypes.Structure):
                                                "mean_us")]
 
 
+def serve_one(svc, ctxs, threads, total, warmup):
+    """T native caller threads, each blocking in one pbx_get_tile at a time over `ctxs`
+    (lib/libpbx_servebench.so, no Python in the loop): tiles/s and latency percentiles."""
+    L = ctypes.CDLL(os.path.join(ROOT, "omero-ms-pixel-buffer_amd", "lib", "libpbx_servebench.so"))
+    L.pbx_serve_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ServeStats)]
+    reqs = pbx.make_reqs(ctxs)
+    s = ServeStats()
+    rc = L.pbx_serve_bench(svc.handle, reqs, len(ctxs), threads, total, warmup, ctypes.byref(s))
+    if rc != 0:
+        raise RuntimeError(f"pbx_serve_bench: {rc}")
+    return {"tiles_per_s": round(s.ok / s.seconds, 1), "requests": s.requests, "ok": s.ok,
+            "requests_per_batch": round(s.requests / max(s.batches, 1), 1),
+            "p50_ms": round(s.p50_us / 1e3, 3), "p90_ms": round(s.p90_us / 1e3, 3),
+            "p99_ms": round(s.p99_us / 1e3, 3), "max_ms": round(s.max_us / 1e3, 3),
+            "d2h_gbps": round(s.bytes / s.seconds / 1e9, 1)}
+
+
 def serve_lines(svc, iid, threads=(32, 128, 512)):
     """The served path as the reference drives it: T worker threads (Vert.x
     worker_pool_size, PixelBufferMicroserviceVerticle.java:117-118,224-233), each blocking in
     one getTile at a time -> pbx_get_tile (coalesced into GPU batches), D2H and the JNI-style
     copy of every body included.  Native threads (lib/libpbx_servebench.so), no Python in the
     loop.  512x512 uint16 PNG tiles of the headline plane."""
-    L = ctypes.CDLL(os.path.join(ROOT, "omero-ms-pixel-buffer_amd", "lib", "libpbx_servebench.so"))
-    L.pbx_serve_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
-                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ServeStats)]
     ctxs = grid_ctxs(iid, "png")
-    reqs = pbx.make_reqs(ctxs)
-    res = {}
-    for t in threads:
-        s = ServeStats()
-        total = max(8192, 32 * t)
-        rc = L.pbx_serve_bench(svc.handle, reqs, len(ctxs), t, total, max(2048, 4 * t), ctypes.byref(s))
-        if rc != 0:
-            raise RuntimeError(f"pbx_serve_bench: {rc}")
-        res[f"threads_{t}"] = {
-            "tiles_per_s": round(s.ok / s.seconds, 1), "requests": s.requests, "ok": s.ok,
-            "requests_per_batch": round(s.requests / max(s.batches, 1), 1),
-            "p50_ms": round(s.p50_us / 1e3, 3), "p90_ms": round(s.p90_us / 1e3, 3),
-            "p99_ms": round(s.p99_us / 1e3, 3), "max_ms": round(s.max_us / 1e3, 3),
-            "d2h_gbps": round(s.bytes / s.seconds / 1e9, 1)}
-    return res
+    return {f"threads_{t}": serve_one(svc, ctxs, t, max(8192, 32 * t), max(2048, 4 * t)) for t in threads}
 
 
 def run_stream(svc, req_chunks, barrier, warmup=1, steps=1):
@@ -541,6 +612,9 @@ def extra(out, svc, rank, world, barrier, iid, side):
     progress(rank, "served path")
     # (one node's ranks together: 512 callers per rank only on a single GPU)
     out["served_get_tile_512x512_u16_png"] = serve_lines(svc, iid, (32, 128, 512) if world == 1 else (32, 128))
+    # configs[0]: the reference's own CPU case at its workload, GPU and CPU side by side
+    progress(rank, "configs[0]")
+    out["c1_png_512x512_u8_fake"] = c1_line(svc, rank, world, barrier)
     # configs[1]: raw path, extraction + byte swap (HBM-bound k_extract)
     progress(rank, "raw")
     raw = grid_ctxs(iid, None)

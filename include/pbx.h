@@ -394,7 +394,8 @@ int32_t pbx_node_size(pbx_node* node);
 pbx_ctx* pbx_node_context(pbx_node* node, int32_t k);
 /* The context that serves `req`: *index = a context that holds the plane (the status it would
  * answer is returned: PBX_OK, or the reference's 404 ...), else PBX_E_NOT_RESIDENT with *index =
- * the pbx_shard_of owner, the context the binding should load the plane into. */
+ * the context the binding should load into: the one whose sparse plane owns the rows (bands not
+ * loaded yet), else the pbx_shard_of owner. */
 int pbx_node_route(pbx_node* node, const pbx_tile_req* req, int32_t* index);
 /* pbx_get_tile on the routed context (served_by may be NULL); results are released with
  * pbx_results_release (any context of the node, or NULL). */

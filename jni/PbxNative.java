@@ -108,6 +108,43 @@ final class PbxNative {
     static native byte[] getTile(long ctx, long imageId, int z, int c, int t, int resolution,
                                  int x, int y, int w, int h, String format, int[] statusOut);
 
+    /**
+     * pbx_plane_create_sparse: a plane held as bands of bandRows rows, each loaded on demand
+     * (writeBand) and evicted on its own under the residency budget — region-proportional
+     * residency, as getTileDirect reads only the requested region (:102-109).  ownY0/ownRows
+     * (0/0 = all): the rows this context may hold.  Returns 0 when the key is taken (409).
+     */
+    static native long createSparsePlane(long ctx, long imageId, int z, int c, int t, int level,
+                                         String pixelsType, int sizeX, int sizeY, boolean littleEndian,
+                                         int bandRows, int ownY0, int ownRows);
+
+    /**
+     * pbx_band_write: rows [y0, y0 + rows) of ONE band from data[off ..], e.g. one
+     * getTileDirect(z, c, t, 0, y0, sizeX, rows, data); copied out in pieces.  Returns false
+     * when the band is resident or being loaded by another caller (409).
+     */
+    static native boolean writeBand(long ctx, long planeId, int y0, int rows, int rowBytes, byte[] data,
+                                    int off);
+
+    /** pbx_plane_band_info: bandRows; states[k] = 0 absent, 1 loading, 2 resident (may be null). */
+    static native int bandInfo(long ctx, long planeId, byte[] states);
+
+    /**
+     * pbx_node_init: `n` device contexts in this JVM (devices null = 0..n-1), one per GPU of the
+     * node; nodeContext(node, k) is context k (declare / load planes there).  nodeGetTile routes
+     * a request to the context holding its plane or row band (statusOut[3] = its index; on
+     * NOT_RESIDENT the context to load into).  PixelBufferMicroserviceVerticle.java:224-233.
+     */
+    static native long nodeInit(int n, int[] devices, int pngFilter, boolean tiffDeflate, int tiffTile,
+                                int shardTile);
+
+    static native void nodeShutdown(long node);
+
+    static native long nodeContext(long node, int k);
+
+    static native byte[] nodeGetTile(long node, long imageId, int z, int c, int t, int resolution,
+                                     int x, int y, int w, int h, String format, int[] statusOut);
+
     static final int RESOLUTION_NONE = -1;
 
     /** TileCtx.resolution (Integer, may be null) -> the int getTile takes. */

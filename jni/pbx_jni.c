@@ -305,11 +305,9 @@ JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_
     return (jlong)id;
 }
 
-/* statusOut (length >= 3): [0] w, [1] h after the :92-97 defaulting, [2] the pbx status. */
-JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_getTile(
-        JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint res,
-        jint x, jint y, jint w, jint h, jstring jfmt, jintArray status_out) {
-    (void)cls;
+/* One getTile through a context (node == 0) or a node's router. */
+static jbyteArray tile_call(JNIEnv* env, jlong ctx, jlong node, jlong image, jint z, jint c, jint t, jint res,
+                            jint x, jint y, jint w, jint h, jstring jfmt, jintArray status_out) {
     pbx_tile_req req;
     memset(&req, 0, sizeof req);
     req.image_id = image; req.z = z; req.c = c; req.t = t; req.resolution = res;
@@ -321,12 +319,15 @@ JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNa
     pbx_result r;
     memset(&r, 0, sizeof r);   /* pbx_get_tile may return before it writes the result */
     r.status = PBX_E_INTERNAL;
-    int st = pbx_get_tile(PBX_CTX(ctx), &req, &r);
+    int32_t served_by = -1;
+    int st = node ? pbx_node_get_tile((pbx_node*)(intptr_t)node, &req, &r, &served_by)
+                  : pbx_get_tile(PBX_CTX(ctx), &req, &r);
     /* a call-level failure (null ctx, shutdown, failed plan) leaves the result unfilled */
     const int status = r.owner || r.status == st ? r.status : st;
     if (status_out && (*env)->GetArrayLength(env, status_out) >= 3) {
-        jint v[3] = {r.w, r.h, status};
-        (*env)->SetIntArrayRegion(env, status_out, 0, 3, v);
+        jint v[4] = {r.w, r.h, status, served_by};
+        const jsize n = node && (*env)->GetArrayLength(env, status_out) >= 4 ? 4 : 3;
+        (*env)->SetIntArrayRegion(env, status_out, 0, n, v);
     }
     jbyteArray out = NULL;
     if (status == PBX_OK) {
@@ -338,10 +339,165 @@ JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNa
         out = (*env)->NewByteArray(env, (jsize)r.len);   /* exact length, :188-193 */
         if (out && r.len) (*env)->SetByteArrayRegion(env, out, 0, (jsize)r.len, (const jbyte*)r.data);
     }
-    if (r.owner) pbx_results_release(PBX_CTX(ctx), &r, 1);
+    if (r.owner) pbx_results_release(NULL, &r, 1);
     if (status == PBX_E_INTERNAL) {
         throw_status(env, status);   /* -> 500 */
         return NULL;
     }
     return out;   /* null for every status the reference answers null, and NOT_RESIDENT */
+}
+
+/* statusOut (length >= 3): [0] w, [1] h after the :92-97 defaulting, [2] the pbx status. */
+JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_getTile(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint res,
+        jint x, jint y, jint w, jint h, jstring jfmt, jintArray status_out) {
+    (void)cls;
+    return tile_call(env, ctx, 0, image, z, c, t, res, x, y, w, h, jfmt, status_out);
+}
+
+/* ---- sparse (banded) planes: region-proportional residency */
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_createSparsePlane(
+        JNIEnv* env, jclass cls, jlong ctx, jlong image, jint z, jint c, jint t, jint level,
+        jstring ptype, jint sx, jint sy, jboolean le, jint band_rows, jint own_y0, jint own_rows) {
+    (void)cls;
+    pbx_plane_desc d;
+    fill_desc(&d, image, z, c, t, level, pixel_type(env, ptype), sx, sy, le);
+    uint64_t id = 0;
+    int st = pbx_plane_create_sparse(PBX_CTX(ctx), &d, band_rows, own_y0, own_rows, &id);
+    if (st == PBX_E_EXISTS) return 0;
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return 0;
+    }
+    return (jlong)id;
+}
+
+/* Rows of one band, copied out of the Java array in whole-row pieces (no critical section). */
+JNIEXPORT jboolean JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_writeBand(
+        JNIEnv* env, jclass cls, jlong ctx, jlong plane, jint y0, jint rows, jint row_bytes, jbyteArray data,
+        jint off) {
+    (void)cls;
+    if (!data || rows <= 0 || row_bytes <= 0 || off < 0) {
+        throw_class(env, "java/lang/IllegalArgumentException", "writeBand: bad arguments");
+        return JNI_FALSE;
+    }
+    if ((int64_t)off + (int64_t)rows * row_bytes > (int64_t)(*env)->GetArrayLength(env, data)) {
+        throw_class(env, "java/lang/IllegalArgumentException", "writeBand: array shorter than rows * rowBytes");
+        return JNI_FALSE;
+    }
+    int32_t per = (int32_t)(PIECE_BYTES / (uint32_t)row_bytes);
+    if (per < 1) per = 1;
+    if (per > rows) per = rows;
+    jbyte* buf = malloc((size_t)per * (size_t)row_bytes);
+    if (!buf) {
+        throw_class(env, "java/lang/OutOfMemoryError", "writeBand: native staging buffer");
+        return JNI_FALSE;
+    }
+    jboolean ok = JNI_TRUE;
+    for (int32_t r = 0; r < rows; r += per) {
+        const int32_t k = rows - r < per ? rows - r : per;
+        (*env)->GetByteArrayRegion(env, data, off + r * row_bytes, k * row_bytes, buf);
+        if ((*env)->ExceptionCheck(env)) {
+            ok = JNI_FALSE;
+            break;
+        }
+        int st = pbx_band_write(PBX_CTX(ctx), (uint64_t)plane, y0 + r, k, buf, (uint64_t)k * row_bytes);
+        if (st == PBX_E_EXISTS && r == 0) {  /* resident, or another caller loads it */
+            ok = JNI_FALSE;
+            break;
+        }
+        if (st != PBX_OK) {
+            throw_status(env, st);
+            ok = JNI_FALSE;
+            break;
+        }
+    }
+    free(buf);
+    return ok;
+}
+
+JNIEXPORT jint JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_bandInfo(
+        JNIEnv* env, jclass cls, jlong ctx, jlong plane, jbyteArray states) {
+    (void)cls;
+    int32_t band_rows = 0, nbands = 0;
+    int st = pbx_plane_band_info(PBX_CTX(ctx), (uint64_t)plane, &band_rows, &nbands, NULL);
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return 0;
+    }
+    if (states && nbands > 0) {
+        uint8_t* s = malloc((size_t)nbands);
+        if (!s) {
+            throw_class(env, "java/lang/OutOfMemoryError", "bandInfo");
+            return 0;
+        }
+        st = pbx_plane_band_info(PBX_CTX(ctx), (uint64_t)plane, NULL, NULL, s);
+        jsize n = (*env)->GetArrayLength(env, states);
+        if (n > nbands) n = nbands;
+        if (st == PBX_OK) (*env)->SetByteArrayRegion(env, states, 0, n, (const jbyte*)s);
+        free(s);
+        if (st != PBX_OK) throw_status(env, st);
+    }
+    return band_rows;
+}
+
+/* ---- a node: one context per GPU in this JVM, requests routed to the context holding them */
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_nodeInit(
+        JNIEnv* env, jclass cls, jint n, jintArray devices, jint png_filter, jboolean tiff_deflate, jint tiff_tile,
+        jint shard_tile) {
+    (void)cls;
+    pbx_config cfg;
+    pbx_config_default(&cfg);
+    cfg.png_filter = png_filter;
+    cfg.tiff_deflate = tiff_deflate ? 1 : 0;
+    cfg.tiff_tile = tiff_tile;
+    int32_t* devs = NULL;
+    if (devices) {
+        if ((*env)->GetArrayLength(env, devices) < n) {
+            throw_class(env, "java/lang/IllegalArgumentException", "nodeInit: fewer devices than contexts");
+            return 0;
+        }
+        devs = malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+        if (!devs) {
+            throw_class(env, "java/lang/OutOfMemoryError", "nodeInit");
+            return 0;
+        }
+        (*env)->GetIntArrayRegion(env, devices, 0, n, (jint*)devs);
+    }
+    pbx_node* node = NULL;
+    int st = pbx_node_init(&cfg, n, devs, shard_tile, &node);
+    free(devs);
+    if (st != PBX_OK) {
+        throw_status(env, st);
+        return 0;
+    }
+    return (jlong)(intptr_t)node;
+}
+
+JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_nodeShutdown(
+        JNIEnv* env, jclass cls, jlong node) {
+    (void)env; (void)cls;
+    pbx_node_shutdown((pbx_node*)(intptr_t)node);
+}
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_nodeContext(
+        JNIEnv* env, jclass cls, jlong node, jint k) {
+    (void)cls;
+    pbx_ctx* c = pbx_node_context((pbx_node*)(intptr_t)node, k);
+    if (!c) throw_class(env, "java/lang/IllegalArgumentException", "nodeContext: no such context");
+    return (jlong)(intptr_t)c;
+}
+
+/* statusOut (length >= 4): w, h, status, index of the context that served (or should load) it. */
+JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNative_nodeGetTile(
+        JNIEnv* env, jclass cls, jlong node, jlong image, jint z, jint c, jint t, jint res,
+        jint x, jint y, jint w, jint h, jstring jfmt, jintArray status_out) {
+    (void)cls;
+    if (!node) {
+        throw_class(env, "java/lang/IllegalArgumentException", "nodeGetTile: null node");
+        return NULL;
+    }
+    return tile_call(env, 0, node, image, z, c, t, res, x, y, w, h, jfmt, status_out);
 }

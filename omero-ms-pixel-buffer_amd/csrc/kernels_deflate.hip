@@ -2527,3 +2527,14 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
 }
 
 }  // namespace pbx
+
+// The timing knobs that change the OUTPUT (they skip a phase to time the rest)
+// are for variant builds only: `make OUT=lib/var_<name> EXTRA="-DPBX_TIMING_VARIANT ..."`
+// (scripts/variants.sh).  Any other build that sets one refuses to compile, so the product
+// library lib/libpbx.so can never ship corrupt PNGs (the Makefile refuses the variant flag for
+// OUT=lib).
+#if !defined(PBX_TIMING_VARIANT) && (PBX_LZ_SKIP_STORE || PBX_LZ_SKIP_FILL || PBX_LZ_SKIP_HIST || \
+    PBX_LZ_SKIP_OUT || PBX_ENC_SKIP_WRITE || PBX_ENC_SKIP_PATCH || PBX_ENC_SKIP_CRC || PBX_ENC_SKIP_STORE || \
+    defined(PBX_LZ_FAKE_LOAD))
+#error "output-changing timing knobs (PBX_LZ_SKIP_*, PBX_ENC_SKIP_*, PBX_LZ_FAKE_LOAD) need a variant build (-DPBX_TIMING_VARIANT, OUT=lib/var_*)"
+#endif

@@ -623,11 +623,14 @@ void plane_free(pbx_ctx* ctx, void* dev, size_t bytes) {
 // hold (getPixels + getPixelBuffer, :84-86).
 // pin = false: a probe (node routing) that takes no pin and leaves the LRU stamps alone.
 // kr (sparse planes): the first and last band the region covers, each pinned with the plane.
+// owns (probes): set to true when the answer is NOT_RESIDENT only because bands of rows this
+// context owns are not loaded yet (the node routes such a request to this context).
 int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*& plane, bool pin = true,
-             int32_t* kr = nullptr) {
+             int32_t* kr = nullptr, bool* owns = nullptr) {
     w = r.w;
     h = r.h;
     plane = nullptr;
+    if (owns) *owns = false;
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     auto im = ctx->images.find(r.image_id);
     // :84 getPixels — the image's Pixels row is not known here; the binding looks it up
@@ -699,10 +702,12 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*
     if (p->sparse_rows) {  // every band the rows cover must be resident
         const int32_t k0 = r.y / p->sparse_rows, k1 = (int32_t)(((int64_t)r.y + h - 1) / p->sparse_rows);
         for (int32_t k = k0; k <= k1; k++)
-            if (p->bands[(size_t)k].state != BS_READY)
+            if (p->bands[(size_t)k].state != BS_READY) {
+                if (owns) *owns = true;
                 return fail(PBX_E_NOT_RESIDENT, "rows %d..%lld: band %d (rows %d..%d) of plane z=%d c=%d t=%d level=%d "
                             "not resident", r.y, (long long)r.y + h, k, p->band_lo(k), p->band_hi(k), r.z, r.c, r.t,
                             level);
+            }
         if (kr) {
             kr[0] = k0;
             kr[1] = k1;
@@ -2886,18 +2891,23 @@ int pbx_node_route(pbx_node* node, const pbx_tile_req* req, int32_t* index) {
     const int32_t n = (int32_t)node->ctxs.size();
     const int32_t owner = n == 1 ? 0 : pbx_shard_of(req, node->tile, node->tile, n);
     if (owner < 0) return PBX_E_BADARG;
+    int32_t owning = -1;
     for (int32_t k = 0; k < n; k++) {  // the owner first, then the others in ring order
         const int32_t c = (owner + k) % n;
         int32_t w = 0, h = 0;
         Plane* p = nullptr;
-        const int st = validate(node->ctxs[(size_t)c], *req, w, h, p, false);
+        bool owns = false;
+        const int st = validate(node->ctxs[(size_t)c], *req, w, h, p, false, nullptr, &owns);
         if (st != PBX_E_NOT_RESIDENT) {
             *index = c;
             return st;
         }
+        if (owns && owning < 0) owning = c;
     }
-    *index = owner;  // nobody holds it: the binding loads it into the owner and retries
-    return fail(PBX_E_NOT_RESIDENT, "no context of the node holds the plane (owner %d)", owner);
+    // nobody holds it: the binding loads it where it belongs and retries — into the context
+    // whose sparse plane owns those rows (their bands are not loaded yet), else the shard owner
+    *index = owning >= 0 ? owning : owner;
+    return fail(PBX_E_NOT_RESIDENT, "no context of the node holds the plane (load it into context %d)", *index);
 }
 
 int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, int32_t* served_by) {

@@ -655,6 +655,7 @@ const char* pbxo_content_type(const char* format) {
 typedef struct {
     const uint8_t* plane; int pt, format; int32_t pw, ph, w, h; int first, step, tiles;
     uint64_t bytes;
+    int32_t x0, y0; int single; /* pbxo_bench_at: the one region (x0, y0, w, h) every time */
 } bench_arg;
 
 static void* bench_worker(void* p) {
@@ -668,16 +669,31 @@ static void* bench_worker(void* p) {
         int tx = i % gx, ty = (i / gx) % gy;
         size_t len = 0;
         int32_t ow, oh;
-        pbxo_get_tile(a->plane, 0, a->pt, a->pw, a->ph, tx * a->w, ty * a->h, a->w, a->h,
-                      a->format, out, cap, &len, &ow, &oh);
+        pbxo_get_tile(a->plane, 0, a->pt, a->pw, a->ph, a->single ? a->x0 : tx * a->w,
+                      a->single ? a->y0 : ty * a->h, a->w, a->h, a->format, out, cap, &len, &ow, &oh);
         a->bytes += len;
     }
     free(out);
     return NULL;
 }
 
+static double bench_run(int kind, int pt, int format, int32_t pw, int32_t ph, int single, int32_t x0,
+                        int32_t y0, int32_t w, int32_t h, int tiles, int threads, uint64_t* out_bytes);
+
 double pbxo_bench(int kind, int pt, int format, int32_t pw, int32_t ph, int32_t w, int32_t h,
                   int tiles, int threads, uint64_t* out_bytes) {
+    return bench_run(kind, pt, format, pw, ph, 0, 0, 0, w, h, tiles, threads, out_bytes);
+}
+
+/* BASELINE configs[0]: ONE request (x0, y0, w, h) of a pw x ph plane, `reps` times over
+ * `threads` threads (TileRequestHandler.getTile repeated by the Vert.x worker pool). */
+double pbxo_bench_at(int kind, int pt, int format, int32_t pw, int32_t ph, int32_t x0, int32_t y0,
+                     int32_t w, int32_t h, int reps, int threads, uint64_t* out_bytes) {
+    return bench_run(kind, pt, format, pw, ph, 1, x0, y0, w, h, reps, threads, out_bytes);
+}
+
+static double bench_run(int kind, int pt, int format, int32_t pw, int32_t ph, int single, int32_t x0,
+                        int32_t y0, int32_t w, int32_t h, int tiles, int threads, uint64_t* out_bytes) {
     int bpp = pbxo_bpp(pt);
     uint8_t* plane = (uint8_t*)malloc((size_t)pw * ph * bpp);
     pbxo_gen_region(kind, 0, 0, 0, 0, 0, pt, 0, 0, pw, ph, 0, plane); /* little-endian plane */
@@ -687,7 +703,7 @@ double pbxo_bench(int kind, int pt, int format, int32_t pw, int32_t ph, int32_t 
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
-        bench_arg a = {plane, pt, format, pw, ph, w, h, i, threads, tiles, 0};
+        bench_arg a = {plane, pt, format, pw, ph, w, h, i, threads, tiles, 0, x0, y0, single};
         args[i] = a;
         pthread_create(&th[i], NULL, bench_worker, &args[i]);
     }

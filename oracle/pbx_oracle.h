@@ -114,6 +114,9 @@ const char* pbxo_content_type(const char* format);
  * plane_w x plane_h.  Returns wall seconds; *out_bytes receives the total output bytes. */
 double pbxo_bench(int kind, int pixel_type, int format, int32_t plane_w, int32_t plane_h,
                   int32_t w, int32_t h, int tiles, int threads, uint64_t* out_bytes);
+/* One request (x0, y0, w, h) of the plane `reps` times (BASELINE configs[0]). */
+double pbxo_bench_at(int kind, int pt, int format, int32_t pw, int32_t ph, int32_t x0, int32_t y0,
+                     int32_t w, int32_t h, int reps, int threads, uint64_t* out_bytes);
 
 /* Zarr v2 chunk decode (oracle/zarr_oracle.c).  Codecs = include/pbx.h
  * enum pbx_zarr_codec. */

@@ -50,15 +50,35 @@ for k, cs in sorted(vals.items()):
 # SQ_WAIT_ANY (parked at s_waitcnt / barrier), SQ_WAIT_INST_ANY (issue stalls) and
 # SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES.
 CUS, SIMDS = 256, 1024
+# GRBM_GUI_ACTIVE counts the GPU's busy cycles over the whole counter-collection window of a
+# dispatch, which for a short dispatch is much longer than the kernel itself (r03 reported
+# 6-14 GHz for sub-10 us kernels).  The clock is therefore taken from dispatches of >= 100 us
+# only (their median); shorter dispatches use that clock and are flagged.
+LONG_NS = 100_000
+long_clk = []
+for k, cs in vals.items():
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    if m.get("GRBM_GUI_ACTIVE") and m.get("_dur", 0) >= LONG_NS:
+        c = m["GRBM_GUI_ACTIVE"] / 8 / (m["_dur"] / 1e9)
+        if 0.5e9 < c < 2.6e9:  # MI355X engine clock <= 2.4 GHz
+            long_clk.append(c)
+long_clk.sort()
+ref_clk = long_clk[len(long_clk) // 2] if long_clk else 2.1e9
 issue = {}
 for k, cs in sorted(vals.items()):
     m = {c: sum(v) / len(v) for c, v in cs.items()}
     if "SQ_INSTS_VALU" not in m or not m.get("_dur"):
         continue
     dur_s = m["_dur"] / 1e9
-    clk = m["GRBM_GUI_ACTIVE"] / 8 / dur_s if m.get("GRBM_GUI_ACTIVE") else 2.1e9
+    short = m["_dur"] < LONG_NS
+    clk = ref_clk
+    if not short and m.get("GRBM_GUI_ACTIVE"):
+        c = m["GRBM_GUI_ACTIVE"] / 8 / dur_s
+        clk = c if 0.5e9 < c < 2.6e9 else ref_clk
     cyc = dur_s * clk
     e = {"duration_ms": round(m["_dur"] / 1e6, 4), "clock_ghz": round(clk / 1e9, 3),
+         "clock_source": "reference (dispatch < 100 us: issue fractions indicative only)" if short
+         else "GRBM_GUI_ACTIVE / 8 / duration",
          "valu_busy": round(2 * m["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
          "salu_busy": round(m.get("SQ_INSTS_SALU", 0) / (CUS * cyc), 4),
          "lds_inst_per_cu_cycle": round(m.get("SQ_INSTS_LDS", 0) / (CUS * cyc), 4)}
@@ -92,5 +112,6 @@ if traffic_out:
     issue_name = os.path.basename(traffic_out).replace("traffic", "issue")
     with open(os.path.join(os.path.dirname(traffic_out) or ".", issue_name), "w") as fo:
         json.dump({"rule": "valu_busy = 2 x SQ_INSTS_VALU / (1024 SIMDs x cycles); salu_busy = "
-                           "SQ_INSTS_SALU / (256 CUs x cycles); cycles = duration x GRBM_GUI_ACTIVE/8/duration",
+                           "SQ_INSTS_SALU / (256 CUs x cycles); cycles = duration x GRBM_GUI_ACTIVE/8/duration "
+                           "for dispatches >= 100 us, else x the median clock of those",
                    "kernels": issue}, fo, indent=1)

@@ -79,6 +79,10 @@ def lib():
         L.pbxo_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int32,
                                  ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                                  ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        L.pbxo_bench_at.restype = ctypes.c_double
+        L.pbxo_bench_at.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         _lib = L
     return _lib
 
@@ -212,6 +216,12 @@ def content_type(fmt):
 def bench(kind, pt, fmt, pw, ph, w, h, tiles, threads):
     nb = ctypes.c_uint64()
     sec = lib().pbxo_bench(kind, pt, fmt, pw, ph, w, h, tiles, threads, ctypes.byref(nb))
+    return sec, nb.value
+
+
+def bench_at(kind, pt, fmt, pw, ph, x, y, w, h, reps, threads):
+    nb = ctypes.c_uint64()
+    sec = lib().pbxo_bench_at(kind, pt, fmt, pw, ph, x, y, w, h, reps, threads, ctypes.byref(nb))
     return sec, nb.value
 
 

@@ -98,3 +98,42 @@ void pbx_results_release(pbx_ctx* ctx, pbx_result* r, uint64_t n) {
         fake.releases_results++;
     }
 }
+
+int pbx_plane_create_sparse(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t band_rows, int32_t own_y0,
+                            int32_t own_rows, uint64_t* id) {
+    (void)ctx;
+    fake.creates++;
+    fake.last_desc = *d;
+    fake.sparse_band_rows = band_rows;
+    fake.sparse_own_y0 = own_y0;
+    fake.sparse_own_rows = own_rows;
+    if (fake.create_rc) return fake.create_rc;
+    *id = 88;
+    return 0;
+}
+int pbx_band_write(pbx_ctx* ctx, uint64_t id, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
+    if (fake.band_exists) return PBX_E_EXISTS;
+    return pbx_plane_write_rows(ctx, id, y0, rows, data, bytes);
+}
+int pbx_plane_band_info(pbx_ctx* ctx, uint64_t id, int32_t* band_rows, int32_t* nbands, uint8_t* states) {
+    (void)ctx; (void)id;
+    if (band_rows) *band_rows = fake.sparse_band_rows;
+    if (nbands) *nbands = fake.nbands;
+    if (states)
+        for (int32_t k = 0; k < fake.nbands; k++) states[k] = (uint8_t)(k % 3);
+    return 0;
+}
+int pbx_node_init(const pbx_config* cfg, int32_t n, const int32_t* devices, int32_t shard_tile, pbx_node** out) {
+    (void)cfg; (void)shard_tile;
+    fake.node_n = n;
+    fake.node_dev0 = devices ? devices[0] : -1;
+    *out = (pbx_node*)0x2000;
+    return fake.init_rc;
+}
+void pbx_node_shutdown(pbx_node* node) { (void)node; }
+pbx_ctx* pbx_node_context(pbx_node* node, int32_t k) { (void)node; return k < fake.node_n ? (pbx_ctx*)0x1000 : NULL; }
+int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, int32_t* served_by) {
+    (void)node;
+    if (served_by) *served_by = fake.served_by;
+    return pbx_get_tile(NULL, req, out);
+}

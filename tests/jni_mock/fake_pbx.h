@@ -21,6 +21,9 @@ struct fake_state {
     const uint8_t* body;
     uint64_t body_len;
     int releases_results, bad_release;
+    /* sparse planes and the node router */
+    int32_t sparse_band_rows, sparse_own_y0, sparse_own_rows, band_exists, nbands;
+    int node_n, node_dev0, served_by;
 };
 extern struct fake_state fake;
 #endif

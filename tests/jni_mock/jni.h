@@ -41,6 +41,7 @@ struct JNINativeInterface_ {
     jlongArray (*NewLongArray)(JNIEnv*, jsize);
     void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
     void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*);
+    void (*GetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, jint*);
     void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
     jlong (*GetDirectBufferCapacity)(JNIEnv*, jobject);
 };

@@ -20,6 +20,14 @@ jlong J(registerZarr)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jst
                       jint, jbyteArray, jlongArray, jlong);
 jbyteArray J(getTile)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jint, jint, jint, jint, jstring, jintArray);
 void J(declareImage)(JNIEnv*, jclass, jlong, jlong, jstring, jint, jint, jint, jint, jint, jint);
+jlong J(createSparsePlane)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jstring, jint, jint, jboolean, jint,
+                           jint, jint);
+jboolean J(writeBand)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jbyteArray, jint);
+jint J(bandInfo)(JNIEnv*, jclass, jlong, jlong, jbyteArray);
+jlong J(nodeInit)(JNIEnv*, jclass, jint, jintArray, jint, jboolean, jint, jint);
+jlong J(nodeContext)(JNIEnv*, jclass, jlong, jint);
+jbyteArray J(nodeGetTile)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jint, jint, jint, jint, jint, jstring,
+                          jintArray);
 
 static void reset(void) {
     memset(&fake, 0, sizeof fake);
@@ -174,6 +182,60 @@ int main(void) {
         reset();
         CHECK(J(registerZarr)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 128, 128, 0, 64, 64, 1, &chunks, &offs, 0) == 0);
         CHECK(threw("java/lang/IllegalArgumentException") && fake.zarr_calls == 0);
+    }
+    /* ---- sparse planes: createSparsePlane's arguments, writeBand's pieces and its 409 */
+    {
+        reset();
+        CHECK(J(createSparsePlane)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 100000, 100000, 0, 512, 1024, 2048) == 88);
+        CHECK(!pending[0] && fake.sparse_band_rows == 512 && fake.sparse_own_y0 == 1024 && fake.sparse_own_rows == 2048);
+        reset();
+        fake.create_rc = PBX_E_EXISTS;
+        CHECK(J(createSparsePlane)(env, NULL, 1, 9, 0, 0, 0, 0, &u16, 100, 100, 0, 64, 0, 0) == 0 && !pending[0]);
+        const jint row = 100000 * 2, rows = 512;  /* a 102 MB band: 7 pieces of <= 16 MiB */
+        struct mock_obj a = arr(1, (size_t)row * rows, 1);
+        reset();
+        CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows, row, &a, 0) == 1 && !pending[0]);
+        int32_t y = 1024;
+        for (int i = 0; i < fake.nwrites; i++) {
+            CHECK(fake.w_y0[i] == y && fake.w_bytes[i] <= (16u << 20));
+            y += fake.w_rows[i];
+        }
+        CHECK(y == 1024 + rows && fake.nwrites == 7);
+        reset();
+        fake.band_exists = 1;  /* resident / being loaded: false, no exception */
+        CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows, row, &a, 0) == 0 && !pending[0]);
+        reset();
+        CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows + 1, row, &a, 0) == 0 &&
+              threw("java/lang/IllegalArgumentException"));
+        free(a.data);
+        reset();
+        fake.sparse_band_rows = 512;
+        fake.nbands = 5;
+        struct mock_obj st = arr(1, 5, 1);
+        CHECK(J(bandInfo)(env, NULL, 1, 88, &st) == 512);
+        CHECK(((uint8_t*)st.data)[4] == 1 && ((uint8_t*)st.data)[2] == 2);
+    }
+    /* ---- the node: devices passed through, the serving context reported in statusOut[3] */
+    {
+        reset();
+        struct mock_obj devs = arr(3, 2, 4);
+        ((jint*)devs.data)[0] = 3;
+        ((jint*)devs.data)[1] = 3;
+        jlong node = J(nodeInit)(env, NULL, 2, &devs, 0, 0, 0, 512);
+        CHECK(node != 0 && !pending[0] && fake.node_n == 2 && fake.node_dev0 == 3);
+        CHECK(J(nodeContext)(env, NULL, node, 1) != 0 && !pending[0]);
+        CHECK(J(nodeContext)(env, NULL, node, 2) == 0 && threw("java/lang/IllegalArgumentException"));
+        reset();
+        static const uint8_t body[3] = {7, 8, 9};
+        fake.tile_fill = 1;
+        fake.body = body;
+        fake.body_len = 3;
+        fake.served_by = 1;
+        fake.node_n = 2;
+        struct mock_obj so = arr(3, 4, 4);
+        jbyteArray r = J(nodeGetTile)(env, NULL, node, 9, 0, 0, 0, -1, 0, 0, 8, 8, NULL, &so);
+        CHECK(r && r->len == 3 && ((jint*)so.data)[2] == 0 && ((jint*)so.data)[3] == 1);
+        CHECK(fake.releases_results == 1 && fake.bad_release == 0);
     }
     if (failures) {
         fprintf(stderr, "%d failures\n", failures);

@@ -90,6 +90,10 @@ static void m_SetIntArrayRegion(JNIEnv* e, jintArray a, jsize s, jsize n, const 
     (void)e;
     memcpy((jint*)a->data + s, b, 4 * (size_t)n);
 }
+static void m_GetIntArrayRegion(JNIEnv* e, jintArray a, jsize s, jsize n, jint* b) {
+    (void)e;
+    memcpy(b, (jint*)a->data + s, 4 * (size_t)n);
+}
 static void* m_GetDirectBufferAddress(JNIEnv* e, jobject b) { (void)e; return b && b->kind == 4 ? b->data : NULL; }
 static jlong m_GetDirectBufferCapacity(JNIEnv* e, jobject b) { (void)e; return b && b->kind == 4 ? (jlong)b->len : -1; }
 
@@ -97,7 +101,7 @@ static const struct JNINativeInterface_ table = {
     m_FindClass, m_ThrowNew, m_ExceptionCheck, m_GetStringUTFChars, m_ReleaseStringUTFChars,
     m_GetArrayLength, m_GetByteArrayRegion, m_SetByteArrayRegion, m_NewByteArray,
     m_GetByteArrayElements, m_ReleaseByteArrayElements, m_GetLongArrayElements,
-    m_ReleaseLongArrayElements, m_NewLongArray, m_SetLongArrayRegion, m_SetIntArrayRegion,
+    m_ReleaseLongArrayElements, m_NewLongArray, m_SetLongArrayRegion, m_SetIntArrayRegion, m_GetIntArrayRegion,
     m_GetDirectBufferAddress, m_GetDirectBufferCapacity};
 static JNIEnv envp = &table;
 static JNIEnv* env = &envp;

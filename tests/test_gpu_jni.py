@@ -33,16 +33,17 @@ def test_jni_shim_on_real_library(tmp_path, oracle):
                          timeout=240)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "jni real ok" in out.stdout
-    tiles = {}
+    tiles, served_by = {}, {}
     for line in out.stdout.splitlines():
         if line.startswith("TILE "):
-            _, name, st, n, w, h = line.split()
+            _, name, st, n, w, h, served = line.split()
             body = None
             path = tmp_path / (name + ".bin")
             if path.exists():
                 body = path.read_bytes()
                 assert len(body) == int(n)
             tiles[name] = (int(st), body, int(w), int(h))
+            served_by[name] = int(served)
     assert "BANDS 33" in out.stdout  # 64 MiB bands of 1016 rows
 
     def want(x, y, w, h):
@@ -83,3 +84,13 @@ def test_jni_shim_on_real_library(tmp_path, oracle):
     st, body, _, _ = tiles["after_failure"]
     r, px, _ = oracle.png_decode(body)
     assert st == 0 and r == 0 and px == want(512, 512, 512, 512)
+    # the node: misses name the context owning the rows, the bands loaded there serve them
+    assert tiles["node_a_miss"][0] == 460 and served_by["node_a_miss"] == 0
+    assert tiles["node_b_miss"][0] == 460 and served_by["node_b_miss"] == 1
+    assert tiles["node_c_miss"][0] == 460  # straddles the two owners' rows: nobody serves it
+    st, body, _, _ = tiles["node_a"]
+    assert st == 0 and served_by["node_a"] == 0 and body == want(512, 1000, 512, 512)
+    st, body, _, _ = tiles["node_b"]
+    r, px, _ = oracle.png_decode(body)
+    assert st == 0 and served_by["node_b"] == 1 and r == 0 and px == want(2048, 6000, 512, 512)
+    assert "BANDS1 00000220" in out.stdout  # context 1 holds bands 5 and 6 of the slide only
