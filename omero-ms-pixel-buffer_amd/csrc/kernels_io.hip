@@ -538,7 +538,7 @@ __device__ __forceinline__ uint32_t sub8(uint32_t a, uint32_t b) {  // bytewise 
     return ((a | 0x80808080u) - (b & 0x7F7F7F7Fu)) ^ ((a ^ ~b) & 0x80808080u);
 }
 __device__ __forceinline__ uint32_t avg8(uint32_t a, uint32_t b) {  // bytewise floor((a + b) / 2)
-    return (a & b) + (((a ^ b) >> 1) & 0x7F7F7F7Fu);
+    return __builtin_amdgcn_lerp(a, b, 0u);  // v_lerp_u8: (a + b + round bit 0) >> 1 per byte
 }
 typedef short f2_s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2_s16x2 f2_abs(f2_s16x2 x) {

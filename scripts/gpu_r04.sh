@@ -1,0 +1,56 @@
+# Round-4 GPU recipe (one gpurun call): bash scripts/gpu_r04.sh TAG STAGE...
+#   tests    the round's new -m gpu tests (serving, sparse planes, JNI on the real library, residency)
+#   gputest  the whole -m gpu suite + smoke
+#   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
+#   pmcf     PMC passes of k_filter3 (Sub, Paeth, adaptive): issue + traffic
+#   pmc      PMC passes of the headline deflate chain (scripts/pmc_run.sh, filter passes off)
+#   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
+# Every GPU step has its own time limit; the first failure ends the call.
+set -o pipefail
+TAG=$1; shift
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$TAG
+mkdir -p $O
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+for stage in "$@"; do
+  echo "== stage $stage $(date +%T)"
+  case $stage in
+    tests)
+      timeout -k 10 900 $PYT tests/test_gpu_serving.py tests/test_gpu_sparse.py tests/test_gpu_jni.py \
+        tests/test_gpu_residency.py > $O/pytest_new.log 2>&1 || { tail -60 $O/pytest_new.log; exit 1; }
+      tail -3 $O/pytest_new.log ;;
+    gputest)
+      timeout -k 10 1000 $PYT -m gpu tests > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|ERROR|Error" $O/pytest_gpu.log | head -30; tail -30 $O/pytest_gpu.log; exit 1; }
+      tail -3 $O/pytest_gpu.log
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    probe)
+      timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch.log 2>&1 || { tail -30 $O/subbatch.log; exit 1; }
+      cat $O/subbatch.log | tail -6
+      timeout -k 10 300 python -u scripts/filter_bench.py 1 2 3 4 5 > $O/filter.log 2>&1 || { tail -30 $O/filter.log; exit 1; }
+      cat $O/filter.log ;;
+    pmcf)
+      for f in 1 4 5; do
+        P=$O/pmcf$f
+        mkdir -p $P
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT -d $P/pmc1 -o run --output-format csv -- python3 scripts/filter_bench.py $f > $P/p1.log 2>&1 || { tail -20 $P/p1.log; exit 1; }
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE -d $P/pmc2 -o run --output-format csv -- python3 scripts/filter_bench.py $f > $P/p2.log 2>&1 || { tail -20 $P/p2.log; exit 1; }
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $P/pmc3 -o run --output-format csv -- python3 scripts/filter_bench.py $f > $P/p3.log 2>&1 || { tail -20 $P/p3.log; exit 1; }
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $P/pmc4 -o run --output-format csv -- python3 scripts/filter_bench.py $f > $P/p4.log 2>&1 || { tail -20 $P/p4.log; exit 1; }
+        python3 scripts/pmc_summary.py $P $P/traffic.json > $P/summary.txt 2>&1 || true
+        grep -A 14 '"k_filter3' $P/summary.txt | head -32
+      done ;;
+    pmc)
+      PMC_FILTER=0 bash scripts/pmc_run.sh > $O/pmc_run.log 2>&1 || { tail -30 $O/pmc_run.log; exit 1; }
+      python3 scripts/pmc_summary.py gpurun_out $O/traffic.json > $O/pmc_summary.txt 2>&1 || true
+      tail -60 $O/pmc_summary.txt ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['deflate_chain_ms'], d['roofline']['frac'])"
+      PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err || { tail -20 $O/prof_bench.err; exit 1; }
+      find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \; ;;
+    *) echo "unknown stage $stage"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
