@@ -537,6 +537,10 @@ constexpr uint32_t F2_MAX_RB = 2048;
 __device__ __forceinline__ uint32_t sub8(uint32_t a, uint32_t b) {  // bytewise a - b mod 256
     return ((a | 0x80808080u) - (b & 0x7F7F7F7Fu)) ^ ((a ^ ~b) & 0x80808080u);
 }
+// (a - b) ^ 0x80 per byte: the residual biased by 128 (sub8's last xor folded into its mask)
+__device__ __forceinline__ uint32_t sub8m(uint32_t a, uint32_t b) {
+    return ((a | 0x80808080u) - (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+}
 __device__ __forceinline__ uint32_t avg8(uint32_t a, uint32_t b) {  // bytewise floor((a + b) / 2)
     return __builtin_amdgcn_lerp(a, b, 0u);  // v_lerp_u8: (a + b + round bit 0) >> 1 per byte
 }
@@ -863,7 +867,9 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
         uint4 f[G];
         uint32_t ft = fixed;
         if (ADAPTIVE) {
-            // every candidate ([0] Sub, [1] Up, [2] Avg, [3] Paeth) and its sum of |residual|
+            // every candidate ([0] Sub, [1] Up, [2] Avg, [3] Paeth) as residual ^ 0x80 per byte
+            // (the biased form v_sad_u8 sums |signed residual| from, at the cost of the plain
+            // residual: sub8m) and its sum of |residual|
             uint32_t fw[G][4][4];
             uint32_t sm[5] = {0, 0, 0, 0, 0};
             constexpr uint32_t M = 0x80808080u;
@@ -876,17 +882,17 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
                 const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++) {
-                    fw[g][0][j] = sub8(x[j], l[j]);
-                    fw[g][1][j] = sub8(x[j], u[j]);
-                    fw[g][2][j] = sub8(x[j], avg8(l[j], u[j]));
-                    fw[g][3][j] = sub8(x[j], paeth4(l[j], u[j], lu[j]));
+                    fw[g][0][j] = sub8m(x[j], l[j]);
+                    fw[g][1][j] = sub8m(x[j], u[j]);
+                    fw[g][2][j] = sub8m(x[j], avg8(l[j], u[j]));
+                    fw[g][3][j] = sub8m(x[j], paeth4(l[j], u[j], lu[j]));
                 }
                 if (64 * g + lane < nc) {
 #pragma unroll
                     for (uint32_t j = 0; j < 4; j++) {
                         sm[0] = __builtin_amdgcn_sad_u8(x[j] ^ M, M, sm[0]);
 #pragma unroll
-                        for (uint32_t k = 0; k < 4; k++) sm[k + 1] = __builtin_amdgcn_sad_u8(fw[g][k][j] ^ M, M, sm[k + 1]);
+                        for (uint32_t k = 0; k < 4; k++) sm[k + 1] = __builtin_amdgcn_sad_u8(fw[g][k][j], M, sm[k + 1]);
                     }
                 }
             }
@@ -896,18 +902,19 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
                 const uint32_t v = f3_wave_sum(sm[k]);
                 if (v < bs) { bs = v; best = k; }
             }
-            ft = best;
+            ft = __builtin_amdgcn_readfirstlane(best);  // uniform: the choice is a scalar branch
+            // masks in SGPRs (ft is uniform); per word one v_and + four v_and_or
+            const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
+            const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+            const uint32_t m0 = ~(m1 | m2 | m3 | m4), mx = ft ? M : 0u;
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
-                const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
-                const uint32_t m0 = ~(m1 | m2 | m3 | m4);
                 uint32_t o[4];
                 const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++)
-                    o[j] = (x[j] & m0) | (fw[g][0][j] & m1) | (fw[g][1][j] & m2) | (fw[g][2][j] & m3) |
-                           (fw[g][3][j] & m4);
+                    o[j] = ((x[j] & m0) | (fw[g][0][j] & m1) | (fw[g][1][j] & m2) | (fw[g][2][j] & m3) |
+                            (fw[g][3][j] & m4)) ^ mx;
                 f[g] = make_uint4(o[0], o[1], o[2], o[3]);
             }
         } else {
