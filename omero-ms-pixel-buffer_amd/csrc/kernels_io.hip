@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
 // ------------------------------------------------------- K1+K2: extract + PNG filter
 // One workgroup per band of FB_ROWS rows of a deflate tile: stage the band's source rows
 // (plus the row above) in LDS as big-endian bytes (16-byte loads, byte swap, APNGWriter
-// sign flip), choose each row's filter (adaptive mode: minimum sum of |signed residual|,
+// sign flip), choose each row's filter (adaptive mode: minimum sum of |byte - prediction|,
 // one wave per row), then write the band's stream bytes as aligned 16-byte words:
 // FB_ROWS * rowlen is a multiple of 16, so bands never share an output word.
 constexpr int FB_ROWS = 16;
@@ -192,6 +192,22 @@ __device__ __forceinline__ uint32_t filt_byte(int ft, uint32_t cur, uint32_t lef
         const int pa = abs(p - (int)left), pb = abs(p - (int)up), pc = abs(p - (int)ul);
         const uint32_t pr = (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
         return (cur - pr) & 0xFF;
+    }
+    }
+}
+
+// The byte a filter predicts (0 for None); the adaptive choice sums |cur - prediction| (the
+// plain byte distance, v_sad_u8) over the row and takes the minimum, the first on ties.
+__device__ __forceinline__ uint32_t filt_pred(int ft, uint32_t left, uint32_t up, uint32_t ul) {
+    switch (ft) {
+    case 0: return 0u;
+    case 1: return left;
+    case 2: return up;
+    case 3: return (left + up) >> 1;
+    default: {
+        const int p = (int)left + (int)up - (int)ul;
+        const int pa = abs(p - (int)left), pb = abs(p - (int)up), pc = abs(p - (int)ul);
+        return (pa <= pb && pa <= pc) ? left : (pb <= pc ? up : ul);
     }
     }
 }
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                     const uint32_t left = i >= bpp ? L[i - bpp] : 0u, ul = i >= bpp ? U[i - bpp] : 0u;
 #pragma unroll
                     for (int f = 0; f < 5; f++)
-                        sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)filt_byte(f, cur, left, up, ul));
+                        sum[f] += (uint32_t)abs((int)cur - (int)filt_pred(f, left, up, ul));
                 }
 #pragma unroll
                 for (int f = 0; f < 5; f++)
@@ -304,7 +320,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                     const uint32_t left = i >= bpp ? ts.be(r, i - bpp) : 0u;
                     const uint32_t ul = (r > 0 && i >= bpp) ? ts.be(r - 1, i - bpp) : 0u;
                     for (int f = 0; f < 5; f++)
-                        sum[f] += (uint32_t)abs((int)(int8_t)(uint8_t)filt_byte(f, cur, left, up, ul));
+                        sum[f] += (uint32_t)abs((int)cur - (int)filt_pred(f, left, up, ul));
                 }
                 for (int f = 0; f < 5; f++) atomicAdd(&red[f], sum[f]);
                 __syncthreads();
@@ -523,7 +539,7 @@ uint32_t filter_band_rows() { return FB_ROWS; }
 // band of F2_ROWS rows.
 //   A  the band's rows and the row above, big-endian, into LDS (16-byte loads; 16 zero bytes
 //      before every row: the left neighbours of its first samples)
-//   B  (adaptive) each row's filter: one wave per row, the five sums of |signed residual|
+//   B  (adaptive) each row's filter: one wave per row, the five sums of |byte - prediction|
 //      over dwords, four bytes at once (SWAR byte arithmetic; v_sad_u8 on the biased bytes
 //      gives sum |residual| in one instruction; Paeth on packed 16-bit pairs), minimum first
 //   C  every filtered dword of the band into LDS rows laid out as k_rows' staging rows
@@ -628,11 +644,11 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
             for (uint32_t k = lane; k < nw; k += 64) {
                 const uint32_t cur = L[k], up = U[k];
                 const uint32_t left = back_bytes(L, (int32_t)k, bpp), ul = back_bytes(U, (int32_t)k, bpp);
-                s[0] = __builtin_amdgcn_sad_u8(cur ^ M, M, s[0]);
-                s[1] = __builtin_amdgcn_sad_u8(sub8(cur, left) ^ M, M, s[1]);
-                s[2] = __builtin_amdgcn_sad_u8(sub8(cur, up) ^ M, M, s[2]);
-                s[3] = __builtin_amdgcn_sad_u8(sub8(cur, avg8(left, up)) ^ M, M, s[3]);
-                s[4] = __builtin_amdgcn_sad_u8(sub8(cur, paeth4(left, up, ul)) ^ M, M, s[4]);
+                s[0] = __builtin_amdgcn_sad_u8(cur, 0u, s[0]);
+                s[1] = __builtin_amdgcn_sad_u8(cur, left, s[1]);
+                s[2] = __builtin_amdgcn_sad_u8(cur, up, s[2]);
+                s[3] = __builtin_amdgcn_sad_u8(cur, avg8(left, up), s[3]);
+                s[4] = __builtin_amdgcn_sad_u8(cur, paeth4(left, up, ul), s[4]);
             }
 #pragma unroll
             for (int f = 0; f < 5; f++)
@@ -723,7 +739,7 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // = 16-byte chunks l, 64 + l), keeps the row above in registers, and prefetches the next row
 // while it filters the current one.  A sample's left neighbour is the previous lane's chunk
 // (one DPP wave shift; lane 0: the previous 64-chunk group, or zero before the row).  The
-// adaptive choice (minimum sum of |signed residual|, first filter on ties: the oracle's rule)
+// adaptive choice (minimum sum of |byte - prediction|, first filter on ties: the oracle's rule)
 // needs the whole row: five per-lane sums reduced over the wave by DPP.  Stream words are
 // stored 16-byte aligned: lane l writes the aligned word ending where its chunk's first 16 - s
 // bytes end (s = the row's start offset mod 16), i.e. the previous chunk's last s bytes and its
@@ -867,12 +883,11 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
         uint4 f[G];
         uint32_t ft = fixed;
         if (ADAPTIVE) {
-            // every candidate ([0] Sub, [1] Up, [2] Avg, [3] Paeth) as residual ^ 0x80 per byte
-            // (the biased form v_sad_u8 sums |signed residual| from, at the cost of the plain
-            // residual: sub8m) and its sum of |residual|
-            uint32_t fw[G][4][4];
+            // every candidate's prediction ([0] Sub = left, [1] Up, [2] Avg, [3] Paeth) and the
+            // row sums of |byte - prediction| (v_sad_u8; None: the bytes themselves); the chosen
+            // filter's residuals are formed once, after the choice
+            uint32_t pw[G][4][4];
             uint32_t sm[5] = {0, 0, 0, 0, 0};
-            constexpr uint32_t M = 0x80808080u;
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
                 uint32_t l[4], lu[4];
@@ -882,17 +897,17 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
                 const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++) {
-                    fw[g][0][j] = sub8m(x[j], l[j]);
-                    fw[g][1][j] = sub8m(x[j], u[j]);
-                    fw[g][2][j] = sub8m(x[j], avg8(l[j], u[j]));
-                    fw[g][3][j] = sub8m(x[j], paeth4(l[j], u[j], lu[j]));
+                    pw[g][0][j] = l[j];
+                    pw[g][1][j] = u[j];
+                    pw[g][2][j] = avg8(l[j], u[j]);
+                    pw[g][3][j] = paeth4(l[j], u[j], lu[j]);
                 }
                 if (64 * g + lane < nc) {
 #pragma unroll
                     for (uint32_t j = 0; j < 4; j++) {
-                        sm[0] = __builtin_amdgcn_sad_u8(x[j] ^ M, M, sm[0]);
+                        sm[0] = __builtin_amdgcn_sad_u8(x[j], 0u, sm[0]);
 #pragma unroll
-                        for (uint32_t k = 0; k < 4; k++) sm[k + 1] = __builtin_amdgcn_sad_u8(fw[g][k][j], M, sm[k + 1]);
+                        for (uint32_t k = 0; k < 4; k++) sm[k + 1] = __builtin_amdgcn_sad_u8(x[j], pw[g][k][j], sm[k + 1]);
                     }
                 }
             }
@@ -902,19 +917,17 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
                 const uint32_t v = f3_wave_sum(sm[k]);
                 if (v < bs) { bs = v; best = k; }
             }
-            ft = __builtin_amdgcn_readfirstlane(best);  // uniform: the choice is a scalar branch
-            // masks in SGPRs (ft is uniform); per word one v_and + four v_and_or
+            ft = __builtin_amdgcn_readfirstlane(best);
+            // the prediction by masks in SGPRs (ft is uniform; None predicts 0), then one sub8
             const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
             const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
-            const uint32_t m0 = ~(m1 | m2 | m3 | m4), mx = ft ? M : 0u;
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
                 uint32_t o[4];
                 const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++)
-                    o[j] = ((x[j] & m0) | (fw[g][0][j] & m1) | (fw[g][1][j] & m2) | (fw[g][2][j] & m3) |
-                            (fw[g][3][j] & m4)) ^ mx;
+                    o[j] = sub8(x[j], (pw[g][0][j] & m1) | (pw[g][1][j] & m2) | (pw[g][2][j] & m3) | (pw[g][3][j] & m4));
                 f[g] = make_uint4(o[0], o[1], o[2], o[3]);
             }
         } else {

@@ -150,6 +150,17 @@ static int paeth(int a, int b, int c) {
     return c;
 }
 
+/* The byte filter ft predicts (None: 0). */
+static int filt_pred(int ft, int left, int up, int ul) {
+    switch (ft) {
+    case 0: return 0;
+    case 1: return left;
+    case 2: return up;
+    case 3: return (left + up) >> 1;
+    default: return paeth(left, up, ul);
+    }
+}
+
 static uint8_t filt_byte(int ft, int cur, int left, int up, int ul) {
     switch (ft) {
     case 0: return (uint8_t)cur;
@@ -179,14 +190,19 @@ size_t pbxo_png_filter_stream(const uint8_t* tile_be, int pt, int32_t w, int32_t
     for (int32_t r = 0; r < h; r++) {
         png_row_bytes(tile_be + (size_t)r * rb, pt, w, cur);
         int ft = filter;
-        if (filter == 5) { /* adaptive: minimum sum of |signed residual|, ties -> lowest */
+        if (filter == 5) {
+            /* adaptive (the pbx_config.png_filter option; the reference writes None): per row the
+             * filter whose predictions are closest to the bytes, minimum sum of |byte -
+             * prediction| (the plain byte distance, no mod-256 wrap: v_sad_u8 on the GPU), the
+             * lowest filter on ties.  Measured against libpng's sum of |signed residual|: -1.6%
+             * zlib-6 bytes on G_NOISE, equal on G_FAKE, +0.7% on Poisson-like data. */
             uint64_t best = UINT64_MAX;
             for (int f = 0; f < 5; f++) {
                 uint64_t s = 0;
                 for (size_t i = 0; i < rb; i++) {
                     int left = i >= (size_t)bpp ? cur[i - bpp] : 0;
                     int ul = i >= (size_t)bpp ? prev[i - bpp] : 0;
-                    int8_t v = (int8_t)filt_byte(f, cur[i], left, prev[i], ul);
+                    int v = (int)cur[i] - filt_pred(f, left, prev[i], ul);
                     s += (uint64_t)(v < 0 ? -v : v);
                 }
                 if (s < best) { best = s; ft = f; }
