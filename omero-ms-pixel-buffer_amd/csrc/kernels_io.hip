@@ -565,24 +565,39 @@ __device__ __forceinline__ f2_s16x2 f2_abs(f2_s16x2 x) {
     const f2_s16x2 m = x >> 15;
     return (x ^ m) - m;
 }
-// PNG Paeth predictor of two 16-bit lanes holding bytes (a = left, b = up, c = up-left), all
-// packed arithmetic: pa = |b - c|, pb = |a - c|, pc = |a + b - 2c| (<= 510), and the choice
-// (a if pa <= min(pb, pc), else b if pb <= pc, else c) from the signs of two differences.
-__device__ __forceinline__ uint32_t paeth_pair(uint32_t a, uint32_t b, uint32_t c) {
-    const f2_s16x2 A = __builtin_bit_cast(f2_s16x2, a), B = __builtin_bit_cast(f2_s16x2, b),
-                   C = __builtin_bit_cast(f2_s16x2, c);
-    const f2_s16x2 d1 = B - C, d2 = A - C, d3 = d1 + d2;
-    const f2_s16x2 pa = __builtin_elementwise_max(d1, -d1), pb = __builtin_elementwise_max(d2, -d2),
-                   pc = __builtin_elementwise_max(d3, -d3);
-    const uint32_t na = __builtin_bit_cast(uint32_t, (f2_s16x2)((__builtin_elementwise_min(pb, pc) - pa) >> 15));
-    const uint32_t nb = __builtin_bit_cast(uint32_t, (f2_s16x2)((pc - pb) >> 15));  // -1: pb > pc
+// PNG Paeth predictor (a = left, b = up, c = up-left): pa = |b - c|, pb = |a - c|,
+// pc = |a + b - 2c| (<= 510); a if pa <= min(pb, pc), else b if pb <= pc, else c.
+// Computed in packed f16.  A byte x in a 16-bit lane with 0x64 above it is the f16
+// value 1024 + x (exponent of [1024, 2048): unit steps), so every difference and sum the
+// predictor forms (within +-510) is exact; |d| is one AND of the sign bits; the signs of
+// (min(pb, pc) - pa) and (pc - pb) are the f16 sign bits (never -0: x - x = +0), spread over
+// their lane by one v_pk_ashrrev_i16 each (in asm: the compiler otherwise rewrites the masked
+// selects as per-lane compares and v_cndmask).  The lanes are built by ONE v_perm_b32 per
+// pair (two bytes of a word and the 0x64 bias), and the two results recombined by one more.
+// Checked against the integer rule for all 2^24 (a, b, c) byte triples.
+typedef _Float16 f3_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_sign_mask(uint32_t y) {  // 0xFFFF per negative 16-bit lane
+    uint32_t m;
+    asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(m) : "v"(y));
+    return m;
+}
+__device__ __forceinline__ uint32_t paeth_pair_h(uint32_t a, uint32_t b, uint32_t c) {  // biased lanes
+    const f3_h2 A = __builtin_bit_cast(f3_h2, a), B = __builtin_bit_cast(f3_h2, b), C = __builtin_bit_cast(f3_h2, c);
+    const f3_h2 d1 = B - C, d2 = A - C, d3 = d1 + d2;
+    const f3_h2 pa = __builtin_elementwise_max(d1, -d1), pb = __builtin_elementwise_max(d2, -d2),
+                pc = __builtin_elementwise_max(d3, -d3);
+    const uint32_t na = pk_sign_mask(__builtin_bit_cast(uint32_t, (f3_h2)(__builtin_elementwise_min(pb, pc) - pa)));
+    const uint32_t nb = pk_sign_mask(__builtin_bit_cast(uint32_t, (f3_h2)(pc - pb)));
     const uint32_t t = (nb & c) | (~nb & b);
     return (na & t) | (~na & a);  // na = -1: pa > min(pb, pc)
 }
 __device__ __forceinline__ uint32_t paeth4(uint32_t l, uint32_t u, uint32_t ul) {
-    const uint32_t lo = paeth_pair(l & 0x00FF00FFu, u & 0x00FF00FFu, ul & 0x00FF00FFu);
-    const uint32_t hi = paeth_pair((l >> 8) & 0x00FF00FFu, (u >> 8) & 0x00FF00FFu, (ul >> 8) & 0x00FF00FFu);
-    return lo | (hi << 8);
+    constexpr uint32_t BIAS = 0x64646464u, LO = 0x00060004u, HI = 0x00070005u;  // [b0|b1, 64, b2|b3, 64]
+    const uint32_t rl = paeth_pair_h(__builtin_amdgcn_perm(l, BIAS, LO), __builtin_amdgcn_perm(u, BIAS, LO),
+                                     __builtin_amdgcn_perm(ul, BIAS, LO));
+    const uint32_t rh = paeth_pair_h(__builtin_amdgcn_perm(l, BIAS, HI), __builtin_amdgcn_perm(u, BIAS, HI),
+                                     __builtin_amdgcn_perm(ul, BIAS, HI));
+    return __builtin_amdgcn_perm(rh, rl, 0x06020400u);  // [rl.b0, rh.b0, rl.b2, rh.b2]
 }
 // the bytes bpp before each byte of word k: from words k and k-1 (k-2 for 8-byte samples)
 __device__ __forceinline__ uint32_t back_bytes(const uint32_t* row, int32_t k, uint32_t bpp) {
@@ -831,16 +846,12 @@ __device__ __forceinline__ uint4 f3_pick(const uint4 (&v)[G], uint32_t g) {
     return r;
 }
 
-template <uint32_t G, bool ADAPTIVE>
-__global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                  uint32_t nwaves, uint8_t* __restrict__ stream) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x) * (F3_NT / 64) +
-                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wi >= nwaves) return;  // a whole wave: no barrier in this kernel
-    const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
-    const TileDesc d = dt[ti];
-    const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
+// One wave's run of rows, specialised on the sample size (the left-neighbour shifts, the byte
+// swap and the sign flip are then fixed: no per-row branches or register moves on bpp).
+template <uint32_t G, bool ADAPTIVE, uint32_t BPP>
+__device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t lane, uint8_t* __restrict__ stream) {
+    constexpr uint32_t bpp = BPP;
+    const uint32_t rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
     const uint32_t h = (uint32_t)d.h;
     // uniform row bounds: the row loop and its prefetch stay scalar branches
     const uint32_t r0 = __builtin_amdgcn_readfirstlane((wi - d.blk_first) * F3_RUN);
@@ -1014,6 +1025,23 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
 #pragma unroll
     for (uint32_t k = 0; k + 1 < NB; k++)  // the last nrow % NB rows: already loaded
         if (r + k < r1) step(B[k], B[(k + 1) % NB], r + k);
+}
+
+template <uint32_t G, bool ADAPTIVE>
+__global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                  uint32_t nwaves, uint8_t* __restrict__ stream) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x) * (F3_NT / 64) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wi >= nwaves) return;  // a whole wave: no barrier in this kernel
+    const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
+    const TileDesc d = dt[ti];
+    switch (__builtin_amdgcn_readfirstlane((uint32_t)d.bpp)) {  // a uniform branch
+    case 1: f3_run<G, ADAPTIVE, 1>(d, wi, lane, stream); break;
+    case 2: f3_run<G, ADAPTIVE, 2>(d, wi, lane, stream); break;
+    case 4: f3_run<G, ADAPTIVE, 4>(d, wi, lane, stream); break;
+    default: f3_run<G, ADAPTIVE, 8>(d, wi, lane, stream); break;
+    }
 }
 
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
