@@ -655,7 +655,6 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
             const uint32_t* L = (const uint32_t*)(SA + q * sst + 16);
             const uint32_t* U = (const uint32_t*)(SA + (q - 1) * sst + 16);
             uint32_t s[5] = {0, 0, 0, 0, 0};
-            constexpr uint32_t M = 0x80808080u;
             for (uint32_t k = lane; k < nw; k += 64) {
                 const uint32_t cur = L[k], up = U[k];
                 const uint32_t left = back_bytes(L, (int32_t)k, bpp), ul = back_bytes(U, (int32_t)k, bpp);
