@@ -32,8 +32,9 @@
 // plus the next lane's), so match lengths (capped at CAP) and the positions where a match
 // pays are a few bit operations; the wave then walks only the positions that hold a
 // paying match, scalar, and extends a capped match by one wave-wide compare.  The result
-// is exactly the sequential greedy/lazy parse of ph_parse_emu (its scalar twin).  Matches
-// end inside their sub-segment.  Tokens are kept as per-wave match lists; literals are the
+// is exactly the sequential greedy/lazy parse of ph_parse_emu (its scalar twin).  A match
+// that reaches the end of its sub-segment runs on into the next one (up to 258 bytes, inside
+// the segment), and the next wave parses from its end.  Tokens are kept as per-wave match lists; literals are the
 // positions no match covers, so the later phases (histogram, bit counts, bit writing)
 // walk fixed CH-position thread chunks.
 #pragma once
@@ -194,14 +195,11 @@ PBX_HD void best_match(const SM& S, const SegParams& sp, uint32_t p, uint32_t se
     }
 }
 
-// Full length of a match of distance D at position p that reached the cap (scalar form of
-// the wave-wide compare: 4-byte words at offsets L + 4k, up to min(258, se - p)).
-template <class C, class SM>
-PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint32_t se,
-                              uint32_t L, uint32_t D) {
-    const uint32_t rem = se - p;
-    const uint32_t maxlen = rem < 258 ? rem : 258;
-    if (L < (uint32_t)C::CAP || L >= maxlen) return L;
+// Length of a match of distance D at position p extended past L equal bytes by comparing
+// 4-byte words at offsets L + 4k, up to maxlen (scalar form of the wave-wide compare).
+template <class SM>
+PBX_HD uint32_t extend_to(const SM& S, const SegParams& sp, uint32_t p, uint32_t L, uint32_t D, uint32_t maxlen) {
+    if (L >= maxlen) return L;
     const uint32_t a = sp.wl + p;
     for (uint32_t k = 0; k < 64; k++) {
         const uint32_t o = L + 4 * k;
@@ -215,13 +213,51 @@ PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint
     return maxlen;
 }
 
+// Full length of a match of distance D at position p that reached the cap, inside the
+// sub-segment (up to min(258, se - p)).
+template <class C, class SM>
+PBX_HD uint32_t extend_scalar(const SM& S, const SegParams& sp, uint32_t p, uint32_t se,
+                              uint32_t L, uint32_t D) {
+    const uint32_t rem = se - p;
+    const uint32_t maxlen = rem < 258 ? rem : 258;
+    if (L < (uint32_t)C::CAP) return L;
+    return extend_to(S, sp, p, L, D, maxlen);
+}
+
+// A match that reaches the end of its wave's sub-segment continues into the next one, up to
+// min(258, sl - p) (segment end): runs are not cut at the 2 KiB wave boundaries (G_FAKE's
+// repeated rows: one 258-byte match chain per segment instead of a short match per wave).
+template <class C, class SM>
+PBX_HD uint32_t extend_cross(const SM& S, const SegParams& sp, uint32_t p, uint32_t se, uint32_t L,
+                             uint32_t D) {
+    if (p + L != se || se >= sp.sl) return L;
+    const uint32_t rem = sp.sl - p;
+    return extend_to(S, sp, p, L, D, rem < 258 ? rem : 258);
+}
+
+// End (segment position) of wave w's last recorded match when it runs past the wave's
+// sub-segment, else 0: wave w + 1 parses from there (its first positions are that match's).
+template <class C, class SM>
+PBX_HD uint32_t carry_end(const SM& S, uint32_t w) {
+    const uint32_t nm = S.w_nm[w];
+    if (!nm) return 0u;
+    const uint32_t r = S.mpos[w * C::MAXMW + nm - 1];
+    const uint32_t e = (r & 0xFFFFu) + (r >> 16) + 3;
+    return e > (w + 1) * (uint32_t)C::SUB ? e : 0u;
+}
+
 // The parse of wave w's sub-segment, sequentially (the specification the device's
-// bit-parallel parse reproduces): greedy, one-step lazy on capped lengths.
+// bit-parallel parse reproduces): greedy, one-step lazy on capped lengths, from where the
+// previous wave's last match ends if it runs into this sub-segment (waves in order).
 template <class C, class SM>
 PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
     const uint32_t ss = w * C::SUB;
     const uint32_t se = ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl;
     uint32_t nm = 0, p = ss, cov = 0;
+    if (w > 0) {
+        const uint32_t c = carry_end<C>(S, w - 1);
+        if (c > p) p = c;
+    }
     while (p < se) {
         uint32_t L, D, L1, D1;
         best_match<C>(S, sp, p, se, L, D);
@@ -229,6 +265,7 @@ PBX_HD void ph_parse_emu(uint32_t w, SM& S, const SegParams& sp) {
         best_match<C>(S, sp, p + 1, se, L1, D1);
         if (L1 > L) { p++; continue; }  // lazy: a longer match starts at the next byte
         L = extend_scalar<C>(S, sp, p, se, L, D);
+        L = extend_cross<C>(S, sp, p, se, L, D);
         if (nm < (uint32_t)C::MAXMW) {
             S.mpos[w * C::MAXMW + nm] = p | ((L - 3) << 16);
             S.mdist[w * C::MAXMW + nm] = (uint16_t)(D - 1);
@@ -262,6 +299,9 @@ PBX_HD void walk_tokens(uint32_t tid, const SM& S, const SegParams& sp, F& f) {
     uint32_t pos = cs;
     if (lo > 0) {
         const uint32_t pe = (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3;
+        if (pe > pos) pos = pe;
+    } else if (w > 0) {  // the previous wave's last match may run into this chunk
+        const uint32_t pe = carry_end<C>(S, w - 1);
         if (pe > pos) pos = pe;
     }
     for (uint32_t m = lo; m < nm && pos < ce; m++) {

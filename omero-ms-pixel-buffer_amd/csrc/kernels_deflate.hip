@@ -46,6 +46,7 @@ struct LzSmem {
     alignas(16) uint32_t buf[C::BUFW];
     uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
+    uint32_t w_end[C::NW];  // a wave's last match end when it runs into the next wave (else 0)
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
     alignas(16) uint32_t h8[288 * LZ_HCOPIES];
@@ -724,206 +725,261 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t ss = w * C::SUB;
     const uint32_t se = __builtin_amdgcn_readfirstlane(ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl);
+    const bool active = ss < se;  // (uniform) waves past the segment's end have nothing to parse
     cover = 0;
     smask = 0;
-    if (ss >= se) {
-        if (lane == 0) S.w_nm[w] = 0;
-        return;
-    }
     const uint32_t p0 = ss + 32 * lane, a0 = sp.wl + p0;
-    const uint32_t nval = se > p0 ? se - p0 : 0u;
-    smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0;
-    uint32_t cvb_lo = 0, cvb_hi = 0;  // bytes inside some paying run (the walk's coverage bound, below)
+    bool skip = true;
+    if (active) {
+        const uint32_t nval = se > p0 ? se - p0 : 0u;
+        smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
+        uint32_t cvb_lo = 0, cvb_hi = 0;  // bytes inside some paying run (the walk's coverage bound, below)
+        uint32_t elast = 0;               // some candidate's equality bit at the sub-segment's last byte
 #pragma unroll
-    for (int c = 0; c < NCAND; c++) {
-        const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
-        dd[c] = d;
-        ml[c] = match_minlen(d);
-        uint32_t e = 0;
-        if (d) {
-            if (c < 2) {  // d = 1, 2: the lane's own words shifted by d bytes
-                const uint32_t sh = 32 - 8 * d;
-                if (PBX_LZ_DOT4PACK) {
-                    uint32_t xw[8];
+        for (int c = 0; c < NCAND; c++) {
+            const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
+            dd[c] = d;
+            ml[c] = match_minlen(d);
+            uint32_t e = 0;
+            if (d) {
+                if (c < 2) {  // d = 1, 2: the lane's own words shifted by d bytes
+                    const uint32_t sh = 32 - 8 * d;
+                    if (PBX_LZ_DOT4PACK) {
+                        uint32_t xw[8];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh);
-                    e = pack_zero_bytes8(xw);
-                } else {
+                        for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh);
+                        e = pack_zero_bytes8(xw);
+                    } else {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh)) << (4 * j);
+                        for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(cw[j + 1], cw[j], sh)) << (4 * j);
+                    }
+                } else {  // one row up: unaligned words at a0 - d
+                    const int32_t b = (int32_t)a0 - (int32_t)d;
+                    const int32_t r = b >> 2;
+                    const uint32_t sh = (uint32_t)(b & 3) * 8;
+                    // words r .. r+8 from three aligned 16-byte reads (lanes 32 bytes apart: a
+                    // 2-way conflict per read instead of 8-way on 9 word reads); r mod 4 is the
+                    // same in every lane (a0 - 32 lane is), so the selection is uniform.  Quads
+                    // before the buffer (positions the window mask drops) read quad 0.
+                    const int32_t r4 = r & ~3;
+                    uint32_t q12[12];
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const int32_t at = r4 + 4 * k;
+                        const uint4 v = *(const uint4*)&S.buf[at > 0 ? at : 0];
+                        q12[4 * k] = v.x; q12[4 * k + 1] = v.y; q12[4 * k + 2] = v.z; q12[4 * k + 3] = v.w;
+                    }
+                    uint32_t rw[9];
+                    switch (__builtin_amdgcn_readfirstlane((uint32_t)(r - r4))) {
+                    case 0:
+#pragma unroll
+                        for (int j = 0; j < 9; j++) rw[j] = q12[j];
+                        break;
+                    case 1:
+#pragma unroll
+                        for (int j = 0; j < 9; j++) rw[j] = q12[j + 1];
+                        break;
+                    case 2:
+#pragma unroll
+                        for (int j = 0; j < 9; j++) rw[j] = q12[j + 2];
+                        break;
+                    default:
+#pragma unroll
+                        for (int j = 0; j < 9; j++) rw[j] = q12[j + 3];
+                        break;
+                    }
+                    if (PBX_LZ_DOT4PACK) {
+                        uint32_t xw[8];
+#pragma unroll
+                        for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh);
+                        e = pack_zero_bytes8(xw);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
+                    }
                 }
-            } else {  // one row up: unaligned words at a0 - d
-                const int32_t b = (int32_t)a0 - (int32_t)d;
-                const int32_t r = b >> 2;
-                const uint32_t sh = (uint32_t)(b & 3) * 8;
-                // words r .. r+8 from three aligned 16-byte reads (lanes 32 bytes apart: a
-                // 2-way conflict per read instead of 8-way on 9 word reads); r mod 4 is the
-                // same in every lane (a0 - 32 lane is), so the selection is uniform.  Quads
-                // before the buffer (positions the window mask drops) read quad 0.
-                const int32_t r4 = r & ~3;
-                uint32_t q12[12];
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const int32_t at = r4 + 4 * k;
-                    const uint4 v = *(const uint4*)&S.buf[at > 0 ? at : 0];
-                    q12[4 * k] = v.x; q12[4 * k + 1] = v.y; q12[4 * k + 2] = v.z; q12[4 * k + 3] = v.w;
-                }
-                uint32_t rw[9];
-                switch (__builtin_amdgcn_readfirstlane((uint32_t)(r - r4))) {
-                case 0:
-#pragma unroll
-                    for (int j = 0; j < 9; j++) rw[j] = q12[j];
-                    break;
-                case 1:
-#pragma unroll
-                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 1];
-                    break;
-                case 2:
-#pragma unroll
-                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 2];
-                    break;
-                default:
-#pragma unroll
-                    for (int j = 0; j < 9; j++) rw[j] = q12[j + 3];
-                    break;
-                }
-                if (PBX_LZ_DOT4PACK) {
-                    uint32_t xw[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) xw[j] = cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh);
-                    e = pack_zero_bytes8(xw);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; j++) e |= zero_nibble(cw[j + 1] ^ funnel32(rw[j + 1], rw[j], sh)) << (4 * j);
-                }
+                const uint32_t vm = a0 >= d ? 0xFFFFFFFFu : (d - a0 >= 32 ? 0u : 0xFFFFFFFFu << (d - a0));
+                e &= vm & smask;
             }
-            const uint32_t vm = a0 >= d ? 0xFFFFFFFFu : (d - a0 >= 32 ? 0u : 0xFFFFFFFFu << (d - a0));
-            e &= vm & smask;
+            // the next lane's E (wave_shl:1; lane 63: none, matches stay in the sub-segment)
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x130, 0xF, 0xF, false);
+            exlo[c] = e;
+            exhi[c] = nx;
+            if (d) {
+                // (E | next lane's E << 32) >> k, low word: one funnel shift (v_alignbit) each
+                uint32_t r = e & __builtin_amdgcn_alignbit(nx, e, 1) & __builtin_amdgcn_alignbit(nx, e, 2);
+                if (ml[c] >= 4) r &= __builtin_amdgcn_alignbit(nx, e, 3);
+                if (ml[c] >= 6) r &= __builtin_amdgcn_alignbit(nx, e, 4) & __builtin_amdgcn_alignbit(nx, e, 5);
+                M |= r;
+                // [j, j + ml) for every paying start j of the lane: bits inside the lane (lo) and
+                // the ones past its end (hi)
+                uint32_t dlo = r | (r << 1) | (r << 2), dhi = (r >> 31) | (r >> 30);
+                if (ml[c] >= 4) { dlo |= r << 3; dhi |= r >> 29; }
+                if (ml[c] >= 6) { dlo |= (r << 4) | (r << 5); dhi |= (r >> 28) | (r >> 27); }
+                cvb_lo |= dlo;
+                cvb_hi |= dhi;
+                elast |= e;
+            }
         }
-        // the next lane's E (wave_shl:1; lane 63: none, matches stay in the sub-segment)
-        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x130, 0xF, 0xF, false);
-        exlo[c] = e;
-        exhi[c] = nx;
-        if (d) {
-            // (E | next lane's E << 32) >> k, low word: one funnel shift (v_alignbit) each
-            uint32_t r = e & __builtin_amdgcn_alignbit(nx, e, 1) & __builtin_amdgcn_alignbit(nx, e, 2);
-            if (ml[c] >= 4) r &= __builtin_amdgcn_alignbit(nx, e, 3);
-            if (ml[c] >= 6) r &= __builtin_amdgcn_alignbit(nx, e, 4) & __builtin_amdgcn_alignbit(nx, e, 5);
-            M |= r;
-            // [j, j + ml) for every paying start j of the lane: bits inside the lane (lo) and
-            // the ones past its end (hi)
-            uint32_t dlo = r | (r << 1) | (r << 2), dhi = (r >> 31) | (r >> 30);
-            if (ml[c] >= 4) { dlo |= r << 3; dhi |= r >> 29; }
-            if (ml[c] >= 6) { dlo |= (r << 4) | (r << 5); dhi |= (r >> 28) | (r >> 27); }
-            cvb_lo |= dlo;
-            cvb_hi |= dhi;
-        }
-    }
 #ifndef PBX_LZ_COVBOUND
 #define PBX_LZ_COVBOUND 1  // skip the walk when its matches cannot reach MINCOV (0: always walk)
 #endif
-    // Every match the walk records lies inside a run of >= ml equal bytes of its candidate,
-    // i.e. inside the union of [j, j + ml) over that candidate's paying starts j; a match
-    // extended past CAP lies in a run of >= CAP >= MINCOV bytes.  So the walk's coverage is at
-    // most the wave's count of such bytes (per lane, bytes past the lane's chunk counted too:
-    // an overestimate), and below MINCOV the walk would drop all its matches (noise: most
-    // waves hold a few 3-4 byte runs): the same result without the walk.
-    if (PBX_LZ_COVBOUND &&
-        wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) < (uint32_t)C::MINCOV) {
-        if (lane == 0) S.w_nm[w] = 0;
-        return;
+        // Every match the walk records lies inside a run of >= ml equal bytes of its candidate,
+        // i.e. inside the union of [j, j + ml) over that candidate's paying starts j; a match
+        // extended past CAP lies in a run of >= CAP >= MINCOV bytes.  So the walk's coverage is at
+        // most the wave's count of such bytes (per lane, bytes past the lane's chunk counted too:
+        // an overestimate), and below MINCOV the walk would drop all its matches (noise: most
+        // waves hold a few 3-4 byte runs): the same result without the walk.  A match that reaches
+        // the sub-segment's last byte may run on into the next one (extend_cross), past that
+        // count: the bound then does not hold, and the wave walks.
+        const uint32_t tl = (se - 1 - ss) >> 5, il = (se - 1 - ss) & 31;
+        const bool reach = (((uint32_t)__builtin_amdgcn_readlane(elast, tl) >> il) & 1u) != 0 && se < sp.sl;
+        skip = PBX_LZ_COVBOUND && !reach &&
+               wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) <
+                   (uint32_t)C::MINCOV;
     }
     const uint64_t B = __ballot(M != 0);
-    const uint32_t lsub = se - ss;
-    uint32_t nm = 0, o = 0, cov = 0;
-    while (o < lsub) {
-        // the first position >= o where a match pays
-        const uint32_t t0 = o >> 5;
-        uint32_t k = 0xFFFFFFFFu;
-        const uint32_t mt = __builtin_amdgcn_readlane(M, t0) & (0xFFFFFFFFu << (o & 31));
-        if (mt) {
-            k = (t0 << 5) + (uint32_t)__builtin_ctz(mt);
-        } else if (t0 < 63) {
-            const uint64_t bb = B & (~0ull << (t0 + 1));
-            if (bb) {
-                const uint32_t t2 = (uint32_t)__builtin_ctzll(bb);
-                k = (t2 << 5) + (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(M, t2));
+    const uint32_t lsub = active ? se - ss : 0u;
+    uint32_t nm = 0, cov = 0, last_end = 0;
+    // The greedy walk over the paying positions from o0 (sub-segment offset): records, the
+    // lane's covered positions, the end of the last match (uniform).
+    auto walk = [&](uint32_t o0) {
+        nm = 0;
+        cov = 0;
+        last_end = 0;
+        cover = 0;
+        uint32_t o = o0;
+        while (o < lsub) {
+            // the first position >= o where a match pays
+            const uint32_t t0 = o >> 5;
+            uint32_t k = 0xFFFFFFFFu;
+            const uint32_t mt = __builtin_amdgcn_readlane(M, t0) & (0xFFFFFFFFu << (o & 31));
+            if (mt) {
+                k = (t0 << 5) + (uint32_t)__builtin_ctz(mt);
+            } else if (t0 < 63) {
+                const uint64_t bb = B & (~0ull << (t0 + 1));
+                if (bb) {
+                    const uint32_t t2 = (uint32_t)__builtin_ctzll(bb);
+                    k = (t2 << 5) + (uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(M, t2));
+                }
             }
-        }
-        k = __builtin_amdgcn_readfirstlane(k);
-        if (k >= lsub) break;
-        const uint32_t t = k >> 5, i = k & 31;
-        uint32_t L = 0, D = 0, Dc = 0, L1 = 0;
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (k >= lsub) break;
+            const uint32_t t = k >> 5, i = k & 31;
+            uint32_t L = 0, D = 0, Dc = 0, L1 = 0;
 #pragma unroll
-        for (int c = 0; c < NCAND; c++) {
-            if (!dd[c]) continue;
-            // (readlane returns int: cast through uint32_t, no sign extension)
-            const uint64_t ex = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(exhi[c], t) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane(exlo[c], t);
-            uint32_t n0 = (uint32_t)__builtin_ctzll(~(ex >> i));
-            uint32_t n1 = (uint32_t)__builtin_ctzll(~(ex >> (i + 1)));
-            n0 = n0 < (uint32_t)C::CAP ? n0 : (uint32_t)C::CAP;
-            n1 = n1 < (uint32_t)C::CAP ? n1 : (uint32_t)C::CAP;
-            if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; Dc = (uint32_t)c; }
-            if (n1 >= ml[c] && n1 > L1) L1 = n1;
-        }
-        L = __builtin_amdgcn_readfirstlane(L);
-        D = __builtin_amdgcn_readfirstlane(D);
-        Dc = __builtin_amdgcn_readfirstlane(Dc);
-        L1 = __builtin_amdgcn_readfirstlane(L1);
-        if (L < 3 || L1 > L) { o = k + 1; continue; }  // lazy: a longer match starts next
-        const uint32_t p = ss + k;
-        const uint32_t rem = se - p;
-        const uint32_t maxlen = rem < 258 ? rem : 258;
+            for (int c = 0; c < NCAND; c++) {
+                if (!dd[c]) continue;
+                // (readlane returns int: cast through uint32_t, no sign extension)
+                const uint64_t ex = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(exhi[c], t) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(exlo[c], t);
+                uint32_t n0 = (uint32_t)__builtin_ctzll(~(ex >> i));
+                uint32_t n1 = (uint32_t)__builtin_ctzll(~(ex >> (i + 1)));
+                n0 = n0 < (uint32_t)C::CAP ? n0 : (uint32_t)C::CAP;
+                n1 = n1 < (uint32_t)C::CAP ? n1 : (uint32_t)C::CAP;
+                if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; Dc = (uint32_t)c; }
+                if (n1 >= ml[c] && n1 > L1) L1 = n1;
+            }
+            L = __builtin_amdgcn_readfirstlane(L);
+            D = __builtin_amdgcn_readfirstlane(D);
+            Dc = __builtin_amdgcn_readfirstlane(Dc);
+            L1 = __builtin_amdgcn_readfirstlane(L1);
+            if (L < 3 || L1 > L) { o = k + 1; continue; }  // lazy: a longer match starts next
+            const uint32_t p = ss + k;
+            const uint32_t rem = se - p;
+            const uint32_t maxlen = rem < 258 ? rem : 258;
 #ifndef PBX_LZ_MASKEXT
 #define PBX_LZ_MASKEXT 1  // extend capped matches from the lanes' equality masks (0: LDS compare)
 #endif
-        if (PBX_LZ_MASKEXT && C::CAP == 32 && L >= (uint32_t)C::CAP && L < maxlen) {
-            // the run of the chosen candidate's equality bits from position k over the wave's
-            // masks: the rest of lane t, the whole lanes after it (a ballot of all-ones masks),
-            // and the first bits of the next lane; masked bits (past se) end it, so capped at
-            // maxlen it is the length the byte compare below finds
-            static_assert(NCAND == 3, "three candidate masks");
-            const uint32_t es = Dc == 0 ? exlo[0] : Dc == 1 ? exlo[1] : exlo[2];
-            const uint64_t full = __ballot(es == 0xFFFFFFFFu);
-            uint32_t run = 32 - i;  // a capped length of CAP = 32: the rest of lane t is equal
-            if (t < 63) {
-                const uint32_t nf = (uint32_t)__builtin_ctzll(~(full >> (t + 1)));  // whole lanes after t
-                const uint32_t t2 = t + 1 + nf;  // the first lane that is not (all its bits < 32)
-                run += 32 * nf;
-                if (t2 < 64) run += (uint32_t)__builtin_ctz(~(uint32_t)__builtin_amdgcn_readlane(es, t2));
+            // one wave-wide compare of 4 bytes per lane extends the match from L up to lim
+            auto extend_lds = [&](uint32_t lim) {
+                const uint32_t a = sp.wl + p, off = L + 4 * lane;
+                const uint32_t x = off < lim ? (lds_ld4(S, a - D + off) ^ lds_ld4(S, a + off)) : 0u;
+                const uint64_t mm = __ballot(off >= lim || x != 0);
+                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+                const uint32_t xf = __builtin_amdgcn_readlane(x, f);
+                const uint32_t of = L + 4 * f;
+                const uint32_t l = of >= lim ? lim : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
+                L = __builtin_amdgcn_readfirstlane(l < lim ? l : lim);
+            };
+            if (PBX_LZ_MASKEXT && C::CAP == 32 && L >= (uint32_t)C::CAP && L < maxlen) {
+                // the run of the chosen candidate's equality bits from position k over the wave's
+                // masks: the rest of lane t, the whole lanes after it (a ballot of all-ones masks),
+                // and the first bits of the next lane; masked bits (past se) end it, so capped at
+                // maxlen it is the length the byte compare below finds
+                static_assert(NCAND == 3, "three candidate masks");
+                const uint32_t es = Dc == 0 ? exlo[0] : Dc == 1 ? exlo[1] : exlo[2];
+                const uint64_t full = __ballot(es == 0xFFFFFFFFu);
+                uint32_t run = 32 - i;  // a capped length of CAP = 32: the rest of lane t is equal
+                if (t < 63) {
+                    const uint32_t nf = (uint32_t)__builtin_ctzll(~(full >> (t + 1)));  // whole lanes after t
+                    const uint32_t t2 = t + 1 + nf;  // the first lane that is not (all its bits < 32)
+                    run += 32 * nf;
+                    if (t2 < 64) run += (uint32_t)__builtin_ctz(~(uint32_t)__builtin_amdgcn_readlane(es, t2));
+                }
+                L = __builtin_amdgcn_readfirstlane(run < maxlen ? run : maxlen);
+            } else if (L >= (uint32_t)C::CAP && L < maxlen) {
+                extend_lds(maxlen);
             }
-            L = __builtin_amdgcn_readfirstlane(run < maxlen ? run : maxlen);
-        } else if (L >= (uint32_t)C::CAP && L < maxlen) {
-            // one wave-wide compare of 4 bytes per lane extends the match past the cap
-            const uint32_t a = sp.wl + p, off = L + 4 * lane;
-            const uint32_t x = off < maxlen ? (lds_ld4(S, a - D + off) ^ lds_ld4(S, a + off)) : 0u;
-            const uint64_t mm = __ballot(off >= maxlen || x != 0);
-            const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-            const uint32_t xf = __builtin_amdgcn_readlane(x, f);
-            const uint32_t of = L + 4 * f;
-            const uint32_t l = of >= maxlen ? maxlen : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
-            L = __builtin_amdgcn_readfirstlane(l < maxlen ? l : maxlen);
-        }
-        if (nm < (uint32_t)C::MAXMW) {
-            if (lane == 0) S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
-            nm++;
-            cov += L;
-            // positions [p, p + L) of this lane's chunk are covered
-            const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + L - p0;
-            if (p + L > p0 && p < p0 + 32) {
-                const uint32_t h = hi < 32 ? hi : 32u;
-                cover |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << lo);
+            // a match reaching the end of the sub-segment runs on into the next one (extend_cross)
+            if (p + L == se && se < sp.sl) {
+                const uint32_t r2 = sp.sl - p;
+                const uint32_t lim = r2 < 258 ? r2 : 258;
+                if (L < lim) extend_lds(lim);
             }
+            if (nm < (uint32_t)C::MAXMW) {
+                if (lane == 0) S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
+                nm++;
+                cov += L;
+                last_end = p + L;
+                // positions [p, p + L) of this lane's chunk are covered
+                const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + L - p0;
+                if (p + L > p0 && p < p0 + 32) {
+                    const uint32_t h = hi < 32 ? hi : 32u;
+                    cover |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << lo);
+                }
+            }
+            o = k + L;
         }
-        o = k + L;
+        // ph_parse_emu's rule: matches covering < MINCOV bytes are dropped (literals only)
+        if (cov < (uint32_t)C::MINCOV) {
+            nm = 0;
+            cover = 0;
+            last_end = 0;
+        }
+    };
+    if (active && !skip) walk(0);
+    // Matches cross the wave boundaries (ph_parse_emu: wave w parses from where wave w - 1's last
+    // match ends).  Every wave walked from its own start; a wave whose predecessor's FINAL last
+    // match runs into it walks again from that match's end, in wave order.  Only segments where
+    // some wave's match ran past its sub-segment need that (runs: G_FAKE; noise: almost never).
+    if (lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
+    __syncthreads();
+    uint32_t any = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < C::NW; j++) any |= S.w_end[j];
+    if (__builtin_amdgcn_readfirstlane(any)) {
+#pragma unroll 1
+        for (uint32_t j = 1; j < (uint32_t)C::NW; j++) {
+            if (w == j) {
+                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
+                if (c > ss) {
+                    if (!skip) walk(c - ss);
+                    if (lane == 0) S.w_end[j] = last_end > se ? last_end : 0u;
+                }
+            }
+            __syncthreads();
+        }
     }
-    // ph_parse_emu's rule: matches covering < MINCOV bytes are dropped (literals only)
-    if (cov < (uint32_t)C::MINCOV) {
-        nm = 0;
-        cover = 0;
+    // the positions [ss, c) the previous wave's last match covers are not literals here
+    if (w > 0 && active) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[w - 1]);
+        if (c > p0) {
+            const uint32_t h = c - p0 < 32 ? c - p0 : 32u;
+            cover |= h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u;
+        }
     }
     // the kept matches' length and distance symbols, one match per lane (this wave's own
     // records: LDS operations of one wave complete in order)
@@ -1936,7 +1992,12 @@ __device__ __forceinline__ bool build_slots(uint32_t tid, const SM& S, const Seg
         const uint32_t l = a > cs ? a - cs : 0u, h = b - cs < 32 ? b - cs : 32u;
         if (b > cs && l < 32) covered |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << l);
     };
-    if (lo > 0) cover(mp[lo - 1] & 0xFFFFu, (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3);
+    if (lo > 0) {
+        cover(mp[lo - 1] & 0xFFFFu, (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3);
+    } else if (w > 0) {  // the previous wave's last match may run into this chunk (walk_tokens)
+        const uint32_t pe = carry_end<C>(S, w - 1);
+        if (pe > cs) cover(cs, pe);
+    }
     uint32_t m1 = lo;
     while (m1 < nm && (mp[m1] & 0xFFFFu) < ce) {
         cover(mp[m1] & 0xFFFFu, (mp[m1] & 0xFFFFu) + (mp[m1] >> 16) + 3);

@@ -30,6 +30,12 @@ for stage in "$@"; do
       cat $O/subbatch.log | tail -6
       timeout -k 10 300 python -u scripts/filter_bench.py 1 2 3 4 5 > $O/filter.log 2>&1 || { tail -30 $O/filter.log; exit 1; }
       cat $O/filter.log ;;
+    fvar)
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_*/libpbx.so; do
+        echo "-- $L"
+        PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/filter_bench.py 1 2 4 5 > $O/fvar.log 2>&1 || { tail -20 $O/fvar.log; exit 1; }
+        cat $O/fvar.log
+      done ;;
     pmcf)
       for f in 1 4 5; do
         P=$O/pmcf$f

@@ -42,10 +42,11 @@ def test_crc_combine_matches_zlib():
         assert _emu.crc_combine(zlib.crc32(a), zlib.crc32(b), lb) == zlib.crc32(a + b)
 
 
-@pytest.mark.parametrize("kind,limit", [(2, 1.01), (1, 1.30)])
+@pytest.mark.parametrize("kind,limit", [(2, 1.01), (1, 1.03)])
 def test_ratio_vs_zlib6(oracle, kind, limit):
     """512x512 uint16 PNG stream: GPU deflate within 1% of zlib-6 on G_NOISE (the headline
-    generator) and within 30% on G_FAKE (per-16 KiB-segment Huffman headers dominate)."""
+    generator) and within 3% on G_FAKE (one repeated row: matches run across the waves'
+    2 KiB sub-segments, so only the 33 segment boundaries cut the 258-byte match chain)."""
     t = oracle.gen_region(kind, oracle.UINT16, 0, 0, 512, 512)
     s = oracle.png_filter_stream(t, oracle.UINT16, 512, 512, 0).tobytes()
     z, _ = _emu.deflate(s, 1025)
@@ -64,8 +65,10 @@ def test_filtered_streams(oracle, filt):
 @pytest.mark.parametrize("kind", ["random", "periodic", "rows"])
 def test_lz77_records_cover_the_segment(kind):
     """LZ77 stage records (what k_lz77 writes and the GPU test compares): per segment the
-    literals plus the match lengths cover exactly the segment's bytes, every match lies in
-    its wave's sub-segment, uses a candidate distance (1, 2, one row) and pays."""
+    literals plus the match lengths cover exactly the segment's bytes, every match starts in
+    its wave's sub-segment and ends inside the segment (a match may run on into the next
+    wave's sub-segment, whose parse then starts at its end: no two matches overlap), uses a
+    candidate distance (1, 2, one row) and pays."""
     rng = np.random.default_rng(3)
     rowlen = 301
     if kind == "random":
@@ -82,13 +85,15 @@ def test_lz77_records_cover_the_segment(kind):
     for k in range(n):
         sl = min(seg, len(s) - k * seg)
         lits = int(hist[k][:256].sum())
-        covered = 0
+        covered, prev_end = 0, 0
         for w in range(nw):
             for m in range(int(mrec[k][w])):
                 pm = int(mrec[k][nw + w * mw + m])
                 d = int(mrec[k][nw + nw * mw + w * mw + m]) + 1
                 p, ln = pm & 0xFFFF, (pm >> 16) + 3
-                assert w * 2048 <= p and p + ln <= min((w + 1) * 2048, sl)
+                assert w * 2048 <= p < min((w + 1) * 2048, sl) and p + ln <= sl
+                assert p >= prev_end
+                prev_end = p + ln
                 assert d in (1, 2, rowlen)
                 assert ln >= (3 if d <= 256 else 4 if d <= 4096 else 6)
                 covered += ln
