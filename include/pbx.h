@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 7
+#define PBX_ABI_VERSION 8
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -304,6 +304,24 @@ int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result
 /* Results go back to the context that produced them (ctx may be NULL). */
 void pbx_results_release(pbx_ctx* ctx, pbx_result* results, uint64_t n);
 
+/* Stage timings under the reference's tracing span names (TileRequestHandler.java:81
+ * "get_tile", :104 "get_tile_direct", :147 "create_metadata", :180 "write_image").  A request is
+ * served inside a batch, so the stages are the batch's (HIP events on its kernel stream; the
+ * caller times its own get_tile span around pbx_get_tile):
+ *   get_tile_direct_ms  the region gather from HBM (raw/TIFF extract kernel); 0 for a PNG-only
+ *                       batch, whose gather is fused into the filter/deflate kernels
+ *   write_image_ms      PNG row filters + deflate (LZ77, Huffman, encode) of the whole batch
+ *   create_metadata_ms  container framing: IHDR/IDAT/IEND or the TIFF IFD, chunk CRCs
+ *   batch_ms            the batch's device time, first to last kernel
+ *   d2h_ms              host wall time from queuing the batch's device->host copy to its end
+ *   batch_tiles         requests in the batch
+ * Returns PBX_E_BADARG for a result without a body (error statuses, released results). */
+typedef struct pbx_spans {
+    double get_tile_direct_ms, write_image_ms, create_metadata_ms, batch_ms, d2h_ms;
+    uint64_t batch_tiles;
+} pbx_spans;
+int pbx_result_spans(const pbx_result* r, pbx_spans* out);
+
 /* Batched async: pbx_submit plans and launches n independent getTile
  * requests and returns at once; pbx_wait blocks until the batch has finished (timeout_us < 0:
  * no limit; 0: poll), fills out[0..n) (the array given to pbx_submit) exactly like
@@ -374,7 +392,7 @@ int pbx_set_kernel_streams(pbx_ctx* ctx, int32_t streams, int32_t stagger);
 
 /* sizeof of the ABI structs, for bindings to check their layouts: pbx_config,
  * pbx_plane_desc, pbx_tile_req, pbx_result, pbx_batch_stats, pbx_image_desc,
- * pbx_residency_stats (in that order).  Returns the number of structs (7). */
+ * pbx_residency_stats, pbx_spans (in that order).  Returns the number of structs (8). */
 int pbx_abi_sizes(uint64_t* sizes, int n);
 
 /* ---- A node: N device contexts in ONE process ----

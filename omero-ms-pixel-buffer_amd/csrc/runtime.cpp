@@ -327,6 +327,7 @@ struct HostBlock {
     std::atomic<int> refs{0};
     pbx_ctx* ctx = nullptr;
     void* pinned = nullptr;
+    pbx_spans spans{};  // the batch's stage timings (pbx_result_spans)
 };
 
 }  // namespace
@@ -2586,6 +2587,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
         const hipError_t e = hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming);
         if (e != hipSuccess) return fail_hb(e);
     }
+    const auto t_copy = std::chrono::steady_clock::now();
     {   // the copies are queued back to back on the copy stream (several completers may have
         // theirs in flight: the link never waits for a host round trip); the wait is outside
         std::lock_guard<std::mutex> cg(ctx->copy_mu);
@@ -2598,6 +2600,18 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
         if (e != hipSuccess) return fail_hb(e);
     }
     if (const hipError_t e = hipEventSynchronize(b->ev_copy)) return fail_hb(e);
+    {   // the span timings (events of a finished batch: no wait)
+        float ms[5] = {0, 0, 0, 0, 0};
+        const int ij[5][2] = {{1, 2}, {2, 3}, {3, 7}, {7, 8}, {0, 8}};
+        for (int q = 0; q < 5; q++) (void)hipEventElapsedTime(&ms[q], b->ev[ij[q][0]], b->ev[ij[q][1]]);
+        pbx_spans& sp = hb->spans;
+        sp.get_tile_direct_ms = ms[0];
+        sp.write_image_ms = (double)ms[1] + ms[2];
+        sp.create_metadata_ms = ms[3];
+        sp.batch_ms = ms[4];
+        sp.d2h_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_copy).count();
+        sp.batch_tiles = n;
+    }
     int refs = 0;
     for (size_t k = 0; k < b->ft.size(); k++) {
         const TileDesc& d = b->ft[k];
@@ -2665,6 +2679,14 @@ void pbx_results_release(pbx_ctx* ctx, pbx_result* res, uint64_t n) {
             delete hb;
         }
     }
+}
+
+int pbx_result_spans(const pbx_result* r, pbx_spans* out) {
+    if (!r || !out) return fail(PBX_E_BADARG, "null argument");
+    const HostBlock* hb = (const HostBlock*)r->owner;
+    if (!hb) return fail(PBX_E_BADARG, "result without a body (status %d, or released)", r->status);
+    *out = hb->spans;
+    return PBX_OK;
 }
 
 int pbx_get_tiles(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_result* out) {
@@ -2741,12 +2763,12 @@ int pbx_wait(pbx_ctx* ctx, pbx_ticket* t, int64_t timeout_us) {
 }
 
 int pbx_abi_sizes(uint64_t* sizes, int n) {
-    const uint64_t v[7] = {sizeof(pbx_config), sizeof(pbx_plane_desc), sizeof(pbx_tile_req),
+    const uint64_t v[8] = {sizeof(pbx_config), sizeof(pbx_plane_desc), sizeof(pbx_tile_req),
                            sizeof(pbx_result), sizeof(pbx_batch_stats), sizeof(pbx_image_desc),
-                           sizeof(pbx_residency_stats)};
+                           sizeof(pbx_residency_stats), sizeof(pbx_spans)};
     if (!sizes || n < 0) return fail(PBX_E_BADARG, "null argument");
-    for (int i = 0; i < n && i < 7; i++) sizes[i] = v[i];
-    return 7;
+    for (int i = 0; i < n && i < 8; i++) sizes[i] = v[i];
+    return 8;
 }
 
 int pbx_test_huffman(pbx_ctx* ctx, const uint32_t* hist, const uint32_t* sl_last, uint32_t nseg,

@@ -24,6 +24,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+import time
 from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -113,6 +114,12 @@ class PbxBatchStats(ctypes.Structure):
                   "ms_lz77", "ms_huff", "ms_encode")] + [("blocks", ctypes.c_uint64)]
 
 
+class PbxSpans(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in
+                ("get_tile_direct_ms", "write_image_ms", "create_metadata_ms", "batch_ms", "d2h_ms")] + \
+               [("batch_tiles", ctypes.c_uint64)]
+
+
 # Every symbol include/pbx.h declares (tests check the library exports all of them).
 EXPORTS = [
     "pbx_config_default", "pbx_init", "pbx_shutdown", "pbx_last_error", "pbx_abi_version",
@@ -128,7 +135,7 @@ EXPORTS = [
     "pbx_plane_write_rows", "pbx_plane_commit", "pbx_plane_lookup", "pbx_set_residency_budget",
     "pbx_residency_stats_get", "pbx_test_fail_batch", "pbx_node_init", "pbx_node_shutdown",
     "pbx_node_size", "pbx_node_context", "pbx_node_route", "pbx_node_get_tile",
-    "pbx_plane_create_sparse", "pbx_band_write", "pbx_plane_band_info",
+    "pbx_plane_create_sparse", "pbx_band_write", "pbx_plane_band_info", "pbx_result_spans",
 ]
 
 _lib = None
@@ -212,6 +219,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_node_route.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(i32)]
     L.pbx_node_get_tile.argtypes = [vp, ctypes.POINTER(PbxTileReq), ctypes.POINTER(PbxResult),
                                     ctypes.POINTER(i32)]
+    L.pbx_result_spans.argtypes = [ctypes.POINTER(PbxResult), ctypes.POINTER(PbxSpans)]
     _lib = L
     return L
 
@@ -779,7 +787,6 @@ class PixelsService:
         (TileRequestHandler.java:86,107-109,201-211): declare the image, create the plane (or
         only `band` = (y0, rows) of it), stream its rows from `source` in bands of about
         `band_bytes`, commit.  If another caller is loading the same key, wait for it."""
-        import time
         self.declare_image(pixels)
         key = (pixels.image_id, z, c, t, level)
         with self._exclusive(key):
@@ -819,7 +826,6 @@ class PixelsService:
         the sparse plane of the key (created if absent, bands of self.sparse_band_rows rows) gets
         the bands that rows [y, y + h) cover, each read from `source` once; bands another
         caller is loading are waited for.  Returns the plane id."""
-        import time
         self.declare_image(pixels)
         key = (pixels.image_id, z, c, t, level)
         sx, sy = source.level_size(pixels, level)
@@ -889,7 +895,10 @@ class PixelsService:
 
     # One getTile (pbx_get_tile): safe to call from many threads at once; concurrent
     # calls are coalesced into batches by the library (ctypes releases the GIL).
-    def get_tile(self, ctx: TileCtx) -> Tuple[int, Optional[bytes]]:
+    def get_tile(self, ctx: TileCtx, spans: Optional[dict] = None) -> Tuple[int, Optional[bytes]]:
+        """(status, body).  ``spans``: a dict that receives the serving batch's stage timings
+        (pbx_result_spans: get_tile_direct_ms, write_image_ms, create_metadata_ms, batch_ms,
+        d2h_ms, batch_tiles) when the request has a body."""
         req = ctx.to_req()
         res = PbxResult()
         lib().pbx_get_tile(self._h, ctypes.byref(req), ctypes.byref(res))
@@ -897,6 +906,10 @@ class PixelsService:
             body = ctypes.string_at(res.data, res.len) if res.status == OK and res.len else (
                 b"" if res.status == OK else None)
             ctx.region["width"], ctx.region["height"] = res.w, res.h
+            if spans is not None and res.owner:
+                sp = PbxSpans()
+                if lib().pbx_result_spans(ctypes.byref(res), ctypes.byref(sp)) == OK:
+                    spans.update({f: getattr(sp, f) for f, _ in PbxSpans._fields_})
         finally:
             lib().pbx_results_release(self._h, ctypes.byref(res), 1)
         return res.status, body
@@ -1154,11 +1167,34 @@ class TileRequestHandler:
     LOAD_ATTEMPTS = 4
 
     def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx,
-                 source: Optional[PixelSource] = None, band: Optional[Tuple[int, int]] = None):
+                 source: Optional[PixelSource] = None, band: Optional[Tuple[int, int]] = None,
+                 tracer=None):
+        """``tracer``: optional ``tracer(name, ms, tags)`` called with the reference's span
+        names (TileRequestHandler.java:81 get_tile, :104 get_tile_direct, :147 create_metadata,
+        :180 write_image; :84 get_pixels and getTileDirect reads of a cold plane as
+        get_pixels / load_region): the device stages are those of the batch that served the
+        request (pbx_result_spans), get_tile is this call's wall time."""
         self.pixels_service = pixels_service
         self.tile_ctx = tile_ctx
         self.source = source
         self.band = band
+        self.tracer = tracer
+
+    def _span(self, name: str, ms: float, **tags) -> None:
+        if self.tracer is not None:
+            self.tracer(name, ms, tags)
+
+    def _serve(self):
+        """One pbx_get_tile with the batch's stage spans."""
+        sp = {} if self.tracer is not None else None
+        status, body = self.pixels_service.get_tile(self.tile_ctx, sp)
+        if sp:
+            tags = {"batch_tiles": sp["batch_tiles"]}
+            self._span("get_tile_direct", sp["get_tile_direct_ms"], **tags)
+            self._span("create_metadata", sp["create_metadata_ms"], **tags)
+            self._span("write_image", sp["write_image_ms"], **tags)
+            self._span("d2h", sp["d2h_ms"], **tags)
+        return status, body
 
     @staticmethod
     def _answer(status: int, body: Optional[bytes]) -> Optional[bytes]:
@@ -1170,11 +1206,20 @@ class TileRequestHandler:
         return body if status == OK else None
 
     def get_tile(self, client=None) -> Optional[bytes]:
+        t0 = time.perf_counter()
+        try:
+            return self._get_tile()
+        finally:
+            self._span("get_tile", (time.perf_counter() - t0) * 1e3)
+
+    def _get_tile(self) -> Optional[bytes]:
         svc, tc = self.pixels_service, self.tile_ctx
-        status, body = svc.get_tile(tc)
+        status, body = self._serve()
         if status != E_NOT_RESIDENT or self.source is None:
             return self._answer(status, body)
+        t1 = time.perf_counter()
         pixels = self.source.get_pixels(tc.imageId)
+        self._span("get_pixels", (time.perf_counter() - t1) * 1e3)
         if pixels is None:
             return None  # :130-132 "Cannot find Image"
         level = 0
@@ -1188,11 +1233,13 @@ class TileRequestHandler:
         if self.band is not None and not (self.band[0] <= y and y + h <= self.band[0] + self.band[1]):
             return None  # rows of another context's band
         for _ in range(self.LOAD_ATTEMPTS):
+            t1 = time.perf_counter()
             if svc.sparse_band_rows:
                 svc.load_bands(self.source, pixels, tc.z, tc.c, tc.t, level, y, h, own=self.band)
             else:
                 svc.load_plane(self.source, pixels, tc.z, tc.c, tc.t, level, self.band)
-            status, body = svc.get_tile(tc)
+            self._span("load_region", (time.perf_counter() - t1) * 1e3)
+            status, body = self._serve()
             if status != E_NOT_RESIDENT:
                 return self._answer(status, body)
         raise PbxError(E_INTERNAL, "Image:%d z=%d c=%d t=%d: the plane could not be held resident "

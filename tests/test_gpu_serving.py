@@ -112,6 +112,40 @@ def test_cold_image_404s_load_nothing(service, oracle):
     service.release_image(iid)
 
 
+def test_stage_spans_under_the_reference_names(service, oracle):
+    """The reference's tracing spans (TileRequestHandler.java:81 get_tile, :104 get_tile_direct,
+    :147 create_metadata, :180 write_image): a cold PNG request records get_pixels and the
+    region load, then the serving batch's device stages; a raw request's gather is its
+    get_tile_direct, a PNG's is inside write_image."""
+    iid = next(_ids)
+    src = CountingSource(oracle, {iid: pbx.Pixels(iid, pbx.UINT16, 1500, 900)})
+    seen = []
+    tracer = lambda name, ms, tags: seen.append((name, ms, tags))
+    tc = pbx.TileCtx(iid, 0, 0, 0, 64, 32, 512, 256, format="png")
+    body = pbx.TileRequestHandler(service, tc, src, tracer=tracer).get_tile()
+    r, px, _ = oracle.png_decode(body)
+    assert r == 0 and px == oracle.gen_region(NOISE, pbx.UINT16, 64, 32, 512, 256, seed=11).tobytes()
+    names = [n for n, _, _ in seen]
+    assert names[-1] == "get_tile" and {"get_pixels", "load_region", "get_tile_direct",
+                                        "create_metadata", "write_image", "d2h"} <= set(names)
+    sp = {n: (ms, t) for n, ms, t in seen}
+    assert sp["write_image"][0] > 0 and sp["create_metadata"][0] >= 0
+    assert sp["write_image"][1]["batch_tiles"] >= 1
+    assert sp["get_tile"][0] >= sp["write_image"][0]
+    seen.clear()
+    tc = pbx.TileCtx(iid, 0, 0, 0, 0, 0, 256, 256)
+    body = pbx.TileRequestHandler(service, tc, src, tracer=tracer).get_tile()
+    assert body == oracle.gen_region(NOISE, pbx.UINT16, 0, 0, 256, 256, seed=11).tobytes()
+    sp = {n: ms for n, ms, _ in seen}
+    assert "get_pixels" not in sp and sp["get_tile_direct"] > 0 and sp["write_image"] < 0.05
+    # an error status has no body and no batch spans
+    seen.clear()
+    assert pbx.TileRequestHandler(service, pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64, format="jpg"),
+                                  src, tracer=tracer).get_tile() is None
+    assert [n for n, _, _ in seen] == ["get_tile"]
+    service.release_image(iid)
+
+
 def test_eviction_between_load_and_retry_is_never_404(oracle):
     """a budget that holds ONE plane and concurrent requests to two planes: a plane
     evicted between its load and the retry is loaded again; every tile is served exactly, none

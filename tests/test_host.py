@@ -26,12 +26,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_struct_sizes_match_bindings():
-    sizes = (ctypes.c_uint64 * 7)()
-    assert pbx.lib().pbx_abi_sizes(sizes, 7) == 7
+    sizes = (ctypes.c_uint64 * 8)()
+    assert pbx.lib().pbx_abi_sizes(sizes, 8) == 8
     assert list(sizes) == [ctypes.sizeof(t) for t in (pbx.PbxConfig, pbx.PbxPlaneDesc,
                                                       pbx.PbxTileReq, pbx.PbxResult,
                                                       pbx.PbxBatchStats, pbx.PbxImageDesc,
-                                                      pbx.PbxResidencyStats)]
+                                                      pbx.PbxResidencyStats, pbx.PbxSpans)]
 
 
 def test_jni_shim_matches_abi():
@@ -50,7 +50,7 @@ def test_jni_shim_matches_abi():
 
 def test_enums_and_names():
     L = pbx.lib()
-    assert L.pbx_abi_version() == 7
+    assert L.pbx_abi_version() == 8
     assert L.pbx_format_from_string(None) == pbx.FMT_RAW
     assert L.pbx_format_from_string(b"png") == pbx.FMT_PNG
     assert L.pbx_format_from_string(b"tif") == pbx.FMT_TIF
