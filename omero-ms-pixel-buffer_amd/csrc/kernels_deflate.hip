@@ -950,27 +950,28 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             last_end = 0;
         }
     };
-    if (active && !skip) walk(0);
     // Matches cross the wave boundaries (ph_parse_emu: wave w parses from where wave w - 1's last
-    // match ends).  Every wave walked from its own start; a wave whose predecessor's FINAL last
-    // match runs into it walks again from that match's end, in wave order.  Only segments where
-    // some wave's match ran past its sub-segment need that (runs: G_FAKE; noise: almost never).
-    if (lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
-    __syncthreads();
-    uint32_t any = 0;
-#pragma unroll
-    for (int j = 0; j + 1 < C::NW; j++) any |= S.w_end[j];
-    if (__builtin_amdgcn_readfirstlane(any)) {
+    // match ends).  Round 0: every wave walks from its own start.  A wave whose predecessor's
+    // FINAL last match runs into it walks again from that match's end, in wave order (round j:
+    // wave j).  Only segments where some wave's match ran past its sub-segment need the rounds
+    // (runs: G_FAKE; noise: almost never).  (One call site of the walk: its registers once.)
 #pragma unroll 1
-        for (uint32_t j = 1; j < (uint32_t)C::NW; j++) {
-            if (w == j) {
-                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
-                if (c > ss) {
-                    if (!skip) walk(c - ss);
-                    if (lane == 0) S.w_end[j] = last_end > se ? last_end : 0u;
-                }
-            }
-            __syncthreads();
+    for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
+        uint32_t o0 = 0;
+        bool go = j == 0 && active && !skip;
+        if (j > 0 && w == j) {
+            const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
+            go = c > ss && !skip;
+            o0 = c - ss;
+        }
+        if (go) walk(o0);
+        if ((j == 0 || go) && lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
+        __syncthreads();
+        if (j == 0) {
+            uint32_t any = 0;
+#pragma unroll
+            for (int q = 0; q + 1 < C::NW; q++) any |= S.w_end[q];
+            if (__builtin_amdgcn_readfirstlane(any) == 0) break;
         }
     }
     // the positions [ss, c) the previous wave's last match covers are not literals here
