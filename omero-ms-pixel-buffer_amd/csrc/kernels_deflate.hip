@@ -1721,13 +1721,16 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         const uint32_t eb = i < 288 ? (i > 256 ? len_sym_ebits(i) : 0u) : dist_sym_ebits(i < 318 ? i - 288 : 0);
         cost[j] = skip ? 0u : L + eb;
     }
+#ifndef PBX_HUFF_ONEREAD
+#define PBX_HUFF_ONEREAD 0  // timing bound only (variant build): no second histogram read, wrong output
+#endif
     for (uint32_t k0 = 0; k0 < nsg; k0 += HUFF_LDSEG) {
         uint32_t hr[HUFF_LDSEG][5];
 #pragma unroll
         for (uint32_t k = 0; k < HUFF_LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++)
-                hr[k][j] = k0 + k < nsg ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+                hr[k][j] = k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : k;
 #pragma unroll
         for (uint32_t k = 0; k < HUFF_LDSEG; k++) {
             uint32_t d = 0;
@@ -2597,6 +2600,6 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
 // OUT=lib).
 #if !defined(PBX_TIMING_VARIANT) && (PBX_LZ_SKIP_STORE || PBX_LZ_SKIP_FILL || PBX_LZ_SKIP_HIST || \
     PBX_LZ_SKIP_OUT || PBX_ENC_SKIP_WRITE || PBX_ENC_SKIP_PATCH || PBX_ENC_SKIP_CRC || PBX_ENC_SKIP_STORE || \
-    defined(PBX_LZ_FAKE_LOAD))
-#error "output-changing timing knobs (PBX_LZ_SKIP_*, PBX_ENC_SKIP_*, PBX_LZ_FAKE_LOAD) need a variant build (-DPBX_TIMING_VARIANT, OUT=lib/var_*)"
+    PBX_HUFF_ONEREAD || defined(PBX_LZ_FAKE_LOAD))
+#error "output-changing timing knobs (PBX_LZ_SKIP_*, PBX_ENC_SKIP_*, PBX_HUFF_ONEREAD, PBX_LZ_FAKE_LOAD) need a variant build (-DPBX_TIMING_VARIANT, OUT=lib/var_*)"
 #endif

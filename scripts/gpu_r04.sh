@@ -2,6 +2,9 @@
 #   tests    the round's new -m gpu tests (serving, sparse planes, JNI on the real library, residency)
 #   gputest  the whole -m gpu suite + smoke
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
+#   fvar     the PNG filter kernels of the var_f3* builds
+#   cvar     the deflate chain of the chain variant builds (k_huff one read, k_encode from the plane,
+#            k_lz77 without its stream store) next to the product library
 #   pmcf     PMC passes of k_filter3 (Sub, Paeth, adaptive): issue + traffic
 #   pmc      PMC passes of the headline deflate chain (scripts/pmc_run.sh, filter passes off)
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
@@ -31,10 +34,19 @@ for stage in "$@"; do
       timeout -k 10 300 python -u scripts/filter_bench.py 1 2 3 4 5 > $O/filter.log 2>&1 || { tail -30 $O/filter.log; exit 1; }
       cat $O/filter.log ;;
     fvar)
-      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_*/libpbx.so; do
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_f3*/libpbx.so; do
         echo "-- $L"
         PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/filter_bench.py 1 2 4 5 > $O/fvar.log 2>&1 || { tail -20 $O/fvar.log; exit 1; }
         cat $O/fvar.log
+      done ;;
+    cvar)
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_huff1/libpbx.so \
+               omero-ms-pixel-buffer_amd/lib/var_encplane/libpbx.so omero-ms-pixel-buffer_amd/lib/var_lznostore/libpbx.so; do
+        for g in noise fake; do
+          echo "-- $L $g"
+          PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/prof_workload.py $g 6 > $O/cvar.log 2>&1 || { tail -20 $O/cvar.log; exit 1; }
+          tail -2 $O/cvar.log
+        done
       done ;;
     pmcf)
       for f in 1 4 5; do
