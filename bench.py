@@ -515,6 +515,25 @@ def c5_shard(reqs, rank, world):
     return [i for i, c in enumerate(reqs) if world == 1 or pbx.shard_of(c, world) == rank]
 
 
+def zlib6_sample(svc, pid, n=16):
+    """The IDAT zlib stream of n grid tiles (512x512 uint16 PNG, filter None) against zlib
+    level 6 of the same scanlines (java.util.zip.Deflater's default, the reference's ImageIO
+    PNG writer): bytes per tile both ways and the ratio."""
+    import zlib
+    import numpy as np
+    sample = [pbx.TileCtx(pid, 0, 0, 0, (j * 7 % GRID) * TILE, (j * 5 % GRID) * TILE, TILE, TILE)
+              for j in range(n)]
+    raw = [b for _, b in svc.get_tiles(sample)]
+    png = [b for _, b in svc.get_tiles([pbx.TileCtx(pid, 0, 0, 0, c.region["x"], c.region["y"], TILE, TILE,
+                                                    format="png") for c in sample])]
+    z6 = sum(len(zlib.compress(np.concatenate([np.zeros((TILE, 1), np.uint8),
+                                               np.frombuffer(b, np.uint8).reshape(TILE, 2 * TILE)], 1).tobytes(), 6))
+             for b in raw)
+    mine = sum(int.from_bytes(b[91:95], "big") for b in png)  # the single IDAT's length field
+    return {"tiles": n, "idat_bytes_per_tile": round(mine / n, 1), "zlib6_bytes_per_tile": round(z6 / n, 1),
+            "ratio": round(mine / z6, 4)}
+
+
 def adaptive_filter_line(svc, rank, world, barrier, side):
     """PNG with the adaptive per-row filter (cfg.png_filter = ADAPTIVE: k_filter picks
     None/Sub/Up/Avg/Paeth per row by minimum sum |residual|), on G_NOISE, G_FAKE and a
@@ -666,7 +685,8 @@ def extra(out, svc, rank, world, barrier, iid, side):
     dtf, sf, _ = secondary_steps(svc, fk, 3, 2, barrier)
     out["png_fake_4096x512x512_u16"] = {
         "tiles_per_s": round(len(fk) * 3 * world / dtf, 1), **wall_vs_kernels(dtf, 3, sf),
-        "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1)}
+        "compressed_bytes_per_tile": round(sf[-1].deflate_out_bytes / len(fk), 1),
+        "vs_zlib6": zlib6_sample(svc, 2)}
     # the adaptive PNG filter (option; the reference writes filter None)
     progress(rank, "adaptive filter")
     out["png_adaptive_filter_512x512_u16"] = adaptive_filter_line(svc, rank, world, barrier, side)

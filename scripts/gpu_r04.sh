@@ -2,6 +2,7 @@
 #   tests    the round's new -m gpu tests (serving, sparse planes, JNI on the real library, residency)
 #   gputest  the whole -m gpu suite + smoke
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
+#   probe3   the sub-batch probe on three kernel streams (sub-batches overlap)
 #   fvar     the PNG filter kernels of the var_f3* builds
 #   cvar     the deflate chain of the chain variant builds (k_huff one read, k_encode from the plane,
 #            k_lz77 without its stream store) next to the product library
@@ -33,6 +34,9 @@ for stage in "$@"; do
       cat $O/subbatch.log | tail -6
       timeout -k 10 300 python -u scripts/filter_bench.py 1 2 3 4 5 > $O/filter.log 2>&1 || { tail -30 $O/filter.log; exit 1; }
       cat $O/filter.log ;;
+    probe3)
+      PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
+      tail -6 $O/subbatch3.log ;;
     fvar)
       for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_f3*/libpbx.so; do
         echo "-- $L"
