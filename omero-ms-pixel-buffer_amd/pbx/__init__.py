@@ -1248,18 +1248,28 @@ class TileRequestHandler:
     getTile = get_tile
 
 
-def handle_get_tile(service: PixelsService, body: str, source: Optional[PixelSource] = None):
+def handle_get_tile(service: PixelsService, body: str, source: Optional[PixelSource] = None, tracer=None):
     """PixelBufferVerticle.getTile (PixelBufferVerticle.java:90-147) over the JSON body.
 
     Returns (status, payload bytes or message, headers).  400 for an undecodable TileCtx,
-    404 when the handler returns null, 500 for any other failure.
+    404 when the handler returns null, 500 for any other failure.  ``tracer``: as
+    TileRequestHandler's, plus the consumer's own span "handle_get_tile" (:101-104).
     """
+    t0 = time.perf_counter()
+    try:
+        return _handle_get_tile(service, body, source, tracer)
+    finally:
+        if tracer is not None:
+            tracer("handle_get_tile", (time.perf_counter() - t0) * 1e3, {})
+
+
+def _handle_get_tile(service, body, source, tracer):
     try:
         ctx = TileCtx.from_json(body)
     except Exception:
         return 400, b"Illegal tile context", {}
     try:
-        tile = TileRequestHandler(service, ctx, source).get_tile()
+        tile = TileRequestHandler(service, ctx, source, tracer=tracer).get_tile()
     except PbxError as e:
         return (400 if e.status == E_BADARG else 500), b"Exception while retrieving tile", {}
     if tile is None:

@@ -143,6 +143,11 @@ def test_stage_spans_under_the_reference_names(service, oracle):
     assert pbx.TileRequestHandler(service, pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64, format="jpg"),
                                   src, tracer=tracer).get_tile() is None
     assert [n for n, _, _ in seen] == ["get_tile"]
+    # the event-bus consumer's own span closes the request
+    seen.clear()
+    st, _, _ = pbx.handle_get_tile(service, pbx.TileCtx(iid, 0, 0, 0, 0, 0, 128, 128).to_json(), src,
+                                   tracer=tracer)
+    assert st == 200 and [n for n, _, _ in seen][-2:] == ["get_tile", "handle_get_tile"]
     service.release_image(iid)
 
 
