@@ -149,15 +149,12 @@ def load_traffic(kernel):
     (profiles/*pmc*/traffic.json, written by scripts/pmc_summary.py: FETCH_SIZE doubled
     per the gfx950 rule + WRITE_SIZE, same workload as this bench's batch)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "traffic.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        t = json.load(f)
-    k = t.get("kernels", {}).get(kernel)
-    if not k:
-        return None, None
-    return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(files[-1], ROOT)
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "traffic.json")), reverse=True):
+        with open(fn) as f:
+            k = json.load(f).get("kernels", {}).get(kernel)
+        if k:  # the latest pass that profiled this kernel (filter-only passes hold no k_encode)
+            return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(fn, ROOT)
+    return None, None
 
 
 def load_issue(kernels=("k_encode", "k_lz77")):
@@ -165,17 +162,15 @@ def load_issue(kernels=("k_encode", "k_lz77")):
     (profiles/*pmc*/issue.json, scripts/pmc_summary.py: VALU busy = 2 cycles per wave64 VALU
     instruction per SIMD-cycle, SALU busy = 1 per CU-cycle, wave-time split), same workload."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "issue.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        t = json.load(f)
-    out = {k: t["kernels"][k] for k in kernels if k in t.get("kernels", {})}
-    if not out:
-        return None
-    out["source"] = os.path.relpath(files[-1], ROOT)
-    out["rule"] = t.get("rule")
-    return out
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "issue.json")), reverse=True):
+        with open(fn) as f:
+            t = json.load(f)
+        out = {k: t["kernels"][k] for k in kernels if k in t.get("kernels", {})}
+        if out:  # the latest pass that profiled the deflate kernels
+            out["source"] = os.path.relpath(fn, ROOT)
+            out["rule"] = t.get("rule")
+            return out
+    return None
 
 
 def cpu_model():
