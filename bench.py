@@ -40,6 +40,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TILE, GRID = 512, 64
 KSTREAMS, KSTAGGER = int(os.environ.get("PBX_KSTREAMS", "3")), 1  # the library's defaults
 PIPE_DEPTH = int(os.environ.get("PBX_BENCH_DEPTH", "2"))  # batches in flight
+HEADLINE_SUB = int(os.environ.get("PBX_BENCH_SUB", "0"))  # headline sub-batch tiles (0: one batch per step)
 
 
 def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
@@ -47,35 +48,51 @@ def grid_ctxs(image_id, fmt, n=GRID * GRID, tile=TILE):
                         format=fmt) for i in range(n)]
 
 
-def run_steps(svc, ctxs, steps, warmup, barrier):
+class StepStats:
+    """pbx_batch_stats summed over the sub-batches of one step (counts, bytes and kernel ms)."""
+
+    def __init__(self, parts):
+        for f, _ in pbx.PbxBatchStats._fields_:
+            setattr(self, f, sum(getattr(p, f) for p in parts))
+
+
+def run_steps(svc, ctxs, steps, warmup, barrier, sub=0):
     """Warmup, then `steps` timed steps; returns (seconds, per-step stats, mean host ms).
 
     Steps are pipelined PIPE_DEPTH deep, as a server feeds its GPU: the host plans and
     launches batch k+1 (request validation, descriptors, upload) while earlier batches run,
-    then waits for the oldest one (its own completion event).  The request array is built
-    once."""
-    reqs = pbx.make_reqs(ctxs)
+    then waits for the oldest one (its own completion event).  The request arrays are built
+    once.  sub > 0: a step's requests go as batches of `sub` tiles (PIPE_DEPTH steps' worth
+    in flight); its stats are their sums."""
+    parts = [ctxs] if sub <= 0 else [ctxs[i:i + sub] for i in range(0, len(ctxs), sub)]
+    reqs = [pbx.make_reqs(p) for p in parts]
+    depth = PIPE_DEPTH * len(parts)
 
     def one_pass(n, record):
         q = []
         host = 0.0
         out = []
+        acc = []
 
         def retire():
             b = q.pop(0)
             b.sync()
             if record:
-                out.append(b.stats())
+                acc.append(b.stats())
+                if len(acc) == len(parts):
+                    out.append(acc[0] if len(parts) == 1 else StepStats(acc))
+                    acc.clear()
             b.close()
 
         for _ in range(n):
-            t0 = time.perf_counter()
-            b = pbx.Batch(svc, reqs=reqs)
-            b.launch()
-            host += time.perf_counter() - t0
-            q.append(b)
-            if len(q) >= PIPE_DEPTH:
-                retire()
+            for r in reqs:
+                t0 = time.perf_counter()
+                b = pbx.Batch(svc, reqs=r)
+                b.launch()
+                host += time.perf_counter() - t0
+                q.append(b)
+                if len(q) >= depth:
+                    retire()
         while q:
             retire()
         return out, host
@@ -859,7 +876,7 @@ def main():
     svc.register_plane(iid, 0, 0, 0, pbx.UINT16, side, side, generator="noise", seed=0,
                        plane_no=rank)
     ctxs = grid_ctxs(iid, "png")
-    dt, stats, host_ms = run_steps(svc, ctxs, args.steps, args.warmup, barrier)
+    dt, stats, host_ms = run_steps(svc, ctxs, args.steps, args.warmup, barrier, HEADLINE_SUB)
     t = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -875,7 +892,7 @@ def main():
     # launch order), the configuration the committed rocprofv3 kernel trace uses
     # (PBX_KSTREAMS=1); its tiles/s is reported beside the headline.
     svc.set_kernel_streams(1, 0)
-    dts, stats, _ = run_steps(svc, ctxs, args.steps, 1, barrier)
+    dts, stats, _ = run_steps(svc, ctxs, args.steps, 1, barrier, HEADLINE_SUB)
     svc.set_kernel_streams(KSTREAMS, KSTAGGER)
     serial_rate = len(ctxs) * args.steps / dts
 
@@ -911,7 +928,8 @@ def main():
                                "uint16 plane (BASELINE configs[1] shape, metric's PNG format)",
                    "tiles_per_gpu": len(ctxs), "tile": "512x512", "pixel_type": "uint16",
                    "format": "png", "png_filter": "none (reference APNGWriter)",
-                   "parallelism": f"dp{world} (request sharding, no collectives)"},
+                   "parallelism": f"dp{world} (request sharding, no collectives)",
+                   "batches_per_step": 1 if HEADLINE_SUB <= 0 else -(-len(ctxs) // HEADLINE_SUB)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
