@@ -47,6 +47,7 @@ struct LzSmem {
     uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
     uint32_t w_end[C::NW];  // a wave's last match end when it runs into the next wave (else 0)
+    uint32_t w_end0[C::NW];  // the same after round 0 (never rewritten: the rounds test)
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
     alignas(16) uint32_t h8[288 * LZ_HCOPIES];
@@ -965,12 +966,18 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
             o0 = c - ss;
         }
         if (go) walk(o0);
-        if ((j == 0 || go) && lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
+        if ((j == 0 || go) && lane == 0) {
+            S.w_end[w] = last_end > se ? last_end : 0u;
+            if (j == 0) S.w_end0[w] = last_end > se ? last_end : 0u;
+        }
         __syncthreads();
         if (j == 0) {
+            // from w_end0, which no round rewrites: a wave still reading here while a faster one
+            // already writes w_end in round 1 must reach the same decision (else the waves would
+            // run different numbers of barriers)
             uint32_t any = 0;
 #pragma unroll
-            for (int q = 0; q + 1 < C::NW; q++) any |= S.w_end[q];
+            for (int q = 0; q + 1 < C::NW; q++) any |= S.w_end0[q];
             if (__builtin_amdgcn_readfirstlane(any) == 0) break;
         }
     }

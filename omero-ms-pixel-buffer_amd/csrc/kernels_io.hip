@@ -577,8 +577,11 @@ __device__ __forceinline__ f2_s16x2 f2_abs(f2_s16x2 x) {
 // Checked against the integer rule for all 2^24 (a, b, c) byte triples.
 typedef _Float16 f3_h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_sign_mask(uint32_t y) {  // 0xFFFF per negative 16-bit lane
+    // The shift counts come from an SGPR holding 15 in BOTH halves: an inline constant 15
+    // reaches only the low lane of a packed operand (the high lane then reads its bits 31:16,
+    // 0, and was not shifted at all: wrong Paeth choices in bytes 2 and 3 on the GPU).
     uint32_t m;
-    asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(m) : "v"(y));
+    asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(m) : "s"(0x000F000Fu), "v"(y));
     return m;
 }
 __device__ __forceinline__ uint32_t paeth_pair_h(uint32_t a, uint32_t b, uint32_t c) {  // biased lanes

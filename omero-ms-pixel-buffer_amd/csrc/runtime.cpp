@@ -73,12 +73,24 @@ enum PlaneState : int {
 // TileRequestHandler.java:102-109).
 enum BandState : int { BS_ABSENT = 0, BS_LOADING = 1, BS_READY = 2 };
 
+// A plane or band that has just been loaded is not evicted until a batch has read it, or
+// FRESH_NS has passed (a loader that went away): otherwise, under a budget smaller than the
+// working set, concurrent loaders evict each other's planes between the load and the retry
+// that was to read them, and every request is loaded again and again.  A
+// loader that finds only fresh or pinned memory gets PBX_E_NO_SPACE and retries later.
+constexpr int64_t FRESH_NS = 2000000000;
+inline int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 struct Band {
     uint8_t* dev = nullptr;      // the band's rows at the plane's pitch + 256 B slack
     size_t bytes = 0;
     int state = BS_ABSENT;
     int64_t pins = 0;            // planned batches that read it
     uint64_t last_use = 0;
+    int64_t fresh_until = 0;     // loaded, not served yet: not evicted before this (fresh_now)
     uint32_t rows_left = 0;      // BS_LOADING: rows not written yet
     int32_t writers = 0;         // pbx_band_write calls in flight
     std::vector<uint8_t> rows_done;
@@ -105,6 +117,7 @@ struct Plane {
     bool indexed = false;        // reachable from ctx->index (false once released)
     int64_t pins = 0;            // planned batches / running kernels that read the plane
     uint64_t last_use = 0;       // LRU tick of the last request served from it
+    int64_t fresh_until = 0;     // loaded, not served yet: not evicted before this (fresh_now)
     std::vector<uint8_t> rows_done;  // PS_FILLING host planes: which band rows were written
     uint64_t rows_left = 0;
     int32_t writers = 0;         // pbx_plane_write_rows calls in flight (commit waits for none)
@@ -461,6 +474,7 @@ int registry_insert(pbx_ctx* ctx, std::vector<Plane>& ps, uint64_t* ids) {
     }
     for (size_t k = 0; k < ps.size(); k++) {
         ps[k].state = PS_READY;
+        ps[k].fresh_until = mono_ns() + FRESH_NS;
         Plane* q = registry_add(ctx, ps[k]);
         ps[k].id = q->id;
         if (ids) ids[k] = q->id;
@@ -518,17 +532,18 @@ bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_fr
     Plane* v = nullptr;
     Band* vb = nullptr;
     uint64_t best = UINT64_MAX;
+    const int64_t now = mono_ns();
     for (auto& kv : ctx->planes) {
         Plane* p = kv.second;
         if (!p->indexed || p->state != PS_READY) continue;
         if (p->sparse_rows) {
             for (Band& b : p->bands)
-                if (b.state == BS_READY && b.pins == 0 && b.dev && b.last_use < best) {
+                if (b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now && b.last_use < best) {
                     best = b.last_use;
                     v = p;
                     vb = &b;
                 }
-        } else if (p->pins == 0 && p->dev && p->last_use < best) {
+        } else if (p->pins == 0 && p->dev && p->fresh_until <= now && p->last_use < best) {
             best = p->last_use;
             v = p;
             vb = nullptr;
@@ -554,13 +569,14 @@ bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_fr
 // Bytes an eviction could return now (idle planes and idle bands), under reg_mu.
 uint64_t idle_bytes_locked(pbx_ctx* ctx) {
     uint64_t idle = 0;
+    const int64_t now = mono_ns();
     for (auto& kv : ctx->planes) {
         const Plane* p = kv.second;
         if (!p->indexed || p->state != PS_READY) continue;
         if (p->sparse_rows) {
             for (const Band& b : p->bands)
-                if (b.state == BS_READY && b.pins == 0 && b.dev) idle += b.bytes;
-        } else if (p->pins == 0 && p->dev) {
+                if (b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now) idle += b.bytes;
+        } else if (p->pins == 0 && p->dev && p->fresh_until <= now) {
             idle += p->bytes;
         }
     }
@@ -718,6 +734,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*
         for (int32_t k = k0; k <= k1; k++) {
             p->bands[(size_t)k].pins++;
             p->bands[(size_t)k].last_use = tick;
+            p->bands[(size_t)k].fresh_until = 0;
         }
     } else if (kr) {
         kr[0] = kr[1] = -1;
@@ -725,6 +742,7 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*
     if (!pin) return PBX_OK;
     p->pins++;
     p->last_use = ++ctx->use_tick;
+    p->fresh_until = 0;
     plane = p;
     return PBX_OK;
 }
@@ -1305,6 +1323,7 @@ int plane_create(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t y0, int32_t nrow
     if (d->source != PBX_SRC_HOST) {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         q->state = PS_READY;
+        q->fresh_until = mono_ns() + FRESH_NS;
     }
     *out = q;
     return PBX_OK;
@@ -1358,6 +1377,7 @@ int plane_commit(pbx_ctx* ctx, Plane* q) {
     q->rows_done.shrink_to_fit();
     q->state = PS_READY;
     q->last_use = ++ctx->use_tick;
+    q->fresh_until = mono_ns() + FRESH_NS;
     return PBX_OK;
 }
 
@@ -1551,6 +1571,7 @@ int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* dat
         b.rows_done.shrink_to_fit();
         b.state = BS_READY;
         b.last_use = ++ctx->use_tick;
+        b.fresh_until = mono_ns() + FRESH_NS;
     }
     return PBX_OK;
 }

@@ -1165,6 +1165,17 @@ class TileRequestHandler:
     context is a closed registry: not resident -> None (404)."""
 
     LOAD_ATTEMPTS = 4
+    NO_SPACE_WAIT_S = 30.0
+
+    def _never_fits(self, pixels: "Pixels", level: int) -> bool:
+        """The plane (or one band of it) is larger than the whole residency budget."""
+        budget = self.pixels_service.residency_stats()["budget"]
+        if not budget:
+            return False
+        sx, sy = self.source.level_size(pixels, level)
+        rows = self.pixels_service.sparse_band_rows or sy
+        pitch = (sx * BYTES_PER_PIXEL[pixels.pixel_type] + 255) // 256 * 256
+        return pitch * min(rows, sy) + 256 > budget
 
     def __init__(self, pixels_service: PixelsService, tile_ctx: TileCtx,
                  source: Optional[PixelSource] = None, band: Optional[Tuple[int, int]] = None,
@@ -1232,12 +1243,23 @@ class TileRequestHandler:
         y, h = tc.y, (tc.h or pixels.size_y)  # :92-97 defaulting from the full-resolution size
         if self.band is not None and not (self.band[0] <= y and y + h <= self.band[0] + self.band[1]):
             return None  # rows of another context's band
-        for _ in range(self.LOAD_ATTEMPTS):
+        attempts, deadline = 0, time.monotonic() + self.NO_SPACE_WAIT_S
+        while attempts < self.LOAD_ATTEMPTS:
             t1 = time.perf_counter()
-            if svc.sparse_band_rows:
-                svc.load_bands(self.source, pixels, tc.z, tc.c, tc.t, level, y, h, own=self.band)
-            else:
-                svc.load_plane(self.source, pixels, tc.z, tc.c, tc.t, level, self.band)
+            try:
+                if svc.sparse_band_rows:
+                    svc.load_bands(self.source, pixels, tc.z, tc.c, tc.t, level, y, h, own=self.band)
+                else:
+                    svc.load_plane(self.source, pixels, tc.z, tc.c, tc.t, level, self.band)
+            except PbxError as e:
+                # the budget is held by planes other requests are reading or have just loaded
+                # (the library keeps a fresh plane until its first read): wait for them, unless
+                # the plane could never fit
+                if e.status != E_NO_SPACE or time.monotonic() > deadline or self._never_fits(pixels, level):
+                    raise
+                time.sleep(0.002)
+                continue
+            attempts += 1
             self._span("load_region", (time.perf_counter() - t1) * 1e3)
             status, body = self._serve()
             if status != E_NOT_RESIDENT:

@@ -42,7 +42,7 @@ def _streams():
 def test_gpu_lz77_matches_emulator(service, case):
     name, pt, a = _streams()[case]
     h, w = a.shape
-    iid = 9100 + case
+    iid = 9_500_000 + case
     if name.endswith("512"):  # little-endian plane: the byte-swapping fill (the headline's)
         service.register_plane(iid, 0, 0, 0, pt, w, h, data=a.astype("<u2"), big_endian=False)
     else:

@@ -23,7 +23,7 @@ import _emu
 
 pytestmark = pytest.mark.gpu
 
-_ids = itertools.count(700000, 10)
+_ids = itertools.count(650000, 10)  # disjoint from test_gpu_sweep (700000..)
 FAKE, NOISE = 1, 2
 
 
@@ -178,7 +178,9 @@ def test_eviction_between_load_and_retry_is_never_404(oracle):
         with ThreadPoolExecutor(16) as ex:
             outcomes = list(ex.map(one, ctxs))
         assert not errors, errors[:4]
-        assert outcomes.count("ok") >= len(ctxs) - 8  # at most a few give up after 4 loads
+        # a loaded plane is kept until its first read (the library's fresh protection) and a
+        # loader that finds the budget held waits: (almost) nothing is given up
+        assert outcomes.count("ok") >= len(ctxs) - 2, outcomes
         assert svc.residency_stats()["evictions"] >= 1
 
 
