@@ -59,11 +59,16 @@ def test_gpu_lz77_matches_emulator(service, case):
     stream = b"".join(b"\x00" + raw[r * w * bpp:(r + 1) * w * bpp] for r in range(h))
     eh, em = _emu.lz77(stream, 1 + w * bpp)
     assert gh.shape == eh.shape
+    nw = L.pbxemu_threads() // 64
+
+    def records(m, wv):  # (position, length, distance) of wave wv's kept matches
+        n = int(m[wv])
+        return [(int(m[nw + wv * 256 + j]) & 0xFFFF, (int(m[nw + wv * 256 + j]) >> 16) + 3,
+                 int(m[nw + nw * 256 + wv * 256 + j]) + 1) for j in range(n)]
+
     for k in range(nseg):
-        assert (gh[k] == eh[k]).all(), (name, k, np.nonzero(gh[k] != eh[k])[0][:8])
-        nw = L.pbxemu_threads() // 64
-        assert (gm[k][:nw] == em[k][:nw]).all(), (name, k)
-        for wv in range(nw):
-            n = int(em[k][wv])
-            for off in (nw + wv * 256, nw + nw * 256 + wv * 256):
-                assert (gm[k][off:off + n] == em[k][off:off + n]).all(), (name, k, wv)
+        for wv in range(nw):  # the match records first: they say where a difference starts
+            g, e = records(gm[k], wv), records(em[k], wv)
+            assert g == e, (name, k, wv, [x for x in g if x not in e][:4], [x for x in e if x not in g][:4])
+        assert (gh[k] == eh[k]).all(), (name, k, np.nonzero(gh[k] != eh[k])[0][:8],
+                                        gh[k][gh[k] != eh[k]][:8], eh[k][gh[k] != eh[k]][:8])
