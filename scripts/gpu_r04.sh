@@ -34,6 +34,10 @@ for stage in "$@"; do
       cat $O/subbatch.log | tail -6
       timeout -k 10 300 python -u scripts/filter_bench.py 1 2 3 4 5 > $O/filter.log 2>&1 || { tail -30 $O/filter.log; exit 1; }
       cat $O/filter.log ;;
+    lz77)  # the LZ77 parity test alone; its failure is reported, the later stages still run
+      timeout -k 10 300 $PYT tests/test_gpu_lz77.py > $O/pytest_lz77.log 2>&1; rc=$?
+      [ $rc -eq 124 ] || [ $rc -eq 137 ] && { tail -20 $O/pytest_lz77.log; exit 1; }
+      grep -E "^E  |passed|failed" $O/pytest_lz77.log | head -20 ;;
     probe3)
       PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
       tail -6 $O/subbatch3.log ;;
