@@ -46,8 +46,10 @@ struct LzSmem {
     alignas(16) uint32_t buf[C::BUFW];
     uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    uint32_t w_end[C::NW];  // a wave's last match end when it runs into the next wave (else 0)
-    uint32_t w_end0[C::NW];  // the same after round 0 (never rewritten: the rounds test)
+    // a wave's last match end when it runs into the next wave (else 0), and whether the wave
+    // walked again, per carry round (double-buffered: round r reads round r - 1's)
+    uint32_t w_endb[2][C::NW];
+    uint32_t w_chg[2][C::NW];
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
     alignas(16) uint32_t h8[288 * LZ_HCOPIES];
@@ -721,7 +723,7 @@ __device__ __forceinline__ uint32_t pack_zero_bytes8(const uint32_t (&x)[8]) {
 // wave-wide extension of a capped match.  Each lane also collects the positions of its
 // chunk covered by recorded matches (cover), for the histogram.
 template <class C, class SM>
-__device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uint32_t (&cw)[9],
+__device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uint32_t (&cw)[9],
                              uint32_t& cover, uint32_t& smask) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t ss = w * C::SUB;
@@ -737,7 +739,6 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         const uint32_t nval = se > p0 ? se - p0 : 0u;
         smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
         uint32_t cvb_lo = 0, cvb_hi = 0;  // bytes inside some paying run (the walk's coverage bound, below)
-        uint32_t elast = 0;               // some candidate's equality bit at the sub-segment's last byte
 #pragma unroll
         for (int c = 0; c < NCAND; c++) {
             const uint32_t d = __builtin_amdgcn_readfirstlane(cand_dist(sp, c));
@@ -821,7 +822,6 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                 if (ml[c] >= 6) { dlo |= (r << 4) | (r << 5); dhi |= (r >> 28) | (r >> 27); }
                 cvb_lo |= dlo;
                 cvb_hi |= dhi;
-                elast |= e;
             }
         }
 #ifndef PBX_LZ_COVBOUND
@@ -834,9 +834,14 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         // an overestimate), and below MINCOV the walk would drop all its matches (noise: most
         // waves hold a few 3-4 byte runs): the same result without the walk.  A match that reaches
         // the sub-segment's last byte may run on into the next one (extend_cross), past that
-        // count: the bound then does not hold, and the wave walks.
+        // count: the bound then does not hold, and the wave walks.  Such a match lies in a run of
+        // >= ml equal bytes ending at the last byte, so se - ml is a paying start and the last
+        // byte is in the union above (this lane's bits, or the previous lane's bits past its
+        // chunk): exactly the waves where a paying run reaches the last byte walk.
         const uint32_t tl = (se - 1 - ss) >> 5, il = (se - 1 - ss) & 31;
-        const bool reach = (((uint32_t)__builtin_amdgcn_readlane(elast, tl) >> il) & 1u) != 0 && se < sp.sl;
+        const uint32_t in_lo = (uint32_t)__builtin_amdgcn_readlane(cvb_lo, tl) >> il;
+        const uint32_t in_hi = tl ? (uint32_t)__builtin_amdgcn_readlane(cvb_hi, tl - 1) >> il : 0u;
+        const bool reach = ((in_lo | in_hi) & 1u) != 0 && se < sp.sl;
         skip = PBX_LZ_COVBOUND && !reach &&
                wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) <
                    (uint32_t)C::MINCOV;
@@ -899,12 +904,17 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                 const uint32_t a = sp.wl + p, off = L + 4 * lane;
                 const uint32_t x = off < lim ? (lds_ld4(S, a - D + off) ^ lds_ld4(S, a + off)) : 0u;
                 const uint64_t mm = __ballot(off >= lim || x != 0);
-                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-                const uint32_t xf = __builtin_amdgcn_readlane(x, f);
-                const uint32_t of = L + 4 * f;
-                const uint32_t l = of >= lim ? lim : of + ((uint32_t)__builtin_ctz(xf | 0x80000000u) >> 3);
+                // no lane stopped: the 256 bytes from L are all equal (L < 6 reaching lim = 258
+                // from a sub-segment's last bytes), so the match runs to lim (ctz of 0 is no index)
+                uint32_t l = lim;
+                if (mm) {
+                    const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+                    const uint32_t of = L + 4 * f;
+                    if (of < lim) l = of + ((uint32_t)__builtin_ctz(__builtin_amdgcn_readlane(x, f) | 0x80000000u) >> 3);
+                }
                 L = __builtin_amdgcn_readfirstlane(l < lim ? l : lim);
             };
+            uint32_t runk = 0;  // the chosen candidate's run of equal bytes from k (mask extension)
             if (PBX_LZ_MASKEXT && C::CAP == 32 && L >= (uint32_t)C::CAP && L < maxlen) {
                 // the run of the chosen candidate's equality bits from position k over the wave's
                 // masks: the rest of lane t, the whole lanes after it (a ballot of all-ones masks),
@@ -920,6 +930,7 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                     run += 32 * nf;
                     if (t2 < 64) run += (uint32_t)__builtin_ctz(~(uint32_t)__builtin_amdgcn_readlane(es, t2));
                 }
+                runk = __builtin_amdgcn_readfirstlane(run);
                 L = __builtin_amdgcn_readfirstlane(run < maxlen ? run : maxlen);
             } else if (L >= (uint32_t)C::CAP && L < maxlen) {
                 extend_lds(maxlen);
@@ -930,19 +941,48 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
                 const uint32_t lim = r2 < 258 ? r2 : 258;
                 if (L < lim) extend_lds(lim);
             }
+            uint32_t adv = L;  // positions the recorded matches take
             if (nm < (uint32_t)C::MAXMW) {
                 if (lane == 0) S.mrl[w * C::MAXMW + nm] = (p - ss) | ((L - 3) << 11) | (Dc << 19);
                 nm++;
-                cov += L;
-                last_end = p + L;
-                // positions [p, p + L) of this lane's chunk are covered
-                const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + L - p0;
-                if (p + L > p0 && p < p0 + 32) {
+#ifndef PBX_LZ_CHAIN
+#define PBX_LZ_CHAIN 1  // full 258-byte matches down a long run recorded together (0: one per step)
+#endif
+                // A run of the chosen candidate longer than two full matches: the walk would take
+                // 258 more at k + 258 m (m = 1, 2, ...) while the run holds 258 more from there, the
+                // match stays inside the sub-segment, and no earlier candidate (which wins ties) has
+                // 32 equal bytes there -- the lazy rule cannot fire at the cap.  Lane m - 1 checks
+                // chain position m (the earlier candidates' masks fetched by ds_bpermute); the
+                // leading run of passing lanes is recorded at once (G_FAKE: a whole sub-segment in
+                // one step instead of eight).
+                if (PBX_LZ_CHAIN && L == 258 && runk >= 2 * 258) {
+                    const uint32_t m = lane + 1, km = k + 258 * m;
+                    bool ok = lane < 8 && runk >= 258 * (m + 1) && km + 258 < lsub;
+                    const uint32_t tq = km >> 5 < 63 ? km >> 5 : 63u, iq = km & 31;
+#pragma unroll
+                    for (int c = 0; c < NCAND - 1; c++) {
+                        if ((uint32_t)c >= Dc) break;  // (uniform)
+                        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * tq), (int)exlo[c]);
+                        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * tq), (int)exhi[c]);
+                        const uint64_t ex = (((uint64_t)hi << 32) | lo) >> iq;
+                        ok = ok && (uint32_t)ex != 0xFFFFFFFFu;
+                    }
+                    uint32_t nok = (uint32_t)__builtin_ctzll(~__ballot(ok));
+                    if (nok > (uint32_t)C::MAXMW - nm) nok = (uint32_t)C::MAXMW - nm;
+                    if (lane < nok) S.mrl[w * C::MAXMW + nm + lane] = km | (255u << 11) | (Dc << 19);
+                    nm += nok;
+                    adv += 258 * nok;
+                }
+                cov += adv;
+                last_end = p + adv;
+                // positions [p, p + adv) of this lane's chunk are covered
+                const uint32_t lo = p > p0 ? p - p0 : 0u, hi = p + adv - p0;
+                if (p + adv > p0 && p < p0 + 32) {
                     const uint32_t h = hi < 32 ? hi : 32u;
                     cover |= (h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u) & (0xFFFFFFFFu << lo);
                 }
             }
-            o = k + L;
+            o = k + adv;
         }
         // ph_parse_emu's rule: matches covering < MINCOV bytes are dropped (literals only)
         if (cov < (uint32_t)C::MINCOV) {
@@ -952,42 +992,44 @@ __device__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uin
         }
     };
     // Matches cross the wave boundaries (ph_parse_emu: wave w parses from where wave w - 1's last
-    // match ends).  Round 0: every wave walks from its own start.  A wave whose predecessor's
-    // FINAL last match runs into it walks again from that match's end, in wave order (round j:
-    // wave j).  Only segments where some wave's match ran past its sub-segment need the rounds
-    // (runs: G_FAKE; noise: almost never).  (One call site of the walk: its registers once.)
+    // match ends, waves in order).  Round 0: every wave walks from its own start.  Round r: every
+    // wave whose carry-in (its predecessor's carry-out after round r - 1) differs from the one
+    // its current walk started from walks again, all such waves in parallel (double-buffered
+    // carries: round r reads round r - 1's), until no carry-in changes.  After round r waves
+    // 0..r hold their final walks, so this ends with the serial parse in at most NW - 1 rounds;
+    // on G_FAKE's rows a carry-out rarely depends on the carry-in (a row start resets the match
+    // phase), so one round settles it.  Noise: almost never a round at all.
+    // (one call site of the walk: two inlined copies spill registers to scratch)
+    uint32_t used = 0, cout = 0;  // the carry-in of the wave's current walk (0: its own start), its carry-out
 #pragma unroll 1
-    for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
-        uint32_t o0 = 0;
-        bool go = j == 0 && active && !skip;
-        if (j > 0 && w == j) {
-            const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
-            go = c > ss && !skip;
-            o0 = c - ss;
+    for (uint32_t r = 0; r < (uint32_t)C::NW; r++) {
+        const uint32_t cur = r & 1u, prev = cur ^ 1u;
+        uint32_t cin = 0;
+        if (r && w) {
+            cin = __builtin_amdgcn_readfirstlane(S.w_endb[prev][w - 1]);
+            if (cin <= ss) cin = 0;
         }
-        if (go) walk(o0);
-        if ((j == 0 || go) && lane == 0) {
-            S.w_end[w] = last_end > se ? last_end : 0u;
-            if (j == 0) S.w_end0[w] = last_end > se ? last_end : 0u;
+        const bool ch = r == 0 || cin != used;
+        if (ch) {
+            used = cin;
+            if (active && !skip) walk(cin ? cin - ss : 0u);
+            cout = last_end > se ? last_end : 0u;
+        }
+        if (lane == 0) {
+            S.w_endb[cur][w] = cout;
+            S.w_chg[cur][w] = ch ? 1u : 0u;
         }
         __syncthreads();
-        if (j == 0) {
-            // from w_end0, which no round rewrites: a wave still reading here while a faster one
-            // already writes w_end in round 1 must reach the same decision (else the waves would
-            // run different numbers of barriers)
-            uint32_t any = 0;
+        // round 0: go on if some wave's match runs into the next one; later: if some wave walked
+        uint32_t more = 0;
 #pragma unroll
-            for (int q = 0; q + 1 < C::NW; q++) any |= S.w_end0[q];
-            if (__builtin_amdgcn_readfirstlane(any) == 0) break;
-        }
+        for (int q = 0; q < C::NW; q++) more |= r ? S.w_chg[cur][q] : (q + 1 < C::NW ? S.w_endb[0][q] : 0u);
+        if (__builtin_amdgcn_readfirstlane(more) == 0) break;
     }
-    // the positions [ss, c) the previous wave's last match covers are not literals here
-    if (w > 0 && active) {
-        const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[w - 1]);
-        if (c > p0) {
-            const uint32_t h = c - p0 < 32 ? c - p0 : 32u;
-            cover |= h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u;
-        }
+    // the positions [ss, used) the previous wave's last match covers are not literals here
+    if (used > p0) {
+        const uint32_t h = used - p0 < 32 ? used - p0 : 32u;
+        cover |= h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u;
     }
     // the kept matches' length and distance symbols, one match per lane (this wave's own
     // records: LDS operations of one wave complete in order)
@@ -1174,6 +1216,13 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
     }
     stamp();
+    // the chunk's words again, from LDS: not held in registers across the parse (its walk needs them)
+    uint32_t cb[8];
+    {
+        const uint4 q0 = *(const uint4*)&S.buf[wi], q1 = *(const uint4*)&S.buf[wi + 4];
+        cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
+        cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
+    }
     // literal histogram of the chunk (positions no recorded match covers), 8 interleaved
     // copies against same-address LDS atomics, branch-free: a covered position adds into the
     // lane's own sink word.  Adler-32 partial sums from the same words.
@@ -1187,14 +1236,14 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
             // noisy data): the bin address only, no per-position select
 #pragma unroll
             for (int j = 0; j < 32; j++) {
-                const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+                const uint32_t bt = (cb[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
                 atomicAdd(&S.h8[bt * LZ_HCOPIES + cp], 1u);
             }
         } else {
             const uint32_t sink = (uint32_t)(&S.hdummy[lane] - S.h8);
 #pragma unroll
             for (int j = 0; j < 32; j++) {
-                const uint32_t bt = (cw[1 + (j >> 2)] >> ((j & 3) * 8)) & 0xFFu;
+                const uint32_t bt = (cb[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
                 atomicAdd(&S.h8[((lit >> j) & 1u) ? bt * LZ_HCOPIES + cp : sink], 1u);
             }
         }
@@ -1206,7 +1255,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         n = ce - cs;
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)C::CH / 4; k++) {
-            const uint32_t v = cw[1 + k];  // bytes past the segment are zero in buf
+            const uint32_t v = cb[k];  // bytes past the segment are zero in buf
             const uint32_t e = (uint32_t)C::CH - 4 * k;
             s1 = dot4_u8(v, 0x01010101u, s1);
             s2 = dot4_u8(v, e | ((e - 1) << 8) | ((e - 2) << 16) | ((e - 3) << 24), s2);

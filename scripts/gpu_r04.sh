@@ -48,8 +48,8 @@ for stage in "$@"; do
         cat $O/fvar.log
       done ;;
     cvar)
-      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_huff1/libpbx.so \
-               omero-ms-pixel-buffer_amd/lib/var_encplane/libpbx.so omero-ms-pixel-buffer_amd/lib/var_lznostore/libpbx.so; do
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_*/libpbx.so; do
+        case $L in *var_f3*) continue ;; esac
         for g in noise fake; do
           echo "-- $L $g"
           PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/prof_workload.py $g 6 > $O/cvar.log 2>&1 || { tail -20 $O/cvar.log; exit 1; }
