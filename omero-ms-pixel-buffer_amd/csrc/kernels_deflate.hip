@@ -46,10 +46,7 @@ struct LzSmem {
     alignas(16) uint32_t buf[C::BUFW];
     uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    // a wave's last match end when it runs into the next wave (else 0), and whether the wave
-    // walked again, per carry round (double-buffered: round r reads round r - 1's)
-    uint32_t w_endb[2][C::NW];
-    uint32_t w_chg[2][C::NW];
+    uint32_t w_end[C::NW];  // a wave's last match end when it runs into the next wave (else 0)
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
     alignas(16) uint32_t h8[288 * LZ_HCOPIES];
@@ -732,6 +729,26 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     cover = 0;
     smask = 0;
     const uint32_t p0 = ss + 32 * lane, a0 = sp.wl + p0;
+    // Boundary after wave b (lane b < NW - 1): a paying run ends at that sub-segment's last byte
+    // (ml equal bytes of a candidate there, ml = match_minlen), the only way a match of wave b
+    // can run on into wave b + 1.  From the bytes alone, the same in every wave: a uniform
+    // decision, no barrier (noise: almost never; then every wave's parse is final at once).
+    uint32_t reachm;
+    {
+        bool rb = false;
+        const uint32_t e = (lane + 1) * (uint32_t)C::SUB, a = sp.wl + e;
+        if (lane + 1 < (uint32_t)C::NW && e < sp.sl) {
+#pragma unroll
+            for (int c = 0; c < NCAND; c++) {
+                const uint32_t d = cand_dist(sp, c), ml_ = match_minlen(d);
+                if (!d || a < ml_ + d) continue;  // (the run's first source byte before the window)
+                bool eq = true;
+                for (uint32_t j = 1; j <= ml_; j++) eq = eq && lds_byte(S, a - j) == lds_byte(S, a - j - d);
+                rb = rb || eq;
+            }
+        }
+        reachm = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)__ballot(rb));
+    }
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0;
     bool skip = true;
@@ -838,10 +855,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         // >= ml equal bytes ending at the last byte, so se - ml is a paying start and the last
         // byte is in the union above (this lane's bits, or the previous lane's bits past its
         // chunk): exactly the waves where a paying run reaches the last byte walk.
-        const uint32_t tl = (se - 1 - ss) >> 5, il = (se - 1 - ss) & 31;
-        const uint32_t in_lo = (uint32_t)__builtin_amdgcn_readlane(cvb_lo, tl) >> il;
-        const uint32_t in_hi = tl ? (uint32_t)__builtin_amdgcn_readlane(cvb_hi, tl - 1) >> il : 0u;
-        const bool reach = ((in_lo | in_hi) & 1u) != 0 && se < sp.sl;
+        const bool reach = ((reachm >> w) & 1u) != 0;
         skip = PBX_LZ_COVBOUND && !reach &&
                wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) <
                    (uint32_t)C::MINCOV;
@@ -992,39 +1006,30 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         }
     };
     // Matches cross the wave boundaries (ph_parse_emu: wave w parses from where wave w - 1's last
-    // match ends, waves in order).  Round 0: every wave walks from its own start.  Round r: every
-    // wave whose carry-in (its predecessor's carry-out after round r - 1) differs from the one
-    // its current walk started from walks again, all such waves in parallel (double-buffered
-    // carries: round r reads round r - 1's), until no carry-in changes.  After round r waves
-    // 0..r hold their final walks, so this ends with the serial parse in at most NW - 1 rounds;
-    // on G_FAKE's rows a carry-out rarely depends on the carry-in (a row start resets the match
-    // phase), so one round settles it.  Noise: almost never a round at all.
-    // (one call site of the walk: two inlined copies spill registers to scratch)
-    uint32_t used = 0, cout = 0;  // the carry-in of the wave's current walk (0: its own start), its carry-out
+    // match ends, waves in order).  Round 0: every wave walks from its own start.  Only if some
+    // boundary is reachable (reachm, uniform): round j (a barrier each, boundaries that cannot be
+    // reached skipped) lets wave j walk again from where wave j - 1's final last match ends.
+    // (One call site of the walk: two inlined copies spill registers to scratch.)
+    uint32_t used = 0;  // the carry-in of the wave's final walk (0: from its own start)
 #pragma unroll 1
-    for (uint32_t r = 0; r < (uint32_t)C::NW; r++) {
-        const uint32_t cur = r & 1u, prev = cur ^ 1u;
-        uint32_t cin = 0;
-        if (r && w) {
-            cin = __builtin_amdgcn_readfirstlane(S.w_endb[prev][w - 1]);
-            if (cin <= ss) cin = 0;
+    for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
+        bool go = j == 0 && active && !skip;
+        uint32_t o0 = 0;
+        if (j) {
+            if (((reachm >> (j - 1)) & 1u) == 0) continue;  // (uniform) wave j's start is final
+            if (w == j) {
+                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
+                if (c > ss) {
+                    used = c;
+                    go = !skip;
+                    o0 = c - ss;
+                }
+            }
         }
-        const bool ch = r == 0 || cin != used;
-        if (ch) {
-            used = cin;
-            if (active && !skip) walk(cin ? cin - ss : 0u);
-            cout = last_end > se ? last_end : 0u;
-        }
-        if (lane == 0) {
-            S.w_endb[cur][w] = cout;
-            S.w_chg[cur][w] = ch ? 1u : 0u;
-        }
+        if (go) walk(o0);
+        if (reachm == 0) break;  // (uniform) no match runs into another wave: no barrier at all
+        if ((j == 0 || w == j) && lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
         __syncthreads();
-        // round 0: go on if some wave's match runs into the next one; later: if some wave walked
-        uint32_t more = 0;
-#pragma unroll
-        for (int q = 0; q < C::NW; q++) more |= r ? S.w_chg[cur][q] : (q + 1 < C::NW ? S.w_endb[0][q] : 0u);
-        if (__builtin_amdgcn_readfirstlane(more) == 0) break;
     }
     // the positions [ss, used) the previous wave's last match covers are not literals here
     if (used > p0) {
