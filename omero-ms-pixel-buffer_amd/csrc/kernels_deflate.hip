@@ -742,8 +742,10 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             for (int c = 0; c < NCAND; c++) {
                 const uint32_t d = cand_dist(sp, c), ml_ = match_minlen(d);
                 if (!d || a < ml_ + d) continue;  // (the run's first source byte before the window)
-                bool eq = true;
-                for (uint32_t j = 1; j <= ml_; j++) eq = eq && lds_byte(S, a - j) == lds_byte(S, a - j - d);
+                // bytes [a - ml, a) against d back: unaligned 4-byte LDS reads (ml = 3, 4 or 6)
+                const uint32_t x = lds_ld4(S, a - ml_) ^ lds_ld4(S, a - ml_ - d);
+                bool eq = (x & (ml_ == 3 ? 0x00FFFFFFu : 0xFFFFFFFFu)) == 0;
+                if (ml_ == 6) eq = eq && ((lds_ld4(S, a - 2) ^ lds_ld4(S, a - 2 - d)) & 0xFFFFu) == 0;
                 rb = rb || eq;
             }
         }
