@@ -2,6 +2,7 @@
 #   tests    the round's new -m gpu tests (serving, sparse planes, JNI on the real library, residency)
 #   gputest  the whole -m gpu suite + smoke
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
+#   ab       alternating A/B against the pre-carry kernels (var_precarry)
 #   probe3   the sub-batch probe on three kernel streams (sub-batches overlap)
 #   fvar     the PNG filter kernels of the var_f3* builds
 #   cvar     the deflate chain of the chain variant builds (k_huff one read, k_encode from the plane,
@@ -38,6 +39,15 @@ for stage in "$@"; do
       timeout -k 10 300 $PYT tests/test_gpu_lz77.py > $O/pytest_lz77.log 2>&1; rc=$?
       [ $rc -eq 124 ] || [ $rc -eq 137 ] && { tail -20 $O/pytest_lz77.log; exit 1; }
       grep -E "^E  |passed|failed" $O/pytest_lz77.log | head -20 ;;
+    ab)  # alternating A/B of the product library against the pre-carry kernels (var_precarry)
+      for i in 1 2 3; do
+        for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_precarry/libpbx.so; do
+          for g in noise fake; do
+            PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/prof_workload.py $g 5 > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
+            echo "$i $L $(tail -1 $O/ab.log)"
+          done
+        done
+      done ;;
     probe3)
       PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
       tail -6 $O/subbatch3.log ;;
