@@ -750,6 +750,9 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             }
         }
         reachm = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)__ballot(rb));
+#ifdef PBX_LZ_NOREACH  // timing bound only (variant build): no boundary reachable, wrong output on runs
+        reachm = 0;
+#endif
     }
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0;
@@ -1225,11 +1228,16 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     stamp();
     // the chunk's words again, from LDS: not held in registers across the parse (its walk needs them)
     uint32_t cb[8];
+#ifdef PBX_LZ_CBKEEP  // experiment: the words kept in registers instead
+#pragma unroll
+    for (int k = 0; k < 8; k++) cb[k] = cw[k + 1];
+#else
     {
         const uint4 q0 = *(const uint4*)&S.buf[wi], q1 = *(const uint4*)&S.buf[wi + 4];
         cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
         cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
     }
+#endif
     // literal histogram of the chunk (positions no recorded match covers), 8 interleaved
     // copies against same-address LDS atomics, branch-free: a covered position adds into the
     // lane's own sink word.  Adler-32 partial sums from the same words.
@@ -2663,6 +2671,6 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
 // OUT=lib).
 #if !defined(PBX_TIMING_VARIANT) && (PBX_LZ_SKIP_STORE || PBX_LZ_SKIP_FILL || PBX_LZ_SKIP_HIST || \
     PBX_LZ_SKIP_OUT || PBX_ENC_SKIP_WRITE || PBX_ENC_SKIP_PATCH || PBX_ENC_SKIP_CRC || PBX_ENC_SKIP_STORE || \
-    PBX_HUFF_ONEREAD || defined(PBX_LZ_FAKE_LOAD))
+    PBX_HUFF_ONEREAD || defined(PBX_LZ_FAKE_LOAD) || defined(PBX_LZ_NOREACH))
 #error "output-changing timing knobs (PBX_LZ_SKIP_*, PBX_ENC_SKIP_*, PBX_HUFF_ONEREAD, PBX_LZ_FAKE_LOAD) need a variant build (-DPBX_TIMING_VARIANT, OUT=lib/var_*)"
 #endif

@@ -41,8 +41,8 @@ for stage in "$@"; do
       grep -E "^E  |passed|failed" $O/pytest_lz77.log | head -20 ;;
     ab)  # alternating A/B of the product library against the pre-carry kernels (var_precarry)
       for i in 1 2 3; do
-        for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_precarry/libpbx.so; do
-          for g in noise fake; do
+        for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-omero-ms-pixel-buffer_amd/lib/var_precarry/libpbx.so}; do
+          for g in ${AB_GENS:-noise fake}; do
             PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/prof_workload.py $g 5 > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
             echo "$i $L $(tail -1 $O/ab.log)"
           done
