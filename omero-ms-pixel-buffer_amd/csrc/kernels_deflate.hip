@@ -738,14 +738,16 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         bool rb = false;
         const uint32_t e = (lane + 1) * (uint32_t)C::SUB, a = sp.wl + e;
         if (lane + 1 < (uint32_t)C::NW && e < sp.sl) {
-#pragma unroll
-            for (int c = 0; c < NCAND; c++) {
-                const uint32_t d = cand_dist(sp, c), ml_ = match_minlen(d);
-                if (!d || a < ml_ + d) continue;  // (the run's first source byte before the window)
-                // bytes [a - ml, a) against d back: unaligned 4-byte LDS reads (ml = 3, 4 or 6)
-                const uint32_t x = lds_ld4(S, a - ml_) ^ lds_ld4(S, a - ml_ - d);
-                bool eq = (x & (ml_ == 3 ? 0x00FFFFFFu : 0xFFFFFFFFu)) == 0;
-                if (ml_ == 6) eq = eq && ((lds_ld4(S, a - 2) ^ lds_ld4(S, a - 2 - d)) & 0xFFFFu) == 0;
+            // the 8 bytes before the boundary: one aligned 8-byte LDS read (wl and e are
+            // multiples of 16); distances 1 and 2 (ml = 3) compare them among themselves
+            const uint2 v = *(const uint2*)&S.buf[(a >> 2) - 2];
+            const uint64_t x = ((uint64_t)v.y << 32) | v.x;  // bytes a - 8 .. a - 1
+            rb = ((x ^ (x << 8)) >> 40) == 0 || ((x ^ (x << 16)) >> 40) == 0;
+            // one row up (ml = 4, or 6 past 4 KiB), when the run's sources are in the window
+            const uint32_t d = cand_dist(sp, 2), mlr = match_minlen(d);
+            if (d && a >= mlr + d) {
+                bool eq = v.y == lds_ld4(S, a - 4 - d);
+                if (mlr == 6) eq = eq && ((v.x >> 16) ^ (lds_ld4(S, a - 6 - d) & 0xFFFFu)) == 0;
                 rb = rb || eq;
             }
         }
@@ -1226,9 +1228,9 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
     }
     stamp();
-    // the chunk's words again, from LDS: not held in registers across the parse (its walk needs them)
+    // the chunk's words for the histogram and Adler-32
     uint32_t cb[8];
-#ifdef PBX_LZ_CBKEEP  // experiment: the words kept in registers instead
+#ifndef PBX_LZ_CBRELOAD  // experiment: reloaded (kept in registers: 0.08 ms faster, profiles/r04i/)
 #pragma unroll
     for (int k = 0; k < 8; k++) cb[k] = cw[k + 1];
 #else
