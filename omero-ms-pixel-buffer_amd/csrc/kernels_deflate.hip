@@ -2050,7 +2050,7 @@ constexpr uint32_t SLOT_NONE = 288;
 template <class C, class SM>
 __device__ __forceinline__ bool build_slots(uint32_t tid, const SM& S, const SegParams& sp,
                                             const uint32_t (&cb)[C::CH / 4],
-                                            uint32_t (&slot)[C::CH + 2]) {
+                                            uint32_t (&slot)[C::CH + 2], uint32_t carry) {
     const uint32_t cs = tid * C::CH;
     const uint32_t ce = cs + C::CH < sp.sl ? cs + C::CH : sp.sl;
     const uint32_t w = (cs / C::SUB) < (uint32_t)C::NW ? cs / C::SUB : (uint32_t)C::NW - 1;
@@ -2071,9 +2071,8 @@ __device__ __forceinline__ bool build_slots(uint32_t tid, const SM& S, const Seg
     };
     if (lo > 0) {
         cover(mp[lo - 1] & 0xFFFFu, (mp[lo - 1] & 0xFFFFu) + (mp[lo - 1] >> 16) + 3);
-    } else if (w > 0) {  // the previous wave's last match may run into this chunk (walk_tokens)
-        const uint32_t pe = carry_end<C>(S, w - 1);
-        if (pe > cs) cover(cs, pe);
+    } else if (carry > cs) {  // the previous wave's last match runs into this chunk (walk_tokens)
+        cover(cs, carry);
     }
     uint32_t m1 = lo;
     while (m1 < nm && (mp[m1] & 0xFFFFu) < ce) {
@@ -2171,9 +2170,10 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     // the empty asm uses make the compiler wait for all of them at one point)
     const uint32_t* mg = mrec + (size_t)seg * MREC_WORDS;
     SegInfo gi;  // everything the encoder needs about its segment / tile
-    uint32_t nmw;
+    uint32_t nmw, nmp;
     {
         nmw = mg[w];
+        nmp = w ? mg[w - 1] : 0u;  // the previous wave's matches: its last may run into this wave
         static_assert(sizeof(SegInfo) == 80, "five 16-byte words");
         const uint4* src = (const uint4*)&info[seg];
         const uint4 g0 = src[0], g1 = src[1], g2 = src[2], g3 = src[3], g4 = src[4];
@@ -2296,7 +2296,15 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     uint32_t nbits = 0;
     bool lit_only = false;
     if (!stored) {
-        lit_only = build_slots<C>(tid, S, sp, cb, slot);
+        // where the previous wave's last match ends when it runs into this wave (carry_end):
+        // scalar loads of its last record, only when it kept matches (noise: almost never)
+        uint32_t carry = 0;
+        if (nmp) {
+            const uint32_t r = mg[C::NW + (w - 1) * C::MAXMW + nmp - 1];
+            const uint32_t e = (r & 0xFFFFu) + (r >> 16) + 3;
+            carry = e > w * (uint32_t)C::SUB ? e : 0u;
+        }
+        lit_only = build_slots<C>(tid, S, sp, cb, slot, carry);
 #pragma unroll
         for (int i = 0; i < C::CH + 2; i += 2) nbits += (slot[i] >> 27) + (slot[i + 1] >> 27);
     }
