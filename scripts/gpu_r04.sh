@@ -3,6 +3,7 @@
 #   gputest  the whole -m gpu suite + smoke
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
 #   ab       alternating A/B against the pre-carry kernels (var_precarry)
+#   rehearse the N-rank bench path, two ranks on one GPU
 #   probe3   the sub-batch probe on three kernel streams (sub-batches overlap)
 #   fvar     the PNG filter kernels of the var_f3* builds
 #   cvar     the deflate chain of the chain variant builds (k_huff one read, k_encode from the plane,
@@ -48,6 +49,9 @@ for stage in "$@"; do
           done
         done
       done ;;
+    rehearse)  # the N-rank bench path with both ranks on the box's one GPU (PBX_BENCH_ONE_GPU)
+      PBX_BENCH_ONE_GPU=1 timeout -k 10 900 python -u bench.py --gpus 2 --steps 5 --warmup 2 > $O/rehearse.json 2> $O/rehearse.err || { tail -30 $O/rehearse.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/rehearse.json')); print(d['n_gpus'], d['value'], sorted(k for k in d if isinstance(d[k], dict))[:40])" ;;
     probe3)
       PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
       tail -6 $O/subbatch3.log ;;
