@@ -1879,8 +1879,6 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
     info[g].zoff = container_zoff(dt[i]);
     info[g].flags = (k == s0 ? SF_FIRST : 0u) | (k + 1 == s1 ? SF_LAST : 0u) | ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
 }
-    }
-}
 
 // ================================================================ k_seg_sizes
 __device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
