@@ -38,7 +38,7 @@ import pbx  # noqa: E402
 METRIC = "tiles/sec (512x512 uint16 PNG) + achieved HBM GB/s at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TILE, GRID = 512, 64
-KSTREAMS, KSTAGGER = int(os.environ.get("PBX_KSTREAMS", "3")), 1  # the library's defaults
+KSTREAMS, KSTAGGER = int(os.environ.get("PBX_KSTREAMS", "3")), int(os.environ.get("PBX_KSTAGGER", "1"))  # the library's defaults
 PIPE_DEPTH = int(os.environ.get("PBX_BENCH_DEPTH", "2"))  # batches in flight
 HEADLINE_SUB = int(os.environ.get("PBX_BENCH_SUB", "0"))  # headline sub-batch tiles (0: one batch per step)
 

@@ -4,6 +4,7 @@
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
 #   ab       alternating A/B against the pre-carry kernels (var_precarry)
 #   rehearse the N-rank bench path, two ranks on one GPU
+#   knobs    the headline under other pipelining settings
 #   probe3   the sub-batch probe on three kernel streams (sub-batches overlap)
 #   fvar     the PNG filter kernels of the var_f3* builds
 #   cvar     the deflate chain of the chain variant builds (k_huff one read, k_encode from the plane,
@@ -52,6 +53,12 @@ for stage in "$@"; do
     rehearse)  # the N-rank bench path with both ranks on the box's one GPU (PBX_BENCH_ONE_GPU)
       PBX_BENCH_ONE_GPU=1 timeout -k 10 900 python -u bench.py --gpus 2 --steps 5 --warmup 2 > $O/rehearse.json 2> $O/rehearse.err || { tail -30 $O/rehearse.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/rehearse.json')); print(d['n_gpus'], d['value'], sorted(k for k in d if isinstance(d[k], dict))[:40])" ;;
+    knobs)  # the headline under other pipelining settings (streams / stagger / depth / sub-batches)
+      for kv in "3 1 2 0" "3 1 3 0" "2 1 2 0" "4 1 3 0" "3 2 2 0" "3 0 2 0" "3 1 2 1024" "3 1 4 1024" "4 1 8 512"; do
+        set -- $kv
+        PBX_KSTREAMS=$1 PBX_KSTAGGER=$2 PBX_BENCH_DEPTH=$3 PBX_BENCH_SUB=$4 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-extra --no-cpu-baseline > $O/knob.json 2> $O/knob.err || { tail -20 $O/knob.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/knob.json')); print('streams $1 stagger $2 depth $3 sub $4:', d['value'], d['ms_per_step'])"
+      done ;;
     probe3)
       PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
       tail -6 $O/subbatch3.log ;;
