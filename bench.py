@@ -802,7 +802,7 @@ def launch_ranks(n, argv):
 def dry_run(args, world, rank):
     """The N > 1 plumbing without HIP: rendezvous, barrier, timed no-op steps, max-over-ranks."""
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+        init_gloo()
     met = torch.ones(1, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(met)
@@ -840,6 +840,20 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def init_gloo():
+    """gloo's process group, its connection messages ("[Gloo] Rank r is connected ...", written
+    to the C-level stdout) sent to stderr: rank 0's stdout carries the one JSON line only."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", init_method="env://")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -863,7 +877,7 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
     if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
+        init_gloo()
     # PBX_BENCH_ONE_GPU=1: every rank on GPU 0 (a rehearsal of the N-rank path on a one-GPU
     # box; per-rank numbers then share one device)
     dev = 0 if os.environ.get("PBX_BENCH_ONE_GPU") else local
