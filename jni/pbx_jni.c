@@ -15,6 +15,7 @@
  * ByteBuffers, so the GPU work never stalls the JVM's garbage collector. */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -28,10 +29,15 @@ static void throw_class(JNIEnv* env, const char* cls, const char* msg) {
     if (c) (*env)->ThrowNew(env, c, msg);
 }
 
+/* The message starts "pbx status <code>: " (e.g. 507: the residency budget is held; the
+ * handler waits and loads again). */
 static void throw_status(JNIEnv* env, int st) {
+    char msg[512];
+    const char* e = pbx_last_error();
+    snprintf(msg, sizeof msg, "pbx status %d: %s", st, e ? e : "");
     throw_class(env, st == PBX_E_BADARG || st == PBX_E_NOTFOUND || st == PBX_E_EXISTS
                          ? "java/lang/IllegalArgumentException" : "java/lang/RuntimeException",
-                pbx_last_error());
+                msg);
 }
 
 static int pixel_type(JNIEnv* env, jstring s) {

@@ -131,7 +131,7 @@ int main(void) {
         reset();
         fake.create_rc = PBX_E_NO_SPACE;
         CHECK(J(createPlane)(env, NULL, 1, 9, 0, 1, 0, 0, &u16, 100, 200, 0, 0, 0) == 0 &&
-              threw("java/lang/RuntimeException"));
+              threw("java/lang/RuntimeException") && strstr(pending, "pbx status 507: ") != NULL);
     }
     /* ---- planeState, declareImage */
     {
