@@ -392,3 +392,24 @@ def test_incompressible_tiles_stored_per_segment(service, adaptive_service, orac
     assert r == 0 and meta["compression"] == 8 and px == tile.tobytes()
     z2, _ = _emu.deflate(tile.tobytes(), 1024)
     assert tif[160:160 + len(z2)] == z2
+
+
+@pytest.mark.parametrize("origin", [(0, 0), (1024, 3072), (7680, 512), (13, 7)])
+def test_fake_u16_tiles_cross_wave_matches(service, oracle, origin):
+    """512x512 uint16 G_FAKE tiles (rows repeating: matches run across the waves' 2 KiB
+    sub-segments, and every boundary of a segment takes a carry round): the zlib stream is
+    the CPU emulation of the deflate workgroups byte for byte, it inflates to the oracle's
+    scanlines, and it stays within 3% of zlib-6."""
+    iid = next(_ids)
+    service.register_plane(iid, 0, 0, 0, pbx.UINT16, 8192, 4096, generator="fake")
+    x, y = origin
+    (st, body), = service.get_tiles([pbx.TileCtx(iid, 0, 0, 0, x, y, 512, 512, format="png")])
+    assert st == pbx.OK
+    tile = oracle.gen_region(1, pbx.UINT16, x, y, 512, 512)
+    stream = oracle.png_filter_stream(tile, pbx.UINT16, 512, 512, 0).tobytes()
+    r, idat = oracle.png_inflate_idat(body, len(stream))
+    assert r == 0 and idat == stream
+    z, _ = _emu.deflate(stream, 1025)
+    assert body[99:99 + len(z)] == z
+    assert len(z) <= 1.03 * len(zlib.compress(stream, 6)) + 64
+    service.release_plane(service.lookup_plane(iid, 0, 0, 0)[0])
