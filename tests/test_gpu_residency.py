@@ -291,3 +291,31 @@ def test_concurrent_misses_load_once(oracle):
             list(ex.map(worker, range(32)))
         assert not errors, errors[:5]
         assert src.reads == 3  # each plane (one band each) read once
+
+
+def test_fresh_plane_is_kept_until_read(oracle):
+    """A plane just loaded is not evicted before a request has read it: under a budget of one
+    plane a second plane cannot be made room for (507) until the first one is served; then it
+    is evicted (LRU) and the second loads.  A plane larger than the whole budget is a 507 at
+    once, whatever is fresh."""
+    pt, side = pbx.UINT16, 1024
+    pbytes = (side * 2 + 255) // 256 * 256 * side + 256
+    iid = next(_ids)
+    with pbx.PixelsService() as svc:
+        svc.set_residency_budget(int(1.5 * pbytes))
+        svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=11)  # fresh
+        with pytest.raises(pbx.PbxError) as e:
+            svc.register_plane(iid, 0, 1, 0, pt, side, side, generator="noise", seed=11)
+        assert e.value.status == pbx.E_NO_SPACE
+        assert svc.residency_stats()["evictions"] == 0
+        st, body = svc.get_tile(pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64))  # its first read
+        assert st == pbx.OK and body == _tile(oracle, pt, 0, 0, 64, 64)
+        svc.register_plane(iid, 0, 1, 0, pt, side, side, generator="noise", seed=11)
+        s = svc.residency_stats()
+        assert s["evictions"] == 1 and s["resident_bytes"] <= s["budget"]
+        assert svc.get_tile(pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64))[0] == pbx.E_NOT_RESIDENT
+        st, body = svc.get_tile(pbx.TileCtx(iid, 0, 1, 0, 8, 8, 64, 64))
+        assert st == pbx.OK and body == _tile(oracle, pt, 8, 8, 64, 64, c=1)
+        with pytest.raises(pbx.PbxError) as e:
+            svc.register_plane(iid + 1, 0, 0, 0, pt, 2 * side, side, generator="noise")
+        assert e.value.status == pbx.E_NO_SPACE
