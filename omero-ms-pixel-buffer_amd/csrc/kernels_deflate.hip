@@ -1013,23 +1013,33 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         }
     };
     // Matches cross the wave boundaries (ph_parse_emu: wave w parses from where wave w - 1's last
-    // match ends, waves in order).  Round 0: every wave walks from its own start.  Only if some
-    // boundary is reachable (reachm, uniform): round j (a barrier each, boundaries that cannot be
-    // reached skipped) lets wave j walk again from where wave j - 1's final last match ends.
-    // (One call site of the walk: two inlined copies spill registers to scratch.)
-    uint32_t used = 0;  // the carry-in of the wave's final walk (0: from its own start)
+    // match ends, waves in order).  Round 0: every wave walks from a predicted start: its own
+    // start when its boundary cannot be reached, else where a chain of 258-byte matches from
+    // the segment start would cross it (one run over the whole segment, G_FAKE's repeated rows:
+    // every prediction right).  Only if some boundary is reachable (reachm, uniform): one
+    // barrier, then the first wave f whose start was wrong (waves before it walked from their
+    // final start, by induction from wave 0); round j >= f (a barrier each, boundaries that
+    // cannot be reached skipped) lets wave j walk again from where wave j - 1's final last
+    // match ends, when that differs from its round-0 start.  The records equal the serial
+    // parse's whatever the predictions.  (One call site of the walk: two inlined copies spill
+    // registers to scratch.)
+    auto pred = [&](uint32_t j) -> uint32_t {  // (uniform) wave j's predicted start
+        const uint32_t s = j * (uint32_t)C::SUB;
+        return j && ((reachm >> (j - 1)) & 1u) ? 258u * ((s + 257u) / 258u) : s;
+    };
+    // (nothing but reachm stays live across the walks: SGPR spills)
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
         bool go = j == 0 && active && !skip;
-        uint32_t o0 = 0;
+        uint32_t o0 = j == 0 ? pred(w) - ss : 0u;
         if (j) {
             if (((reachm >> (j - 1)) & 1u) == 0) continue;  // (uniform) wave j's start is final
             if (w == j) {
                 const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
-                if (c > ss) {
-                    used = c;
-                    go = !skip;
-                    o0 = c - ss;
+                const uint32_t a = c > ss ? c : ss;
+                if (a != pred(w)) {
+                    go = active && !skip;
+                    o0 = a - ss;
                 }
             }
         }
@@ -1037,8 +1047,29 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         if (reachm == 0) break;  // (uniform) no match runs into another wave: no barrier at all
         if ((j == 0 || w == j) && lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
         __syncthreads();
+        if (j == 0) {
+            uint32_t f = (uint32_t)C::NW;
+            for (uint32_t i = 1; i < (uint32_t)C::NW; i++) {
+                if (((reachm >> (i - 1)) & 1u) == 0) continue;
+                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[i - 1]), si = i * (uint32_t)C::SUB;
+                if ((c > si ? c : si) != pred(i)) {
+                    f = i;
+                    break;
+                }
+            }
+            if (f == (uint32_t)C::NW) break;  // (uniform) every start was right: no more rounds
+            // rounds only from wave f on: the boundaries before wave f - 1's end are final (bit
+            // f - 1 stays set, so reachm stays nonzero)
+            reachm &= 0xFFFFFFFFu << (f - 1);
+        }
     }
     // the positions [ss, used) the previous wave's last match covers are not literals here
+    // (w_end[w - 1] holds that match's final end: every write of it is followed by a barrier)
+    uint32_t used = 0;
+    if (reachm && w) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[w - 1]);
+        used = c > ss ? c : 0u;
+    }
     if (used > p0) {
         const uint32_t h = used - p0 < 32 ? used - p0 : 32u;
         cover |= h >= 32 ? 0xFFFFFFFFu : (1u << h) - 1u;

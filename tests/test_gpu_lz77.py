@@ -35,10 +35,16 @@ def _streams():
     rep = np.repeat(rng.integers(0, 65536, (10, 512)), 8, axis=0).astype(">u2")
     rep[5::13] = rng.integers(0, 65536, (len(rep[5::13]), 512))
     out.append(("rowrep512", pbx.UINT16, rep))
+    # one run over whole segments (k_lz77's predicted wave starts right), and the same run
+    # broken at a few random pixels (predictions wrong from some wave on: serial rounds)
+    out.append(("zeros512", pbx.UINT16, np.zeros((80, 512), ">u2")))
+    brk = np.full((80, 512), 0x1234, ">u2")
+    brk.flat[rng.choice(80 * 512, 40, replace=False)] = rng.integers(0, 65536, 40)
+    out.append(("runbreak512", pbx.UINT16, brk))
     return out
 
 
-@pytest.mark.parametrize("case", range(9))
+@pytest.mark.parametrize("case", range(11))
 def test_gpu_lz77_matches_emulator(service, case):
     name, pt, a = _streams()[case]
     h, w = a.shape
