@@ -678,9 +678,60 @@ __device__ __forceinline__ bool fill_fast_any(uint32_t* buf, const DirectRows& d
 // Correct (every -m gpu test green) but slower: k_lz77 1.48 -> 1.36 ms, k_encode 1.57 ->
 // 1.92 ms, the conversion's VALU in the issue-bound encoder (profiles/r03_p17/).  0 (default):
 // k_lz77 stores the bytes from its fill registers and k_encode reads them back.
+// 2: the same for 16-bit byte-swapped samples (fast-fill mode 5, the headline), each lane
+// converting its own 32 bytes in registers: three 16-byte plane loads, the byte swap and a
+// per-lane byte alignment (plane_words_swap16), no LDS.
 #ifndef PBX_ENC_FROM_PLANE
 #define PBX_ENC_FROM_PLANE 0
 #endif
+
+// Bytes [q, q + 32) of a row's converted data (16-bit samples byte-swapped) as 8 words; bytes
+// outside [0, rb) are 0 (a PNG row's filter byte sits at q = -1).  rp: the row in the plane
+// (nullptr: no row, all 0).  Chunks at 16-byte offsets inside the row only are loaded.
+__device__ __forceinline__ void row_bytes32_swap16(const uint8_t* rp, int32_t q, uint32_t rb, uint32_t (&o)[8]) {
+    const int32_t b16 = q & ~15;  // (floor for negative q)
+    uint32_t z[12];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int32_t off = b16 + 16 * k;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (rp && off >= 0 && off < (int32_t)rb) v = swap16(gload16(rp + off), 2);
+        z[4 * k] = v.x; z[4 * k + 1] = v.y; z[4 * k + 2] = v.z; z[4 * k + 3] = v.w;
+    }
+    const uint32_t s = (uint32_t)(q - b16);  // 0..15: the first byte's offset in z
+    // word selection by masks (a select the compiler would turn into a scratch-indexed array)
+    const uint32_t m1 = 0u - ((s >> 2) & 1u), m2 = 0u - ((s >> 3) & 1u);
+    uint32_t y[11];
+#pragma unroll
+    for (int i = 0; i < 11; i++) y[i] = z[i] ^ ((z[i] ^ z[i + 1]) & m1);
+    uint32_t t[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) t[i] = y[i] ^ ((y[i] ^ y[i + 2]) & m2);
+#pragma unroll
+    for (int m = 0; m < 8; m++) o[m] = __builtin_amdgcn_alignbyte(t[m + 1], t[m], s & 3u);
+}
+
+// Stream bytes [B, B + 32) of a direct tile of fast-fill mode 5 (k_lz77 stored none): row r's
+// bytes, then (a chunk that crosses into row r + 1: rows are longer than 32 bytes) row r + 1's
+// from its filter byte on.  Rows past the tile's last are 0.
+__device__ __forceinline__ void plane_words_swap16(const DirectRows& dr, uint32_t B, uint32_t (&cb)[8]) {
+    const uint32_t r = div_rcp(B, dr.rowlen, dr.rcp);
+    const uint32_t col = B - r * dr.rowlen;
+    const uint8_t* rp = r < dr.h ? dr.row0 + (int64_t)r * dr.pitch : nullptr;
+    row_bytes32_swap16(rp, (int32_t)col - (int32_t)dr.fb, dr.rb, cb);
+    const uint32_t k = dr.rowlen - col;  // bytes of row r in the chunk
+    if (k < 32) {
+        const uint8_t* rn = r + 1 < dr.h ? dr.row0 + (int64_t)(r + 1) * dr.pitch : nullptr;
+        uint32_t nb[8];
+        row_bytes32_swap16(rn, -(int32_t)k - (int32_t)dr.fb, dr.rb, nb);
+#pragma unroll
+        for (uint32_t m = 0; m < 8; m++) {
+            const int32_t a = (int32_t)k - 4 * (int32_t)m;  // bytes of word m from row r
+            const uint32_t mask = a <= 0 ? 0u : a >= 4 ? 0xFFFFFFFFu : (1u << (8 * a)) - 1u;
+            cb[m] = (cb[m] & mask) | (nb[m] & ~mask);
+        }
+    }
+}
 
 // ==================================================================== k_lz77
 // Zero bytes of x as 4 bits (bit j: byte j of x is zero).
@@ -1207,8 +1258,10 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     if (PBX_LZ_SKIP_FILL) {
     } else if (direct && PBX_LZ_FAST_FILL &&
                fill_fast_any<C::NT>(S.buf, dr, (uint32_t)sp.base, sp.wl + sp.sl, nz, tid,
-                                    PBX_LZ_SKIP_STORE || PBX_ENC_FROM_PLANE ? nullptr
-                                                                            : stream + d.out_off + sp.base + sp.wl,
+                                    PBX_LZ_SKIP_STORE || PBX_ENC_FROM_PLANE == 1 ||
+                                            (PBX_ENC_FROM_PLANE == 2 && fast_fill_mode(dr) == 5u)
+                                        ? nullptr
+                                        : stream + d.out_off + sp.base + sp.wl,
                                     sp.wl)) {
         stored = true;  // (or not needed: k_encode reads the plane)
         if (PROF) stamp();
@@ -2251,8 +2304,19 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
     uint32_t cb[C::CH / 4];
     DirectRows dr;
     dr.init(d);
-    const uint32_t fmode = PBX_ENC_FROM_PLANE && PBX_LZ_FAST_FILL && (d.flags & TF_DIRECT) ? fast_fill_mode(dr) : 0u;
-    if (fmode) {
+    const uint32_t fmode = PBX_ENC_FROM_PLANE == 1 && PBX_LZ_FAST_FILL && (d.flags & TF_DIRECT) ? fast_fill_mode(dr) : 0u;
+    const bool rmode = PBX_ENC_FROM_PLANE == 2 && PBX_LZ_FAST_FILL && (d.flags & TF_DIRECT) && fast_fill_mode(dr) == 5u;
+    if (rmode) {
+        // k_lz77 stored no bytes: the lane's 32 bytes from the plane rows, converted in registers
+        const uint32_t cs = tid * C::CH;
+        plane_words_swap16(dr, (uint32_t)(seg_off - d.out_off) + cs, cb);
+#pragma unroll
+        for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end, branch-free
+            const int32_t keep = (int32_t)sp.sl - (int32_t)(cs + 4 * k);
+            const uint32_t kb = keep <= 0 ? 0u : keep >= 4 ? 32u : 8u * (uint32_t)keep;
+            cb[k] &= (uint32_t)((1ull << kb) - 1ull);
+        }
+    } else if (fmode) {
         // k_lz77 stored no bytes: the wave converts its 2 KiB of the segment from the plane
         // rows into its part of out[] (fill_fast as one 64-thread group, zero past the
         // segment), each lane reads its 32 bytes back and zeroes them.  Wave-local: the LDS
