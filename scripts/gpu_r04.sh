@@ -11,6 +11,8 @@
 #            k_lz77 without its stream store) next to the product library
 #   pmcf     PMC passes of k_filter3 (Sub, Paeth, adaptive): issue + traffic
 #   pmc      PMC passes of the headline deflate chain (scripts/pmc_run.sh, filter passes off)
+#   parity   the output-parity suites alone
+#   kstats   rocprofv3 kernel averages of a short headline run
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
 # Every GPU step has its own time limit; the first failure ends the call.
 set -o pipefail
@@ -92,6 +94,14 @@ for stage in "$@"; do
       PMC_FILTER=0 bash scripts/pmc_run.sh > $O/pmc_run.log 2>&1 || { tail -30 $O/pmc_run.log; exit 1; }
       python3 scripts/pmc_summary.py gpurun_out $O/traffic.json > $O/pmc_summary.txt 2>&1 || true
       tail -60 $O/pmc_summary.txt ;;
+    parity)  # the output-parity suites (PNG / TIFF bytes against the oracle and the emulator)
+      timeout -k 10 400 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_sweep.py \
+        tests/test_gpu_lz77.py tests/test_gpu_huffman.py > $O/pytest_parity.log 2>&1 || { grep -E "FAILED|^E " $O/pytest_parity.log | head -30; tail -5 $O/pytest_parity.log; exit 1; }
+      tail -1 $O/pytest_parity.log ;;
+    kstats)  # the rocprofv3 kernel averages of a short serial-pass headline run
+      PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kprof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $O/kprof_bench.json 2> $O/kprof_bench.err || { tail -20 $O/kprof_bench.err; exit 1; }
+      find $O/kprof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_short.csv \;
+      cut -d, -f1-4 $O/kernel_stats_short.csv | head -12 ;;
     bench)
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['deflate_chain_ms'], d['roofline']['frac'])"
