@@ -2599,27 +2599,6 @@ __device__ __forceinline__ uint32_t crc_be32(uint32_t c, uint32_t v) {  // v's 4
     return crc_u8(c, v);
 }
 
-// a * b mod P (crc_multmodp) with the dependent chain four times shorter: b x, b x^2, b x^3
-// and b x^4 straight from b, since P's five low bits are zero (the reductions of b's four low
-// bits do not interact).  k_frame's serial combines are bound by this chain.
-__device__ __forceinline__ uint32_t crc_mul_fast(uint32_t a, uint32_t b) {
-    constexpr uint32_t P = CRC_POLY;
-    static_assert((CRC_POLY & 0x1Fu) == 0, "the stride needs P's four low bits zero");
-    auto bm = [](uint32_t v, int k) { return (uint32_t)((int32_t)(v << (31 - k)) >> 31); };  // bit k as a mask
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 31; i >= 3; i -= 4) {
-        const uint32_t m0 = bm(b, 0), m1 = bm(b, 1), m2 = bm(b, 2), m3 = bm(b, 3);
-        const uint32_t b1 = (b >> 1) ^ (m0 & P);
-        const uint32_t b2 = (b >> 2) ^ (m0 & (P >> 1)) ^ (m1 & P);
-        const uint32_t b3 = (b >> 3) ^ (m0 & (P >> 2)) ^ (m1 & (P >> 1)) ^ (m2 & P);
-        const uint32_t b4 = (b >> 4) ^ (m0 & (P >> 3)) ^ (m1 & (P >> 2)) ^ (m2 & (P >> 1)) ^ (m3 & P);
-        p ^= (bm(a, i) & b) ^ (bm(a, i - 1) & b1) ^ (bm(a, i - 2) & b2) ^ (bm(a, i - 3) & b3);
-        b = b4;
-    }
-    return p;
-}
-
 constexpr uint32_t FOURCC(char a, char b, char c, char d) {
     return ((uint32_t)(uint8_t)a << 24) | ((uint32_t)(uint8_t)b << 16) | ((uint32_t)(uint8_t)c << 8) | (uint8_t)d;
 }
@@ -2645,6 +2624,7 @@ __device__ __forceinline__ uint32_t put_chunk_w(uint8_t* o, uint32_t type, const
     return 12 + n;
 }
 
+
 // One thread per tile: everything around the segments' bytes, and the bytes two segments
 // of a block share (SegInfo.part), joined in stream order into the output and the IDAT CRC.
 __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, uint32_t ndt,
@@ -2658,12 +2638,19 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
     uint8_t* base = out + offs[i];
     const bool tiff = (d.flags & TF_TIFF) != 0;
     const uint32_t zoff = container_zoff(d);
+    uint32_t s1 = 0, s2 = 0, payload = 0;
+#pragma unroll 4
+    for (uint32_t k = 0; k < d.seg_count; k++) {  // (unrolled: four segments' loads in flight)
+        const SegInfo& g = info[d.seg_first + k];
+        adler_combine(s1, s2, g.adler_s1, g.adler_s2, g.sl);
+    }
     const uint32_t nb = tile_blocks(d.seg_count, PBX_TILE_BLK_CAP(d));
-    uint32_t payload = 0;
     for (uint32_t k = 0; k < nb; k++) payload += blk[d.hblk_first + k].nbytes;
+    const uint32_t adler = adler_final(s1, s2, d.stream_len);
     const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;
     base[zoff] = 0x78;      // CMF: deflate, 32 KiB window
     base[zoff + 1] = 0x9C;  // FLG: default level (Deflater -1 == 6), check bits
+    put_be32(base + pos, adler);
     uint32_t o = 8;
     if (!tiff) {
         const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
@@ -2679,72 +2666,42 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
         put_be32(base + o, ZLIB_HDR_BYTES + payload + 4);
         put_be32(base + o + 4, FOURCC('I', 'D', 'A', 'T'));
     }
-    // CRC over type + zlib stream (PNG), joined from the segments' CRCs and shared bytes, and
-    // the Adler-32, in one pass over the tile's segments in stream order (its blocks' segments
-    // are consecutive: SF_FIRST / SF_LAST mark them), the records of FB segments loaded
-    // together (one round trip per FB segments instead of one per segment)
+    // CRC over type + zlib stream (PNG), joined from the segments' CRCs and shared bytes
     uint32_t c = tiff ? 0u
                       : crc_u8(crc_u8(crc_be32(0xFFFFFFFFu, FOURCC('I', 'D', 'A', 'T')), 0x78), 0x9C) ^ 0xFFFFFFFFu;
-    uint32_t s1 = 0, s2 = 0;
     uint8_t* z = base + zoff + ZLIB_HDR_BYTES;
-    bool pend = false;
-    uint32_t pv = 0, pidx = 0, boff = 0;
-    auto flush = [&]() {
-        z[boff + pidx] = (uint8_t)pv;
-        if (!tiff) c = crc_u8(c ^ 0xFFFFFFFFu, pv) ^ 0xFFFFFFFFu;
-        pend = false;
-    };
-    constexpr uint32_t FB = 4;
-    static_assert(sizeof(SegInfo) >= 64, "the first four 16-byte words hold the fields used here");
-    for (uint32_t q0 = 0; q0 < d.seg_count; q0 += FB) {
-        uint4 r[FB][4];
-#pragma unroll
-        for (uint32_t j = 0; j < FB; j++) {
-            const uint32_t q = q0 + j < d.seg_count ? q0 + j : q0;
-            const uint4* src = (const uint4*)&info[d.seg_first + q];
-#pragma unroll
-            for (int k = 0; k < 4; k++) r[j][k] = src[k];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < FB; j++) {
-            if (q0 + j >= d.seg_count) break;
-            // (SegInfo words: sl last wl rowlen | s1 s2 btype hdr_bits | bit0 bit1 crc crc_op |
-            // blk flags part bitsum)
-            const uint32_t sl = r[j][0].x, last = r[j][0].y, as1 = r[j][1].x, as2 = r[j][1].y;
-            const uint32_t bit0 = r[j][2].x, bit1 = r[j][2].y, crc = r[j][2].z, crc_op = r[j][2].w;
-            const uint32_t bk = r[j][3].x, fl = r[j][3].y, part = r[j][3].z;
-            adler_combine(s1, s2, as1, as2, sl);
-            if (fl & SF_FIRST) {  // a block starts: its byte offset in the zlib payload
-                pend = false;
-                boff = blk[bk].off;
-            }
-            const uint32_t b0 = bit0 >> 3, le = bit1 - 8 * b0, o0 = (bit0 & 7u) ? 1u : 0u;
-            uint32_t o1 = last ? (le + 7) >> 3 : le >> 3;
+    for (uint32_t k = 0; k < nb; k++) {
+        const BlkInfo bi = blk[d.hblk_first + k];
+        bool pend = false;
+        uint32_t pv = 0, pidx = 0;
+        auto flush = [&]() {
+            const uint8_t v = (uint8_t)pv;
+            z[bi.off + pidx] = v;
+            if (!tiff) c = crc_u8(c ^ 0xFFFFFFFFu, v) ^ 0xFFFFFFFFu;
+            pend = false;
+        };
+        for (uint32_t q = 0; q < bi.nseg; q++) {
+            const SegInfo& g = info[bi.seg0 + q];
+            const uint32_t b0 = g.bit0 >> 3, le = g.bit1 - 8 * b0, o0 = (g.bit0 & 7u) ? 1u : 0u;
+            uint32_t o1 = g.last ? (le + 7) >> 3 : le >> 3;
             if (o1 < o0) o1 = o0;
-            if (part & SP_HEAD) {
+            if (g.part & SP_HEAD) {
                 if (!pend) { pend = true; pv = 0; pidx = b0; }
-                pv |= part & 0xFFu;
+                pv |= g.part & 0xFFu;
             }
             if (o1 > o0) {
                 if (pend) flush();
-                if (!tiff) c = crc_mul_fast(crc_op, c) ^ crc;  // (crc_combine_op)
+                if (!tiff) c = crc_combine_op(c, g.crc, g.crc_op);
             }
-            if (part & SP_TAIL) {
+            if (g.part & SP_TAIL) {
                 if (pend) flush();
                 pend = true;
-                pv = (part >> 8) & 0xFFu;
-                pidx = bit1 >> 3;
+                pv = (g.part >> 8) & 0xFFu;
+                pidx = g.bit1 >> 3;
             }
-            if ((fl & SF_LAST) && pend) flush();
         }
+        if (pend) flush();
     }
-    static_assert(offsetof(SegInfo, sl) == 0 && offsetof(SegInfo, last) == 4 && offsetof(SegInfo, adler_s1) == 16 &&
-                      offsetof(SegInfo, adler_s2) == 20 && offsetof(SegInfo, bit0) == 32 && offsetof(SegInfo, bit1) == 36 &&
-                      offsetof(SegInfo, crc) == 40 && offsetof(SegInfo, crc_op) == 44 && offsetof(SegInfo, blk) == 48 &&
-                      offsetof(SegInfo, flags) == 52 && offsetof(SegInfo, part) == 56,
-                  "SegInfo layout read by k_frame");
-    const uint32_t adler = adler_final(s1, s2, d.stream_len);
-    put_be32(base + pos, adler);
     if (d.flags & TF_TILED) return;  // header and tile arrays: k_tiff_tiled
     if (tiff) {
         write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8,
