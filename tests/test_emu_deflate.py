@@ -62,7 +62,7 @@ def test_filtered_streams(oracle, filt):
     assert zlib.decompress(z) == s
 
 
-@pytest.mark.parametrize("kind", ["random", "periodic", "rows"])
+@pytest.mark.parametrize("kind", ["random", "periodic", "rows", "runs"])
 def test_lz77_records_cover_the_segment(kind):
     """LZ77 stage records (what k_lz77 writes and the GPU test compares): per segment the
     literals plus the match lengths cover exactly the segment's bytes, every match starts in
@@ -75,9 +75,16 @@ def test_lz77_records_cover_the_segment(kind):
         s = rng.integers(0, 256, 50000, dtype=np.uint8).tobytes()
     elif kind == "periodic":
         s = (bytes(range(5)) * 20000)[:50000]
-    else:
+    elif kind == "rows":
         row = rng.integers(0, 256, rowlen, dtype=np.uint8).tobytes()
         s = (row * 200)[:50000]
+    else:  # runs of random lengths (3..3000 bytes): many run across the waves' 2 KiB boundaries
+        parts, n = [], 0
+        while n < 50000:
+            ln = int(rng.integers(3, 3000))
+            parts.append(bytes([int(rng.integers(0, 256))]) * ln)
+            n += ln
+        s = b"".join(parts)[:50000]
     hist, mrec = _emu.lz77(s, rowlen)
     n = _emu.lib().pbxemu_nsegs(len(s))
     seg = (-(-len(s) // n) + 15) // 16 * 16
@@ -99,6 +106,21 @@ def test_lz77_records_cover_the_segment(kind):
                 covered += ln
         assert lits + covered == sl
         assert hist[k][256] == 1  # end of block
+
+
+def test_runs_across_wave_boundaries_roundtrip():
+    """Runs of random lengths through the whole deflate emulator: matches carried across the
+    waves' sub-segments decode to the input."""
+    rng = np.random.default_rng(11)
+    parts, n = [], 0
+    while n < 200000:
+        ln = int(rng.integers(1, 5000))
+        parts.append(bytes([int(rng.integers(0, 256))]) * ln)
+        n += ln
+    s = b"".join(parts)[:200000]
+    z, _ = _emu.deflate(s, 1025)
+    assert zlib.decompress(z) == s
+    assert len(z) <= 1.1 * len(zlib.compress(s, 6)) + 64
 
 
 def skewed_block_stream(seed=7):

@@ -41,10 +41,18 @@ def _streams():
     brk = np.full((80, 512), 0x1234, ">u2")
     brk.flat[rng.choice(80 * 512, 40, replace=False)] = rng.integers(0, 65536, 40)
     out.append(("runbreak512", pbx.UINT16, brk))
+    # runs of random lengths (1..3000 samples) laid row after row: predictions right and
+    # wrong at random waves, carries of every length
+    vals, n = [], 0
+    while n < 80 * 512:
+        ln = int(rng.integers(1, 3000))
+        vals.append(np.full(ln, int(rng.integers(0, 65536)), np.uint16))
+        n += ln
+    out.append(("randruns512", pbx.UINT16, np.concatenate(vals)[:80 * 512].reshape(80, 512).astype(">u2")))
     return out
 
 
-@pytest.mark.parametrize("case", range(11))
+@pytest.mark.parametrize("case", range(12))
 def test_gpu_lz77_matches_emulator(service, case):
     name, pt, a = _streams()[case]
     h, w = a.shape
