@@ -2,7 +2,7 @@
 #   tests    the round's new -m gpu tests (serving, sparse planes, JNI on the real library, residency)
 #   gputest  the whole -m gpu suite + smoke
 #   probe    sub-batch probe (Infinity Cache lever) and the PNG filter kernels alone
-#   ab       alternating A/B against the pre-carry kernels (var_precarry)
+#   ab       alternating A/B of the product library against the variant builds in AB_LIBS
 #   rehearse the N-rank bench path, two ranks on one GPU
 #   knobs    the headline under other pipelining settings
 #   probe3   the sub-batch probe on three kernel streams (sub-batches overlap)
@@ -43,9 +43,10 @@ for stage in "$@"; do
       timeout -k 10 300 $PYT tests/test_gpu_lz77.py > $O/pytest_lz77.log 2>&1; rc=$?
       [ $rc -eq 124 ] || [ $rc -eq 137 ] && { tail -20 $O/pytest_lz77.log; exit 1; }
       grep -E "^E  |passed|failed" $O/pytest_lz77.log | head -20 ;;
-    ab)  # alternating A/B of the product library against the pre-carry kernels (var_precarry)
+    ab)  # alternating A/B of the product library against variant builds (AB_LIBS: their libpbx.so paths,
+         # built beforehand with make OUT=lib/var_<name>; none given: the product library alone)
       for i in 1 2 3; do
-        for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-omero-ms-pixel-buffer_amd/lib/var_precarry/libpbx.so}; do
+        for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
           for g in ${AB_GENS:-noise fake}; do
             PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/prof_workload.py $g 5 > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
             echo "$i $L $(tail -1 $O/ab.log)"
