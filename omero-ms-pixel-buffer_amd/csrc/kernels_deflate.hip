@@ -46,7 +46,11 @@ struct LzSmem {
     alignas(16) uint32_t buf[C::BUFW];
     uint32_t mrl[C::NW * C::MAXMW];
     uint32_t w_nm[C::NW];
-    uint32_t w_end[C::NW];  // a wave's last match end when it runs into the next wave (else 0)
+    // per repair round (double-buffered by round parity): a wave's last match end when it runs
+    // into the next wave (else 0), and the start its current records were walked from
+    // (0xFFFFFFFF: a wave whose walk is skipped, any start gives the same result)
+    uint32_t w_end[2][C::NW];
+    uint32_t w_st[2][C::NW];
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
     alignas(16) uint32_t h8[288 * LZ_HCOPIES];
@@ -1068,57 +1072,54 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     // start when its boundary cannot be reached, else where a chain of 258-byte matches from
     // the segment start would cross it (one run over the whole segment, G_FAKE's repeated rows:
     // every prediction right).  Only if some boundary is reachable (reachm, uniform): one
-    // barrier, then the first wave f whose start was wrong (waves before it walked from their
-    // final start, by induction from wave 0); round j >= f (a barrier each, boundaries that
-    // cannot be reached skipped) lets wave j walk again from where wave j - 1's final last
-    // match ends, when that differs from its round-0 start.  The records equal the serial
-    // parse's whatever the predictions.  (One call site of the walk: two inlined copies spill
+    // barrier per round, then one lane per wave checks that wave's start against where the
+    // previous wave's latest walk ends; while some start is wrong, EVERY wave whose start is
+    // wrong walks again, all at once, from that end (round 4 repaired them one wave per round
+    // in wave order).  The first wrong wave's predecessor walked from its final start (by
+    // induction from wave 0), so each round fixes at least one more wave: at most NW - 1 repair
+    // rounds, the records equal the serial parse's whatever the predictions.  Where a wave's
+    // last match end does not depend on where it starts -- a run broken inside it, as at the
+    // filter byte of every row of a filtered stream -- one round fixes every wave
+    // (scripts/carry_sim.py: G_FAKE with the Up/Sub/adaptive filter, 6.9 serial rounds per
+    // segment before, 1.5 now).  (One call site of the walk: two inlined copies spill
     // registers to scratch.)
-    auto pred = [&](uint32_t j) -> uint32_t {  // (uniform) wave j's predicted start
-        const uint32_t s = j * (uint32_t)C::SUB;
-        return j && ((reachm >> (j - 1)) & 1u) ? 258u * ((s + 257u) / 258u) : s;
-    };
-    // (nothing but reachm stays live across the walks: SGPR spills)
+    uint32_t st = ss;  // (uniform) the start of this wave's current records
+    if (w && ((reachm >> (w - 1)) & 1u)) st = 258u * ((ss + 257u) / 258u);
+    uint32_t cur = 0;
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
         bool go = j == 0 && active && !skip;
-        uint32_t o0 = j == 0 ? pred(w) - ss : 0u;
-        if (j) {
-            if (((reachm >> (j - 1)) & 1u) == 0) continue;  // (uniform) wave j's start is final
-            if (w == j) {
-                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[j - 1]);
-                const uint32_t a = c > ss ? c : ss;
-                if (a != pred(w)) {
-                    go = active && !skip;
-                    o0 = a - ss;
-                }
+        uint32_t o0 = st - ss;
+        if (j && w) {
+            const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[cur ^ 1u][w - 1]);
+            const uint32_t a = c > ss ? c : ss;
+            if (a != st) {
+                st = a;
+                go = active && !skip;
+                o0 = a - ss;
             }
         }
         if (go) walk(o0);
         if (reachm == 0) break;  // (uniform) no match runs into another wave: no barrier at all
-        if ((j == 0 || w == j) && lane == 0) S.w_end[w] = last_end > se ? last_end : 0u;
-        __syncthreads();
-        if (j == 0) {
-            uint32_t f = (uint32_t)C::NW;
-            for (uint32_t i = 1; i < (uint32_t)C::NW; i++) {
-                if (((reachm >> (i - 1)) & 1u) == 0) continue;
-                const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[i - 1]), si = i * (uint32_t)C::SUB;
-                if ((c > si ? c : si) != pred(i)) {
-                    f = i;
-                    break;
-                }
-            }
-            if (f == (uint32_t)C::NW) break;  // (uniform) every start was right: no more rounds
-            // rounds only from wave f on: the boundaries before wave f - 1's end are final (bit
-            // f - 1 stays set, so reachm stays nonzero)
-            reachm &= 0xFFFFFFFFu << (f - 1);
+        if (lane == 0) {
+            S.w_end[cur][w] = last_end > se ? last_end : 0u;
+            S.w_st[cur][w] = active && !skip ? st : 0xFFFFFFFFu;
         }
+        __syncthreads();
+        // lane i (1 <= i < NW): is wave i's start where wave i - 1's latest walk ends?
+        bool bad = false;
+        if (lane && lane < (uint32_t)C::NW) {
+            const uint32_t c = S.w_end[cur][lane - 1], si = lane * (uint32_t)C::SUB, sv = S.w_st[cur][lane];
+            bad = sv != 0xFFFFFFFFu && (c > si ? c : si) != sv;
+        }
+        if (__ballot(bad) == 0 || j + 1 == (uint32_t)C::NW) break;  // (uniform) every start is final
+        cur ^= 1u;
     }
     // the positions [ss, used) the previous wave's last match covers are not literals here
-    // (w_end[w - 1] holds that match's final end: every write of it is followed by a barrier)
+    // (w_end[cur][w - 1] holds that match's final end: written before the last barrier)
     uint32_t used = 0;
     if (reachm && w) {
-        const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[w - 1]);
+        const uint32_t c = __builtin_amdgcn_readfirstlane(S.w_end[cur][w - 1]);
         used = c > ss ? c : 0u;
     }
     if (used > p0) {

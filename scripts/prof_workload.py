@@ -1,5 +1,5 @@
 """Profiling workload: the bench's batch (4096 x 512^2 uint16 G_NOISE tiles -> PNG), run
-`n` times (default 3), no phase stamps.  Used under rocprofv3 (kernel trace / PMC)."""
+`n` times (default 3), no phase stamps; $PBX_PW_FILTER picks the PNG filter (default None).  Used under rocprofv3 (kernel trace / PMC)."""
 import os
 import sys
 
@@ -9,7 +9,7 @@ import pbx  # noqa: E402
 
 gen = sys.argv[1] if len(sys.argv) > 1 else "noise"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-svc = pbx.PixelsService(device=0)
+svc = pbx.PixelsService(device=0, png_filter=int(os.environ.get("PBX_PW_FILTER", "0")))
 svc.register_plane(1, 0, 0, 0, pbx.UINT16, 32768, 32768, generator=gen)
 ctxs = [pbx.TileCtx(1, 0, 0, 0, (i % 64) * 512, (i // 64) * 512, 512, 512, format="png")
         for i in range(4096)]

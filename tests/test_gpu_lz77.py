@@ -86,3 +86,49 @@ def test_gpu_lz77_matches_emulator(service, case):
             assert g == e, (name, k, wv, [x for x in g if x not in e][:4], [x for x in e if x not in g][:4])
         assert (gh[k] == eh[k]).all(), (name, k, np.nonzero(gh[k] != eh[k])[0][:8],
                                         gh[k][gh[k] != eh[k]][:8], eh[k][gh[k] != eh[k]][:8])
+
+
+def _records(m, nw, wv):
+    n = int(m[wv])
+    return [(int(m[nw + wv * 256 + j]) & 0xFFFF, (int(m[nw + wv * 256 + j]) >> 16) + 3,
+             int(m[nw + nw * 256 + wv * 256 + j]) + 1) for j in range(n)]
+
+
+@pytest.mark.parametrize("filt", [1, 2, 4, 5])
+@pytest.mark.parametrize("kind", ["ramp", "ramp_broken"])
+def test_gpu_lz77_filtered_ramp_rows(oracle, filt, kind):
+    """Row-filtered FakeReader ramps: Up and the adaptive choice turn
+    every row into the filter byte and a run of zeros, Sub into the first sample and a period-2
+    run, so every run breaks at each row's filter byte and k_lz77's predicted wave starts (a
+    258-byte chain from the segment start) are wrong in nearly every wave: the repair rounds
+    must still give the serial parse's records exactly."""
+    rng = np.random.default_rng(11 + filt)
+    w, h = 512, 96
+    a = np.tile((np.arange(w) + 300).astype(np.uint16), (h, 1))
+    if kind == "ramp_broken":  # a few pixels and whole rows off the ramp
+        a.flat[rng.choice(w * h, 24, replace=False)] = rng.integers(0, 65536, 24)
+        a[rng.choice(h, 5, replace=False)] = rng.integers(0, 65536, (5, w))
+    with pbx.PixelsService(png_filter=filt) as svc:
+        iid = 9_600_000 + filt
+        svc.register_plane(iid, 0, 0, 0, pbx.UINT16, w, h, data=a.astype("<u2"), big_endian=False)
+        b = pbx.Batch(svc, [pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="png")])
+        b.launch()
+        b.sync()
+        nseg = b.stats().segments
+        L = _emu.lib()
+        gh, gm = b.lz77_records(nseg, L.pbxemu_hist_words(), L.pbxemu_mrec_words())
+        b.close()
+    tile_be = np.frombuffer(a.astype(">u2").tobytes(), np.uint8)
+    stream = oracle.png_filter_stream(tile_be, pbx.UINT16, w, h, filt).tobytes()
+    eh, em = _emu.lz77(stream, 1 + w * 2)
+    assert gh.shape == eh.shape
+    nw = L.pbxemu_threads() // 64
+    carried = 0
+    for k in range(nseg):
+        for wv in range(nw):
+            g, e = _records(gm[k], nw, wv), _records(em[k], nw, wv)
+            assert g == e, (kind, filt, k, wv, [x for x in g if x not in e][:4], [x for x in e if x not in g][:4])
+            carried += bool(e) and e[-1][0] + e[-1][1] > (wv + 1) * 2048
+        assert (gh[k] == eh[k]).all(), (kind, filt, k, np.nonzero(gh[k] != eh[k])[0][:8])
+    if kind == "ramp":
+        assert carried >= nseg  # matches do run across the wave boundaries here
