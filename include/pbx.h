@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PBX_ABI_VERSION 8
+#define PBX_ABI_VERSION 9
 
 /* Status codes are the HTTP status the reference's event-bus consumer ends with:
  * getTile() == null -> message.fail(404) (PixelBufferVerticle.java:111-114);
@@ -92,6 +92,12 @@ typedef struct pbx_config {
     int32_t tiff_tile;       /* 0 (reference) = TIFF as one strip; T = tiled TIFF (TIFF 6.0 s.15)
                                 of T x T tiles, edge tiles zero-padded; T a multiple of 16 in
                                 [16, 4096]; with tiff_deflate every tile is its own zlib stream */
+    int32_t request_timeout_us; /* deadline of one pbx_get_tile / pbx_node_get_tile call: past it
+                                the call answers PBX_E_INTERNAL (500), as the reference's
+                                event-bus send timeout does (PixelBufferMicroserviceVerticle.java:
+                                148-151 default 15 s, :356-366 timeout -> 500); the late batch's
+                                results are released when it completes.  0 = $PBX_REQUEST_TIMEOUT_US,
+                                else 15,000,000; < 0 = no deadline */
 } pbx_config;
 
 typedef struct pbx_ctx pbx_ctx;
@@ -425,6 +431,12 @@ int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, 
  * context keeps serving.  0 disables.  $PBX_FAIL_BATCH=k does the same for the k-th launch
  * since pbx_init. */
 int pbx_test_fail_batch(pbx_ctx* ctx, uint64_t ahead);
+/* Stall injection (test hook): the `ahead`-th batch launched by this context from now on (1 =
+ * the next) never completes until pbx_test_stall_batch(ctx, 0) releases it (a one-wave kernel
+ * ahead of its kernels spins on a host flag; it also ends by itself after 30 s).  Later batches
+ * queue behind it on the device, as behind a wedged one.  Callers of pbx_get_tile get 500 at
+ * their deadline (pbx_config.request_timeout_us).  0 releases the stall and disarms. */
+int pbx_test_stall_batch(pbx_ctx* ctx, uint64_t ahead);
 
 /* Request sharding across GPUs (one process per GPU, no collectives): the rank that
  * owns a request, by hash of (image, z, c, t, tile column, tile row) for tile_w x tile_h

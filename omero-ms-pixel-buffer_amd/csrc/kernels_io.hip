@@ -413,6 +413,26 @@ hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- test hook: a batch that never completes
+// pbx_test_stall_batch: one wave spins on a flag in mapped pinned host memory until the host
+// clears it, or until `limit` ticks of the constant 100 MHz clock (s_memrealtime) have passed,
+// so the spin always ends on its own.  The batch's kernels queue behind it on its stream: to
+// its callers the batch is a wedged device (the reference's event-bus send timeout,
+// PixelBufferMicroserviceVerticle.java:148-151,352-366).
+__global__ void k_stall(const uint32_t* flag, uint64_t limit) {
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v == 0 || wall_clock64() - t0 >= limit) break;
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+
+hipError_t launch_stall(hipStream_t st, const uint32_t* flag, uint64_t limit_ticks) {
+    hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, st, flag, limit_ticks);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------- K1+K2 fast rows (filter None)
 // The stream of a filter-None PNG tile is row r = [0] ++ big-endian row bytes, and of a
 // deflate-TIFF tile the row bytes alone.  One workgroup per band of RB_ROWS rows (whose

@@ -20,6 +20,9 @@ hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t
 hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch, int32_t sx, int32_t sy,
                              uint8_t* dst, int64_t dpitch, int32_t dx, int32_t dy, int32_t pixel_type,
                              bool be);
+// test hook (pbx_test_stall_batch): one wave spinning until *flag == 0 or limit_ticks of the
+// 100 MHz constant clock
+hipError_t launch_stall(hipStream_t st, const uint32_t* flag, uint64_t limit_ticks);
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
                           uint32_t nblocks, uint8_t* out);
 // Tiled-TIFF headers (IFD + TileOffsets/TileByteCounts), one workgroup per response: after

@@ -320,6 +320,17 @@ struct pbx_ctx {
     // counted over every batch launch of this context; $PBX_FAIL_BATCH or
     // pbx_test_fail_batch) completes with a device failure (500 for its requests)
     std::atomic<uint64_t> launch_seq{0}, fail_at{0};
+    // request deadline of pbx_get_tile (pbx_config.request_timeout_us resolved; <= 0: none)
+    int64_t timeout_us = 15000000;
+    std::atomic<uint64_t> late_requests{0};  // calls answered 500 at their deadline
+    // stall injection (pbx_test_stall_batch): the batch launched with ordinal stall_at starts
+    // behind k_stall, which spins while *stall_flag (mapped pinned host memory) is nonzero
+    std::atomic<uint64_t> stall_at{0};
+    uint32_t* stall_flag = nullptr;
+    // uncoalesced pbx_get_tile calls past their deadline: their tickets and result slots,
+    // finished and released by later calls and by pbx_shutdown
+    std::mutex late_mu;
+    std::vector<std::pair<pbx_ticket*, pbx_result*>> late;
 };
 
 namespace {
@@ -812,6 +823,44 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
     return PBX_OK;
 }
 
+// A pbx_get_tile call past its deadline: 500, as the reference's event-bus reply timeout
+// (PixelBufferMicroserviceVerticle.java:148-151,356-366).
+static int deadline_result(pbx_ctx* ctx, const pbx_tile_req& r, pbx_result* out) {
+    ctx->late_requests++;
+    out->status = PBX_E_INTERNAL;
+    out->format = r.format;
+    out->w = r.w;
+    out->h = r.h;
+    out->data = nullptr;
+    out->len = 0;
+    out->owner = nullptr;
+    return fail(PBX_E_INTERNAL, "request deadline of %lld us exceeded", (long long)ctx->timeout_us);
+}
+
+// Uncoalesced calls that passed their deadline: finish the batches that have completed (all
+// of them when `block`), release their results and free their slots.
+static void collect_late(pbx_ctx* ctx, bool block) {
+    std::vector<std::pair<pbx_ticket*, pbx_result*>> todo, keep;
+    {
+        std::lock_guard<std::mutex> g(ctx->late_mu);
+        todo.swap(ctx->late);
+    }
+    if (todo.empty()) return;
+    const std::string err = g_err;  // (the caller's last error survives the collection)
+    for (auto& tr : todo) {
+        if (pbx_wait(ctx, tr.first, block ? -1 : 0) == PBX_E_PENDING) {
+            keep.push_back(tr);
+            continue;
+        }
+        pbx_results_release(ctx, tr.second, 1);
+        delete[] tr.second;
+    }
+    g_err = err;
+    if (keep.empty()) return;
+    std::lock_guard<std::mutex> g(ctx->late_mu);
+    ctx->late.insert(ctx->late.end(), keep.begin(), keep.end());
+}
+
 // Request coalescer behind pbx_get_tile: the reference runs getTile on up to
 // worker_pool_size concurrent Vert.x worker threads, one request each
 // (PixelBufferMicroserviceVerticle.java:117-118,224-233; PixelBufferVerticle.java:109-110).
@@ -822,10 +871,12 @@ static int run_batch(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_res
 // back) and wake their callers.
 struct Coalescer {
     static constexpr size_t MAX_BATCH = 1 << 16;
+    // Heap-allocated: a caller that gives up at its deadline leaves it to the completer, which
+    // releases the late result and frees it (abandoned).
     struct Pending {
         pbx_tile_req req;
-        pbx_result* out;
-        bool done = false;
+        pbx_result res{};
+        bool done = false, abandoned = false;
         int rc = PBX_OK;
         std::string err;
         std::condition_variable cv;  // this caller only: no thundering herd per batch
@@ -875,17 +926,42 @@ struct Coalescer {
         launcher.join();
         for (auto& t : completers) t.join();
     }
+    // One request, blocking until its batch is fetched or its deadline (ctx->timeout_us, the
+    // reference's event-bus send timeout, PixelBufferMicroserviceVerticle.java:148-151) has
+    // passed: then 500 (:356-366).  A request still queued is withdrawn; one whose batch is in
+    // flight is abandoned to the completer, which releases its result when the batch ends.
     int submit(const pbx_tile_req& r, pbx_result* out) {
-        Pending p;
-        p.req = r;
-        p.out = out;
+        Pending* p = new Pending();
+        p->req = r;
         std::unique_lock<std::mutex> g(mu);
-        if (stop) return fail(PBX_E_INTERNAL, "context is shutting down");
-        queue.push_back(&p);
+        if (stop) {
+            delete p;
+            return fail(PBX_E_INTERNAL, "context is shutting down");
+        }
+        queue.push_back(p);
         cv_launch.notify_one();
-        p.cv.wait(g, [&] { return p.done; });
-        if (p.rc != PBX_OK) g_err = p.err;
-        return p.rc;
+        const int64_t to = ctx->timeout_us;
+        if (to > 0) {
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(to);
+            if (!p->cv.wait_until(g, until, [&] { return p->done; })) {
+                const auto it = std::find(queue.begin(), queue.end(), p);
+                if (it != queue.end()) {
+                    queue.erase(it);
+                    delete p;
+                } else {
+                    p->abandoned = true;
+                }
+                g.unlock();
+                return deadline_result(ctx, r, out);
+            }
+        } else {
+            p->cv.wait(g, [&] { return p->done; });
+        }
+        *out = p->res;
+        const int rc = p->rc;
+        if (rc != PBX_OK) g_err = p->err;
+        delete p;
+        return rc;
     }
     void launch_loop() {
         (void)hipSetDevice(ctx->device);
@@ -939,7 +1015,7 @@ struct Coalescer {
                 if (f.rc != PBX_OK) f.err = g_err;
             }
             for (size_t i = 0; i < n; i++) {
-                pbx_result& o = *f.reqs[i]->out;
+                pbx_result& o = f.reqs[i]->res;
                 if (f.rc == PBX_OK) {
                     o = res[i];
                 } else {
@@ -954,15 +1030,24 @@ struct Coalescer {
                 }
             }
             if (f.b) pbx_batch_destroy(ctx, f.b);
+            std::vector<Pending*> late;  // callers gone at their deadline
             {
                 std::lock_guard<std::mutex> g(mu);
                 for (Pending* p : f.reqs) {
+                    if (p->abandoned) {
+                        late.push_back(p);
+                        continue;
+                    }
                     p->rc = f.rc;
                     p->err = f.err;
                     p->done = true;
                     p->cv.notify_one();  // under mu: the caller cannot return (and free p) first
                 }
                 inflight--;
+            }
+            for (Pending* p : late) {
+                pbx_results_release(ctx, &p->res, 1);
+                delete p;
             }
             cv_launch.notify_one();
             cv_complete.notify_all();  // (shutdown: the other completers see inflight == 0)
@@ -1030,6 +1115,8 @@ int pbx_config_default(pbx_config* cfg) {
     if (td) cfg->tiff_deflate = atoi(td);
     const char* tt = getenv("PBX_TIFF_TILE");
     if (tt) cfg->tiff_tile = atoi(tt);
+    cfg->request_timeout_us = 15000000;  // the reference's event-bus send timeout (15 s)
+    if (const char* rt = getenv("PBX_REQUEST_TIMEOUT_US")) cfg->request_timeout_us = atoi(rt);
     return PBX_OK;
 }
 
@@ -1056,6 +1143,11 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     ctx->device = dev;
     ctx->cfg = cfg;
     ctx->hpool.pinned = true;
+    ctx->timeout_us = cfg.request_timeout_us;
+    if (ctx->timeout_us == 0) {
+        const char* rt = getenv("PBX_REQUEST_TIMEOUT_US");
+        ctx->timeout_us = rt ? atoll(rt) : 15000000;
+    }
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
@@ -1084,8 +1176,10 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
 
 void pbx_shutdown(pbx_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 0u, __ATOMIC_SEQ_CST);  // a stalled batch ends
     delete ctx->coal;  // drains queued requests, joins its threads
     ctx->coal = nullptr;
+    collect_late(ctx, true);
     (void)hipSetDevice(ctx->device);
     (void)sync_kernel_streams(ctx);
     (void)hipStreamSynchronize(ctx->copy_stream);
@@ -1105,6 +1199,7 @@ void pbx_shutdown(pbx_ctx* ctx) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
+    if (ctx->stall_flag) (void)hipHostFree(ctx->stall_flag);
     delete ctx;
 }
 
@@ -2413,6 +2508,8 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     b->ordinal = ++ctx->launch_seq;
     b->inject_fail = b->ordinal == ctx->fail_at.load();
     HIP_TRY(hipEventRecord(b->ev[0], st));
+    if (b->ordinal == ctx->stall_at.load() && ctx->stall_flag)  // test hook: a wedged batch
+        HIP_TRY(launch_stall(st, ctx->stall_flag, 30ull * 100000000ull));
     if (nft) HIP_TRY(hipMemcpyAsync(b->d_ft, b->h_desc, ft_bytes, hipMemcpyHostToDevice, st));
     if (ndt)
         HIP_TRY(hipMemcpyAsync(b->d_dt, (uint8_t*)b->h_desc + ft_bytes, dt_bytes, hipMemcpyHostToDevice, st));
@@ -2865,9 +2962,53 @@ int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {
 
 int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
     if (!ctx || !req || !out) return fail(PBX_E_BADARG, "null argument");
-    const int st = ctx->coal ? ctx->coal->submit(*req, out) : run_batch(ctx, req, 1, out);
+    int st;
+    if (ctx->coal) {
+        st = ctx->coal->submit(*req, out);
+    } else if (ctx->timeout_us <= 0) {
+        st = run_batch(ctx, req, 1, out);
+    } else {  // one batch per call, waited for until the deadline
+        collect_late(ctx, false);
+        const auto t0 = std::chrono::steady_clock::now();
+        pbx_result* own = new pbx_result[1]();
+        pbx_ticket* t = nullptr;
+        st = pbx_submit(ctx, req, 1, own, &t);
+        if (st == PBX_OK) {
+            const int64_t spent = std::chrono::duration_cast<std::chrono::microseconds>(
+                std::chrono::steady_clock::now() - t0).count();
+            st = pbx_wait(ctx, t, std::max<int64_t>(0, ctx->timeout_us - spent));
+            if (st == PBX_E_PENDING) {
+                {
+                    std::lock_guard<std::mutex> g(ctx->late_mu);
+                    ctx->late.emplace_back(t, own);
+                }
+                return deadline_result(ctx, *req, out);
+            }
+            *out = own[0];
+        }
+        delete[] own;
+    }
     if (st) return st;
     return out->status;
+}
+
+int pbx_test_stall_batch(pbx_ctx* ctx, uint64_t ahead) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    if (!ahead) {  // release: no lock, a launch may be waiting behind the stalled batch
+        ctx->stall_at = 0;
+        if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 0u, __ATOMIC_SEQ_CST);
+        return PBX_OK;
+    }
+    std::lock_guard<std::mutex> run(ctx->run_mu);  // launches are ordered under run_mu
+    if (ensure_device(ctx)) return PBX_E_INTERNAL;
+    if (!ctx->stall_flag) {
+        void* p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        ctx->stall_flag = (uint32_t*)p;
+    }
+    __atomic_store_n(ctx->stall_flag, 1u, __ATOMIC_SEQ_CST);
+    ctx->stall_at = ctx->launch_seq.load() + ahead;
+    return PBX_OK;
 }
 
 int pbx_test_fail_batch(pbx_ctx* ctx, uint64_t ahead) {

@@ -53,7 +53,8 @@ class PbxConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("png_filter", ctypes.c_int32),
                 ("tiff_deflate", ctypes.c_int32), ("segment_bytes", ctypes.c_int32),
                 ("max_batch_bytes", ctypes.c_uint64), ("coalesce", ctypes.c_int32),
-                ("stage_rows", ctypes.c_int32), ("tiff_tile", ctypes.c_int32)]
+                ("stage_rows", ctypes.c_int32), ("tiff_tile", ctypes.c_int32),
+                ("request_timeout_us", ctypes.c_int32)]
 
 
 class PbxPlaneDesc(ctypes.Structure):
@@ -136,6 +137,7 @@ EXPORTS = [
     "pbx_residency_stats_get", "pbx_test_fail_batch", "pbx_node_init", "pbx_node_shutdown",
     "pbx_node_size", "pbx_node_context", "pbx_node_route", "pbx_node_get_tile",
     "pbx_plane_create_sparse", "pbx_band_write", "pbx_plane_band_info", "pbx_result_spans",
+    "pbx_test_stall_batch",
 ]
 
 _lib = None
@@ -207,6 +209,7 @@ def lib() -> ctypes.CDLL:
     L.pbx_test_huffman.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 2 + [ctypes.c_uint32] + \
         [ctypes.c_void_p] * 2
     L.pbx_test_fail_batch.argtypes = [vp, u64]
+    L.pbx_test_stall_batch.argtypes = [vp, u64]
     L.pbx_plane_create_sparse.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), i32, i32, i32, ctypes.POINTER(u64)]
     L.pbx_band_write.argtypes = [vp, u64, i32, i32, vp, u64]
     L.pbx_plane_band_info.argtypes = [vp, u64, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
@@ -442,7 +445,7 @@ def ngff_multiscales(image_dir: str):
 
 def make_config(device: Optional[int] = None, png_filter: int = FILTER_NONE,
                 tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False,
-                tiff_tile: Optional[int] = None) -> PbxConfig:
+                tiff_tile: Optional[int] = None, request_timeout_us: Optional[int] = None) -> PbxConfig:
     cfg = PbxConfig()
     _check(lib().pbx_config_default(ctypes.byref(cfg)))
     cfg.device = -1 if device is None else device
@@ -452,6 +455,8 @@ def make_config(device: Optional[int] = None, png_filter: int = FILTER_NONE,
     cfg.stage_rows = 1 if stage_rows else 0
     if tiff_tile is not None:  # else $PBX_TIFF_TILE or 0 (one strip, the reference's)
         cfg.tiff_tile = int(tiff_tile)
+    if request_timeout_us is not None:  # else $PBX_REQUEST_TIMEOUT_US or 15 s (the event-bus send timeout)
+        cfg.request_timeout_us = int(request_timeout_us)
     return cfg
 
 
@@ -464,7 +469,8 @@ class PixelsService:
 
     def __init__(self, device: Optional[int] = None, png_filter: int = FILTER_NONE,
                  tiff_deflate: bool = False, coalesce: bool = True, stage_rows: bool = False,
-                 tiff_tile: Optional[int] = None, sparse_band_rows: int = 0, _handle=None):
+                 tiff_tile: Optional[int] = None, sparse_band_rows: int = 0,
+                 request_timeout_us: Optional[int] = None, _handle=None):
         """sparse_band_rows > 0: planes the handler opens on demand are sparse planes of bands
         of that many rows (region-proportional residency); 0: whole planes (or the handler's
         row band)."""
@@ -477,7 +483,8 @@ class PixelsService:
             self._h = ctypes.c_void_p(_handle)
             return
         L = lib()
-        cfg = make_config(device, png_filter, tiff_deflate, coalesce, stage_rows, tiff_tile)
+        cfg = make_config(device, png_filter, tiff_deflate, coalesce, stage_rows, tiff_tile,
+                          request_timeout_us)
         h = ctypes.c_void_p()
         _check(L.pbx_init(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -755,6 +762,11 @@ class PixelsService:
     def test_fail_batch(self, ahead: int) -> None:
         """Fault injection: the `ahead`-th batch launched from now on fails (500s); 0 = off."""
         _check(lib().pbx_test_fail_batch(self._h, ahead))
+
+    def test_stall_batch(self, ahead: int) -> None:
+        """Stall injection: the `ahead`-th batch launched from now on does not complete until
+        test_stall_batch(0) releases it (its callers get 500 at their deadline)."""
+        _check(lib().pbx_test_stall_batch(self._h, ahead))
 
     # ------------------------------------------------------------- opening planes on demand
     def _exclusive(self, key):

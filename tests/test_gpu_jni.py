@@ -6,7 +6,8 @@ handler of INTEGRATION.md §2 runs (TileRequestHandler.java:84-128; PixelBufferV
 (2.18 GB: more than a Java byte[] holds), commitPlane, getTile raw / png / tif (rows above
 2 GiB), NOT_RESIDENT, the reference's 404s (region, format "jpg" on a resident and on a cold
 image, Java-int overflow), registerZarr of a c-blosc 1.21 fixture, and an injected device
-failure (RuntimeException -> 500) after which the context keeps serving.  Every body is
+failure (RuntimeException -> 500) after which the context keeps serving, and a stalled batch
+(RuntimeException -> 500 at the request deadline, then served again).  Every body is
 checked against the CPU oracle."""
 import json
 import os
@@ -29,8 +30,9 @@ def test_jni_shim_on_real_library(tmp_path, oracle):
     if not os.path.exists(EXE):  # built by __graft_entry__.build(); gcc is on the box as well
         subprocess.check_call(["make", "-s", "-C", MOCK])
     enc = os.path.join(ROOT, "tests", "golden", "zarr", ZARR + ".enc")
+    env = dict(os.environ, PBX_REQUEST_TIMEOUT_US="3000000")  # the "stalled" request's deadline
     out = subprocess.run([EXE, str(tmp_path), enc, "77", "100"], capture_output=True, text=True,
-                         timeout=240)
+                         timeout=240, env=env)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "jni real ok" in out.stdout
     tiles, served_by = {}, {}
@@ -84,6 +86,14 @@ def test_jni_shim_on_real_library(tmp_path, oracle):
     st, body, _, _ = tiles["after_failure"]
     r, px, _ = oracle.png_decode(body)
     assert st == 0 and r == 0 and px == want(512, 512, 512, 512)
+    # a stalled batch: RuntimeException (500) at the 3 s deadline; released, the next is served
+    assert tiles["stalled"][0] == 500 and tiles["stalled"][1] is None
+    assert "EXC stalled java/lang/RuntimeException" in out.stdout
+    stall_ms = int(out.stdout.split("STALL_MS ")[1].split()[0])
+    assert 3000 <= stall_ms < 5000, stall_ms
+    st, body, _, _ = tiles["after_stall"]
+    r, px, _ = oracle.png_decode(body)
+    assert st == 0 and r == 0 and px == want(1024, 1024, 512, 512)
     # the node: misses name the context owning the rows, the bands loaded there serve them
     assert tiles["node_a_miss"][0] == 460 and served_by["node_a_miss"] == 0
     assert tiles["node_b_miss"][0] == 460 and served_by["node_b_miss"] == 1

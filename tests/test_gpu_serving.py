@@ -5,6 +5,8 @@
 * the reference's 404s are answered before anything is loaded (:84, :100-103, :125-132);
 * a device failure fails its batch with 500 and nothing else (PixelBufferVerticle.java:
   131-146; SURVEY.md §5 fault injection), through the coalescer and the batch paths;
+* a batch that never completes answers 500 at the request deadline (the event-bus send
+  timeout, PixelBufferMicroserviceVerticle.java:148-151,356-366) and nothing else;
 * N device contexts in one process (the reference's one JVM, PixelBufferMicroserviceVerticle.
   java:117-118,224-233): requests routed by band ownership and pbx_shard_of.
 
@@ -12,6 +14,7 @@ Every body is checked against the CPU oracle (oracle/pbx_oracle.c).
 """
 import itertools
 import threading
+import time
 import zlib
 from concurrent.futures import ThreadPoolExecutor
 
@@ -250,6 +253,100 @@ def test_failed_batch_is_500_for_its_requests_only(oracle):
         assert all(s == (404 if r.x == side - 10 else 0) for r, (s, _) in zip(reqs[:8], t1.wait()))
         assert all(s == (404 if r.x == side - 10 else 500) for r, (s, _) in zip(reqs[8:16], t2.wait()))
         assert [s for s, _ in svc.get_tiles(reqs[16:24])] == [404 if r.x == side - 10 else 0 for r in reqs[16:24]]
+
+
+def _check_body(oracle, tc, st, body, pt, seed):
+    assert st == pbx.OK, st
+    want = oracle.gen_region(NOISE, pt, tc.x, tc.y, tc.w, tc.h, seed=seed)
+    if tc.format is None:
+        assert body == want.tobytes()
+    elif tc.format == "png":
+        r, px, _ = oracle.png_decode(body)
+        assert r == 0 and px == want.tobytes()
+    else:
+        assert body == oracle.tiff_encode(want, pt, tc.w, tc.h)[1]
+
+
+def test_stalled_batch_answers_500_at_deadline(oracle):
+    """the reference bounds every getTile by the event-bus send timeout
+    (PixelBufferMicroserviceVerticle.java:148-151; a timeout is a 500, :356-366).  A batch that
+    never completes (pbx_test_stall_batch: its kernels queue behind a spinning wave) answers its
+    caller 500 at pbx_config.request_timeout_us while 31 other callers, whose batches queue
+    behind it on the device, get every body exact once the stall is released; no caller stays
+    parked, and the context serves normally afterwards, on every path."""
+    iid = next(_ids)
+    pt, side, seed = pbx.UINT16, 4096, 12
+    D = 1.5  # seconds
+    with pbx.PixelsService(request_timeout_us=int(D * 1e6)) as svc:
+        svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=seed)
+        rng = np.random.default_rng(6)
+        reqs = []
+        for k in range(256):
+            x, y = (int(v) for v in rng.integers(0, side - 256, 2))
+            reqs.append(pbx.TileCtx(iid, 0, 0, 0, x, y, 256, 256, format=["png", None, "tif"][k % 3]))
+        st, body = svc.get_tile(reqs[0])  # warm: the first batch allocates the pools
+        _check_body(oracle, reqs[0], st, body, pt, seed)
+        svc.test_stall_batch(1)
+        stalled = {}
+
+        def caller_a():
+            t = time.monotonic()
+            stalled["res"] = svc.get_tile(reqs[1])
+            stalled["s"] = time.monotonic() - t
+
+        ta = threading.Thread(target=caller_a)
+        ta.start()
+        time.sleep(0.6)  # the stalled batch holds reqs[1] alone; the rest queue behind it
+        out = [None] * len(reqs)
+
+        def worker(w):
+            for j in range(2 + w, len(reqs), 31):
+                out[j] = svc.get_tile(reqs[j])
+
+        with ThreadPoolExecutor(31) as ex:
+            futs = [ex.submit(worker, w) for w in range(31)]
+            ta.join(timeout=D + 5)
+            assert not ta.is_alive(), "the stalled request's caller is still parked"
+            svc.test_stall_batch(0)  # release: the late batch completes, the queue drains
+            for f in futs:
+                f.result(timeout=60)
+        st, body = stalled["res"]
+        assert st == pbx.E_INTERNAL and body is None
+        assert D - 0.05 <= stalled["s"] < D + 1.0, stalled["s"]
+        for j in range(2, len(reqs)):
+            _check_body(oracle, reqs[j], *out[j], pt, seed)
+        # the context serves on: coalescer, event-bus consumer, batches
+        _check_body(oracle, reqs[1], *svc.get_tile(reqs[1]), pt, seed)
+        st, _, _ = pbx.handle_get_tile(svc, reqs[2].to_json())
+        assert st == 200
+        svc.test_stall_batch(1)
+        t = time.monotonic()
+        st, _, _ = pbx.handle_get_tile(svc, reqs[3].to_json())  # the event-bus reply: 500
+        assert st == 500 and time.monotonic() - t < D + 1.0
+        svc.test_stall_batch(0)
+        res = svc.get_tiles(reqs[:8])
+        for tc, (st, body) in zip(reqs[:8], res):
+            _check_body(oracle, tc, st, body, pt, seed)
+    # one batch per call (coalesce off) and the node's routed call take the same deadline
+    with pbx.PixelsService(coalesce=False, request_timeout_us=int(D * 1e6)) as svc:
+        svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=seed)
+        _check_body(oracle, reqs[0], *svc.get_tile(reqs[0]), pt, seed)
+        svc.test_stall_batch(1)
+        t = time.monotonic()
+        st, body = svc.get_tile(reqs[1])
+        assert st == pbx.E_INTERNAL and body is None and D - 0.05 <= time.monotonic() - t < D + 1.0
+        svc.test_stall_batch(0)
+        for tc in reqs[2:6]:  # (the first of them also collects the late batch)
+            _check_body(oracle, tc, *svc.get_tile(tc), pt, seed)
+    with pbx.PixelsNode(1, devices=[0], request_timeout_us=int(D * 1e6)) as node:
+        node.services[0].register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=seed)
+        node.services[0].test_stall_batch(1)
+        t = time.monotonic()
+        st, body, k = node.get_tile(reqs[1])
+        assert st == pbx.E_INTERNAL and body is None and time.monotonic() - t < D + 1.0
+        node.services[0].test_stall_batch(0)
+        st, body, k = node.get_tile(reqs[2])
+        _check_body(oracle, reqs[2], st, body, pt, seed)
 
 
 # ---------------------------------------------------------------- node routing

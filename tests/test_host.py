@@ -50,7 +50,7 @@ def test_jni_shim_matches_abi():
 
 def test_enums_and_names():
     L = pbx.lib()
-    assert L.pbx_abi_version() == 8
+    assert L.pbx_abi_version() == 9
     assert L.pbx_format_from_string(None) == pbx.FMT_RAW
     assert L.pbx_format_from_string(b"png") == pbx.FMT_PNG
     assert L.pbx_format_from_string(b"tif") == pbx.FMT_TIF
