@@ -203,11 +203,20 @@ int pbx_plane_create_sparse(pbx_ctx* ctx, const pbx_plane_desc* desc, int32_t ba
 /* Rows [y0, y0 + rows) of ONE band (packed, desc->byte_order), as getTileDirect(z, c, t, 0, y0,
  * sizeX, rows) returns them; the first write of an absent band allocates it (507 if it cannot be
  * made to fit), the write that completes it makes it resident.  409 if the band is resident (or
- * another caller is allocating it).  data == NULL: generate the rows (generator planes). */
+ * another caller is allocating it).  data == NULL: generate the rows (generator planes).  A
+ * failed write fails the band's whole load (every writer of it: load it again). */
 int pbx_band_write(pbx_ctx* ctx, uint64_t plane_id, int32_t y0, int32_t rows, const void* data,
                    uint64_t bytes);
+/* A loader that gives up on the band holding row y0 part-way (a failed piece, a Java exception
+ * between pieces): the band goes back to absent and its HBM is returned (at once, or by the last
+ * write still in flight); a resident or absent band is left as it is.  A write that fails does
+ * the same by itself, and a band left loading with no write for 10 s is started over by the
+ * next writer (or evicted).  400 for a plane that is not sparse. */
+int pbx_band_abort(pbx_ctx* ctx, uint64_t plane_id, int32_t y0);
 /* band_rows and the number of bands of a sparse plane; states (may be NULL, nbands entries):
- * 0 absent (never loaded, or evicted), 1 loading, 2 resident.  400 for a plane that is not sparse. */
+ * 0 absent (never loaded, or evicted), 1 loading, 2 resident.  A band whose load failed, or that
+ * has been loading without a write for 10 s (a loader that went away), reads as 0 and its HBM is
+ * returned.  400 for a plane that is not sparse. */
 int pbx_plane_band_info(pbx_ctx* ctx, uint64_t plane_id, int32_t* band_rows, int32_t* nbands, uint8_t* states);
 
 /* HBM residency budget for planes (bytes; 0 = none, the default, or $PBX_HBM_BUDGET_MB).  A
@@ -437,6 +446,9 @@ int pbx_test_fail_batch(pbx_ctx* ctx, uint64_t ahead);
  * queue behind it on the device, as behind a wedged one.  Callers of pbx_get_tile get 500 at
  * their deadline (pbx_config.request_timeout_us).  0 releases the stall and disarms. */
 int pbx_test_stall_batch(pbx_ctx* ctx, uint64_t ahead);
+/* Upload failure injection (test hook): the `ahead`-th pbx_band_write from now on fails after
+ * joining its band's load, as a failed host-to-device copy would.  0 disables. */
+int pbx_test_fail_band_write(pbx_ctx* ctx, uint64_t ahead);
 
 /* Request sharding across GPUs (one process per GPU, no collectives): the rank that
  * owns a request, by hash of (image, z, c, t, tile column, tile row) for tile_w x tile_h

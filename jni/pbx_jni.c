@@ -405,6 +405,8 @@ JNIEXPORT jboolean JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNati
         const int32_t k = rows - r < per ? rows - r : per;
         (*env)->GetByteArrayRegion(env, data, off + r * row_bytes, k * row_bytes, buf);
         if ((*env)->ExceptionCheck(env)) {
+            /* the pieces written so far would leave the band loading: give it back */
+            if (r) (void)pbx_band_abort(PBX_CTX(ctx), (uint64_t)plane, y0);
             ok = JNI_FALSE;
             break;
         }
@@ -413,7 +415,7 @@ JNIEXPORT jboolean JNICALL Java_com_glencoesoftware_omero_ms_pixelbuffer_PbxNati
             ok = JNI_FALSE;
             break;
         }
-        if (st != PBX_OK) {
+        if (st != PBX_OK) {  /* (a failed write has already reset the band) */
             throw_status(env, st);
             ok = JNI_FALSE;
             break;

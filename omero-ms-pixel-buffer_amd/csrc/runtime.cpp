@@ -79,6 +79,10 @@ enum BandState : int { BS_ABSENT = 0, BS_LOADING = 1, BS_READY = 2 };
 // that was to read them, and every request is loaded again and again.  A
 // loader that finds only fresh or pinned memory gets PBX_E_NO_SPACE and retries later.
 constexpr int64_t FRESH_NS = 2000000000;
+// A band left BS_LOADING with no writer for this long (a loader that failed part-way or went
+// away) is reclaimed: the next writer starts it over, and eviction may return its HBM
+// (pbx_ctx::stale_ns; $PBX_BAND_STALE_MS for tests).
+constexpr int64_t STALE_NS = 10000000000;
 inline int64_t mono_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
@@ -93,6 +97,8 @@ struct Band {
     int64_t fresh_until = 0;     // loaded, not served yet: not evicted before this (fresh_now)
     uint32_t rows_left = 0;      // BS_LOADING: rows not written yet
     int32_t writers = 0;         // pbx_band_write calls in flight
+    bool failed = false;         // BS_LOADING: a write failed; the last writer out resets the band
+    int64_t touched = 0;         // BS_LOADING: mono_ns of the last write activity
     std::vector<uint8_t> rows_done;
 };
 
@@ -331,6 +337,8 @@ struct pbx_ctx {
     // finished and released by later calls and by pbx_shutdown
     std::mutex late_mu;
     std::vector<std::pair<pbx_ticket*, pbx_result*>> late;
+    int64_t stale_ns = STALE_NS;  // a loading band without writers this long is reclaimed
+    std::atomic<uint64_t> band_writes{0}, fail_band_write_at{0};  // pbx_test_fail_band_write
 };
 
 namespace {
@@ -548,12 +556,15 @@ bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_fr
         Plane* p = kv.second;
         if (!p->indexed || p->state != PS_READY) continue;
         if (p->sparse_rows) {
-            for (Band& b : p->bands)
-                if (b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now && b.last_use < best) {
-                    best = b.last_use;
+            for (Band& b : p->bands) {
+                const bool stale = b.state == BS_LOADING && b.writers == 0 && b.dev && now - b.touched > ctx->stale_ns;
+                const uint64_t age = stale ? 0 : b.last_use;  // stale loads go first
+                if (((b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now) || stale) && age < best) {
+                    best = age;
                     v = p;
                     vb = &b;
                 }
+            }
         } else if (p->pins == 0 && p->dev && p->fresh_until <= now && p->last_use < best) {
             best = p->last_use;
             v = p;
@@ -570,6 +581,8 @@ bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_fr
     *dev = nullptr;
     if (vb) {
         vb->state = BS_ABSENT;
+        vb->rows_done.clear();
+        vb->failed = false;
         ctx->band_evictions++;
     } else {
         v->state = PS_EVICTED;
@@ -586,7 +599,9 @@ uint64_t idle_bytes_locked(pbx_ctx* ctx) {
         if (!p->indexed || p->state != PS_READY) continue;
         if (p->sparse_rows) {
             for (const Band& b : p->bands)
-                if (b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now) idle += b.bytes;
+                if ((b.state == BS_READY && b.pins == 0 && b.dev && b.fresh_until <= now) ||
+                    (b.state == BS_LOADING && b.writers == 0 && b.dev && now - b.touched > ctx->stale_ns))
+                    idle += b.bytes;
         } else if (p->pins == 0 && p->dev && p->fresh_until <= now) {
             idle += p->bytes;
         }
@@ -1168,6 +1183,7 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
         return fail(PBX_E_INTERNAL, "init: %s", hipGetErrorString(e));
     }
     if (const char* fb = getenv("PBX_FAIL_BATCH")) ctx->fail_at = strtoull(fb, nullptr, 10);
+    if (const char* bs = getenv("PBX_BAND_STALE_MS")) ctx->stale_ns = (int64_t)atoll(bs) * 1000000;
     ctx->reaper.start(dev);
     if (cfg.coalesce) ctx->coal = new Coalescer(ctx);
     *out = ctx;
@@ -1186,7 +1202,9 @@ void pbx_shutdown(pbx_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->upload_stream);
     ctx->reaper.finish();  // frees what it still holds
     for (auto& kv : ctx->planes) {  // records of released planes still pinned by undestroyed
-        (void)hipFree(kv.second->dev);  // batches are leaked with those batches
+        std::vector<std::pair<void*, size_t>> blocks;  // batches are leaked with those batches
+        kv.second->memory(blocks);  // the whole plane's HBM, or every resident band's
+        for (auto& m : blocks) (void)hipFree(m.first);
         delete kv.second;
     }
     ctx->planes.clear();
@@ -1578,6 +1596,24 @@ int pbx_plane_create_sparse(pbx_ctx* ctx, const pbx_plane_desc* d, int32_t band_
 
 namespace {
 
+// A loading band back to absent (under reg_mu); its HBM goes to `to_free`.
+void band_reset_locked(Band& b, std::vector<std::pair<void*, size_t>>& to_free) {
+    if (b.dev) to_free.emplace_back(b.dev, b.bytes);
+    b.dev = nullptr;
+    b.state = BS_ABSENT;
+    b.rows_done.clear();
+    b.rows_left = 0;
+    b.failed = false;
+}
+
+// free_planes under reg_mu (the memory goes to the reaper, the bytes stop counting)
+void free_planes_locked(pbx_ctx* ctx, const std::vector<std::pair<void*, size_t>>& to_free) {
+    for (auto& f : to_free) {
+        ctx->reaper.put(f.first);
+        ctx->resident_bytes -= f.second;
+    }
+}
+
 // Rows [y0, y0 + rows) of one band of a sparse plane: the first write of an absent band
 // allocates it (within the budget, evicting idle planes / bands), the last one publishes it.
 // data == NULL on a generator plane generates the rows on the GPU instead.
@@ -1598,47 +1634,56 @@ int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* dat
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     Band& b = q->bands[(size_t)k];
     bool alloc = false;
-    size_t nbytes = 0;
+    const size_t nbytes = (size_t)q->pitch * (size_t)(hi - lo) + 256;
+    std::vector<std::pair<void*, size_t>> stale;
     {
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         if (b.state == BS_READY) return fail(PBX_E_EXISTS, "band %d is resident", k);
+        // a load that failed part-way, or whose loader went away, starts over
+        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || mono_ns() - b.touched > ctx->stale_ns))
+            band_reset_locked(b, stale);
         if (b.state == BS_ABSENT) {
             b.state = BS_LOADING;
+            b.failed = false;
             b.rows_done.assign((size_t)(hi - lo), 0);
             b.rows_left = (uint32_t)(hi - lo);
             alloc = true;
-        } else if (!b.dev) {
-            return fail(PBX_E_EXISTS, "band %d is being allocated by another caller", k);
+        } else if (!b.dev || b.failed) {
+            free_planes_locked(ctx, stale);
+            return fail(PBX_E_EXISTS, "band %d is being allocated (or reset) by another caller", k);
         }
-        nbytes = (size_t)q->pitch * (size_t)(hi - lo) + 256;
         b.writers++;
+        b.touched = mono_ns();
+        free_planes_locked(ctx, stale);
     }
-    auto undo = [&](int rc) {
+    // A failed write fails the whole load: the band is reset (its HBM returned) by the last
+    // writer to leave, never under another writer's upload.
+    auto leave_failed = [&](int rc) {
         const std::string msg = g_err;
         std::vector<std::pair<void*, size_t>> to_free;
         {
             std::lock_guard<std::mutex> g(ctx->reg_mu);
             b.writers--;
-            if (alloc) {  // the band goes back to absent; what it allocated is returned
-                if (b.dev) to_free.emplace_back(b.dev, b.bytes);
-                b.dev = nullptr;
-                b.state = BS_ABSENT;
-                b.rows_done.clear();
-            }
+            b.failed = true;
+            b.touched = mono_ns();
+            if (b.writers == 0) band_reset_locked(b, to_free);
+            free_planes_locked(ctx, to_free);
         }
-        free_planes(ctx, to_free);
         g_err = msg;
         return rc;
     };
     if (alloc) {
         uint8_t* dev = nullptr;
-        if (int rc = plane_alloc(ctx, nbytes, &dev)) return undo(rc);
+        if (int rc = plane_alloc(ctx, nbytes, &dev)) return leave_failed(rc);
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         b.dev = dev;
         b.bytes = nbytes;
     }
     hipError_t e = hipSuccess;
     int rc = PBX_OK;
+    if (++ctx->band_writes == ctx->fail_band_write_at.load())  // test hook: this write's upload fails
+        return leave_failed(fail(PBX_E_INTERNAL, "injected upload failure in band write %llu",
+                                 (unsigned long long)ctx->band_writes.load()));
     {
         std::lock_guard<std::mutex> u(ctx->upload_mu);
         if (alloc) e = hipMemsetAsync(b.dev + (size_t)q->pitch * (size_t)(hi - lo), 0, 256, ctx->upload_stream);
@@ -1653,15 +1698,24 @@ int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* dat
         }
     }
     if (e != hipSuccess) rc = fail(PBX_E_INTERNAL, "band write: %s", hipGetErrorString(e));
-    if (rc) return undo(rc);
+    if (rc) return leave_failed(rc);
     std::lock_guard<std::mutex> g(ctx->reg_mu);
+    if (b.failed || b.state != BS_LOADING || b.rows_done.size() != (size_t)(hi - lo)) {
+        // another writer failed meanwhile: this load is void; the last writer out resets it
+        std::vector<std::pair<void*, size_t>> to_free;
+        b.writers--;
+        if (b.writers == 0) band_reset_locked(b, to_free);
+        free_planes_locked(ctx, to_free);
+        return fail(PBX_E_INTERNAL, "band %d: another write of this load failed; load it again", k);
+    }
     b.writers--;
+    b.touched = mono_ns();
     for (int32_t r = y0 - lo; r < y0 - lo + rows; r++)
         if (!b.rows_done[(size_t)r]) {
             b.rows_done[(size_t)r] = 1;
             b.rows_left--;
         }
-    if (b.rows_left == 0 && b.writers == 0 && b.state == BS_LOADING) {  // the last write publishes it
+    if (b.rows_left == 0 && b.writers == 0) {  // the last write publishes it
         b.rows_done.clear();
         b.rows_done.shrink_to_fit();
         b.state = BS_READY;
@@ -1685,13 +1739,38 @@ int pbx_band_write(pbx_ctx* ctx, uint64_t id, int32_t y0, int32_t rows, const vo
     return rc;
 }
 
+int pbx_band_abort(pbx_ctx* ctx, uint64_t id, int32_t y0) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    std::vector<std::pair<void*, size_t>> to_free;
+    std::lock_guard<std::mutex> g(ctx->reg_mu);
+    auto it = ctx->planes.find(id);
+    if (it == ctx->planes.end() || !it->second->indexed) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
+    Plane* p = it->second;
+    if (!p->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)id);
+    if (y0 < 0 || y0 >= p->size_y) return fail(PBX_E_BADARG, "row %d outside the plane", y0);
+    Band& b = p->bands[(size_t)(y0 / p->sparse_rows)];
+    if (b.state != BS_LOADING) return PBX_OK;
+    b.failed = true;  // writers still in flight: the last one out resets the band
+    if (b.writers == 0) band_reset_locked(b, to_free);
+    free_planes_locked(ctx, to_free);
+    return PBX_OK;
+}
+
 int pbx_plane_band_info(pbx_ctx* ctx, uint64_t id, int32_t* band_rows, int32_t* nbands, uint8_t* states) {
     if (!ctx) return fail(PBX_E_BADARG, "null ctx");
     std::lock_guard<std::mutex> g(ctx->reg_mu);
     auto it = ctx->planes.find(id);
     if (it == ctx->planes.end() || !it->second->indexed) return fail(PBX_E_NOTFOUND, "no plane %llu", (unsigned long long)id);
-    const Plane* p = it->second;
+    Plane* p = it->second;
     if (!p->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)id);
+    // bands left loading by a loader that failed or went away read as absent (and give their
+    // HBM back): a binding waiting for them loads them again
+    std::vector<std::pair<void*, size_t>> stale;
+    const int64_t now = mono_ns();
+    for (Band& b : p->bands)
+        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || now - b.touched > ctx->stale_ns))
+            band_reset_locked(b, stale);
+    free_planes_locked(ctx, stale);
     if (band_rows) *band_rows = p->sparse_rows;
     if (nbands) *nbands = (int32_t)p->bands.size();
     if (states)
@@ -2990,6 +3069,12 @@ int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
     }
     if (st) return st;
     return out->status;
+}
+
+int pbx_test_fail_band_write(pbx_ctx* ctx, uint64_t ahead) {
+    if (!ctx) return fail(PBX_E_BADARG, "null ctx");
+    ctx->fail_band_write_at = ahead ? ctx->band_writes.load() + ahead : 0;
+    return PBX_OK;
 }
 
 int pbx_test_stall_batch(pbx_ctx* ctx, uint64_t ahead) {

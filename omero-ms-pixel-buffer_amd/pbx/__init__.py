@@ -137,7 +137,7 @@ EXPORTS = [
     "pbx_residency_stats_get", "pbx_test_fail_batch", "pbx_node_init", "pbx_node_shutdown",
     "pbx_node_size", "pbx_node_context", "pbx_node_route", "pbx_node_get_tile",
     "pbx_plane_create_sparse", "pbx_band_write", "pbx_plane_band_info", "pbx_result_spans",
-    "pbx_test_stall_batch",
+    "pbx_test_stall_batch", "pbx_band_abort", "pbx_test_fail_band_write",
 ]
 
 _lib = None
@@ -210,8 +210,10 @@ def lib() -> ctypes.CDLL:
         [ctypes.c_void_p] * 2
     L.pbx_test_fail_batch.argtypes = [vp, u64]
     L.pbx_test_stall_batch.argtypes = [vp, u64]
+    L.pbx_test_fail_band_write.argtypes = [vp, u64]
     L.pbx_plane_create_sparse.argtypes = [vp, ctypes.POINTER(PbxPlaneDesc), i32, i32, i32, ctypes.POINTER(u64)]
     L.pbx_band_write.argtypes = [vp, u64, i32, i32, vp, u64]
+    L.pbx_band_abort.argtypes = [vp, u64, i32]
     L.pbx_plane_band_info.argtypes = [vp, u64, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
     L.pbx_node_init.argtypes = [ctypes.POINTER(PbxConfig), i32, ctypes.POINTER(i32), i32, ctypes.POINTER(vp)]
     L.pbx_node_shutdown.argtypes = [vp]
@@ -751,6 +753,10 @@ class PixelsService:
         else:
             _check(lib().pbx_band_write(self._h, plane_id, y0, rows, data, len(data)))
 
+    def band_abort(self, plane_id: int, y0: int) -> None:
+        """pbx_band_abort: give back the band holding row y0 when its load is abandoned."""
+        _check(lib().pbx_band_abort(self._h, plane_id, y0))
+
     def band_info(self, plane_id: int) -> Tuple[int, List[int]]:
         """(band_rows, [state of band k]) of a sparse plane (BS_ABSENT / BS_LOADING / BS_READY)."""
         br, nb = ctypes.c_int32(), ctypes.c_int32()
@@ -762,6 +768,10 @@ class PixelsService:
     def test_fail_batch(self, ahead: int) -> None:
         """Fault injection: the `ahead`-th batch launched from now on fails (500s); 0 = off."""
         _check(lib().pbx_test_fail_batch(self._h, ahead))
+
+    def test_fail_band_write(self, ahead: int) -> None:
+        """Upload failure injection: the `ahead`-th band write from now on fails; 0 = off."""
+        _check(lib().pbx_test_fail_band_write(self._h, ahead))
 
     def test_stall_batch(self, ahead: int) -> None:
         """Stall injection: the `ahead`-th batch launched from now on does not complete until

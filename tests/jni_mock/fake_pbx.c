@@ -115,6 +115,12 @@ int pbx_band_write(pbx_ctx* ctx, uint64_t id, int32_t y0, int32_t rows, const vo
     if (fake.band_exists) return PBX_E_EXISTS;
     return pbx_plane_write_rows(ctx, id, y0, rows, data, bytes);
 }
+int pbx_band_abort(pbx_ctx* ctx, uint64_t id, int32_t y0) {
+    (void)ctx; (void)id;
+    fake.band_aborts++;
+    fake.abort_y0 = y0;
+    return 0;
+}
 int pbx_plane_band_info(pbx_ctx* ctx, uint64_t id, int32_t* band_rows, int32_t* nbands, uint8_t* states) {
     (void)ctx; (void)id;
     if (band_rows) *band_rows = fake.sparse_band_rows;

@@ -6,7 +6,8 @@
 #define FAKE_MAX_WRITES 64
 struct fake_state {
     int init_rc, declare_rc, create_rc, commit_rc, lookup_rc, lookup_state;
-    int creates, commits, releases, nwrites, write_fail_at;
+    int creates, commits, releases, nwrites, write_fail_at, band_aborts;
+    int32_t abort_y0;
     int32_t w_y0[FAKE_MAX_WRITES], w_rows[FAKE_MAX_WRITES];
     uint64_t w_bytes[FAKE_MAX_WRITES];
     uint8_t w_first[FAKE_MAX_WRITES], w_last[FAKE_MAX_WRITES];

@@ -207,6 +207,16 @@ int main(void) {
         reset();
         CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows + 1, row, &a, 0) == 0 &&
               threw("java/lang/IllegalArgumentException"));
+        /* a Java exception between pieces: the pieces written so far are given back
+         * (pbx_band_abort), so the band does not stay loading */
+        reset();
+        region_fail_after = 3;
+        CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows, row, &a, 0) == 0 && threw("java/lang/InternalError"));
+        CHECK(fake.nwrites == 3 && fake.band_aborts == 1 && fake.abort_y0 == 1024);
+        reset();  /* an exception before any piece: nothing to give back */
+        region_fail_after = 0;
+        CHECK(J(writeBand)(env, NULL, 1, 88, 1024, rows, row, &a, 0) == 0 && threw("java/lang/InternalError"));
+        CHECK(fake.nwrites == 0 && fake.band_aborts == 0);
         free(a.data);
         reset();
         fake.sparse_band_rows = 512;

@@ -48,8 +48,15 @@ static jboolean m_ExceptionCheck(JNIEnv* e) { (void)e; return pending[0] != 0; }
 static const char* m_GetStringUTFChars(JNIEnv* e, jstring s, jboolean* c) { (void)e; (void)c; return (const char*)s->data; }
 static void m_ReleaseStringUTFChars(JNIEnv* e, jstring s, const char* p) { (void)e; (void)s; (void)p; }
 static jsize m_GetArrayLength(JNIEnv* e, jarray a) { (void)e; return (jsize)a->len; }
+static int region_fail_after = -1;  /* > 0: that many GetByteArrayRegion calls succeed, the next throws */
 static void m_GetByteArrayRegion(JNIEnv* e, jbyteArray a, jsize s, jsize n, jbyte* buf) {
     (void)e;
+    if (region_fail_after == 0) {
+        region_fail_after = -1;
+        snprintf(pending, sizeof pending, "java/lang/InternalError");
+        return;
+    }
+    if (region_fail_after > 0) region_fail_after--;
     if (s < 0 || n < 0 || (size_t)s + (size_t)n > a->len) {
         snprintf(pending, sizeof pending, "java/lang/ArrayIndexOutOfBoundsException");
         return;

@@ -9,6 +9,7 @@ the GPU and served bit-exact.  Every body is checked against the CPU oracle's ge
 """
 import itertools
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -216,3 +217,91 @@ def test_generated_sparse_plane_and_release_under_batch(service, oracle):
         assert st == pbx.OK
         check(oracle, pt, c, body)
     assert service.residency_stats()["resident_bytes"] < before
+
+
+def _rows(oracle, x_size, y0, rows, seed=SEED):
+    return oracle.gen_region(NOISE, pbx.UINT16, 0, y0, x_size, rows, seed=seed).tobytes()
+
+
+def test_band_load_failures_give_the_band_back(oracle, monkeypatch):
+    """a band whose load fails part-way never keeps HBM nor stays loading.
+    (1) A write that fails after another piece of the band was written resets the band: absent,
+    its bytes returned; a reload serves exact pixels.  (2) A failure while a second writer of
+    the same band is still uploading: the band is reset only when that writer leaves (no upload
+    lands in freed HBM), and that writer is told its load is void.  (3) pbx_band_abort after a
+    partial load (the JNI shim's path for a Java exception between pieces).  (4) A band left
+    loading by a loader that went away is started over by the next writer after the stale
+    time ($PBX_BAND_STALE_MS)."""
+    monkeypatch.setenv("PBX_BAND_STALE_MS", "300")
+    sx, sy, B = 4096, 2048, 512
+    with pbx.PixelsService() as svc:
+        iid = next(_ids)
+        pid = svc.create_sparse_plane(iid, 0, 0, 0, pbx.UINT16, sx, sy, B)
+        base = svc.residency_stats()["resident_bytes"]
+
+        def tile_ok(y):
+            st, body = svc.get_tile(pbx.TileCtx(iid, 0, 0, 0, 100, y, 512, 256))
+            assert st == pbx.OK and body == oracle.gen_region(NOISE, pbx.UINT16, 100, y, 512, 256,
+                                                                 seed=SEED).tobytes()
+
+        # (1) piece 1 written, piece 2's upload fails
+        svc.band_write(pid, 0, 256, _rows(oracle, sx, 0, 256))
+        assert svc.band_info(pid)[1][0] == 1  # loading
+        svc.test_fail_band_write(1)
+        with pytest.raises(pbx.PbxError):
+            svc.band_write(pid, 256, 256, _rows(oracle, sx, 256, 256))
+        assert svc.band_info(pid)[1][0] == 0
+        assert svc.residency_stats()["resident_bytes"] == base
+        assert svc.get_tile(pbx.TileCtx(iid, 0, 0, 0, 0, 0, 64, 64))[0] == pbx.E_NOT_RESIDENT
+        svc.band_write(pid, 0, 512, _rows(oracle, sx, 0, 512))
+        tile_ok(100)
+
+        # (2) two writers of band 1: the second fails while the first uploads 512 rows
+        big = _rows(oracle, sx, 512, 512)
+        svc.band_write(pid, 512, 8, big[:8 * sx * 2])  # the band exists (loading, allocated)
+        errs = {}
+
+        def first():
+            try:
+                svc.band_write(pid, 520, 504, big[8 * sx * 2:])
+            except pbx.PbxError as e:
+                errs["first"] = e.status
+        th = threading.Thread(target=first)
+        svc.test_fail_band_write(2)  # the first writer's call is write 1 from here, this one write 2
+        th.start()
+        try:
+            svc.band_write(pid, 512, 8, big[:8 * sx * 2])
+        except pbx.PbxError as e:
+            errs["second"] = e.status
+        th.join(timeout=60)
+        # whichever ordering happened, the band is never published half-written: either both
+        # writes failed and the band is absent, or the failed write came first, the band was
+        # reset and the other write started it over (loading, its rows only)
+        st1 = svc.band_info(pid)[1][1]
+        assert "second" in errs or "first" in errs
+        if st1 == 2:
+            raise AssertionError("a band with a failed write was published")
+        svc.band_abort(pid, 512)
+        assert svc.band_info(pid)[1][1] == 0
+        svc.band_write(pid, 512, 512, big)
+        tile_ok(700)
+        assert svc.residency_stats()["resident_bytes"] == base + 2 * (sx * 2 * B + 256)
+
+        # (3) partial load, then the loader gives up: absent, bytes returned, reload works
+        svc.band_write(pid, 1024, 100, _rows(oracle, sx, 1024, 100))
+        svc.band_abort(pid, 1024)
+        assert svc.band_info(pid)[1][2] == 0
+        assert svc.residency_stats()["resident_bytes"] == base + 2 * (sx * 2 * B + 256)
+        svc.band_write(pid, 1024, 512, _rows(oracle, sx, 1024, 512))
+        tile_ok(1200)
+
+        # (4) a loader that went away part-way: the band reads as loading within the stale time,
+        # then as absent (its HBM returned), so a waiting binding loads it again
+        svc.band_write(pid, 1536, 100, b"\xff" * (sx * 2 * 100))  # never finished
+        assert svc.band_info(pid)[1][3] == 1
+        time.sleep(0.5)
+        assert svc.band_info(pid)[1][3] == 0
+        assert svc.residency_stats()["resident_bytes"] == base + 3 * (sx * 2 * B + 256)
+        svc.band_write(pid, 1536, 512, _rows(oracle, sx, 1536, 512))
+        tile_ok(1700)
+        assert svc.band_info(pid)[1] == [2, 2, 2, 2]
