@@ -112,7 +112,9 @@ struct Plane {
     size_t bytes = 0;
     int32_t band_y0 = 0, band_rows = 0;  // resident rows (band_rows == size_y: the whole plane)
     // sparse planes: held as bands of sparse_rows rows (bands[k]), `dev` unused; band_y0 /
-    // band_rows are then the rows this context may hold (another context owns the rest)
+    // band_rows are then the rows this context owns: requests whose first row lies there are
+    // served here (another context owns the rest), incl. the bands past the owned rows that a
+    // region straddling their end covers (guest bands, loaded on demand like the owned ones)
     int32_t sparse_rows = 0;
     std::vector<Band> bands;
     int32_t gen_source = 0;      // sparse generator planes: bands are generated on demand
@@ -130,11 +132,9 @@ struct Plane {
     // the kernels address rows by their index in the whole plane
     uint8_t* base() const { return dev - (int64_t)band_y0 * pitch; }
     bool whole() const { return !sparse_rows && band_y0 == 0 && band_rows == size_y; }
-    // sparse: rows of band k, [y0, y1)
-    int32_t band_lo(int32_t k) const { return std::max(k * sparse_rows, band_y0); }
-    int32_t band_hi(int32_t k) const {
-        return (int32_t)std::min<int64_t>({(int64_t)(k + 1) * sparse_rows, size_y, (int64_t)band_y0 + band_rows});
-    }
+    // sparse: rows of band k, [y0, y1) (the owned rows start at a band start)
+    int32_t band_lo(int32_t k) const { return k * sparse_rows; }
+    int32_t band_hi(int32_t k) const { return (int32_t)std::min<int64_t>((int64_t)(k + 1) * sparse_rows, size_y); }
     uint8_t* band_base(int32_t k) const { return bands[(size_t)k].dev - (int64_t)band_lo(k) * pitch; }
     // every HBM block the record holds
     void memory(std::vector<std::pair<void*, size_t>>& out) const {
@@ -738,8 +738,11 @@ int validate(pbx_ctx* ctx, const pbx_tile_req& r, int32_t& w, int32_t& h, Plane*
     // getTileDirect outside the plane throws (upstream PixelBuffer) -> 404
     if (r.x < 0 || r.y < 0 || (int64_t)r.x + w > p->size_x || (int64_t)r.y + h > p->size_y)
         return fail(PBX_E_NOTFOUND, "region outside plane");
-    // a row band: rows outside it belong to another context
-    if (r.y < p->band_y0 || (int64_t)r.y + h > (int64_t)p->band_y0 + p->band_rows)
+    // a row band: rows outside it belong to another context; a sparse plane serves every region
+    // whose first row it owns (the bands past the owned rows such a region covers are loaded
+    // here as guest bands: the reference's getTileDirect serves any region of the plane)
+    if (r.y < p->band_y0 || r.y >= (int64_t)p->band_y0 + p->band_rows ||
+        (!p->sparse_rows && (int64_t)r.y + h > (int64_t)p->band_y0 + p->band_rows))
         return fail(PBX_E_NOT_RESIDENT, "rows %d..%lld outside the resident band %d..%d", r.y,
                     (long long)r.y + h, p->band_y0, p->band_y0 + p->band_rows);
     if (p->sparse_rows) {  // every band the rows cover must be resident
@@ -1619,9 +1622,10 @@ void free_planes_locked(pbx_ctx* ctx, const std::vector<std::pair<void*, size_t>
 // data == NULL on a generator plane generates the rows on the GPU instead.
 int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* data, uint64_t bytes) {
     if (!q->sparse_rows) return fail(PBX_E_BADARG, "plane %llu is not a sparse plane", (unsigned long long)q->id);
-    if (rows <= 0 || y0 < q->band_y0 || (int64_t)y0 + rows > (int64_t)q->band_y0 + q->band_rows)
-        return fail(PBX_E_BADARG, "rows %d+%d outside the rows %d+%d this context may hold", y0, rows, q->band_y0,
-                    q->band_rows);
+    // any band of the plane: the owned ones, and guest bands that regions straddling the end of
+    // the owned rows cover (validate routes a region by its first row)
+    if (rows <= 0 || y0 < 0 || (int64_t)y0 + rows > q->size_y)
+        return fail(PBX_E_BADARG, "rows %d+%d outside the plane (%d rows)", y0, rows, q->size_y);
     const int32_t k = y0 / q->sparse_rows;
     const int32_t lo = q->band_lo(k), hi = q->band_hi(k);
     if (y0 + rows > hi) return fail(PBX_E_BADARG, "rows %d+%d cross the end of band %d (rows %d..%d)", y0, rows, k, lo, hi);

@@ -864,8 +864,9 @@ class PixelsService:
             else:
                 pid = found[0]
         B, states = self.band_info(pid)
-        lo, hi = (own[0], own[0] + own[1]) if own is not None else (0, sy)
-        y0, y1 = max(y, lo), min(y + h, hi, sy)
+        # every band the rows cover: the owned ones, and the guest bands past the owned rows that
+        # a region starting in them covers (the reference's getTileDirect serves any region)
+        y0, y1 = max(y, 0), min(y + h, sy)
         for k in range(y0 // B, (y1 + B - 1) // B) if y1 > y0 else ():
             if states[k] == BS_READY:
                 continue
@@ -876,7 +877,7 @@ class PixelsService:
                     if st == BS_READY:
                         break
                     if st == BS_ABSENT:
-                        r0, r1 = max(k * B, lo), min((k + 1) * B, hi, sy)
+                        r0, r1 = k * B, min((k + 1) * B, sy)
                         try:
                             self.band_write(pid, r0, r1 - r0,
                                             source.read_rows(pixels, z, c, t, level, r0, r1 - r0))
@@ -1263,8 +1264,10 @@ class TileRequestHandler:
             svc.declare_image(pixels)  # the retry answers the reference's 404
             return self._answer(*svc.get_tile(tc))
         y, h = tc.y, (tc.h or pixels.size_y)  # :92-97 defaulting from the full-resolution size
-        if self.band is not None and not (self.band[0] <= y and y + h <= self.band[0] + self.band[1]):
-            return None  # rows of another context's band
+        if self.band is not None and not (self.band[0] <= y < self.band[0] + self.band[1] and (
+                svc.sparse_band_rows or y + h <= self.band[0] + self.band[1])):
+            return None  # rows of another context's band (a sparse plane serves every region
+            #              that starts in its rows, a whole-row band only those inside it)
         attempts, deadline = 0, time.monotonic() + self.NO_SPACE_WAIT_S
         while attempts < self.LOAD_ATTEMPTS:
             t1 = time.perf_counter()

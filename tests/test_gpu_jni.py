@@ -97,7 +97,12 @@ def test_jni_shim_on_real_library(tmp_path, oracle):
     # the node: misses name the context owning the rows, the bands loaded there serve them
     assert tiles["node_a_miss"][0] == 460 and served_by["node_a_miss"] == 0
     assert tiles["node_b_miss"][0] == 460 and served_by["node_b_miss"] == 1
-    assert tiles["node_c_miss"][0] == 460  # straddles the two owners' rows: nobody serves it
+    # straddles the two owners' rows: routed to the owner of its first row, which loads the
+    # other owner's band as a guest band and serves it
+    assert tiles["node_c_miss"][0] == 460 and served_by["node_c_miss"] == 0
+    st, body, _, _ = tiles["node_c"]
+    tile = np.frombuffer(want(4000, 3900, 512, 512), np.uint8)
+    assert st == 0 and served_by["node_c"] == 0 and body == oracle.tiff_encode(tile, oracle.UINT16, 512, 512)[1]
     st, body, _, _ = tiles["node_a"]
     assert st == 0 and served_by["node_a"] == 0 and body == want(512, 1000, 512, 512)
     st, body, _, _ = tiles["node_b"]

@@ -136,9 +136,11 @@ def test_band_eviction_under_budget(oracle):
 
 
 def test_foreign_rows_stay_not_resident(oracle):
-    """A rank's share (own rows [0, 51200) of a 100000-row slide): rows of another rank answer
-    NOT_RESIDENT in the library and None in the handler, and nothing is read for them;
-    pbx_band_write refuses them; requests in the share load their bands."""
+    """A rank's share (own rows [0, 51200) of a 100000-row slide): regions that start in rows of
+    another rank answer NOT_RESIDENT in the library and None in the handler, and nothing is read
+    for them; requests in the share load their bands; a region that starts in the share and runs
+    past its end is served here, its rows past the share loaded as a guest band (ADVICE r04:
+    the reference's getTileDirect serves any region of the plane)."""
     pt, side, B = pbx.UINT16, 100000, 512
     iid = next(_ids)
     src = RowSource(oracle, {iid: pbx.Pixels(iid, pt, side, side)})
@@ -154,10 +156,16 @@ def test_foreign_rows_stay_not_resident(oracle):
         assert st == pbx.E_NOT_RESIDENT
         edge = pbx.TileCtx(iid, 0, 0, 0, 0, 51200 - 100, 64, 200)  # half in the share
         (st, _), = svc.get_tiles([edge])
-        assert st == pbx.E_NOT_RESIDENT
+        assert st == pbx.E_NOT_RESIDENT  # its guest band is not loaded yet
+        check(oracle, pt, edge, pbx.TileRequestHandler(svc, edge, src, band=own).get_tile())
         pid = svc.lookup_plane(iid, 0, 0, 0)[0]
+        states = svc.band_info(pid)[1]
+        assert states[99] == 2 and states[100] == 2  # the share's last band and one guest band
+        assert sum(states) == 2 * 2 and src.reads == 2  # the guest band is the one more read
+        (st, _), = svc.get_tiles([foreign])
+        assert st == pbx.E_NOT_RESIDENT  # still another rank's region
         with pytest.raises(pbx.PbxError) as e:
-            svc.band_write(pid, 60000 // B * B, B, bytes(B * side * 2))
+            svc.band_write(pid, side - 100, 200, bytes(200 * side * 2))  # past the plane
         assert e.value.status == pbx.E_BADARG
 
 
