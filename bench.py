@@ -174,6 +174,22 @@ def load_traffic(kernel):
     return None, None
 
 
+CHAIN_KERNELS = ("k_seg_map", "k_lz77", "k_huff", "k_seg_sizes", "k_scan_offsets", "k_encode", "k_frame")
+
+
+def load_chain_traffic():
+    """HBM bytes per launch of the whole deflate chain (every kernel of a headline batch) from
+    the latest committed PMC passes that profiled it: (bytes, source)."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*", "traffic.json")), reverse=True):
+        with open(fn) as f:
+            ks = json.load(f).get("kernels", {})
+        if "k_lz77" in ks and "k_encode" in ks:
+            return (sum(ks[k]["fetch_bytes"] + ks[k]["write_bytes"] for k in CHAIN_KERNELS if k in ks),
+                    os.path.relpath(fn, ROOT))
+    return None, None
+
+
 def load_issue(kernels=("k_encode", "k_lz77")):
     """The issue roofline of the deflate kernels from the latest committed PMC passes
     (profiles/*pmc*/issue.json, scripts/pmc_summary.py: VALU busy = 2 cycles per wave64 VALU
@@ -574,8 +590,11 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 else:
                     held.append((s_, s_.register_plane(pid, 0, 0, 0, pbx.UINT16, sz, sz, data=pois,
                                                        big_endian=False)))
-            n = (sz // TILE) ** 2
-            ctxs = grid_ctxs(pid, "png", n=min(n, GRID * GRID))
+            # a 4096-tile batch like the headline's on every plane: the 8192^2 Poisson plane's 256
+            # tiles 16 times each (a batch of its 256 tiles alone measures launch latency)
+            g = sz // TILE
+            ctxs = [pbx.TileCtx(pid, 0, 0, 0, (i % g) * TILE, (i // g % g) * TILE, TILE, TILE, format="png")
+                    for i in range(GRID * GRID)]
             dt, st, _ = secondary_steps(sa, ctxs, 3, 1, barrier)
             sample = [pbx.TileCtx(pid, 0, 0, 0, (j * 7 % (sz // TILE)) * TILE,
                                   (j * 5 % (sz // TILE)) * TILE, TILE, TILE) for j in range(8)]
@@ -589,7 +608,8 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 rows = np.frombuffer(b, np.uint8).reshape(TILE, TILE * 2)
                 z6 += len(zlib.compress(np.concatenate([np.zeros((TILE, 1), np.uint8), rows], 1).tobytes(), 6))
             out[name] = {
-                "tiles_per_s": round(len(ctxs) * 3 * world / dt, 1),
+                "tiles_per_s": round(len(ctxs) * 3 * world / dt, 1), "batch_tiles": len(ctxs),
+                "distinct_tiles": g * g,
                 **wall_vs_kernels(dt, 3, st),
                 "k_filter_ms": round(mean(st, "ms_filter"), 3),
                 "k_filter_frac": round((st[-1].in_bytes + st[-1].stream_bytes) / (mean(st, "ms_filter") * 1e-3)
@@ -928,11 +948,20 @@ def main():
                    "gbps": round(b / (ms * 1e-3) / 1e9, 1),
                    "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
                for k, (ms, b) in kern.items()}
+    # the dominant kernel: the longest mean HIP-event time of the SERIAL pass (one kernel
+    # stream: no overlap stretches a kernel), with its byte definition stated in the line
+    byte_def = {"k_lz77": "plane tile bytes read + filtered stream written + 1280 B histogram per segment",
+                "k_huff": "1280 B histogram read per segment + 1920 B codes/header written per block",
+                "k_encode": "filtered stream read + zlib payload written"}
     dom = max(kern, key=lambda k: kern[k][0])
     dom_ms, dom_bytes = kern[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(dom)
     chain_ms = mean(stats, "ms_deflate") + mean(stats, "ms_assemble")
+    # SURVEY §8(d) "PNG end-to-end": the plane bytes the tiles read + the PNG bytes written,
+    # per step, over the whole step's time (all kernels, launches and host planning)
+    e2e_bytes = st.in_bytes + st.deflate_out_bytes
+    chain_traffic, chain_src = load_chain_traffic()
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -948,7 +977,12 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": dom, "kernel_ms": round(dom_ms, 3),
-                     "alg_bytes_per_launch": int(dom_bytes),
+                     "kernel_choice": "longest mean HIP-event time of the serial pass",
+                     "alg_bytes_per_launch": int(dom_bytes), "alg_bytes_definition": byte_def[dom],
+                     "end_to_end_frac": round(e2e_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "end_to_end_bytes_per_step": int(e2e_bytes),
+                     "chain_traffic_ratio": (round(chain_traffic / e2e_bytes, 3) if chain_traffic else None),
+                     "chain_traffic_bytes": chain_traffic, "chain_traffic_source": chain_src,
                      "note": "deflate kernels are VALU-issue/latency-bound integer work, not "
                              "HBM-bound; the HBM-bound extraction kernel (k_extract) is in "
                              "raw_4096x512x512_u16; their issue roofline is in `issue`",

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -388,6 +389,7 @@ struct pbx_batch {
     uint64_t* h_offs_pin = nullptr;  // in h_desc: the deflate tiles' output offsets, D2H'd by the
     bool offs_ready = false;         // kernel stream at the end of a launch that will be fetched
     hipEvent_t ev_copy = nullptr;    // the fetch's D2H on the copy stream
+    std::chrono::steady_clock::time_point t_done;  // the fetch saw the kernels complete (PBX_TIMELINE)
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
     bool launched = false;
@@ -891,10 +893,14 @@ struct Coalescer {
     static constexpr size_t MAX_BATCH = 1 << 16;
     // Heap-allocated: a caller that gives up at its deadline leaves it to the completer, which
     // releases the late result and frees it (abandoned).
+    using clk = std::chrono::steady_clock;
     struct Pending {
         pbx_tile_req req;
         pbx_result res{};
         bool done = false, abandoned = false;
+        // PBX_TIMELINE: submitted, taken by the launcher, planned, launched, kernels seen
+        // complete, fetched (D2H done), caller woken
+        clk::time_point t[7];
         int rc = PBX_OK;
         std::string err;
         std::condition_variable cv;  // this caller only: no thundering herd per batch
@@ -923,6 +929,10 @@ struct Coalescer {
     std::deque<Flight> flights;
     int inflight = 0;
     bool stop = false;
+    // PBX_TIMELINE=1: per-request stage durations (us), summarised on stderr at shutdown
+    // (the configs[0] single-request latency breakdown, scripts/c1_latency.py)
+    bool timeline = getenv("PBX_TIMELINE") != nullptr;
+    std::vector<std::array<double, 6>> tl;
     std::thread launcher;
     std::vector<std::thread> completers;
 
@@ -943,6 +953,19 @@ struct Coalescer {
         cv_complete.notify_all();
         launcher.join();
         for (auto& t : completers) t.join();
+        if (timeline && !tl.empty()) {
+            static const char* name[6] = {"queue_to_launcher", "plan", "launch_enqueue", "kernels_to_seen_done",
+                                          "fetch_d2h", "wake_caller"};
+            fprintf(stderr, "[pbx timeline] %zu requests, us p50/p90/p99:", tl.size());
+            for (int k = 0; k < 6; k++) {
+                std::vector<double> v;
+                for (auto& a : tl) v.push_back(a[k]);
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, " %s %.1f/%.1f/%.1f", name[k], v[v.size() / 2], v[v.size() * 9 / 10],
+                        v[std::min(v.size() - 1, v.size() * 99 / 100)]);
+            }
+            fprintf(stderr, "\n");
+        }
     }
     // One request, blocking until its batch is fetched or its deadline (ctx->timeout_us, the
     // reference's event-bus send timeout, PixelBufferMicroserviceVerticle.java:148-151) has
@@ -951,6 +974,7 @@ struct Coalescer {
     int submit(const pbx_tile_req& r, pbx_result* out) {
         Pending* p = new Pending();
         p->req = r;
+        if (timeline) p->t[0] = clk::now();
         std::unique_lock<std::mutex> g(mu);
         if (stop) {
             delete p;
@@ -978,6 +1002,12 @@ struct Coalescer {
         *out = p->res;
         const int rc = p->rc;
         if (rc != PBX_OK) g_err = p->err;
+        if (timeline) {
+            p->t[6] = clk::now();
+            std::array<double, 6> a;
+            for (int k = 0; k < 6; k++) a[k] = std::chrono::duration<double, std::micro>(p->t[k + 1] - p->t[k]).count();
+            tl.push_back(a);  // (under mu)
+        }
         delete p;
         return rc;
     }
@@ -998,11 +1028,18 @@ struct Coalescer {
             std::vector<pbx_tile_req> reqs(take.size());
             for (size_t i = 0; i < take.size(); i++) reqs[i] = take[i]->req;
             Flight f{nullptr, std::move(take), PBX_OK, {}};
+            clk::time_point t1, t2, t3;
+            if (timeline) t1 = clk::now();
             {
                 std::lock_guard<std::mutex> run(ctx->run_mu);
                 f.rc = pbx_batch_plan(ctx, reqs.data(), reqs.size(), &f.b);
+                if (timeline) t2 = clk::now();
                 if (f.rc == PBX_OK) f.rc = batch_launch(ctx, f.b, false, true);
                 if (f.rc != PBX_OK) f.err = g_err;
+            }
+            if (timeline) {
+                t3 = clk::now();
+                for (Pending* p : f.reqs) { p->t[1] = t1; p->t[2] = t2; p->t[3] = t3; }
             }
             ctx->n_batches++;
             ctx->n_requests += reqs.size();
@@ -1031,6 +1068,10 @@ struct Coalescer {
             if (f.rc == PBX_OK) {
                 f.rc = pbx_batch_fetch(ctx, f.b, res.data());
                 if (f.rc != PBX_OK) f.err = g_err;
+            }
+            if (timeline && f.b) {
+                const clk::time_point t5 = clk::now();
+                for (Pending* p : f.reqs) { p->t[4] = f.b->t_done; p->t[5] = t5; }
             }
             for (size_t i = 0; i < n; i++) {
                 pbx_result& o = f.reqs[i]->res;
@@ -2755,6 +2796,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     // Wait for this batch only (later batches may already run on the kernel stream) and
     // copy on the copy stream, so the D2H overlaps the next batch's kernels.
     HIP_TRY(hipEventSynchronize(b->ev[8]));
+    b->t_done = std::chrono::steady_clock::now();
     // a device failure shows when the batch's completion is collected (hipErrorLaunchFailure
     // at the event); the injected one takes the same way (PixelBufferVerticle.java:141-146: 500)
     if (b->inject_fail)
