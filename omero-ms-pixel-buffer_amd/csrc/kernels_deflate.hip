@@ -2751,7 +2751,7 @@ static hipError_t crc_tables_ready() {
     return res[dev];
 }
 
-hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev, hipEvent_t* ev2) {
+hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev, hipEvent_t* ev2, bool fine) {
     if (!a.ntiles || !a.nseg) return hipSuccess;
     if (const hipError_t e = crc_tables_ready(); e != hipSuccess) return e;
     const bool prof = a.stamps != nullptr;
@@ -2766,7 +2766,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
         hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
                            a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg,
                            a.uniform_rcp);
-    if (ev) (void)hipEventRecord(ev[0], st);
+    if (ev && fine) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof)
         hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
@@ -2774,12 +2774,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     else
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
-    if (ev) (void)hipEventRecord(ev[1], st);
+    if (ev && fine) (void)hipEventRecord(ev[1], st);
     if (ev2) (void)hipEventRecord(ev2[1], st);
     hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
                        a.blk, a.sizes);
     hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
-    if (ev) (void)hipEventRecord(ev[2], st);
+    if (ev && fine) (void)hipEventRecord(ev[2], st);
     if (ev2) (void)hipEventRecord(ev2[2], st);
     if (prof)
         hipLaunchKernelGGL((k_encode<DC, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,

@@ -78,9 +78,10 @@ struct DeflateLaunch {
     uint32_t uniform_rcp = 0;   // recip32(uniform_nseg)
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.
-// ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode.
+// ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode;
+// with fine = false only ev[3] (the serving path's spans need no more).
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev = nullptr,
-                          hipEvent_t* ev2 = nullptr);
+                          hipEvent_t* ev2 = nullptr, bool fine = true);
 size_t deflate_lds_bytes(int kernel);  // 0 k_lz77, 1 k_huff, 2 k_encode
 // k_huff alone (test hook): blk[].seg0 / .nseg and info[].sl / .last must be set.
 hipError_t launch_huffman(hipStream_t st, uint32_t nblk, BlkInfo* blk, SegInfo* info,

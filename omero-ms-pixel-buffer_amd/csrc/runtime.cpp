@@ -226,6 +226,50 @@ struct Pool {
     }
 };
 
+// Reused HIP events (a batch takes up to ten; creating and destroying them per batch cost
+// the single-request path host time on every request).
+struct EventPool {
+    unsigned flags = hipEventDefault;
+    std::mutex mu;
+    std::vector<hipEvent_t> free_ev;
+    hipError_t get(hipEvent_t* e) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_ev.empty()) {
+                *e = free_ev.back();
+                free_ev.pop_back();
+                return hipSuccess;
+            }
+        }
+        return hipEventCreateWithFlags(e, flags);
+    }
+    void put(hipEvent_t e) {
+        if (!e) return;
+        std::lock_guard<std::mutex> g(mu);
+        free_ev.push_back(e);
+    }
+    void release_all() {
+        std::lock_guard<std::mutex> g(mu);
+        for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
+        free_ev.clear();
+    }
+};
+
+// Waits for an event: small batches (the single-request latency path) poll it for up to
+// `spin_us` first -- a blocking wait wakes the thread tens of microseconds after the GPU is
+// done -- then block.
+hipError_t wait_event(hipEvent_t e, int64_t spin_us) {
+    if (spin_us > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() >= until) break;
+        }
+    }
+    return hipEventSynchronize(e);
+}
+
 }  // namespace
 
 struct Coalescer;
@@ -322,6 +366,14 @@ struct pbx_ctx {
     // residency (reg_mu)
     uint64_t budget = 0, resident_bytes = 0, use_tick = 0, evictions = 0, evicted_bytes = 0, band_evictions = 0;
     Pool dpool, hpool;
+    EventPool evpool, evpool_sync;  // timing events (batch stages), sync-only events (copies)
+    // batches of at most this many requests poll their completion events (wait_event) for
+    // up to spin_us before blocking ($PBX_SPIN_US, default 2000; 0 = always block)
+    uint32_t spin_max_reqs = 8;
+    int64_t spin_us = 2000;
+    // lite batches whose output arenas fit this many bytes write them straight into pinned
+    // host memory (pbx_batch::h_zc; $PBX_ZC_MAX, default 4 MiB, 0 = always D2H)
+    uint64_t zc_max = 4u << 20;
     Reaper reaper;  // hipFree of plane HBM, off the serving threads
     // fault injection (tests): the batch launched with ordinal fail_at (1-based,
     // counted over every batch launch of this context; $PBX_FAIL_BATCH or
@@ -392,6 +444,15 @@ struct pbx_batch {
     std::chrono::steady_clock::time_point t_done;  // the fetch saw the kernels complete (PBX_TIMELINE)
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
+    // lite: a batch of the serving path (fetched by the coalescer) records only the events its
+    // spans need (start, after the extract kernel, before k_frame, end): every event record is
+    // a marker packet that costs the device a few microseconds between two kernels
+    bool lite = false;
+    // zero-copy output (small lite batches): the fixed and deflate output arenas live in one
+    // pinned host block [fixed | png at zc_png_at] that the kernels write over PCIe, so the
+    // results need no D2H round trip; the block becomes the results' HostBlock at the fetch
+    void* h_zc = nullptr;
+    uint64_t zc_png_at = 0;
     bool launched = false;
     bool attempted = false;  // batch_launch began enqueuing work (it may have failed midway)
     uint64_t ordinal = 0;    // launch ordinal in the context (fault injection)
@@ -793,6 +854,11 @@ void batch_unpin(pbx_ctx* ctx, pbx_batch* b) {
 }
 
 void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
+    if (b->zc_png_at || b->h_zc) {  // the output arenas were in the zero-copy block
+        b->d_fixed = b->d_png = nullptr;
+        if (b->h_zc) ctx->hpool.put(b->h_zc);
+        b->h_zc = nullptr;
+    }
     void** bufs[] = {&b->d_ft,   &b->d_dt,    &b->d_fixed, &b->d_stream, &b->d_info, &b->d_hist,
                      &b->d_mrec, &b->d_codes, &b->d_sizes, &b->d_offs,   &b->d_png,  &b->d_stamps,
                      &b->d_segmap, &b->d_blk, &b->d_th, &b->d_bridge};
@@ -897,7 +963,8 @@ struct Coalescer {
     struct Pending {
         pbx_tile_req req;
         pbx_result res{};
-        bool done = false, abandoned = false;
+        std::atomic<bool> done{false};  // set under mu; a spinning caller polls it unlocked
+        bool abandoned = false;
         // PBX_TIMELINE: submitted, taken by the launcher, planned, launched, kernels seen
         // complete, fetched (D2H done), caller woken
         clk::time_point t[7];
@@ -983,9 +1050,19 @@ struct Coalescer {
         queue.push_back(p);
         cv_launch.notify_one();
         const int64_t to = ctx->timeout_us;
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(to > 0 ? to : 0);
+        // a lone caller (an idle coalescer: the single-request latency path) polls for its
+        // result before it blocks -- a condition-variable wake-up costs it ~15 us
+        if (ctx->spin_us > 0 && queue.size() + (size_t)inflight <= 2) {
+            g.unlock();
+            const int64_t su = to > 0 ? std::min<int64_t>(ctx->spin_us, to) : ctx->spin_us;
+            const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(su);
+            while (!p->done.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < spin_until) {
+            }
+            g.lock();
+        }
         if (to > 0) {
-            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(to);
-            if (!p->cv.wait_until(g, until, [&] { return p->done; })) {
+            if (!p->cv.wait_until(g, until, [&] { return p->done.load(); })) {
                 const auto it = std::find(queue.begin(), queue.end(), p);
                 if (it != queue.end()) {
                     queue.erase(it);
@@ -997,7 +1074,7 @@ struct Coalescer {
                 return deadline_result(ctx, r, out);
             }
         } else {
-            p->cv.wait(g, [&] { return p->done; });
+            p->cv.wait(g, [&] { return p->done.load(); });
         }
         *out = p->res;
         const int rc = p->rc;
@@ -1099,7 +1176,7 @@ struct Coalescer {
                     }
                     p->rc = f.rc;
                     p->err = f.err;
-                    p->done = true;
+                    p->done.store(true, std::memory_order_release);
                     p->cv.notify_one();  // under mu: the caller cannot return (and free p) first
                 }
                 inflight--;
@@ -1202,6 +1279,9 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     ctx->device = dev;
     ctx->cfg = cfg;
     ctx->hpool.pinned = true;
+    ctx->evpool_sync.flags = hipEventDisableTiming;
+    if (const char* su = getenv("PBX_SPIN_US")) ctx->spin_us = atoll(su);
+    if (const char* zm = getenv("PBX_ZC_MAX")) ctx->zc_max = strtoull(zm, nullptr, 10);
     ctx->timeout_us = cfg.request_timeout_us;
     if (ctx->timeout_us == 0) {
         const char* rt = getenv("PBX_REQUEST_TIMEOUT_US");
@@ -1254,6 +1334,8 @@ void pbx_shutdown(pbx_ctx* ctx) {
     ctx->planes.clear();
     ctx->dpool.release_all();
     ctx->hpool.release_all();
+    ctx->evpool.release_all();
+    ctx->evpool_sync.release_all();
     for (int k = 1; k < 4; k++)
         if (ctx->kstream[k]) (void)hipStreamDestroy(ctx->kstream[k]);
     for (auto& r : ctx->stage_ev)
@@ -2611,6 +2693,22 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
         }
     }
     const size_t ns = b->nseg;
+    b->lite = fetch_follows && !overlap;
+    if (b->lite && !b->h_zc && !b->d_fixed && !b->d_png && ctx->zc_max) {
+        const uint64_t at = (b->fixed_bytes + 255) & ~(uint64_t)255;
+        if (at + b->png_cap + 256 <= ctx->zc_max) {
+            b->h_zc = ctx->hpool.get(at + b->png_cap + 256, &err);
+            void* dp = nullptr;
+            if (b->h_zc && hipHostGetDevicePointer(&dp, b->h_zc, 0) == hipSuccess) {
+                b->d_fixed = dp;
+                b->d_png = (uint8_t*)dp + at;
+                b->zc_png_at = at | 1u;  // (bit 0: the block is in use even when at == 0)
+            } else if (b->h_zc) {
+                ctx->hpool.put(b->h_zc);
+                b->h_zc = nullptr;
+            }
+        }
+    }
     if (!dget(b->d_ft, ft_bytes) || !dget(b->d_dt, dt_bytes) || !dget(b->d_fixed, b->fixed_bytes) ||
         !dget(b->d_stream, b->stream_cap) || !dget(b->d_info, ns * sizeof(SegInfo)) ||
         !dget(b->d_hist, ns * HIST_WORDS * 4) || !dget(b->d_mrec, ns * MREC_WORDS * 4) ||
@@ -2620,7 +2718,8 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
         !dget(b->d_segmap, ns * sizeof(uint32_t)) || !dget(b->d_th, th_bytes))
         return fail(PBX_E_INTERNAL, "device alloc: %s", hipGetErrorString(err));
     if (!b->ev[0])
-        for (auto& e : b->ev) HIP_TRY(hipEventCreate(&e));
+        for (auto& e : b->ev) HIP_TRY(ctx->evpool.get(&e));
+    const bool fine = !b->lite;  // every stage's event (the batch API: pbx_batch_stats_get)
     const int nks = ctx->nks.load();
     const bool multi = overlap && nks > 1 && b->nseg > 0;
     const int ks = multi ? (int)(ctx->kturn++ % (uint32_t)nks) : 0;
@@ -2652,9 +2751,9 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
                                      (size_t)(r1 - r0), hipMemcpyDeviceToDevice, st));
         }
     }
-    HIP_TRY(hipEventRecord(b->ev[1], st));
+    if (fine) HIP_TRY(hipEventRecord(b->ev[1], st));
     HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
-    HIP_TRY(hipEventRecord(b->ev[2], st));
+    if (fine || nft) HIP_TRY(hipEventRecord(b->ev[2], st));
     const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;
     HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
@@ -2664,7 +2763,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles + b->nfilt2_tiles + b->nfilt3_tiles,
                           ndt - b->ndirect_tiles - b->nrows_tiles - b->nfilt2_tiles - b->nfilt3_tiles,
                           b->filt_blocks, (uint8_t*)b->d_stream));
-    HIP_TRY(hipEventRecord(b->ev[3], st));
+    if (fine) HIP_TRY(hipEventRecord(b->ev[3], st));
     // Diagnostic build of the deflate kernel: PBX_PHASE_PROFILE=1 stamps every phase.
     static const bool prof = getenv("PBX_PHASE_PROFILE") != nullptr;
     if (prof && !b->d_stamps && !dget(b->d_stamps, (size_t)b->nseg * 32 * sizeof(uint64_t)))
@@ -2692,10 +2791,10 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     a.uniform_rcp = recip32(a.uniform_nseg);
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
-        HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr));
+        HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr, fine));
         ctx->last_ks = multi ? ks : -1;
     } else {
-        for (int k = 4; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
+        for (int k = fine ? 4 : 7; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
     }
     HIP_TRY(launch_tiff_tiled(st, (const TiledHdr*)b->d_th, nth, (uint8_t*)b->d_fixed, (const uint64_t*)b->d_offs,
                               (uint8_t*)b->d_png));
@@ -2711,7 +2810,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
 int pbx_batch_sync(pbx_ctx* ctx, pbx_batch* b) {
     if (!ctx || !b) return fail(PBX_E_BADARG, "null argument");
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
-    if (b->launched) HIP_TRY(hipEventSynchronize(b->ev[8]));
+    if (b->launched) HIP_TRY(wait_event(b->ev[8], b->reqs.size() <= ctx->spin_max_reqs ? ctx->spin_us : 0));
     if (b->inject_fail)
         return fail(PBX_E_INTERNAL, "injected device failure in batch %llu", (unsigned long long)b->ordinal);
     if (b->d_stamps && b->nseg) {  // PBX_PHASE_PROFILE diagnostic: mean cycles per phase
@@ -2753,6 +2852,7 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
     s->blocks = b->nblk;
     if (b->launched) {
         if (ensure_device(ctx)) return PBX_E_INTERNAL;
+        if (b->lite) return fail(PBX_E_BADARG, "stage timings of a serving-path batch are not recorded");
         HIP_TRY(hipEventSynchronize(b->ev[8]));
         auto el = [&](int i, int j, double& out) -> int {
             float ms = 0;
@@ -2795,7 +2895,8 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     if (ensure_device(ctx)) return PBX_E_INTERNAL;
     // Wait for this batch only (later batches may already run on the kernel stream) and
     // copy on the copy stream, so the D2H overlaps the next batch's kernels.
-    HIP_TRY(hipEventSynchronize(b->ev[8]));
+    const int64_t spin = n <= ctx->spin_max_reqs ? ctx->spin_us : 0;
+    HIP_TRY(wait_event(b->ev[8], spin));
     b->t_done = std::chrono::steady_clock::now();
     // a device failure shows when the batch's completion is collected (hipErrorLaunchFailure
     // at the event); the injected one takes the same way (PixelBufferVerticle.java:141-146: 500)
@@ -2815,23 +2916,30 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     hipError_t err = hipSuccess;
     HostBlock* hb = new HostBlock();
     hb->ctx = ctx;
-    hb->pinned = ctx->hpool.get(b->fixed_bytes + png_total + 256, &err);
+    const bool zc = b->h_zc != nullptr;  // the kernels wrote the outputs into host memory
+    if (zc) {
+        hb->pinned = b->h_zc;
+        b->h_zc = nullptr;  // the results own it now
+    } else {
+        hb->pinned = ctx->hpool.get(b->fixed_bytes + png_total + 256, &err);
+    }
     if (!hb->pinned) {
         delete hb;
         return fail(PBX_E_INTERNAL, "pinned alloc: %s", hipGetErrorString(err));
     }
     uint8_t* h = (uint8_t*)hb->pinned;
+    uint8_t* hp = h + (zc ? (b->zc_png_at & ~(uint64_t)1) : b->fixed_bytes);  // the deflate outputs
     auto fail_hb = [&](hipError_t e) {
         ctx->hpool.put(hb->pinned);
         delete hb;
         return fail(PBX_E_INTERNAL, "fetch: %s", hipGetErrorString(e));
     };
-    if (!b->ev_copy) {
-        const hipError_t e = hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming);
+    if (!b->ev_copy && !zc) {
+        const hipError_t e = ctx->evpool_sync.get(&b->ev_copy);
         if (e != hipSuccess) return fail_hb(e);
     }
     const auto t_copy = std::chrono::steady_clock::now();
-    {   // the copies are queued back to back on the copy stream (several completers may have
+    if (!zc) {  // the copies are queued back to back on the copy stream (several completers may have
         // theirs in flight: the link never waits for a host round trip); the wait is outside
         std::lock_guard<std::mutex> cg(ctx->copy_mu);
         hipError_t e = hipSuccess;
@@ -2842,11 +2950,18 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
         if (e == hipSuccess) e = hipEventRecord(b->ev_copy, ctx->copy_stream);
         if (e != hipSuccess) return fail_hb(e);
     }
-    if (const hipError_t e = hipEventSynchronize(b->ev_copy)) return fail_hb(e);
-    {   // the span timings (events of a finished batch: no wait)
+    if (!zc)
+        if (const hipError_t e = wait_event(b->ev_copy, spin)) return fail_hb(e);
+    {   // the span timings (events of a finished batch: no wait); a lite batch recorded only
+        // start (0), after the extract (2, when it had one), before k_frame (7) and end (8)
         float ms[5] = {0, 0, 0, 0, 0};
-        const int ij[5][2] = {{1, 2}, {2, 3}, {3, 7}, {7, 8}, {0, 8}};
-        for (int q = 0; q < 5; q++) (void)hipEventElapsedTime(&ms[q], b->ev[ij[q][0]], b->ev[ij[q][1]]);
+        const bool ext = !b->lite || !b->ft.empty();
+        const int w0 = b->lite ? (ext ? 2 : 0) : 2;
+        const int ij[5][2] = {{b->lite ? 0 : 1, 2}, {w0, b->lite ? 7 : 3}, {3, 7}, {7, 8}, {0, 8}};
+        for (int q = 0; q < 5; q++) {
+            if ((q == 0 && !ext) || (q == 2 && b->lite)) continue;
+            (void)hipEventElapsedTime(&ms[q], b->ev[ij[q][0]], b->ev[ij[q][1]]);
+        }
         pbx_spans& sp = hb->spans;
         sp.get_tile_direct_ms = ms[0];
         sp.write_image_ms = (double)ms[1] + ms[2];
@@ -2868,7 +2983,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
     for (uint32_t k = 0; k < ndt; k++) {
         if (b->dt[k].flags & TF_TILED) continue;
         pbx_result& r = out[b->dt_req[k]];
-        r.data = h + b->fixed_bytes + b->h_offs[k];
+        r.data = hp + b->h_offs[k];
         r.len = b->h_offs[k + 1] - b->h_offs[k];
         r.owner = hb;
         refs++;
@@ -2880,7 +2995,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
             r.data = h + t.off;
             r.len = tiff_tiled_data_offset(t.n) + (uint64_t)t.n * t.t * t.t * t.bpp;
         } else {
-            r.data = h + b->fixed_bytes + b->h_offs[t.first];
+            r.data = hp + b->h_offs[t.first];
             r.len = b->h_offs[t.first + t.n] - b->h_offs[t.first];
         }
         r.owner = hb;
@@ -2903,9 +3018,8 @@ void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
     if (b->ev_copy) (void)hipEventSynchronize(b->ev_copy);
     batch_unpin(ctx, b);
     free_batch_device(ctx, b);
-    for (auto& e : b->ev)
-        if (e) (void)hipEventDestroy(e);
-    if (b->ev_copy) (void)hipEventDestroy(b->ev_copy);
+    for (auto& e : b->ev) ctx->evpool.put(e);
+    ctx->evpool_sync.put(b->ev_copy);
     delete b;
 }
 
