@@ -57,6 +57,9 @@ struct LzSmem {
     uint32_t hdummy[64];  // per-lane sink of the branch-free histogram (covered positions)
     uint32_t dfreq[32];
     uint32_t red[3 * C::NW];
+#ifdef PBX_LZ_PAD_LDS  // experiments only: LDS a prefetch ring would take (occupancy probe)
+    uint32_t pad[PBX_LZ_PAD_LDS / 4];
+#endif
 };
 
 // Per-tree arrays of the literal/length tree (288 slots) and the distance tree (32 slots)
@@ -1140,6 +1143,33 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     if (lane == 0) S.w_nm[w] = nm;
 }
 
+// Container bytes before the zlib stream: TIFF header, PNG chunks up to the IDAT data, or
+// (tiled TIFF) the response header in front of its first sub-tile only.
+__device__ __forceinline__ uint32_t container_zoff(const TileDesc& d) {
+    return (d.flags & TF_TILED) ? d.tiff_hdr : (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
+}
+
+// Segment g of tile i (descriptor d): its Huffman block by inverting block_seg0
+// (j = ((k + 1) nb - 1) / n, checked for every n <= 300), the block's record from its first
+// segment, and the segment's record fields the later kernels read (k_seg_map; k_lz77 itself
+// in batches of equal segment counts).
+__device__ __forceinline__ void seg_map_one(const TileDesc& d, uint32_t i, uint32_t g, SegInfo* __restrict__ info,
+                                            BlkInfo* __restrict__ blk) {
+    const uint32_t f = d.seg_first, n = d.seg_count, hb = d.hblk_first;
+    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(d));
+    const uint32_t k = g - f;
+    const uint32_t j = (uint32_t)(((uint64_t)(k + 1) * nb - 1) / n);
+    const uint32_t s0 = block_seg0(j, n, nb), s1 = block_seg0(j + 1, n, nb);
+    if (k == s0) {
+        blk[hb + j].seg0 = f + s0;
+        blk[hb + j].nseg = s1 - s0;
+    }
+    info[g].blk = hb + j;
+    info[g].tile = i;
+    info[g].zoff = container_zoff(d);
+    info[g].flags = (k == s0 ? SF_FIRST : 0u) | (k + 1 == s1 ? SF_LAST : 0u) | ((d.flags & TF_TIFF) ? SF_TIFF : 0u);
+}
+
 // The whole descriptor in one round of scalar loads: the fence keeps the compiler from
 // sinking the plane fields' loads past the branches into a second dependent round.
 __device__ __forceinline__ TileDesc load_desc(const TileDesc* p) {
@@ -1230,9 +1260,10 @@ template <class C, bool PROF>
 __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, uint8_t* __restrict__ stream,
-                                                SegInfo* __restrict__ info, uint32_t* __restrict__ hist,
+                                                SegInfo* __restrict__ info, BlkInfo* __restrict__ blk,
+                                                uint32_t* __restrict__ hist,
                                                 uint32_t* __restrict__ mrec, uint64_t* __restrict__ stamps,
-                                                uint32_t uniform_nseg, uint32_t uniform_rcp) {
+                                                uint32_t uniform_nseg, uint32_t uniform_rcp, uint32_t self_map) {
     __shared__ LzSmem<C> S;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t seg = xcd_remap(blockIdx.x, gridDim.x);
@@ -1243,8 +1274,10 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     };
     stamp();
     // (tiles of equal segment counts: the tile by a division, one dependent load less)
-    const TileDesc d = load_desc(dt + (uniform_nseg ? div_rcp(seg, uniform_nseg, uniform_rcp) : seg_tile[seg]));
+    const uint32_t ti = uniform_nseg ? div_rcp(seg, uniform_nseg, uniform_rcp) : seg_tile[seg];
+    const TileDesc d = load_desc(dt + ti);
     const SegParams sp = seg_params(d, seg - d.seg_first);
+    if (self_map && tid == 0) seg_map_one(d, ti, seg, info, blk);  // (small batches: no k_seg_map launch)
     const bool direct = (d.flags & TF_DIRECT) != 0;
     DirectRows dr;  // (before the branch: one round of descriptor loads, not two)
     dr.init(d);
@@ -1759,10 +1792,17 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
 #define PBX_HUFF_LDSEG 12  // 4: 0.215 ms, 8: 0.213, 12: 0.208 (profiles/r03_p19/; VGPRs 51 -> 73, occupancy still set by LDS)
 #endif
 constexpr uint32_t HUFF_LDSEG = PBX_HUFF_LDSEG;  // k_huff: segments whose histogram loads are in flight together
+constexpr uint32_t HUFF_SMALL_BLKS = 256;   // batches of at most this many blocks: k_huff<.., 34>
+constexpr uint32_t FRAME_WAVE_TILES = 256;  // batches of at most this many tiles: k_frame_wave
+constexpr uint32_t LZ_SELF_MAP_SEGS = 2048;  // k_lz77 maps its segment in batches of at most this many
 
 // One Huffman block = the BLK_SEGS (or fewer, at a tile's end) consecutive segments of
 // one tile whose histograms it sums; one wave per block.
-template <class C, bool PROF>
+// LDSEG: segments whose histogram loads are in flight together.  Large batches take 12 (the
+// registers of more would cut the kernel's occupancy, profiles/r03_p19/); a small batch (the
+// single-request latency path: one block, one wave on the chip) loads up to 34 segments' at
+// once, one round of loads instead of three for a 512x512 uint16 tile.
+template <class C, bool PROF, uint32_t LDSEG = HUFF_LDSEG>
 __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict__ blk,
                                              SegInfo* __restrict__ info,
                                              const uint32_t* __restrict__ hist,
@@ -1780,15 +1820,15 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     stamp();
     // the segments' histograms summed (read again, L2-hot, for their bit counts at the end)
     uint32_t hs[5] = {0, 0, 0, 0, 0};
-    for (uint32_t k0 = 0; k0 < nsg; k0 += HUFF_LDSEG) {  // HUFF_LDSEG segments' loads in flight
-        uint32_t hr[HUFF_LDSEG][5];
+    for (uint32_t k0 = 0; k0 < nsg; k0 += LDSEG) {  // LDSEG segments' loads in flight
+        uint32_t hr[LDSEG][5];
 #pragma unroll
-        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
+        for (uint32_t k = 0; k < LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++)
                 hr[k][j] = k0 + k < nsg ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
+        for (uint32_t k = 0; k < LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++) hs[j] += hr[k][j];
     }
@@ -1882,15 +1922,15 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
 #ifndef PBX_HUFF_ONEREAD
 #define PBX_HUFF_ONEREAD 0  // timing bound only (variant build): no second histogram read, wrong output
 #endif
-    for (uint32_t k0 = 0; k0 < nsg; k0 += HUFF_LDSEG) {
-        uint32_t hr[HUFF_LDSEG][5];
+    for (uint32_t k0 = 0; k0 < nsg; k0 += LDSEG) {
+        uint32_t hr[LDSEG][5];
 #pragma unroll
-        for (uint32_t k = 0; k < HUFF_LDSEG; k++)
+        for (uint32_t k = 0; k < LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++)
                 hr[k][j] = k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : k;
 #pragma unroll
-        for (uint32_t k = 0; k < HUFF_LDSEG; k++) {
+        for (uint32_t k = 0; k < LDSEG; k++) {
             uint32_t d = 0;
 #pragma unroll
             for (int j = 0; j < 5; j++) d += cost[j] * hr[k][j];
@@ -1907,17 +1947,20 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         bt = 0; hdr = 0; dbits = 0;
         nbytes = block_nbytes(0, 0, sl, last, nsg);
     }
-    // stored: every segment is its own stored block (5-byte header + its bytes)
-    uint32_t run = bt == 0 ? 0u : hdr;
-    for (uint32_t k = 0; k < nsg; k++) {
-        const uint32_t d = bt == 0 ? 8 * (5 + S.sls[k]) : S.dk[k];
-        if (tid == 0) {
+    // stored: every segment is its own stored block (5-byte header + its bytes).  Lane k
+    // writes segment k's bit range [bit0, bit1): the bits before it by a wave scan.
+    static_assert(BLK_SEGS <= 64, "one lane per segment of a block");
+    {
+        const uint32_t k = tid;
+        const uint32_t d = k < nsg ? (bt == 0 ? 8 * (5 + S.sls[k]) : S.dk[k]) : 0u;
+        const uint32_t st = (bt == 0 ? 0u : hdr) + wave_incl_scan_dpp(d) - d;  // run before segment k
+        if (k < nsg) {
             SegInfo& g = info[seg0 + k];
             g.btype = bt;
             g.hdr_bits = hdr;
-            g.bit0 = k == 0 ? 0u : run;
-            run += d;
-            g.bit1 = k + 1 < nsg ? run : last ? (bt == 0 ? 8 * nbytes : run + (S.lcode[256] >> 16)) : 8 * nbytes;
+            g.bit0 = k == 0 ? 0u : st;
+            const uint32_t e = st + d;
+            g.bit1 = k + 1 < nsg ? e : last ? (bt == 0 ? 8 * nbytes : e + (S.lcode[256] >> 16)) : 8 * nbytes;
         }
     }
     if (tid == 0) {
@@ -1926,12 +1969,6 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         blk[b].fin = last;
     }
     stamp();
-}
-
-// Container bytes before the zlib stream: TIFF header, PNG chunks up to the IDAT data, or
-// (tiled TIFF) the response header in front of its first sub-tile only.
-__device__ __forceinline__ uint32_t container_zoff(const TileDesc& d) {
-    return (d.flags & TF_TILED) ? d.tiff_hdr : (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
 }
 
 // ================================================================= k_seg_map
@@ -1949,20 +1986,8 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
     if (g >= nseg) return;
     const uint32_t i = uniform_nseg ? div_rcp(g, uniform_nseg, uniform_rcp)
                                     : upper_index(ndt, g, [&](uint32_t t) { return dt[t].seg_first; });
-    const uint32_t f = dt[i].seg_first, n = dt[i].seg_count, hb = dt[i].hblk_first;
-    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(dt[i]));
-    const uint32_t k = g - f;
-    const uint32_t j = (uint32_t)(((uint64_t)(k + 1) * nb - 1) / n);
-    const uint32_t s0 = block_seg0(j, n, nb), s1 = block_seg0(j + 1, n, nb);
-    if (k == s0) {
-        blk[hb + j].seg0 = f + s0;
-        blk[hb + j].nseg = s1 - s0;
-    }
     seg_tile[g] = i;
-    info[g].blk = hb + j;
-    info[g].tile = i;
-    info[g].zoff = container_zoff(dt[i]);
-    info[g].flags = (k == s0 ? SF_FIRST : 0u) | (k + 1 == s1 ? SF_LAST : 0u) | ((dt[i].flags & TF_TIFF) ? SF_TIFF : 0u);
+    seg_map_one(dt[i], i, g, info, blk);
 }
 
 // ================================================================ k_seg_sizes
@@ -1986,8 +2011,46 @@ __global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ 
     sizes[i] = container_bytes(d, off);
 }
 
+// A batch of at most 1024 tiles: k_seg_sizes and k_scan_offsets in one launch (thread t
+// sizes tile t).  offs_host (or nullptr): a copy of the offsets in mapped pinned memory, so
+// the serving path reads them without a D2H copy at the end of the launch.
+__global__ __launch_bounds__(1024) void k_sizes_scan(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                     BlkInfo* __restrict__ blk, uint64_t* __restrict__ offs,
+                                                     uint64_t* __restrict__ offs_host) {
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x;
+    uint64_t s = 0;
+    if (tid < ndt) {
+        const TileDesc& d = dt[tid];
+        uint32_t off = 0;
+        const uint32_t nb = tile_blocks(d.seg_count, PBX_TILE_BLK_CAP(d));
+        for (uint32_t k = 0; k < nb; k++) {
+            BlkInfo& g = blk[d.hblk_first + k];
+            g.off = off;
+            off += g.nbytes;
+        }
+        s = container_bytes(d, off);
+    }
+    part[tid] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint64_t v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    if (tid < ndt) {
+        offs[tid] = part[tid] - s;
+        if (offs_host) offs_host[tid] = part[tid] - s;
+    }
+    if (tid == 1023) {
+        offs[ndt] = part[1023];
+        if (offs_host) offs_host[ndt] = part[1023];
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restrict__ sizes, uint32_t n,
-                                                       uint64_t* __restrict__ offs) {
+                                                       uint64_t* __restrict__ offs, uint64_t* __restrict__ offs_host) {
     __shared__ uint64_t part[1024];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (n + 1023) / 1024;
@@ -2003,8 +2066,15 @@ __global__ __launch_bounds__(1024) void k_scan_offsets(const uint64_t* __restric
         __syncthreads();
     }
     uint64_t run = part[tid] - s;
-    for (uint32_t i = b; i < e; i++) { offs[i] = run; run += sizes[i]; }
-    if (tid == 1023) offs[n] = part[1023];
+    for (uint32_t i = b; i < e; i++) {
+        offs[i] = run;
+        if (offs_host) offs_host[i] = run;
+        run += sizes[i];
+    }
+    if (tid == 1023) {
+        offs[n] = part[1023];
+        if (offs_host) offs_host[n] = part[1023];
+    }
 }
 
 // ==================================================================== k_encode
@@ -2589,12 +2659,7 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
 // ===================================================================== k_frame
 
 // CRC-32 register updates from values (reflected, raw: the caller applies the pre/post xor)
-__device__ __forceinline__ uint32_t crc_u8(uint32_t c, uint32_t b) {
-    c ^= b & 0xFFu;
-#pragma unroll
-    for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((c & 1u) ? CRC_POLY : 0u);
-    return c;
-}
+__device__ __forceinline__ uint32_t crc_u8(uint32_t c, uint32_t b) { return crc_byte4(c, b); }
 __device__ __forceinline__ uint32_t crc_be32(uint32_t c, uint32_t v) {  // v's 4 bytes, big-endian
     c = crc_u8(c, v >> 24); c = crc_u8(c, v >> 16); c = crc_u8(c, v >> 8);
     return crc_u8(c, v);
@@ -2626,17 +2691,10 @@ __device__ __forceinline__ uint32_t put_chunk_w(uint8_t* o, uint32_t type, const
 }
 
 
-// One thread per tile: everything around the segments' bytes, and the bytes two segments
-// of a block share (SegInfo.part), joined in stream order into the output and the IDAT CRC.
-__global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                              const SegInfo* __restrict__ info,
-                                              const BlkInfo* __restrict__ blk,
-                                              const uint64_t* __restrict__ offs,
-                                              uint8_t* __restrict__ out) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= ndt) return;
-    const TileDesc d = dt[i];
-    uint8_t* base = out + offs[i];
+// One tile: everything around the segments' bytes, and the bytes two segments of a block
+// share (SegInfo.part), joined in stream order into the output and the IDAT CRC.
+__device__ __forceinline__ void frame_tile(const TileDesc& d, uint8_t* __restrict__ base,
+                                           const SegInfo* __restrict__ info, const BlkInfo* __restrict__ blk) {
     const bool tiff = (d.flags & TF_TIFF) != 0;
     const uint32_t zoff = container_zoff(d);
     uint32_t s1 = 0, s2 = 0, payload = 0;
@@ -2716,6 +2774,134 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
     put_be32(base + pos + 16, 0xAE426082u);  // its CRC
 }
 
+// One thread per tile (large batches: 64 tiles' serial joins in lockstep per wave).
+__global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                              const SegInfo* __restrict__ info,
+                                              const BlkInfo* __restrict__ blk,
+                                              const uint64_t* __restrict__ offs,
+                                              uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc d = dt[i];
+    frame_tile(d, out + offs[i], info, blk);
+}
+
+// The same bytes for a small batch (the single-request latency path), one wave per tile: a
+// tile's serial join is ~33 dependent CRC multiplies (~18 us for one tile on an idle chip).
+// Lane k takes segment k (64 at a time): its Adler-32 term (bytes after it by a wave scan)
+// and its CRC item -- the byte it shares with segment k - 1 when its bits start mid-byte,
+// written here, then the bytes it owns: crc(v || own) = crc(v) x^(8 |own|) + crc(own).  The
+// items are joined in stream order by a 6-level lane tree ((I1, O1) then (I2, O2) =
+// (I1 O2 + I2, O1 O2)) with nibble-step multiplies; lanes 1-3 write the PNG chunks before
+// IDAT.  A tile with a segment that owns no byte (all its bits inside one byte: the byte is
+// then shared by three segments) takes frame_tile on lane 0.
+__global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                   const SegInfo* __restrict__ info,
+                                                   const BlkInfo* __restrict__ blk,
+                                                   const uint64_t* __restrict__ offs,
+                                                   uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    if (i >= ndt) return;
+    const TileDesc d = dt[i];
+    uint8_t* base = out + offs[i];
+    const bool tiff = (d.flags & TF_TIFF) != 0;
+    const uint32_t zoff = container_zoff(d), n = d.seg_count, f = d.seg_first;
+    // every segment owns a byte (the tree's item form), else the serial join
+    bool degen = false;
+    for (uint32_t k = lane; k < n; k += 64) {
+        const SegInfo& g = info[f + k];
+        const uint32_t b0 = g.bit0 >> 3, le = g.bit1 - 8 * b0, o0 = (g.bit0 & 7u) ? 1u : 0u;
+        const uint32_t o1 = g.last ? (le + 7) >> 3 : le >> 3;
+        degen = degen || o1 <= o0;
+    }
+    if (__builtin_amdgcn_ballot_w64(degen)) {
+        if (lane == 0) frame_tile(d, base, info, blk);
+        return;
+    }
+    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(d));
+    uint32_t payload = 0;
+    for (uint32_t k = lane; k < nb; k += 64) payload += blk[d.hblk_first + k].nbytes;
+    payload = wave_sum(payload);
+    uint8_t* z = base + zoff + ZLIB_HDR_BYTES;
+    constexpr uint32_t X0 = 1u << 31;  // the operator x^0
+    const uint32_t X8 = crc_x8pow2(0);
+    // raw Adler sums, and the IDAT CRC (conditioned) from "IDAT" 78 9C on
+    uint32_t s1 = 0, s2 = 0;
+    uint64_t before = 0;
+    uint32_t c = crc_u8(crc_u8(crc_be32(0xFFFFFFFFu, FOURCC('I', 'D', 'A', 'T')), 0x78), 0x9C) ^ 0xFFFFFFFFu;
+    for (uint32_t k0 = 0; k0 < n; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool v = k < n;
+        const SegInfo& g = info[f + (v ? k : 0u)];
+        const uint32_t sl = v ? g.sl : 0u, a1 = v ? g.adler_s1 : 0u, a2 = v ? g.adler_s2 : 0u;
+        const uint32_t part = v ? g.part : 0u, bit0 = v ? g.bit0 : 0u;
+        const uint32_t pp = v && k ? info[f + k - 1].part : 0u;
+        // Adler: s2 gains a1 x (bytes after this segment)
+        const uint32_t incl = wave_incl_scan_dpp(sl);
+        const uint64_t after = d.stream_len - (before + incl);
+        const uint32_t t2 = (uint32_t)(((uint64_t)a1 * (after % ADLER_BASE) + a2) % ADLER_BASE);
+        s1 = (s1 + wave_sum(a1) % ADLER_BASE) % ADLER_BASE;
+        s2 = (s2 + wave_sum(t2) % ADLER_BASE) % ADLER_BASE;
+        before += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // (segments < 4 GiB)
+        // the byte shared with segment k - 1 (its tail bits | this segment's head bits)
+        uint32_t I = v ? g.crc : 0u, O = v ? g.crc_op : X0;
+        if (v && (part & SP_HEAD)) {
+            const uint32_t sb = (part & 0xFFu) | ((pp & SP_TAIL) ? (pp >> 8) & 0xFFu : 0u);
+            z[blk[g.blk].off + (bit0 >> 3)] = (uint8_t)sb;
+            if (!tiff) {
+                const uint32_t cb = crc_byte4(0xFFFFFFFFu, sb) ^ 0xFFFFFFFFu;
+                I = crc_multmodp4(O, cb) ^ I;
+                O = crc_multmodp4(O, X8);
+            }
+        }
+        if (!tiff) {
+#pragma unroll
+            for (int s = 1; s < 64; s <<= 1) {  // (I, O) of lanes [lane, lane + 2s) on lane % 2s == 0
+                const uint32_t I2 = (uint32_t)__shfl_down((int)I, s, 64), O2 = (uint32_t)__shfl_down((int)O, s, 64);
+                const bool has = lane + s < 64;
+                const uint32_t In = crc_multmodp4(O2, I) ^ I2, On = crc_multmodp4(O, O2);
+                I = has ? In : I;
+                O = has ? On : O;
+            }
+            const uint32_t Ic = (uint32_t)__builtin_amdgcn_readfirstlane((int)I);
+            const uint32_t Oc = (uint32_t)__builtin_amdgcn_readfirstlane((int)O);
+            c = crc_multmodp4(Oc, c) ^ Ic;
+        }
+    }
+    const uint32_t adler = adler_final(s1, s2, d.stream_len);
+    const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;
+    if (lane == 0) {
+        z[-2] = 0x78;  // CMF: deflate, 32 KiB window
+        z[-1] = 0x9C;  // FLG: default level, check bits
+        put_be32(base + pos, adler);
+    }
+    if (d.flags & TF_TILED) return;  // header and tile arrays: k_tiff_tiled
+    if (tiff) {
+        if (lane == 0)
+            write_tiff_header(base, d.w, d.h, d.bpp, tiff_sample_format(d.pixel_type), 8, ZLIB_HDR_BYTES + payload + 4);
+        return;
+    }
+    if (lane == 0) {
+        const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+        for (int j = 0; j < 8; j++) base[j] = sig[j];
+        put_be32(base + PNG_IDAT_DATA_OFF - 8, ZLIB_HDR_BYTES + payload + 4);
+        put_be32(base + PNG_IDAT_DATA_OFF - 4, FOURCC('I', 'D', 'A', 'T'));
+        put_be32(base + pos + 4, crc_be32(c ^ 0xFFFFFFFFu, adler) ^ 0xFFFFFFFFu);
+        put_be32(base + pos + 8, 0);  // IEND
+        put_be32(base + pos + 12, FOURCC('I', 'E', 'N', 'D'));
+        put_be32(base + pos + 16, 0xAE426082u);
+    } else if (lane == 1) {  // IHDR: w, h, bit depth, colour type / compression / filter / interlace 0
+        const uint32_t ihdr[3] = {(uint32_t)d.w, (uint32_t)d.h, (8u * (uint32_t)d.bpp) << 24};
+        put_chunk_w(base + PNG_SIG_BYTES, FOURCC('I', 'H', 'D', 'R'), ihdr, 1);
+    } else if (lane == 2) {  // acTL: 1 frame, 0 plays
+        const uint32_t actl[2] = {1u, 0u};
+        put_chunk_w(base + PNG_SIG_BYTES + PNG_IHDR_BYTES, FOURCC('a', 'c', 'T', 'L'), actl, 0);
+    } else if (lane == 3) {  // fcTL: seq 0, w, h, offsets 0, delay 0/0, ops 0
+        const uint32_t fctl[3] = {0u, (uint32_t)d.w, (uint32_t)d.h};
+        put_chunk_w(base + PNG_SIG_BYTES + PNG_IHDR_BYTES + PNG_ACTL_BYTES, FOURCC('f', 'c', 'T', 'L'), fctl, 14);
+    }
+}
+
 // ================================================================== launchers
 size_t deflate_lds_bytes(int kernel) {
     return kernel == 0 ? sizeof(LzSmem<DC>) : kernel == 1 ? sizeof(HuffSmem<DC>) : sizeof(EncSmem<DC>);
@@ -2755,30 +2941,42 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     if (!a.ntiles || !a.nseg) return hipSuccess;
     if (const hipError_t e = crc_tables_ready(); e != hipSuccess) return e;
     const bool prof = a.stamps != nullptr;
-    hipLaunchKernelGGL(k_seg_map, dim3((a.nseg + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles, a.nseg,
-                       a.uniform_nseg, a.uniform_rcp, a.seg_tile, a.info, a.blk);
+    // a small batch of equal segment counts: k_lz77 maps its own segment (one launch less on
+    // the latency path; in large batches the mapping's divisions cost k_lz77 more than the
+    // separate launch, profiles/r05k/)
+    const uint32_t self_map = a.uniform_nseg && a.nseg <= LZ_SELF_MAP_SEGS ? 1u : 0u;
+    if (!self_map)
+        hipLaunchKernelGGL(k_seg_map, dim3((a.nseg + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles, a.nseg,
+                           a.uniform_nseg, a.uniform_rcp, a.seg_tile, a.info, a.blk);
     const uint32_t lz_grid = a.nseg;
     if (prof)
         hipLaunchKernelGGL((k_lz77<DC, true>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg,
-                           a.uniform_rcp);
+                           a.nseg, a.stream, a.info, a.blk, a.hist, a.mrec, a.stamps, a.uniform_nseg,
+                           a.uniform_rcp, self_map);
     else
         hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.hist, a.mrec, a.stamps, a.uniform_nseg,
-                           a.uniform_rcp);
+                           a.nseg, a.stream, a.info, a.blk, a.hist, a.mrec, a.stamps, a.uniform_nseg,
+                           a.uniform_rcp, self_map);
     if (ev && fine) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof)
         hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
+                           a.hist, a.codes, a.stamps);
+    else if (a.nblk <= HUFF_SMALL_BLKS)  // a small batch: every segment's histogram loads at once
+        hipLaunchKernelGGL((k_huff<DC, false, 34>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
     else
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
     if (ev && fine) (void)hipEventRecord(ev[1], st);
     if (ev2) (void)hipEventRecord(ev2[1], st);
-    hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
-                       a.blk, a.sizes);
-    hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs);
+    if (a.ntiles <= 1024) {
+        hipLaunchKernelGGL(k_sizes_scan, dim3(1), dim3(1024), 0, st, a.tiles, a.ntiles, a.blk, a.offs, a.offs_host);
+    } else {
+        hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,
+                           a.blk, a.sizes);
+        hipLaunchKernelGGL(k_scan_offsets, dim3(1), dim3(1024), 0, st, a.sizes, a.ntiles, a.offs, a.offs_host);
+    }
     if (ev && fine) (void)hipEventRecord(ev[2], st);
     if (ev2) (void)hipEventRecord(ev2[2], st);
     if (prof)
@@ -2791,8 +2989,12 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
                            a.uniform_nseg, a.uniform_rcp);
     if (ev) (void)hipEventRecord(ev[3], st);
     if (ev2) (void)hipEventRecord(ev2[3], st);
-    hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
-                       a.blk, a.offs, a.out);
+    if (a.ntiles <= FRAME_WAVE_TILES)  // small batch: a wave per tile (latency)
+        hipLaunchKernelGGL(k_frame_wave, dim3(a.ntiles), dim3(64), 0, st, a.tiles, a.ntiles, a.info, a.blk,
+                           a.offs, a.out);
+    else
+        hipLaunchKernelGGL(k_frame, dim3((a.ntiles + 63) / 64), dim3(64), 0, st, a.tiles, a.ntiles, a.info,
+                           a.blk, a.offs, a.out);
     return hipGetLastError();
 }
 

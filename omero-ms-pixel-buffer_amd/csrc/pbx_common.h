@@ -262,6 +262,31 @@ PBX_HD uint32_t crc_combine_op(uint32_t crc1, uint32_t crc2, uint32_t op2) {
     return crc_multmodp(op2, crc1) ^ crc2;
 }
 
+// c * x^4 mod P in one step: P's five low bits are zero, so the four bits shifted out decide
+// alone (a chain of ~3 dependent operations instead of 4 x 3).  Latency forms for the
+// single-request path (k_frame_wave); equal to crc_multmodp / the bitwise update.
+PBX_HD uint32_t crc_x4(uint32_t c) {
+    return (c >> 4) ^ ((c & 1u) ? (CRC_POLY >> 3) : 0u) ^ ((c & 2u) ? (CRC_POLY >> 2) : 0u) ^
+           ((c & 4u) ? (CRC_POLY >> 1) : 0u) ^ ((c & 8u) ? CRC_POLY : 0u);
+}
+// a(x) * b(x) mod P by Horner over a's nibbles, highest powers first (b x^0..x^3 up front).
+PBX_HD uint32_t crc_multmodp4(uint32_t a, uint32_t b) {
+    const uint32_t b1 = (b >> 1) ^ ((b & 1u) ? CRC_POLY : 0u);
+    const uint32_t b2 = (b >> 2) ^ ((b & 1u) ? (CRC_POLY >> 1) : 0u) ^ ((b & 2u) ? CRC_POLY : 0u);
+    const uint32_t b3 = (b >> 3) ^ ((b & 1u) ? (CRC_POLY >> 2) : 0u) ^ ((b & 2u) ? (CRC_POLY >> 1) : 0u) ^
+                        ((b & 4u) ? CRC_POLY : 0u);
+    uint32_t p = 0;
+#pragma unroll
+    for (int s = 7; s >= 0; s--) {  // powers 4s .. 4s+3 <-> bits 31-4s .. 28-4s of a
+        const uint32_t t = ((a >> (31 - 4 * s)) & 1u ? b : 0u) ^ ((a >> (30 - 4 * s)) & 1u ? b1 : 0u) ^
+                           ((a >> (29 - 4 * s)) & 1u ? b2 : 0u) ^ ((a >> (28 - 4 * s)) & 1u ? b3 : 0u);
+        p = crc_x4(p) ^ t;
+    }
+    return p;
+}
+// one byte into a (raw, reflected) CRC register
+PBX_HD uint32_t crc_byte4(uint32_t c, uint32_t b) { return crc_x4(crc_x4(c ^ (b & 0xFFu))); }
+
 // Bytewise CRC with a caller-provided 256-entry table (LDS on the device).
 PBX_HD uint32_t crc_update(const uint32_t* table, uint32_t crc, uint8_t b) {
     return table[(crc ^ b) & 0xFF] ^ (crc >> 8);

@@ -70,6 +70,7 @@ struct DeflateLaunch {
     uint32_t nblk;
     uint64_t* sizes;        // [ntiles] container bytes
     uint64_t* offs;         // [ntiles + 1] exclusive scan of sizes (offs[ntiles] = total)
+    uint64_t* offs_host = nullptr;  // or a mapped pinned copy of offs, written by the scan
     uint8_t* out;           // compacted containers
     uint64_t* stamps;       // [nseg * 32] phase clocks (diagnostics) or nullptr
     uint32_t* seg_tile;     // [nseg] tile of every segment (k_seg_map)

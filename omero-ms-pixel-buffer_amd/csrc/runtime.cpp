@@ -2789,6 +2789,11 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     for (uint32_t k = 1; k < ndt && a.uniform_nseg; k++)
         if (b->dt[k].seg_count != a.uniform_nseg) a.uniform_nseg = 0;
     a.uniform_rcp = recip32(a.uniform_nseg);
+    // the serving path reads the tile offsets from a mapped copy the scan writes (no D2H
+    // copy at the end of the launch)
+    void* offs_dev = nullptr;
+    if (fetch_follows && ndt && b->lite && hipHostGetDevicePointer(&offs_dev, b->h_offs_pin, 0) == hipSuccess)
+        a.offs_host = (uint64_t*)offs_dev;
     if (prof) HIP_TRY(hipMemsetAsync(b->d_stamps, 0, (size_t)b->nseg * 32 * sizeof(uint64_t), st));
     if (ndt) {
         HIP_TRY(launch_deflate(st, a, b->ev + 4, multi ? ctx->stage_ev[ks] : nullptr, fine));
@@ -2799,7 +2804,8 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     HIP_TRY(launch_tiff_tiled(st, (const TiledHdr*)b->d_th, nth, (uint8_t*)b->d_fixed, (const uint64_t*)b->d_offs,
                               (uint8_t*)b->d_png));
     if (fetch_follows && ndt) {
-        HIP_TRY(hipMemcpyAsync(b->h_offs_pin, b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        if (!a.offs_host)
+            HIP_TRY(hipMemcpyAsync(b->h_offs_pin, b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         b->offs_ready = true;
     }
     HIP_TRY(hipEventRecord(b->ev[8], st));
