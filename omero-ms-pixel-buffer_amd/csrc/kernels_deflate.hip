@@ -1789,7 +1789,7 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
 }
 
 #ifndef PBX_HUFF_LDSEG
-#define PBX_HUFF_LDSEG 12  // 4: 0.215 ms, 8: 0.213, 12: 0.208 (profiles/r03_p19/; VGPRs 51 -> 73, occupancy still set by LDS)
+#define PBX_HUFF_LDSEG 17  // 4: 0.215 ms, 8: 0.213, 12: 0.208 (profiles/r03_p19/); one block per tile: 8: 0.131, 12: 0.124, 17: 0.119, 24: 0.158 (99 / 134 VGPRs: 4 / 3 waves per SIMD, profiles/r05r/)
 #endif
 constexpr uint32_t HUFF_LDSEG = PBX_HUFF_LDSEG;  // k_huff: segments whose histogram loads are in flight together
 constexpr uint32_t HUFF_SMALL_BLKS = 256;   // batches of at most this many blocks: k_huff<.., 34>
@@ -1798,8 +1798,8 @@ constexpr uint32_t LZ_SELF_MAP_SEGS = 2048;  // k_lz77 maps its segment in batch
 
 // One Huffman block = the BLK_SEGS (or fewer, at a tile's end) consecutive segments of
 // one tile whose histograms it sums; one wave per block.
-// LDSEG: segments whose histogram loads are in flight together.  Large batches take 12 (the
-// registers of more would cut the kernel's occupancy, profiles/r03_p19/); a small batch (the
+// LDSEG: segments whose histogram loads are in flight together.  Large batches take 17 (the
+// registers of more would cut the kernel's occupancy, profiles/r05r/); a small batch (the
 // single-request latency path: one block, one wave on the chip) loads up to 34 segments' at
 // once, one round of loads instead of three for a 512x512 uint16 tile.
 template <class C, bool PROF, uint32_t LDSEG = HUFF_LDSEG>
