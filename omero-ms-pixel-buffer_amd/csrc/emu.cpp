@@ -342,4 +342,24 @@ uint32_t pbxemu_crc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
     return crc_combine_op(crc1, crc2, crc_x8n(len2));
 }
 
+// The latency forms k_frame_wave uses (pbx_common.h) against zlib's bitwise ones: the number
+// of the n seeded random pairs (and bytes) on which they differ.
+uint64_t pbxemu_crc_fast_mismatches(uint64_t n, uint64_t seed) {
+    uint64_t x = seed | 1, bad = 0;
+    auto next = [&]() {  // splitmix64
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return (uint32_t)(z ^ (z >> 31));
+    };
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t a = (i % 7) ? next() : crc_x8n(next() & 0xFFFFFu), b = next(), v = next() & 0xFFu;
+        if (crc_multmodp4(a, b) != crc_multmodp(a, b)) bad++;
+        uint32_t c = b ^ v;
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((c & 1u) ? CRC_POLY : 0u);
+        if (crc_byte4(b, v) != c) bad++;
+    }
+    return bad;
+}
+
 }  // extern "C"

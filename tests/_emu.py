@@ -33,6 +33,8 @@ def lib():
         L.pbxemu_mrec_words.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.pbxemu_crc_fast_mismatches.restype = ctypes.c_uint64
+        L.pbxemu_crc_fast_mismatches.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         _lib = L
     return _lib
 
@@ -52,6 +54,10 @@ def deflate(data: bytes, rowlen: int):
 
 def crc_combine(c1, c2, len2):
     return lib().pbxemu_crc_combine(c1, c2, len2)
+
+
+def crc_fast_mismatches(n, seed):
+    return lib().pbxemu_crc_fast_mismatches(n, seed)
 
 
 def huffman(hist, sl, last):

@@ -34,6 +34,12 @@ def test_roundtrip(n, kind):
     assert pos == len(z) - 4
 
 
+def test_crc_nibble_step_forms_match_zlib():
+    """k_frame_wave's CRC multiply (Horner over nibbles, x^4 in one step) and byte update equal
+    zlib's bitwise multmodp / CRC update on 2 M seeded random pairs (operators x^(8n) among them)."""
+    assert _emu.crc_fast_mismatches(2_000_000, 7) == 0
+
+
 def test_crc_combine_matches_zlib():
     rng = np.random.default_rng(1)
     for la, lb in [(0, 5), (5, 0), (1, 1), (100, 3000), (17, 65537)]:
