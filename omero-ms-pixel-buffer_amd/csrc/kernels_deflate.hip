@@ -599,7 +599,14 @@ __device__ void fill_fast(uint32_t* buf, const DirectRows& dr, uint32_t B, uint3
 #pragma unroll
         for (uint32_t j = 0; j < FR; j++) {  // unconditional loads (clamped row): exact counters
             const uint32_t r = ra + (i0 + j < nrows ? i0 + j : i0);
+#ifdef PBX_LZ_FAKE_LOAD  // timing experiment only: hashed bytes, no plane reads
+            {
+                const uint64_t h = splitmix64((uint64_t)(uintptr_t)(dr.row0 + (int64_t)r * dr.pitch + 16 * lane));
+                x[j] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(h * 3), (uint32_t)(h >> 17));
+            }
+#else
             x[j] = gload16(dr.row0 + (int64_t)r * dr.pitch + 16 * (lane < nc ? lane : 0u));
+#endif
         }
         const uint32_t r0 = ra + i0;
         const uint8_t* rp0 = dr.row0 + (int64_t)r0 * dr.pitch;
