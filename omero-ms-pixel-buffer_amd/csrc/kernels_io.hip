@@ -951,16 +951,32 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
                 if (v < bs) { bs = v; best = k; }
             }
             ft = __builtin_amdgcn_readfirstlane(best);
-            // the prediction by masks in SGPRs (ft is uniform; None predicts 0), then one sub8
-            const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
-            const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+#ifndef PBX_F3_ADAPT_SELECT
+#define PBX_F3_ADAPT_SELECT 1  // 1: the chosen prediction by a uniform branch; 0: by masks in SGPRs
+#endif
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
                 uint32_t o[4];
                 const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
+                if (PBX_F3_ADAPT_SELECT) {
+                    // ft is uniform (an SGPR): a scalar branch to the one subtraction it needs
+                    if (ft == 0) {
 #pragma unroll
-                for (uint32_t j = 0; j < 4; j++)
-                    o[j] = sub8(x[j], (pw[g][0][j] & m1) | (pw[g][1][j] & m2) | (pw[g][2][j] & m3) | (pw[g][3][j] & m4));
+                        for (uint32_t j = 0; j < 4; j++) o[j] = x[j];
+                    } else {
+                        const uint32_t k = ft - 1;
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++)
+                            o[j] = sub8(x[j], k == 0 ? pw[g][0][j] : k == 1 ? pw[g][1][j] : k == 2 ? pw[g][2][j] : pw[g][3][j]);
+                    }
+                } else {
+                    // the prediction by masks in SGPRs (None predicts 0), then one sub8
+                    const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
+                    const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++)
+                        o[j] = sub8(x[j], (pw[g][0][j] & m1) | (pw[g][1][j] & m2) | (pw[g][2][j] & m3) | (pw[g][3][j] & m4));
+                }
                 f[g] = make_uint4(o[0], o[1], o[2], o[3]);
             }
         } else {
