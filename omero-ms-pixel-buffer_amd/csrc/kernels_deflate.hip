@@ -1155,6 +1155,9 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
 __device__ __forceinline__ uint32_t container_zoff(const TileDesc& d) {
     return (d.flags & TF_TILED) ? d.tiff_hdr : (d.flags & TF_TIFF) ? TIFF_DATA_OFFSET : PNG_IDAT_DATA_OFF;
 }
+__device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
+    return container_zoff(d) + ZLIB_HDR_BYTES + payload + ((d.flags & TF_TIFF) ? 4 : PNG_TAIL_BYTES);
+}
 
 // Segment g of tile i (descriptor d): its Huffman block by inverting block_seg0
 // (j = ((k + 1) nb - 1) / n, checked for every n <= 300), the block's record from its first
@@ -1810,11 +1813,16 @@ constexpr uint32_t LZ_SELF_MAP_SEGS = 2048;  // k_lz77 maps its segment in batch
 // single-request latency path: one block, one wave on the chip) loads up to 34 segments' at
 // once, one round of loads instead of three for a 512x512 uint16 tile.
 template <class C, bool PROF, uint32_t LDSEG = HUFF_LDSEG>
+// solo (a batch of one tile in one block, the single-request path): the block also writes the
+// tile's output offsets (and their mapped copy), so no k_sizes_scan launch follows.
 __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict__ blk,
                                              SegInfo* __restrict__ info,
                                              const uint32_t* __restrict__ hist,
                                              uint32_t* __restrict__ codes,
-                                             uint64_t* __restrict__ stamps) {
+                                             uint64_t* __restrict__ stamps,
+                                             const TileDesc* __restrict__ solo = nullptr,
+                                             uint64_t* __restrict__ offs = nullptr,
+                                             uint64_t* __restrict__ offs_host = nullptr) {
     __shared__ HuffSmem<C> S;
     const uint32_t tid = threadIdx.x;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -1825,7 +1833,11 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         nst++;
     };
     stamp();
-    // the segments' histograms summed (read again, L2-hot, for their bit counts at the end)
+    // the segments' histograms summed (read again, L2-hot, for their bit counts at the end;
+    // the small-batch variant keeps its first round in registers for that instead: one wave
+    // on the CU has the registers, and a lone block waits on every load round)
+    constexpr bool KEEP = LDSEG > 24;
+    uint32_t hr0[KEEP ? LDSEG : 1][5];
     uint32_t hs[5] = {0, 0, 0, 0, 0};
     for (uint32_t k0 = 0; k0 < nsg; k0 += LDSEG) {  // LDSEG segments' loads in flight
         uint32_t hr[LDSEG][5];
@@ -1838,6 +1850,12 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         for (uint32_t k = 0; k < LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++) hs[j] += hr[k][j];
+        if (KEEP && k0 == 0) {
+#pragma unroll
+            for (uint32_t k = 0; k < (KEEP ? LDSEG : 1); k++)
+#pragma unroll
+                for (int j = 0; j < 5; j++) hr0[k][j] = hr[k][j];
+        }
     }
 #pragma unroll
     for (int j = 0; j < 5; j++) {
@@ -1935,7 +1953,8 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         for (uint32_t k = 0; k < LDSEG; k++)
 #pragma unroll
             for (int j = 0; j < 5; j++)
-                hr[k][j] = k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : k;
+                hr[k][j] = KEEP && k0 == 0 ? hr0[KEEP ? k : 0][j]
+                           : k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : k;
 #pragma unroll
         for (uint32_t k = 0; k < LDSEG; k++) {
             uint32_t d = 0;
@@ -1974,6 +1993,16 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         blk[b].nbytes = nbytes;
         blk[b].data_bits = dbits;
         blk[b].fin = last;
+        if (solo) {
+            const uint64_t sz = container_bytes(*solo, nbytes);
+            blk[b].off = 0;
+            offs[0] = 0;
+            offs[1] = sz;
+            if (offs_host) {
+                offs_host[0] = 0;
+                offs_host[1] = sz;
+            }
+        }
     }
     stamp();
 }
@@ -1998,9 +2027,6 @@ __global__ __launch_bounds__(256) void k_seg_map(const TileDesc* __restrict__ dt
 }
 
 // ================================================================ k_seg_sizes
-__device__ __forceinline__ uint64_t container_bytes(const TileDesc& d, uint64_t payload) {
-    return container_zoff(d) + ZLIB_HDR_BYTES + payload + ((d.flags & TF_TIFF) ? 4 : PNG_TAIL_BYTES);
-}
 
 __global__ __launch_bounds__(256) void k_seg_sizes(const TileDesc* __restrict__ dt, uint32_t ndt,
                                                    BlkInfo* __restrict__ blk,
@@ -2813,22 +2839,17 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
     uint8_t* base = out + offs[i];
     const bool tiff = (d.flags & TF_TIFF) != 0;
     const uint32_t zoff = container_zoff(d), n = d.seg_count, f = d.seg_first;
-    // every segment owns a byte (the tree's item form), else the serial join
-    bool degen = false;
-    for (uint32_t k = lane; k < n; k += 64) {
-        const SegInfo& g = info[f + k];
-        const uint32_t b0 = g.bit0 >> 3, le = g.bit1 - 8 * b0, o0 = (g.bit0 & 7u) ? 1u : 0u;
-        const uint32_t o1 = g.last ? (le + 7) >> 3 : le >> 3;
-        degen = degen || o1 <= o0;
+    // Two dependent rounds of loads (a lone tile waits on each, ~1 us): the descriptor, then
+    // every segment's record, the part of the one before it and the tile's block records
+    // (lane j: block j; a segment finds its block's offset in the lanes).
+    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(d)), hb = d.hblk_first;
+    uint32_t bnb = 0, boff = 0;
+    if (lane < nb) {
+        bnb = blk[hb + lane].nbytes;
+        boff = blk[hb + lane].off;
     }
-    if (__builtin_amdgcn_ballot_w64(degen)) {
-        if (lane == 0) frame_tile(d, base, info, blk);
-        return;
-    }
-    const uint32_t nb = tile_blocks(n, PBX_TILE_BLK_CAP(d));
-    uint32_t payload = 0;
-    for (uint32_t k = lane; k < nb; k += 64) payload += blk[d.hblk_first + k].nbytes;
-    payload = wave_sum(payload);
+    uint32_t payload = bnb;
+    for (uint32_t k = lane + 64; k < nb; k += 64) payload += blk[hb + k].nbytes;
     uint8_t* z = base + zoff + ZLIB_HDR_BYTES;
     constexpr uint32_t X0 = 1u << 31;  // the operator x^0
     const uint32_t X8 = crc_x8pow2(0);
@@ -2841,8 +2862,20 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
         const bool v = k < n;
         const SegInfo& g = info[f + (v ? k : 0u)];
         const uint32_t sl = v ? g.sl : 0u, a1 = v ? g.adler_s1 : 0u, a2 = v ? g.adler_s2 : 0u;
-        const uint32_t part = v ? g.part : 0u, bit0 = v ? g.bit0 : 0u;
+        const uint32_t part = v ? g.part : 0u, bit0 = v ? g.bit0 : 0u, bit1 = v ? g.bit1 : 0u;
+        const uint32_t last = v ? g.last : 0u, gb = v ? g.blk : hb, gcrc = v ? g.crc : 0u;
+        const uint32_t gop = v ? g.crc_op : X0;
         const uint32_t pp = v && k ? info[f + k - 1].part : 0u;
+        // every segment owns a byte (the tree's item form), else the serial join (the shared
+        // bytes written so far are the values it writes too)
+        {
+            const uint32_t b0 = bit0 >> 3, le = bit1 - 8 * b0, o0 = (bit0 & 7u) ? 1u : 0u;
+            const uint32_t o1 = last ? (le + 7) >> 3 : le >> 3;
+            if (__builtin_amdgcn_ballot_w64(v && o1 <= o0)) {
+                if (lane == 0) frame_tile(d, base, info, blk);
+                return;
+            }
+        }
         // Adler: s2 gains a1 x (bytes after this segment)
         const uint32_t incl = wave_incl_scan_dpp(sl);
         const uint64_t after = d.stream_len - (before + incl);
@@ -2850,11 +2883,14 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
         s1 = (s1 + wave_sum(a1) % ADLER_BASE) % ADLER_BASE;
         s2 = (s2 + wave_sum(t2) % ADLER_BASE) % ADLER_BASE;
         before += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // (segments < 4 GiB)
+        // the block's offset: from its lane (blocks 64.. from memory)
+        const uint32_t bj = gb - hb;
+        const uint32_t bo_l = (uint32_t)__shfl((int)boff, (int)(bj < 64 ? bj : 0u), 64);
         // the byte shared with segment k - 1 (its tail bits | this segment's head bits)
-        uint32_t I = v ? g.crc : 0u, O = v ? g.crc_op : X0;
+        uint32_t I = gcrc, O = gop;
         if (v && (part & SP_HEAD)) {
             const uint32_t sb = (part & 0xFFu) | ((pp & SP_TAIL) ? (pp >> 8) & 0xFFu : 0u);
-            z[blk[g.blk].off + (bit0 >> 3)] = (uint8_t)sb;
+            z[(bj < 64 ? bo_l : blk[gb].off) + (bit0 >> 3)] = (uint8_t)sb;
             if (!tiff) {
                 const uint32_t cb = crc_byte4(0xFFFFFFFFu, sb) ^ 0xFFFFFFFFu;
                 I = crc_multmodp4(O, cb) ^ I;
@@ -2875,6 +2911,7 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
             c = crc_multmodp4(Oc, c) ^ Ic;
         }
     }
+    payload = wave_sum(payload);
     const uint32_t adler = adler_final(s1, s2, d.stream_len);
     const uint64_t pos = zoff + ZLIB_HDR_BYTES + payload;
     if (lane == 0) {
@@ -2952,6 +2989,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     // the latency path; in large batches the mapping's divisions cost k_lz77 more than the
     // separate launch, profiles/r05k/)
     const uint32_t self_map = a.uniform_nseg && a.nseg <= LZ_SELF_MAP_SEGS ? 1u : 0u;
+    const bool solo = !prof && a.ntiles == 1 && a.nblk == 1;  // one tile, one Huffman block
     if (!self_map)
         hipLaunchKernelGGL(k_seg_map, dim3((a.nseg + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles, a.nseg,
                            a.uniform_nseg, a.uniform_rcp, a.seg_tile, a.info, a.blk);
@@ -2971,13 +3009,14 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
                            a.hist, a.codes, a.stamps);
     else if (a.nblk <= HUFF_SMALL_BLKS)  // a small batch: every segment's histogram loads at once
         hipLaunchKernelGGL((k_huff<DC, false, 34>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
-                           a.hist, a.codes, a.stamps);
+                           a.hist, a.codes, a.stamps, solo ? a.tiles : nullptr, a.offs, a.offs_host);
     else
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
     if (ev && fine) (void)hipEventRecord(ev[1], st);
     if (ev2) (void)hipEventRecord(ev2[1], st);
-    if (a.ntiles <= 1024) {
+    if (solo) {  // (k_huff wrote the offsets)
+    } else if (a.ntiles <= 1024) {
         hipLaunchKernelGGL(k_sizes_scan, dim3(1), dim3(1024), 0, st, a.tiles, a.ntiles, a.blk, a.offs, a.offs_host);
     } else {
         hipLaunchKernelGGL(k_seg_sizes, dim3((a.ntiles + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles,

@@ -999,6 +999,9 @@ struct Coalescer {
     // PBX_TIMELINE=1: per-request stage durations (us), summarised on stderr at shutdown
     // (the configs[0] single-request latency breakdown, scripts/c1_latency.py)
     bool timeline = getenv("PBX_TIMELINE") != nullptr;
+    // a request that finds the coalescer idle is launched by its own thread ($PBX_DIRECT=0: always
+    // by the launcher thread)
+    bool direct = !getenv("PBX_DIRECT") || atoi(getenv("PBX_DIRECT")) != 0;
     std::vector<std::array<double, 6>> tl;
     std::thread launcher;
     std::vector<std::thread> completers;
@@ -1047,9 +1050,19 @@ struct Coalescer {
             delete p;
             return fail(PBX_E_INTERNAL, "context is shutting down");
         }
-        queue.push_back(p);
-        cv_launch.notify_one();
         const int64_t to = ctx->timeout_us;
+        if (queue.empty() && inflight == 0 && direct) {
+            // an idle coalescer: this thread plans and launches its own request (no hand-off
+            // to the launcher thread, whose wake-up the lone request would wait for); the
+            // completer fetches it as any other batch, so the deadline below still holds
+            inflight++;
+            g.unlock();
+            launch_take(std::vector<Pending*>{p});
+            g.lock();
+        } else {
+            queue.push_back(p);
+            cv_launch.notify_one();
+        }
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(to > 0 ? to : 0);
         // a lone caller (an idle coalescer: the single-request latency path) polls for its
         // result before it blocks -- a condition-variable wake-up costs it ~15 us
@@ -1102,6 +1115,16 @@ struct Coalescer {
                 }
                 inflight++;
             }
+            launch_take(std::move(take));
+        }
+        std::lock_guard<std::mutex> g(mu);
+        cv_complete.notify_all();
+    }
+    // Plans and launches one batch of taken requests (inflight already counts it) and hands
+    // it to the completers.
+    void launch_take(std::vector<Pending*> take) {
+        (void)hipSetDevice(ctx->device);
+        {
             std::vector<pbx_tile_req> reqs(take.size());
             for (size_t i = 0; i < take.size(); i++) reqs[i] = take[i]->req;
             Flight f{nullptr, std::move(take), PBX_OK, {}};
@@ -1126,8 +1149,6 @@ struct Coalescer {
             }
             cv_complete.notify_one();
         }
-        std::lock_guard<std::mutex> g(mu);
-        cv_complete.notify_all();
     }
     void complete_loop() {
         (void)hipSetDevice(ctx->device);
