@@ -657,6 +657,17 @@ PBX_HD void ph_rle_mark(uint32_t tid, SM& S) {
         if (i == 0 || cl_len_at(S, i) != cl_len_at(S, i - 1)) Ops::aor(&S.rbm[i >> 5], 1u << (i & 31));
 }
 
+// rle_nsyms without its loop (the device's wave-level RLE): 18s of 138 then the remainder
+// (one more 18 from 11, one 17 from 3, else plain zeros); v, 16s of 6, then the remainder.
+PBX_HD uint32_t rle_nsyms_closed(uint32_t v, uint32_t run) {
+    if (v == 0) {
+        const uint32_t q = run / 138, m = run % 138;
+        return q + (m >= 3 ? 1u : m);
+    }
+    const uint32_t r1 = run - 1;
+    return 1 + r1 / 6 + ((r1 % 6) >= 3 ? 1u : r1 % 6);
+}
+
 PBX_HD uint32_t rle_nsyms(uint32_t v, uint32_t run) {
     if (v == 0) {
         uint32_t n = 0;

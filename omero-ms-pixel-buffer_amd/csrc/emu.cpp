@@ -344,6 +344,15 @@ uint32_t pbxemu_crc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
 
 // The latency forms k_frame_wave uses (pbx_common.h) against zlib's bitwise ones: the number
 // of the n seeded random pairs (and bytes) on which they differ.
+// rle_nsyms_closed (the device's wave RLE) against rle_nsyms for every run of every length
+// value: the number of mismatches.
+uint32_t pbxemu_rle_closed_mismatches(void) {
+    uint32_t bad = 0;
+    for (uint32_t v = 0; v < 16; v++)
+        for (uint32_t run = 1; run <= 320; run++) bad += rle_nsyms_closed(v, run) != rle_nsyms(v, run);
+    return bad;
+}
+
 uint64_t pbxemu_crc_fast_mismatches(uint64_t n, uint64_t seed) {
     uint64_t x = seed | 1, bad = 0;
     auto next = [&]() {  // splitmix64

@@ -1692,6 +1692,68 @@ __device__ __forceinline__ void assign_wave(SM& S, uint32_t lane) {
     }
 }
 
+// The code-length RLE (ph_rle_mark / _count / the scan / _emit) on one wave, same symbols
+// and counts: lane l holds code lengths l, l + 64, ..; run starts by DPP compares and five
+// ballots (no run-start bitmask walked in LDS), every run's length from the next set bit of
+// the masks, its symbol count in closed form, the offsets by a wave scan, then each run's
+// first lane writes its symbols.
+template <class SM>
+__device__ __forceinline__ void rle_wave(SM& S, uint32_t lane) {
+    const uint32_t hlit = S.misc[M_HLIT], ntot = hlit + S.misc[M_HDIST];
+    uint32_t v[5];
+    uint64_t M[5];
+    uint32_t prev_last = 0xFFFFFFFFu;  // (position -1: no length)
+#pragma unroll
+    for (int it = 0; it < 5; it++) {
+        const uint32_t i = lane + 64u * it;
+        v[it] = i < ntot ? (i < hlit ? S.lcode[i] >> 16 : S.dcode[i - hlit] >> 16) : 0xFFu;
+        const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp((int)prev_last, (int)v[it], 0x138, 0xF, 0xF, false);  // wave_shr:1
+        M[it] = __ballot(i < ntot && v[it] != pv);
+        prev_last = (uint32_t)__builtin_amdgcn_readlane((int)v[it], 63);
+    }
+    uint32_t F[5];  // the first run start in the blocks after it (ntot: none)
+    F[4] = ntot;
+#pragma unroll
+    for (int it = 3; it >= 0; it--) F[it] = M[it + 1] ? 64u * (it + 1) + (uint32_t)__builtin_ctzll(M[it + 1]) : F[it + 1];
+    uint32_t cnt[5], run[5], base = 0, off[5];
+#pragma unroll
+    for (int it = 0; it < 5; it++) {
+        const uint32_t i = lane + 64u * it;
+        const bool st = (M[it] >> lane) & 1ull;
+        const uint64_t hi = lane < 63 ? M[it] & (~0ull << (lane + 1)) : 0ull;
+        const uint32_t nx = hi ? 64u * it + (uint32_t)__builtin_ctzll(hi) : F[it];
+        run[it] = st ? (nx < ntot ? nx : ntot) - i : 0u;
+        const uint32_t c = st ? rle_nsyms_closed(v[it], run[it]) : 0u;
+        cnt[it] = c;
+        const uint32_t incl = wave_incl_scan_dpp(c);
+        off[it] = base + incl - c;
+        base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    if (lane == 0) S.misc[M_NRLE] = base;
+    uint32_t* cf = S.hw.clfreq;
+#pragma unroll
+    for (int it = 0; it < 5; it++) {
+        if (!cnt[it]) continue;
+        uint32_t k = off[it], r = run[it];
+        const uint32_t x = v[it];
+        if (x == 0) {
+            while (r >= 11) {
+                const uint32_t n = r < 138 ? r : 138;
+                S.rle[k++] = 18u | ((n - 11) << 8); atomicAdd(&cf[18], 1u); r -= n;
+            }
+            if (r >= 3) { S.rle[k++] = 17u | ((r - 3) << 8); atomicAdd(&cf[17], 1u); r = 0; }
+            while (r) { S.rle[k++] = 0; atomicAdd(&cf[0], 1u); r--; }
+        } else {
+            S.rle[k++] = x; atomicAdd(&cf[x], 1u); r--;
+            while (r >= 3) {
+                const uint32_t n = r < 6 ? r : 6;
+                S.rle[k++] = 16u | ((n - 3) << 8); atomicAdd(&cf[16], 1u); r -= n;
+            }
+            while (r) { S.rle[k++] = x; atomicAdd(&cf[x], 1u); r--; }
+        }
+    }
+}
+
 // The 19-symbol code-length code on one wave (lane s = symbol s); same result as ph_clen:
 // stable (freq, symbol) order, serial two-queue merge on lane-held arrays, depths, zlib's
 // overflow repair at 7 bits, longest codes to the least frequent, canonical codes.
@@ -1897,17 +1959,26 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     ph_rle_init<C>(tid, S);
     __syncthreads();
     stamp();
-    ph_rle_mark<C, DevOps>(tid, S);
-    __syncthreads();
-    ph_rle_count<C>(tid, S);
-    __syncthreads();
-    {
-        const uint32_t nr = wave_scan_excl_add<RLEN>(S.rcnt, tid);
-        if (tid == 0) S.misc[M_NRLE] = nr;
+#ifndef PBX_HUFF_RLE_WAVE
+#define PBX_HUFF_RLE_WAVE 0  // 0: the generic phases of deflate_seg.h (the emulator's)
+#endif
+    if (PBX_HUFF_RLE_WAVE) {
+        rle_wave(S, tid);
+        __syncthreads();
+        stamp();
+    } else {
+        ph_rle_mark<C, DevOps>(tid, S);
+        __syncthreads();
+        ph_rle_count<C>(tid, S);
+        __syncthreads();
+        {
+            const uint32_t nr = wave_scan_excl_add<RLEN>(S.rcnt, tid);
+            if (tid == 0) S.misc[M_NRLE] = nr;
+        }
+        __syncthreads();
+        stamp();
+        ph_rle_emit<C, DevOps>(tid, S);
     }
-    __syncthreads();
-    stamp();
-    ph_rle_emit<C, DevOps>(tid, S);
     __syncthreads();
     stamp();
     clen_wave(S, tid);

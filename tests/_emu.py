@@ -34,6 +34,7 @@ def lib():
         L.pbxemu_crc_combine.restype = ctypes.c_uint32
         L.pbxemu_crc_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         L.pbxemu_crc_fast_mismatches.restype = ctypes.c_uint64
+        L.pbxemu_rle_closed_mismatches.restype = ctypes.c_uint32
         L.pbxemu_crc_fast_mismatches.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         _lib = L
     return _lib
@@ -58,6 +59,10 @@ def crc_combine(c1, c2, len2):
 
 def crc_fast_mismatches(n, seed):
     return lib().pbxemu_crc_fast_mismatches(n, seed)
+
+
+def rle_closed_mismatches():
+    return lib().pbxemu_rle_closed_mismatches()
 
 
 def huffman(hist, sl, last):

@@ -40,6 +40,12 @@ def test_crc_nibble_step_forms_match_zlib():
     assert _emu.crc_fast_mismatches(2_000_000, 7) == 0
 
 
+def test_rle_symbol_counts_closed_form():
+    """k_huff's wave-level code-length RLE counts each run's symbols in closed form: equal to the
+    emulator's loop (rle_nsyms) for every run length 1..320 of every code length 0..15."""
+    assert _emu.rle_closed_mismatches() == 0
+
+
 def test_crc_combine_matches_zlib():
     rng = np.random.default_rng(1)
     for la, lb in [(0, 5), (5, 0), (1, 1), (100, 3000), (17, 65537)]:
