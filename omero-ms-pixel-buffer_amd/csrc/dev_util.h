@@ -107,7 +107,7 @@ __device__ uint32_t wave_scan_excl_add(uint32_t* arr, uint32_t lane) {
 }
 
 __device__ __forceinline__ uint32_t bswap16x2(uint32_t v) {
-    return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu);
+    return __builtin_amdgcn_perm(v, v, 0x02030001u);  // [b1, b0, b3, b2]: one v_perm_b32
 }
 
 // Swap each big-endian sample of a 16-byte vector to/from little-endian.

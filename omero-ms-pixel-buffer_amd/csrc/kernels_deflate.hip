@@ -1960,9 +1960,9 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     __syncthreads();
     stamp();
 #ifndef PBX_HUFF_RLE_WAVE
-#define PBX_HUFF_RLE_WAVE 0  // 0: the generic phases of deflate_seg.h (the emulator's)
+#define PBX_HUFF_RLE_WAVE 1  // 1: rle_wave (five ballots); 0: the generic phases of deflate_seg.h (the emulator's); 2: rle_wave in the batch variant only
 #endif
-    if (PBX_HUFF_RLE_WAVE) {
+    if (PBX_HUFF_RLE_WAVE == 1 || (PBX_HUFF_RLE_WAVE == 2 && !KEEP)) {
         rle_wave(S, tid);
         __syncthreads();
         stamp();

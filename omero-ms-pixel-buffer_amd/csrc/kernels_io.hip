@@ -822,6 +822,36 @@ __device__ __forceinline__ uint32_t f3_wave_sum(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
+// Sums over the wave of five per-lane values.  Four go through gfx950's lane swaps: the upper
+// 32 lanes of one register trade places with the lower 32 of another (v_permlane32_swap), so
+// one add leaves s0's 32-lane partials in lanes 0-31 and s1's in 32-63 (likewise s2 / s3);
+// swapping odd 16-lane rows of that with even rows of the other (v_permlane16_swap) and one
+// add leaves rows holding s0, s2, s1, s3; four row_shr steps finish all four at once (lane 15
+// of each row).  s4 takes the plain path.  14 VALU operations fewer than five f3_wave_sums.
+#ifndef PBX_F3_SWAP_SUMS
+#define PBX_F3_SWAP_SUMS 1
+#endif
+__device__ __forceinline__ void f3_wave_sums5(const uint32_t (&s)[5], uint32_t (&t)[5]) {
+    if (!PBX_F3_SWAP_SUMS) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) t[k] = f3_wave_sum(s[k]);
+        return;
+    }
+    const auto p01 = __builtin_amdgcn_permlane32_swap(s[0], s[1], false, false);
+    const auto p23 = __builtin_amdgcn_permlane32_swap(s[2], s[3], false, false);
+    const uint32_t a = p01[0] + p01[1], b = p23[0] + p23[1];  // [s0 | s1], [s2 | s3]
+    const auto q = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    uint32_t x = q[0] + q[1];  // rows: s0, s2, s1, s3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    t[0] = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    t[2] = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    t[1] = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    t[3] = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    t[4] = f3_wave_sum(s[4]);
+}
 // The previous lane's chunk (wave shift right by one lane); lane 0 gets `first`.
 __device__ __forceinline__ uint4 f3_prev_lane(const uint4& x, const uint4& first) {
     return make_uint4((uint32_t)__builtin_amdgcn_update_dpp((int)first.x, (int)x.x, 0x138, 0xF, 0xF, false),
@@ -868,6 +898,86 @@ __device__ __forceinline__ uint4 f3_pick(const uint4 (&v)[G], uint32_t g) {
     return r;
 }
 
+// Paeth's f16 lane forms of a row (paeth_pair_h): word j of chunk g as [0] = bytes 0, 1 and
+// [1] = bytes 2, 3, each byte in a 16-bit lane under 0x64 (one v_perm_b32 each), and the same
+// forms of the bytes bpp to their left.  In this layout the left forms are other words' forms
+// (bpp 2: [0] = the previous word's [1], [1] = this word's [0]; bpp 4 / 8: the word one / two
+// back), or one v_alignbyte each (bpp 1), so a row's forms are built once, reused as the next
+// row's up forms, and only the previous lane's last words cross lanes (one DPP each; lane 0:
+// the previous chunk group's lane 63, or zero bytes before the row).
+constexpr uint32_t F3_PF_LO = 0x00050004u, F3_PF_HI = 0x00070006u, F3_PF_BIAS = 0x64646464u;
+constexpr uint32_t F3_PF_ZERO = 0x64006400u;  // the form of two zero bytes
+template <uint32_t G, uint32_t BPP>
+__device__ __forceinline__ void f3_paeth_forms(const uint4 (&v)[G], uint32_t (&X)[G][4][2],
+                                               uint32_t (&L)[G][4][2]) {
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) {
+        const uint32_t w[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            X[g][j][0] = __builtin_amdgcn_perm(w[j], F3_PF_BIAS, F3_PF_LO);
+            X[g][j][1] = __builtin_amdgcn_perm(w[j], F3_PF_BIAS, F3_PF_HI);
+        }
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) {
+        // the previous lane's forms of words 2 and 3 (only those the sample size reads)
+        uint32_t P[2][2];
+#pragma unroll
+        for (uint32_t j = 2; j < 4; j++)
+#pragma unroll
+            for (uint32_t s = 0; s < 2; s++) {
+                const bool need = BPP == 8 || (j == 3 && (BPP == 4 || s == 1));
+                if (!need) { P[j - 2][s] = 0; continue; }
+                const uint32_t first = g ? (uint32_t)__builtin_amdgcn_readlane((int)X[g - 1][j][s], 63) : F3_PF_ZERO;
+                P[j - 2][s] = (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)X[g][j][s], 0x138, 0xF, 0xF, false);
+            }
+        auto W = [&](int j, uint32_t s) -> uint32_t { return j >= 0 ? X[g][j][s] : P[j + 2][s]; };
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (BPP == 1) {
+                L[g][j][0] = __builtin_amdgcn_alignbyte(X[g][j][0], W(j - 1, 1), 2);
+                L[g][j][1] = __builtin_amdgcn_alignbyte(X[g][j][1], X[g][j][0], 2);
+            } else if (BPP == 2) {
+                L[g][j][0] = W(j - 1, 1);
+                L[g][j][1] = X[g][j][0];
+            } else if (BPP == 4) {
+                L[g][j][0] = W(j - 1, 0);
+                L[g][j][1] = W(j - 1, 1);
+            } else {
+                L[g][j][0] = W(j - 2, 0);
+                L[g][j][1] = W(j - 2, 1);
+            }
+        }
+    }
+}
+// Paeth's two decisions for a pair of bytes (paeth_pair_h without the selects): the f16 sign
+// bit of each lane set where pa > min(pb, pc) (na) and where pb > pc (nb).
+__device__ __forceinline__ void paeth_pair_signs(uint32_t a, uint32_t b, uint32_t c, uint32_t& na, uint32_t& nb) {
+    const f3_h2 A = __builtin_bit_cast(f3_h2, a), B = __builtin_bit_cast(f3_h2, b), C = __builtin_bit_cast(f3_h2, c);
+    const f3_h2 d1 = B - C, d2 = A - C, d3 = d1 + d2;
+    const f3_h2 pa = __builtin_elementwise_max(d1, -d1), pb = __builtin_elementwise_max(d2, -d2),
+                pc = __builtin_elementwise_max(d3, -d3);
+    na = __builtin_bit_cast(uint32_t, (f3_h2)(__builtin_elementwise_min(pb, pc) - pa));
+    nb = __builtin_bit_cast(uint32_t, (f3_h2)(pc - pb));
+}
+// Paeth's prediction of a word from the forms of its left, up and up-left bytes and the same
+// bytes as words (a, b, c): the four lanes' sign bits become a byte mask in ONE v_perm_b32
+// (selectors 8..11 replicate bits 15 / 31 of each source), and two bitwise selects pick
+// c over b, then that over a, byte by byte.
+__device__ __forceinline__ uint32_t f3_paeth_word(const uint32_t (&l)[2], const uint32_t (&u)[2], const uint32_t (&ul)[2],
+                                                  uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t na0, nb0, na1, nb1;
+    paeth_pair_signs(l[0], u[0], ul[0], na0, nb0);
+    paeth_pair_signs(l[1], u[1], ul[1], na1, nb1);
+    const uint32_t ma = __builtin_amdgcn_perm(na1, na0, 0x0B0A0908u), mb = __builtin_amdgcn_perm(nb1, nb0, 0x0B0A0908u);
+    const uint32_t t = (mb & c) | (~mb & b);
+    return (ma & t) | (~ma & a);
+}
+#ifndef PBX_F3_CARRY
+#define PBX_F3_CARRY 1  // 1: a row's Paeth forms are kept for the next row; 0: rebuilt from it
+#endif
+
 // One wave's run of rows, specialised on the sample size (the left-neighbour shifts, the byte
 // swap and the sign flip are then fixed: no per-row branches or register moves on bpp).
 template <uint32_t G, bool ADAPTIVE, uint32_t BPP>
@@ -897,22 +1007,58 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
             uint4 q = v[g];
             if (swap) q = swap16(q, (int)bpp);
             if (flip) q = flip_msb(q, (int)bpp);
-            v[g] = 64 * g + lane < nc ? q : Z;
+            // by a mask, not a select of the two vectors (which the compiler may turn into
+            // a select between their stack slots: scratch); only a group the row ends in
+            if (nc < 64 * (g + 1)) {
+                const uint32_t m = 0u - (uint32_t)(64 * g + lane < nc);
+                q = make_uint4(q.x & m, q.y & m, q.z & m, q.w & m);
+            }
+            v[g] = q;
         }
     };
     const uint32_t rs = r0 ? r0 - 1 : 0;  // first row filtered (the one before the run: not stored)
     const uint32_t rl = r1 - 1;
     uint4 tail = Z;  // the previous row's last filtered chunk (uniform)
     const uint32_t cl = nc - 1, gl = cl >> 6, ll = cl & 63;
+    // Paeth's forms of the row above (PBX_F3_CARRY: the previous step's own, else rebuilt)
+    // and (PBX_F3_CARRY) its left bytes as words
+    uint32_t UF[G][4][2], ULF[G][4][2], ULB[G][4];
     // filter row r (cur, converted here) against up (already converted) and store it
     auto step = [&](const uint4 (&up)[G], uint4 (&cur)[G], uint32_t r) {
         conv(cur);
-        uint4 lft[G], ul[G];
+        uint4 lft[G];
 #pragma unroll
-        for (uint32_t g = 0; g < G; g++) {
+        for (uint32_t g = 0; g < G; g++)
             lft[g] = g ? f3_prev_lane(cur[g], f3_readlane(cur[g - 1], 63)) : f3_prev_lane0(cur[g]);
-            ul[g] = g ? f3_prev_lane(up[g], f3_readlane(up[g - 1], 63)) : f3_prev_lane0(up[g]);
-        }
+        // the Paeth prediction of every word (forms of this row built here; the row above's
+        // kept from the previous step, or rebuilt)
+        auto paeth_row = [&](const uint32_t (&lw)[G][4], uint32_t (&pp)[G][4]) {  // lw: left bytes
+            uint32_t XF[G][4][2], LF[G][4][2];
+            f3_paeth_forms<G, BPP>(cur, XF, LF);
+            if (!PBX_F3_CARRY) f3_paeth_forms<G, BPP>(up, UF, ULF);
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t c = PBX_F3_CARRY ? ULB[g][j] : __builtin_amdgcn_perm(ULF[g][j][1], ULF[g][j][0], 0x06040200u);
+                    pp[g][j] = f3_paeth_word(LF[g][j], UF[g][j], ULF[g][j], lw[g][j], u[j], c);
+                }
+            }
+            if (PBX_F3_CARRY) {
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++)
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        ULB[g][j] = lw[g][j];
+#pragma unroll
+                        for (uint32_t s = 0; s < 2; s++) {
+                            UF[g][j][s] = XF[g][j][s];
+                            ULF[g][j][s] = LF[g][j][s];
+                        }
+                    }
+            }
+        };
         uint4 f[G];
         uint32_t ft = fixed;
         if (ADAPTIVE) {
@@ -921,11 +1067,13 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
             // filter's residuals are formed once, after the choice
             uint32_t pw[G][4][4];
             uint32_t sm[5] = {0, 0, 0, 0, 0};
+            uint32_t pp[G][4], lw[G][4];
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) f3_left(cur[g], lft[g], bpp, lw[g]);
+            paeth_row(lw, pp);
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                uint32_t l[4], lu[4];
-                f3_left(cur[g], lft[g], bpp, l);
-                f3_left(up[g], ul[g], bpp, lu);
+                const uint32_t(&l)[4] = lw[g];
                 const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
                 const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
 #pragma unroll
@@ -933,7 +1081,7 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
                     pw[g][0][j] = l[j];
                     pw[g][1][j] = u[j];
                     pw[g][2][j] = avg8(l[j], u[j]);
-                    pw[g][3][j] = paeth4(l[j], u[j], lu[j]);
+                    pw[g][3][j] = pp[g][j];
                 }
                 if (64 * g + lane < nc) {
 #pragma unroll
@@ -944,46 +1092,75 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
                     }
                 }
             }
-            uint32_t best = 0, bs = f3_wave_sum(sm[0]);
+            uint32_t tot[5];
+            f3_wave_sums5(sm, tot);
+            uint32_t best = 0, bs = tot[0];
 #pragma unroll
             for (uint32_t k = 1; k < 5; k++) {
-                const uint32_t v = f3_wave_sum(sm[k]);
-                if (v < bs) { bs = v; best = k; }
+                if (tot[k] < bs) { bs = tot[k]; best = k; }
             }
             ft = __builtin_amdgcn_readfirstlane(best);
 #ifndef PBX_F3_ADAPT_SELECT
 #define PBX_F3_ADAPT_SELECT 1  // 1: the chosen prediction by a uniform branch; 0: by masks in SGPRs
 #endif
+            if (PBX_F3_ADAPT_SELECT) {
+                // ft is uniform (an SGPR): one scalar branch per row to the subtraction it
+                // needs.  Each arm ends in its own (empty) asm statement: otherwise the
+                // compiler sinks the four identical sub8 chains below the branch and selects
+                // their operand per word (~100 scalar instructions and branches a row).
+                auto resid = [&](auto kc) {  // kc: the candidate's index as a type (a constant)
+                    constexpr uint32_t k = decltype(kc)::value;
 #pragma unroll
-            for (uint32_t g = 0; g < G; g++) {
-                uint32_t o[4];
-                const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
-                if (PBX_F3_ADAPT_SELECT) {
-                    // ft is uniform (an SGPR): a scalar branch to the one subtraction it needs
-                    if (ft == 0) {
+                    for (uint32_t g = 0; g < G; g++) {
+                        uint32_t o[4];
+                        const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
 #pragma unroll
-                        for (uint32_t j = 0; j < 4; j++) o[j] = x[j];
-                    } else {
-                        const uint32_t k = ft - 1;
-#pragma unroll
-                        for (uint32_t j = 0; j < 4; j++)
-                            o[j] = sub8(x[j], k == 0 ? pw[g][0][j] : k == 1 ? pw[g][1][j] : k == 2 ? pw[g][2][j] : pw[g][3][j]);
+                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], pw[g][k][j]);
+                        f[g] = make_uint4(o[0], o[1], o[2], o[3]);
                     }
+                };
+                if (ft == 0) {
+#pragma unroll
+                    for (uint32_t g = 0; g < G; g++) f[g] = cur[g];
+                    asm volatile("; f3 none");
+                } else if (ft == 1) {
+                    resid(std::integral_constant<uint32_t, 0>{});
+                    asm volatile("; f3 sub");
+                } else if (ft == 2) {
+                    resid(std::integral_constant<uint32_t, 1>{});
+                    asm volatile("; f3 up");
+                } else if (ft == 3) {
+                    resid(std::integral_constant<uint32_t, 2>{});
+                    asm volatile("; f3 avg");
                 } else {
-                    // the prediction by masks in SGPRs (None predicts 0), then one sub8
-                    const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
-                    const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+                    resid(std::integral_constant<uint32_t, 3>{});
+                    asm volatile("; f3 paeth");
+                }
+            } else {
+                // the prediction by masks in SGPRs (None predicts 0), then one sub8
+                const uint32_t m1 = 0u - (uint32_t)(ft == 1), m2 = 0u - (uint32_t)(ft == 2);
+                const uint32_t m3 = 0u - (uint32_t)(ft == 3), m4 = 0u - (uint32_t)(ft == 4);
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++) {
+                    uint32_t o[4];
+                    const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
 #pragma unroll
                     for (uint32_t j = 0; j < 4; j++)
                         o[j] = sub8(x[j], (pw[g][0][j] & m1) | (pw[g][1][j] & m2) | (pw[g][2][j] & m3) | (pw[g][3][j] & m4));
+                    f[g] = make_uint4(o[0], o[1], o[2], o[3]);
                 }
-                f[g] = make_uint4(o[0], o[1], o[2], o[3]);
             }
         } else {
             // one filter for every row: only it (ft is uniform: a scalar branch)
+            uint32_t pp[G][4], lw[G][4];
+            if (ft == 4) {
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++) f3_left(cur[g], lft[g], bpp, lw[g]);
+                paeth_row(lw, pp);
+            }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                uint32_t l[4], lu[4], o[4];
+                uint32_t l[4], o[4];
                 const uint32_t x[4] = {cur[g].x, cur[g].y, cur[g].z, cur[g].w};
                 const uint32_t u[4] = {up[g].x, up[g].y, up[g].z, up[g].w};
                 if (ft == 2) {
@@ -998,9 +1175,8 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
 #pragma unroll
                         for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], avg8(l[j], u[j]));
                     } else {
-                        f3_left(up[g], ul[g], bpp, lu);
 #pragma unroll
-                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], paeth4(l[j], u[j], lu[j]));
+                        for (uint32_t j = 0; j < 4; j++) o[j] = sub8(x[j], pp[g][j]);
                     }
                 }
                 f[g] = make_uint4(o[0], o[1], o[2], o[3]);
@@ -1050,9 +1226,16 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
 #pragma unroll
         for (uint32_t g = 0; g < G; g++) B[0][g] = Z;
     }
+    if (PBX_F3_CARRY && (ADAPTIVE || fixed == 4)) {
+        f3_paeth_forms<G, BPP>(B[0], UF, ULF);
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++)
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) ULB[g][j] = __builtin_amdgcn_perm(ULF[g][j][1], ULF[g][j][0], 0x06040200u);
+    }
     const uint32_t nrow = r1 - rs, nfull = nrow - nrow % NB;
     uint32_t r = rs;
-    for (; r < rs + nfull; r += NB) {
+    for (; r < rs + nfull; r = __builtin_amdgcn_readfirstlane(r + NB)) {
 #pragma unroll
         for (uint32_t k = 0; k < NB; k++) {
             step(B[k], B[(k + 1) % NB], r + k);
