@@ -798,11 +798,28 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     // (ml equal bytes of a candidate there, ml = match_minlen), the only way a match of wave b
     // can run on into wave b + 1.  From the bytes alone, the same in every wave: a uniform
     // decision, no barrier (noise: almost never; then every wave's parse is final at once).
-    uint32_t reachm;
-    {
+#ifndef PBX_LZ_REACH_LATE
+#define PBX_LZ_REACH_LATE 1  // the boundary test after the candidate masks, loads unconditional
+#endif
+    auto reach_test = [&]() -> uint32_t {
         bool rb = false;
-        const uint32_t e = (lane + 1) * (uint32_t)C::SUB, a = sp.wl + e;
-        if (lane + 1 < (uint32_t)C::NW && e < sp.sl) {
+        const uint32_t e = (lane + 1) * (uint32_t)C::SUB;
+        const bool ok = lane + 1 < (uint32_t)C::NW && e < sp.sl;
+        if (PBX_LZ_REACH_LATE) {
+            // every lane loads (clamped addresses, no divergent branch): the loads can issue
+            // with the candidate masks' and are waited for once
+            const uint32_t a = ok ? sp.wl + e : 8u;
+            const uint2 v = *(const uint2*)&S.buf[(a >> 2) - 2];
+            const uint64_t x = ((uint64_t)v.y << 32) | v.x;  // bytes a - 8 .. a - 1
+            rb = ((x ^ (x << 8)) >> 40) == 0 || ((x ^ (x << 16)) >> 40) == 0;
+            const uint32_t d = cand_dist(sp, 2), mlr = match_minlen(d);
+            const bool okr = d && a >= mlr + d;
+            const uint32_t ar = okr ? a : 8u + mlr + d;
+            bool eq = v.y == lds_ld4(S, ar - 4 - d);
+            if (mlr == 6) eq = eq && ((v.x >> 16) ^ (lds_ld4(S, ar - 6 - d) & 0xFFFFu)) == 0;
+            rb = ok && (rb || (okr && eq));
+        } else if (ok) {
+            const uint32_t a = sp.wl + e;
             // the 8 bytes before the boundary: one aligned 8-byte LDS read (wl and e are
             // multiples of 16); distances 1 and 2 (ml = 3) compare them among themselves
             const uint2 v = *(const uint2*)&S.buf[(a >> 2) - 2];
@@ -816,13 +833,19 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
                 rb = rb || eq;
             }
         }
-        reachm = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)__ballot(rb));
+        uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)__ballot(rb));
 #ifdef PBX_LZ_NOREACH  // timing bound only (variant build): no boundary reachable, wrong output on runs
-        reachm = 0;
+        m = 0;
 #endif
-    }
+#ifdef PBX_LZ_REACH_DISCARD  // timing only (variant build): the test computed, its result dropped
+        asm volatile("" ::"s"(m));
+        m = 0;
+#endif
+        return m;
+    };
+    uint32_t reachm = PBX_LZ_REACH_LATE ? 0u : reach_test();
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
-    uint32_t M = 0;
+    uint32_t M = 0, cvb_n = 0;
     bool skip = true;
     if (active) {
         const uint32_t nval = se > p0 ? se - p0 : 0u;
@@ -927,10 +950,18 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         // >= ml equal bytes ending at the last byte, so se - ml is a paying start and the last
         // byte is in the union above (this lane's bits, or the previous lane's bits past its
         // chunk): exactly the waves where a paying run reaches the last byte walk.
-        const bool reach = ((reachm >> w) & 1u) != 0;
-        skip = PBX_LZ_COVBOUND && !reach &&
-               wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi)) <
-                   (uint32_t)C::MINCOV;
+        cvb_n = wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi));
+    }
+    if (PBX_LZ_REACH_LATE) reachm = reach_test();
+    if (active) skip = PBX_LZ_COVBOUND && !((reachm >> w) & 1u) && cvb_n < (uint32_t)C::MINCOV;
+#ifndef PBX_LZ_EARLY_OUT
+#define PBX_LZ_EARLY_OUT 1
+#endif
+    // (uniform) no boundary of the segment reachable and this wave's walk would keep nothing
+    // (noise: most waves): no records, no walk, no carry rounds -- the round-3 early return
+    if (PBX_LZ_EARLY_OUT && reachm == 0 && skip) {
+        if (lane == 0) S.w_nm[w] = 0;
+        return;
     }
     const uint64_t B = __ballot(M != 0);
     const uint32_t lsub = active ? se - ss : 0u;
@@ -3124,6 +3155,6 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
 // OUT=lib).
 #if !defined(PBX_TIMING_VARIANT) && (PBX_LZ_SKIP_STORE || PBX_LZ_SKIP_FILL || PBX_LZ_SKIP_HIST || \
     PBX_LZ_SKIP_OUT || PBX_ENC_SKIP_WRITE || PBX_ENC_SKIP_PATCH || PBX_ENC_SKIP_CRC || PBX_ENC_SKIP_STORE || \
-    PBX_HUFF_ONEREAD || defined(PBX_LZ_FAKE_LOAD) || defined(PBX_LZ_NOREACH))
+    PBX_HUFF_ONEREAD || defined(PBX_LZ_FAKE_LOAD) || defined(PBX_LZ_NOREACH) || defined(PBX_LZ_REACH_DISCARD))
 #error "output-changing timing knobs (PBX_LZ_SKIP_*, PBX_ENC_SKIP_*, PBX_HUFF_ONEREAD, PBX_LZ_FAKE_LOAD) need a variant build (-DPBX_TIMING_VARIANT, OUT=lib/var_*)"
 #endif

@@ -806,9 +806,12 @@ constexpr uint32_t F3_NT = 256;
 #ifndef PBX_F3_NB
 #define PBX_F3_NB 0
 #endif
-template <uint32_t G, bool ADAPTIVE>
+#ifndef PBX_F3_NB_SIMPLE
+#define PBX_F3_NB_SIMPLE 6  // Sub / Up / Avg rows (fewest registers per row)
+#endif
+template <uint32_t G, uint32_t FT>
 constexpr uint32_t F3_NB() {
-    return PBX_F3_NB ? PBX_F3_NB : G == 1 ? (ADAPTIVE ? 5 : 6) : 4;
+    return PBX_F3_NB ? PBX_F3_NB : G == 1 ? (FT == 5 ? 5 : FT == 4 ? 6 : PBX_F3_NB_SIMPLE) : 4;
 }
 
 // Sum over the wave: row prefix sums (row_shr, zero shifted in), then row_bcast:15 / :31 carry
@@ -980,7 +983,7 @@ __device__ __forceinline__ uint32_t f3_paeth_word(const uint32_t (&l)[2], const 
 
 // One wave's run of rows, specialised on the sample size (the left-neighbour shifts, the byte
 // swap and the sign flip are then fixed: no per-row branches or register moves on bpp).
-template <uint32_t G, bool ADAPTIVE, uint32_t BPP>
+template <uint32_t G, uint32_t FT, uint32_t BPP>
 __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t lane, uint8_t* __restrict__ stream) {
     constexpr uint32_t bpp = BPP;
     const uint32_t rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
@@ -989,7 +992,8 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
     const uint32_t r0 = __builtin_amdgcn_readfirstlane((wi - d.blk_first) * F3_RUN);
     const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + F3_RUN < h ? r0 + F3_RUN : h);
     const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
-    const uint32_t fixed = (uint32_t)d.filter;  // 1..4 (ADAPTIVE: 5)
+    constexpr bool ADAPTIVE = FT == 5;
+    constexpr uint32_t fixed = FT;  // the batch's filter: 1..4, 5 = adaptive (every tile's d.filter)
     const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
     uint8_t* out = stream + d.out_off;
     const uint4 Z = make_uint4(0, 0, 0, 0);
@@ -1216,7 +1220,7 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
     // B[k + 1] = cur, the other NB - 2 = loads in flight.  Moving registers that a load is still
     // filling would make the compiler wait for every load (vmcnt(0)) each row; loads are
     // unconditional (clamped to the run's last row) so the counters stay exact.
-    constexpr uint32_t NB = F3_NB<G, ADAPTIVE>();
+    constexpr uint32_t NB = F3_NB<G, FT>();
     uint4 B[NB][G];
     load_row(rs ? rs - 1 : 0, B[0]);
 #pragma unroll
@@ -1248,7 +1252,7 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
         if (r + k < r1) step(B[k], B[(k + 1) % NB], r + k);
 }
 
-template <uint32_t G, bool ADAPTIVE>
+template <uint32_t G, uint32_t FT>
 __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ dt, uint32_t ndt,
                                                   uint32_t nwaves, uint8_t* __restrict__ stream) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1258,25 +1262,34 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
     const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
     const TileDesc d = dt[ti];
     switch (__builtin_amdgcn_readfirstlane((uint32_t)d.bpp)) {  // a uniform branch
-    case 1: f3_run<G, ADAPTIVE, 1>(d, wi, lane, stream); break;
-    case 2: f3_run<G, ADAPTIVE, 2>(d, wi, lane, stream); break;
-    case 4: f3_run<G, ADAPTIVE, 4>(d, wi, lane, stream); break;
-    default: f3_run<G, ADAPTIVE, 8>(d, wi, lane, stream); break;
+    case 1: f3_run<G, FT, 1>(d, wi, lane, stream); break;
+    case 2: f3_run<G, FT, 2>(d, wi, lane, stream); break;
+    case 4: f3_run<G, FT, 4>(d, wi, lane, stream); break;
+    default: f3_run<G, FT, 8>(d, wi, lane, stream); break;
     }
 }
 
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
-                          uint32_t max_rb, bool adaptive, uint8_t* stream) {
+                          uint32_t max_rb, uint32_t filter, uint8_t* stream) {
     if (!ntiles || !nwaves) return hipSuccess;
+    if (filter < 1 || filter > 5) return hipErrorInvalidValue;  // every tile's d.filter (the batch's)
     const uint32_t blocks = (nwaves + F3_NT / 64 - 1) / (F3_NT / 64);
     const dim3 g(blocks), b(F3_NT);
-    if (max_rb <= 1024) {
-        if (adaptive) hipLaunchKernelGGL((k_filter3<1, true>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
-        else hipLaunchKernelGGL((k_filter3<1, false>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
-    } else {
-        if (adaptive) hipLaunchKernelGGL((k_filter3<2, true>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
-        else hipLaunchKernelGGL((k_filter3<2, false>), g, b, 0, st, d_tiles, ntiles, nwaves, stream);
+    // one body per filter: a fixed filter's kernel holds only its own registers
+#define PBX_F3_LAUNCH(GG)                                                                                     \
+    switch (filter) {                                                                                        \
+    case 1: hipLaunchKernelGGL((k_filter3<GG, 1>), g, b, 0, st, d_tiles, ntiles, nwaves, stream); break;   \
+    case 2: hipLaunchKernelGGL((k_filter3<GG, 2>), g, b, 0, st, d_tiles, ntiles, nwaves, stream); break;   \
+    case 3: hipLaunchKernelGGL((k_filter3<GG, 3>), g, b, 0, st, d_tiles, ntiles, nwaves, stream); break;   \
+    case 4: hipLaunchKernelGGL((k_filter3<GG, 4>), g, b, 0, st, d_tiles, ntiles, nwaves, stream); break;   \
+    default: hipLaunchKernelGGL((k_filter3<GG, 5>), g, b, 0, st, d_tiles, ntiles, nwaves, stream); break;  \
     }
+    if (max_rb <= 1024) {
+        PBX_F3_LAUNCH(1)
+    } else {
+        PBX_F3_LAUNCH(2)
+    }
+#undef PBX_F3_LAUNCH
     return hipGetLastError();
 }
 

@@ -41,9 +41,10 @@ hipError_t launch_filter2(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
                           uint32_t max_rb, uint8_t* stream);
 uint32_t filter2_band_rows();
 // PNG-filtered tiles with rows of whole 16-byte chunks (<= filter3_max_rb()): one wave per run
-// of filter3_run_rows() rows, no LDS (k_filter3); nwaves = the runs of every tile
+// of filter3_run_rows() rows, no LDS (k_filter3); nwaves = the runs of every tile; filter =
+// the batch's PNG filter (1..4, 5 = adaptive), which every tile's d.filter holds
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
-                          uint32_t max_rb, bool adaptive, uint8_t* stream);
+                          uint32_t max_rb, uint32_t filter, uint8_t* stream);
 uint32_t filter3_run_rows();
 uint32_t filter3_max_rb();
 uint32_t filter2_max_rb();

@@ -430,6 +430,7 @@ struct pbx_batch {
     uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
     uint32_t nfilt2_tiles = 0, filt2_blocks = 0, filt2_max_rb = 0;  // k_filter2 group
     uint32_t nfilt3_tiles = 0, filt3_waves = 0, filt3_max_rb = 0;   // k_filter3 group
+    uint32_t filt3_filter = 0;  // its PNG filter (the context's: every k_filter3 tile's d.filter)
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -2661,6 +2662,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.blk_first = b->filt3_waves;  // first wave (run of rows) of the tile
             b->filt3_waves += (uint32_t)((d.h + filter3_run_rows() - 1) / filter3_run_rows());
             b->filt3_max_rb = std::max<uint32_t>(b->filt3_max_rb, d.rowlen - 1);
+            b->filt3_filter = d.filter;
         } else {
             d.blk_first = b->filt_blocks;
             b->filt_blocks += (uint32_t)((d.h + filter_band_rows() - 1) / filter_band_rows());
@@ -2780,7 +2782,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
                            (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter3(st, d_rows + b->nrows_tiles + b->nfilt2_tiles, b->nfilt3_tiles, b->filt3_waves,
-                           b->filt3_max_rb, ctx->cfg.png_filter == PBX_FILTER_ADAPTIVE, (uint8_t*)b->d_stream));
+                           b->filt3_max_rb, b->filt3_filter, (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter(st, d_rows + b->nrows_tiles + b->nfilt2_tiles + b->nfilt3_tiles,
                           ndt - b->ndirect_tiles - b->nrows_tiles - b->nfilt2_tiles - b->nfilt3_tiles,
                           b->filt_blocks, (uint8_t*)b->d_stream));
