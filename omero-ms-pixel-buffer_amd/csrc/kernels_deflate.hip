@@ -1530,6 +1530,18 @@ __device__ __forceinline__ void sort512_wave(uint32_t* keys, uint32_t lane) {
         if (lane * 8 + r < KEYN) keys[lane * 8 + r] = v[r];
 }
 
+// LDS visibility among the lanes of ONE wave (its LDS operations complete in order): no
+// workgroup barrier, so the waves of a workgroup can run different trees (k_huff<.., 2>).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <bool WS>
+__device__ __forceinline__ void huff_sync() {
+    if (WS) wave_lds_sync(); else __syncthreads();
+}
+
 // The Huffman merge of tree T on one wave, in rounds.  Internal nodes are created in
 // non-decreasing weight order, so once node ni-1 (weight W) exists every node still to come
 // weighs >= W: the remaining leaves of weight <= W and the internal nodes not yet consumed
@@ -1538,13 +1550,14 @@ __device__ __forceinline__ void sort512_wave(uint32_t* keys, uint32_t lane) {
 // next round; a lone element pairs with the next leaf.  About 16 rounds replace the ~285
 // steps of the serial merge and give exactly its records (twoqueue_serial in deflate_seg.h,
 // which the emulator runs): step s = li0 | qi0 << 10 | cnt << 20.
-template <class SM>
+template <bool WS = false, class SM>
 __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(S.misc[T ? M_ND : M_NL]);
     const uint32_t base = __builtin_amdgcn_readfirstlane(T ? S.misc[M_NL] : 0u);
     const uint32_t* sk = S.hs.skey + base;
     uint32_t* iq = S.hs.iw[T];        // internal weights (aA, dB are free until the parents)
-    uint16_t* M = S.hs.leafpar.v;     // merged prefix: leaf index | 0x8000, or internal index
+    uint16_t* M = S.hs.leafpar[T];    // merged prefix: leaf index | 0x8000, or internal index
+                                      // (<= n entries: tree T's own part, the trees may run at once)
     uint32_t* rq = S.hs.rec[T];
     uint16_t* rs = S.hs.rst[T];
     if (n < 2) {
@@ -1557,7 +1570,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
         rs[0] = 0;
     }
     uint32_t li = 2, qi = 0, ni = 1, nr = 1;
-    __syncthreads();
+    huff_sync<WS>();
     while (ni + 1 < n) {
         if (lane == 0) rs[nr] = (uint16_t)ni;  // this round creates nodes ni..
         nr++;
@@ -1577,7 +1590,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
                 rq[ni] = li | (qi << 10) | (1u << 20);
             }
             li++; qi++; ni++;
-            __syncthreads();
+            huff_sync<WS>();
             continue;
         }
         for (uint32_t e = lane; e < a; e += 64) {  // leaf li+e: after internal nodes < it
@@ -1598,7 +1611,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
             }
             M[e + lo - li] = (uint16_t)(qi + e);
         }
-        __syncthreads();
+        huff_sync<WS>();
         const uint32_t m = P >> 1;
         // leaves among the first p merged elements, from the element at p
         auto leaves_before = [&](uint32_t p, uint32_t x) -> uint32_t {
@@ -1619,7 +1632,7 @@ __device__ __forceinline__ void huff_rounds_wave(SM& S, uint32_t T, uint32_t lan
         li += lb;
         qi += 2 * m - lb;
         ni += m;
-        __syncthreads();
+        huff_sync<WS>();
     }
     if (lane == 0) {
         rs[nr] = (uint16_t)ni;
@@ -1647,7 +1660,7 @@ __device__ __forceinline__ void parents_wave(SM& S, uint32_t tid) {
 // Depth of every internal node, root first: a node's parent is created in a later merge
 // round, so the rounds taken in reverse order each resolve in one parallel step (instead
 // of pointer jumping).  Result in dB, as ph_jump leaves it.
-template <class SM>
+template <bool WS = false, class SM>
 __device__ __forceinline__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint32_t nr = __builtin_amdgcn_readfirstlane(S.nrounds[T]);
     if (nr == 0) return;
@@ -1655,11 +1668,11 @@ __device__ __forceinline__ void depths_wave(SM& S, uint32_t T, uint32_t lane) {
     const uint16_t* par = S.hs.aA[T];
     const uint32_t root = S.hs.rst[T][nr] - 1u;  // the last round creates only the root
     if (lane == 0) dd[root] = 0;
-    __syncthreads();
+    huff_sync<WS>();
     for (int32_t r = (int32_t)nr - 2; r >= 0; r--) {
         const uint32_t k0 = S.hs.rst[T][r], k1 = S.hs.rst[T][r + 1];
         for (uint32_t k = k0 + lane; k < k1; k += 64) dd[k] = (uint16_t)(dd[par[k]] + 1);
-        __syncthreads();
+        huff_sync<WS>();
     }
 }
 
@@ -1788,7 +1801,7 @@ __device__ __forceinline__ void rle_wave(SM& S, uint32_t lane) {
 // The 19-symbol code-length code on one wave (lane s = symbol s); same result as ph_clen:
 // stable (freq, symbol) order, serial two-queue merge on lane-held arrays, depths, zlib's
 // overflow repair at 7 bits, longest codes to the least frequent, canonical codes.
-template <class SM>
+template <bool WS = false, class SM>
 __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
     const bool sy = lane < 19;
     uint32_t f = sy ? S.hw.clfreq[lane] : 0u;
@@ -1881,7 +1894,7 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
         S.hw.clcode[lane] = len ? (bitrev(code, len) | (len << 16)) : 0u;
         S.hw.clfreq[lane] = f;
     }
-    __syncthreads();
+    huff_sync<WS>();
     const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
     uint32_t o = 0;
 #pragma unroll
@@ -1896,6 +1909,10 @@ __device__ __forceinline__ void clen_wave(SM& S, uint32_t lane) {
 #endif
 constexpr uint32_t HUFF_LDSEG = PBX_HUFF_LDSEG;  // k_huff: segments whose histogram loads are in flight together
 constexpr uint32_t HUFF_SMALL_BLKS = 256;   // batches of at most this many blocks: k_huff<.., 34>
+#ifndef PBX_HUFF_SMALL_WAVES
+#define PBX_HUFF_SMALL_WAVES 2  // k_huff<.., 34>'s waves: 2 = the distance tree on a second wave
+#endif
+constexpr uint32_t HUFF_SMALL_WAVES = PBX_HUFF_SMALL_WAVES;
 constexpr uint32_t FRAME_WAVE_TILES = 256;  // batches of at most this many tiles: k_frame_wave
 constexpr uint32_t LZ_SELF_MAP_SEGS = 2048;  // k_lz77 maps its segment in batches of at most this many
 
@@ -1905,10 +1922,13 @@ constexpr uint32_t LZ_SELF_MAP_SEGS = 2048;  // k_lz77 maps its segment in batch
 // registers of more would cut the kernel's occupancy, profiles/r05r/); a small batch (the
 // single-request latency path: one block, one wave on the chip) loads up to 34 segments' at
 // once, one round of loads instead of three for a 512x512 uint16 tile.
-template <class C, bool PROF, uint32_t LDSEG = HUFF_LDSEG>
+// NWV = 2 (small batches): a second wave builds the distance tree (merge rounds and depths)
+// while the first builds the literal/length tree; everything else is the first wave's, with
+// wave-level LDS syncs instead of workgroup barriers.
+template <class C, bool PROF, uint32_t LDSEG = HUFF_LDSEG, uint32_t NWV = 1>
 // solo (a batch of one tile in one block, the single-request path): the block also writes the
 // tile's output offsets (and their mapped copy), so no k_sizes_scan launch follows.
-__global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict__ blk,
+__global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __restrict__ blk,
                                              SegInfo* __restrict__ info,
                                              const uint32_t* __restrict__ hist,
                                              uint32_t* __restrict__ codes,
@@ -1917,12 +1937,16 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
                                              uint64_t* __restrict__ offs = nullptr,
                                              uint64_t* __restrict__ offs_host = nullptr) {
     __shared__ HuffSmem<C> S;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x & 63;  // the lane (the code below is one wave's)
+    const uint32_t wv = NWV > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    const bool w0 = wv == 0;
+    // a sync among the lanes doing a phase: the workgroup's barrier when it is one wave
+    auto bar = [&]() { huff_sync<(NWV > 1)>(); };
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t seg0 = blk[b].seg0, nsg = blk[b].nseg;
     uint32_t nst = 0;
     auto stamp = [&]() {
-        if (PROF && tid == 0) stamps[(size_t)seg0 * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
+        if (PROF && threadIdx.x == 0) stamps[(size_t)seg0 * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
         nst++;
     };
     stamp();
@@ -1932,6 +1956,19 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
     constexpr bool KEEP = LDSEG > 24;
     uint32_t hr0[KEEP ? LDSEG : 1][5];
     uint32_t hs[5] = {0, 0, 0, 0, 0};
+    uint32_t sl = 0, last = 0;
+    // the solo tile's container fields, for its output size at the end (loaded now: a lone
+    // block would otherwise wait on one more load round there)
+    uint32_t solo_flags = 0, solo_hdr = 0;
+    if (solo) {
+        solo_flags = solo->flags;
+        solo_hdr = solo->tiff_hdr;
+    }
+    if (w0) {  // (NWV = 2: the second wave waits at the barrier after the sort)
+    // the segments' lengths (lane k: segment k) and the last one's flag, issued with the
+    // histogram loads (one round trip for all of them)
+    const uint32_t my_sl = tid < nsg ? info[seg0 + tid].sl : 0u;
+    last = info[seg0 + nsg - 1].last;
     for (uint32_t k0 = 0; k0 < nsg; k0 += LDSEG) {  // LDSEG segments' loads in flight
         uint32_t hr[LDSEG][5];
 #pragma unroll
@@ -1956,78 +1993,86 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         const uint32_t v = i == 256 ? 1u : hs[j];  // one end of block (every segment counted one)
         if (i < 288) S.lfreq[i] = v; else S.dfreq[i - 288] = v;
     }
-    // the segments' lengths: lane k loads segment k's (one round trip), kept in LDS
-    const uint32_t my_sl = tid < nsg ? info[seg0 + tid].sl : 0u;
     if (tid < nsg) S.sls[tid] = my_sl;
-    const uint32_t sl = wave_sum(my_sl);
-    const uint32_t last = info[seg0 + nsg - 1].last;
+    sl = wave_sum(my_sl);
     ph_huff_init<C>(tid, S);
-    __syncthreads();
+    bar();
     ph_keys<C, DevOps>(tid, S);
-    __syncthreads();
+    bar();
     stamp();
     sort512_wave(S.hs.skey, tid);
+    }
     __syncthreads();
     stamp();
-    huff_rounds_wave(S, 0, tid);
-    huff_rounds_wave(S, 1, tid);
+    if (NWV > 1) {
+        huff_rounds_wave<true>(S, wv, tid);  // wave T builds tree T
+    } else {
+        huff_rounds_wave(S, 0, tid);
+        huff_rounds_wave(S, 1, tid);
+    }
     __syncthreads();
     stamp();
-    parents_wave(S, tid);
+    if (w0) parents_wave(S, tid);
     __syncthreads();
     stamp();
-    depths_wave(S, 0, tid);
-    depths_wave(S, 1, tid);
+    if (NWV > 1) {
+        depths_wave<true>(S, wv, tid);
+        __syncthreads();
+        if (!w0) return;  // the rest is the first wave's (no workgroup barrier follows)
+    } else {
+        depths_wave(S, 0, tid);
+        depths_wave(S, 1, tid);
+    }
     stamp();
     ph_leafdepth<C, DevOps>(tid, S);
-    __syncthreads();
+    bar();
     stamp();
     ph_fixblc<C>(tid, S);
-    __syncthreads();
+    bar();
     stamp();
     assign_wave(S, tid);
-    __syncthreads();
+    bar();
     ph_rle_init<C>(tid, S);
-    __syncthreads();
+    bar();
     stamp();
 #ifndef PBX_HUFF_RLE_WAVE
 #define PBX_HUFF_RLE_WAVE 1  // 1: rle_wave (five ballots); 0: the generic phases of deflate_seg.h (the emulator's); 2: rle_wave in the batch variant only
 #endif
     if (PBX_HUFF_RLE_WAVE == 1 || (PBX_HUFF_RLE_WAVE == 2 && !KEEP)) {
         rle_wave(S, tid);
-        __syncthreads();
+        bar();
         stamp();
     } else {
         ph_rle_mark<C, DevOps>(tid, S);
-        __syncthreads();
+        bar();
         ph_rle_count<C>(tid, S);
-        __syncthreads();
+        bar();
         {
             const uint32_t nr = wave_scan_excl_add<RLEN>(S.rcnt, tid);
             if (tid == 0) S.misc[M_NRLE] = nr;
         }
-        __syncthreads();
+        bar();
         stamp();
         ph_rle_emit<C, DevOps>(tid, S);
     }
-    __syncthreads();
+    bar();
     stamp();
-    clen_wave(S, tid);
-    __syncthreads();
+    clen_wave<(NWV > 1)>(S, tid);
+    bar();
     stamp();
     ph_rle_bits<C>(tid, S);
-    __syncthreads();
+    bar();
     {
         const uint32_t hb = wave_scan_excl_add<RLEN>(S.rboff, tid);
         if (tid == 0) S.misc[M_HDRBITS] = hb;
     }
-    __syncthreads();
+    bar();
     ph_choose<C>(tid, S, sl, last, nsg);
-    __syncthreads();
+    bar();
     stamp();
     ph_codes<C>(tid, S);
     ph_header<C, DevOps>(tid, S, last);
-    __syncthreads();
+    bar();
     stamp();
     uint32_t* cg = codes + (size_t)b * CODE_WORDS;
     for (uint32_t i = tid; i < CODE_WORDS; i += 64)
@@ -2066,12 +2111,22 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
             if (tid == 0 && k0 + k < nsg) S.dk[k0 + k] = d;
         }
     }
-    __syncthreads();
+    bar();
     // a segment's share of a Huffman-coded block must fit k_encode's output buffer
     // (deflate_seg.h seg_share_fits); else the block is stored
     uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
     uint32_t dbits = S.misc[M_DATABITS];
-    if (bt != 0 && !seg_shares_fit<C>(S.dk, nsg, hdr, S.lcode[256] >> 16, last, nbytes)) {
+    // (deflate_seg.h seg_shares_fit: lane k checks segment k's share, bit offsets by a scan)
+    bool fits;
+    {
+        static_assert(BLK_SEGS <= 64, "one lane per segment of a block");
+        const uint32_t dkl = tid < nsg ? S.dk[tid] : 0u, incl = wave_incl_scan_dpp(dkl);
+        const uint64_t run1 = (uint64_t)hdr + incl, run0 = run1 - dkl;
+        const uint64_t b0 = tid == 0 ? 0 : run0;
+        const uint64_t b1 = tid + 1 < nsg ? run1 : last ? run1 + (S.lcode[256] >> 16) : 8ull * nbytes;
+        fits = __builtin_amdgcn_ballot_w64(tid < nsg && b1 - b0 > 8ull * (uint64_t)C::SEG) == 0;
+    }
+    if (bt != 0 && !fits) {
         bt = 0; hdr = 0; dbits = 0;
         nbytes = block_nbytes(0, 0, sl, last, nsg);
     }
@@ -2096,7 +2151,10 @@ __global__ __launch_bounds__(64) void k_huff(uint32_t nblk, BlkInfo* __restrict_
         blk[b].data_bits = dbits;
         blk[b].fin = last;
         if (solo) {
-            const uint64_t sz = container_bytes(*solo, nbytes);
+            TileDesc sd{};
+            sd.flags = solo_flags;
+            sd.tiff_hdr = solo_hdr;
+            const uint64_t sz = container_bytes(sd, nbytes);
             blk[b].off = 0;
             offs[0] = 0;
             offs[1] = sz;
@@ -3000,8 +3058,11 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
             }
         }
         if (!tiff) {
+            // levels past the segments present combine identity items only: stop there
+            const uint32_t nk = __builtin_amdgcn_readfirstlane(n - k0 < 64 ? n - k0 : 64u);
 #pragma unroll
             for (int s = 1; s < 64; s <<= 1) {  // (I, O) of lanes [lane, lane + 2s) on lane % 2s == 0
+                if ((uint32_t)s >= nk) break;
                 const uint32_t I2 = (uint32_t)__shfl_down((int)I, s, 64), O2 = (uint32_t)__shfl_down((int)O, s, 64);
                 const bool has = lane + s < 64;
                 const uint32_t In = crc_multmodp4(O2, I) ^ I2, On = crc_multmodp4(O, O2);
@@ -3106,12 +3167,16 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
                            a.uniform_rcp, self_map);
     if (ev && fine) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
-    if (prof)
+    if (prof && a.nblk <= HUFF_SMALL_BLKS)  // (the phase profile of the variant that runs)
+        hipLaunchKernelGGL((k_huff<DC, true, 34, HUFF_SMALL_WAVES>), dim3(a.nblk), dim3(64 * HUFF_SMALL_WAVES), 0, st,
+                           a.nblk, a.blk, a.info, a.hist, a.codes, a.stamps);
+    else if (prof)
         hipLaunchKernelGGL((k_huff<DC, true>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
     else if (a.nblk <= HUFF_SMALL_BLKS)  // a small batch: every segment's histogram loads at once
-        hipLaunchKernelGGL((k_huff<DC, false, 34>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
-                           a.hist, a.codes, a.stamps, solo ? a.tiles : nullptr, a.offs, a.offs_host);
+        hipLaunchKernelGGL((k_huff<DC, false, 34, HUFF_SMALL_WAVES>), dim3(a.nblk), dim3(64 * HUFF_SMALL_WAVES), 0, st,
+                           a.nblk, a.blk, a.info, a.hist, a.codes, a.stamps, solo ? a.tiles : nullptr, a.offs,
+                           a.offs_host);
     else
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);
