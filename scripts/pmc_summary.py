@@ -17,8 +17,9 @@ for f in sorted(glob.glob(os.path.join(base, "pmc[1-9]", "*counter_collection.cs
     per = defaultdict(lambda: defaultdict(float))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if "k_filter3" in k:  # fixed vs adaptive variants apart
-            k = "pbx::k_filter3_adaptive" if "true" in k else "pbx::k_filter3_fixed"
+        if "k_filter3" in k:  # fixed vs adaptive variants apart (k_filter3<G, FT>: FT 5 = adaptive)
+            ad = "true" in k or k.replace(" ", "").rstrip(">").endswith(("5u", ",5"))
+            k = "pbx::k_filter3_adaptive" if ad else "pbx::k_filter3_fixed"
         k = k.split("<")[0]
         per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
         per[(k, r["Dispatch_Id"])]["_dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
