@@ -2613,11 +2613,16 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         const uint4 q1 = (PBX_NT_STREAM & 2) ? gload16_nt(p1) : *(const uint4*)p1;
         cb[0] = q0.x; cb[1] = q0.y; cb[2] = q0.z; cb[3] = q0.w;
         cb[4] = q1.x; cb[5] = q1.y; cb[6] = q1.z; cb[7] = q1.w;
+#ifndef PBX_ENC_MASK_TAIL
+#define PBX_ENC_MASK_TAIL 1  // mask only in the chunks the segment ends in or past (0: every chunk)
+#endif
+        if (!PBX_ENC_MASK_TAIL || cs + C::CH > sp.sl) {  // (full waves skip it: ~50 VALU a lane)
 #pragma unroll
-        for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end, branch-free
-            const int32_t keep = (int32_t)sp.sl - (int32_t)(cs + 4 * k);
-            const uint32_t kb = keep <= 0 ? 0u : keep >= 4 ? 32u : 8u * (uint32_t)keep;
-            cb[k] &= (uint32_t)((1ull << kb) - 1ull);
+            for (int k = 0; k < C::CH / 4; k++) {  // mask bytes past the segment end
+                const int32_t keep = (int32_t)sp.sl - (int32_t)(cs + 4 * k);
+                const uint32_t kb = keep <= 0 ? 0u : keep >= 4 ? 32u : 8u * (uint32_t)keep;
+                cb[k] &= (uint32_t)((1ull << kb) - 1ull);
+            }
         }
     }
     const BlkInfo bi = blk[gi.blk];       // scalar loads, needed at the end
@@ -2675,7 +2680,9 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
         }
         lit_only = build_slots<C>(tid, S, sp, cb, slot, carry);
 #pragma unroll
-        for (int i = 0; i < C::CH + 2; i += 2) nbits += (slot[i] >> 27) + (slot[i + 1] >> 27);
+        for (int i = 0; i < C::CH + 2; i++) nbits = dot4_u8(slot[i], 0x01000000u, nbits);
+        // (a slot's value is < 2^24, so its top byte is 8 x its bit count: one v_dot4 each)
+        nbits >>= 3;
     }
     // the slicing tables (needed after barrier 3): loaded now, stored before barrier 2
     if (tid < 64 * PBX_CRC_SLICES) ((uint4*)&S.crc_t[0][0])[tid] = ((const uint4*)&kCrcTables.t[0][0])[tid];
