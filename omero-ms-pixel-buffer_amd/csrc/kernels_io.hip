@@ -772,7 +772,7 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // ------------------------------------------- K1+K2: streaming PNG filter rows
 // PNG tiles with a Sub/Up/Avg/Paeth or adaptive filter, rows of whole 16-byte chunks
 // (w * bpp % 16 == 0, <= 2 KiB; 16-byte aligned source rows).  No LDS and no barriers: one
-// WAVE per run of F3_RUN consecutive rows of one tile holds a whole row in registers (lane l
+// WAVE per run of f3_run_rows() consecutive rows of one tile holds a whole row in registers (lane l
 // = 16-byte chunks l, 64 + l), keeps the row above in registers, and prefetches the next row
 // while it filters the current one.  A sample's left neighbour is the previous lane's chunk
 // (one DPP wave shift; lane 0: the previous 64-chunk group, or zero before the row).  The
@@ -782,15 +782,20 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // bytes end (s = the row's start offset mod 16), i.e. the previous chunk's last s bytes and its
 // own first 16 - s (k_rows' layout); lane 0 of a row writes the word that holds the previous
 // row's tail and the filter byte.  That word needs the previous row's filtered tail, so a run
-// also filters the row before it (without storing it): 1/F3_RUN extra reads, no cross-wave
+// also filters the row before it (without storing it): 1/run extra reads, no cross-wave
 // hand-off.
 #ifndef PBX_F3_RUN
-#define PBX_F3_RUN 32
+#define PBX_F3_RUN 32  // rows a wave filters (Sub, Up, adaptive)
+#endif
+#ifndef PBX_F3_RUN_AP
+#define PBX_F3_RUN_AP 16  // Avg and Paeth: shorter runs, more waves in flight (profiles/r05zi/)
 #endif
 #ifndef PBX_F3_NTS
 #define PBX_F3_NTS 0
 #endif
-constexpr uint32_t F3_RUN = PBX_F3_RUN;
+__host__ __device__ constexpr uint32_t f3_run_rows(uint32_t filter) {
+    return filter == 3 || filter == 4 ? PBX_F3_RUN_AP : PBX_F3_RUN;
+}
 // stream stores: nontemporal (the stream is re-read only by the next kernel, from HBM anyway)
 __device__ __forceinline__ void f3_store(uint8_t* p, const uint4& v) {
     if (PBX_F3_NTS) {
@@ -989,8 +994,9 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
     const uint32_t rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
     const uint32_t h = (uint32_t)d.h;
     // uniform row bounds: the row loop and its prefetch stay scalar branches
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane((wi - d.blk_first) * F3_RUN);
-    const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + F3_RUN < h ? r0 + F3_RUN : h);
+    constexpr uint32_t RUN = f3_run_rows(FT);
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane((wi - d.blk_first) * RUN);
+    const uint32_t r1 = __builtin_amdgcn_readfirstlane(r0 + RUN < h ? r0 + RUN : h);
     const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
     constexpr bool ADAPTIVE = FT == 5;
     constexpr uint32_t fixed = FT;  // the batch's filter: 1..4, 5 = adaptive (every tile's d.filter)
@@ -1293,7 +1299,7 @@ hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntil
     return hipGetLastError();
 }
 
-uint32_t filter3_run_rows() { return F3_RUN; }
+uint32_t filter3_run_rows(uint32_t filter) { return f3_run_rows(filter); }
 uint32_t filter3_max_rb() { return 2048; }
 uint32_t filter2_max_rb() { return F2_MAX_RB; }
 

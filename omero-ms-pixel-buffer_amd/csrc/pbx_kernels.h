@@ -45,7 +45,7 @@ uint32_t filter2_band_rows();
 // the batch's PNG filter (1..4, 5 = adaptive), which every tile's d.filter holds
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
                           uint32_t max_rb, uint32_t filter, uint8_t* stream);
-uint32_t filter3_run_rows();
+uint32_t filter3_run_rows(uint32_t filter);  // rows per wave for the PNG filter 1..5
 uint32_t filter3_max_rb();
 uint32_t filter2_max_rb();
 

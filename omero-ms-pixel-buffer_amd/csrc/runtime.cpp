@@ -2660,7 +2660,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             b->filt2_max_rb = std::max<uint32_t>(b->filt2_max_rb, d.rowlen - 1);
         } else if (k < b->ndirect_tiles + b->nrows_tiles + b->nfilt2_tiles + b->nfilt3_tiles) {
             d.blk_first = b->filt3_waves;  // first wave (run of rows) of the tile
-            b->filt3_waves += (uint32_t)((d.h + filter3_run_rows() - 1) / filter3_run_rows());
+            b->filt3_waves += (uint32_t)((d.h + filter3_run_rows(d.filter) - 1) / filter3_run_rows(d.filter));
             b->filt3_max_rb = std::max<uint32_t>(b->filt3_max_rb, d.rowlen - 1);
             b->filt3_filter = d.filter;
         } else {
