@@ -50,6 +50,7 @@ struct LzSmem {
     // into the next wave (else 0), and the start its current records were walked from
     // (0xFFFFFFFF: a wave whose walk is skipped, any start gives the same result)
     uint32_t w_end[2][C::NW];
+    uint32_t reachw;  // PBX_LZ_REACH_MASKS: bit b = the boundary after wave b can be reached
     uint32_t w_st[2][C::NW];
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
@@ -802,6 +803,10 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
 #ifndef PBX_LZ_REACH_LATE
 #define PBX_LZ_REACH_LATE 1  // the boundary test after the candidate masks, loads unconditional
 #endif
+#ifndef PBX_LZ_REACH_MASKS
+#define PBX_LZ_REACH_MASKS 0  // 1: each wave tests its own boundary from lane 63's candidate masks,
+                              // the bits meet in LDS across one barrier (no LDS loads)
+#endif
     auto reach_test = [&]() -> uint32_t {
         bool rb = false;
         const uint32_t e = (lane + 1) * (uint32_t)C::SUB;
@@ -816,7 +821,8 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             const uint32_t d = cand_dist(sp, 2), mlr = match_minlen(d);
             const bool okr = d && a >= mlr + d;
             const uint32_t ar = okr ? a : 8u + mlr + d;
-            bool eq = v.y == lds_ld4(S, ar - 4 - d);
+            // the last mlr bytes (mlr = 3 for rows of <= 256 bytes: a 3-byte run pays)
+            bool eq = ((v.y ^ lds_ld4(S, ar - 4 - d)) >> (mlr == 3 ? 8u : 0u)) == 0;
             if (mlr == 6) eq = eq && ((v.x >> 16) ^ (lds_ld4(S, ar - 6 - d) & 0xFFFFu)) == 0;
             rb = ok && (rb || (okr && eq));
         } else if (ok) {
@@ -829,7 +835,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             // one row up (ml = 4, or 6 past 4 KiB), when the run's sources are in the window
             const uint32_t d = cand_dist(sp, 2), mlr = match_minlen(d);
             if (d && a >= mlr + d) {
-                bool eq = v.y == lds_ld4(S, a - 4 - d);
+                bool eq = ((v.y ^ lds_ld4(S, a - 4 - d)) >> (mlr == 3 ? 8u : 0u)) == 0;
                 if (mlr == 6) eq = eq && ((v.x >> 16) ^ (lds_ld4(S, a - 6 - d) & 0xFFFFu)) == 0;
                 rb = rb || eq;
             }
@@ -844,7 +850,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
 #endif
         return m;
     };
-    uint32_t reachm = PBX_LZ_REACH_LATE ? 0u : reach_test();
+    uint32_t reachm = PBX_LZ_REACH_LATE || PBX_LZ_REACH_MASKS ? 0u : reach_test();
     uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
     uint32_t M = 0, cvb_n = 0;
     bool skip = true;
@@ -953,7 +959,26 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         // chunk): exactly the waves where a paying run reaches the last byte walk.
         cvb_n = wave_sum((uint32_t)__builtin_popcount(cvb_lo) + (uint32_t)__builtin_popcount(cvb_hi));
     }
-    if (PBX_LZ_REACH_LATE) reachm = reach_test();
+    if (PBX_LZ_REACH_MASKS) {
+        // the boundary after this wave: a paying run (ml equal bytes of a candidate) ends at
+        // its last byte, i.e. the top ml bits of lane 63's equality mask are set (masked past
+        // the segment's end and before the window, as the LDS form's conditions)
+        uint32_t own = 0;
+        if (active && w + 1 < (uint32_t)C::NW && se == ss + (uint32_t)C::SUB && se < sp.sl) {
+            bool rb = false;
+#pragma unroll
+            for (int c = 0; c < NCAND; c++) {
+                const uint32_t need = 0xFFFFFFFFu << (32 - ml[c]);
+                rb = rb || (dd[c] != 0 && (exlo[c] & need) == need);
+            }
+            own = (uint32_t)__builtin_amdgcn_readlane((int)rb, 63);
+        }
+        if (lane == 0 && own) atomicOr(&S.reachw, 1u << w);
+        __syncthreads();
+        reachm = __builtin_amdgcn_readfirstlane(S.reachw);
+    } else if (PBX_LZ_REACH_LATE) {
+        reachm = reach_test();
+    }
     if (active) skip = PBX_LZ_COVBOUND && !((reachm >> w) & 1u) && cvb_n < (uint32_t)C::MINCOV;
 #ifndef PBX_LZ_EARLY_OUT
 #define PBX_LZ_EARLY_OUT 1
@@ -1352,6 +1377,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     }
     for (uint32_t k = tid; k < 288 * LZ_HCOPIES; k += C::NT) S.h8[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
+    if (tid == 0) S.reachw = 0;
     if (PROF) {  // diagnostics: wave 0's fill done
         __builtin_amdgcn_s_waitcnt(0);
         stamp();

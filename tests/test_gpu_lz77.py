@@ -132,3 +132,52 @@ def test_gpu_lz77_filtered_ramp_rows(oracle, filt, kind):
         assert (gh[k] == eh[k]).all(), (kind, filt, k, np.nonzero(gh[k] != eh[k])[0][:8])
     if kind == "ramp":
         assert carried >= nseg  # matches do run across the wave boundaries here
+
+
+@pytest.mark.parametrize("boundary", [1, 3, 6])
+@pytest.mark.parametrize("run", [3, 4])
+def test_gpu_lz77_short_rowup_run_at_wave_boundary(service, boundary, run):
+    """Rows of <= 256 bytes (row-up distance <= 256: a 3-byte match pays) with a row-up run of
+    exactly `run` bytes ending at a sub-segment's last byte and going on for 45 more: the
+    serial parse takes the 3-byte match there and extends it across the boundary, so k_lz77's
+    boundary test must count a 3-byte row-up run as reachable (a 4-byte test missed it and the
+    next wave parsed the run on its own)."""
+    a, stream, e = _short_rowup_case(boundary, run)
+    h, w = a.shape
+    iid = 9_700_000 + 10 * boundary + run
+    service.register_plane(iid, 0, 0, 0, pbx.UINT8, w, h, data=a, big_endian=True)
+    b = pbx.Batch(service, [pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="png")])
+    b.launch()
+    b.sync()
+    nseg = b.stats().segments
+    L = _emu.lib()
+    gh, gm = b.lz77_records(nseg, L.pbxemu_hist_words(), L.pbxemu_mrec_words())
+    b.close()
+    eh, em = _emu.lz77(stream, 1 + w)
+    nw = L.pbxemu_threads() // 64
+    ew = _records(em[0], nw, boundary - 1)
+    assert ew and ew[-1][0] == e - run and ew[-1][0] + ew[-1][1] > e  # the carried match
+    for k in range(nseg):
+        for wv in range(nw):
+            g, x = _records(gm[k], nw, wv), _records(em[k], nw, wv)
+            assert g == x, (boundary, run, k, wv, [y for y in g if y not in x][:4], [y for y in x if y not in g][:4])
+        assert (gh[k] == eh[k]).all(), (boundary, run, k, np.nonzero(gh[k] != eh[k])[0][:8])
+
+
+def _short_rowup_case(boundary, run, w=100, h=400):
+    """uint8 noise (rowlen w + 1) whose stream bytes [e - run, e + 45) equal the row above's
+    (e = 2048 boundary) and byte e - run - 1 does not; returns (pixels, PNG stream, e)."""
+    rng = np.random.default_rng(100 * boundary + run)
+    a = rng.integers(0, 256, (h, w)).astype(np.uint8)
+    rl = w + 1
+    e = 2048 * boundary
+    assert (e - run - 1) % rl != 0  # the byte before the run is a pixel, not a filter byte
+    for p in range(e - run, e + 45):  # in stream order: row-up sources are final
+        if p % rl:
+            a[p // rl, p % rl - 1] = a[p // rl - 1, p % rl - 1]
+    q = e - run - 1
+    a[q // rl, q % rl - 1] = (int(a[q // rl - 1, q % rl - 1]) + 1) % 256
+    raw = a.tobytes()
+    stream = b"".join(b"\x00" + raw[i * w:(i + 1) * w] for i in range(h))
+    assert stream[e - run:e + 45] == stream[e - run - rl:e + 45 - rl] and stream[q] != stream[q - rl]
+    return a, stream, e
