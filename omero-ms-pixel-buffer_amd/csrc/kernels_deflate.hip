@@ -2178,6 +2178,7 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
         blk[b].data_bits = dbits;
         blk[b].fin = last;
         if (solo) {
+            blk[b].pad[0] = 0;  // k_encode's count of finished workgroups (the last frames the tile)
             TileDesc sd{};
             sd.flags = solo_flags;
             sd.tiff_hdr = solo_hdr;
@@ -2522,7 +2523,15 @@ __device__ __forceinline__ bool build_slots(uint32_t tid, const SM& S, const Seg
 // the match counts, then the bytes, matches and codes); the CRC tables, needed last, are
 // loaded while the slots are built.  The segment's bytes go P = -bytes mod 32 bytes into
 // out[], so the CRC chunks are 32-byte aligned.
-template <class C, bool PROF>
+// k_frame_wave's work for one tile on one wave (below); the single-request path runs it at
+// the end of k_encode, in the workgroup that finishes last
+template <bool LR>
+__device__ void frame_wave_tile(const TileDesc& d, uint8_t* __restrict__ base, const SegInfo* __restrict__ info,
+                                const BlkInfo* __restrict__ blk, uint32_t lane);
+
+// FRAME (the single-tile batch only: its own instantiation, so the framing code's registers
+// never reach the batch kernel's allocation): the last workgroup frames the tile
+template <class C, bool PROF, bool FRAME = false>
 __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict__ dt,
                                                   const uint32_t* __restrict__ seg_tile,
                                                   uint32_t nseg, const uint8_t* __restrict__ stream,
@@ -2533,7 +2542,8 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
                                                   const uint64_t* __restrict__ offs,
                                                   uint8_t* __restrict__ out,
                                                   uint64_t* __restrict__ stamps,
-                                                  uint32_t uniform_nseg, uint32_t uniform_rcp) {
+                                                  uint32_t uniform_nseg, uint32_t uniform_rcp,
+                                                  uint32_t* __restrict__ frame_ctr = nullptr) {
     static_assert(C::CH == 32 && C::CRCC == 32, "two 16-byte loads per thread chunk");
     static_assert(C::SUB == 64 * C::CH && C::NW * C::SUB <= 4 * C::OUTW, "a wave's bytes staged in its part of out[]");
     __shared__ EncSmem<C> S;
@@ -2900,6 +2910,22 @@ __global__ __launch_bounds__(C::NT, 8) void k_encode(const TileDesc* __restrict_
             finish(raw);
         }
     }
+    // a single-tile batch (frame_ctr, zeroed by k_huff): the workgroup that finishes last
+    // frames the tile -- k_frame_wave's work without its launch (wave 0: thread 0 wrote this
+    // segment's record above; the fences order it before the count, and the others' before
+    // the reads of theirs)
+    if (FRAME && w == 0) {
+        uint32_t lastw = 0;
+        if (lane == 0) {
+            __threadfence();
+            lastw = atomicAdd(frame_ctr, 1u) == nseg - 1 ? 1u : 0u;
+        }
+        if (__builtin_amdgcn_readfirstlane(lastw)) {
+            __threadfence();
+            const TileDesc td = load_desc(dt);
+            frame_wave_tile<true>(td, out + offs[0], info, blk, lane);
+        }
+    }
     stamp();
 }
 
@@ -3042,15 +3068,25 @@ __global__ __launch_bounds__(64) void k_frame(const TileDesc* __restrict__ dt, u
 // (I1 O2 + I2, O1 O2)) with nibble-step multiplies; lanes 1-3 write the PNG chunks before
 // IDAT.  A tile with a segment that owns no byte (all its bits inside one byte: the byte is
 // then shared by three segments) takes frame_tile on lane 0.
-__global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ dt, uint32_t ndt,
-                                                   const SegInfo* __restrict__ info,
-                                                   const BlkInfo* __restrict__ blk,
-                                                   const uint64_t* __restrict__ offs,
-                                                   uint8_t* __restrict__ out) {
-    const uint32_t i = blockIdx.x, lane = threadIdx.x;
-    if (i >= ndt) return;
-    const TileDesc d = dt[i];
-    uint8_t* base = out + offs[i];
+// LR: low register use (loops not unrolled), for the copy inside k_encode's 64-VGPR budget
+__device__ __forceinline__ uint32_t crc_multmodp4_lr(uint32_t a, uint32_t b) {
+    const uint32_t b1 = (b >> 1) ^ ((b & 1u) ? CRC_POLY : 0u);
+    const uint32_t b2 = (b >> 2) ^ ((b & 1u) ? (CRC_POLY >> 1) : 0u) ^ ((b & 2u) ? CRC_POLY : 0u);
+    const uint32_t b3 = (b >> 3) ^ ((b & 1u) ? (CRC_POLY >> 2) : 0u) ^ ((b & 2u) ? (CRC_POLY >> 1) : 0u) ^
+                        ((b & 4u) ? CRC_POLY : 0u);
+    uint32_t p = 0;
+#pragma unroll 1
+    for (int s = 7; s >= 0; s--) {
+        const uint32_t t = ((a >> (31 - 4 * s)) & 1u ? b : 0u) ^ ((a >> (30 - 4 * s)) & 1u ? b1 : 0u) ^
+                           ((a >> (29 - 4 * s)) & 1u ? b2 : 0u) ^ ((a >> (28 - 4 * s)) & 1u ? b3 : 0u);
+        p = crc_x4(p) ^ t;
+    }
+    return p;
+}
+template <bool LR>
+__device__ void frame_wave_tile(const TileDesc& d, uint8_t* __restrict__ base, const SegInfo* __restrict__ info,
+                                const BlkInfo* __restrict__ blk, uint32_t lane) {
+    auto mul = [](uint32_t a, uint32_t b) { return LR ? crc_multmodp4_lr(a, b) : crc_multmodp4(a, b); };
     const bool tiff = (d.flags & TF_TIFF) != 0;
     const uint32_t zoff = container_zoff(d), n = d.seg_count, f = d.seg_first;
     // Two dependent rounds of loads (a lone tile waits on each, ~1 us): the descriptor, then
@@ -3107,25 +3143,34 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
             z[(bj < 64 ? bo_l : blk[gb].off) + (bit0 >> 3)] = (uint8_t)sb;
             if (!tiff) {
                 const uint32_t cb = crc_byte4(0xFFFFFFFFu, sb) ^ 0xFFFFFFFFu;
-                I = crc_multmodp4(O, cb) ^ I;
-                O = crc_multmodp4(O, X8);
+                I = mul(O, cb) ^ I;
+                O = mul(O, X8);
             }
         }
         if (!tiff) {
             // levels past the segments present combine identity items only: stop there
             const uint32_t nk = __builtin_amdgcn_readfirstlane(n - k0 < 64 ? n - k0 : 64u);
-#pragma unroll
-            for (int s = 1; s < 64; s <<= 1) {  // (I, O) of lanes [lane, lane + 2s) on lane % 2s == 0
-                if ((uint32_t)s >= nk) break;
+            // (I, O) of lanes [lane, lane + 2s) on lane % 2s == 0
+            auto level = [&](uint32_t s) {
                 const uint32_t I2 = (uint32_t)__shfl_down((int)I, s, 64), O2 = (uint32_t)__shfl_down((int)O, s, 64);
                 const bool has = lane + s < 64;
-                const uint32_t In = crc_multmodp4(O2, I) ^ I2, On = crc_multmodp4(O, O2);
+                const uint32_t In = mul(O2, I) ^ I2, On = mul(O, O2);
                 I = has ? In : I;
                 O = has ? On : O;
+            };
+            if (LR) {
+#pragma unroll 1
+                for (uint32_t s = 1; s < nk; s <<= 1) level(s);
+            } else {
+#pragma unroll
+                for (int s = 1; s < 64; s <<= 1) {
+                    if ((uint32_t)s >= nk) break;
+                    level((uint32_t)s);
+                }
             }
             const uint32_t Ic = (uint32_t)__builtin_amdgcn_readfirstlane((int)I);
             const uint32_t Oc = (uint32_t)__builtin_amdgcn_readfirstlane((int)O);
-            c = crc_multmodp4(Oc, c) ^ Ic;
+            c = mul(Oc, c) ^ Ic;
         }
     }
     payload = wave_sum(payload);
@@ -3161,6 +3206,17 @@ __global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ 
         const uint32_t fctl[3] = {0u, (uint32_t)d.w, (uint32_t)d.h};
         put_chunk_w(base + PNG_SIG_BYTES + PNG_IHDR_BYTES + PNG_ACTL_BYTES, FOURCC('f', 'c', 'T', 'L'), fctl, 14);
     }
+}
+
+__global__ __launch_bounds__(64) void k_frame_wave(const TileDesc* __restrict__ dt, uint32_t ndt,
+                                                   const SegInfo* __restrict__ info,
+                                                   const BlkInfo* __restrict__ blk,
+                                                   const uint64_t* __restrict__ offs,
+                                                   uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x;
+    if (i >= ndt) return;
+    const TileDesc d = dt[i];
+    frame_wave_tile<false>(d, out + offs[i], info, blk, threadIdx.x);
 }
 
 // ================================================================== launchers
@@ -3207,6 +3263,10 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     // separate launch, profiles/r05k/)
     const uint32_t self_map = a.uniform_nseg && a.nseg <= LZ_SELF_MAP_SEGS ? 1u : 0u;
     const bool solo = !prof && a.ntiles == 1 && a.nblk == 1;  // one tile, one Huffman block
+#ifndef PBX_ENC_FRAME_SOLO
+#define PBX_ENC_FRAME_SOLO 0  // 1: a solo tile framed by k_encode's last workgroup, no k_frame_wave (measured: no gain, profiles/r05zk/)
+#endif
+    const bool solo_frame = solo && PBX_ENC_FRAME_SOLO;
     if (!self_map)
         hipLaunchKernelGGL(k_seg_map, dim3((a.nseg + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles, a.nseg,
                            a.uniform_nseg, a.uniform_rcp, a.seg_tile, a.info, a.blk);
@@ -3251,12 +3311,18 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
                            a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
                            a.uniform_nseg, a.uniform_rcp);
     else
-        hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
-                           a.uniform_nseg, a.uniform_rcp);
+        if (solo_frame)
+            hipLaunchKernelGGL((k_encode<DC, false, true>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
+                               a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
+                               a.uniform_nseg, a.uniform_rcp, &a.blk[0].pad[0]);
+        else
+            hipLaunchKernelGGL((k_encode<DC, false>), dim3(a.nseg), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
+                               a.nseg, a.stream, a.info, a.blk, a.mrec, a.codes, a.offs, a.out, a.stamps,
+                               a.uniform_nseg, a.uniform_rcp);
     if (ev) (void)hipEventRecord(ev[3], st);
     if (ev2) (void)hipEventRecord(ev2[3], st);
-    if (a.ntiles <= FRAME_WAVE_TILES)  // small batch: a wave per tile (latency)
+    if (solo_frame) {  // (k_encode's last workgroup framed the tile)
+    } else if (a.ntiles <= FRAME_WAVE_TILES)  // small batch: a wave per tile (latency)
         hipLaunchKernelGGL(k_frame_wave, dim3(a.ntiles), dim3(64), 0, st, a.tiles, a.ntiles, a.info, a.blk,
                            a.offs, a.out);
     else
