@@ -181,3 +181,58 @@ def _short_rowup_case(boundary, run, w=100, h=400):
     stream = b"".join(b"\x00" + raw[i * w:(i + 1) * w] for i in range(h))
     assert stream[e - run:e + 45] == stream[e - run - rl:e + 45 - rl] and stream[q] != stream[q - rl]
     return a, stream, e
+
+
+
+def _structured_stream(rng, rowbytes, h, ncopies):
+    """A filter-None PNG stream (h rows of rowbytes + 1 bytes) with random runs: ncopies forward
+    copies of random length (3..300) at distance 1, 2 or one row, at random places (filter
+    bytes stay 0, so a copy over one breaks there); returns (row bytes (h, rowbytes), stream)."""
+    rl = rowbytes + 1
+    s = bytearray(rng.integers(0, 256, h * rl).astype(np.uint8).tobytes())
+    for r in range(h):
+        s[r * rl] = 0
+    for _ in range(ncopies):
+        d = [1, 2, rl][int(rng.integers(3))]
+        p = int(rng.integers(d, len(s)))
+        ln = int(rng.integers(3, 301))
+        for q in range(p, min(p + ln, len(s))):
+            if q % rl:
+                s[q] = s[q - d]
+    return np.frombuffer(bytes(s), np.uint8).reshape(h, rl)[:, 1:].copy(), bytes(s)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_lz77_structured_fuzz(service, seed):
+    """Random tiles of random row lengths (4..8401 bytes: row-up distance above and below the
+    256-byte and 4 KiB thresholds of match_minlen) full of runs at distances 1, 2 and one row
+    landing anywhere -- across sub-segment and segment boundaries, filter bytes, the window --
+    as big-endian 8-bit planes and little-endian 16-bit ones (the byte-swapping fill): every
+    segment's records and histogram equal the emulator's serial parse."""
+    rng = np.random.default_rng(7000 + seed)
+    L = _emu.lib()
+    nw = L.pbxemu_threads() // 64
+    for t in range(8):
+        w = int(rng.choice([3, 17, 100, 255, 256, 300, 511, 700, 2047, 4095, 4200]))
+        bpp = 1 + t % 2
+        h = max(3, int(rng.integers(20000, 80000)) // (w * bpp + 1))
+        rows, stream = _structured_stream(rng, w * bpp, h, int(rng.integers(20, 400)))
+        iid = 9_800_000 + 100 * seed + t
+        if bpp == 1:
+            service.register_plane(iid, 0, 0, 0, pbx.UINT8, w, h, data=rows, big_endian=True)
+        else:
+            a = rows.view(">u2").astype("<u2")
+            service.register_plane(iid, 0, 0, 0, pbx.UINT16, w, h, data=a, big_endian=False)
+        b = pbx.Batch(service, [pbx.TileCtx(iid, 0, 0, 0, 0, 0, w, h, format="png")])
+        b.launch()
+        b.sync()
+        nseg = b.stats().segments
+        gh, gm = b.lz77_records(nseg, L.pbxemu_hist_words(), L.pbxemu_mrec_words())
+        b.close()
+        eh, em = _emu.lz77(stream, w * bpp + 1)
+        assert gh.shape == eh.shape
+        for k in range(nseg):
+            for wv in range(nw):
+                g, x = _records(gm[k], nw, wv), _records(em[k], nw, wv)
+                assert g == x, (seed, t, w, h, k, wv, [y for y in g if y not in x][:4], [y for y in x if y not in g][:4])
+            assert (gh[k] == eh[k]).all(), (seed, t, w, h, k, np.nonzero(gh[k] != eh[k])[0][:8])
