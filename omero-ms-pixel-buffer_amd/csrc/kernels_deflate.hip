@@ -1507,6 +1507,59 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
         return (lane & 32u) ? p[0] : p[1];
     }
 }
+// Wave sums of N per-lane values at once, the sum of value k landing in lane k (k < N <= 64):
+// a transposing butterfly.  Slot k starts in register k; at each lane distance h = 32 .. 1
+// the registers pair up (k, k + h) and trade halves so that one add leaves slot k's partial
+// sums in the lanes whose bit h is clear and slot k + h's where it is set -- gfx950's lane
+// swaps for 32 and 16, then DPP row mirror (8), half-row mirror (4) and quad permutes (2, 1),
+// each folded into its add (a mirror partner differs in bit h and agrees in the bits already
+// split; the mirrors' merged lane classes still cover each row once).  Registers that hold
+// no slot below N are skipped at compile time: 17 values take 111 VALU instructions, 34 take
+// 141, against 17 / 34 wave_sum row scans and lane reads.
+__device__ constexpr bool lane_sums_nz(uint32_t n, uint32_t w, uint32_t j) {  // register j of w holds a slot < n
+    for (uint32_t s = j; s < 64; s += w)
+        if (s < n) return true;
+    return false;
+}
+template <uint32_t H>
+__device__ __forceinline__ uint32_t lane_sums_step(uint32_t x, uint32_t y, uint32_t lane) {
+    const bool hi = (lane & H) != 0;
+    const uint32_t keep = hi ? y : x, send = hi ? x : y;
+    constexpr int ctl = H == 8 ? 0x140 : H == 4 ? 0x141 : H == 2 ? 0x4E : 0xB1;  // row_mirror, row_half_mirror, quad_perm
+    return keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, ctl, 0xF, 0xF, false);
+}
+template <uint32_t N>
+__device__ __forceinline__ uint32_t wave_sums_to_lanes(const uint32_t (&v)[N], uint32_t lane) {
+    static_assert(N >= 1 && N <= 64, "one slot per lane");
+    uint32_t r[32];
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) {
+        if (lane_sums_nz(N, 64, j) || lane_sums_nz(N, 64, j + 32)) {
+            const auto p = __builtin_amdgcn_permlane32_swap(v[j < N ? j : 0], j + 32 < N ? v[j + 32 < N ? j + 32 : 0] : 0u,
+                                                            false, false);
+            r[j] = p[0] + p[1];
+        } else {
+            r[j] = 0;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) {
+        if (lane_sums_nz(N, 32, j) || lane_sums_nz(N, 32, j + 16)) {
+            const auto p = __builtin_amdgcn_permlane16_swap(r[j], r[j + 16], false, false);
+            r[j] = p[0] + p[1];
+        } else {
+            r[j] = 0;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) r[j] = lane_sums_nz(N, 16, j) || lane_sums_nz(N, 16, j + 8) ? lane_sums_step<8>(r[j], r[j + 8], lane) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) r[j] = lane_sums_nz(N, 8, j) || lane_sums_nz(N, 8, j + 4) ? lane_sums_step<4>(r[j], r[j + 4], lane) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 2; j++) r[j] = lane_sums_nz(N, 4, j) || lane_sums_nz(N, 4, j + 2) ? lane_sums_step<2>(r[j], r[j + 2], lane) : 0u;
+    return lane_sums_step<1>(r[0], r[1], lane);
+}
+
 template <uint32_t M>
 __device__ __forceinline__ void lane_xor8(const uint32_t (&v)[8], uint32_t (&o)[8], uint32_t lane) {
 #pragma unroll
@@ -2121,6 +2174,10 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
 #ifndef PBX_HUFF_ONEREAD
 #define PBX_HUFF_ONEREAD 0  // timing bound only (variant build): no second histogram read, wrong output
 #endif
+#ifndef PBX_HUFF_LANE_SUMS
+#define PBX_HUFF_LANE_SUMS 1  // 1: the segments' dot products summed by one transposing butterfly (lane k: segment k); 0: a wave_sum each
+#endif
+    uint32_t dkl = 0;  // lane k: segment k's token bits
     for (uint32_t k0 = 0; k0 < nsg; k0 += LDSEG) {
         uint32_t hr[LDSEG][5];
 #pragma unroll
@@ -2128,17 +2185,32 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
 #pragma unroll
             for (int j = 0; j < 5; j++)
                 hr[k][j] = KEEP && k0 == 0 ? hr0[KEEP ? k : 0][j]
-                           : k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : k;
+                           : k0 + k < nsg && !PBX_HUFF_ONEREAD ? hist[(size_t)(seg0 + k0 + k) * HIST_WORDS + tid + 64 * j] : 0u;
+        uint32_t dv[LDSEG];
 #pragma unroll
         for (uint32_t k = 0; k < LDSEG; k++) {
             uint32_t d = 0;
 #pragma unroll
             for (int j = 0; j < 5; j++) d += cost[j] * hr[k][j];
-            d = wave_sum(d);
-            if (tid == 0 && k0 + k < nsg) S.dk[k0 + k] = d;
+            dv[k] = d;
+        }
+        if (PBX_HUFF_LANE_SUMS) {
+            uint32_t t = wave_sums_to_lanes(dv, tid);  // lane k: segment k0 + k (k < LDSEG)
+            if (k0) {  // to lane k0 + k
+                t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((tid - k0) & 63u) << 2), (int)t);
+                t = tid >= k0 && tid < k0 + LDSEG ? t : 0u;
+            }
+            dkl += t;
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < LDSEG; k++) {
+                const uint32_t d = wave_sum(dv[k]);
+                if (tid == 0 && k0 + k < nsg) S.dk[k0 + k] = d;
+            }
         }
     }
     bar();
+    if (!PBX_HUFF_LANE_SUMS) dkl = tid < nsg ? S.dk[tid] : 0u;
     // a segment's share of a Huffman-coded block must fit k_encode's output buffer
     // (deflate_seg.h seg_share_fits); else the block is stored
     uint32_t bt = S.misc[M_BTYPE], hdr = S.misc[M_HDRBITS], nbytes = S.misc[M_NBYTES];
@@ -2147,7 +2219,7 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
     bool fits;
     {
         static_assert(BLK_SEGS <= 64, "one lane per segment of a block");
-        const uint32_t dkl = tid < nsg ? S.dk[tid] : 0u, incl = wave_incl_scan_dpp(dkl);
+        const uint32_t incl = wave_incl_scan_dpp(dkl);
         const uint64_t run1 = (uint64_t)hdr + incl, run0 = run1 - dkl;
         const uint64_t b0 = tid == 0 ? 0 : run0;
         const uint64_t b1 = tid + 1 < nsg ? run1 : last ? run1 + (S.lcode[256] >> 16) : 8ull * nbytes;
@@ -2162,7 +2234,7 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
     static_assert(BLK_SEGS <= 64, "one lane per segment of a block");
     {
         const uint32_t k = tid;
-        const uint32_t d = k < nsg ? (bt == 0 ? 8 * (5 + S.sls[k]) : S.dk[k]) : 0u;
+        const uint32_t d = k < nsg ? (bt == 0 ? 8 * (5 + S.sls[k]) : dkl) : 0u;
         const uint32_t st = (bt == 0 ? 0u : hdr) + wave_incl_scan_dpp(d) - d;  // run before segment k
         if (k < nsg) {
             SegInfo& g = info[seg0 + k];
