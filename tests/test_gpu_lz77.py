@@ -2,6 +2,8 @@
 wave-wide extension, interleaved literal histograms) against the CPU emulator's sequential
 greedy/lazy parse (ph_parse_emu), segment by segment: the symbol histogram and every match
 record must be identical.  Through the C-ABI test hook pbx_test_batch_lz77."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -236,3 +238,60 @@ def test_gpu_lz77_structured_fuzz(service, seed):
                 g, x = _records(gm[k], nw, wv), _records(em[k], nw, wv)
                 assert g == x, (seed, t, w, h, k, wv, [y for y in g if y not in x][:4], [y for y in x if y not in g][:4])
             assert (gh[k] == eh[k]).all(), (seed, t, w, h, k, np.nonzero(gh[k] != eh[k])[0][:8])
+
+
+def _structured_rows(rng, rowbytes, h, ncopies):
+    """numpy form of _structured_stream for larger cases: runs at distance 1 / 2 (pattern
+    fills) and one row (slice copies of at most a row), filter bytes zeroed afterwards."""
+    rl = rowbytes + 1
+    s = rng.integers(0, 256, h * rl).astype(np.uint8)
+    for _ in range(ncopies):
+        d = [1, 2, rl][int(rng.integers(3))]
+        p = int(rng.integers(d, s.size))
+        ln = min(int(rng.integers(3, 301)), s.size - p)
+        if d < 3:
+            s[p:p + ln] = np.resize(s[p - d:p], ln)
+        else:
+            ln = min(ln, rl)
+            s[p:p + ln] = s[p - d:p - d + ln]
+    s[::rl] = 0
+    return s.reshape(h, rl)[:, 1:].copy(), s.tobytes()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_png_structured_fuzz_bytes(service, seed):
+    """End to end on run-structured data: 320 tiles of random heights in one batch (more
+    Huffman blocks than the small-batch k_huff takes: the batch kernels), 8- and 16-bit
+    planes of row lengths across match_minlen's thresholds -- every tile's zlib stream equals
+    the emulator's deflate byte for byte and inflates to the tile's scanlines, and its PNG
+    chunks carry valid CRCs (zlib.crc32 over type + data)."""
+    rng = np.random.default_rng(8100 + seed)
+    ctxs, streams = [], []
+    for wi, w in enumerate([3, 100, 256, 300, 700, 2100]):
+        bpp = 1 + wi % 2
+        hs = [max(1, int(rng.integers(2000, 40000)) // (w * bpp + 1)) for _ in range(320 // 6 + 1)]
+        rows, stream = _structured_rows(rng, w * bpp, sum(hs), 60 * len(hs))
+        iid = 9_900_000 + 100 * seed + wi
+        if bpp == 1:
+            service.register_plane(iid, 0, 0, 0, pbx.UINT8, w, sum(hs), data=rows, big_endian=True)
+        else:
+            service.register_plane(iid, 0, 0, 0, pbx.UINT16, w, sum(hs), data=rows.view(">u2").astype("<u2"),
+                                   big_endian=False)
+        y = 0
+        for h in hs:
+            ctxs.append(pbx.TileCtx(iid, 0, 0, 0, 0, y, w, h, format="png"))
+            rl = w * bpp + 1
+            streams.append((stream[y * rl:(y + h) * rl], rl))
+            y += h
+    res = service.get_tiles(ctxs)
+    for i, ((st, body), (stream, rl)) in enumerate(zip(res, streams)):
+        assert st == pbx.OK, i
+        z, _ = _emu.deflate(stream, rl)
+        assert body[99:99 + len(z)] == z, (seed, i, rl, len(stream))
+        assert zlib.decompress(z) == stream
+        o = 8
+        while o < len(body):  # every chunk: length, type, data, CRC-32 of type + data
+            n = int.from_bytes(body[o:o + 4], "big")
+            assert zlib.crc32(body[o + 4:o + 8 + n]) == int.from_bytes(body[o + 8 + n:o + 12 + n], "big"), (i, body[o + 4:o + 8])
+            o += 12 + n
+        assert o == len(body) and body[-8:-4] == b"IEND"
