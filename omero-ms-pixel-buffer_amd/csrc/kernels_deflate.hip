@@ -51,6 +51,8 @@ struct LzSmem {
     // (0xFFFFFFFF: a wave whose walk is skipped, any start gives the same result)
     uint32_t w_end[2][C::NW];
     uint32_t reachw;  // PBX_LZ_REACH_MASKS: bit b = the boundary after wave b can be reached
+    uint32_t dbg_walk, dbg_round;  // PBX_PHASE_PROFILE: walk steps of the workgroup, repair rounds
+    uint32_t dbg_twalk, dbg_tsync;  // PBX_LZ_WALK_PROF: wave 0's cycles in walks / in the rounds' barriers and checks
     uint32_t w_st[2][C::NW];
     // literal/length histogram, LZ_HCOPIES interleaved copies (lane & 7): lanes of different
     // copies never share a bank, same-symbol atomics of one instruction spread over 8 words
@@ -786,9 +788,10 @@ __device__ __forceinline__ uint32_t pack_zero_bytes8(const uint32_t (&x)[8]) {
 // positions (M), scalar: lengths at k and k+1 from readlane'd masks, the lazy rule, the
 // wave-wide extension of a capped match.  Each lane also collects the positions of its
 // chunk covered by recorded matches (cover), for the histogram.
-template <class C, class SM>
+template <class C, class SM, bool PROF = false>
 __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uint32_t (&cw)[9],
                              uint32_t& cover, uint32_t& smask) {
+    uint32_t nsteps = 0;  // (PROF) walk steps of this wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t ss = w * C::SUB;
     const uint32_t se = __builtin_amdgcn_readfirstlane(ss + C::SUB < sp.sl ? ss + C::SUB : sp.sl);
@@ -851,7 +854,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         return m;
     };
     uint32_t reachm = PBX_LZ_REACH_LATE || PBX_LZ_REACH_MASKS ? 0u : reach_test();
-    uint32_t exlo[NCAND], exhi[NCAND], ml[NCAND], dd[NCAND];
+    uint32_t exlo[NCAND] = {}, exhi[NCAND] = {}, ml[NCAND] = {3, 3, 3}, dd[NCAND] = {};
     uint32_t M = 0, cvb_n = 0;
     bool skip = true;
     if (active) {
@@ -991,6 +994,12 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     }
     const uint64_t B = __ballot(M != 0);
     const uint32_t lsub = active ? se - ss : 0u;
+#ifndef PBX_LZ_VCAND
+#define PBX_LZ_VCAND 1  // the walk's candidate lengths in VALU, lane c for candidate c (0: scalar loop)
+#endif
+    // lane c < NCAND: candidate c's distance present and its match_minlen (the walk's VALU form)
+    const bool vok = lane < (uint32_t)NCAND && (lane == 0 ? dd[0] : lane == 1 ? dd[1] : dd[2]) != 0;
+    const uint32_t vml = lane == 0 ? ml[0] : lane == 1 ? ml[1] : ml[2];
     uint32_t nm = 0, cov = 0, last_end = 0;
     // The greedy walk over the paying positions from o0 (sub-segment offset): records, the
     // lane's covered positions, the end of the last match (uniform).
@@ -1001,6 +1010,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         cover = 0;
         uint32_t o = o0;
         while (o < lsub) {
+            if (PROF) nsteps++;
             // the first position >= o where a match pays
             const uint32_t t0 = o >> 5;
             uint32_t k = 0xFFFFFFFFu;
@@ -1018,6 +1028,35 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             if (k >= lsub) break;
             const uint32_t t = k >> 5, i = k & 31;
             uint32_t L = 0, D = 0, Dc = 0, L1 = 0;
+            if (PBX_LZ_VCAND) {
+                // lane c (< NCAND) evaluates candidate c at k and k + 1 in VALU (the scalar unit
+                // is the CU's bottleneck while every wave walks: run-heavy streams); the best
+                // (length, then the earliest candidate) by a max over the quad of packed
+                // (n0 << 2 | 3 - c), two DPP steps
+                static_assert(NCAND == 3 && C::CAP == 32, "three candidates, 32-bit windows");
+                const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane(exlo[0], t), h0 = (uint32_t)__builtin_amdgcn_readlane(exhi[0], t);
+                const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane(exlo[1], t), h1 = (uint32_t)__builtin_amdgcn_readlane(exhi[1], t);
+                const uint32_t l2 = (uint32_t)__builtin_amdgcn_readlane(exlo[2], t), h2 = (uint32_t)__builtin_amdgcn_readlane(exhi[2], t);
+                const uint32_t xl = lane == 0 ? l0 : lane == 1 ? l1 : l2, xh = lane == 0 ? h0 : lane == 1 ? h1 : h2;
+                const uint32_t q0 = ~__builtin_amdgcn_alignbit(xh, xl, i);
+                const uint32_t q1 = ~(i < 31 ? __builtin_amdgcn_alignbit(xh, xl, i + 1) : xh);
+                const uint32_t n0 = q0 ? (uint32_t)__builtin_ctz(q0) : 32u, n1 = q1 ? (uint32_t)__builtin_ctz(q1) : 32u;
+                uint32_t v0 = vok && n0 >= vml ? (n0 << 2) | (3u - lane) : 0u;
+                uint32_t v1 = vok && n1 >= vml ? n1 : 0u;
+                auto qmax = [](uint32_t v) {  // over the quad: quad_perm 1,0,3,2 then 2,3,0,1
+                    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+                    v = v > o ? v : o;
+                    const uint32_t o2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+                    return v > o2 ? v : o2;
+                };
+                v0 = qmax(v0);
+                v1 = qmax(v1);
+                const uint32_t best = __builtin_amdgcn_readfirstlane(v0);
+                L1 = __builtin_amdgcn_readfirstlane(v1);
+                L = best >> 2;
+                Dc = best ? 3u - (best & 3u) : 0u;
+                D = best ? (Dc == 0 ? dd[0] : Dc == 1 ? dd[1] : dd[2]) : 0u;
+            } else {
 #pragma unroll
             for (int c = 0; c < NCAND; c++) {
                 if (!dd[c]) continue;
@@ -1030,6 +1069,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
                 n1 = n1 < (uint32_t)C::CAP ? n1 : (uint32_t)C::CAP;
                 if (n0 >= ml[c] && n0 > L) { L = n0; D = dd[c]; Dc = (uint32_t)c; }
                 if (n1 >= ml[c] && n1 > L1) L1 = n1;
+            }
             }
             L = __builtin_amdgcn_readfirstlane(L);
             D = __builtin_amdgcn_readfirstlane(D);
@@ -1152,9 +1192,10 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     // registers to scratch.)
     uint32_t st = ss;  // (uniform) the start of this wave's current records
     if (w && ((reachm >> (w - 1)) & 1u)) st = 258u * ((ss + 257u) / 258u);
-    uint32_t cur = 0;
+    uint32_t cur = 0, jr = 0;
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {
+        jr = j;
         bool go = j == 0 && active && !skip;
         uint32_t o0 = st - ss;
         if (j && w) {
@@ -1166,7 +1207,12 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
                 o0 = a - ss;
             }
         }
+#ifndef PBX_LZ_WALK_PROF
+#define PBX_LZ_WALK_PROF 0  // diagnostics (variant build, PROF kernels): wave 0's walk / round cycles in phase slots 1 and 2
+#endif
+        const uint64_t tw0 = PROF && PBX_LZ_WALK_PROF ? __builtin_amdgcn_s_memtime() : 0;
         if (go) walk(o0);
+        if (PROF && PBX_LZ_WALK_PROF && w == 0 && lane == 0) S.dbg_twalk += (uint32_t)(__builtin_amdgcn_s_memtime() - tw0);
         if (reachm == 0) break;  // (uniform) no match runs into another wave: no barrier at all
         if (lane == 0) {
             S.w_end[cur][w] = last_end > se ? last_end : 0u;
@@ -1179,6 +1225,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             const uint32_t c = S.w_end[cur][lane - 1], si = lane * (uint32_t)C::SUB, sv = S.w_st[cur][lane];
             bad = sv != 0xFFFFFFFFu && (c > si ? c : si) != sv;
         }
+        if (PROF && PBX_LZ_WALK_PROF && w == 0 && lane == 0) S.dbg_tsync += (uint32_t)(__builtin_amdgcn_s_memtime() - tw0);
         if (__ballot(bad) == 0 || j + 1 == (uint32_t)C::NW) break;  // (uniform) every start is final
         cur ^= 1u;
     }
@@ -1205,6 +1252,10 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
         atomicAdd(&S.dfreq[sy], 1u);
     }
     if (lane == 0) S.w_nm[w] = nm;
+    if (PROF && lane == 0) {
+        atomicAdd(&S.dbg_walk, nsteps);
+        if (w == 0) S.dbg_round = jr;
+    }
 }
 
 // Container bytes before the zlib stream: TIFF header, PNG chunks up to the IDAT data, or
@@ -1378,6 +1429,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
     for (uint32_t k = tid; k < 288 * LZ_HCOPIES; k += C::NT) S.h8[k] = 0;
     if (tid < 32) S.dfreq[tid] = 0;
     if (tid == 0) S.reachw = 0;
+    if (PROF && tid == 0) S.dbg_walk = S.dbg_twalk = S.dbg_tsync = 0;
     if (PROF) {  // diagnostics: wave 0's fill done
         __builtin_amdgcn_s_waitcnt(0);
         stamp();
@@ -1411,7 +1463,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         const uint32_t nval = sp.sl > p0 ? sp.sl - p0 : 0u;
         smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
     } else {
-        ph_parse_dev<C>(tid, S, sp, cw, cover, smask);
+        ph_parse_dev<C, LzSmem<C>, PROF>(tid, S, sp, cw, cover, smask);
     }
     stamp();
     // the chunk's words for the histogram and Adler-32
@@ -1481,6 +1533,19 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
 #endif
     if (!PBX_LZ_SKIP_OUT) lz_write_out<C>(S, seg, sp, d.out_off + sp.base + sp.wl, info, hist, mrec, tid);
     stamp();
+    // (diagnostics: slot 7 = slot 6 + the walk steps, so the lz77 report's "7:" is their mean;
+    // slots 30/31 (unused by k_encode) differ by 1 + 1000 x the repair rounds: encode "7:")
+    if (PROF && tid == 0) {
+        const uint64_t t6 = stamps[(size_t)seg * STAMP_STRIDE + 6];
+        stamps[(size_t)seg * STAMP_STRIDE + 7] = t6 + S.dbg_walk;
+        stamps[(size_t)seg * STAMP_STRIDE + 30] = t6;
+        stamps[(size_t)seg * STAMP_STRIDE + 31] = t6 + 1 + 1000ull * S.dbg_round;
+        if (PBX_LZ_WALK_PROF) {  // "1:" wave 0's walk cycles, "2:" its round cycles (walks included)
+            const uint64_t t0 = stamps[(size_t)seg * STAMP_STRIDE];
+            stamps[(size_t)seg * STAMP_STRIDE + 1] = t0 + 1 + S.dbg_twalk;
+            stamps[(size_t)seg * STAMP_STRIDE + 2] = t0 + 2 + S.dbg_twalk + S.dbg_tsync;
+        }
+    }
 }
 
 // ==================================================================== k_huff
