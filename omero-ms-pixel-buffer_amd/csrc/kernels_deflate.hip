@@ -788,7 +788,7 @@ __device__ __forceinline__ uint32_t pack_zero_bytes8(const uint32_t (&x)[8]) {
 // positions (M), scalar: lengths at k and k+1 from readlane'd masks, the lazy rule, the
 // wave-wide extension of a capped match.  Each lane also collects the positions of its
 // chunk covered by recorded matches (cover), for the histogram.
-template <class C, class SM, bool PROF = false>
+template <class C, class SM, bool PROF = false, bool VC = false>
 __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParams& sp, const uint32_t (&cw)[9],
                              uint32_t& cover, uint32_t& smask) {
     uint32_t nsteps = 0;  // (PROF) walk steps of this wave
@@ -995,8 +995,13 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     const uint64_t B = __ballot(M != 0);
     const uint32_t lsub = active ? se - ss : 0u;
 #ifndef PBX_LZ_VCAND
-#define PBX_LZ_VCAND 1  // the walk's candidate lengths in VALU, lane c for candidate c (0: scalar loop)
+#define PBX_LZ_VCAND 2  // the walk's candidate lengths in VALU, lane c for candidate c: 1 always, 2 in the
+                        // run-dense waves of row-filtered batches (VC), 0 never
 #endif
+    // (2: row-filtered streams put runs in every wave, every wave of the CU walks at once and the
+    // scalar unit is the bound; elsewhere -- filter None, noise -- the kernel keeps the scalar
+    // loop only: the VALU form measured 1-9% slower there, profiles/r05zs, r05zt)
+    const bool vcand = PBX_LZ_VCAND == 1 || (PBX_LZ_VCAND == 2 && VC && cvb_n >= (uint32_t)C::SUB / 2);
     // lane c < NCAND: candidate c's distance present and its match_minlen (the walk's VALU form)
     const bool vok = lane < (uint32_t)NCAND && (lane == 0 ? dd[0] : lane == 1 ? dd[1] : dd[2]) != 0;
     const uint32_t vml = lane == 0 ? ml[0] : lane == 1 ? ml[1] : ml[2];
@@ -1028,7 +1033,7 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
             if (k >= lsub) break;
             const uint32_t t = k >> 5, i = k & 31;
             uint32_t L = 0, D = 0, Dc = 0, L1 = 0;
-            if (PBX_LZ_VCAND) {
+            if (vcand) {
                 // lane c (< NCAND) evaluates candidate c at k and k + 1 in VALU (the scalar unit
                 // is the CU's bottleneck while every wave walks: run-heavy streams); the best
                 // (length, then the earliest candidate) by a max over the quad of packed
@@ -1374,7 +1379,7 @@ __device__ __forceinline__ void lz_write_out(const LzSmem<C>& S, uint32_t seg, c
 #else
 #define PBX_LZ_BOUNDS __launch_bounds__(C::NT)
 #endif
-template <class C, bool PROF>
+template <class C, bool PROF, bool VC = false>
 __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
                                                 const uint32_t* __restrict__ seg_tile,
                                                 uint32_t nseg, uint8_t* __restrict__ stream,
@@ -1463,7 +1468,7 @@ __global__ PBX_LZ_BOUNDS void k_lz77(const TileDesc* __restrict__ dt,
         const uint32_t nval = sp.sl > p0 ? sp.sl - p0 : 0u;
         smask = nval >= 32 ? 0xFFFFFFFFu : (1u << nval) - 1u;
     } else {
-        ph_parse_dev<C, LzSmem<C>, PROF>(tid, S, sp, cw, cover, smask);
+        ph_parse_dev<C, LzSmem<C>, PROF, VC>(tid, S, sp, cw, cover, smask);
     }
     stamp();
     // the chunk's words for the histogram and Adler-32
@@ -3408,14 +3413,15 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
         hipLaunchKernelGGL(k_seg_map, dim3((a.nseg + 255) / 256), dim3(256), 0, st, a.tiles, a.ntiles, a.nseg,
                            a.uniform_nseg, a.uniform_rcp, a.seg_tile, a.info, a.blk);
     const uint32_t lz_grid = a.nseg;
-    if (prof)
-        hipLaunchKernelGGL((k_lz77<DC, true>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.blk, a.hist, a.mrec, a.stamps, a.uniform_nseg,
-                           a.uniform_rcp, self_map);
-    else
-        hipLaunchKernelGGL((k_lz77<DC, false>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile,
-                           a.nseg, a.stream, a.info, a.blk, a.hist, a.mrec, a.stamps, a.uniform_nseg,
-                           a.uniform_rcp, self_map);
+#define PBX_LZ_LAUNCH(P, V)                                                                                  \
+    hipLaunchKernelGGL((k_lz77<DC, P, V>), dim3(lz_grid), dim3(DC::NT), 0, st, a.tiles, a.seg_tile, a.nseg,   \
+                       a.stream, a.info, a.blk, a.hist, a.mrec, a.stamps, a.uniform_nseg, a.uniform_rcp, self_map)
+    if (prof) {
+        if (a.row_filtered) PBX_LZ_LAUNCH(true, true); else PBX_LZ_LAUNCH(true, false);
+    } else {
+        if (a.row_filtered) PBX_LZ_LAUNCH(false, true); else PBX_LZ_LAUNCH(false, false);
+    }
+#undef PBX_LZ_LAUNCH
     if (ev && fine) (void)hipEventRecord(ev[0], st);
     if (ev2) (void)hipEventRecord(ev2[0], st);
     if (prof && a.nblk <= HUFF_SMALL_BLKS)  // (the phase profile of the variant that runs)

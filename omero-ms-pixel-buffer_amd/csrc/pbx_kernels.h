@@ -78,6 +78,7 @@ struct DeflateLaunch {
     uint32_t cus = 256;     // compute units of the device (persistent grids)
     uint32_t uniform_nseg = 0;  // every tile has this many segments (tile = seg / it), or 0
     uint32_t uniform_rcp = 0;   // recip32(uniform_nseg)
+    bool row_filtered = false;  // some tile's stream is PNG-row-filtered (k_lz77's VALU walk form)
 };
 // k_lz77, k_huff, k_seg_sizes + k_scan_offsets, k_encode, k_frame.
 // ev[0..3] (and ev2[0..3] if given) are recorded after k_lz77, k_huff, k_scan_offsets, k_encode;

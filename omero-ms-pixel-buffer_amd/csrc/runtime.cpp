@@ -2812,6 +2812,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     for (uint32_t k = 1; k < ndt && a.uniform_nseg; k++)
         if (b->dt[k].seg_count != a.uniform_nseg) a.uniform_nseg = 0;
     a.uniform_rcp = recip32(a.uniform_nseg);
+    for (uint32_t k = 0; k < ndt && !a.row_filtered; k++) a.row_filtered = b->dt[k].filter != 0;
     // the serving path reads the tile offsets from a mapped copy the scan writes (no D2H
     // copy at the end of the launch)
     void* offs_dev = nullptr;
