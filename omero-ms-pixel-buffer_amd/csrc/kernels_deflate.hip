@@ -1196,7 +1196,23 @@ __device__ __forceinline__ void ph_parse_dev(uint32_t tid, SM& S, const SegParam
     // segment before, 1.5 now).  (One call site of the walk: two inlined copies spill
     // registers to scratch.)
     uint32_t st = ss;  // (uniform) the start of this wave's current records
-    if (w && ((reachm >> (w - 1)) & 1u)) st = 258u * ((ss + 257u) / 258u);
+#ifndef PBX_LZ_ROWPRED
+#define PBX_LZ_ROWPRED 1  // row-filtered batches (VC): predict from the row start, not the segment start
+#endif
+    if (w && ((reachm >> (w - 1)) & 1u)) {
+        if (VC && PBX_LZ_ROWPRED && sp.rowlen > 2) {
+            // a row-filtered stream's runs break at every row's filter byte: predict where a chain
+            // of 258-byte matches from the boundary's row start would cross it, capped at the next
+            // row start (scripts/carry_sim.py, Up/Paeth/adaptive G_FAKE: 1.52 -> 0.15 repair rounds
+            // per segment, Sub/Avg 1.42 -> 0.55)
+            const uint32_t p = (uint32_t)((sp.base + sp.wl + ss) % sp.rowlen);
+            uint32_t cand = 258u * ((p + 257u) / 258u);
+            cand = cand < sp.rowlen ? cand : sp.rowlen;
+            st = ss + cand - p;
+        } else {
+            st = 258u * ((ss + 257u) / 258u);
+        }
+    }
     uint32_t cur = 0, jr = 0;
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)C::NW; j++) {

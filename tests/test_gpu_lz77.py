@@ -258,20 +258,28 @@ def _structured_rows(rng, rowbytes, h, ncopies):
     return s.reshape(h, rl)[:, 1:].copy(), s.tobytes()
 
 
+@pytest.mark.parametrize("filt", [0, 5])
 @pytest.mark.parametrize("seed", range(4))
-def test_gpu_png_structured_fuzz_bytes(service, seed):
+def test_gpu_png_structured_fuzz_bytes(oracle, seed, filt):
     """End to end on run-structured data: 320 tiles of random heights in one batch (more
     Huffman blocks than the small-batch k_huff takes: the batch kernels), 8- and 16-bit
     planes of row lengths across match_minlen's thresholds -- every tile's zlib stream equals
     the emulator's deflate byte for byte and inflates to the tile's scanlines, and its PNG
-    chunks carry valid CRCs (zlib.crc32 over type + data)."""
+    chunks carry valid CRCs (zlib.crc32 over type + data).  With the adaptive row filter (filt 5:
+    the row-filtered k_lz77 variant, its VALU walk and row-start predictions) the emulator deflates
+    the GPU's own filtered scanlines and the PNG decodes to the plane's pixels."""
+    with pbx.PixelsService(png_filter=filt) as service:
+        _png_structured_fuzz(service, oracle, seed, filt)
+
+
+def _png_structured_fuzz(service, oracle, seed, filt):
     rng = np.random.default_rng(8100 + seed)
     ctxs, streams = [], []
     for wi, w in enumerate([3, 100, 256, 300, 700, 2100]):
         bpp = 1 + wi % 2
         hs = [max(1, int(rng.integers(2000, 40000)) // (w * bpp + 1)) for _ in range(320 // 6 + 1)]
         rows, stream = _structured_rows(rng, w * bpp, sum(hs), 60 * len(hs))
-        iid = 9_900_000 + 100 * seed + wi
+        iid = 9_900_000 + 1000 * filt + 100 * seed + wi
         if bpp == 1:
             service.register_plane(iid, 0, 0, 0, pbx.UINT8, w, sum(hs), data=rows, big_endian=True)
         else:
@@ -281,11 +289,16 @@ def test_gpu_png_structured_fuzz_bytes(service, seed):
         for h in hs:
             ctxs.append(pbx.TileCtx(iid, 0, 0, 0, 0, y, w, h, format="png"))
             rl = w * bpp + 1
-            streams.append((stream[y * rl:(y + h) * rl], rl))
+            streams.append((stream[y * rl:(y + h) * rl], rl, rows[y:y + h].tobytes(), w, h, bpp))
             y += h
     res = service.get_tiles(ctxs)
-    for i, ((st, body), (stream, rl)) in enumerate(zip(res, streams)):
+    for i, ((st, body), (stream, rl, px, w, h, bpp)) in enumerate(zip(res, streams)):
         assert st == pbx.OK, i
+        if filt:  # the GPU's filtered scanlines; the pixels must come back exactly
+            n = int.from_bytes(body[91:95], "big")  # IDAT length
+            stream = zlib.decompress(body[99:95 + n + 4])
+            r, dpx, _ = oracle.png_decode(body)
+            assert r == 0 and dpx == px, (seed, i)
         z, _ = _emu.deflate(stream, rl)
         assert body[99:99 + len(z)] == z, (seed, i, rl, len(stream))
         assert zlib.decompress(z) == stream
