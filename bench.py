@@ -206,6 +206,20 @@ def load_issue(kernels=("k_encode", "k_lz77")):
     return None
 
 
+def load_rocprof_ms(kernel):
+    """The rocprofv3 kernel-trace average (ms) of `kernel` in the latest committed summary of
+    the headline's serial pass (profiles/*/kernel_stats.csv, PBX_KSTREAMS=1): (ms, source)."""
+    import csv
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "kernel_stats.csv")), reverse=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Name", "")
+                if f"::{kernel}<" in name or f"::{kernel}(" in name:
+                    return float(row["AverageNs"]) * 1e-6, os.path.relpath(fn, ROOT)
+    return None, None
+
+
 def cpu_model():
     """The host CPU model string (quote the CPU with the baseline)."""
     try:
@@ -571,12 +585,15 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
     import zlib
     import numpy as np
     out = {}
-    rng = np.random.default_rng(1234 + rank)
-    ps = 8192  # Poisson-like plane: lambda drifting 200..300 over the plane
+    # Poisson-like plane of the headline's size (4096 distinct tiles): lambda drifting 200..300
+    # over the plane in 64-px steps, drawn on the GPU (torch.poisson), registered from host memory
+    ps = side
     yy, xx = np.mgrid[0:ps:64, 0:ps:64]
     lam = 200.0 + 100.0 * (0.5 + 0.25 * np.sin(xx / 900.0) + 0.25 * np.cos(yy / 1300.0))
-    lam = np.repeat(np.repeat(lam, 64, 0), 64, 1)
-    pois = rng.poisson(lam).astype(np.uint16)
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    lam_t = torch.from_numpy(lam.astype(np.float32)).cuda().repeat_interleave(64, 0).repeat_interleave(64, 1)
+    pois = torch.poisson(lam_t, generator=gen).to(torch.int16).cpu().numpy().view(np.uint16)
+    del lam_t
     with pbx.PixelsService(device=torch.cuda.current_device(), png_filter=pbx.FILTER_ADAPTIVE) as sa:
         sa.set_kernel_streams(1, 0)  # serial: k_filter_ms is the kernel's own time
         for k, (name, gen, sz) in enumerate((("noise", "noise", side), ("fake", "fake", side),
@@ -590,8 +607,7 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 else:
                     held.append((s_, s_.register_plane(pid, 0, 0, 0, pbx.UINT16, sz, sz, data=pois,
                                                        big_endian=False)))
-            # a 4096-tile batch like the headline's on every plane: the 8192^2 Poisson plane's 256
-            # tiles 16 times each (a batch of its 256 tiles alone measures launch latency)
+            # a 4096-tile batch like the headline's on every plane, 4096 distinct tiles
             g = sz // TILE
             ctxs = [pbx.TileCtx(pid, 0, 0, 0, (i % g) * TILE, (i // g % g) * TILE, TILE, TILE, format="png")
                     for i in range(GRID * GRID)]
@@ -676,6 +692,19 @@ def extra(out, svc, rank, world, barrier, iid, side):
         "k_extract_ms": round(ms_ext, 3),
         "k_extract_gbps": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9, 1),
         "k_extract_frac": round(2 * sr[-1].in_bytes / (ms_ext * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    # the same grid at an odd x (x * bpp mod 16 = 6, as most of the reference's arbitrary-x
+    # requests, TileCtx.java:73-85): k_extract's realigned path
+    progress(rank, "raw unaligned")
+    rawu = [pbx.TileCtx(iid, 0, 0, 0, (i % GRID) * TILE + (3 if i % GRID < GRID - 1 else -5),
+                        (i // GRID) * TILE, TILE, TILE) for i in range(GRID * GRID)]
+    dtu, su, _ = secondary_steps(svc, rawu, 5, 2, barrier)
+    ms_u = mean(su, "ms_extract")
+    out["raw_unaligned_4096x512x512_u16"] = {
+        "tiles_per_s": round(len(rawu) * 5 * world / dtu, 1), **wall_vs_kernels(dtu, 5, su),
+        "x_times_bpp_mod_16": 6,
+        "k_extract_ms": round(ms_u, 3),
+        "k_extract_gbps": round(2 * su[-1].in_bytes / (ms_u * 1e-3) / 1e9, 1),
+        "k_extract_frac": round(2 * su[-1].in_bytes / (ms_u * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
     # A/B: the same headline batch with the filter-None rows staged in a stream buffer by
     # k_rows first (cfg.stage_rows), instead of assembled from the plane inside k_lz77
     progress(rank, "staged rows")
@@ -962,6 +991,7 @@ def main():
     # per step, over the whole step's time (all kernels, launches and host planning)
     e2e_bytes = st.in_bytes + st.deflate_out_bytes
     chain_traffic, chain_src = load_chain_traffic()
+    rp_ms, rp_src = load_rocprof_ms(dom)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -976,7 +1006,15 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "limiter": "issue / latency, not HBM bandwidth: the deflate kernels wait on "
+                                "dependent LDS and memory steps with VALU and SALU below saturation "
+                                "(`issue`); `bound` names the roof the line is priced against (HBM)",
                      "kernel": dom, "kernel_ms": round(dom_ms, 3),
+                     "kernel_ms_source": "HIP events around the kernel on its own stream, serial pass",
+                     "rocprof_kernel_ms": round(rp_ms, 4) if rp_ms else None,
+                     "rocprof_source": rp_src,
+                     "hip_event_over_rocprof": round(dom_ms / rp_ms, 3) if rp_ms else None,
+                     "frac_at_rocprof_ms": round(dom_bytes / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if rp_ms else None,
                      "kernel_choice": "longest mean HIP-event time of the serial pass",
                      "alg_bytes_per_launch": int(dom_bytes), "alg_bytes_definition": byte_def[dom],
                      "end_to_end_frac": round(e2e_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),

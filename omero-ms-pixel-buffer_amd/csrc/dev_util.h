@@ -56,6 +56,27 @@ __device__ __forceinline__ uint32_t upper_index(uint32_t n, uint32_t v, F key) {
     return lo;
 }
 
+// The same search by a whole wave (all 64 lanes active, the same n and v in every lane): each
+// round probes 64 evenly spaced keys at once and keeps the span between the last probe <= v
+// and the next, so 4096 keys take 2 dependent rounds of loads instead of 12.
+template <class F>
+__device__ __forceinline__ uint32_t upper_index_wave(uint32_t n, uint32_t v, F key) {
+    const uint32_t lane = __lane_id();
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t step = (hi - lo) / 64 + 1;  // 64 probes cover [lo, hi]
+        const uint32_t p = lo + lane * step;
+        const bool le = p <= hi && key(p) <= v;
+        const uint64_t m = __ballot(le);           // lane 0 (p = lo) is always set
+        const uint32_t t = 63u - (uint32_t)__builtin_clzll(m);
+        const uint32_t nlo = lo + t * step;
+        const uint32_t nhi = nlo + step - 1 < hi ? nlo + step - 1 : hi;
+        lo = __builtin_amdgcn_readfirstlane(nlo);
+        hi = __builtin_amdgcn_readfirstlane(nhi);
+    }
+    return lo;
+}
+
 // Inclusive prefix sum over the wave by DPP alone (no ds_bpermute round trips): row scans by
 // row_shr (zero shifted in), then row_bcast:15 / :31 carry the row totals into the rows above.
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
@@ -148,6 +169,20 @@ __device__ __forceinline__ void funnel16(const uint4& lo, const uint4& hi, uint3
     w[1] = __builtin_amdgcn_alignbit(t2, t1, sh);
     w[2] = __builtin_amdgcn_alignbit(t3, t2, sh);
     w[3] = __builtin_amdgcn_alignbit(t4, t3, sh);
+}
+
+// 16 bytes from an address of any alignment in global memory: the aligned 16-byte word at or
+// below it and (unless it is aligned) the next one, funnel-shifted.  Reads up to 31 bytes past
+// `p`: callers stay inside a plane's pitched rows and its 256 B of over-read slack.
+__device__ __forceinline__ uint4 gload16u(const uint8_t* p) {
+    const uint32_t bs = (uint32_t)(uintptr_t)p & 15u;
+    const uint8_t* a = p - bs;
+    const uint4 lo = gload16(a);
+    uint4 hi = lo;
+    if (bs) hi = gload16(a + 16);
+    uint32_t w[4];
+    funnel16(lo, hi, bs, w);
+    return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 }  // namespace pbx

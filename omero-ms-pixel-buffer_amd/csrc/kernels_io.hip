@@ -137,7 +137,7 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
 __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft, uint32_t nft,
                                                  uint8_t* __restrict__ out) {
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t ti = upper_index(nft, b, [&](uint32_t i) { return ft[i].blk_first; });
+    const uint32_t ti = upper_index_wave(nft, b, [&](uint32_t i) { return ft[i].blk_first; });
     const TileDesc d = ft[ti];
     const uint32_t rb = (uint32_t)d.w * (uint32_t)d.bpp;
     const uint32_t r0 = (b - d.blk_first) * d.rows_per_blk;
@@ -153,12 +153,65 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
     const bool fast = !d.vw && (((uintptr_t)src0 | (uintptr_t)base | (uintptr_t)d.pitch | rb) & 15u) == 0;
     const bool swap = (d.flags & TF_SWAP) != 0;
     if (fast) {
+        // EXT_U loads per thread in flight before their stores (a block's ~16 KiB of rows is
+        // one round: 4 KiB per wave in flight instead of 1)
+#ifndef PBX_EXT_U
+#define PBX_EXT_U 4
+#endif
+        constexpr uint32_t EXT_U = PBX_EXT_U;
         const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
-        for (uint32_t i = tid; i < nv; i += 256) {
-            const uint32_t r = r0 + i / n16, v = i % n16;
-            uint4 q = gload16(src0 + (int64_t)r * d.pitch + 16 * v);
+        for (uint32_t i0 = tid; i0 < nv; i0 += 256 * EXT_U) {
+            uint4 q[EXT_U];
+#pragma unroll
+            for (uint32_t k = 0; k < EXT_U; k++) {
+                const uint32_t i = i0 + 256 * k, r = r0 + i / n16, v = i - (i / n16) * n16;
+                if (i < nv) q[k] = gload16(src0 + (int64_t)r * d.pitch + 16 * v);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < EXT_U; k++) {
+                const uint32_t i = i0 + 256 * k, r = r0 + i / n16, v = i - (i / n16) * n16;
+                if (i >= nv) break;
+                if (swap) q[k] = swap16(q[k], d.bpp);
+                gstore16(base + (size_t)r * rb + 16 * v, q[k]);
+            }
+        }
+    } else if (!d.vw && rb >= 16) {
+        // Any other region (x * bpp not a multiple of 16, or rows of a length that is not): the
+        // output is one contiguous run of (r1 - r0) * rb bytes at a 16-byte aligned base, so
+        // every whole 16-byte output word of this block is built from 16 source bytes loaded
+        // as two aligned words and funnel-shifted (gload16u).  Its bytes lie in row r from
+        // column c on, and -- when fewer than 16 remain in the row -- in row r + 1 from column
+        // 0: that part is loaded from n1 bytes before row r + 1's start and merged by a byte
+        // mask.  Rows hold whole samples and c is a multiple of bpp (16 and rb are), so the
+        // byte swap is swap16 on the assembled word.  The up-to-15 bytes at each end of the
+        // block's run share an output word with the neighbouring block: written singly.
+        const uint32_t f0 = r0 * rb, f1 = r1 * rb;
+        const uint32_t w0 = (f0 + 15) >> 4, w1 = f1 >> 4;
+        for (uint32_t wi = w0 + tid; wi < w1; wi += 256) {
+            const uint32_t o = wi << 4, r = o / rb, c = o - r * rb, n1 = rb - c;
+            uint4 q = gload16u(src0 + (int64_t)r * d.pitch + c);
+            if (n1 < 16) {  // the word runs into row r + 1
+                const uint4 q2 = gload16u(src0 + (int64_t)(r + 1) * d.pitch - n1);
+                auto keep = [&](uint32_t j) {  // bytes of word j that come from row r
+                    return n1 >= 4 * j + 4 ? 0xFFFFFFFFu : n1 <= 4 * j ? 0u : (1u << (8 * (n1 - 4 * j))) - 1u;
+                };
+                const uint32_t m0 = keep(0), m1 = keep(1), m2 = keep(2), m3 = keep(3);
+                q.x = (q.x & m0) | (q2.x & ~m0);
+                q.y = (q.y & m1) | (q2.y & ~m1);
+                q.z = (q.z & m2) | (q2.z & ~m2);
+                q.w = (q.w & m3) | (q2.w & ~m3);
+            }
             if (swap) q = swap16(q, d.bpp);
-            *(uint4*)(base + (size_t)r * rb + 16 * v) = q;
+            gstore16(base + o, q);
+        }
+        const uint32_t h_end = f1 < (w0 << 4) ? f1 : (w0 << 4);
+        const uint32_t t_beg = (w1 << 4) > h_end ? (w1 << 4) : h_end;
+        const uint32_t i = tid < 16 ? f0 + tid : t_beg + (tid - 16);
+        if (tid < 32 && (tid < 16 ? i < h_end : i < f1)) {
+            TileStream ts;
+            ts.init(d, nullptr);
+            const uint32_t r = i / rb, c = i - r * rb;
+            base[i] = (uint8_t)ts.be(r, c);
         }
     } else {
         TileStream ts;
@@ -223,7 +276,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                                                 uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t r0 = (b - d.blk_first) * FB_ROWS;
     const uint32_t r1 = r0 + FB_ROWS < (uint32_t)d.h ? r0 + FB_ROWS : (uint32_t)d.h;
@@ -233,8 +286,9 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
     const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
     const uint32_t rbp = ((rb + 15) & ~15u) + 16;
     uint32_t* ftype = (uint32_t*)(sm + FB_LDS - 256);
-    const bool fast = !d.vw && (uint64_t)(FB_ROWS + 1) * rbp + 256 <= (uint64_t)FB_LDS &&
-                      ((((uintptr_t)src0) | (uintptr_t)d.pitch) & 15) == 0;
+    // (source rows of any alignment: gload16u; the pitch of every plane, band and bridge is a
+    // multiple of 256)
+    const bool fast = !d.vw && (uint64_t)(FB_ROWS + 1) * rbp + 256 <= (uint64_t)FB_LDS;
     const uint32_t o0 = r0 * rowlen, o1 = r1 * rowlen;
     if (fast) {
         const uint32_t nq = r1 - r0 + 1, nc = (rb + 15) >> 4;
@@ -244,11 +298,11 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
             const int64_t row = (int64_t)r0 - 1 + q;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (row >= 0 && png) {
-                v = gload16(src0 + row * d.pitch + 16 * c);
+                v = gload16u(src0 + row * d.pitch + 16 * c);
                 if (swap) v = swap16(v, bpp);
                 if (flip) v = flip_msb(v, bpp);
             } else if (row >= 0) {
-                v = gload16(src0 + row * d.pitch + 16 * c);
+                v = gload16u(src0 + row * d.pitch + 16 * c);
                 if (swap) v = swap16(v, bpp);
             }
             *(uint4*)(sm + q * rbp + 16 * c) = v;
@@ -437,8 +491,9 @@ hipError_t launch_stall(hipStream_t st, const uint32_t* flag, uint64_t limit_tic
 // The stream of a filter-None PNG tile is row r = [0] ++ big-endian row bytes, and of a
 // deflate-TIFF tile the row bytes alone.  One workgroup per band of RB_ROWS rows (whose
 // stream bytes start and end 16-byte aligned, as RB_ROWS * rowlen is a multiple of 16):
-// the band's source rows are loaded once with aligned 16-byte loads (byte swap and sign
-// flip applied there, where the sample boundaries are known) into LDS rows padded to
+// the band's source rows are loaded once as 16-byte words (realigned in registers when the
+// region's x * bpp is not a multiple of 16; byte swap and sign flip applied there, where the
+// sample boundaries are known) into LDS rows padded to
 // 16 bytes, then every aligned 16-byte stream word is assembled from 5 LDS words with
 // funnel shifts; the few words that straddle a row end merge two rows with byte masks.
 constexpr int RB_NT = 256;
@@ -465,7 +520,7 @@ __global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt,
                                                 uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lrow[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
     const uint32_t rowlen = d.rowlen, rb = rowlen - fb, bpp = d.bpp;
@@ -479,7 +534,8 @@ __global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt,
     uint32_t* rows = lrow + 4;
     for (uint32_t i = tid; i < nr * nc; i += RB_NT) {
         const uint32_t q = i / nc, c = i - q * nc;
-        uint4 v = gload16(src0 + (int64_t)q * d.pitch + 16 * c);
+        // (source rows of any alignment: gload16u realigns; 16 c is a sample boundary)
+        uint4 v = gload16u(src0 + (int64_t)q * d.pitch + 16 * c);
         if (swap) v = swap16(v, (int)bpp);
         if (flip) v = flip_msb(v, (int)bpp);
         *(uint4*)(rows + q * rw + 4 * c) = v;
@@ -646,7 +702,7 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
                                                   uint32_t rbq_max, uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t ti = upper_index(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t r0 = (b - d.blk_first) * F2_ROWS;
     const uint32_t nr = (uint32_t)d.h - r0 < F2_ROWS ? (uint32_t)d.h - r0 : F2_ROWS;

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <functional>
 #include <tuple>
 #include <type_traits>
 #include <unordered_map>
@@ -258,6 +259,12 @@ struct EventPool {
 // Waits for an event: small batches (the single-request latency path) poll it for up to
 // `spin_us` first -- a blocking wait wakes the thread tens of microseconds after the GPU is
 // done -- then block.
+// A spinning thread's pause between polls (spin loops without one take cores
+// from the JVM's workers and storm the HIP runtime with queries).
+inline void cpu_relax() {
+    for (int k = 0; k < 8; k++) __builtin_ia32_pause();
+}
+
 hipError_t wait_event(hipEvent_t e, int64_t spin_us) {
     if (spin_us > 0) {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
@@ -265,6 +272,7 @@ hipError_t wait_event(hipEvent_t e, int64_t spin_us) {
             const hipError_t q = hipEventQuery(e);
             if (q != hipErrorNotReady) return q;
             if (std::chrono::steady_clock::now() >= until) break;
+            cpu_relax();
         }
     }
     return hipEventSynchronize(e);
@@ -285,6 +293,14 @@ struct Reaper {
     bool stop = false;
     std::thread th;
     int device = 0;
+    // Housekeeping between frees: while `ticking`, tick() runs every few ms (outside mu) until
+    // it reports nothing left -- the uncoalesced pbx_get_tile calls parked at their deadline
+    // are collected here, so their pins and pool blocks go back even if the context goes idle
+    // (ADVICE r05).  poke() starts it; pokes counts them so that a poke during a tick that
+    // found nothing is not lost.
+    std::function<bool()> tick;
+    bool ticking = false, in_tick = false;
+    uint64_t pokes = 0;
 
     void start(int dev) {
         device = dev;
@@ -294,15 +310,28 @@ struct Reaper {
         (void)hipSetDevice(device);
         std::unique_lock<std::mutex> g(mu);
         for (;;) {
-            cv.wait(g, [&] { return stop || !q.empty(); });
-            if (q.empty()) break;  // stopping, nothing left
-            std::vector<void*> take(q.begin(), q.end());
-            q.clear();
-            busy++;
-            g.unlock();
-            for (void* p : take) (void)hipFree(p);
-            g.lock();
-            busy--;
+            auto ready = [&] { return stop || !q.empty(); };
+            if (ticking) cv.wait_for(g, std::chrono::milliseconds(2), ready);
+            else cv.wait(g, [&] { return ready() || ticking; });
+            if (stop && q.empty()) break;  // stopping, nothing left
+            if (!q.empty()) {
+                std::vector<void*> take(q.begin(), q.end());
+                q.clear();
+                busy++;
+                g.unlock();
+                for (void* p : take) (void)hipFree(p);
+                g.lock();
+                busy--;
+            }
+            if (ticking && tick) {
+                const uint64_t seen = pokes;
+                in_tick = true;
+                g.unlock();
+                const bool more = tick();
+                g.lock();
+                in_tick = false;
+                if (!more && pokes == seen) ticking = false;
+            }
             cv_idle.notify_all();
         }
     }
@@ -313,6 +342,21 @@ struct Reaper {
             q.push_back(p);
         }
         cv.notify_one();
+    }
+    void poke() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            ticking = true;
+            pokes++;
+        }
+        cv.notify_one();
+    }
+    // No further ticks (shutdown): waits for one in progress.
+    void stop_ticking() {
+        std::unique_lock<std::mutex> g(mu);
+        tick = nullptr;
+        ticking = false;
+        cv_idle.wait(g, [&] { return !in_tick; });
     }
     // Waits until every handed-over block is back with the device (an allocation that ran out
     // of memory retries only after that).
@@ -873,6 +917,16 @@ void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
 
 }  // namespace
 
+// Rows of one k_extract workgroup: about this many bytes ($PBX_EXT_BLK, default 16 KiB).
+static uint32_t ext_blk_bytes() {
+    static const uint32_t v = [] {
+        const char* e = getenv("PBX_EXT_BLK");
+        const long x = e ? atol(e) : 16384;
+        return (uint32_t)std::min<long>(1 << 20, std::max<long>(1024, x));
+    }();
+    return v;
+}
+
 static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_follows);
 
 // One synchronous batch: plan + launch under run_mu (launches stay in order on the
@@ -1042,37 +1096,47 @@ struct Coalescer {
     // reference's event-bus send timeout, PixelBufferMicroserviceVerticle.java:148-151) has
     // passed: then 500 (:356-366).  A request still queued is withdrawn; one whose batch is in
     // flight is abandoned to the completer, which releases its result when the batch ends.
-    int submit(const pbx_tile_req& r, pbx_result* out) {
+    // `to` (us, <= 0: none) is the call's deadline, counted from entry: neither the plan and
+    // launch of a direct request nor a wait for ctx->run_mu may run past it.
+    int submit(const pbx_tile_req& r, pbx_result* out, int64_t to) {
+        const auto t_in = clk::now();
+        const auto until = t_in + std::chrono::microseconds(to > 0 ? to : 0);
         Pending* p = new Pending();
         p->req = r;
-        if (timeline) p->t[0] = clk::now();
+        if (timeline) p->t[0] = t_in;
         std::unique_lock<std::mutex> g(mu);
         if (stop) {
             delete p;
             return fail(PBX_E_INTERNAL, "context is shutting down");
         }
-        const int64_t to = ctx->timeout_us;
+        bool launched = false;
         if (queue.empty() && inflight == 0 && direct) {
             // an idle coalescer: this thread plans and launches its own request (no hand-off
-            // to the launcher thread, whose wake-up the lone request would wait for); the
-            // completer fetches it as any other batch, so the deadline below still holds
-            inflight++;
-            g.unlock();
-            launch_take(std::vector<Pending*>{p});
-            g.lock();
-        } else {
+            // to the launcher thread, whose wake-up the lone request would wait for) -- but only
+            // if run_mu is free now: a thread holding it (a release_cached syncing a wedged
+            // device, a batch launch) could keep a direct caller past its deadline, so such a
+            // request goes to the launcher and this thread waits on its deadline.  The
+            // completer fetches a direct batch as any other, so the deadline below holds.
+            std::unique_lock<std::mutex> run(ctx->run_mu, std::try_to_lock);
+            if (run.owns_lock()) {
+                inflight++;
+                g.unlock();
+                launch_take(std::vector<Pending*>{p}, &run);
+                g.lock();
+                launched = true;
+            }
+        }
+        if (!launched) {
             queue.push_back(p);
             cv_launch.notify_one();
         }
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(to > 0 ? to : 0);
         // a lone caller (an idle coalescer: the single-request latency path) polls for its
         // result before it blocks -- a condition-variable wake-up costs it ~15 us
         if (ctx->spin_us > 0 && queue.size() + (size_t)inflight <= 2) {
             g.unlock();
-            const int64_t su = to > 0 ? std::min<int64_t>(ctx->spin_us, to) : ctx->spin_us;
-            const auto spin_until = std::chrono::steady_clock::now() + std::chrono::microseconds(su);
-            while (!p->done.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < spin_until) {
-            }
+            auto spin_until = t_in + std::chrono::microseconds(ctx->spin_us);
+            if (to > 0 && until < spin_until) spin_until = until;
+            while (!p->done.load(std::memory_order_acquire) && clk::now() < spin_until) cpu_relax();
             g.lock();
         }
         if (to > 0) {
@@ -1123,7 +1187,8 @@ struct Coalescer {
     }
     // Plans and launches one batch of taken requests (inflight already counts it) and hands
     // it to the completers.
-    void launch_take(std::vector<Pending*> take) {
+    // `held`: run_mu already taken by the caller (the direct path); released here after the launch.
+    void launch_take(std::vector<Pending*> take, std::unique_lock<std::mutex>* held = nullptr) {
         (void)hipSetDevice(ctx->device);
         {
             std::vector<pbx_tile_req> reqs(take.size());
@@ -1132,11 +1197,13 @@ struct Coalescer {
             clk::time_point t1, t2, t3;
             if (timeline) t1 = clk::now();
             {
-                std::lock_guard<std::mutex> run(ctx->run_mu);
+                std::unique_lock<std::mutex> own;
+                if (!held) own = std::unique_lock<std::mutex>(ctx->run_mu);
                 f.rc = pbx_batch_plan(ctx, reqs.data(), reqs.size(), &f.b);
                 if (timeline) t2 = clk::now();
                 if (f.rc == PBX_OK) f.rc = batch_launch(ctx, f.b, false, true);
                 if (f.rc != PBX_OK) f.err = g_err;
+                if (held) held->unlock();
             }
             if (timeline) {
                 t3 = clk::now();
@@ -1330,6 +1397,11 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     }
     if (const char* fb = getenv("PBX_FAIL_BATCH")) ctx->fail_at = strtoull(fb, nullptr, 10);
     if (const char* bs = getenv("PBX_BAND_STALE_MS")) ctx->stale_ns = (int64_t)atoll(bs) * 1000000;
+    ctx->reaper.tick = [ctx] {
+        collect_late(ctx, false);
+        std::lock_guard<std::mutex> g(ctx->late_mu);
+        return !ctx->late.empty();
+    };
     ctx->reaper.start(dev);
     if (cfg.coalesce) ctx->coal = new Coalescer(ctx);
     *out = ctx;
@@ -1341,6 +1413,7 @@ void pbx_shutdown(pbx_ctx* ctx) {
     if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 0u, __ATOMIC_SEQ_CST);  // a stalled batch ends
     delete ctx->coal;  // drains queued requests, joins its threads
     ctx->coal = nullptr;
+    ctx->reaper.stop_ticking();  // (no late collection on the reaper thread from here on)
     collect_late(ctx, true);
     (void)hipSetDevice(ctx->device);
     (void)sync_kernel_streams(ctx);
@@ -2494,7 +2567,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                 g.p = pp;
                 g.x = r.x; g.y = r.y; g.w = w; g.h = h; g.k0 = kr[0]; g.k1 = kr[1];
                 g.xo = ((int64_t)r.x * bpp) & 255;  // same alignment as in the plane rows
-                g.bp = (g.xo + (int64_t)w * bpp + 16 + 255) & ~(int64_t)255;  // + vector over-read
+                g.bp = (g.xo + (int64_t)w * bpp + 32 + 255) & ~(int64_t)255;  // + vector over-read (gload16u: 31 B)
                 g.off = b->bridge_bytes;
                 b->bridge_bytes += (uint64_t)g.bp * (uint64_t)h + 256;
                 b->bridges.push_back(g);
@@ -2569,7 +2642,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         if (!deflate) {
             if (r.format == PBX_FMT_TIF) d.flags |= TF_TIFF;
             const uint32_t rb = (uint32_t)w * bpp;
-            d.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(16384 / std::max<uint32_t>(rb, 1)));
+            d.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(ext_blk_bytes() / std::max<uint32_t>(rb, 1)));
             const uint32_t blks = (uint32_t)((h + d.rows_per_blk - 1) / d.rows_per_blk);
             d.blk_first = b->ext_blocks;
             b->ext_blocks += blks;
@@ -2593,15 +2666,16 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             // from the plane (TF_DIRECT: no k_rows; k_lz77 writes the stream for k_encode);
             // cfg.stage_rows routes them through k_rows (vector funnel copy) instead.
             // Filtered or odd-shaped tiles go to the banded k_filter.
+            // (k_rows reads source rows of any alignment; k_lz77's direct fill needs them aligned)
             const uint32_t rb = (uint32_t)w * bpp;
-            const bool rows_ok = d.filter == 0 && d.rowlen >= 32 && rb <= ROWS_MAX_RB &&
-                                 ((uint64_t)d.x * bpp % 16) == 0;
+            const bool rows_ok = d.filter == 0 && d.rowlen >= 32 && rb <= ROWS_MAX_RB;
+            const bool aligned = ((uint64_t)d.x * bpp % 16) == 0;
             // filtered PNG rows of whole dwords: dword-wide filter arithmetic (k_filter2)
             const bool filt2_ok = (d.flags & TF_PNGROWS) && d.filter != 0 && rb % 4 == 0 && rb >= 16 &&
                                   rb <= filter2_max_rb() && ((uint64_t)d.x * bpp % 16) == 0;
             // filtered PNG rows of whole 16-byte chunks: the streaming one-wave-per-run k_filter3
             const bool filt3_ok = use_f3 && filt2_ok && rb % 16 == 0 && rb <= filter3_max_rb();
-            if (rows_ok && bpp <= 4 && !ctx->cfg.stage_rows) {
+            if (rows_ok && aligned && bpp <= 4 && !ctx->cfg.stage_rows) {
                 d.flags |= TF_DIRECT;
                 dt_direct.push_back(d);
                 req_direct.push_back((uint32_t)i);
@@ -3229,36 +3303,88 @@ int pbx_shard_of(const pbx_tile_req* r, int32_t tw, int32_t th, int32_t world) {
     return (int)(k % (uint64_t)world);
 }
 
-int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
-    if (!ctx || !req || !out) return fail(PBX_E_BADARG, "null argument");
+}  // extern "C"
+
+// One getTile with a deadline of `to` us from now (<= 0: none).  Uncoalesced contexts plan and
+// launch the lite single-request batch themselves (as run_batch; run_mu waited for only until the
+// deadline), poll its completion until the deadline, and past it park the batch for the reaper
+// thread's collector (the ticket's pins and pool blocks return even if the context
+// then goes idle).
+static int get_tile_within(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out, int64_t to) {
     int st;
     if (ctx->coal) {
-        st = ctx->coal->submit(*req, out);
-    } else if (ctx->timeout_us <= 0) {
+        st = ctx->coal->submit(*req, out, to);
+    } else if (to <= 0) {
         st = run_batch(ctx, req, 1, out);
-    } else {  // one batch per call, waited for until the deadline
-        collect_late(ctx, false);
-        const auto t0 = std::chrono::steady_clock::now();
-        pbx_result* own = new pbx_result[1]();
-        pbx_ticket* t = nullptr;
-        st = pbx_submit(ctx, req, 1, own, &t);
-        if (st == PBX_OK) {
-            const int64_t spent = std::chrono::duration_cast<std::chrono::microseconds>(
-                std::chrono::steady_clock::now() - t0).count();
-            st = pbx_wait(ctx, t, std::max<int64_t>(0, ctx->timeout_us - spent));
-            if (st == PBX_E_PENDING) {
-                {
-                    std::lock_guard<std::mutex> g(ctx->late_mu);
-                    ctx->late.emplace_back(t, own);
-                }
-                return deadline_result(ctx, *req, out);
+    } else {
+        using clk = std::chrono::steady_clock;
+        const auto until = clk::now() + std::chrono::microseconds(to);
+        pbx_batch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> run(ctx->run_mu, std::defer_lock);
+            while (!run.try_lock()) {
+                if (clk::now() >= until) return deadline_result(ctx, *req, out);
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
             }
-            *out = own[0];
+            st = pbx_batch_plan(ctx, req, 1, &b);
+            if (st) return st;
+            st = batch_launch(ctx, b, false, true);
         }
-        delete[] own;
+        ctx->n_batches++;
+        ctx->n_requests++;
+        if (st == PBX_OK) {
+            if (ensure_device(ctx)) return PBX_E_INTERNAL;
+            const auto spin_until = clk::now() + std::chrono::microseconds(ctx->spin_us);
+            int64_t nap = 5;
+            for (;;) {
+                const hipError_t q = hipEventQuery(b->ev[8]);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) break;  // the fetch reports the device error
+                const auto now = clk::now();
+                if (now >= until) {  // parked: the reaper's collector releases it when it ends
+                    pbx_ticket* t = new pbx_ticket();
+                    t->b = b;
+                    t->out = new pbx_result[1]();
+                    {
+                        std::lock_guard<std::mutex> g(ctx->late_mu);
+                        ctx->late.emplace_back(t, t->out);
+                    }
+                    ctx->reaper.poke();
+                    return deadline_result(ctx, *req, out);
+                }
+                if (now < spin_until) {
+                    cpu_relax();
+                } else {
+                    std::this_thread::sleep_for(std::chrono::microseconds(nap));
+                    nap = std::min<int64_t>(nap * 2, 200);
+                }
+            }
+            st = pbx_batch_fetch(ctx, b, out);
+        }
+        if (st != PBX_OK) {  // as run_batch: a device failure is this request's 500
+            const std::string msg = g_err;
+            out->status = b->status[0] == PBX_OK ? PBX_E_INTERNAL : b->status[0];
+            out->format = req->format;
+            out->w = b->w[0];
+            out->h = b->h[0];
+            out->data = nullptr;
+            out->len = 0;
+            out->owner = nullptr;
+            pbx_batch_destroy(ctx, b);
+            g_err = msg;
+            return st;
+        }
+        pbx_batch_destroy(ctx, b);
     }
     if (st) return st;
     return out->status;
+}
+
+extern "C" {
+
+int pbx_get_tile(pbx_ctx* ctx, const pbx_tile_req* req, pbx_result* out) {
+    if (!ctx || !req || !out) return fail(PBX_E_BADARG, "null argument");
+    return get_tile_within(ctx, req, out, ctx->timeout_us);
 }
 
 int pbx_test_fail_band_write(pbx_ctx* ctx, uint64_t ahead) {
@@ -3371,13 +3497,22 @@ int pbx_node_route(pbx_node* node, const pbx_tile_req* req, int32_t* index) {
 
 int pbx_node_get_tile(pbx_node* node, const pbx_tile_req* req, pbx_result* out, int32_t* served_by) {
     if (!node || !req || !out) return fail(PBX_E_BADARG, "null argument");
+    // One deadline for the whole call: the retry gets what the first attempt left.
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     int st = PBX_E_NOT_RESIDENT;
     for (int attempt = 0; attempt < 2; attempt++) {  // a plane evicted between route and get
         int32_t k = 0;
         const int r = pbx_node_route(node, req, &k);
         if (r == PBX_E_BADARG) return r;
         if (served_by) *served_by = k;
-        st = pbx_get_tile(node->ctxs[(size_t)k], req, out);
+        pbx_ctx* c = node->ctxs[(size_t)k];
+        int64_t to = c->timeout_us;
+        if (to > 0 && attempt) {
+            to -= std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count();
+            if (to <= 0) return deadline_result(c, *req, out);
+        }
+        st = get_tile_within(c, req, out, to);
         if (st != PBX_E_NOT_RESIDENT || r == PBX_E_NOT_RESIDENT) break;
     }
     return st;

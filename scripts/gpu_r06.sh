@@ -13,6 +13,8 @@
 #   pmc      PMC passes of the headline deflate chain (scripts/pmc_run.sh, filter passes off)
 #   parity   the output-parity suites alone
 #   kstats   rocprofv3 kernel averages of a short headline run
+#   raw      k_extract alone (scripts/raw_probe.py), aligned / unaligned, PBX_EXT_BLK 16-64 KiB
+#   c5       configs[4]'s pass alone (scripts/c5_pass.py) and its rocprofv3 kernel trace
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
 # Every GPU step has its own time limit; the first failure ends the call.
 set -o pipefail
@@ -102,6 +104,20 @@ for stage in "$@"; do
       PBX_KSTREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kprof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $O/kprof_bench.json 2> $O/kprof_bench.err || { tail -20 $O/kprof_bench.err; exit 1; }
       find $O/kprof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_short.csv \;
       cut -d, -f1-4 $O/kernel_stats_short.csv | head -12 ;;
+    raw)  # k_extract alone, aligned and unaligned, at several workgroup sizes
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
+        for eb in ${EXT_BLKS:-16384 32768 65536}; do
+          echo "-- $L"
+          PBX_LIB=$PWD/$L PBX_EXT_BLK=$eb timeout -k 10 200 python -u scripts/raw_probe.py 5 > $O/raw.log 2>&1 || { tail -20 $O/raw.log; exit 1; }
+          cat $O/raw.log
+        done
+      done ;;
+    c5)
+      timeout -k 10 300 python -u scripts/c5_pass.py 3 > $O/c5_pass.log 2>&1 || { tail -20 $O/c5_pass.log; exit 1; }
+      cat $O/c5_pass.log
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c5prof -o run --output-format csv -- python3 scripts/c5_pass.py 1 > $O/c5_prof.log 2>&1 || { tail -20 $O/c5_prof.log; exit 1; }
+      find $O/c5prof -name "*kernel_stats.csv" -exec cp {} $O/c5_kernel_stats.csv \;
+      cut -d, -f1-4 $O/c5_kernel_stats.csv | head -16 ;;
     bench)
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['deflate_chain_ms'], d['roofline']['frac'])"

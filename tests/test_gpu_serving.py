@@ -349,6 +349,66 @@ def test_stalled_batch_answers_500_at_deadline(oracle):
         _check_body(oracle, reqs[2], st, body, pt, seed)
 
 
+def test_direct_caller_keeps_deadline_while_run_mu_held(oracle):
+    """a lone request that finds the coalescer idle is planned and launched
+    by its own thread -- but only if the launch lock (run_mu) is free.  Here a batch submitted
+    outside the coalescer stalls on the device and pbx_release_cached holds run_mu while it waits
+    for the kernel streams; a lone pbx_get_tile must still answer 500 at its deadline
+    (PixelBufferMicroserviceVerticle.java:148-151,356-366), and everything completes exactly once
+    the stall is released."""
+    iid = next(_ids)
+    pt, side, seed = pbx.UINT16, 2048, 13
+    D = 1.0
+    with pbx.PixelsService(request_timeout_us=int(D * 1e6)) as svc:
+        svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=seed)
+        reqs = [pbx.TileCtx(iid, 0, 0, 0, 100 * k, 37 * k, 256, 200, format=["png", None, "tif"][k % 3])
+                for k in range(6)]
+        _check_body(oracle, reqs[0], *svc.get_tile(reqs[0]), pt, seed)
+        svc.test_stall_batch(1)
+        ticket = svc.submit([reqs[1]])  # pbx_submit: stalled on the device, not the coalescer's
+        holder = threading.Thread(target=svc.release_cached)  # takes run_mu, waits for the streams
+        holder.start()
+        time.sleep(0.3)
+        assert holder.is_alive()
+        t = time.monotonic()
+        st, body = svc.get_tile(reqs[2])  # the coalescer is idle: the direct path
+        took = time.monotonic() - t
+        svc.test_stall_batch(0)
+        holder.join(timeout=30)
+        assert not holder.is_alive()
+        assert st == pbx.E_INTERNAL and body is None
+        assert D - 0.05 <= took < D + 0.5, took
+        (s1, b1), = ticket.wait()
+        _check_body(oracle, reqs[1], s1, b1, pt, seed)
+        for tc in reqs[2:]:
+            _check_body(oracle, tc, *svc.get_tile(tc), pt, seed)
+
+
+def test_uncoalesced_late_batch_is_collected_while_idle(oracle):
+    """an uncoalesced pbx_get_tile past its deadline parks its batch; the
+    context's reaper thread collects it once it completes, with no later call on the context,
+    so its plane pin goes: a plane released meanwhile gives its HBM back."""
+    iid = next(_ids)
+    pt, side, seed = pbx.UINT16, 2048, 14
+    D = 0.5
+    with pbx.PixelsService(coalesce=False, request_timeout_us=int(D * 1e6)) as svc:
+        before = svc.residency_stats()["resident_bytes"]
+        pid = svc.register_plane(iid, 0, 0, 0, pt, side, side, generator="noise", seed=seed)
+        tc = pbx.TileCtx(iid, 0, 0, 0, 64, 64, 256, 256, format="png")
+        _check_body(oracle, tc, *svc.get_tile(tc), pt, seed)
+        svc.test_stall_batch(1)
+        t = time.monotonic()
+        st, body = svc.get_tile(tc)
+        assert st == pbx.E_INTERNAL and body is None and D - 0.05 <= time.monotonic() - t < D + 0.5
+        svc.release_plane(pid)  # the parked batch still pins it
+        assert svc.residency_stats()["resident_bytes"] > before
+        svc.test_stall_batch(0)
+        deadline = time.monotonic() + 5
+        while svc.residency_stats()["resident_bytes"] > before and time.monotonic() < deadline:
+            time.sleep(0.02)
+        assert svc.residency_stats()["resident_bytes"] == before
+
+
 # ---------------------------------------------------------------- node routing
 
 def test_node_two_contexts_one_device(oracle):
