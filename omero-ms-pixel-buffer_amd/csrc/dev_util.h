@@ -185,4 +185,38 @@ __device__ __forceinline__ uint4 gload16u(const uint8_t* p) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Realigned 16-byte loads for a wave whose lanes read consecutive 16-byte pieces of a row (lane
+// l + 1 at lane l's address + 16): a lane's upper aligned word is its right neighbour's lower
+// one, so it is taken by one DPP wave shift instead of a second load.  Issue first (addresses
+// shared by DPP before any load: the loads a lane still needs -- lane 63, a lane whose
+// neighbour is inactive or elsewhere -- go out with the others), finish after.  Issue and
+// finish must run with the same lanes active.
+struct ULoad {
+    uint4 lo, hi;
+    uint32_t bs;
+    bool own;
+};
+__device__ __forceinline__ uint32_t dpp_from_next(uint32_t x, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x130, 0xF, 0xF, false);  // wave_shl:1
+}
+__device__ __forceinline__ void uload_issue(ULoad& u, const uint8_t* p) {
+    u.bs = (uint32_t)(uintptr_t)p & 15u;
+    const uint8_t* a = p - u.bs;
+    const uint64_t ai = (uint64_t)(uintptr_t)a;
+    const uint64_t na = (uint64_t)dpp_from_next((uint32_t)ai, 0u) |
+                        ((uint64_t)dpp_from_next((uint32_t)(ai >> 32), 0u) << 32);
+    u.own = u.bs != 0 && na != ai + 16;
+    u.lo = gload16(a);
+    u.hi = u.lo;
+    if (u.own) u.hi = gload16(a + 16);
+}
+__device__ __forceinline__ uint4 uload_finish(const ULoad& u) {
+    const uint4 nlo = make_uint4(dpp_from_next(u.lo.x, 0u), dpp_from_next(u.lo.y, 0u),
+                                 dpp_from_next(u.lo.z, 0u), dpp_from_next(u.lo.w, 0u));
+    const uint4 hi = u.own ? u.hi : nlo;
+    uint32_t w[4];
+    funnel16(u.lo, hi, u.bs, w);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 }  // namespace pbx

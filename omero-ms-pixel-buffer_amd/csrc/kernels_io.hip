@@ -18,6 +18,15 @@
 
 namespace pbx {
 
+// The tile of a workgroup: the scalar binary search (descriptor keys through the scalar cache)
+// or, with -DPBX_IO_WAVE_SEARCH, the 64-probe wave search (upper_index_wave: 2 rounds of
+// vector gathers for 4096 tiles) -- measured slower (profiles/r06f/).
+#ifdef PBX_IO_WAVE_SEARCH
+#define PBX_IO_UPPER_INDEX upper_index_wave
+#else
+#define PBX_IO_UPPER_INDEX upper_index
+#endif
+
 // ------------------------------------------------------------------- synthetic planes
 // Rows [y0, y0 + rows) of the plane (a row band, or the whole plane), row y0 at `out`.
 __global__ __launch_bounds__(256) void k_gen_plane(uint8_t* __restrict__ out, int64_t pitch,
@@ -137,7 +146,7 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
 __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft, uint32_t nft,
                                                  uint8_t* __restrict__ out) {
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t ti = upper_index_wave(nft, b, [&](uint32_t i) { return ft[i].blk_first; });
+    const uint32_t ti = PBX_IO_UPPER_INDEX(nft, b, [&](uint32_t i) { return ft[i].blk_first; });
     const TileDesc d = ft[ti];
     const uint32_t rb = (uint32_t)d.w * (uint32_t)d.bpp;
     const uint32_t r0 = (b - d.blk_first) * d.rows_per_blk;
@@ -187,22 +196,45 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
         // block's run share an output word with the neighbouring block: written singly.
         const uint32_t f0 = r0 * rb, f1 = r1 * rb;
         const uint32_t w0 = (f0 + 15) >> 4, w1 = f1 >> 4;
-        for (uint32_t wi = w0 + tid; wi < w1; wi += 256) {
-            const uint32_t o = wi << 4, r = o / rb, c = o - r * rb, n1 = rb - c;
-            uint4 q = gload16u(src0 + (int64_t)r * d.pitch + c);
-            if (n1 < 16) {  // the word runs into row r + 1
-                const uint4 q2 = gload16u(src0 + (int64_t)(r + 1) * d.pitch - n1);
-                auto keep = [&](uint32_t j) {  // bytes of word j that come from row r
-                    return n1 >= 4 * j + 4 ? 0xFFFFFFFFu : n1 <= 4 * j ? 0u : (1u << (8 * (n1 - 4 * j))) - 1u;
-                };
-                const uint32_t m0 = keep(0), m1 = keep(1), m2 = keep(2), m3 = keep(3);
-                q.x = (q.x & m0) | (q2.x & ~m0);
-                q.y = (q.y & m1) | (q2.y & ~m1);
-                q.z = (q.z & m2) | (q2.z & ~m2);
-                q.w = (q.w & m3) | (q2.w & ~m3);
+        // EXTU_U words per thread in flight; a lane's upper source word comes from its right
+        // neighbour (uload_*), the second row's part of a row-crossing word by its own loads
+#ifndef PBX_EXTU_U
+#define PBX_EXTU_U 2
+#endif
+        constexpr uint32_t U = PBX_EXTU_U;
+        for (uint32_t wb = w0 + tid; wb < w1; wb += 256 * U) {
+            ULoad a[U];
+            uint4 q2[U];
+            uint32_t n1[U];
+#pragma unroll
+            for (uint32_t k = 0; k < U; k++) {
+                const uint32_t wi = wb + 256 * k;
+                if (wi >= w1) break;  // (the lanes past the end leave the later rounds together)
+                const uint32_t o = wi << 4, r = o / rb, c = o - r * rb;
+                n1[k] = rb - c;
+                uload_issue(a[k], src0 + (int64_t)r * d.pitch + c);
+                // the word runs into row r + 1: loaded from n1 bytes before that row's start
+                if (n1[k] < 16) q2[k] = gload16u(src0 + (int64_t)(r + 1) * d.pitch - n1[k]);
             }
-            if (swap) q = swap16(q, d.bpp);
-            gstore16(base + o, q);
+#pragma unroll
+            for (uint32_t k = 0; k < U; k++) {
+                const uint32_t wi = wb + 256 * k;
+                if (wi >= w1) break;
+                uint4 q = uload_finish(a[k]);
+                if (n1[k] < 16) {
+                    const uint32_t n = n1[k];
+                    auto keep = [&](uint32_t j) {  // bytes of word j that come from row r
+                        return n >= 4 * j + 4 ? 0xFFFFFFFFu : n <= 4 * j ? 0u : (1u << (8 * (n - 4 * j))) - 1u;
+                    };
+                    const uint32_t m0 = keep(0), m1 = keep(1), m2 = keep(2), m3 = keep(3);
+                    q.x = (q.x & m0) | (q2[k].x & ~m0);
+                    q.y = (q.y & m1) | (q2[k].y & ~m1);
+                    q.z = (q.z & m2) | (q2[k].z & ~m2);
+                    q.w = (q.w & m3) | (q2[k].w & ~m3);
+                }
+                if (swap) q = swap16(q, d.bpp);
+                gstore16(base + (wi << 4), q);
+            }
         }
         const uint32_t h_end = f1 < (w0 << 4) ? f1 : (w0 << 4);
         const uint32_t t_beg = (w1 << 4) > h_end ? (w1 << 4) : h_end;
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                                                 uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = PBX_IO_UPPER_INDEX(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t r0 = (b - d.blk_first) * FB_ROWS;
     const uint32_t r1 = r0 + FB_ROWS < (uint32_t)d.h ? r0 + FB_ROWS : (uint32_t)d.h;
@@ -296,15 +328,14 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
         for (uint32_t i = tid; i < nq * nc; i += 256) {
             const uint32_t q = i / nc, c = i - q * nc;
             const int64_t row = (int64_t)r0 - 1 + q;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (row >= 0 && png) {
-                v = gload16u(src0 + row * d.pitch + 16 * c);
-                if (swap) v = swap16(v, bpp);
-                if (flip) v = flip_msb(v, bpp);
-            } else if (row >= 0) {
-                v = gload16u(src0 + row * d.pitch + 16 * c);
-                if (swap) v = swap16(v, bpp);
-            }
+            // (every lane loads -- the row above the tile's first row from row 0, then zeroed --
+            // so the realigned loads can share words between neighbouring lanes)
+            ULoad u;
+            uload_issue(u, src0 + (row >= 0 ? row : 0) * d.pitch + 16 * c);
+            uint4 v = uload_finish(u);
+            if (swap) v = swap16(v, bpp);
+            if (png && flip) v = flip_msb(v, bpp);
+            if (row < 0) v = make_uint4(0, 0, 0, 0);
             *(uint4*)(sm + q * rbp + 16 * c) = v;
         }
         __syncthreads();
@@ -520,7 +551,7 @@ __global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt,
                                                 uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lrow[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = PBX_IO_UPPER_INDEX(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t fb = (d.flags & TF_PNGROWS) ? 1u : 0u;
     const uint32_t rowlen = d.rowlen, rb = rowlen - fb, bpp = d.bpp;
@@ -534,8 +565,10 @@ __global__ __launch_bounds__(RB_NT) void k_rows(const TileDesc* __restrict__ dt,
     uint32_t* rows = lrow + 4;
     for (uint32_t i = tid; i < nr * nc; i += RB_NT) {
         const uint32_t q = i / nc, c = i - q * nc;
-        // (source rows of any alignment: gload16u realigns; 16 c is a sample boundary)
-        uint4 v = gload16u(src0 + (int64_t)q * d.pitch + 16 * c);
+        // (source rows of any alignment: realigned loads; 16 c is a sample boundary)
+        ULoad u;
+        uload_issue(u, src0 + (int64_t)q * d.pitch + 16 * c);
+        uint4 v = uload_finish(u);
         if (swap) v = swap16(v, (int)bpp);
         if (flip) v = flip_msb(v, (int)bpp);
         *(uint4*)(rows + q * rw + 4 * c) = v;
@@ -702,7 +735,7 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
                                                   uint32_t rbq_max, uint8_t* __restrict__ stream) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t ti = upper_index_wave(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
+    const uint32_t ti = PBX_IO_UPPER_INDEX(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
     const uint32_t r0 = (b - d.blk_first) * F2_ROWS;
     const uint32_t nr = (uint32_t)d.h - r0 < F2_ROWS ? (uint32_t)d.h - r0 : F2_ROWS;

@@ -394,6 +394,12 @@ struct pbx_ctx {
     hipEvent_t stage_ev[4][4] = {};     // [stream][stage]
     std::atomic<int> last_ks{-1};       // stream of the last overlapped deflate batch
     hipStream_t copy_stream = nullptr;  // D2H of finished batches, overlapping later kernels
+    // Pipelined batches holding both raw / TIFF tiles and deflate tiles run their HBM-bound
+    // k_extract on this stream, beside their own (and the previous batch's) issue-bound deflate
+    // chain on the kernel stream; consecutive batches' extracts stay in order here.
+    // $PBX_SPLIT_EXTRACT=0: one stream per batch, as before.
+    hipStream_t xstream = nullptr;
+    bool split_extract = true;
     hipStream_t upload_stream = nullptr;  // H2D of plane rows (pbx_plane_write_rows / register)
     std::mutex reg_mu;   // plane registry
     std::mutex run_mu;   // plan + launch of one batch at a time on the stream
@@ -448,6 +454,10 @@ hipError_t sync_kernel_streams(pbx_ctx* ctx) {
         const hipError_t e = hipStreamSynchronize(k ? ctx->kstream[k] : ctx->stream);
         if (r == hipSuccess) r = e;
     }
+    if (ctx->xstream) {
+        const hipError_t e = hipStreamSynchronize(ctx->xstream);
+        if (r == hipSuccess) r = e;
+    }
     return r;
 }
 
@@ -489,6 +499,11 @@ struct pbx_batch {
     std::chrono::steady_clock::time_point t_done;  // the fetch saw the kernels complete (PBX_TIMELINE)
     // start, H2D, extract, filter, lz77, huff, offsets, encode, frame
     hipEvent_t ev[9] = {};
+    // split launches (pbx_ctx::xstream): the extract kernel's completion on xstream (sync
+    // event, recorded twice: descriptors uploaded on the kernel stream, then extract done) and
+    // the kernel stream's own start of the row kernels (timing: ms_filter)
+    bool split = false;
+    hipEvent_t ev_x = nullptr, ev_fs = nullptr;
     // lite: a batch of the serving path (fetched by the coalescer) records only the events its
     // spans need (start, after the extract kernel, before k_frame, end): every event record is
     // a marker packet that costs the device a few microseconds between two kernels
@@ -1381,6 +1396,8 @@ int pbx_init(const pbx_config* cfg_in, pbx_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking);
+    if (const char* sx = getenv("PBX_SPLIT_EXTRACT")) ctx->split_extract = atoi(sx) != 0;
     if (const char* hb = getenv("PBX_HBM_BUDGET_MB")) ctx->budget = (uint64_t)strtoull(hb, nullptr, 10) << 20;
     if (const char* ks = getenv("PBX_KSTREAMS")) ctx->nks = std::min(4, std::max(1, atoi(ks)));
     else ctx->nks = 3;
@@ -1438,6 +1455,7 @@ void pbx_shutdown(pbx_ctx* ctx) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
+    if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
     if (ctx->stall_flag) (void)hipHostFree(ctx->stall_flag);
     delete ctx;
 }
@@ -2848,9 +2866,22 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
                                      (size_t)(r1 - r0), hipMemcpyDeviceToDevice, st));
         }
     }
-    if (fine) HIP_TRY(hipEventRecord(b->ev[1], st));
-    HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
-    if (fine || nft) HIP_TRY(hipEventRecord(b->ev[2], st));
+    b->split = multi && nft && ndt && ctx->split_extract;
+    if (b->split) {  // k_extract on xstream, once the descriptors (and bridges) are up
+        if (!b->ev_x) HIP_TRY(ctx->evpool_sync.get(&b->ev_x));
+        if (!b->ev_fs) HIP_TRY(ctx->evpool.get(&b->ev_fs));
+        HIP_TRY(hipEventRecord(b->ev_x, st));
+        HIP_TRY(hipStreamWaitEvent(ctx->xstream, b->ev_x, 0));
+        HIP_TRY(hipEventRecord(b->ev[1], ctx->xstream));
+        HIP_TRY(launch_extract(ctx->xstream, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
+        HIP_TRY(hipEventRecord(b->ev[2], ctx->xstream));
+        HIP_TRY(hipEventRecord(b->ev_x, ctx->xstream));
+        HIP_TRY(hipEventRecord(b->ev_fs, st));
+    } else {
+        if (fine) HIP_TRY(hipEventRecord(b->ev[1], st));
+        HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
+        if (fine || nft) HIP_TRY(hipEventRecord(b->ev[2], st));
+    }
     const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;
     HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
@@ -2899,6 +2930,7 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
     } else {
         for (int k = fine ? 4 : 7; k < 8; k++) HIP_TRY(hipEventRecord(b->ev[k], st));
     }
+    if (b->split) HIP_TRY(hipStreamWaitEvent(st, b->ev_x, 0));  // the batch ends when both are done
     HIP_TRY(launch_tiff_tiled(st, (const TiledHdr*)b->d_th, nth, (uint8_t*)b->d_fixed, (const uint64_t*)b->d_offs,
                               (uint8_t*)b->d_png));
     if (fetch_follows && ndt) {
@@ -2964,7 +2996,12 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
             out = ms;
             return PBX_OK;
         };
-        if (el(1, 2, s->ms_extract) || el(2, 3, s->ms_filter) || el(3, 7, s->ms_deflate) ||
+        if (b->split) {  // the row kernels start on the kernel stream at ev_fs
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, b->ev_fs, b->ev[3]));
+            s->ms_filter = ms;
+        }
+        if (el(1, 2, s->ms_extract) || (!b->split && el(2, 3, s->ms_filter)) || el(3, 7, s->ms_deflate) ||
             el(7, 8, s->ms_assemble) || el(0, 8, s->ms_total) || el(3, 4, s->ms_lz77) ||
             el(4, 5, s->ms_huff) || el(6, 7, s->ms_encode))
             return PBX_E_INTERNAL;
@@ -3066,6 +3103,7 @@ int pbx_batch_fetch(pbx_ctx* ctx, pbx_batch* b, pbx_result* out) {
             if ((q == 0 && !ext) || (q == 2 && b->lite)) continue;
             (void)hipEventElapsedTime(&ms[q], b->ev[ij[q][0]], b->ev[ij[q][1]]);
         }
+        if (b->split) (void)hipEventElapsedTime(&ms[1], b->ev_fs, b->ev[3]);  // (extract on xstream)
         pbx_spans& sp = hb->spans;
         sp.get_tile_direct_ms = ms[0];
         sp.write_image_ms = (double)ms[1] + ms[2];
@@ -3124,6 +3162,8 @@ void pbx_batch_destroy(pbx_ctx* ctx, pbx_batch* b) {
     free_batch_device(ctx, b);
     for (auto& e : b->ev) ctx->evpool.put(e);
     ctx->evpool_sync.put(b->ev_copy);
+    ctx->evpool_sync.put(b->ev_x);
+    ctx->evpool.put(b->ev_fs);
     delete b;
 }
 

@@ -14,6 +14,7 @@
 #   parity   the output-parity suites alone
 #   kstats   rocprofv3 kernel averages of a short headline run
 #   raw      k_extract alone (scripts/raw_probe.py), aligned / unaligned, PBX_EXT_BLK 16-64 KiB
+#   hwq      the headline and configs[4] under GPU_MAX_HW_QUEUES 4 / 8 / 16
 #   c5       configs[4]'s pass alone (scripts/c5_pass.py) and its rocprofv3 kernel trace
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
 # Every GPU step has its own time limit; the first failure ends the call.
@@ -105,16 +106,30 @@ for stage in "$@"; do
       find $O/kprof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_short.csv \;
       cut -d, -f1-4 $O/kernel_stats_short.csv | head -12 ;;
     raw)  # k_extract alone, aligned and unaligned, at several workgroup sizes
-      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
+      for i in 1 2; do for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
         for eb in ${EXT_BLKS:-16384 32768 65536}; do
           echo "-- $L"
           PBX_LIB=$PWD/$L PBX_EXT_BLK=$eb timeout -k 10 200 python -u scripts/raw_probe.py 5 > $O/raw.log 2>&1 || { tail -20 $O/raw.log; exit 1; }
           cat $O/raw.log
         done
+      done; done ;;
+    hwq)  # hardware queues per process (GPU_MAX_HW_QUEUES): the headline and configs[4] at 4 / 8 / 16
+      for q in 4 8 16 4 8; do
+        GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-extra --no-cpu-baseline > $O/hwq.json 2> $O/hwq.err || { tail -20 $O/hwq.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/hwq.json')); print('hwq $q headline', d['value'], d['ms_per_step'], d['kernel_streams']['serial_pass_tiles_per_s'])"
+        GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python -u scripts/c5_pass.py 2 > $O/hwq_c5.log 2>&1 || { tail -20 $O/hwq_c5.log; exit 1; }
+        echo "hwq $q c5: $(grep 'pass 1' $O/hwq_c5.log)"
       done ;;
     c5)
-      timeout -k 10 300 python -u scripts/c5_pass.py 3 > $O/c5_pass.log 2>&1 || { tail -20 $O/c5_pass.log; exit 1; }
+      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
+        echo "-- $L"
+        PBX_LIB=$PWD/$L timeout -k 10 300 python -u scripts/c5_pass.py 3 > $O/c5_pass.log 2>&1 || { tail -20 $O/c5_pass.log; exit 1; }
+        cat $O/c5_pass.log
+      done
+      echo "-- product, PBX_SPLIT_EXTRACT=0"
+      PBX_SPLIT_EXTRACT=0 timeout -k 10 300 python -u scripts/c5_pass.py 3 > $O/c5_pass.log 2>&1 || { tail -20 $O/c5_pass.log; exit 1; }
       cat $O/c5_pass.log
+      timeout -k 10 300 python -u scripts/c5_pass.py 3 > $O/c5_pass.log 2>&1 || { tail -20 $O/c5_pass.log; exit 1; }
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c5prof -o run --output-format csv -- python3 scripts/c5_pass.py 1 > $O/c5_prof.log 2>&1 || { tail -20 $O/c5_prof.log; exit 1; }
       find $O/c5prof -name "*kernel_stats.csv" -exec cp {} $O/c5_kernel_stats.csv \;
       cut -d, -f1-4 $O/c5_kernel_stats.csv | head -16 ;;

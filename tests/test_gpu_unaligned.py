@@ -122,3 +122,53 @@ def test_unaligned_full_size_tiles(oracle):
             assert r == 0 and idat == stream, (pt, x, y, w, h)
         else:
             assert body == obody, (pt, x, y, w, h, fmt)
+
+
+def test_pipelined_mixed_batches_split_extract(oracle):
+    """Pipelined device-resident batches (pbx_batch_launch: the bench's form) that hold raw /
+    TIFF tiles next to PNG tiles run their k_extract on the context's extract stream beside
+    the deflate chain (runtime.cpp pbx_ctx::xstream); four such batches in flight at once,
+    every response against the oracle."""
+    side = 4096
+    rng = np.random.default_rng(67)
+    with pbx.PixelsService() as svc:
+        host, ids = {}, {}
+        for pt in (pbx.UINT8, pbx.INT32, pbx.FLOAT):
+            ids[pt] = next(_ids)
+            svc.register_plane(ids[pt], 0, 0, 0, pt, side, side, generator="noise", seed=0)
+            host[pt] = oracle.gen_region(2, pt, 0, 0, side, side)
+        batches = []
+        for _ in range(4):
+            ctxs, meta = [], []
+            for k in range(96):
+                pt = (pbx.UINT8, pbx.INT32, pbx.FLOAT)[int(rng.integers(3))]
+                w, h = int(rng.integers(1, 5)) * 256, int(rng.integers(1, 5)) * 256
+                x, y = int(rng.integers(0, side - w + 1)), int(rng.integers(0, side - h + 1))
+                fmt = (None, "tif", "png")[int(rng.integers(3))]
+                ctxs.append(pbx.TileCtx(ids[pt], 0, 0, 0, x, y, w, h, format=fmt))
+                meta.append((pt, x, y, w, h, fmt))
+            batches.append((pbx.Batch(svc, ctxs), meta))
+        for b, _ in batches:  # all four launched before any is waited for
+            b.launch()
+        results = []
+        for b, meta in batches:
+            b.sync()
+            results.append((b.fetch(), meta))
+            b.close()
+    n = 0
+    for res, meta in results:
+        for (pt, x, y, w, h, fmt), (st, body) in zip(meta, res):
+            fcode = {None: oracle.FMT_RAW, "png": oracle.FMT_PNG, "tif": oracle.FMT_TIF}[fmt]
+            ost, obody, _, _ = oracle.get_tile(host[pt], True, pt, side, side, x, y, w, h, fcode)
+            assert st == (pbx.OK if ost == 0 else ost), (pt, x, y, w, h, fmt)
+            if st != pbx.OK:
+                continue
+            n += 1
+            if fmt == "png":
+                tile = oracle.extract_be(host[pt], True, pt, side * oracle.BPP[pt], x, y, w, h)
+                stream = oracle.png_filter_stream(tile, pt, w, h, 0).tobytes()
+                r, idat = oracle.png_inflate_idat(body, len(stream))
+                assert r == 0 and idat == stream, (pt, x, y, w, h)
+            else:
+                assert body == obody, (pt, x, y, w, h, fmt)
+    assert n > 250
