@@ -101,6 +101,10 @@ struct Band {
     int32_t writers = 0;         // pbx_band_write calls in flight
     bool failed = false;         // BS_LOADING: a write failed; the last writer out resets the band
     int64_t touched = 0;         // BS_LOADING: mono_ns of the last write activity
+    // the last load went idle past stale_ns and was reset: the next load must start at the
+    // band's first row, so a late piece of the reset load fails instead of starting a load
+    // that could never complete
+    bool stale_reset = false;
     std::vector<uint8_t> rows_done;
 };
 
@@ -703,6 +707,7 @@ bool evict_one_locked(pbx_ctx* ctx, std::vector<std::pair<void*, size_t>>& to_fr
     ctx->evicted_bytes += bytes;
     *dev = nullptr;
     if (vb) {
+        if (vb->state == BS_LOADING) vb->stale_reset = true;  // (a stale load: see Band)
         vb->state = BS_ABSENT;
         vb->rows_done.clear();
         vb->failed = false;
@@ -1880,9 +1885,17 @@ int band_write(pbx_ctx* ctx, Plane* q, int32_t y0, int32_t rows, const void* dat
         std::lock_guard<std::mutex> g(ctx->reg_mu);
         if (b.state == BS_READY) return fail(PBX_E_EXISTS, "band %d is resident", k);
         // a load that failed part-way, or whose loader went away, starts over
-        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || mono_ns() - b.touched > ctx->stale_ns))
+        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || mono_ns() - b.touched > ctx->stale_ns)) {
+            if (!b.failed) b.stale_reset = true;
             band_reset_locked(b, stale);
+        }
+        if (b.state == BS_ABSENT && b.stale_reset && y0 != lo) {
+            free_planes_locked(ctx, stale);
+            return fail(PBX_E_INTERNAL, "band %d: its load was idle for more than %lld ms and was reset; "
+                        "write it again from row %d", k, (long long)(ctx->stale_ns / 1000000), lo);
+        }
         if (b.state == BS_ABSENT) {
+            b.stale_reset = false;
             b.state = BS_LOADING;
             b.failed = false;
             b.rows_done.assign((size_t)(hi - lo), 0);
@@ -2008,8 +2021,10 @@ int pbx_plane_band_info(pbx_ctx* ctx, uint64_t id, int32_t* band_rows, int32_t* 
     std::vector<std::pair<void*, size_t>> stale;
     const int64_t now = mono_ns();
     for (Band& b : p->bands)
-        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || now - b.touched > ctx->stale_ns))
+        if (b.state == BS_LOADING && b.writers == 0 && (b.failed || now - b.touched > ctx->stale_ns)) {
+            if (!b.failed) b.stale_reset = true;
             band_reset_locked(b, stale);
+        }
     free_planes_locked(ctx, stale);
     if (band_rows) *band_rows = p->sparse_rows;
     if (nbands) *nbands = (int32_t)p->bands.size();

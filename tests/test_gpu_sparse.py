@@ -313,3 +313,23 @@ def test_band_load_failures_give_the_band_back(oracle, monkeypatch):
         svc.band_write(pid, 1536, 512, _rows(oracle, sx, 1536, 512))
         tile_ok(1700)
         assert svc.band_info(pid)[1] == [2, 2, 2, 2]
+
+        # (5) ADVICE r05: a live loader whose pieces come more than the stale time apart has its
+        # load reset under it; its next piece fails (500, load again from the band's first row)
+        # instead of silently starting a load that could never complete
+        pid2 = svc.create_sparse_plane(next(_ids), 0, 0, 0, pbx.UINT16, sx, 1024, B)
+        svc.band_write(pid2, 0, 100, _rows(oracle, sx, 0, 100))
+        time.sleep(0.5)
+        with pytest.raises(pbx.PbxError) as ei:
+            svc.band_write(pid2, 100, 412, _rows(oracle, sx, 100, 412))
+        assert ei.value.status == pbx.E_INTERNAL
+        assert svc.band_info(pid2)[1] == [0, 0]
+        # the same after band_info did the reset: a piece past the first row still fails
+        svc.band_write(pid2, 512, 64, _rows(oracle, sx, 512, 64))
+        time.sleep(0.5)
+        assert svc.band_info(pid2)[1] == [0, 0]
+        with pytest.raises(pbx.PbxError):
+            svc.band_write(pid2, 576, 448, _rows(oracle, sx, 576, 448))
+        svc.band_write(pid2, 512, 512, _rows(oracle, sx, 512, 512))  # from the first row: loads
+        svc.band_write(pid2, 0, 512, _rows(oracle, sx, 0, 512))
+        assert svc.band_info(pid2)[1] == [2, 2]
