@@ -143,6 +143,11 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
 }
 
 // ------------------------------------------------------------------------ extraction
+// UA: the batch holds regions whose rows are not whole 16-byte words at 16-byte aligned
+// sources (the host knows: x * bpp and w * bpp mod 16); without them the kernel is the aligned
+// path alone (22 VGPRs instead of 54: configs[3]'s all-aligned pass read 5.29 TB/s with the
+// unaligned path compiled in, 5.48 without, profiles/r06j/).
+template <bool UA>
 __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft, uint32_t nft,
                                                  uint8_t* __restrict__ out) {
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
                 gstore16(base + (size_t)r * rb + 16 * v, q[k]);
             }
         }
-    } else if (!d.vw && rb >= 16) {
+    } else if (UA && !d.vw && rb >= 16) {
         // Any other region (x * bpp not a multiple of 16, or rows of a length that is not): the
         // output is one contiguous run of (r1 - r0) * rb bytes at a 16-byte aligned base, so
         // every whole 16-byte output word of this block is built from 16 source bytes loaded
@@ -492,9 +497,15 @@ hipError_t launch_gen_plane(hipStream_t st, uint8_t* out, int64_t pitch, int32_t
 }
 
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                          uint32_t nblocks, uint8_t* out) {
+                          uint32_t nblocks, uint8_t* out, bool unaligned) {
     if (!ntiles || !nblocks) return hipSuccess;
-    hipLaunchKernelGGL(k_extract, dim3(nblocks), dim3(256), 0, st, d_tiles, ntiles, out);
+#ifdef PBX_EXT_ALWAYS_UA  // A/B: every batch through the instantiation with the unaligned path
+    unaligned = true;
+#endif
+    if (unaligned)
+        hipLaunchKernelGGL(k_extract<true>, dim3(nblocks), dim3(256), 0, st, d_tiles, ntiles, out);
+    else
+        hipLaunchKernelGGL(k_extract<false>, dim3(nblocks), dim3(256), 0, st, d_tiles, ntiles, out);
     return hipGetLastError();
 }
 
@@ -873,17 +884,26 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // row's tail and the filter byte.  That word needs the previous row's filtered tail, so a run
 // also filters the row before it (without storing it): 1/run extra reads, no cross-wave
 // hand-off.
+// Rows a wave filters, per filter.  Round 6 (profiles/r06j/): a fixed filter's wave loads its
+// whole run (and the row before it) at once -- a ring of run + 1 row buffers, no load waits
+// behind a filtered row -- and exits, like k_extract's workgroups: Sub / Up / Avg 0.59-0.62 ->
+// 0.64 of HBM peak with runs of 24 rows (100 VGPRs of rows, three waves per SIMD), Paeth
+// 0.60 -> 0.625 with runs of 12 (its forms need more registers a row); the adaptive choice
+// keeps its 5-row ring over 32-row runs (the short-run forms spill it: 0.47-0.53).
 #ifndef PBX_F3_RUN
-#define PBX_F3_RUN 32  // rows a wave filters (Sub, Up, adaptive)
+#define PBX_F3_RUN 24  // Sub, Up, Avg
 #endif
-#ifndef PBX_F3_RUN_AP
-#define PBX_F3_RUN_AP 16  // Avg and Paeth: shorter runs, more waves in flight (profiles/r05zi/)
+#ifndef PBX_F3_RUN_P
+#define PBX_F3_RUN_P 12  // Paeth
+#endif
+#ifndef PBX_F3_RUN_AD
+#define PBX_F3_RUN_AD 32  // adaptive
 #endif
 #ifndef PBX_F3_NTS
 #define PBX_F3_NTS 0
 #endif
 __host__ __device__ constexpr uint32_t f3_run_rows(uint32_t filter) {
-    return filter == 3 || filter == 4 ? PBX_F3_RUN_AP : PBX_F3_RUN;
+    return filter == 4 ? PBX_F3_RUN_P : filter == 5 ? PBX_F3_RUN_AD : PBX_F3_RUN;
 }
 // stream stores: nontemporal (the stream is re-read only by the next kernel, from HBM anyway)
 __device__ __forceinline__ void f3_store(uint8_t* p, const uint4& v) {
@@ -900,12 +920,9 @@ constexpr uint32_t F3_NT = 256;
 #ifndef PBX_F3_NB
 #define PBX_F3_NB 0
 #endif
-#ifndef PBX_F3_NB_SIMPLE
-#define PBX_F3_NB_SIMPLE 6  // Sub / Up / Avg rows (fewest registers per row)
-#endif
 template <uint32_t G, uint32_t FT>
-constexpr uint32_t F3_NB() {
-    return PBX_F3_NB ? PBX_F3_NB : G == 1 ? (FT == 5 ? 5 : FT == 4 ? 6 : PBX_F3_NB_SIMPLE) : 4;
+constexpr uint32_t F3_NB() {  // fixed filters, rows <= 1 KiB: the whole run and the row before it
+    return PBX_F3_NB ? PBX_F3_NB : G == 1 ? (FT == 5 ? 5 : f3_run_rows(FT) + 1) : 4;
 }
 
 // Sum over the wave: row prefix sums (row_shr, zero shifted in), then row_bcast:15 / :31 carry

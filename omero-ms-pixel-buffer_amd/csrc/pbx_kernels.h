@@ -24,7 +24,7 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
 // 100 MHz constant clock
 hipError_t launch_stall(hipStream_t st, const uint32_t* flag, uint64_t limit_ticks);
 hipError_t launch_extract(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles,
-                          uint32_t nblocks, uint8_t* out);
+                          uint32_t nblocks, uint8_t* out, bool unaligned);
 // Tiled-TIFF headers (IFD + TileOffsets/TileByteCounts), one workgroup per response: after
 // k_extract for uncompressed responses (in `fixed`), after k_frame for deflate ones (`zout`).
 hipError_t launch_tiff_tiled(hipStream_t st, const TiledHdr* d_th, uint32_t nth, uint8_t* fixed,

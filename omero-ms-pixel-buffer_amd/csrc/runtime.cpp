@@ -483,6 +483,7 @@ struct pbx_batch {
     std::vector<TiledHdr> th;              // tiled-TIFF responses (their sub-tiles carry TF_TILED)
     std::vector<uint32_t> th_req;
     uint32_t ext_blocks = 0, nseg = 0, nblk = 0, filt_blocks = 0;
+    bool ext_unaligned = false;  // some k_extract tile is not whole aligned 16-byte words (k_extract<true>)
     // dt = [direct tiles | k_rows tiles | k_filter2 tiles | k_filter3 tiles | k_filter tiles |
     //       tiled-TIFF sub-tiles]
     uint32_t ndirect_tiles = 0, nrows_tiles = 0, rows_blocks = 0, rows_max_rb = 0;
@@ -936,6 +937,13 @@ void free_batch_device(pbx_ctx* ctx, pbx_batch* b) {
 }
 
 }  // namespace
+
+// k_extract's aligned path takes the tile: no padding, and its rows start and end on 16-byte
+// words (plane and bridge rows are 256-aligned and keep a region's column alignment, fixed
+// arena offsets are 16-byte aligned)
+static bool ext_aligned(const TileDesc& d) {
+    return !d.vw && ((int64_t)d.x * d.bpp) % 16 == 0 && ((int64_t)d.w * d.bpp) % 16 == 0;
+}
 
 // Rows of one k_extract workgroup: about this many bytes ($PBX_EXT_BLK, default 16 KiB).
 static uint32_t ext_blk_bytes() {
@@ -2659,6 +2667,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                         b->ext_blocks += (T + s.rows_per_blk - 1) / s.rows_per_blk;
                         s.out_off = th.off + D + k * sub;
                         b->ft.push_back(s);
+                        b->ext_unaligned |= !ext_aligned(s);
                         b->ft_req.push_back((uint32_t)i);
                     } else {
                         s.filter = 0;
@@ -2682,6 +2691,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
             d.out_off = b->fixed_bytes;
             b->fixed_bytes += ((r.format == PBX_FMT_TIF ? TIFF_DATA_OFFSET : 0) + tile_bytes + 255) & ~255ull;
             b->ft.push_back(d);
+            b->ext_unaligned |= !ext_aligned(d);
             b->ft_req.push_back((uint32_t)i);
         } else {
             if (r.format == PBX_FMT_PNG) {
@@ -2888,13 +2898,15 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
         HIP_TRY(hipEventRecord(b->ev_x, st));
         HIP_TRY(hipStreamWaitEvent(ctx->xstream, b->ev_x, 0));
         HIP_TRY(hipEventRecord(b->ev[1], ctx->xstream));
-        HIP_TRY(launch_extract(ctx->xstream, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
+        HIP_TRY(launch_extract(ctx->xstream, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed,
+                                b->ext_unaligned));
         HIP_TRY(hipEventRecord(b->ev[2], ctx->xstream));
         HIP_TRY(hipEventRecord(b->ev_x, ctx->xstream));
         HIP_TRY(hipEventRecord(b->ev_fs, st));
     } else {
         if (fine) HIP_TRY(hipEventRecord(b->ev[1], st));
-        HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed));
+        HIP_TRY(launch_extract(st, (const TileDesc*)b->d_ft, nft, b->ext_blocks, (uint8_t*)b->d_fixed,
+                                b->ext_unaligned));
         if (fine || nft) HIP_TRY(hipEventRecord(b->ev[2], st));
     }
     const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;

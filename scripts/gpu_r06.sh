@@ -15,6 +15,7 @@
 #   kstats   rocprofv3 kernel averages of a short headline run
 #   raw      k_extract alone (scripts/raw_probe.py), aligned / unaligned, PBX_EXT_BLK 16-64 KiB
 #   hwq      the headline and configs[4] under GPU_MAX_HW_QUEUES 4 / 8 / 16
+#   c4       configs[3]'s TIFF pass on one channel (scripts/c4_probe.py), product vs AB_LIBS
 #   c5       configs[4]'s pass alone (scripts/c5_pass.py) and its rocprofv3 kernel trace
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
 # Every GPU step has its own time limit; the first failure ends the call.
@@ -68,11 +69,11 @@ for stage in "$@"; do
       PROBE_KSTREAMS=3 timeout -k 10 300 python -u scripts/subbatch_probe.py 5 > $O/subbatch3.log 2>&1 || { tail -30 $O/subbatch3.log; exit 1; }
       tail -6 $O/subbatch3.log ;;
     fvar)
-      for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_f3*/libpbx.so; do
+      for i in 1 2; do for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_f3*/libpbx.so; do
         echo "-- $L"
-        PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/filter_bench.py 1 2 4 5 > $O/fvar.log 2>&1 || { tail -20 $O/fvar.log; exit 1; }
+        PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/filter_bench.py ${FILTERS:-1 2 3 4 5} > $O/fvar.log 2>&1 || { tail -20 $O/fvar.log; exit 1; }
         cat $O/fvar.log
-      done ;;
+      done; done ;;
     cvar)
       for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_*/libpbx.so; do
         case $L in *var_f3*) continue ;; esac
@@ -120,6 +121,12 @@ for stage in "$@"; do
         GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python -u scripts/c5_pass.py 2 > $O/hwq_c5.log 2>&1 || { tail -20 $O/hwq_c5.log; exit 1; }
         echo "hwq $q c5: $(grep 'pass 1' $O/hwq_c5.log)"
       done ;;
+    c4)  # configs[3]'s TIFF pass on one channel, the product library and AB_LIBS, twice
+      for i in 1 2; do for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
+        echo "-- $L"
+        PBX_LIB=$PWD/$L timeout -k 10 300 python -u scripts/c4_probe.py > $O/c4.log 2>&1 || { tail -20 $O/c4.log; exit 1; }
+        cat $O/c4.log
+      done; done ;;
     c5)
       for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
         echo "-- $L"
