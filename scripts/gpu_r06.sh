@@ -70,6 +70,7 @@ for stage in "$@"; do
       tail -6 $O/subbatch3.log ;;
     fvar)
       for i in 1 2; do for L in omero-ms-pixel-buffer_amd/lib/libpbx.so omero-ms-pixel-buffer_amd/lib/var_f3*/libpbx.so; do
+        [ -f "$L" ] || continue
         echo "-- $L"
         PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/filter_bench.py ${FILTERS:-1 2 3 4 5} > $O/fvar.log 2>&1 || { tail -20 $O/fvar.log; exit 1; }
         cat $O/fvar.log
