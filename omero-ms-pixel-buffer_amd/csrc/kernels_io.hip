@@ -889,7 +889,7 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 // behind a filtered row -- and exits, like k_extract's workgroups: Sub / Up / Avg 0.59-0.62 ->
 // 0.64 of HBM peak with runs of 24 rows (100 VGPRs of rows, three waves per SIMD), Paeth
 // 0.60 -> 0.625 with runs of 12 (its forms need more registers a row); the adaptive choice
-// keeps its 5-row ring over 32-row runs (the short-run forms spill it: 0.47-0.53).
+// keeps its 5-row ring, over runs of 24 rows (the run-at-once forms spill it: 0.47-0.53).
 #ifndef PBX_F3_RUN
 #define PBX_F3_RUN 24  // Sub, Up, Avg
 #endif
@@ -897,7 +897,7 @@ uint32_t filter2_band_rows() { return F2_ROWS; }
 #define PBX_F3_RUN_P 12  // Paeth
 #endif
 #ifndef PBX_F3_RUN_AD
-#define PBX_F3_RUN_AD 32  // adaptive
+#define PBX_F3_RUN_AD 24  // adaptive (32: 0.559-0.564, 16: 0.559-0.561, 48: 0.567, 24: 0.573-0.575 of HBM, profiles/r06n/)
 #endif
 #ifndef PBX_F3_NTS
 #define PBX_F3_NTS 0
