@@ -2101,7 +2101,8 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
                                              uint64_t* __restrict__ stamps,
                                              const TileDesc* __restrict__ solo = nullptr,
                                              uint64_t* __restrict__ offs = nullptr,
-                                             uint64_t* __restrict__ offs_host = nullptr) {
+                                             uint64_t* __restrict__ offs_host = nullptr,
+                                             uint32_t solo_nseg = 0) {
     __shared__ HuffSmem<C> S;
     const uint32_t tid = threadIdx.x & 63;  // the lane (the code below is one wave's)
     const uint32_t wv = NWV > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
@@ -2109,7 +2110,9 @@ __global__ __launch_bounds__(64 * NWV) void k_huff(uint32_t nblk, BlkInfo* __res
     // a sync among the lanes doing a phase: the workgroup's barrier when it is one wave
     auto bar = [&]() { huff_sync<(NWV > 1)>(); };
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const uint32_t seg0 = blk[b].seg0, nsg = blk[b].nseg;
+    // (solo: the block is the tile's segments 0..nseg-1, known at launch -- no dependent load of
+    // its record before the histogram loads)
+    const uint32_t seg0 = solo_nseg ? 0u : blk[b].seg0, nsg = solo_nseg ? solo_nseg : blk[b].nseg;
     uint32_t nst = 0;
     auto stamp = [&]() {
         if (PROF && threadIdx.x == 0) stamps[(size_t)seg0 * STAMP_STRIDE + 8 + nst] = __builtin_amdgcn_s_memtime();
@@ -3412,6 +3415,9 @@ static hipError_t crc_tables_ready() {
     return res[dev];
 }
 
+#ifndef PBX_HUFF_SOLO_ARGS
+#define PBX_HUFF_SOLO_ARGS 1  // a solo block's segment range as a launch argument (0: loaded from its record)
+#endif
 hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev, hipEvent_t* ev2, bool fine) {
     if (!a.ntiles || !a.nseg) return hipSuccess;
     if (const hipError_t e = crc_tables_ready(); e != hipSuccess) return e;
@@ -3449,7 +3455,7 @@ hipError_t launch_deflate(hipStream_t st, const DeflateLaunch& a, hipEvent_t* ev
     else if (a.nblk <= HUFF_SMALL_BLKS)  // a small batch: every segment's histogram loads at once
         hipLaunchKernelGGL((k_huff<DC, false, 34, HUFF_SMALL_WAVES>), dim3(a.nblk), dim3(64 * HUFF_SMALL_WAVES), 0, st,
                            a.nblk, a.blk, a.info, a.hist, a.codes, a.stamps, solo ? a.tiles : nullptr, a.offs,
-                           a.offs_host);
+                           a.offs_host, solo && PBX_HUFF_SOLO_ARGS ? a.nseg : 0u);
     else
         hipLaunchKernelGGL((k_huff<DC, false>), dim3(a.nblk), dim3(64), 0, st, a.nblk, a.blk, a.info,
                            a.hist, a.codes, a.stamps);

@@ -16,6 +16,7 @@
 #   raw      k_extract alone (scripts/raw_probe.py), aligned / unaligned, PBX_EXT_BLK 16-64 KiB
 #   hwq      the headline and configs[4] under GPU_MAX_HW_QUEUES 4 / 8 / 16
 #   c4       configs[3]'s TIFF pass on one channel (scripts/c4_probe.py), product vs AB_LIBS
+#   c1       configs[0]'s served latency (scripts/c1_latency.py), product vs AB_LIBS
 #   c5       configs[4]'s pass alone (scripts/c5_pass.py) and its rocprofv3 kernel trace
 #   bench    the full bench.py line + the rocprofv3 kernel trace of a serial pass
 # Every GPU step has its own time limit; the first failure ends the call.
@@ -127,6 +128,12 @@ for stage in "$@"; do
         echo "-- $L"
         PBX_LIB=$PWD/$L timeout -k 10 300 python -u scripts/c4_probe.py > $O/c4.log 2>&1 || { tail -20 $O/c4.log; exit 1; }
         cat $O/c4.log
+      done; done ;;
+    c1)  # configs[0]'s served single-request latency, product vs AB_LIBS, three alternations
+      for i in 1 2 3; do for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
+        echo "== $L"
+        PBX_LIB=$PWD/$L timeout -k 10 200 python -u scripts/c1_latency.py 3000 > $O/c1.log 2>&1 || { tail -20 $O/c1.log; exit 1; }
+        grep served $O/c1.log
       done; done ;;
     c5)
       for L in omero-ms-pixel-buffer_amd/lib/libpbx.so ${AB_LIBS:-}; do
