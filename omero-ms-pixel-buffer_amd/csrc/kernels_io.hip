@@ -170,9 +170,12 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
         // EXT_U loads per thread in flight before their stores (a block's ~16 KiB of rows is
         // one round: 4 KiB per wave in flight instead of 1)
 #ifndef PBX_EXT_U
-#define PBX_EXT_U 4
+#define PBX_EXT_U 8  // all-aligned batches (k_extract<false>): configs[3] 5.29 -> 5.61 TB/s over 4 (profiles/r06r/)
 #endif
-        constexpr uint32_t EXT_U = PBX_EXT_U;
+#ifndef PBX_EXT_U_UA
+#define PBX_EXT_U_UA 4  // k_extract<true>: 8 here costs its unaligned path 10% (registers)
+#endif
+        constexpr uint32_t EXT_U = UA ? PBX_EXT_U_UA : PBX_EXT_U;
         const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
         for (uint32_t i0 = tid; i0 < nv; i0 += 256 * EXT_U) {
             uint4 q[EXT_U];

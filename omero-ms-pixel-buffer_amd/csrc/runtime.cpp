@@ -945,14 +945,21 @@ static bool ext_aligned(const TileDesc& d) {
     return !d.vw && ((int64_t)d.x * d.bpp) % 16 == 0 && ((int64_t)d.w * d.bpp) % 16 == 0;
 }
 
-// Rows of one k_extract workgroup: about this many bytes ($PBX_EXT_BLK, default 16 KiB).
-static uint32_t ext_blk_bytes() {
-    static const uint32_t v = [] {
+// Rows of one k_extract workgroup: about this many bytes ($PBX_EXT_BLK for aligned tiles,
+// $PBX_EXT_BLK_UA for the realigned path; 16 KiB each).  32 KiB unaligned blocks move the
+// headline grid at x*bpp mod 16 = 6 faster (0.824 -> 0.797 ms) but configs[4]'s stream of
+// smaller launches slower (548k -> 535k tiles/s), profiles/r06t/: the baseline config wins.
+static uint32_t ext_blk_bytes(bool aligned) {
+    static const uint32_t v[2] = {[] {
+        const char* e = getenv("PBX_EXT_BLK_UA");
+        const long x = e ? atol(e) : 16384;
+        return (uint32_t)std::min<long>(1 << 20, std::max<long>(1024, x));
+    }(), [] {
         const char* e = getenv("PBX_EXT_BLK");
         const long x = e ? atol(e) : 16384;
         return (uint32_t)std::min<long>(1 << 20, std::max<long>(1024, x));
-    }();
-    return v;
+    }()};
+    return v[aligned ? 1 : 0];
 }
 
 static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_follows);
@@ -2684,7 +2691,7 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
         if (!deflate) {
             if (r.format == PBX_FMT_TIF) d.flags |= TF_TIFF;
             const uint32_t rb = (uint32_t)w * bpp;
-            d.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(ext_blk_bytes() / std::max<uint32_t>(rb, 1)));
+            d.rows_per_blk = std::max<uint32_t>(1, (uint32_t)(ext_blk_bytes(ext_aligned(d)) / std::max<uint32_t>(rb, 1)));
             const uint32_t blks = (uint32_t)((h + d.rows_per_blk - 1) / d.rows_per_blk);
             d.blk_first = b->ext_blocks;
             b->ext_blocks += blks;
