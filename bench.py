@@ -577,7 +577,8 @@ def zlib6_sample(svc, pid, n=16):
 
 
 def adaptive_filter_line(svc, rank, world, barrier, side):
-    """PNG with the adaptive per-row filter (cfg.png_filter = ADAPTIVE: k_filter picks
+    """PNG with the adaptive filter (cfg.png_filter = ADAPTIVE: k_adaptive_mode first decides
+    per tile whether filtering pays -- if not, every row is None -- else the filter kernels pick
     None/Sub/Up/Avg/Paeth per row by minimum sum |residual|), on G_NOISE, G_FAKE and a
     Poisson-like plane: tiles/s (device-resident, like the headline) and bytes per tile
     against the filter-None path and zlib-6 of the filter-None stream (the reference's

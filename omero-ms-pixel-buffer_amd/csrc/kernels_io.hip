@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
             *(uint4*)(sm + q * rbp + 16 * c) = v;
         }
         __syncthreads();
-        if (png && d.filter == 5) {
+        if (png && d.filter == 5) {  // (tile mode None: every ftype 0, sums unused)
             for (uint32_t q = 1 + wv; q < nq; q += 4) {
                 const uint8_t* L = sm + q * rbp;
                 const uint8_t* U = L - rbp;
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                 for (int f = 0; f < 5; f++)
 #pragma unroll
                     for (int off = 32; off > 0; off >>= 1) sum[f] += __shfl_xor(sum[f], off, 64);
-                if (lane == 0) ftype[q - 1] = block_min_filter(sum, nullptr, 0);
+                if (lane == 0) ftype[q - 1] = (d.flags & TF_ANONE) ? 0u : block_min_filter(sum, nullptr, 0);
             }
             __syncthreads();
         }
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
                 if (tid == 0) {
                     int best = 0;
                     for (int f = 1; f < 5; f++) if (red[f] < red[best]) best = f;
-                    ftype[r - r0] = (uint32_t)best;
+                    ftype[r - r0] = (d.flags & TF_ANONE) ? 0u : (uint32_t)best;
                 }
                 __syncthreads();
             }
@@ -437,6 +437,127 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
             out[o] = (uint8_t)byte;
         }
     }
+}
+
+// ------------------------------------------------------- adaptive filter: the tile mode
+// The pbx_config.png_filter = adaptive option first asks, per tile, whether filtering pays at
+// all (on microscope-like 16-bit data the per-row minimum-distance rule picks
+// Sub/Paeth rows that deflate worse than the raw rows).  On the tile's middle row r* = h/2
+// (row r* - 1 above it, zeros above the tile): the best of Sub/Up/Avg/Paeth by the sum of
+// |byte - prediction| (the first on ties), then None against it by the sum, over the two byte
+// planes (i mod bpp) & 1, of the squared counts of the row's byte values -- the larger, the
+// more concentrated the bytes, the fewer bits; None wins ties.  TF_ANONE sends every row of
+// the tile to None (k_filter / k_filter2 / k_filter3 read it); the oracle's
+// adaptive_tile_none (oracle/pbx_oracle.c) is the same rule.  One workgroup per tile; two rows
+// of byte reads and 2 KiB of LDS counters: microseconds a batch.
+// rows_cap: LDS bytes for the two staged rows (the batch's widest adaptive row; wider ones
+// read their bytes from the plane)
+__global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt, uint32_t ndt,
+                                                       uint32_t rows_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+    uint32_t* cnt = (uint32_t*)sm;  // [candidate][byte plane][byte]
+    uint8_t* rows = sm + 4096;
+    __shared__ uint32_t red[4];
+    __shared__ unsigned long long q2[2];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    if (t >= ndt) return;
+    const TileDesc d = dt[t];
+    if (d.filter != 5 || !(d.flags & TF_PNGROWS)) return;  // uniform: the whole workgroup
+    TileStream ts;
+    ts.init(d, nullptr);
+    const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp;
+    const int64_t rs = d.h / 2;
+    const uint32_t rbp = ((rb + 15) & ~15u) + 16;
+    const bool staged = !d.vw && 2 * rbp <= rows_cap;
+    for (uint32_t k = tid; k < 1024; k += 256) cnt[k] = 0;
+    if (tid < 4) red[tid] = 0;
+    if (tid < 2) q2[tid] = 0;
+    if (staged) {  // rows r* - 1 (zeros above the tile) and r*: k_filter's staging (any alignment)
+        const uint32_t nc = (rb + 15) >> 4;
+        const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
+        const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
+        for (uint32_t i = tid; i < 2 * nc; i += 256) {
+            const uint32_t q = i / nc, c = i - q * nc;
+            const int64_t row = rs - 1 + q;
+            ULoad u;
+            uload_issue(u, src0 + (row >= 0 ? row : 0) * d.pitch + 16 * c);
+            uint4 v = uload_finish(u);
+            if (swap) v = swap16(v, bpp);
+            if (flip) v = flip_msb(v, bpp);
+            if (row < 0) v = make_uint4(0, 0, 0, 0);
+            *(uint4*)(rows + q * rbp + 16 * c) = v;
+        }
+    }
+    __syncthreads();
+    const uint8_t* U = rows;
+    const uint8_t* L = rows + rbp;
+    auto bytes = [&](uint32_t i, uint32_t& cur, uint32_t& left, uint32_t& up, uint32_t& ul) {
+        if (staged) {
+            cur = L[i];
+            up = U[i];
+            left = i >= bpp ? L[i - bpp] : 0u;
+            ul = i >= bpp ? U[i - bpp] : 0u;
+        } else {
+            cur = ts.be(rs, i);
+            up = rs > 0 ? ts.be(rs - 1, i) : 0u;
+            left = i >= bpp ? ts.be(rs, i - bpp) : 0u;
+            ul = (rs > 0 && i >= bpp) ? ts.be(rs - 1, i - bpp) : 0u;
+        }
+    };
+    uint32_t sum[4] = {0, 0, 0, 0};
+    for (uint32_t i = tid; i < rb; i += 256) {
+        uint32_t cur, left, up, ul;
+        bytes(i, cur, left, up, ul);
+#pragma unroll
+        for (int f = 1; f < 5; f++) sum[f - 1] += (uint32_t)abs((int)cur - (int)filt_pred(f, left, up, ul));
+    }
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum[f] += __shfl_xor(sum[f], off, 64);
+        if (lane == 0) atomicAdd(&red[f], sum[f]);
+    }
+    __syncthreads();
+    int fb = 1;
+    for (int f = 2; f < 5; f++)
+        if (red[f - 1] < red[fb - 1]) fb = f;
+    for (uint32_t i = tid; i < rb; i += 256) {
+        uint32_t cur, left, up, ul;
+        bytes(i, cur, left, up, ul);
+        const uint32_t pl = (i & (bpp - 1)) & 1u;
+        atomicAdd(&cnt[pl * 256 + cur], 1u);
+        atomicAdd(&cnt[512 + pl * 256 + filt_byte(fb, cur, left, up, ul)], 1u);
+    }
+    __syncthreads();
+    unsigned long long a = 0, b = 0;
+    for (uint32_t k = tid; k < 512; k += 256) {
+        a += (unsigned long long)cnt[k] * cnt[k];
+        b += (unsigned long long)cnt[512 + k] * cnt[512 + k];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&q2[0], a);
+        atomicAdd(&q2[1], b);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const bool none = rb > 0 && d.h > 0 && q2[0] >= q2[1];
+        dt[t].flags = none ? (d.flags | TF_ANONE) : (d.flags & ~TF_ANONE);
+    }
+}
+
+hipError_t launch_adaptive_mode(hipStream_t st, TileDesc* d_tiles, uint32_t ntiles, uint32_t max_rb) {
+    if (!ntiles) return hipSuccess;
+    // the two rows of the widest tile in LDS, up to 2 x 16 KiB (+ 4 KiB of counters): small
+    // workgroups stay many to a CU
+    const uint32_t rbp = ((max_rb + 15) & ~15u) + 16;
+    const uint32_t rows_cap = 2 * rbp <= 32768u ? 2 * rbp : 0u;
+    hipLaunchKernelGGL(k_adaptive_mode, dim3(ntiles), dim3(256), 4096 + rows_cap, st, d_tiles, ntiles, rows_cap);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------- tiled-TIFF headers
@@ -781,7 +902,7 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
             const uint32_t* L = (const uint32_t*)(SA + q * sst + 16);
             const uint32_t* U = (const uint32_t*)(SA + (q - 1) * sst + 16);
             uint32_t s[5] = {0, 0, 0, 0, 0};
-            for (uint32_t k = lane; k < nw; k += 64) {
+            for (uint32_t k = (d.flags & TF_ANONE) ? nw : lane; k < nw; k += 64) {
                 const uint32_t cur = L[k], up = U[k];
                 const uint32_t left = back_bytes(L, (int32_t)k, bpp), ul = back_bytes(U, (int32_t)k, bpp);
                 s[0] = __builtin_amdgcn_sad_u8(cur, 0u, s[0]);
@@ -797,7 +918,7 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
             if (lane == 0) {
                 uint32_t best = 0;
                 for (uint32_t f = 1; f < 5; f++) if (s[f] < s[best]) best = f;
-                ftype[q - 1] = best;
+                ftype[q - 1] = (d.flags & TF_ANONE) ? 0u : best;  // the tile mode: None on every row
             }
         }
         __syncthreads();
@@ -1097,7 +1218,7 @@ __device__ __forceinline__ uint32_t f3_paeth_word(const uint32_t (&l)[2], const 
 
 // One wave's run of rows, specialised on the sample size (the left-neighbour shifts, the byte
 // swap and the sign flip are then fixed: no per-row branches or register moves on bpp).
-template <uint32_t G, uint32_t FT, uint32_t BPP>
+template <uint32_t G, uint32_t FT, uint32_t BPP, bool NONE>
 __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t lane, uint8_t* __restrict__ stream) {
     constexpr uint32_t bpp = BPP;
     const uint32_t rb = (uint32_t)d.w * bpp, nc = rb >> 4, rowlen = d.rowlen;
@@ -1180,7 +1301,11 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
         };
         uint4 f[G];
         uint32_t ft = fixed;
-        if (ADAPTIVE) {
+        if (NONE) {  // an adaptive tile in the None mode (k_adaptive_mode): the rows as they are
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) f[g] = cur[g];
+            ft = 0;
+        } else if (ADAPTIVE) {
             // every candidate's prediction ([0] Sub = left, [1] Up, [2] Avg, [3] Paeth) and the
             // row sums of |byte - prediction| (v_sad_u8; None: the bytes themselves); the chosen
             // filter's residuals are formed once, after the choice
@@ -1345,7 +1470,7 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
 #pragma unroll
         for (uint32_t g = 0; g < G; g++) B[0][g] = Z;
     }
-    if (PBX_F3_CARRY && (ADAPTIVE || fixed == 4)) {
+    if (PBX_F3_CARRY && !NONE && (ADAPTIVE || fixed == 4)) {
         f3_paeth_forms<G, BPP>(B[0], UF, ULF);
 #pragma unroll
         for (uint32_t g = 0; g < G; g++)
@@ -1376,11 +1501,21 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
     if (wi >= nwaves) return;  // a whole wave: no barrier in this kernel
     const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
     const TileDesc d = dt[ti];
-    switch (__builtin_amdgcn_readfirstlane((uint32_t)d.bpp)) {  // a uniform branch
-    case 1: f3_run<G, FT, 1>(d, wi, lane, stream); break;
-    case 2: f3_run<G, FT, 2>(d, wi, lane, stream); break;
-    case 4: f3_run<G, FT, 4>(d, wi, lane, stream); break;
-    default: f3_run<G, FT, 8>(d, wi, lane, stream); break;
+    const uint32_t bpp = __builtin_amdgcn_readfirstlane((uint32_t)d.bpp);
+    if (FT == 5 && (__builtin_amdgcn_readfirstlane(d.flags) & TF_ANONE)) {  // uniform branches
+        switch (bpp) {
+        case 1: f3_run<G, FT, 1, true>(d, wi, lane, stream); break;
+        case 2: f3_run<G, FT, 2, true>(d, wi, lane, stream); break;
+        case 4: f3_run<G, FT, 4, true>(d, wi, lane, stream); break;
+        default: f3_run<G, FT, 8, true>(d, wi, lane, stream); break;
+        }
+        return;
+    }
+    switch (bpp) {
+    case 1: f3_run<G, FT, 1, false>(d, wi, lane, stream); break;
+    case 2: f3_run<G, FT, 2, false>(d, wi, lane, stream); break;
+    case 4: f3_run<G, FT, 4, false>(d, wi, lane, stream); break;
+    default: f3_run<G, FT, 8, false>(d, wi, lane, stream); break;
     }
 }
 

@@ -31,6 +31,8 @@ enum : uint32_t {
     TF_DIRECT = 16u,   // filter-None rows, 16-byte aligned source, bpp <= 4: k_lz77
                        // assembles the stream from the plane (no k_rows pass)
     TF_TILED = 32u,    // one T x T sub-tile of a tiled-TIFF response (header by k_tiff_tiled)
+    TF_ANONE = 64u,    // adaptive PNG tile whose rows all take filter None (the tile mode: set
+                       // or cleared on the device by k_adaptive_mode every launch)
     TF_BRIDGE = 1u << 30,  // host only, cleared before upload: `plane` is an offset into the
                            // batch's bridge buffer (a region straddling sparse-plane bands)
 };

@@ -46,6 +46,10 @@ uint32_t filter2_band_rows();
 hipError_t launch_filter3(hipStream_t st, const TileDesc* d_tiles, uint32_t ntiles, uint32_t nwaves,
                           uint32_t max_rb, uint32_t filter, uint8_t* stream);
 uint32_t filter3_run_rows(uint32_t filter);  // rows per wave for the PNG filter 1..5
+// The adaptive option's tile mode, before the filter kernels: TF_ANONE of every adaptive PNG
+// tile of d_tiles[0, ntiles) (one workgroup per tile; other tiles are left alone); max_rb: the
+// widest of their rows in bytes.
+hipError_t launch_adaptive_mode(hipStream_t st, TileDesc* d_tiles, uint32_t ntiles, uint32_t max_rb);
 uint32_t filter3_max_rb();
 uint32_t filter2_max_rb();
 

@@ -490,6 +490,8 @@ struct pbx_batch {
     uint32_t nfilt2_tiles = 0, filt2_blocks = 0, filt2_max_rb = 0;  // k_filter2 group
     uint32_t nfilt3_tiles = 0, filt3_waves = 0, filt3_max_rb = 0;   // k_filter3 group
     uint32_t filt3_filter = 0;  // its PNG filter (the context's: every k_filter3 tile's d.filter)
+    bool adaptive = false;      // some PNG tile takes the adaptive filter (k_adaptive_mode first)
+    uint32_t adaptive_max_rb = 0;  // the widest row (bytes) of those tiles
     uint64_t fixed_bytes = 0, stream_cap = 0, png_cap = 0;
     uint64_t in_bytes = 0, stream_bytes = 0;
     // device buffers (pool blocks)
@@ -2705,6 +2707,10 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                 d.flags |= TF_PNGROWS;
                 if (pl.pixel_type == PBX_INT8 || pl.pixel_type == PBX_INT16) d.flags |= TF_FLIP;
                 d.filter = filter;
+                if (filter == PBX_FILTER_ADAPTIVE) {
+                    b->adaptive = true;
+                    b->adaptive_max_rb = std::max<uint32_t>(b->adaptive_max_rb, (uint32_t)w * bpp);
+                }
                 d.rowlen = 1 + (uint32_t)w * bpp;
             } else {
                 d.flags |= TF_TIFF;
@@ -2917,6 +2923,9 @@ static int batch_launch(pbx_ctx* ctx, pbx_batch* b, bool overlap, bool fetch_fol
         if (fine || nft) HIP_TRY(hipEventRecord(b->ev[2], st));
     }
     const TileDesc* d_rows = (const TileDesc*)b->d_dt + b->ndirect_tiles;
+    if (b->adaptive)  // the tile mode of every adaptive tile (the filtered ones follow k_rows')
+        HIP_TRY(launch_adaptive_mode(st, (TileDesc*)b->d_dt + b->ndirect_tiles + b->nrows_tiles,
+                                     ndt - b->ndirect_tiles - b->nrows_tiles, b->adaptive_max_rb));
     HIP_TRY(launch_rows(st, d_rows, b->nrows_tiles, b->rows_blocks, b->rows_max_rb, (uint8_t*)b->d_stream));
     HIP_TRY(launch_filter2(st, d_rows + b->nrows_tiles, b->nfilt2_tiles, b->filt2_blocks, b->filt2_max_rb,
                            (uint8_t*)b->d_stream));

@@ -54,10 +54,13 @@ void pbxo_extract_be(const uint8_t* plane, int plane_big_endian, int pixel_type,
                      uint8_t* out);
 
 /* PNG filtered stream for a big-endian tile: h rows of (filter byte || row), with the
- * APNGWriter int8/int16 sign-bit flip.  filter: 0..4 fixed, 5 = adaptive (min sum of
- * |signed residual|).  Returns bytes written (h*(1+w*bpp)). */
+ * APNGWriter int8/int16 sign-bit flip.  filter: 0..4 fixed, 5 = adaptive (per tile: None on
+ * every row when its middle row says filtering does not pay -- pbxo_adaptive_tile_none --
+ * else per row the minimum sum of |byte - prediction|).  Returns bytes written (h*(1+w*bpp)). */
 size_t pbxo_png_filter_stream(const uint8_t* tile_be, int pixel_type, int32_t w, int32_t h,
                               int filter, uint8_t* out);
+/* The adaptive option's tile mode: 1 when the tile's rows all take filter None. */
+int pbxo_adaptive_tile_none(const uint8_t* tile_be, int pixel_type, int32_t w, int32_t h);
 
 /* Encoders.  Return PBXO_OK or PBXO_E_NOTFOUND (unsupported type -> getTile returns null).
  * *len receives the exact output length (TileRequestHandler.java:188-193). */

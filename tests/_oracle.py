@@ -44,6 +44,7 @@ def lib():
         L.pbxo_png_filter_stream.restype = ctypes.c_size_t
         L.pbxo_png_filter_stream.argtypes = [u8p, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.c_int, u8p]
+        L.pbxo_adaptive_tile_none.argtypes = [u8p, ctypes.c_int, ctypes.c_int32, ctypes.c_int32]
         L.pbxo_png_encode.argtypes = [u8p, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_int, u8p, ctypes.c_size_t, szp]
         L.pbxo_tiff_encode.argtypes = [u8p, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, u8p,
@@ -108,6 +109,11 @@ def png_filter_stream(tile_be, pt, w, h, filt=0):
     out = np.zeros(h * (1 + w * BPP[pt]), np.uint8)
     lib().pbxo_png_filter_stream(_p(tile_be), pt, w, h, filt, _p(out))
     return out
+
+
+def adaptive_tile_none(tile_be, pt, w, h):
+    """The adaptive option's tile mode: True when every row of the tile takes filter None."""
+    return bool(lib().pbxo_adaptive_tile_none(_p(tile_be), pt, w, h))
 
 
 def png_encode(tile_be, pt, w, h, level=6):

@@ -126,3 +126,47 @@ def test_wholeslide_deflate_tiff_pass_sample(oracle):
     assert len(checks) >= 512
     assert all(ok), [checks[i][:5] for i, v in enumerate(ok) if not v][:8]
     assert any(a[3] == 160 and a[4] == 160 for a in checks)
+
+
+def test_adaptive_tile_mode_poisson(oracle):
+    """The adaptive filter's tile mode (k_adaptive_mode, kernels_io.hip) on a
+    Poisson-like uint16 plane (microscope counts, lambda drifting 200..300, the bench's
+    adaptive_filter_line plane) and on G_FAKE: regions that go to k_filter3 (rows of 16-byte
+    chunks), k_filter2 (rows of dwords) and the banded k_filter (odd x or odd widths) in one
+    batch, every IDAT equal to the oracle's adaptive scanlines, the None-mode tiles exactly the
+    oracle's (adaptive_tile_none), and the 64 whole 512^2 Poisson tiles no larger in total than
+    the same tiles through filter None."""
+    side, T = 4096, 512
+    rng = np.random.default_rng(1234)
+    yy, xx = np.mgrid[0:side:64, 0:side:64]
+    lam = 200.0 + 100.0 * (0.5 + 0.25 * np.sin(xx / 900.0) + 0.25 * np.cos(yy / 1300.0))
+    pois = rng.poisson(np.repeat(np.repeat(lam, 64, 0), 64, 1)).astype(np.uint16)
+    pois_be = pois.astype(">u2").view(np.uint8).reshape(side, side * 2)
+    fake_be = oracle.gen_region(FAKE, pbx.UINT16, 0, 0, side, 64).reshape(64, side * 2)
+    regions = [(0, (i % 8) * T, (i // 8) * T, T, T) for i in range(64)]  # k_filter3
+    for k in range(96):
+        w = int(rng.choice([8, 24, 40, 136, 250, 1030, 1001]))  # 16 B chunks, dwords, odd
+        h = int(rng.integers(1, 61))
+        x = int(rng.integers(0, side - w)) & ~(7 if k % 3 else 0)
+        y = int(rng.integers(0, 64 - h + 1)) if k % 4 == 0 else int(rng.integers(0, side - h))
+        regions.append((1 if k % 4 == 0 else 0, x, y, w, h))
+    with pbx.PixelsService(png_filter=pbx.FILTER_ADAPTIVE) as sa, pbx.PixelsService() as sn:
+        for s_ in (sa, sn):
+            s_.register_plane(7, 0, 0, 0, pbx.UINT16, side, side, data=pois, big_endian=False)
+            s_.register_plane(8, 0, 0, 0, pbx.UINT16, side, side, generator="fake")
+        ctxs = [pbx.TileCtx(7 + p, 0, 0, 0, x, y, w, h, format="png") for p, x, y, w, h in regions]
+        _, ad = _run(sa, ctxs)
+        _, no = _run(sn, ctxs[:64])
+    n_none = 0
+    for (p, x, y, w, h), body in zip(regions, ad):
+        src = pois_be if p == 0 else fake_be
+        tile = np.ascontiguousarray(src[y:y + h, 2 * x:2 * (x + w)]).reshape(-1)
+        want = oracle.png_filter_stream(tile, pbx.UINT16, w, h, pbx.FILTER_ADAPTIVE).tobytes()
+        rc, idat = oracle.png_inflate_idat(body, len(want))
+        assert rc == 0 and idat == want, (p, x, y, w, h)
+        mode = oracle.adaptive_tile_none(tile, pbx.UINT16, w, h)
+        filt = np.frombuffer(idat, np.uint8).reshape(h, 1 + 2 * w)[:, 0]
+        assert not mode or not filt.any(), (p, x, y, w, h)
+        n_none += mode
+    assert n_none >= 64  # every whole Poisson tile, at least
+    assert sum(map(len, ad[:64])) <= sum(map(len, no))

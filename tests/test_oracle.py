@@ -124,3 +124,65 @@ def test_grid_pixel_checker_catches_a_wrong_tile(oracle):
     assert oracle.check_png_grid_pixels(bodies, oracle.UINT16, 64, 32, 3, 0) == []
     bodies[4] = bodies[1]
     assert oracle.check_png_grid_pixels(bodies, oracle.UINT16, 64, 32, 3, 0) == [4]
+
+
+def _np_tile_none(tile_be, pt, w, h):
+    """The adaptive tile mode restated in numpy (oracle/pbx_oracle.c adaptive_tile_none): on the
+    middle row, the best of Sub/Up/Avg/Paeth by sum |byte - prediction| against None by the sum
+    over the byte planes (i mod bpp) & 1 of squared byte-value counts; None wins ties."""
+    bpp = BPP_OF[pt]
+    rb = w * bpp
+    rows = np.asarray(tile_be, np.uint8).reshape(h, rb).astype(np.int64)
+    if pt in (0, 2):  # int8 / int16: APNGWriter's sign flip of the most significant byte
+        rows[:, 0::bpp] ^= 0x80
+    rs = h // 2
+    cur = rows[rs]
+    up = rows[rs - 1] if rs > 0 else np.zeros(rb, np.int64)
+    left = np.concatenate([np.zeros(bpp, np.int64), cur[:-bpp]])[:rb]
+    ul = np.concatenate([np.zeros(bpp, np.int64), up[:-bpp]])[:rb]
+    p = left + up - ul
+    pa, pb, pc = np.abs(p - left), np.abs(p - up), np.abs(p - ul)
+    paeth = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, up, ul))
+    preds = [left, up, (left + up) >> 1, paeth]
+    sads = [int(np.abs(cur - q).sum()) for q in preds]
+    fb = int(np.argmin(sads))
+    resid = (cur - preds[fb]) & 0xFF
+    plane = (np.arange(rb) % bpp) & 1
+
+    def q2(v):
+        return sum(int((np.bincount(v[plane == k], minlength=256) ** 2).sum()) for k in (0, 1))
+
+    return q2(cur) >= q2(resid)
+
+
+BPP_OF = [1, 1, 2, 2, 4, 4, 4, 8]
+
+
+def test_adaptive_tile_mode(oracle):
+    """The adaptive filter's tile mode: the C oracle against the numpy
+    restatement above on synthetic and Poisson-like tiles; a None-mode tile's stream is the
+    filter-None stream, and on Poisson-like 16-bit tiles (microscope counts) the adaptive stream
+    deflates no larger than None, as it did not before the tile mode."""
+    rng = np.random.default_rng(6)
+    cases = []
+    for kind in (1, 2):
+        for pt, w, h in ((oracle.UINT16, 64, 9), (oracle.UINT8, 37, 5), (oracle.INT16, 33, 4),
+                         (oracle.INT8, 100, 2), (oracle.UINT16, 1, 1), (oracle.UINT16, 128, 64)):
+            cases.append((oracle.gen_region(kind, pt, 3, 7, w, h), pt, w, h))
+    for lam in (3.0, 40.0, 400.0):
+        v = rng.poisson(lam, (64, 128)).astype(">u2")
+        cases.append((np.frombuffer(v.tobytes(), np.uint8).copy(), oracle.UINT16, 128, 64))
+    modes = []
+    for t, pt, w, h in cases:
+        m = oracle.adaptive_tile_none(t, pt, w, h)
+        assert m == _np_tile_none(t, pt, w, h), (pt, w, h)
+        s = oracle.png_filter_stream(t, pt, w, h, 5)
+        if m:
+            assert s.tobytes() == oracle.png_filter_stream(t, pt, w, h, 0).tobytes()
+        modes.append(m)
+    assert modes[-3:] == [True, True, True]  # Poisson-like: filtering does not pay
+    assert not modes[5]  # G_FAKE 128x64 uint16: its gradients pay for the filters
+    for t, pt, w, h in cases[-3:]:
+        a = len(zlib.compress(oracle.png_filter_stream(t, pt, w, h, 5).tobytes(), 6))
+        n = len(zlib.compress(oracle.png_filter_stream(t, pt, w, h, 0).tobytes(), 6))
+        assert a <= n
