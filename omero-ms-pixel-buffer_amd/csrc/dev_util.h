@@ -199,6 +199,7 @@ struct ULoad {
 __device__ __forceinline__ uint32_t dpp_from_next(uint32_t x, uint32_t old) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x130, 0xF, 0xF, false);  // wave_shl:1
 }
+template <bool NT = false>  // NT: nontemporal loads (source read once)
 __device__ __forceinline__ void uload_issue(ULoad& u, const uint8_t* p) {
     u.bs = (uint32_t)(uintptr_t)p & 15u;
     const uint8_t* a = p - u.bs;
@@ -206,9 +207,9 @@ __device__ __forceinline__ void uload_issue(ULoad& u, const uint8_t* p) {
     const uint64_t na = (uint64_t)dpp_from_next((uint32_t)ai, 0u) |
                         ((uint64_t)dpp_from_next((uint32_t)(ai >> 32), 0u) << 32);
     u.own = u.bs != 0 && na != ai + 16;
-    u.lo = gload16(a);
+    u.lo = NT ? gload16_nt(a) : gload16(a);
     u.hi = u.lo;
-    if (u.own) u.hi = gload16(a + 16);
+    if (u.own) u.hi = NT ? gload16_nt(a + 16) : gload16(a + 16);
 }
 __device__ __forceinline__ uint4 uload_finish(const ULoad& u) {
     const uint4 nlo = make_uint4(dpp_from_next(u.lo.x, 0u), dpp_from_next(u.lo.y, 0u),

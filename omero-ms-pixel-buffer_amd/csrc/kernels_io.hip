@@ -176,20 +176,26 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
 #define PBX_EXT_U_UA 4  // k_extract<true>: 8 here costs its unaligned path 10% (registers)
 #endif
         constexpr uint32_t EXT_U = UA ? PBX_EXT_U_UA : PBX_EXT_U;
+#ifndef PBX_EXT_NT
+#define PBX_EXT_NT 3  // bit 0: nontemporal loads, bit 1: nontemporal stores (both: the headline grid
+                      // 5.55 -> 6.03-6.15 TB/s aligned, configs[4] 549k -> 570k tiles/s, profiles/r06zb/)
+#endif
         const uint32_t n16 = rb >> 4, nv = (r1 - r0) * n16;
         for (uint32_t i0 = tid; i0 < nv; i0 += 256 * EXT_U) {
             uint4 q[EXT_U];
 #pragma unroll
             for (uint32_t k = 0; k < EXT_U; k++) {
                 const uint32_t i = i0 + 256 * k, r = r0 + i / n16, v = i - (i / n16) * n16;
-                if (i < nv) q[k] = gload16(src0 + (int64_t)r * d.pitch + 16 * v);
+                if (i < nv) q[k] = (PBX_EXT_NT & 1) ? gload16_nt(src0 + (int64_t)r * d.pitch + 16 * v)
+                                                    : gload16(src0 + (int64_t)r * d.pitch + 16 * v);
             }
 #pragma unroll
             for (uint32_t k = 0; k < EXT_U; k++) {
                 const uint32_t i = i0 + 256 * k, r = r0 + i / n16, v = i - (i / n16) * n16;
                 if (i >= nv) break;
                 if (swap) q[k] = swap16(q[k], d.bpp);
-                gstore16(base + (size_t)r * rb + 16 * v, q[k]);
+                if (PBX_EXT_NT & 2) gstore16_nt(base + (size_t)r * rb + 16 * v, q[k]);
+                else gstore16(base + (size_t)r * rb + 16 * v, q[k]);
             }
         }
     } else if (UA && !d.vw && rb >= 16) {
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
                 if (wi >= w1) break;  // (the lanes past the end leave the later rounds together)
                 const uint32_t o = wi << 4, r = o / rb, c = o - r * rb;
                 n1[k] = rb - c;
-                uload_issue(a[k], src0 + (int64_t)r * d.pitch + c);
+                uload_issue<(PBX_EXT_NT & 1) != 0>(a[k], src0 + (int64_t)r * d.pitch + c);
                 // the word runs into row r + 1: loaded from n1 bytes before that row's start
                 if (n1[k] < 16) q2[k] = gload16u(src0 + (int64_t)(r + 1) * d.pitch - n1[k]);
             }
@@ -241,7 +247,8 @@ __global__ __launch_bounds__(256) void k_extract(const TileDesc* __restrict__ ft
                     q.w = (q.w & m3) | (q2[k].w & ~m3);
                 }
                 if (swap) q = swap16(q, d.bpp);
-                gstore16(base + (wi << 4), q);
+                if (PBX_EXT_NT & 2) gstore16_nt(base + (wi << 4), q);
+                else gstore16(base + (wi << 4), q);
             }
         }
         const uint32_t h_end = f1 < (w0 << 4) ? f1 : (w0 << 4);
@@ -1030,6 +1037,9 @@ __host__ __device__ constexpr uint32_t f3_run_rows(uint32_t filter) {
     return filter == 4 ? PBX_F3_RUN_P : filter == 5 ? PBX_F3_RUN_AD : PBX_F3_RUN;
 }
 // stream stores: nontemporal (the stream is re-read only by the next kernel, from HBM anyway)
+#ifndef PBX_F3_NTL
+#define PBX_F3_NTL 0  // nontemporal plane loads in k_filter3 (Sub / Up / Paeth 11-16% slower, profiles/r06zb/)
+#endif
 __device__ __forceinline__ void f3_store(uint8_t* p, const uint4& v) {
     if (PBX_F3_NTS) {
         pbx_v4u x;
@@ -1238,7 +1248,7 @@ __device__ __forceinline__ void f3_run(const TileDesc& d, uint32_t wi, uint32_t 
 #pragma unroll
         for (uint32_t g = 0; g < G; g++) {
             const uint32_t c = 64 * g + lane;
-            v[g] = gload16(rp + 16 * (c < nc ? c : 0u));
+            v[g] = PBX_F3_NTL ? gload16_nt(rp + 16 * (c < nc ? c : 0u)) : gload16(rp + 16 * (c < nc ? c : 0u));
         }
     };
     auto conv = [&](uint4 (&v)[G]) {  // big-endian samples (and the sign flip), zero past the row
