@@ -459,7 +459,11 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
 // of byte reads and 2 KiB of LDS counters: microseconds a batch.
 // rows_cap: LDS bytes for the two staged rows (the batch's widest adaptive row; wider ones
 // read their bytes from the plane)
-__global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt, uint32_t ndt,
+#ifndef PBX_AM_NT
+#define PBX_AM_NT 128  // (256: 28.5 us per 4096 tiles, 128: 24.8, 64: 25.0; profiles/r06ze/)
+#endif
+constexpr uint32_t AM_NT = PBX_AM_NT;  // threads per tile
+__global__ __launch_bounds__(AM_NT) void k_adaptive_mode(TileDesc* __restrict__ dt, uint32_t ndt,
                                                        uint32_t rows_cap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
     uint32_t* cnt = (uint32_t*)sm;  // [candidate][byte plane][byte]
@@ -476,14 +480,14 @@ __global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt
     const int64_t rs = d.h / 2;
     const uint32_t rbp = ((rb + 15) & ~15u) + 16;
     const bool staged = !d.vw && 2 * rbp <= rows_cap;
-    for (uint32_t k = tid; k < 1024; k += 256) cnt[k] = 0;
+    for (uint32_t k = tid; k < 1024; k += AM_NT) cnt[k] = 0;
     if (tid < 4) red[tid] = 0;
     if (tid < 2) q2[tid] = 0;
     if (staged) {  // rows r* - 1 (zeros above the tile) and r*: k_filter's staging (any alignment)
         const uint32_t nc = (rb + 15) >> 4;
         const uint8_t* src0 = d.plane + (int64_t)d.y * d.pitch + (int64_t)d.x * bpp;
         const bool swap = (d.flags & TF_SWAP) != 0, flip = (d.flags & TF_FLIP) != 0;
-        for (uint32_t i = tid; i < 2 * nc; i += 256) {
+        for (uint32_t i = tid; i < 2 * nc; i += AM_NT) {
             const uint32_t q = i / nc, c = i - q * nc;
             const int64_t row = rs - 1 + q;
             ULoad u;
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt
         }
     };
     uint32_t sum[4] = {0, 0, 0, 0};
-    for (uint32_t i = tid; i < rb; i += 256) {
+    for (uint32_t i = tid; i < rb; i += AM_NT) {
         uint32_t cur, left, up, ul;
         bytes(i, cur, left, up, ul);
 #pragma unroll
@@ -528,7 +532,7 @@ __global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt
     int fb = 1;
     for (int f = 2; f < 5; f++)
         if (red[f - 1] < red[fb - 1]) fb = f;
-    for (uint32_t i = tid; i < rb; i += 256) {
+    for (uint32_t i = tid; i < rb; i += AM_NT) {
         uint32_t cur, left, up, ul;
         bytes(i, cur, left, up, ul);
         const uint32_t pl = (i & (bpp - 1)) & 1u;
@@ -537,7 +541,7 @@ __global__ __launch_bounds__(256) void k_adaptive_mode(TileDesc* __restrict__ dt
     }
     __syncthreads();
     unsigned long long a = 0, b = 0;
-    for (uint32_t k = tid; k < 512; k += 256) {
+    for (uint32_t k = tid; k < 512; k += AM_NT) {
         a += (unsigned long long)cnt[k] * cnt[k];
         b += (unsigned long long)cnt[512 + k] * cnt[512 + k];
     }
@@ -563,7 +567,7 @@ hipError_t launch_adaptive_mode(hipStream_t st, TileDesc* d_tiles, uint32_t ntil
     // workgroups stay many to a CU
     const uint32_t rbp = ((max_rb + 15) & ~15u) + 16;
     const uint32_t rows_cap = 2 * rbp <= 32768u ? 2 * rbp : 0u;
-    hipLaunchKernelGGL(k_adaptive_mode, dim3(ntiles), dim3(256), 4096 + rows_cap, st, d_tiles, ntiles, rows_cap);
+    hipLaunchKernelGGL(k_adaptive_mode, dim3(ntiles), dim3(AM_NT), 4096 + rows_cap, st, d_tiles, ntiles, rows_cap);
     return hipGetLastError();
 }
 
