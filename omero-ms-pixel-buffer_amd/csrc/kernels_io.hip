@@ -79,37 +79,62 @@ __device__ __forceinline__ T ds_mean4(T a, T b, T c, T d) {
     }
 }
 
-// One level: a thread makes N = 8 / sizeof(T) output samples of a row from one aligned
-// 16-byte load per input row (input rows are 256-aligned, so group g starts at byte 16 g) and
-// stores them as one 8-byte word; the last, partial group of a row goes sample by sample.
+// One level: a thread makes DS_G groups of N = 8 / sizeof(T) output samples of a row, each
+// from one aligned 16-byte load per input row (input rows are 256-aligned, so group g starts
+// at byte 16 g), all loads issued before the means; whole groups are stored as one 8-byte
+// (DS_G = 1) or 16-byte (DS_G = 2) word; the last, partial group of a row goes sample by sample.
+#ifndef PBX_DS_G
+#define PBX_DS_G 1  // (2: 0.684, with nontemporal loads 0.652; profiles/r06zg/)
+#endif
+#ifndef PBX_DS_NT
+#define PBX_DS_NT 1  // bit 0: nontemporal loads, bit 1: nontemporal stores (1: 0.697 -> 0.768 of HBM peak, profiles/r06zg/)
+#endif
+constexpr int DS_G = PBX_DS_G;
 template <class T>
 __global__ __launch_bounds__(256) void k_downsample(const uint8_t* __restrict__ src, int64_t spitch,
                                                     int32_t sx, int32_t sy, uint8_t* __restrict__ dst,
                                                     int64_t dpitch, int32_t dx, int32_t dy, bool be) {
     constexpr int N = 8 / sizeof(T);
-    const uint64_t ngx = ((uint64_t)dx + N - 1) / N, total = ngx * (uint64_t)dy;
+    const uint64_t ngx = ((uint64_t)dx + N * DS_G - 1) / (N * DS_G), total = ngx * (uint64_t)dy;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-        const int32_t y = (int32_t)(i / ngx), g = (int32_t)(i - (uint64_t)y * ngx), x0 = g * N;
+        const int32_t y = (int32_t)(i / ngx), sg = (int32_t)(i - (uint64_t)y * ngx);
         const int32_t y0 = 2 * y, y1 = 2 * y + 1 < sy ? 2 * y + 1 : sy - 1;
         const uint8_t* r0 = src + (int64_t)y0 * spitch;
         const uint8_t* r1 = src + (int64_t)y1 * spitch;
-        T* out = (T*)(dst + (int64_t)y * dpitch) + x0;
-        if (2 * x0 + 2 * N <= sx) {
-            const uint4 va = gload16(r0 + 16 * g), vb = gload16(r1 + 16 * g);
-            T a[2 * N], b[2 * N], m[N];
-            __builtin_memcpy(a, &va, 16);
-            __builtin_memcpy(b, &vb, 16);
+        const int32_t g0 = sg * DS_G;
+        T* out = (T*)(dst + (int64_t)y * dpitch) + g0 * N;
+        if (2 * (g0 + DS_G) * N <= sx) {
+            uint4 va[DS_G], vb[DS_G];
 #pragma unroll
-            for (int j = 0; j < N; j++)
-                m[j] = ds_swap(ds_mean4(ds_swap(a[2 * j], be), ds_swap(a[2 * j + 1], be),
-                                        ds_swap(b[2 * j], be), ds_swap(b[2 * j + 1], be)), be);
-            uint2 w;
-            __builtin_memcpy(&w, m, 8);
-            *(uint2*)out = w;
+            for (int k = 0; k < DS_G; k++) {
+                va[k] = (PBX_DS_NT & 1) ? gload16_nt(r0 + 16 * (g0 + k)) : gload16(r0 + 16 * (g0 + k));
+                vb[k] = (PBX_DS_NT & 1) ? gload16_nt(r1 + 16 * (g0 + k)) : gload16(r1 + 16 * (g0 + k));
+            }
+            T m[N * DS_G];
+#pragma unroll
+            for (int k = 0; k < DS_G; k++) {
+                T a[2 * N], b[2 * N];
+                __builtin_memcpy(a, &va[k], 16);
+                __builtin_memcpy(b, &vb[k], 16);
+#pragma unroll
+                for (int j = 0; j < N; j++)
+                    m[k * N + j] = ds_swap(ds_mean4(ds_swap(a[2 * j], be), ds_swap(a[2 * j + 1], be),
+                                                    ds_swap(b[2 * j], be), ds_swap(b[2 * j + 1], be)), be);
+            }
+            if constexpr (DS_G == 2) {
+                uint4 w;
+                __builtin_memcpy(&w, m, 16);
+                if (PBX_DS_NT & 2) gstore16_nt(out, w);
+                else gstore16(out, w);
+            } else {
+                uint2 w;
+                __builtin_memcpy(&w, m, 8);
+                *(uint2*)out = w;
+            }
         } else {
-            for (int32_t j = 0; j < N && x0 + j < dx; j++) {
-                const int32_t xa = 2 * (x0 + j), xb = xa + 1 < sx ? xa + 1 : sx - 1;
+            for (int32_t j = 0; j < N * DS_G && g0 * N + j < dx; j++) {
+                const int32_t xa = 2 * (g0 * N + j), xb = xa + 1 < sx ? xa + 1 : sx - 1;
                 const T* p0 = (const T*)r0;
                 const T* p1 = (const T*)r1;
                 out[j] = ds_swap(ds_mean4(ds_swap(p0[xa], be), ds_swap(p0[xb], be), ds_swap(p1[xa], be),
@@ -123,7 +148,7 @@ hipError_t launch_downsample(hipStream_t st, const uint8_t* src, int64_t spitch,
                              uint8_t* dst, int64_t dpitch, int32_t dx, int32_t dy, int32_t pixel_type,
                              bool be) {
     static const int bpps[PT_N] = {1, 1, 2, 2, 4, 4, 4, 8};
-    const uint64_t n = 8 / bpps[pixel_type];
+    const uint64_t n = 8 / bpps[pixel_type] * DS_G;
     const uint64_t total = ((uint64_t)dx + n - 1) / n * (uint64_t)dy;
     uint64_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
