@@ -73,7 +73,9 @@ enum pbx_byte_order { PBX_BIG_ENDIAN = 0, PBX_LITTLE_ENDIAN = 1 };
 enum pbx_source { PBX_SRC_HOST = 0, PBX_SRC_GEN_FAKE = 1, PBX_SRC_GEN_NOISE = 2 };
 
 /* PNG scanline filter used by the encoder.  NONE is what the reference's APNGWriter
- * writes (filter byte 0 on every row); the others decode to identical pixels. */
+ * writes (filter byte 0 on every row); the others decode to identical pixels.  ADAPTIVE: per
+ * tile, NONE on every row when the tile's middle row says filtering does not pay, else per row
+ * the filter with the smallest sum of |byte - prediction|. */
 enum pbx_png_filter {
     PBX_FILTER_NONE = 0, PBX_FILTER_SUB = 1, PBX_FILTER_UP = 2, PBX_FILTER_AVG = 3,
     PBX_FILTER_PAETH = 4, PBX_FILTER_ADAPTIVE = 5
