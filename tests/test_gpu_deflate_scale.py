@@ -170,3 +170,43 @@ def test_adaptive_tile_mode_poisson(oracle):
         n_none += mode
     assert n_none >= 64  # every whole Poisson tile, at least
     assert sum(map(len, ad[:64])) <= sum(map(len, no))
+
+
+@pytest.mark.parametrize("pt", [pbx.INT8, pbx.UINT8, pbx.INT16, pbx.UINT16])
+def test_adaptive_tile_mode_types_and_small_shapes(oracle, pt):
+    """The tile mode on every PNG pixel type (the int8 / int16 sign flip comes before the mode's
+    byte counts) and on small shapes: one row (the middle row's prediction row is zeros above
+    the tile), one or two samples per row, rows of one 16-byte chunk; Poisson-like counts
+    around a per-type offset and G_FAKE side by side in one batch, every IDAT equal to the
+    oracle's adaptive scanlines and the None-mode tiles exactly the oracle's."""
+    side = 1024
+    bpp = oracle.BPP[pt]
+    rng = np.random.default_rng(90 + pt)
+    lam = 20.0 if bpp == 1 else 300.0
+    dt = {pbx.INT8: "i1", pbx.UINT8: "u1", pbx.INT16: ">i2", pbx.UINT16: ">u2"}[pt]
+    base = -60 if pt == pbx.INT8 else 0 if bpp == 1 else -2000 if pt == pbx.INT16 else 1000
+    pois = (rng.poisson(lam, (side, side)) + base).astype(dt)
+    pois_be = np.frombuffer(pois.tobytes(), np.uint8).reshape(side, side * bpp)
+    fake_be = oracle.gen_region(FAKE, pt, 0, 0, side, side).reshape(side, side * bpp)
+    shapes = [(1, 1), (2, 1), (3, 2), (1, 7), (16 // bpp, 1), (16 // bpp, 5), (33, 1), (64, 64),
+              (100, 3), (257, 9), (512, 40), (1000, 2)]
+    regions = []
+    for k, (w, h) in enumerate(shapes * 2):
+        p = k % 2
+        x = int(rng.integers(0, side - w)) & (~15 if k % 3 else ~0)
+        y = int(rng.integers(0, side - h))
+        regions.append((p, x, y, w, h))
+    with pbx.PixelsService(png_filter=pbx.FILTER_ADAPTIVE) as svc:
+        svc.register_plane(9, 0, 0, 0, pt, side, side, data=pois_be.reshape(-1), big_endian=True)
+        svc.register_plane(10, 0, 0, 0, pt, side, side, generator="fake")
+        ctxs = [pbx.TileCtx(9 + p, 0, 0, 0, x, y, w, h, format="png") for p, x, y, w, h in regions]
+        _, bodies = _run(svc, ctxs)
+    modes = []
+    for (p, x, y, w, h), body in zip(regions, bodies):
+        src = pois_be if p == 0 else fake_be
+        tile = np.ascontiguousarray(src[y:y + h, bpp * x:bpp * (x + w)]).reshape(-1)
+        want = oracle.png_filter_stream(tile, pt, w, h, pbx.FILTER_ADAPTIVE).tobytes()
+        rc, idat = oracle.png_inflate_idat(body, len(want))
+        assert rc == 0 and idat == want, (p, x, y, w, h)
+        modes.append(oracle.adaptive_tile_none(tile, pt, w, h))
+    assert any(modes) and not all(modes)
