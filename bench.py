@@ -629,8 +629,11 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 "distinct_tiles": g * g,
                 **wall_vs_kernels(dt, 3, st),
                 "k_filter_ms": round(mean(st, "ms_filter"), 3),
-                "k_filter_frac": round((st[-1].in_bytes + st[-1].stream_bytes) / (mean(st, "ms_filter") * 1e-3)
-                                       / 1e9 / HBM_PEAK_GBPS, 4),
+                # (the filter pass moves the bytes of the tiles it filters: None-mode tiles of
+                # TF_DIRECT's geometry skip it, k_lz77 reads their rows from the plane)
+                "k_filter_frac": round((st[-1].in_bytes + st[-1].stream_bytes - st[-1].direct_bytes)
+                                       / (mean(st, "ms_filter") * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "none_mode_direct_tiles": st[-1].direct_tiles,
                 "deflate_chain_ms": round(mean(st, "ms_deflate") + mean(st, "ms_assemble"), 3),
                 "sample_bytes_per_tile": {"adaptive": round(sum(map(len, png_ad)) / 8, 1),
                                           "filter_none": round(sum(map(len, png_no)) / 8, 1),

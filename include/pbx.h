@@ -372,6 +372,9 @@ typedef struct pbx_batch_stats {
     double ms_extract, ms_filter, ms_deflate, ms_assemble, ms_total;
     double ms_lz77, ms_huff, ms_encode;
     uint64_t blocks;         /* deflate blocks (segments sharing one Huffman code) */
+    /* adaptive-filter PNG tiles in the None mode read by k_lz77 straight from the plane (no
+     * filter pass), and their bytes as in_bytes + stream_bytes count them */
+    uint64_t direct_tiles, direct_bytes;
 } pbx_batch_stats;
 int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* out);
 

@@ -350,6 +350,7 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t ti = PBX_IO_UPPER_INDEX(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
+    if (d.flags & TF_DIRECT) return;  // an adaptive tile in the None mode: k_lz77 reads the plane
     const uint32_t r0 = (b - d.blk_first) * FB_ROWS;
     const uint32_t r1 = r0 + FB_ROWS < (uint32_t)d.h ? r0 + FB_ROWS : (uint32_t)d.h;
     const uint32_t bpp = d.bpp, rb = (uint32_t)d.w * bpp, rowlen = d.rowlen;
@@ -582,7 +583,8 @@ __global__ __launch_bounds__(AM_NT) void k_adaptive_mode(TileDesc* __restrict__ 
     __syncthreads();
     if (tid == 0) {
         const bool none = rb > 0 && d.h > 0 && q2[0] >= q2[1];
-        dt[t].flags = none ? (d.flags | TF_ANONE) : (d.flags & ~TF_ANONE);
+        const uint32_t f = d.flags & ~(TF_ANONE | TF_DIRECT);
+        dt[t].flags = none ? (f | TF_ANONE | ((d.flags & TF_DIRECT_OK) ? TF_DIRECT : 0u)) : f;
     }
 }
 
@@ -908,6 +910,7 @@ __global__ __launch_bounds__(F2_NT) void k_filter2(const TileDesc* __restrict__ 
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t ti = PBX_IO_UPPER_INDEX(ndt, b, [&](uint32_t i) { return dt[i].blk_first; });
     const TileDesc d = dt[ti];
+    if (d.flags & TF_DIRECT) return;  // an adaptive tile in the None mode: k_lz77 reads the plane
     const uint32_t r0 = (b - d.blk_first) * F2_ROWS;
     const uint32_t nr = (uint32_t)d.h - r0 < F2_ROWS ? (uint32_t)d.h - r0 : F2_ROWS;
     const uint32_t bpp = (uint32_t)d.bpp, rb = (uint32_t)d.w * bpp, nw = rb >> 2;
@@ -1541,7 +1544,9 @@ __global__ __launch_bounds__(F3_NT) void k_filter3(const TileDesc* __restrict__ 
     const uint32_t ti = __builtin_amdgcn_readfirstlane(upper_index(ndt, wi, [&](uint32_t i) { return dt[i].blk_first; }));
     const TileDesc d = dt[ti];
     const uint32_t bpp = __builtin_amdgcn_readfirstlane((uint32_t)d.bpp);
-    if (FT == 5 && (__builtin_amdgcn_readfirstlane(d.flags) & TF_ANONE)) {  // uniform branches
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(d.flags);
+    if (FT == 5 && (fl & TF_DIRECT)) return;  // None mode, read from the plane by k_lz77
+    if (FT == 5 && (fl & TF_ANONE)) {  // uniform branches
         switch (bpp) {
         case 1: f3_run<G, FT, 1, true>(d, wi, lane, stream); break;
         case 2: f3_run<G, FT, 2, true>(d, wi, lane, stream); break;

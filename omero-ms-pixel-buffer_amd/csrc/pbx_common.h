@@ -33,6 +33,9 @@ enum : uint32_t {
     TF_TILED = 32u,    // one T x T sub-tile of a tiled-TIFF response (header by k_tiff_tiled)
     TF_ANONE = 64u,    // adaptive PNG tile whose rows all take filter None (the tile mode: set
                        // or cleared on the device by k_adaptive_mode every launch)
+    TF_DIRECT_OK = 128u,  // adaptive PNG tile of TF_DIRECT's geometry: in the None mode
+                          // k_adaptive_mode sets TF_DIRECT on it (no filter pass; k_lz77 reads
+                          // its rows from the plane)
     TF_BRIDGE = 1u << 30,  // host only, cleared before upload: `plane` is an offset into the
                            // batch's bridge buffer (a region straddling sparse-plane bands)
 };

@@ -2731,6 +2731,10 @@ int pbx_batch_plan(pbx_ctx* ctx, const pbx_tile_req* reqs, uint64_t n, pbx_batch
                                   rb <= filter2_max_rb() && ((uint64_t)d.x * bpp % 16) == 0;
             // filtered PNG rows of whole 16-byte chunks: the streaming one-wave-per-run k_filter3
             const bool filt3_ok = use_f3 && filt2_ok && rb % 16 == 0 && rb <= filter3_max_rb();
+            // adaptive tiles of the same geometry: direct when their tile mode says None
+            if (d.filter == PBX_FILTER_ADAPTIVE && d.rowlen >= 32 && rb <= ROWS_MAX_RB && aligned && bpp <= 4 &&
+                !ctx->cfg.stage_rows)
+                d.flags |= TF_DIRECT_OK;
             if (rows_ok && aligned && bpp <= 4 && !ctx->cfg.stage_rows) {
                 d.flags |= TF_DIRECT;
                 dt_direct.push_back(d);
@@ -3053,6 +3057,15 @@ int pbx_batch_stats_get(pbx_ctx* ctx, pbx_batch* b, pbx_batch_stats* s) {
             std::vector<uint64_t> offs(ndt + 1);
             HIP_TRY(hipMemcpy(offs.data(), b->d_offs, (ndt + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
             s->deflate_out_bytes = offs[ndt];
+            if (b->adaptive) {  // the tile modes k_adaptive_mode wrote into the descriptors
+                std::vector<TileDesc> dd(ndt);
+                HIP_TRY(hipMemcpy(dd.data(), b->d_dt, ndt * sizeof(TileDesc), hipMemcpyDeviceToHost));
+                for (const TileDesc& d : dd)
+                    if (d.filter == PBX_FILTER_ADAPTIVE && (d.flags & TF_DIRECT)) {
+                        s->direct_tiles++;
+                        s->direct_bytes += (uint64_t)d.w * d.h * d.bpp + d.stream_len;
+                    }
+            }
         }
         s->out_bytes = s->deflate_out_bytes;
         for (size_t k = 0; k < b->ft.size(); k++)

@@ -112,7 +112,8 @@ class PbxBatchStats(ctypes.Structure):
                  "stream_bytes", "out_bytes", "deflate_out_bytes", "segments")] + \
                [(n, ctypes.c_double) for n in
                 ("ms_extract", "ms_filter", "ms_deflate", "ms_assemble", "ms_total",
-                  "ms_lz77", "ms_huff", "ms_encode")] + [("blocks", ctypes.c_uint64)]
+                  "ms_lz77", "ms_huff", "ms_encode")] + \
+               [(n, ctypes.c_uint64) for n in ("blocks", "direct_tiles", "direct_bytes")]
 
 
 class PbxSpans(ctypes.Structure):

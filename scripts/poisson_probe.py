@@ -40,4 +40,5 @@ for name, filt, data in (("noise/none", 0, None), ("poisson/none", 0, pois), ("p
             b.close()
         m = np.mean(np.array(rows), 0)
         print(f"{name:17s} filter {m[0]:.3f} deflate {m[1]:.3f} assemble {m[2]:.3f} total {m[3]:.3f} ms "
-              f"out {st.deflate_out_bytes / 4096:.0f} B/tile segments {st.segments} blocks {st.blocks}", flush=True)
+              f"out {st.deflate_out_bytes / 4096:.0f} B/tile segments {st.segments} blocks {st.blocks} "
+              f"direct {st.direct_tiles}", flush=True)

@@ -155,7 +155,7 @@ def test_adaptive_tile_mode_poisson(oracle):
             s_.register_plane(7, 0, 0, 0, pbx.UINT16, side, side, data=pois, big_endian=False)
             s_.register_plane(8, 0, 0, 0, pbx.UINT16, side, side, generator="fake")
         ctxs = [pbx.TileCtx(7 + p, 0, 0, 0, x, y, w, h, format="png") for p, x, y, w, h in regions]
-        _, ad = _run(sa, ctxs)
+        st_ad, ad = _run(sa, ctxs)
         _, no = _run(sn, ctxs[:64])
     n_none = 0
     for (p, x, y, w, h), body in zip(regions, ad):
@@ -169,6 +169,9 @@ def test_adaptive_tile_mode_poisson(oracle):
         assert not mode or not filt.any(), (p, x, y, w, h)
         n_none += mode
     assert n_none >= 64  # every whole Poisson tile, at least
+    # None-mode tiles of TF_DIRECT's geometry (the 64 whole tiles among them) skip the filter
+    # pass: k_lz77 reads their rows from the plane
+    assert 64 <= st_ad.direct_tiles <= n_none
     assert sum(map(len, ad[:64])) <= sum(map(len, no))
 
 
