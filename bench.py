@@ -631,9 +631,13 @@ def adaptive_filter_line(svc, rank, world, barrier, side):
                 "k_filter_ms": round(mean(st, "ms_filter"), 3),
                 # (the filter pass moves the bytes of the tiles it filters: None-mode tiles of
                 # TF_DIRECT's geometry skip it, k_lz77 reads their rows from the plane)
-                "k_filter_frac": round((st[-1].in_bytes + st[-1].stream_bytes - st[-1].direct_bytes)
-                                       / (mean(st, "ms_filter") * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "k_filter_frac": (round((st[-1].in_bytes + st[-1].stream_bytes - st[-1].direct_bytes)
+                                        / (mean(st, "ms_filter") * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                  if 2 * st[-1].direct_tiles < len(ctxs) else None),
                 "none_mode_direct_tiles": st[-1].direct_tiles,
+                **({"k_filter_note": "most tiles skip the filter pass (None mode, read from the plane by "
+                                     "k_lz77): k_filter_ms is k_adaptive_mode and the idle launch"}
+                   if 2 * st[-1].direct_tiles >= len(ctxs) else {}),
                 "deflate_chain_ms": round(mean(st, "ms_deflate") + mean(st, "ms_assemble"), 3),
                 "sample_bytes_per_tile": {"adaptive": round(sum(map(len, png_ad)) / 8, 1),
                                           "filter_none": round(sum(map(len, png_no)) / 8, 1),
