@@ -480,9 +480,11 @@ __global__ __launch_bounds__(256) void k_filter(const TileDesc* __restrict__ dt,
 // |byte - prediction| (the first on ties), then None against it by the sum, over the two byte
 // planes (i mod bpp) & 1, of the squared counts of the row's byte values -- the larger, the
 // more concentrated the bytes, the fewer bits; None wins ties.  TF_ANONE sends every row of
-// the tile to None (k_filter / k_filter2 / k_filter3 read it); the oracle's
-// adaptive_tile_none (oracle/pbx_oracle.c) is the same rule.  One workgroup per tile; two rows
-// of byte reads and 2 KiB of LDS counters: microseconds a batch.
+// the tile to None (k_filter / k_filter2 / k_filter3 read it), and on a tile the host marked
+// TF_DIRECT_OK the kernel also sets TF_DIRECT: the filter kernels skip it and k_lz77 reads its
+// rows from the plane.  The oracle's adaptive_tile_none (oracle/pbx_oracle.c) is the same
+// rule.  One workgroup per tile: the two rows staged in LDS by 16-byte loads (k_filter's
+// staging), then the sums and 4 KiB of byte counters from LDS (~25 us per 4096 tiles).
 // rows_cap: LDS bytes for the two staged rows (the batch's widest adaptive row; wider ones
 // read their bytes from the plane)
 #ifndef PBX_AM_NT
