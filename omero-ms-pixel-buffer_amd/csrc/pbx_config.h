@@ -23,12 +23,20 @@ namespace pbx {
 #endif
 using DeflateMainCfg = DeflateCfg<PBX_NT, PBX_SEG, PBX_WIN>;
 constexpr uint32_t BLK_SEGS = PBX_BLK;  // segments per Huffman block at most (filter None, TIFF)
-// With a PNG row filter the byte statistics change from row to row, and smaller blocks
-// whose codes follow them compress better (adaptive filter on noise: 3 segments 382 KB,
-// 16 segments 392 KB per 512x512 uint16 tile).  Without a filter one code per tile of up to
-// 64 segments: the same bytes as blocks of 11 on noise (+0.005%), +0.3% on G_FAKE, and a
-// third of the k_huff waves (0.208 -> 0.125 ms per 4096 tiles, profiles/r03_p22-23).
-constexpr uint32_t BLK_SEGS_FILTERED = 3;
+// Row-filtered tiles: at most 16 segments per block (a 512x512 uint16 tile's 33 segments: three
+// blocks of 11).  Rounds 1-5 used 3, measured when blocks of more segments compressed worse (the
+// merge's 16-bit weights wrapped, since fixed); round 6 re-measured 3 / 6 / 11 / 16 / 33 / 64 on
+// the bench's filter lines (profiles/r06zq, r06zr): 16 writes fewer bytes than 3 on every
+// generator and filter (adaptive: G_NOISE 374,988 vs 375,103, G_FAKE 1,785 vs 1,956, Poisson
+// 283,283 vs 283,580 B/tile) in a third of the k_huff blocks (filter lines +8-12% tiles/s);
+// one block per tile (33, 64) is 1% faster again but matches filter None's bytes on Poisson
+// instead of beating them.  Without a filter one code per tile of up to 64 segments: the same
+// bytes as blocks of 11 on noise (+0.005%), +0.3% on G_FAKE, and a third of the k_huff waves
+// (0.208 -> 0.125 ms per 4096 tiles, profiles/r03_p22-23).
+#ifndef PBX_BLK_FILT
+#define PBX_BLK_FILT 16
+#endif
+constexpr uint32_t BLK_SEGS_FILTERED = PBX_BLK_FILT;
 // The planner's longest segment.  A stored Huffman block is one stored block per segment
 // (block_nbytes), so only a segment must fit a stored block's 65535 bytes.
 constexpr uint32_t SPLIT_MAX = PBX_SEG;
