@@ -333,3 +333,56 @@ def test_band_load_failures_give_the_band_back(oracle, monkeypatch):
         svc.band_write(pid2, 512, 512, _rows(oracle, sx, 512, 512))  # from the first row: loads
         svc.band_write(pid2, 0, 512, _rows(oracle, sx, 0, 512))
         assert svc.band_info(pid2)[1] == [2, 2]
+
+
+class PoissonRows(pbx.PixelSource):
+    """Poisson-like uint16 counts (lambda 250) row by row, each row seeded by its index: the
+    rows the adaptive filter's tile mode sends to filter None."""
+
+    def __init__(self, images):
+        self.images = dict(images)
+
+    def get_pixels(self, image_id):
+        return self.images.get(image_id)
+
+    @staticmethod
+    def rows(size_x, y0, n):
+        return np.concatenate([np.random.default_rng(1000 + y).poisson(250.0, size_x).astype(">u2")
+                               for y in range(y0, y0 + n)]).view(np.uint8)
+
+    def read_rows(self, pixels, z, c, t, level, y0, rows):
+        return self.rows(pixels.size_x, y0, rows).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["poisson", "noise"])
+def test_adaptive_filter_on_sparse_bands_and_bridges(oracle, kind):
+    """The adaptive PNG filter on a sparse plane: tiles inside one band and tiles straddling
+    bands (gathered into the batch's bridge buffer), at aligned and odd x, on Poisson-like
+    rows (None mode: the direct path reads the band or the bridge) and on G_NOISE (the filter
+    kernels): every IDAT equals the oracle's adaptive scanlines of the generator's tile."""
+    pt, sx, sy, B = pbx.UINT16, 4096, 4096, 256
+    iid = next(_ids)
+    src = (PoissonRows({iid: pbx.Pixels(iid, pt, sx, sy)}) if kind == "poisson"
+           else RowSource(oracle, {iid: pbx.Pixels(iid, pt, sx, sy)}))
+    regions = [(0, 0, 512, 256), (512, 256, 512, 512), (1024, 200, 512, 112), (8, 250, 256, 10),
+               (3, 700, 300, 77), (2048, 1020, 64, 8), (4000, 500, 96, 300), (17, 255, 33, 2)]
+    with pbx.PixelsService(sparse_band_rows=B, png_filter=pbx.FILTER_ADAPTIVE) as svc:
+        bodies = []
+        for x, y, w, h in regions:
+            tc = pbx.TileCtx(iid, 0, 0, 0, x, y, w, h, format="png")
+            bodies.append(pbx.TileRequestHandler(svc, tc, src).get_tile())
+        ctxs = [pbx.TileCtx(iid, 0, 0, 0, x, y, w, h, format="png") for x, y, w, h in regions]
+        bodies2 = [b for st, b in svc.get_tiles(ctxs)]  # all at once: one batch, bridges included
+    modes = []
+    for (x, y, w, h), b1, b2 in zip(regions, bodies, bodies2):
+        if kind == "poisson":
+            tile = PoissonRows.rows(sx, y, h).reshape(h, sx * 2)[:, 2 * x:2 * (x + w)].reshape(-1).copy()
+        else:
+            tile = oracle.gen_region(NOISE, pt, x, y, w, h, seed=SEED)
+        want_s = oracle.png_filter_stream(tile, pt, w, h, pbx.FILTER_ADAPTIVE).tobytes()
+        for body in (b1, b2):
+            r, idat = oracle.png_inflate_idat(bytes(body), len(want_s))
+            assert r == 0 and idat == want_s, (kind, x, y, w, h)
+        modes.append(oracle.adaptive_tile_none(tile, pt, w, h))
+    if kind == "poisson":
+        assert sum(modes) >= 6
